@@ -1,0 +1,551 @@
+// Torch op registrations for the Induction-Network gfx950 kernels (namespace torch.ops.ina).
+//
+// Every op validates device / dtype / contiguity / shapes on the host BEFORE launching, so a shape
+// that the kernel grid does not assume never reaches the GPU.  Launches go to the current HIP
+// stream (capturable into hipGraphs by the caller).  No op has a CPU implementation: the CPU path
+// of the framework is the pure-PyTorch oracle in models/reference.py.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+#include <torch/library.h>
+
+#include <tuple>
+
+namespace ina {
+struct LstmArgs {
+  const int* inst;
+  int S;
+  const int* word;
+  const int* pos1;
+  const int* pos2;
+  int L;
+  const float* wemb;
+  int E;
+  const float* p1emb;
+  const float* p2emb;
+  int PD;
+  const void* apack;
+  const void* a2pack;
+  const float* bias;
+  void* hraw;
+  float* cst;
+  const float* dH;
+  float* dw_slab;
+  float* dpos_slab;
+  float* dwemb;
+  int bwd_blocks;
+};
+int lstm_fwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
+int lstm_bwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
+bool lstm_supported(int U, int NX);
+size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD);
+
+struct AttnArgs {
+  const void* hraw;
+  const int* inst;
+  const int* mask;
+  int S, L;
+  const void* w1pack;
+  const void* w1tpack;
+  const float* b1;
+  const float* w2;
+  uint32_t seed, thr;
+  float inv_kp;
+  int drop;
+  float* e;
+  float* alphas;
+  const float* de;
+  float* dHraw;
+  float* slab;
+  int blocks;
+};
+int attn_fwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st);
+int attn_bwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st);
+
+int routing_fwd(const float* e, const float* Ws, int E, int N, int K, int Q, int R, int H, float* cls, int blocks,
+                hipStream_t st);
+int routing_bwd(const float* e, const float* Ws, int E, int N, int K, int Q, int R, int H, const float* dcls, float* de,
+                float* slab, int blocks, hipStream_t st);
+size_t routing_lds_bytes(int N, int K, int H, int R, bool bwd);
+
+struct NtnArgs {
+  const float* cls;
+  const float* e;
+  int E, N, K, Q, H, h;
+  const void* mpack;
+  const void* m2pack;
+  const void* wpack;
+  const void* wtpack;
+  const float* wvec;
+  const float* bias;
+  float* probs;
+  const float* dz;
+  float* dcls;
+  float* de;
+  void* dp_out;
+  float* dw_slab;
+  int blocks;
+  int paper;
+};
+int ntn_fwd(const NtnArgs& a, hipStream_t st);
+int ntn_bwd(const NtnArgs& a, hipStream_t st);
+
+int adam_step(float* p, float* m, float* v, const float* g, const unsigned char* l2mask, long n, float lr_t, float b1,
+              float b2, float eps, float gscale, float l2, hipStream_t st);
+int adagrad_step(float* p, float* acc, const float* g, const unsigned char* l2mask, long n, float lr, float gscale,
+                 float l2, hipStream_t st);
+int slab_reduce(const float* slabs, long nslab, long len, float* out, int accumulate, hipStream_t st);
+bool sampler_supported(int N, int K, int Q);
+int sample_episodes(const int* scopes, int R, int E, int N, int K, int Q, uint32_t seed, float nota_rate, int* idx,
+                    int* lab, hipStream_t st);
+}  // namespace ina
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "ina: ", name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), "ina: ", name, " must be contiguous");
+}
+void check(const Tensor& t, const char* name, at::ScalarType dt) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == dt, "ina: ", name, " has dtype ", t.scalar_type(), ", expected ", dt);
+}
+void check_launch(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, "ina: ", what, " launch failed / unsupported configuration (rc=", rc, ")");
+}
+int64_t frag_elems(bool bf16) { return bf16 ? 8 : 1; }
+
+// ------------------------------------------------------------------ LSTM
+std::tuple<Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& word, const Tensor& pos1, const Tensor& pos2,
+                                    const Tensor& wemb, const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack,
+                                    const Tensor& bias, int64_t U, int64_t NX, bool bf16, bool store_c) {
+  check(inst, "inst", at::kInt);
+  check(word, "word", at::kInt);
+  check(pos1, "pos1", at::kInt);
+  check(pos2, "pos2", at::kInt);
+  check(wemb, "wemb", at::kFloat);
+  check(p1emb, "p1emb", at::kFloat);
+  check(p2emb, "p2emb", at::kFloat);
+  check(bias, "bias", at::kFloat);
+  check(apack, "apack", bf16 ? at::kBFloat16 : at::kFloat);
+  TORCH_CHECK(ina::lstm_supported((int)U, (int)NX), "ina.lstm_fwd: unsupported (U, NX) = (", U, ", ", NX, ")");
+  const int64_t S = inst.size(0), L = word.size(1), E = wemb.size(1), PD = p1emb.size(1);
+  TORCH_CHECK(word.sizes() == pos1.sizes() && word.sizes() == pos2.sizes(), "ina.lstm_fwd: token array shapes differ");
+  TORCH_CHECK(E + 2 * PD <= 4 * NX, "ina.lstm_fwd: input dim ", E + 2 * PD, " > 4*NX");
+  TORCH_CHECK(p1emb.size(0) >= 2 * L && p2emb.size(0) >= 2 * L, "ina.lstm_fwd: pos tables need 2L rows");
+  TORCH_CHECK(bias.numel() == 2 * 4 * U, "ina.lstm_fwd: bias must be [2, 4U]");
+  const int64_t U4 = U / 4, KPL = frag_elems(bf16), NKS = (U4 + NX + KPL - 1) / KPL;
+  TORCH_CHECK(apack.numel() == 2 * U4 * NKS * 64 * KPL, "ina.lstm_fwd: apack has ", apack.numel(), " elems, expected ",
+              2 * U4 * NKS * 64 * KPL);
+  TORCH_CHECK(L * 2 * 16 * (int64_t)sizeof(int) * 4 <= 64 * 1024, "ina.lstm_fwd: L too large for the id stage");
+  auto hraw = at::empty({S, L, 2 * U}, word.options().dtype(bf16 ? at::kBFloat16 : at::kFloat));
+  const int64_t ntiles = (S + 15) / 16;
+  Tensor cst = store_c ? at::empty({ntiles, 2, L, U4, 64}, wemb.options()) : at::empty({0}, wemb.options());
+  if (S == 0) return {hraw, cst};
+  ina::LstmArgs a{};
+  a.inst = inst.data_ptr<int>();
+  a.S = (int)S;
+  a.word = word.data_ptr<int>();
+  a.pos1 = pos1.data_ptr<int>();
+  a.pos2 = pos2.data_ptr<int>();
+  a.L = (int)L;
+  a.wemb = wemb.data_ptr<float>();
+  a.E = (int)E;
+  a.p1emb = p1emb.data_ptr<float>();
+  a.p2emb = p2emb.data_ptr<float>();
+  a.PD = (int)PD;
+  a.apack = apack.data_ptr();
+  a.bias = bias.data_ptr<float>();
+  a.hraw = hraw.data_ptr();
+  a.cst = store_c ? cst.data_ptr<float>() : nullptr;
+  check_launch(ina::lstm_fwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_fwd");
+  return {hraw, cst};
+}
+
+std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
+                                            const Tensor& pos2, const Tensor& wemb, const Tensor& p1emb,
+                                            const Tensor& p2emb, const Tensor& apack, const Tensor& a2pack,
+                                            const Tensor& bias, const Tensor& hraw, const Tensor& cst, const Tensor& dH,
+                                            int64_t U, int64_t NX, bool bf16, bool word_grad, int64_t blocks) {
+  check(inst, "inst", at::kInt);
+  check(word, "word", at::kInt);
+  check(pos1, "pos1", at::kInt);
+  check(pos2, "pos2", at::kInt);
+  check(wemb, "wemb", at::kFloat);
+  check(p1emb, "p1emb", at::kFloat);
+  check(p2emb, "p2emb", at::kFloat);
+  check(bias, "bias", at::kFloat);
+  check(cst, "cst", at::kFloat);
+  check(dH, "dH", at::kFloat);
+  check(apack, "apack", bf16 ? at::kBFloat16 : at::kFloat);
+  check(a2pack, "a2pack", bf16 ? at::kBFloat16 : at::kFloat);
+  check(hraw, "hraw", bf16 ? at::kBFloat16 : at::kFloat);
+  TORCH_CHECK(ina::lstm_supported((int)U, (int)NX), "ina.lstm_bwd: unsupported (U, NX)");
+  const int64_t S = inst.size(0), L = word.size(1), E = wemb.size(1), PD = p1emb.size(1);
+  const int64_t DIN = E + 2 * PD, NF = DIN + U + 1, U4 = U / 4, KPL = frag_elems(bf16);
+  TORCH_CHECK(DIN <= 4 * NX, "ina.lstm_bwd: input dim too large");
+  TORCH_CHECK(hraw.size(0) == S && hraw.size(1) == L && hraw.size(2) == 2 * U, "ina.lstm_bwd: hraw shape");
+  TORCH_CHECK(dH.sizes() == hraw.sizes(), "ina.lstm_bwd: dH shape");
+  TORCH_CHECK(cst.numel() == ((S + 15) / 16) * 2 * L * U4 * 64, "ina.lstm_bwd: cst shape");
+  const int64_t NSLOT = U4 + NX;
+  TORCH_CHECK(a2pack.numel() == 2 * ((NSLOT + 3) / 4) * ((4 * U4 + KPL - 1) / KPL) * 64 * KPL, "ina.lstm_bwd: a2pack");
+  TORCH_CHECK(ina::lstm_bwd_lds_bytes((int)U, (int)NX, bf16, (int)L, (int)PD) <= 160 * 1024, "ina.lstm_bwd: LDS budget");
+  const int64_t ngroups = ((S + 15) / 16 + 3) / 4;
+  if (blocks <= 0) blocks = 512;
+  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, ngroups));
+  auto opt = wemb.options();
+  auto dw_slab = at::empty({blocks, 2, 4 * U, NF}, opt);
+  auto dpos_slab = at::empty({blocks, 2, 2, 2 * L, PD}, opt);
+  Tensor dwemb = word_grad ? at::zeros_like(wemb) : at::empty({0}, opt);
+  if (S == 0) {
+    dw_slab.zero_();
+    dpos_slab.zero_();
+    return {dw_slab, dpos_slab, dwemb};
+  }
+  ina::LstmArgs a{};
+  a.inst = inst.data_ptr<int>();
+  a.S = (int)S;
+  a.word = word.data_ptr<int>();
+  a.pos1 = pos1.data_ptr<int>();
+  a.pos2 = pos2.data_ptr<int>();
+  a.L = (int)L;
+  a.wemb = wemb.data_ptr<float>();
+  a.E = (int)E;
+  a.p1emb = p1emb.data_ptr<float>();
+  a.p2emb = p2emb.data_ptr<float>();
+  a.PD = (int)PD;
+  a.apack = apack.data_ptr();
+  a.a2pack = a2pack.data_ptr();
+  a.bias = bias.data_ptr<float>();
+  a.hraw = hraw.data_ptr();
+  a.cst = cst.data_ptr<float>();
+  a.dH = dH.data_ptr<float>();
+  a.dw_slab = dw_slab.data_ptr<float>();
+  a.dpos_slab = dpos_slab.data_ptr<float>();
+  a.dwemb = word_grad ? dwemb.data_ptr<float>() : nullptr;
+  a.bwd_blocks = (int)blocks;
+  check_launch(ina::lstm_bwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_bwd");
+  return {dw_slab, dpos_slab, dwemb};
+}
+
+// ------------------------------------------------------------------ attention
+uint32_t keep_threshold(double kp) {
+  const double t = kp * 4294967296.0;
+  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
+
+std::tuple<Tensor, Tensor> attn_fwd(const Tensor& hraw, const Tensor& inst, const Tensor& mask, const Tensor& w1pack,
+                                    const Tensor& b1, const Tensor& w2, int64_t seed, double keep_prob, int64_t U,
+                                    bool bf16, int64_t blocks) {
+  check(hraw, "hraw", bf16 ? at::kBFloat16 : at::kFloat);
+  check(inst, "inst", at::kInt);
+  check(mask, "mask", at::kInt);
+  check(w1pack, "w1pack", bf16 ? at::kBFloat16 : at::kFloat);
+  check(b1, "b1", at::kFloat);
+  check(w2, "w2", at::kFloat);
+  const int64_t S = hraw.size(0), L = hraw.size(1);
+  TORCH_CHECK(hraw.size(2) == 2 * U, "ina.attn_fwd: hraw last dim must be 2U");
+  TORCH_CHECK(mask.size(1) == L, "ina.attn_fwd: mask length");
+  TORCH_CHECK(b1.numel() == 2 * U && w2.numel() == 2 * U, "ina.attn_fwd: b1/w2 size");
+  const int64_t NT = (L + 15) / 16;
+  TORCH_CHECK(NT >= 1 && NT <= 4, "ina.attn_fwd: L must be <= 64");
+  auto e = at::empty({S, 2 * U}, b1.options());
+  auto alphas = at::empty({S, L}, b1.options());
+  if (S == 0) return {e, alphas};
+  ina::AttnArgs a{};
+  a.hraw = hraw.data_ptr();
+  a.inst = inst.data_ptr<int>();
+  a.mask = mask.data_ptr<int>();
+  a.S = (int)S;
+  a.L = (int)L;
+  a.w1pack = w1pack.data_ptr();
+  a.b1 = b1.data_ptr<float>();
+  a.w2 = w2.data_ptr<float>();
+  a.seed = (uint32_t)seed;
+  a.thr = keep_threshold(keep_prob);
+  a.inv_kp = (float)(1.0 / keep_prob);
+  a.drop = keep_prob < 1.0 ? 1 : 0;
+  a.e = e.data_ptr<float>();
+  a.alphas = alphas.data_ptr<float>();
+  if (blocks <= 0) blocks = 2048;
+  a.blocks = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (S + 3) / 4));
+  check_launch(ina::attn_fwd(a, (int)U, (int)NT, bf16, cur_stream()), "attn_fwd");
+  return {e, alphas};
+}
+
+std::tuple<Tensor, Tensor> attn_bwd(const Tensor& hraw, const Tensor& inst, const Tensor& w1pack, const Tensor& w1tpack,
+                                    const Tensor& b1, const Tensor& w2, int64_t seed, double keep_prob,
+                                    const Tensor& de, const Tensor& alphas, int64_t U, bool bf16, int64_t blocks) {
+  check(hraw, "hraw", bf16 ? at::kBFloat16 : at::kFloat);
+  check(inst, "inst", at::kInt);
+  check(w1pack, "w1pack", bf16 ? at::kBFloat16 : at::kFloat);
+  check(w1tpack, "w1tpack", bf16 ? at::kBFloat16 : at::kFloat);
+  check(b1, "b1", at::kFloat);
+  check(w2, "w2", at::kFloat);
+  check(de, "de", at::kFloat);
+  check(alphas, "alphas", at::kFloat);
+  const int64_t S = hraw.size(0), L = hraw.size(1), H2 = 2 * U;
+  TORCH_CHECK(de.size(0) == S && de.size(1) == H2, "ina.attn_bwd: de shape");
+  TORCH_CHECK(alphas.size(0) == S && alphas.size(1) == L, "ina.attn_bwd: alphas shape");
+  const int64_t NT = (L + 15) / 16;
+  TORCH_CHECK(NT >= 1 && NT <= 4, "ina.attn_bwd: L must be <= 64");
+  if (blocks <= 0) blocks = 1024;
+  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, (S + 3) / 4));
+  auto dH = at::empty({S, L, H2}, de.options());
+  auto slab = at::empty({blocks, H2 * H2 + 2 * H2}, de.options());
+  if (S == 0) {
+    slab.zero_();
+    return {dH, slab};
+  }
+  ina::AttnArgs a{};
+  a.hraw = hraw.data_ptr();
+  a.inst = inst.data_ptr<int>();
+  a.S = (int)S;
+  a.L = (int)L;
+  a.w1pack = w1pack.data_ptr();
+  a.w1tpack = w1tpack.data_ptr();
+  a.b1 = b1.data_ptr<float>();
+  a.w2 = w2.data_ptr<float>();
+  a.seed = (uint32_t)seed;
+  a.thr = keep_threshold(keep_prob);
+  a.inv_kp = (float)(1.0 / keep_prob);
+  a.drop = keep_prob < 1.0 ? 1 : 0;
+  a.de = de.data_ptr<float>();
+  a.alphas = alphas.data_ptr<float>();
+  a.dHraw = dH.data_ptr<float>();
+  a.slab = slab.data_ptr<float>();
+  a.blocks = (int)blocks;
+  check_launch(ina::attn_bwd(a, (int)U, (int)NT, bf16, cur_stream()), "attn_bwd");
+  return {dH, slab};
+}
+
+// ------------------------------------------------------------------ routing
+void check_episode_rows(const Tensor& e, int64_t E, int64_t N, int64_t K, int64_t Q, const char* who) {
+  TORCH_CHECK(e.dim() == 2 && e.size(0) == E * (N * K + N * Q), who, ": e must be [E*(N*K+N*Q), H]");
+}
+
+Tensor routing_fwd(const Tensor& e, const Tensor& Ws, int64_t E, int64_t N, int64_t K, int64_t Q, int64_t R,
+                   int64_t blocks) {
+  check(e, "e", at::kFloat);
+  check(Ws, "W_s", at::kFloat);
+  check_episode_rows(e, E, N, K, Q, "ina.routing_fwd");
+  const int64_t H = e.size(1);
+  TORCH_CHECK(Ws.size(0) == H && Ws.size(1) == H, "ina.routing_fwd: W_s must be [H, H]");
+  TORCH_CHECK(ina::routing_lds_bytes((int)N, (int)K, (int)H, (int)R, false) <= 64 * 1024, "ina.routing_fwd: N*K too large");
+  auto cls = at::empty({E, N, H}, e.options());
+  if (E == 0) return cls;
+  if (blocks <= 0) blocks = 4096;
+  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, E));
+  check_launch(ina::routing_fwd(e.data_ptr<float>(), Ws.data_ptr<float>(), (int)E, (int)N, (int)K, (int)Q, (int)R,
+                                (int)H, cls.data_ptr<float>(), (int)blocks, cur_stream()),
+               "routing_fwd");
+  return cls;
+}
+
+Tensor routing_bwd(const Tensor& e, const Tensor& Ws, const Tensor& dcls, Tensor de, int64_t E, int64_t N, int64_t K,
+                   int64_t Q, int64_t R, int64_t blocks) {
+  check(e, "e", at::kFloat);
+  check(Ws, "W_s", at::kFloat);
+  check(dcls, "dcls", at::kFloat);
+  check(de, "de", at::kFloat);
+  check_episode_rows(e, E, N, K, Q, "ina.routing_bwd");
+  const int64_t H = e.size(1);
+  TORCH_CHECK(de.sizes() == e.sizes(), "ina.routing_bwd: de shape");
+  TORCH_CHECK(dcls.numel() == E * N * H, "ina.routing_bwd: dcls shape");
+  TORCH_CHECK(ina::routing_lds_bytes((int)N, (int)K, (int)H, (int)R, true) <= 64 * 1024, "ina.routing_bwd: N*K too large");
+  if (blocks <= 0) blocks = 2048;
+  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, std::max<int64_t>(E, 1)));
+  auto slab = at::zeros({blocks, H, H}, e.options());
+  if (E == 0) return slab;
+  check_launch(ina::routing_bwd(e.data_ptr<float>(), Ws.data_ptr<float>(), (int)E, (int)N, (int)K, (int)Q, (int)R,
+                                (int)H, dcls.data_ptr<float>(), de.data_ptr<float>(), slab.data_ptr<float>(),
+                                (int)blocks, cur_stream()),
+               "routing_bwd");
+  return slab;
+}
+
+// ------------------------------------------------------------------ NTN
+Tensor ntn_fwd(const Tensor& cls, const Tensor& e, const Tensor& mpack, const Tensor& wpack, const Tensor& wvec,
+               const Tensor& bias, int64_t E, int64_t N, int64_t K, int64_t Q, int64_t h, bool paper, int64_t blocks) {
+  check(cls, "cls", at::kFloat);
+  check(e, "e", at::kFloat);
+  check(mpack, "mpack", at::kBFloat16);
+  check(bias, "bias", at::kFloat);
+  check_episode_rows(e, E, N, K, Q, "ina.ntn_fwd");
+  const int64_t H = e.size(1), MTH = (H + 15) / 16, NKA = (MTH + 1) / 2;
+  TORCH_CHECK(N <= 16 && N * Q <= 64, "ina.ntn_fwd: needs N <= 16 and N*Q <= 64");
+  TORCH_CHECK(MTH == 1 || MTH == 3 || MTH == 4, "ina.ntn_fwd: unsupported H ", H);
+  TORCH_CHECK(cls.numel() == E * N * H, "ina.ntn_fwd: cls shape");
+  TORCH_CHECK(mpack.numel() == h * MTH * NKA * 64 * 8, "ina.ntn_fwd: mpack size");
+  if (paper) {
+    check(wvec, "wvec", at::kFloat);
+    TORCH_CHECK(wvec.numel() == h, "ina.ntn_fwd: paper head w must be [h]");
+  } else {
+    check(wpack, "wpack", at::kBFloat16);
+    TORCH_CHECK(wpack.numel() == ((h + 1) / 2) * 64 * 8, "ina.ntn_fwd: wpack size");
+    TORCH_CHECK(bias.numel() == N, "ina.ntn_fwd: bias must be [N]");
+  }
+  auto probs = at::empty({E, N * Q, N}, e.options());
+  if (E == 0) return probs;
+  ina::NtnArgs a{};
+  a.cls = cls.data_ptr<float>();
+  a.e = e.data_ptr<float>();
+  a.E = (int)E;
+  a.N = (int)N;
+  a.K = (int)K;
+  a.Q = (int)Q;
+  a.H = (int)H;
+  a.h = (int)h;
+  a.mpack = mpack.data_ptr();
+  a.wpack = paper ? nullptr : wpack.data_ptr();
+  a.wvec = paper ? wvec.data_ptr<float>() : nullptr;
+  a.bias = bias.data_ptr<float>();
+  a.probs = probs.data_ptr<float>();
+  a.paper = paper ? 1 : 0;
+  if (blocks <= 0) blocks = 2048;
+  a.blocks = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (E + 3) / 4));
+  check_launch(ina::ntn_fwd(a, cur_stream()), "ntn_fwd");
+  return probs;
+}
+
+std::tuple<Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tensor& e, const Tensor& mpack,
+                                           const Tensor& m2pack, const Tensor& wtpack, const Tensor& wvec,
+                                           const Tensor& dz, Tensor de, int64_t E, int64_t N, int64_t K, int64_t Q,
+                                           int64_t h, bool paper, int64_t blocks) {
+  check(cls, "cls", at::kFloat);
+  check(e, "e", at::kFloat);
+  check(mpack, "mpack", at::kBFloat16);
+  check(m2pack, "m2pack", at::kBFloat16);
+  check(dz, "dz", at::kFloat);
+  check(de, "de", at::kFloat);
+  check_episode_rows(e, E, N, K, Q, "ina.ntn_bwd");
+  const int64_t H = e.size(1), MTH = (H + 15) / 16, NKB = (MTH + 1) / 2;
+  TORCH_CHECK(N <= 16 && N * Q <= 64, "ina.ntn_bwd: needs N <= 16 and N*Q <= 64");
+  TORCH_CHECK(MTH == 1 || MTH == 3 || MTH == 4, "ina.ntn_bwd: unsupported H");
+  TORCH_CHECK(H % 4 == 0, "ina.ntn_bwd: H must be a multiple of 4");
+  TORCH_CHECK(dz.numel() == E * N * Q * N, "ina.ntn_bwd: dz shape");
+  TORCH_CHECK(de.sizes() == e.sizes(), "ina.ntn_bwd: de shape");
+  TORCH_CHECK(m2pack.numel() == h * MTH * NKB * 64 * 8, "ina.ntn_bwd: m2pack size");
+  if (paper) {
+    check(wvec, "wvec", at::kFloat);
+  } else {
+    check(wtpack, "wtpack", at::kBFloat16);
+    TORCH_CHECK(wtpack.numel() == h * 64 * 8, "ina.ntn_bwd: wtpack size");
+  }
+  auto dcls = at::empty({E, N, H}, e.options());
+  auto dp = at::empty({E * N, h * H}, e.options().dtype(at::kBFloat16));
+  auto dw = paper ? at::empty({E, h}, e.options()) : at::empty({E, h, N, N}, e.options());
+  if (E == 0) return {dcls, dp, dw};
+  ina::NtnArgs a{};
+  a.cls = cls.data_ptr<float>();
+  a.e = e.data_ptr<float>();
+  a.E = (int)E;
+  a.N = (int)N;
+  a.K = (int)K;
+  a.Q = (int)Q;
+  a.H = (int)H;
+  a.h = (int)h;
+  a.mpack = mpack.data_ptr();
+  a.m2pack = m2pack.data_ptr();
+  a.wtpack = paper ? nullptr : wtpack.data_ptr();
+  a.wvec = paper ? wvec.data_ptr<float>() : nullptr;
+  a.dz = dz.data_ptr<float>();
+  a.dcls = dcls.data_ptr<float>();
+  a.de = de.data_ptr<float>();
+  a.dp_out = dp.data_ptr();
+  a.dw_slab = dw.data_ptr<float>();
+  a.paper = paper ? 1 : 0;
+  if (blocks <= 0) blocks = 2048;
+  a.blocks = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (E + 3) / 4));
+  check_launch(ina::ntn_bwd(a, cur_stream()), "ntn_bwd");
+  return {dcls, dp, dw};
+}
+
+// ------------------------------------------------------------------ optim / misc
+void adam_step(Tensor p, Tensor m, Tensor v, const Tensor& g, const std::optional<Tensor>& l2mask, double lr_t,
+               double b1, double b2, double eps, double gscale, double l2) {
+  check(p, "p", at::kFloat);
+  check(m, "m", at::kFloat);
+  check(v, "v", at::kFloat);
+  check(g, "g", at::kFloat);
+  const int64_t n = p.numel();
+  TORCH_CHECK(m.numel() == n && v.numel() == n && g.numel() == n, "ina.adam_step: size mismatch");
+  const unsigned char* mk = nullptr;
+  if (l2mask.has_value() && l2mask->defined() && l2mask->numel() > 0) {
+    check(*l2mask, "l2mask", at::kByte);
+    TORCH_CHECK(l2mask->numel() == n, "ina.adam_step: l2mask size");
+    mk = l2mask->data_ptr<unsigned char>();
+  }
+  if (n == 0) return;
+  check_launch(ina::adam_step(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), g.data_ptr<float>(), mk, n,
+                              (float)lr_t, (float)b1, (float)b2, (float)eps, (float)gscale, (float)l2, cur_stream()),
+               "adam_step");
+}
+
+void adagrad_step(Tensor p, Tensor acc, const Tensor& g, const std::optional<Tensor>& l2mask, double lr, double gscale,
+                  double l2) {
+  check(p, "p", at::kFloat);
+  check(acc, "acc", at::kFloat);
+  check(g, "g", at::kFloat);
+  const int64_t n = p.numel();
+  TORCH_CHECK(acc.numel() == n && g.numel() == n, "ina.adagrad_step: size mismatch");
+  const unsigned char* mk = nullptr;
+  if (l2mask.has_value() && l2mask->defined() && l2mask->numel() > 0) {
+    check(*l2mask, "l2mask", at::kByte);
+    mk = l2mask->data_ptr<unsigned char>();
+  }
+  if (n == 0) return;
+  check_launch(ina::adagrad_step(p.data_ptr<float>(), acc.data_ptr<float>(), g.data_ptr<float>(), mk, n, (float)lr,
+                                 (float)gscale, (float)l2, cur_stream()),
+               "adagrad_step");
+}
+
+void slab_reduce(const Tensor& slabs, Tensor out, bool accumulate) {
+  check(slabs, "slabs", at::kFloat);
+  check(out, "out", at::kFloat);
+  const int64_t len = out.numel();
+  TORCH_CHECK(len > 0 && slabs.numel() % len == 0, "ina.slab_reduce: slabs must be [k, out.numel()]");
+  check_launch(ina::slab_reduce(slabs.data_ptr<float>(), slabs.numel() / len, len, out.data_ptr<float>(),
+                                accumulate ? 1 : 0, cur_stream()),
+               "slab_reduce");
+}
+
+std::tuple<Tensor, Tensor> sample_episodes(const Tensor& scopes, int64_t E, int64_t N, int64_t K, int64_t Q, int64_t seed,
+                                           double nota_rate) {
+  check(scopes, "scopes", at::kInt);
+  TORCH_CHECK(scopes.dim() == 2 && scopes.size(1) == 2, "ina.sample_episodes: scopes must be [R, 2]");
+  const int64_t R = scopes.size(0);
+  TORCH_CHECK(N <= R, "ina.sample_episodes: N > number of relations");
+  TORCH_CHECK(ina::sampler_supported((int)N, (int)K, (int)Q), "ina.sample_episodes: N/K/Q too large");
+  auto idx = at::empty({E, N * K + N * Q}, scopes.options());
+  auto lab = at::empty({E, N * Q}, scopes.options());
+  if (E == 0) return {idx, lab};
+  check_launch(ina::sample_episodes(scopes.data_ptr<int>(), (int)R, (int)E, (int)N, (int)K, (int)Q, (uint32_t)seed,
+                                    (float)nota_rate, idx.data_ptr<int>(), lab.data_ptr<int>(), cur_stream()),
+               "sample_episodes");
+  return {idx, lab};
+}
+
+int64_t abi_version() { return 1; }
+
+}  // namespace
+
+TORCH_LIBRARY(ina, m) {
+  m.def("abi_version", &abi_version);
+  m.def("lstm_fwd", &lstm_fwd);
+  m.def("lstm_bwd", &lstm_bwd);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("routing_fwd", &routing_fwd);
+  m.def("routing_bwd", &routing_bwd);
+  m.def("ntn_fwd", &ntn_fwd);
+  m.def("ntn_bwd", &ntn_bwd);
+  m.def("adam_step", &adam_step);
+  m.def("adagrad_step", &adagrad_step);
+  m.def("slab_reduce", &slab_reduce);
+  m.def("sample_episodes", &sample_episodes);
+}

@@ -1,0 +1,86 @@
+"""Build the gfx950 kernel library in-tree: ``induction_network_on_fewrel_amd/_ina_kernels.so``.
+
+* every ``csrc/kernels/*.hip`` is compiled by ``hipcc --offload-arch=gfx950`` (device + host stub),
+* ``csrc/bindings.cpp`` (torch op registrations, host only) by ``g++`` against torch's headers,
+* everything is linked by ``hipcc -shared`` against torch's libs (the process's single HIP runtime).
+
+Incremental: an object is rebuilt when its source or any header is newer. ``python csrc/build.py``
+or ``from csrc.build import build; build()``. Works without a GPU (cross-compilation).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+OUT_DIR = os.path.join(ROOT, "build", "obj")
+LIB = os.path.join(ROOT, "induction_network_on_fewrel_amd", "_ina_kernels.so")
+ARCH = os.environ.get("INA_OFFLOAD_ARCH", "gfx950")
+
+
+def _torch_paths():
+    import torch  # noqa: F401
+    import torch.utils.cpp_extension as ce
+    inc = ce.include_paths()
+    lib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    return inc, lib
+
+
+def _newer(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed:\n" + " ".join(cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def build(verbose: bool = False, jobs: int = 0) -> str:
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    os.makedirs(OUT_DIR, exist_ok=True)
+    headers = glob.glob(os.path.join(CSRC, "include", "*.h"))
+    kernels = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    inc, tlib = _torch_paths()
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    tasks = []
+    objs = []
+    for src in kernels:
+        obj = os.path.join(OUT_DIR, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if _newer(obj, [src, *headers, __file__]):
+            tasks.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
+                          "-I" + os.path.join(CSRC, "include"), "-c", src, "-o", obj])
+    bsrc = os.path.join(CSRC, "bindings.cpp")
+    bobj = os.path.join(OUT_DIR, "bindings.o")
+    objs.append(bobj)
+    if _newer(bobj, [bsrc, __file__]):
+        cxx = shutil.which("g++") or "c++"
+        cmd = [cxx, "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
+               "-D_GLIBCXX_USE_CXX11_ABI=1", "-I/opt/rocm/include"]
+        cmd += ["-I" + p for p in inc]
+        cmd += ["-I" + sysconfig.get_paths()["include"], "-c", bsrc, "-o", bobj]
+        tasks.append(cmd)
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        for out in ex.map(_run, tasks):
+            if verbose and out.strip():
+                print(out)
+    if tasks or not os.path.exists(LIB) or _newer(LIB, objs):
+        cmd = [hipcc, "-shared", "-fPIC", "-o", LIB, *objs, f"-L{tlib}", "-ltorch", "-ltorch_cpu", "-lc10",
+               "-lc10_hip", "-ltorch_hip", f"-Wl,-rpath,{tlib}"]
+        _run(cmd)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

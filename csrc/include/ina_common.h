@@ -1,0 +1,99 @@
+// Shared device helpers for the Induction-Network gfx950 kernels.
+//
+// Conventions used by every kernel in csrc/kernels:
+//  * wave = 64 lanes; MFMA v_mfma_f32_16x16x32_bf16 (bf16 path) or v_mfma_f32_16x16x4_f32
+//    (fp32 path).  For both, lane l holds A[row = l&15][k = KPL*(l>>4) + j] and
+//    B[k = KPL*(l>>4) + j][col = l&15] (j < KPL, KPL = 8 for bf16, 1 for fp32) and the
+//    accumulator C[row = 4*(l>>4) + r][col = l&15], r = 0..3.
+//  * "lane group" q = l >> 4 (0..3); "lane column" n = l & 15.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define INA_DEVICE __device__ __forceinline__
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+namespace ina {
+
+// ------------------------------------------------------------------ bf16 bits
+INA_DEVICE unsigned short f2bf(float f) {
+  __bf16 h = (__bf16)f;  // RNE, NaN-preserving (v_cvt_pk_bf16_f32 on gfx950)
+  return __builtin_bit_cast(unsigned short, h);
+}
+INA_DEVICE float bf2f(unsigned short b) { return __builtin_bit_cast(float, ((uint32_t)b) << 16); }
+INA_DEVICE float round_bf(float f) { return bf2f(f2bf(f)); }
+
+// ------------------------------------------------------------------ MFMA
+INA_DEVICE f32x4_t mfma_bf16(const u16x8_t& a, const u16x8_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+INA_DEVICE f32x4_t mfma_f32(float a, float b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------ math
+INA_DEVICE float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+INA_DEVICE float tanhf_(float x) {
+  // tanh(x) = 1 - 2/(exp(2x)+1); saturates cleanly at +-1, abs err ~1e-7
+  float e = __expf(2.0f * x);
+  return 1.0f - 2.0f / (e + 1.0f);
+}
+
+// ------------------------------------------------------------------ RNG
+// Counter-based hash; bit-identical to models/reference.py::hash_u32.
+INA_DEVICE uint32_t hash_u32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x68E31DA4u;
+  x ^= x >> 16;
+  return x;
+}
+// Dropout keep decision for element `idx` of direction `dir` (reference.py::dropout_keep_mask).
+INA_DEVICE bool dropout_keep(uint32_t seed, uint32_t dir, uint32_t idx, uint32_t thr) {
+  uint32_t salt = seed * 0x9E37u + dir * 0x3C6EF372u + 0x1234567u;
+  uint32_t h = hash_u32(hash_u32(idx ^ salt) + (seed & 0x7FFFFFFFu));
+  return h < thr;
+}
+
+// ------------------------------------------------------------------ reductions
+INA_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+INA_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// sum over the 16 lanes that share a lane group (same l>>4)
+INA_DEVICE float group16_sum(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+INA_DEVICE float group16_max(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// sum over the 4 lane groups (lanes n, n+16, n+32, n+48)
+INA_DEVICE float cross_group_sum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+}  // namespace ina
+
+#define INA_CHECK_LAUNCH()                                                        \
+  do {                                                                            \
+    hipError_t e__ = hipGetLastError();                                           \
+    if (e__ != hipSuccess) return (int)e__;                                       \
+  } while (0)

@@ -1,0 +1,465 @@
+// Fused word-level self-attention pooling, forward and backward (K4 of SURVEY 2.3).
+//
+// Reference (model/layer_module.py:49-98, model/graph.py:52-53):
+//   x_proj = tanh(H @ W1 + b1)            W1 = self_attn/dense/kernel [2u, 2u]
+//   score  = x_proj @ W_a2                W_a2 [2u, 1]
+//   alphas = softmax_t(score + (1 - (mask>0)) * -2^31)
+//   e      = sum_t alphas_t * H_t
+// H is the BiLSTM output *after* the DropoutWrapper output dropout; the dropout mask is
+// regenerated here from the counter-based hash (no mask tensor is stored).
+//
+// One wave processes one sentence at a time (grid-stride).  The projection is computed
+// transposed, P^T[j, tok] = W1^T[j, i] H^T[i, tok], with v_mfma_f32_16x16x32_bf16 (or the f32
+// 16x16x4 form): the B operand is 8 contiguous features of one token (one 16-B load), and the
+// accumulator puts the sentence's tokens on the lane columns so the score / softmax / pooling
+// reductions are 16-lane shuffles.  Backward recomputes P, forms dP^T in the accumulator
+// layout and feeds it straight back as the B operand of dH^T = W1 dP^T; dW1 = H^T dP is
+// accumulated with MFMAs after a wave-private LDS transpose (tokens become the K dimension).
+#include "ina_common.h"
+
+using namespace ina;
+
+namespace {
+
+template <bool BF16>
+struct FT;
+template <>
+struct FT<true> {
+  using frag = u16x8_t;
+  using elem = unsigned short;
+  static constexpr int KPL = 8;
+};
+template <>
+struct FT<false> {
+  using frag = float;
+  using elem = float;
+  static constexpr int KPL = 1;
+};
+
+INA_DEVICE f32x4_t mma(const u16x8_t& a, const u16x8_t& b, const f32x4_t& c) { return mfma_bf16(a, b, c); }
+INA_DEVICE f32x4_t mma(float a, float b, const f32x4_t& c) { return mfma_f32(a, b, c); }
+INA_DEVICE void fset(u16x8_t& f, int j, float v) { f[j] = f2bf(v); }
+INA_DEVICE void fset(float& f, int, float v) { f = v; }
+INA_DEVICE float ld_elem(const unsigned short* p) { return bf2f(*p); }
+INA_DEVICE float ld_elem(const float* p) { return *p; }
+INA_DEVICE unsigned short cvt_elem(float v, unsigned short*) { return f2bf(v); }
+INA_DEVICE float cvt_elem(float v, float*) { return v; }
+INA_DEVICE float rnd(float v, bool bf16) { return bf16 ? round_bf(v) : v; }
+
+INA_DEVICE void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int U, int NT, bool BF16>
+struct AShape {
+  static constexpr int H2 = 2 * U;
+  static constexpr int KPL = FT<BF16>::KPL;
+  static constexpr int KP = BF16 ? ((H2 + 31) / 32) * 32 : ((H2 + 3) / 4) * 4;  // padded feature dim
+  static constexpr int NKS = BF16 ? KP / 32 : KP / 4;                           // proj K-steps
+  static constexpr int MT = (H2 + 15) / 16;                                      // j tiles
+  static constexpr int NKS2 = (4 * MT + KPL - 1) / KPL;                          // dH K-steps (j slots)
+  static constexpr int NV = BF16 ? NKS * 8 : NKS;                               // features per lane per token
+  static constexpr int TOKP = ((NT * 16 + 31) / 32) * 32;                        // LDS token columns
+  static constexpr int RS = TOKP + (BF16 ? 8 : 4);                              // LDS row stride (elements)
+};
+
+// feature index held in slot v (0..NV-1) of lane group q
+template <bool BF16>
+INA_DEVICE int feat_of(int v, int q) {
+  if (BF16) return (v >> 3) * 32 + 8 * q + (v & 7);
+  return 4 * v + q;
+}
+
+// Load the dropout-applied H values of token `tok` for lane group q: out fp32 values (hv) and
+// the MFMA B fragments (rounded for bf16).
+template <int U, int NT, bool BF16>
+INA_DEVICE void load_h(const typename FT<BF16>::elem* __restrict__ hraw, long seq, int tok, int L, int q,
+                       uint32_t seed, uint32_t thr, float inv_kp, bool drop, float* hv) {
+  using Sh = AShape<U, NT, BF16>;
+#pragma unroll
+  for (int v = 0; v < Sh::NV; ++v) {
+    const int k = feat_of<BF16>(v, q);
+    float x = 0.f;
+    if (tok < L && k < Sh::H2) {
+      x = ld_elem(hraw + (seq * L + tok) * Sh::H2 + k);
+      if (drop) {
+        const int dirn = k >= U ? 1 : 0;
+        const uint32_t idx = (uint32_t)((seq * L + tok) * U + (k - dirn * U));
+        x = dropout_keep(seed, dirn, idx, thr) ? x * inv_kp : 0.f;
+      }
+    }
+    hv[v] = x;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+template <int U, int NT, bool BF16>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(
+    const typename FT<BF16>::elem* __restrict__ hraw, const int* __restrict__ inst, const int* __restrict__ maskarr,
+    int S, int L, const typename FT<BF16>::frag* __restrict__ w1pack, const float* __restrict__ b1,
+    const float* __restrict__ w2, uint32_t seed, uint32_t thr, float inv_kp, int drop, float* __restrict__ e_out,
+    float* __restrict__ alphas) {
+  using Sh = AShape<U, NT, BF16>;
+  using frag = typename FT<BF16>::frag;
+  constexpr int H2 = Sh::H2, NKS = Sh::NKS, MT = Sh::MT, NV = Sh::NV, KPL = Sh::KPL;
+  const int lane = threadIdx.x & 63;
+  const int q = lane >> 4, n = lane & 15;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  frag A[MT][NKS];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) A[m][ks] = w1pack[(m * NKS + ks) * 64 + lane];
+  float bj[MT][4], wj[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * m + 4 * q + r;
+      bj[m][r] = j < H2 ? b1[j] : 0.f;
+      wj[m][r] = j < H2 ? w2[j] : 0.f;
+    }
+  for (int s = gw; s < S; s += nw) {
+    const long row = (long)inst[s] * L;
+    float hv[NT][NV];
+    float score[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int tok = 16 * nt + n;
+      load_h<U, NT, BF16>(hraw, s, tok, L, q, seed, thr, inv_kp, drop != 0, hv[nt]);
+      frag B[NKS];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) fset(B[ks], j, rnd(hv[nt][ks * KPL + j], BF16));
+      }
+      float sp = 0.f;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        f32x4_t acc = {bj[m][0], bj[m][1], bj[m][2], bj[m][3]};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) acc = mma(A[m][ks], B[ks], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sp += wj[m][r] * tanhf_(acc[r]);
+      }
+      sp = cross_group_sum(sp);
+      float v = -INFINITY;
+      if (tok < L) {
+        const float m01 = maskarr[row + tok] > 0 ? 1.f : 0.f;
+        v = sp + (1.f - m01) * -2147483648.f;
+      }
+      score[nt] = v;
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) mx = fmaxf(mx, score[nt]);
+    mx = group16_max(mx);
+    float p[NT], sum = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      p[nt] = (16 * nt + n < L) ? __expf(score[nt] - mx) : 0.f;
+      sum += p[nt];
+    }
+    sum = group16_sum(sum);
+    const float inv = 1.f / sum;
+    float ev[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) ev[v] = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const float a = p[nt] * inv;
+      if (q == 0 && 16 * nt + n < L) alphas[(long)s * L + 16 * nt + n] = a;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) ev[v] += a * hv[nt][v];
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) ev[v] = group16_sum(ev[v]);
+    if (n == 0) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int k = feat_of<BF16>(v, q);
+        if (k < H2) e_out[(long)s * H2 + k] = ev[v];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// slab per block: [dW1 (H2*H2, row i, col j) | db1 (H2) | dw2 (H2)]
+template <int U, int NT, bool BF16>
+__global__ __launch_bounds__(256) void attn_bwd_kernel(
+    const typename FT<BF16>::elem* __restrict__ hraw, const int* __restrict__ inst, int S, int L,
+    const typename FT<BF16>::frag* __restrict__ w1pack, const typename FT<BF16>::frag* __restrict__ w1tpack,
+    const float* __restrict__ b1, const float* __restrict__ w2, uint32_t seed, uint32_t thr, float inv_kp,
+    int drop, const float* __restrict__ de, const float* __restrict__ alphas, float* __restrict__ dHraw,
+    float* __restrict__ slab) {
+  using Sh = AShape<U, NT, BF16>;
+  using frag = typename FT<BF16>::frag;
+  using elem = typename FT<BF16>::elem;
+  constexpr int H2 = Sh::H2, NKS = Sh::NKS, MT = Sh::MT, NV = Sh::NV, KPL = Sh::KPL, NKS2 = Sh::NKS2,
+                TOKP = Sh::TOKP, RS = Sh::RS;
+  constexpr int ROWS = MT * 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane >> 4, n = lane & 15;
+  const int gw = blockIdx.x * 4 + wave, nw = gridDim.x * 4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  elem* HT = reinterpret_cast<elem*>(smem) + (size_t)wave * 2 * ROWS * RS;  // [i][tok]
+  elem* DPT = HT + ROWS * RS;                                                  // [j][tok]
+  for (int i = lane; i < 2 * ROWS * RS; i += 64) HT[i] = cvt_elem(0.f, (elem*)nullptr);
+  wave_lds_sync();
+
+  float bj[MT][4], wj[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * m + 4 * q + r;
+      bj[m][r] = j < H2 ? b1[j] : 0.f;
+      wj[m][r] = j < H2 ? w2[j] : 0.f;
+    }
+  f32x4_t accW[MT][MT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < MT; ++b) accW[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float dw2a[MT][4], db1a[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dw2a[m][r] = db1a[m][r] = 0.f;
+
+  for (int s = gw; s < S; s += nw) {
+    // de for the lane's features
+    float dev[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int k = feat_of<BF16>(v, q);
+      dev[v] = k < H2 ? de[(long)s * H2 + k] : 0.f;
+    }
+    float hv[NT][NV], pr[NT][MT][4], al[NT], da[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int tok = 16 * nt + n;
+      load_h<U, NT, BF16>(hraw, s, tok, L, q, seed, thr, inv_kp, drop != 0, hv[nt]);
+      frag B[NKS];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+          const float hr = rnd(hv[nt][ks * KPL + j], BF16);
+          fset(B[ks], j, hr);
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        f32x4_t acc = {bj[m][0], bj[m][1], bj[m][2], bj[m][3]};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) acc = mma(w1pack[(m * NKS + ks) * 64 + lane], B[ks], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pr[nt][m][r] = tanhf_(acc[r]);
+      }
+      al[nt] = tok < L ? alphas[(long)s * L + tok] : 0.f;
+      float d = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) d += dev[v] * hv[nt][v];
+      da[nt] = cross_group_sum(d);
+    }
+    float sd = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) sd += al[nt] * da[nt];
+    sd = group16_sum(sd);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int tok = 16 * nt + n;
+      const float ds = al[nt] * (da[nt] - sd);
+      float dp[MT][4];
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dp[m][r] = ds * wj[m][r] * (1.f - pr[nt][m][r] * pr[nt][m][r]);
+          dw2a[m][r] += ds * pr[nt][m][r];
+          db1a[m][r] += dp[m][r];
+        }
+      // dH^T = W1 dP^T  (+ alpha * de)
+      frag B2[NKS2];
+#pragma unroll
+      for (int ks = 0; ks < NKS2; ++ks) {
+        if constexpr (BF16) {
+          B2[ks] = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        } else {
+          B2[ks] = 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+          const int idx = ks * KPL + j;
+          if (idx < 4 * MT) fset(B2[ks], j, dp[idx >> 2][idx & 3]);
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NKS2; ++ks) acc = mma(w1tpack[(m * NKS2 + ks) * 64 + lane], B2[ks], acc);
+        if (tok < L) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = 16 * m + 4 * q + r;
+            if (i < H2) {
+              float g = acc[r] + al[nt] * de[(long)s * H2 + i];
+              if (drop) {
+                const int dirn = i >= U ? 1 : 0;
+                const uint32_t idx = (uint32_t)(((long)s * L + tok) * U + (i - dirn * U));
+                g = dropout_keep(seed, dirn, idx, thr) ? g * inv_kp : 0.f;
+              }
+              dHraw[((long)s * L + tok) * H2 + i] = g;
+            }
+          }
+        }
+      }
+      // stage H (MFMA operand values) and dP for the dW1 MFMA; tokens are the K dimension
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int k = feat_of<BF16>(v, q);
+        if (k < ROWS) HT[k * RS + tok] = cvt_elem(hv[nt][v], (elem*)nullptr);
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) DPT[(16 * m + 4 * q + r) * RS + tok] = cvt_elem(dp[m][r], (elem*)nullptr);
+    }
+    wave_lds_sync();
+    if constexpr (BF16) {
+#pragma unroll
+      for (int kt = 0; kt < TOKP / 32; ++kt)
+#pragma unroll
+        for (int a = 0; a < MT; ++a) {
+          const u16x8_t fa = *reinterpret_cast<const u16x8_t*>(&HT[(16 * a + n) * RS + 32 * kt + 8 * q]);
+#pragma unroll
+          for (int b = 0; b < MT; ++b) {
+            const u16x8_t fb = *reinterpret_cast<const u16x8_t*>(&DPT[(16 * b + n) * RS + 32 * kt + 8 * q]);
+            accW[a][b] = mfma_bf16(fa, fb, accW[a][b]);
+          }
+        }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < TOKP / 4; ++kt)
+#pragma unroll
+        for (int a = 0; a < MT; ++a) {
+          const float fa = HT[(16 * a + n) * RS + 4 * kt + q];
+#pragma unroll
+          for (int b = 0; b < MT; ++b) {
+            const float fb = DPT[(16 * b + n) * RS + 4 * kt + q];
+            accW[a][b] = mfma_f32(fa, fb, accW[a][b]);
+          }
+        }
+    }
+    wave_lds_sync();
+  }
+  // ---- block reduction into the slab
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  const int NS = H2 * H2 + 2 * H2;
+  for (int i = threadIdx.x; i < NS; i += 256) red[i] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < MT; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * a + 4 * q + r, j = 16 * b + n;
+        if (i < H2 && j < H2) atomicAdd(&red[i * H2 + j], accW[a][b][r]);
+      }
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * m + 4 * q + r;
+      const float d1 = group16_sum(db1a[m][r]);
+      const float d2 = group16_sum(dw2a[m][r]);
+      if (n == 0 && j < H2) {
+        atomicAdd(&red[H2 * H2 + j], d1);
+        atomicAdd(&red[H2 * H2 + H2 + j], d2);
+      }
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NS; i += 256) slab[(size_t)blockIdx.x * NS + i] = red[i];
+}
+
+// ------------------------------------------------------------------------------------------
+namespace ina {
+
+struct AttnArgs {
+  const void* hraw;
+  const int* inst;
+  const int* mask;
+  int S, L;
+  const void* w1pack;
+  const void* w1tpack;
+  const float* b1;
+  const float* w2;
+  uint32_t seed, thr;
+  float inv_kp;
+  int drop;
+  float* e;
+  float* alphas;
+  const float* de;
+  float* dHraw;
+  float* slab;
+  int blocks;
+};
+
+size_t attn_bwd_lds_bytes(int U, int NT, bool bf16) {
+  const int H2 = 2 * U, MT = (H2 + 15) / 16;
+  const int TOKP = ((NT * 16 + 31) / 32) * 32, RS = TOKP + (bf16 ? 8 : 4);
+  size_t a = (size_t)4 * 2 * MT * 16 * RS * (bf16 ? 2 : 4);
+  size_t r = (size_t)(H2 * H2 + 2 * H2) * 4;
+  return a > r ? a : r;
+}
+
+template <int U, int NT, bool BF16>
+static int attn_fwd_t(const AttnArgs& a, hipStream_t st) {
+  using F = FT<BF16>;
+  hipLaunchKernelGGL((attn_fwd_kernel<U, NT, BF16>), dim3(a.blocks), dim3(256), 0, st,
+                     (const typename F::elem*)a.hraw, a.inst, a.mask, a.S, a.L, (const typename F::frag*)a.w1pack,
+                     a.b1, a.w2, a.seed, a.thr, a.inv_kp, a.drop, a.e, a.alphas);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+template <int U, int NT, bool BF16>
+static int attn_bwd_t(const AttnArgs& a, hipStream_t st) {
+  using F = FT<BF16>;
+  const size_t lds = attn_bwd_lds_bytes(U, NT, BF16);
+  hipLaunchKernelGGL((attn_bwd_kernel<U, NT, BF16>), dim3(a.blocks), dim3(256), lds, st,
+                     (const typename F::elem*)a.hraw, a.inst, a.S, a.L, (const typename F::frag*)a.w1pack,
+                     (const typename F::frag*)a.w1tpack, a.b1, a.w2, a.seed, a.thr, a.inv_kp, a.drop, a.de,
+                     a.alphas, a.dHraw, a.slab);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+#define INA_ATTN_CASE(FN, UU)                               \
+  if (U == UU) {                                            \
+    if (NT == 1) return FN<UU, 1, B>(a, st);                \
+    if (NT == 2) return FN<UU, 2, B>(a, st);                \
+    if (NT == 3) return FN<UU, 3, B>(a, st);                \
+    if (NT == 4) return FN<UU, 4, B>(a, st);                \
+  }
+#define INA_ATTN_DISPATCH(FN)                 \
+  if (bf16) {                                 \
+    constexpr bool B = true;                  \
+    INA_ATTN_CASE(FN, 8) INA_ATTN_CASE(FN, 20) INA_ATTN_CASE(FN, 32) \
+  } else {                                    \
+    constexpr bool B = false;                 \
+    INA_ATTN_CASE(FN, 8) INA_ATTN_CASE(FN, 20) INA_ATTN_CASE(FN, 32) \
+  }                                           \
+  return -1;
+
+int attn_fwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st) { INA_ATTN_DISPATCH(attn_fwd_t) }
+int attn_bwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st) { INA_ATTN_DISPATCH(attn_bwd_t) }
+
+}  // namespace ina

@@ -1,0 +1,545 @@
+// Persistent fused BiLSTM forward / BPTT backward for gfx950 (K1 + K2 + K3 + K11 of SURVEY 2.3).
+//
+// Reference semantics: TF BasicLSTMCell inside bidirectional_dynamic_rnn over ALL L steps
+// (model/graph.py:34-49): gates = [x_t ; h_{t-1}] @ W + b, order i,j,f,o,
+// c' = c*sig(f + 1) + sig(i)*tanh(j), h' = tanh(c')*sig(o).  x_t = [word_emb ; pos1_emb ; pos2_emb]
+// gathered in-kernel (model/base.py:76-86).
+//
+// Layout ("lane ownership"): one wave owns 16 sequences of one direction.  Gates are computed
+// transposed, G^T[4U, 16] = W^T[4U, K] x XH^T[K, 16], as U/4 M-tiles of v_mfma_f32_16x16x32_bf16
+// (or v_mfma_f32_16x16x4_f32 in fp32 mode).  Row 16m + 4q + g of M-tile m is gate g of unit
+// 4m + q, so the accumulator of lane (q = l>>4, n = l&15) holds i,j,f,o of unit 4m+q for sequence n
+// in its 4 registers.  The K dimension is laid out so that lane group q supplies exactly the h
+// units it owns (and x features 4xi+q): the recurrence h_t -> B operand never leaves the lane.
+// The backward reuses the same trick for d[x;h] = W dG, and transposes (dG, XH) through
+// wave-private LDS every 2 steps to accumulate dW with MFMAs (32 samples per K-step).
+#include "ina_common.h"
+
+using namespace ina;
+
+namespace {
+
+template <int U, int NX, bool BF16>
+struct Shape {
+  static constexpr int U4 = U / 4;
+  static constexpr int KPL = BF16 ? 8 : 1;                 // k values per lane per MFMA
+  static constexpr int NSLOT = U4 + NX;                    // [h ; x] slots per lane group
+  static constexpr int NKS = (NSLOT + KPL - 1) / KPL;      // fwd K-steps
+  static constexpr int NMT = U4;                           // fwd M-tiles (16 gate rows each)
+  static constexpr int NMT2 = (NSLOT + 3) / 4;             // bwd M-tiles over feature slots
+  static constexpr int NG = 4 * U4;                        // gate slots per lane
+  static constexpr int NKS2 = (NG + KPL - 1) / KPL;        // bwd K-steps over gate slots
+  static constexpr int G4 = 4 * U;                         // gate columns
+  static constexpr int GT = (G4 + 15) / 16;                // dW M-tiles (gate rows)
+  static constexpr int KSTEP_SAMPLES = BF16 ? 32 : 4;      // samples per dW MFMA K-step
+  static constexpr int RS = BF16 ? 40 : 36;                // LDS row stride (elements) for 32 samples
+};
+
+template <bool BF16>
+struct FragT;
+template <>
+struct FragT<true> {
+  using type = u16x8_t;
+  using elem = unsigned short;
+};
+template <>
+struct FragT<false> {
+  using type = float;
+  using elem = float;
+};
+
+template <bool BF16>
+INA_DEVICE void fset(typename FragT<BF16>::type& fr, int j, float v);
+template <>
+INA_DEVICE void fset<true>(u16x8_t& fr, int j, float v) { fr[j] = f2bf(v); }
+template <>
+INA_DEVICE void fset<false>(float& fr, int, float v) { fr = v; }
+
+template <bool BF16>
+INA_DEVICE typename FragT<BF16>::type fzero();
+template <>
+INA_DEVICE u16x8_t fzero<true>() { return u16x8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
+template <>
+INA_DEVICE float fzero<false>() { return 0.f; }
+
+INA_DEVICE f32x4_t mma(const u16x8_t& a, const u16x8_t& b, const f32x4_t& c) { return mfma_bf16(a, b, c); }
+INA_DEVICE f32x4_t mma(float a, float b, const f32x4_t& c) { return mfma_f32(a, b, c); }
+
+INA_DEVICE unsigned short to_elem(float v, unsigned short*) { return f2bf(v); }
+INA_DEVICE float to_elem(float v, float*) { return v; }
+INA_DEVICE float from_elem(unsigned short v) { return bf2f(v); }
+INA_DEVICE float from_elem(float v) { return v; }
+
+// x feature f of token (wid, p1, p2); 0 beyond DIN.
+INA_DEVICE float gather_x(int f, int wid, int p1, int p2, const float* __restrict__ wemb, int E,
+                          const float* __restrict__ p1emb, const float* __restrict__ p2emb, int PD) {
+  if (f < E) return wemb[(long)wid * E + f];
+  if (f < E + PD) return p1emb[p1 * PD + (f - E)];
+  if (f < E + 2 * PD) return p2emb[p2 * PD + (f - E - PD)];
+  return 0.f;
+}
+
+INA_DEVICE void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------
+template <int U, int NX, bool BF16>
+__global__ __launch_bounds__(256) void lstm_fwd_kernel(
+    const int* __restrict__ inst, int S, const int* __restrict__ word, const int* __restrict__ pos1,
+    const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
+    const float* __restrict__ p1emb, const float* __restrict__ p2emb, int PD,
+    const typename FragT<BF16>::type* __restrict__ apack, const float* __restrict__ bias,
+    typename FragT<BF16>::elem* __restrict__ hout, float* __restrict__ cst) {
+  using Sh = Shape<U, NX, BF16>;
+  using frag = typename FragT<BF16>::type;
+  constexpr int U4 = Sh::U4, KPL = Sh::KPL, NKS = Sh::NKS, NMT = Sh::NMT;
+  extern __shared__ __attribute__((aligned(16))) int2 ids_all[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane >> 4, n = lane & 15;
+  const int dir = blockIdx.y;
+  const int ntiles = (S + 15) / 16;
+  const int tile = blockIdx.x * 4 + wave;
+  int2* ids = ids_all + wave * 16 * L;
+  // stage (word, pos1 | pos2 << 16) of the wave's 16 sequences into LDS
+  for (int i = lane; i < 16 * L; i += 64) {
+    int sn = i / L, t = i - sn * L;
+    int sq = tile * 16 + sn;
+    int2 v = make_int2(0, 0);
+    if (tile < ntiles && sq < S) {
+      long r = (long)inst[sq] * L + t;
+      v.x = word[r];
+      v.y = pos1[r] | (pos2[r] << 16);
+    }
+    ids[i] = v;
+  }
+  wave_lds_sync();
+  if (tile >= ntiles) return;
+  const int seq = tile * 16 + n;
+  const bool valid = seq < S;
+
+  frag A[NMT][NKS];
+  const frag* ap = apack + (size_t)dir * NMT * NKS * 64;
+#pragma unroll
+  for (int m = 0; m < NMT; ++m)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) A[m][ks] = ap[(m * NKS + ks) * 64 + lane];
+  float bm[NMT][4];
+#pragma unroll
+  for (int m = 0; m < NMT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bm[m][r] = bias[dir * 4 * U + r * U + 4 * m + q];
+
+  float h[U4], c[U4];
+#pragma unroll
+  for (int m = 0; m < U4; ++m) h[m] = c[m] = 0.f;
+
+  auto load_x = [&](int t, float* xv) {
+    int2 id = ids[n * L + t];
+#pragma unroll
+    for (int xi = 0; xi < NX; ++xi)
+      xv[xi] = gather_x(4 * xi + q, id.x, id.y & 0xffff, id.y >> 16, wemb, E, p1emb, p2emb, PD);
+  };
+  float xv[NX], xn[NX];
+  load_x(dir ? L - 1 : 0, xv);
+  for (int tau = 0; tau < L; ++tau) {
+    const int t = dir ? (L - 1 - tau) : tau;
+    if (tau + 1 < L) load_x(dir ? (L - 2 - tau) : (tau + 1), xn);
+    frag B[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      B[ks] = fzero<BF16>();
+#pragma unroll
+      for (int j = 0; j < KPL; ++j) {
+        const int idx = ks * KPL + j;
+        if (idx < U4)
+          fset<BF16>(B[ks], j, h[idx]);
+        else if (idx - U4 < NX)
+          fset<BF16>(B[ks], j, xv[idx - U4]);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < NMT; ++m) {
+      f32x4_t acc = {bm[m][0], bm[m][1], bm[m][2], bm[m][3]};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) acc = mma(A[m][ks], B[ks], acc);
+      const float ig = sigmoidf_(acc[0]), jg = tanhf_(acc[1]), fg = sigmoidf_(acc[2] + 1.0f),
+                  og = sigmoidf_(acc[3]);
+      c[m] = c[m] * fg + ig * jg;
+      float hv = tanhf_(c[m]) * og;
+      if (BF16) hv = round_bf(hv);  // the stored / recurrent operand value
+      h[m] = hv;
+    }
+    if (valid) {
+      const long o = ((long)seq * L + t) * (2 * U) + dir * U + q;
+#pragma unroll
+      for (int m = 0; m < U4; ++m) hout[o + 4 * m] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
+    }
+    if (cst) {
+      float* cp = cst + (((size_t)tile * 2 + dir) * L + t) * U4 * 64 + lane;
+#pragma unroll
+      for (int m = 0; m < U4; ++m) cp[m * 64] = c[m];
+    }
+#pragma unroll
+    for (int xi = 0; xi < NX; ++xi) xv[xi] = xn[xi];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------------
+// dW slab layout per (block, dir): D[gc][f], gc in [0, 4U), f in [0, DIN + U + 1) where
+// f < DIN are x features, DIN..DIN+U-1 the h units and DIN+U the bias.
+template <int U, int NX, bool BF16>
+__global__ __launch_bounds__(256) void lstm_bwd_kernel(
+    const int* __restrict__ inst, int S, const int* __restrict__ word, const int* __restrict__ pos1,
+    const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
+    const float* __restrict__ p1emb, const float* __restrict__ p2emb, int PD,
+    const typename FragT<BF16>::type* __restrict__ apack, const typename FragT<BF16>::type* __restrict__ a2pack,
+    const float* __restrict__ bias, const typename FragT<BF16>::elem* __restrict__ hraw,
+    const float* __restrict__ cst, const float* __restrict__ dH, float* __restrict__ dw_slab,
+    float* __restrict__ dpos_slab, float* __restrict__ dwemb) {
+  using Sh = Shape<U, NX, BF16>;
+  using frag = typename FragT<BF16>::type;
+  using elem = typename FragT<BF16>::elem;
+  constexpr int U4 = Sh::U4, KPL = Sh::KPL, NKS = Sh::NKS, NMT = Sh::NMT, NMT2 = Sh::NMT2,
+                NKS2 = Sh::NKS2, G4 = Sh::G4, GT = Sh::GT, RS = Sh::RS;
+  const int DIN = E + 2 * PD;
+  const int NF = DIN + U + 1;            // dW feature columns (incl. bias)
+  const int FT = (NF + 15) / 16;         // dW N-tiles (runtime, <= FTMAX)
+  constexpr int FTMAX = (4 * NX + U + 1 + 15) / 16;
+  constexpr int NA = NMT * NKS * 64, NA2 = NMT2 * NKS2 * 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane >> 4, n = lane & 15;
+  const int dir = blockIdx.y;
+  const int ntiles = (S + 15) / 16;
+  const int ngroups = (ntiles + 3) / 4;
+  const int P2 = 2 * L;  // pos table rows
+
+  // ---- LDS carve: [A packs][bias 4U][xpose 4 waves x XROWS x RS][dpos 2*P2*PD]
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  frag* lA = reinterpret_cast<frag*>(smem);
+  frag* lA2 = lA + NA;
+  float* lbias = reinterpret_cast<float*>(lA2 + NA2);
+  size_t off = (size_t)(NA + NA2) * sizeof(frag) + 4 * U * sizeof(float);
+  off = (off + 15) & ~(size_t)15;
+  constexpr int XROWS = GT * 16 + FTMAX * 16;
+  elem* xp_all = reinterpret_cast<elem*>(smem + off);
+  elem* dgT = xp_all + (size_t)wave * XROWS * RS;
+  elem* xhT = dgT + GT * 16 * RS;
+  {
+    size_t xp = (size_t)4 * XROWS * RS * sizeof(elem);
+    const size_t red = (size_t)G4 * (4 * NX + U + 1) * sizeof(float);
+    off += xp > red ? xp : red;
+  }
+  off = (off + 15) & ~(size_t)15;
+  float* dpos_lds = reinterpret_cast<float*>(smem + off);
+  for (int i = threadIdx.x; i < NA; i += 256) lA[i] = apack[(size_t)dir * NA + i];
+  for (int i = threadIdx.x; i < NA2; i += 256) lA2[i] = a2pack[(size_t)dir * NA2 + i];
+  for (int i = threadIdx.x; i < 4 * U; i += 256) lbias[i] = bias[dir * 4 * U + i];
+  for (int i = threadIdx.x; i < 2 * P2 * PD; i += 256) dpos_lds[i] = 0.f;
+  // zero the wave's transpose buffers once (pad rows / columns stay zero; bias row = 1)
+  for (int i = lane; i < XROWS * RS; i += 64) dgT[i] = to_elem(0.f, (elem*)nullptr);
+  wave_lds_sync();
+  for (int i = lane; i < 32; i += 64) xhT[(DIN + U) * RS + i] = to_elem(1.f, (elem*)nullptr);
+  __syncthreads();
+
+  f32x4_t accw[GT][FTMAX];
+#pragma unroll
+  for (int a = 0; a < GT; ++a)
+#pragma unroll
+    for (int b = 0; b < FTMAX; ++b) accw[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int tile = g * 4 + wave;
+    if (tile >= ntiles) continue;  // no block-level barrier inside the group loop
+    const int seq = tile * 16 + n;
+    const bool valid = seq < S;
+    const long rowbase = valid ? (long)inst[seq] * L : 0;
+    const float* cbase = cst + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
+    float dh_rec[U4], dc_rec[U4], ccur[U4];
+#pragma unroll
+    for (int m = 0; m < U4; ++m) {
+      dh_rec[m] = dc_rec[m] = 0.f;
+      ccur[m] = cbase[((size_t)(dir ? 0 : L - 1) * U4 + m) * 64];
+    }
+    for (int tau = L - 1; tau >= 0; --tau) {
+      const int t = dir ? (L - 1 - tau) : tau;
+      const int tp = dir ? t + 1 : t - 1;  // time index of the previous processing step
+      const bool has_prev = tau > 0;
+      // ---- loads
+      const int wid = word[rowbase + t];
+      const int p1 = pos1[rowbase + t], p2 = pos2[rowbase + t];
+      float xv[NX];
+#pragma unroll
+      for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(4 * xi + q, wid, p1, p2, wemb, E, p1emb, p2emb, PD);
+      float hp[U4], cprev[U4], dhin[U4];
+#pragma unroll
+      for (int m = 0; m < U4; ++m) {
+        cprev[m] = has_prev ? cbase[((size_t)tp * U4 + m) * 64] : 0.f;
+        hp[m] = (has_prev && valid) ? from_elem(hraw[((long)seq * L + tp) * (2 * U) + dir * U + 4 * m + q]) : 0.f;
+        dhin[m] = valid ? dH[((long)seq * L + t) * (2 * U) + dir * U + 4 * m + q] : 0.f;
+      }
+      // ---- recompute gates
+      frag B[NKS];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        B[ks] = fzero<BF16>();
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+          const int idx = ks * KPL + j;
+          if (idx < U4)
+            fset<BF16>(B[ks], j, hp[idx]);
+          else if (idx - U4 < NX)
+            fset<BF16>(B[ks], j, xv[idx - U4]);
+        }
+      }
+      float dg[U4][4];
+#pragma unroll
+      for (int m = 0; m < NMT; ++m) {
+        f32x4_t acc = {lbias[0 * U + 4 * m + q], lbias[1 * U + 4 * m + q], lbias[2 * U + 4 * m + q],
+                       lbias[3 * U + 4 * m + q]};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) acc = mma(lA[(m * NKS + ks) * 64 + lane], B[ks], acc);
+        const float ig = sigmoidf_(acc[0]), jg = tanhf_(acc[1]), fg = sigmoidf_(acc[2] + 1.0f),
+                    og = sigmoidf_(acc[3]);
+        const float tc = tanhf_(ccur[m]);
+        const float dh = dh_rec[m] + dhin[m];
+        const float dc = dc_rec[m] + dh * og * (1.f - tc * tc);
+        const float di = dc * jg, dj = dc * ig, df = dc * cprev[m], d_o = dh * tc;
+        dc_rec[m] = dc * fg;
+        dg[m][0] = di * ig * (1.f - ig);
+        dg[m][1] = dj * (1.f - jg * jg);
+        dg[m][2] = df * fg * (1.f - fg);
+        dg[m][3] = d_o * og * (1.f - og);
+        ccur[m] = cprev[m];
+      }
+      // ---- d[x;h] = W dG
+      frag B2[NKS2];
+#pragma unroll
+      for (int ks = 0; ks < NKS2; ++ks) {
+        B2[ks] = fzero<BF16>();
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+          const int idx = ks * KPL + j;
+          if (idx < 4 * U4) fset<BF16>(B2[ks], j, dg[idx >> 2][idx & 3]);
+        }
+      }
+      float dslot[NMT2 * 4];
+#pragma unroll
+      for (int mt = 0; mt < NMT2; ++mt) {
+        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NKS2; ++ks) acc = mma(lA2[(mt * NKS2 + ks) * 64 + lane], B2[ks], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dslot[mt * 4 + r] = acc[r];
+      }
+#pragma unroll
+      for (int m = 0; m < U4; ++m) dh_rec[m] = dslot[m];
+      // x-feature gradients -> pos tables (LDS atomics) / word table (global atomics)
+      if (valid) {
+#pragma unroll
+        for (int xi = 0; xi < NX; ++xi) {
+          const int f = 4 * xi + q;
+          const float v = dslot[U4 + xi];
+          if (f < E) {
+            if (dwemb) atomicAdd(&dwemb[(long)wid * E + f], v);
+          } else if (f < E + PD) {
+            atomicAdd(&dpos_lds[p1 * PD + (f - E)], v);
+          } else if (f < E + 2 * PD) {
+            atomicAdd(&dpos_lds[(P2 + p2) * PD + (f - E - PD)], v);
+          }
+        }
+      }
+      // ---- stage (dG, XH) for the dW MFMA: sample column = n + 16 * (tau & 1)
+      const int scol = n + 16 * (tau & 1);
+#pragma unroll
+      for (int m = 0; m < U4; ++m)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+          dgT[(g4 * U + 4 * m + q) * RS + scol] = to_elem(dg[m][g4], (elem*)nullptr);
+#pragma unroll
+      for (int m = 0; m < U4; ++m) xhT[(DIN + 4 * m + q) * RS + scol] = to_elem(hp[m], (elem*)nullptr);
+#pragma unroll
+      for (int xi = 0; xi < NX; ++xi) {
+        const int f = 4 * xi + q;
+        if (f < DIN) xhT[f * RS + scol] = to_elem(xv[xi], (elem*)nullptr);
+      }
+      if ((tau & 1) == 0) {
+        // chunk {tau+1, tau} complete (columns 16..31 hold tau+1, 0..15 hold tau).  With L odd
+        // the first chunk (tau = L-1) is half filled; the other half is zero because every
+        // flush clears the lane's dG columns below.
+        wave_lds_sync();
+        if constexpr (BF16) {
+#pragma unroll
+          for (int a = 0; a < GT; ++a) {
+            const u16x8_t fa = *reinterpret_cast<const u16x8_t*>(&dgT[(a * 16 + n) * RS + 8 * q]);
+#pragma unroll
+            for (int b = 0; b < FTMAX; ++b) {
+              if (b < FT) {
+                const u16x8_t fb = *reinterpret_cast<const u16x8_t*>(&xhT[(b * 16 + n) * RS + 8 * q]);
+                accw[a][b] = mfma_bf16(fa, fb, accw[a][b]);
+              }
+            }
+          }
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk) {
+#pragma unroll
+            for (int a = 0; a < GT; ++a) {
+              const float fa = dgT[(a * 16 + n) * RS + 4 * kk + q];
+#pragma unroll
+              for (int b = 0; b < FTMAX; ++b) {
+                if (b < FT) {
+                  const float fb = xhT[(b * 16 + n) * RS + 4 * kk + q];
+                  accw[a][b] = mfma_f32(fa, fb, accw[a][b]);
+                }
+              }
+            }
+          }
+        }
+        wave_lds_sync();
+        // clear the sample columns so a half-filled tail chunk contributes nothing stale
+#pragma unroll
+        for (int m = 0; m < U4; ++m)
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            dgT[(g4 * U + 4 * m + q) * RS + n] = to_elem(0.f, (elem*)nullptr);
+            dgT[(g4 * U + 4 * m + q) * RS + n + 16] = to_elem(0.f, (elem*)nullptr);
+          }
+        wave_lds_sync();
+      }
+    }
+  }
+  // ---- reduce dW across the 4 waves through LDS (reuse the transpose region as f32)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(xp_all);
+  const int REDN = G4 * NF;
+  for (int i = threadIdx.x; i < REDN; i += 256) red[i] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < GT; ++a)
+#pragma unroll
+    for (int b = 0; b < FTMAX; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gc = a * 16 + 4 * q + r, f = b * 16 + n;
+        if (b < FT && gc < G4 && f < NF) atomicAdd(&red[gc * NF + f], accw[a][b][r]);
+      }
+  __syncthreads();
+  float* slab = dw_slab + ((size_t)blockIdx.x * 2 + dir) * REDN;
+  for (int i = threadIdx.x; i < REDN; i += 256) slab[i] = red[i];
+  float* ps = dpos_slab + ((size_t)blockIdx.x * 2 + dir) * 2 * P2 * PD;
+  for (int i = threadIdx.x; i < 2 * P2 * PD; i += 256) ps[i] = dpos_lds[i];
+}
+
+// ------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------
+namespace ina {
+
+struct LstmArgs {
+  const int* inst;
+  int S;
+  const int* word;
+  const int* pos1;
+  const int* pos2;
+  int L;
+  const float* wemb;
+  int E;
+  const float* p1emb;
+  const float* p2emb;
+  int PD;
+  const void* apack;
+  const void* a2pack;
+  const float* bias;
+  void* hraw;
+  float* cst;
+  const float* dH;
+  float* dw_slab;
+  float* dpos_slab;
+  float* dwemb;
+  int bwd_blocks;
+};
+
+size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD) {
+  const int KPL = bf16 ? 8 : 1;
+  const int U4 = U / 4, NSLOT = U4 + NX;
+  const int NA = U4 * ((NSLOT + KPL - 1) / KPL) * 64;
+  const int NA2 = ((NSLOT + 3) / 4) * ((4 * U4 + KPL - 1) / KPL) * 64;
+  const int fragb = bf16 ? 16 : 4;
+  const int GT = (4 * U + 15) / 16;
+  const int FTMAX = (4 * NX + U + 1 + 15) / 16;
+  const int RS = bf16 ? 40 : 36;
+  size_t off = (size_t)(NA + NA2) * fragb + 4 * U * 4;
+  off = (off + 15) & ~(size_t)15;
+  size_t xp = (size_t)4 * (GT * 16 + FTMAX * 16) * RS * (bf16 ? 2 : 4);
+  const size_t red = (size_t)4 * U * (4 * NX + U + 1) * 4;
+  off += xp > red ? xp : red;
+  off = (off + 15) & ~(size_t)15;
+  off += (size_t)2 * 2 * L * PD * 4;
+  return off;
+}
+
+template <int U, int NX, bool BF16>
+static int launch_fwd_t(const LstmArgs& a, hipStream_t st) {
+  using frag = typename FragT<BF16>::type;
+  using elem = typename FragT<BF16>::elem;
+  const int ntiles = (a.S + 15) / 16;
+  dim3 grid((ntiles + 3) / 4, 2);
+  size_t lds = (size_t)4 * 16 * a.L * sizeof(int2);
+  hipLaunchKernelGGL((lstm_fwd_kernel<U, NX, BF16>), grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1,
+                     a.pos2, a.L, a.wemb, a.E, a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, a.bias,
+                     (elem*)a.hraw, a.cst);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int U, int NX, bool BF16>
+static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
+  using frag = typename FragT<BF16>::type;
+  using elem = typename FragT<BF16>::elem;
+  dim3 grid(a.bwd_blocks, 2);
+  size_t lds = lstm_bwd_lds_bytes(U, NX, BF16, a.L, a.PD);
+  auto kfn = lstm_bwd_kernel<U, NX, BF16>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kfn, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
+                     a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, (const frag*)a.a2pack, a.bias,
+                     (const elem*)a.hraw, a.cst, a.dH, a.dw_slab, a.dpos_slab, a.dwemb);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+#define INA_LSTM_DISPATCH(FN)                                                        \
+  if (bf16) {                                                                        \
+    if (U == 20 && NX == 4) return FN<20, 4, true>(a, st);                           \
+    if (U == 20 && NX == 16) return FN<20, 16, true>(a, st);                         \
+    if (U == 32 && NX == 4) return FN<32, 4, true>(a, st);                           \
+    if (U == 32 && NX == 16) return FN<32, 16, true>(a, st);                         \
+    if (U == 8 && NX == 4) return FN<8, 4, true>(a, st);                             \
+  } else {                                                                           \
+    if (U == 20 && NX == 4) return FN<20, 4, false>(a, st);                          \
+    if (U == 20 && NX == 16) return FN<20, 16, false>(a, st);                        \
+    if (U == 32 && NX == 4) return FN<32, 4, false>(a, st);                          \
+    if (U == 32 && NX == 16) return FN<32, 16, false>(a, st);                        \
+    if (U == 8 && NX == 4) return FN<8, 4, false>(a, st);                            \
+  }                                                                                  \
+  return -1;
+
+int lstm_fwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st) { INA_LSTM_DISPATCH(launch_fwd_t) }
+int lstm_bwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st) { INA_LSTM_DISPATCH(launch_bwd_t) }
+
+bool lstm_supported(int U, int NX) {
+  return (U == 20 || U == 32 || U == 8) && (NX == 4 || NX == 16);
+}
+
+}  // namespace ina

@@ -1,0 +1,416 @@
+// Fused neural-tensor-layer relation module (K7 + K8 of SURVEY 2.3), bf16 MFMA, fp32 accumulate.
+//
+// Reference (model/layer_module.py:8-47, model/graph.py:81-86):
+//   for s in 0..h-1:  S_s = (C @ M[:,:,s]) @ Q^T          [N, NQ]
+//   V = relu(concat_s(S_s)^T)  with column index s*N + c   [NQ, h*N]
+//   probs = sigmoid(V @ w + b),  w [h*N, N], b [N]        ("reference" head)
+// "paper" head (paper Eq.11): probs[q, c] = sigmoid(sum_s w_s relu(T[q, s, c]) + b).
+//
+// One wave per episode; the 200 tiny GEMMs of the reference become one chained MFMA pipeline per
+// slice pair, entirely in registers:
+//   P_s^T[b, c] = M_s^T[b, a] C^T[a, c]                          (M pre-packed per step)
+//   T_s[c, q]   = P_s[c, b] Q^T[b, q]      P^T accumulator reused as the A operand
+//   logits[q,c']+= relu(T)[(s,c), q]^T w[(s,c), c']   relu(T) accumulators of TWO slices form one
+//                                                      32-deep K step
+// An accumulator tile X (rows 4*(l>>4)+r, column l&15) used as an operand contracts over X's ROW
+// index; two tiles are paired into one K=32 fragment with k = 8q + j <-> row 16*(j>>2) + 4q + (j&3)
+// ("kmap32").  Every memory operand that meets such a fragment is packed with the same map.
+// The backward recomputes P/T and produces dC, dQ (registers, summed over slices), the per-episode
+// dw contribution and dP (bf16, for the dM = C^T dP reduction GEMM across episodes).
+#include "ina_common.h"
+
+using namespace ina;
+
+namespace {
+
+INA_DEVICE u16x8_t pack2(const f32x4_t& x0, const f32x4_t& x1) {
+  u16x8_t f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[j] = f2bf(x0[j]);
+    f[4 + j] = f2bf(x1[j]);
+  }
+  return f;
+}
+INA_DEVICE f32x4_t relu4(const f32x4_t& x) {
+  return f32x4_t{fmaxf(x[0], 0.f), fmaxf(x[1], 0.f), fmaxf(x[2], 0.f), fmaxf(x[3], 0.f)};
+}
+INA_DEVICE int kmap32(int q, int j) { return 16 * (j >> 2) + 4 * q + (j & 3); }
+constexpr f32x4_t Z4 = {0.f, 0.f, 0.f, 0.f};
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+template <int MTH, int QT, bool PAPER>
+__global__ __launch_bounds__(256) void ntn_fwd_kernel(const float* __restrict__ cls, const float* __restrict__ e, int E,
+                                                      int N, int K, int Q, int H, int h,
+                                                      const u16x8_t* __restrict__ mpack,
+                                                      const u16x8_t* __restrict__ wpack,
+                                                      const float* __restrict__ wvec, const float* __restrict__ bias,
+                                                      float* __restrict__ probs) {
+  constexpr int NKA = (MTH + 1) / 2;  // K steps over a (32 each)
+  constexpr int NKB = (MTH + 1) / 2;  // K steps over b (pairs of accumulator tiles)
+  const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  const int NQ = N * Q;
+  for (int ep = gw; ep < E; ep += nw) {
+    const long rq0 = (long)ep * (N * K + NQ) + N * K;
+    u16x8_t Cf[NKA];
+#pragma unroll
+    for (int ka = 0; ka < NKA; ++ka)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int a = 32 * ka + 8 * q + j;
+        Cf[ka][j] = (n < N && a < H) ? f2bf(cls[((long)ep * N + n) * H + a]) : (unsigned short)0;
+      }
+    u16x8_t Qf[QT][NKB];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int qi = 16 * qt + n, b = 32 * kb + kmap32(q, j);
+          Qf[qt][kb][j] = (qi < NQ && b < H) ? f2bf(e[(rq0 + qi) * H + b]) : (unsigned short)0;
+        }
+    f32x4_t Lg[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) Lg[qt] = Z4;
+    const int npair = (h + 1) / 2;
+    for (int p = 0; p < npair; ++p) {
+      f32x4_t V[2][QT];
+#pragma unroll
+      for (int sl = 0; sl < 2; ++sl) {
+        const int s = 2 * p + sl;
+        if (s >= h) {
+#pragma unroll
+          for (int qt = 0; qt < QT; ++qt) V[sl][qt] = Z4;
+          continue;
+        }
+        f32x4_t PT[2 * NKB];
+#pragma unroll
+        for (int mb = 0; mb < 2 * NKB; ++mb) {
+          PT[mb] = Z4;
+          if (mb < MTH) {
+#pragma unroll
+            for (int ka = 0; ka < NKA; ++ka) PT[mb] = mfma_bf16(mpack[((s * MTH + mb) * NKA + ka) * 64 + lane], Cf[ka], PT[mb]);
+          }
+        }
+        u16x8_t PTf[NKB];
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) PTf[kb] = pack2(PT[2 * kb], PT[2 * kb + 1]);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+          f32x4_t T = Z4;
+#pragma unroll
+          for (int kb = 0; kb < NKB; ++kb) T = mfma_bf16(PTf[kb], Qf[qt][kb], T);
+          if (PAPER) {
+            const float ws = wvec[s];
+            const f32x4_t R = relu4(T);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Lg[qt][r] += ws * R[r];
+          } else {
+            V[sl][qt] = relu4(T);
+          }
+        }
+      }
+      if (!PAPER) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) Lg[qt] = mfma_bf16(pack2(V[0][qt], V[1][qt]), wpack[p * 64 + lane], Lg[qt]);
+      }
+    }
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (PAPER) {  // rows c, cols query
+          const int c = 4 * q + r, qi = 16 * qt + n;
+          if (c < N && qi < NQ) probs[((long)ep * NQ + qi) * N + c] = sigmoidf_(Lg[qt][r] + bias[0]);
+        } else {      // rows query, cols c'
+          const int qi = 16 * qt + 4 * q + r, c = n;
+          if (c < N && qi < NQ) probs[((long)ep * NQ + qi) * N + c] = sigmoidf_(Lg[qt][r] + bias[c]);
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Outputs: dcls [E,N,H]; de query rows [S,H]; dp_out bf16 [E*N][h*H] (col s*H + b);
+//          dw_slab [E][h][N][N] (reference head) or [E][h] (paper head).
+template <int MTH, int QT, bool PAPER>
+__global__ __launch_bounds__(256) void ntn_bwd_kernel(
+    const float* __restrict__ cls, const float* __restrict__ e, int E, int N, int K, int Q, int H, int h,
+    const u16x8_t* __restrict__ mpack, const u16x8_t* __restrict__ m2pack, const u16x8_t* __restrict__ wtpack,
+    const float* __restrict__ wvec, const float* __restrict__ dz, float* __restrict__ dcls, float* __restrict__ de,
+    unsigned short* __restrict__ dp_out, float* __restrict__ dw_slab) {
+  constexpr int NKA = (MTH + 1) / 2, NKB = (MTH + 1) / 2, KQ = (QT + 1) / 2;
+  const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  const int NQ = N * Q;
+  const long hH = (long)h * H;
+  for (int ep = gw; ep < E; ep += nw) {
+    const long rq0 = (long)ep * (N * K + NQ) + N * K;
+    const float* dze = dz + (long)ep * NQ * N;
+    u16x8_t Cf[NKA];
+#pragma unroll
+    for (int ka = 0; ka < NKA; ++ka)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int a = 32 * ka + 8 * q + j;
+        Cf[ka][j] = (n < N && a < H) ? f2bf(cls[((long)ep * N + n) * H + a]) : (unsigned short)0;
+      }
+    u16x8_t Qf[QT][NKB];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int qi = 16 * qt + n, b = 32 * kb + kmap32(q, j);
+          Qf[qt][kb][j] = (qi < NQ && b < H) ? f2bf(e[(rq0 + qi) * H + b]) : (unsigned short)0;
+        }
+    // Q^T as the A operand over queries: A[i = b][k = query (kmap32)]
+    u16x8_t QTf[MTH][KQ];
+#pragma unroll
+    for (int mb = 0; mb < MTH; ++mb)
+#pragma unroll
+      for (int kq = 0; kq < KQ; ++kq)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int b = 16 * mb + n, qi = 32 * kq + kmap32(q, j);
+          QTf[mb][kq][j] = (qi < NQ && b < H) ? f2bf(e[(rq0 + qi) * H + b]) : (unsigned short)0;
+        }
+    u16x8_t dzA[QT];           // A[i = query][k = c']
+    u16x8_t dzB[KQ];           // B[k = query (kmap32)][j = c']
+    f32x4_t dzC[QT], dzR[QT];  // accumulator layouts: dzC rows c / cols query, dzR rows query / cols c
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int qi = 16 * qt + n, cp = 8 * q + j;
+        dzA[qt][j] = (qi < NQ && cp < N) ? f2bf(dze[qi * N + cp]) : (unsigned short)0;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = 4 * q + r, qi = 16 * qt + n;
+        dzC[qt][r] = (c < N && qi < NQ) ? dze[qi * N + c] : 0.f;
+        const int qr = 16 * qt + 4 * q + r;
+        dzR[qt][r] = (n < N && qr < NQ) ? dze[qr * N + n] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int kq = 0; kq < KQ; ++kq)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int qi = 32 * kq + kmap32(q, j);
+        dzB[kq][j] = (qi < NQ && n < N) ? f2bf(dze[qi * N + n]) : (unsigned short)0;
+      }
+    f32x4_t dCT[MTH], dQT[MTH][QT];
+#pragma unroll
+    for (int m = 0; m < MTH; ++m) {
+      dCT[m] = Z4;
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) dQT[m][qt] = Z4;
+    }
+    const int npair = (h + 1) / 2;
+    for (int p = 0; p < npair; ++p) {
+      f32x4_t Ps[2][MTH], dTs[2][QT];
+#pragma unroll
+      for (int sl = 0; sl < 2; ++sl) {
+        const int s = 2 * p + sl;
+#pragma unroll
+        for (int m = 0; m < MTH; ++m) Ps[sl][m] = Z4;
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) dTs[sl][qt] = Z4;
+        if (s >= h) continue;
+        // P^T (rows b, cols c) and P (rows c, cols b) from the same fragments (operand swap)
+        f32x4_t PT[2 * NKB];
+#pragma unroll
+        for (int mb = 0; mb < 2 * NKB; ++mb) {
+          PT[mb] = Z4;
+          if (mb < MTH) {
+#pragma unroll
+            for (int ka = 0; ka < NKA; ++ka) {
+              const u16x8_t mf = mpack[((s * MTH + mb) * NKA + ka) * 64 + lane];
+              PT[mb] = mfma_bf16(mf, Cf[ka], PT[mb]);
+              Ps[sl][mb] = mfma_bf16(Cf[ka], mf, Ps[sl][mb]);
+            }
+          }
+        }
+        u16x8_t PTf[NKB];
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) PTf[kb] = pack2(PT[2 * kb], PT[2 * kb + 1]);
+        u16x8_t wt;
+        float ws = 0.f;
+        if (PAPER) {
+          ws = wvec[s];
+        } else {
+          wt = wtpack[(long)s * 64 + lane];
+        }
+        f32x4_t VT[2 * KQ], dTT[2 * KQ];
+#pragma unroll
+        for (int i = 0; i < 2 * KQ; ++i) VT[i] = dTT[i] = Z4;
+        float dwp = 0.f;
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+          f32x4_t T = Z4, TT = Z4;
+#pragma unroll
+          for (int kb = 0; kb < NKB; ++kb) {
+            T = mfma_bf16(PTf[kb], Qf[qt][kb], T);    // rows c, cols query
+            TT = mfma_bf16(Qf[qt][kb], PTf[kb], TT);  // rows query, cols c
+          }
+          f32x4_t dV, dVT;
+          if (PAPER) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              dV[r] = ws * dzC[qt][r];
+              dVT[r] = ws * dzR[qt][r];
+              dwp += fmaxf(TT[r], 0.f) * dzR[qt][r];
+            }
+          } else {
+            dV = mfma_bf16(wt, dzA[qt], Z4);   // rows c, cols query
+            dVT = mfma_bf16(dzA[qt], wt, Z4);  // rows query, cols c
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dTs[sl][qt][r] = T[r] > 0.f ? dV[r] : 0.f;
+            dTT[qt][r] = TT[r] > 0.f ? dVT[r] : 0.f;
+          }
+          VT[qt] = relu4(TT);
+        }
+        // per-episode dw contribution
+        if (PAPER) {
+          dwp = wave_sum(dwp);
+          if (lane == 0) dw_slab[(long)ep * h + s] = dwp;
+        } else {
+          f32x4_t dw = Z4;
+#pragma unroll
+          for (int kq = 0; kq < KQ; ++kq) dw = mfma_bf16(pack2(VT[2 * kq], VT[2 * kq + 1]), dzB[kq], dw);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = 4 * q + r;
+            if (c < N && n < N) dw_slab[(((long)ep * h + s) * N + c) * N + n] = dw[r];
+          }
+        }
+        // dP^T[b, c] = sum_q Q[q, b] dT[c, q]
+        f32x4_t dPT[2 * NKB];
+#pragma unroll
+        for (int mb = 0; mb < 2 * NKB; ++mb) {
+          dPT[mb] = Z4;
+          if (mb < MTH) {
+#pragma unroll
+            for (int kq = 0; kq < KQ; ++kq) dPT[mb] = mfma_bf16(QTf[mb][kq], pack2(dTT[2 * kq], dTT[2 * kq + 1]), dPT[mb]);
+          }
+        }
+        // dC^T[a, c] += sum_b M[a, b, s] dP[c, b]
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+          const u16x8_t dPf = pack2(dPT[2 * kb], dPT[2 * kb + 1]);
+#pragma unroll
+          for (int ma = 0; ma < MTH; ++ma) dCT[ma] = mfma_bf16(m2pack[((s * MTH + ma) * NKB + kb) * 64 + lane], dPf, dCT[ma]);
+        }
+        // dP -> bf16 [E*N][h*H] for the dM reduction GEMM
+        if (n < N) {
+#pragma unroll
+          for (int mb = 0; mb < MTH; ++mb) {
+            const int b0 = 16 * mb + 4 * q;
+            if (b0 < H) {
+              u16x4_t v = {f2bf(dPT[mb][0]), f2bf(dPT[mb][1]), f2bf(dPT[mb][2]), f2bf(dPT[mb][3])};
+              *reinterpret_cast<u16x4_t*>(dp_out + ((long)ep * N + n) * hH + (long)s * H + b0) = v;
+            }
+          }
+        }
+      }
+      // dQ^T[b, q] += sum_{s in pair, c} P_s[c, b] dT_s[c, q]
+#pragma unroll
+      for (int nb = 0; nb < MTH; ++nb) {
+        const u16x8_t Pf = pack2(Ps[0][nb], Ps[1][nb]);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) dQT[nb][qt] = mfma_bf16(Pf, pack2(dTs[0][qt], dTs[1][qt]), dQT[nb][qt]);
+      }
+    }
+    // write dC (rows a, cols c) and dQ (rows b, cols query)
+#pragma unroll
+    for (int ma = 0; ma < MTH; ++ma) {
+      const int a0 = 16 * ma + 4 * q;
+      if (n < N && a0 < H) *reinterpret_cast<f32x4_t*>(dcls + ((long)ep * N + n) * H + a0) = dCT[ma];
+    }
+#pragma unroll
+    for (int nb = 0; nb < MTH; ++nb)
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        const int b0 = 16 * nb + 4 * q, qi = 16 * qt + n;
+        if (qi < NQ && b0 < H) *reinterpret_cast<f32x4_t*>(de + (rq0 + qi) * H + b0) = dQT[nb][qt];
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+namespace ina {
+
+struct NtnArgs {
+  const float* cls;
+  const float* e;
+  int E, N, K, Q, H, h;
+  const void* mpack;
+  const void* m2pack;
+  const void* wpack;
+  const void* wtpack;
+  const float* wvec;
+  const float* bias;
+  float* probs;
+  const float* dz;
+  float* dcls;
+  float* de;
+  void* dp_out;
+  float* dw_slab;
+  int blocks;
+  int paper;
+};
+
+template <int MTH, int QT, bool P>
+static int ntn_fwd_t(const NtnArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((ntn_fwd_kernel<MTH, QT, P>), dim3(a.blocks), dim3(256), 0, st, a.cls, a.e, a.E, a.N, a.K, a.Q, a.H,
+                     a.h, (const u16x8_t*)a.mpack, (const u16x8_t*)a.wpack, a.wvec, a.bias, a.probs);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+template <int MTH, int QT, bool P>
+static int ntn_bwd_t(const NtnArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((ntn_bwd_kernel<MTH, QT, P>), dim3(a.blocks), dim3(256), 0, st, a.cls, a.e, a.E, a.N, a.K, a.Q, a.H,
+                     a.h, (const u16x8_t*)a.mpack, (const u16x8_t*)a.m2pack, (const u16x8_t*)a.wtpack, a.wvec, a.dz,
+                     a.dcls, a.de, (unsigned short*)a.dp_out, a.dw_slab);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+#define INA_NTN_QT(FN, MTH, P)                       \
+  if (QT == 1) return FN<MTH, 1, P>(a, st);          \
+  if (QT == 2) return FN<MTH, 2, P>(a, st);          \
+  if (QT == 4) return FN<MTH, 4, P>(a, st);
+#define INA_NTN_DISPATCH(FN)                                              \
+  const int QT = qt_needed <= 1 ? 1 : (qt_needed <= 2 ? 2 : (qt_needed <= 4 ? 4 : 0)); \
+  if (QT == 0) return -1;                                                 \
+  if (a.paper) {                                                          \
+    if (MTH == 1) { INA_NTN_QT(FN, 1, true) }                             \
+    if (MTH == 3) { INA_NTN_QT(FN, 3, true) }                             \
+    if (MTH == 4) { INA_NTN_QT(FN, 4, true) }                             \
+  } else {                                                                \
+    if (MTH == 1) { INA_NTN_QT(FN, 1, false) }                            \
+    if (MTH == 3) { INA_NTN_QT(FN, 3, false) }                            \
+    if (MTH == 4) { INA_NTN_QT(FN, 4, false) }                            \
+  }                                                                       \
+  return -1;
+
+int ntn_fwd(const NtnArgs& a, hipStream_t st) {
+  const int MTH = (a.H + 15) / 16, qt_needed = (a.N * a.Q + 15) / 16;
+  if (a.N > 16) return -1;
+  INA_NTN_DISPATCH(ntn_fwd_t)
+}
+int ntn_bwd(const NtnArgs& a, hipStream_t st) {
+  const int MTH = (a.H + 15) / 16, qt_needed = (a.N * a.Q + 15) / 16;
+  if (a.N > 16) return -1;
+  INA_NTN_DISPATCH(ntn_bwd_t)
+}
+
+}  // namespace ina

@@ -1,0 +1,84 @@
+// Fused multi-tensor optimizers over ONE flat fp32 parameter buffer (K10 of SURVEY 2.3).
+// The same flat gradient buffer is the data-parallel all-reduce bucket, so the whole update is a
+// single streaming kernel.  Reference: tf.contrib.layers.optimize_loss(optimizer="Adam") with
+// staircase exponential decay (model/base.py:94-99); TF1 Adam update form:
+//   lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t)
+//   m = b1 m + (1 - b1) g ;  v = b2 v + (1 - b2) g^2 ;  p -= lr_t * m / (sqrt(v) + eps)
+// Optional L2 (the reference's dead L2 term, opt-in): g += l2 * p where l2mask[i] != 0.
+// Adagrad (the paper's optimizer, TF1 form): acc += g^2 ; p -= lr * g / sqrt(acc).
+#include "ina_common.h"
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
+                                                   const float* __restrict__ g, const unsigned char* __restrict__ l2mask,
+                                                   long n, float lr_t, float b1, float b2, float eps, float gscale,
+                                                   float l2) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float gi = g[i] * gscale;
+    const float pi = p[i];
+    if (l2mask && l2mask[i]) gi += l2 * pi;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi - lr_t * mi / (sqrtf(vi) + eps);
+  }
+}
+
+__global__ __launch_bounds__(256) void adagrad_kernel(float* __restrict__ p, float* __restrict__ acc,
+                                                      const float* __restrict__ g,
+                                                      const unsigned char* __restrict__ l2mask, long n, float lr,
+                                                      float gscale, float l2) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float gi = g[i] * gscale;
+    const float pi = p[i];
+    if (l2mask && l2mask[i]) gi += l2 * pi;
+    const float a = acc[i] + gi * gi;
+    acc[i] = a;
+    p[i] = pi - lr * gi * rsqrtf(a);
+  }
+}
+
+// Sum `nslab` contiguous slabs of length `len` (fp32) into out (out = sum, or out += sum).
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slabs, long nslab, long len,
+                                                          float* __restrict__ out, int accumulate) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += stride) {
+    float s = 0.f;
+    for (long k = 0; k < nslab; ++k) s += slabs[k * len + i];
+    out[i] = accumulate ? out[i] + s : s;
+  }
+}
+
+namespace ina {
+
+static int grid_for(long n) {
+  long b = (n + 255) / 256;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+int adam_step(float* p, float* m, float* v, const float* g, const unsigned char* l2mask, long n, float lr_t, float b1,
+              float b2, float eps, float gscale, float l2, hipStream_t st) {
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, m, v, g, l2mask, n, lr_t, b1, b2, eps, gscale,
+                     l2);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int adagrad_step(float* p, float* acc, const float* g, const unsigned char* l2mask, long n, float lr, float gscale,
+                 float l2, hipStream_t st) {
+  hipLaunchKernelGGL(adagrad_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, acc, g, l2mask, n, lr, gscale, l2);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int slab_reduce(const float* slabs, long nslab, long len, float* out, int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for(len)), dim3(256), 0, st, slabs, nslab, len, out, accumulate);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace ina

@@ -1,0 +1,171 @@
+"""Single configuration object for the whole engine.
+
+Every knob of the reference is exposed here with the reference's default:
+
+* episode shape N/K/Q and the CLI defaults    -- ``train.py:10-18,24,31-37``
+* model hyper-parameters (``Base.__init__``)  -- ``model/base.py:12-27``
+* routing iterations / NTN slices             -- ``model/layer_module.py:8,101``
+* train-loop cadence                          -- ``model/base.py:115-116``
+* GloVe truncation width                      -- ``util/convert_glove_vec.py:3``
+
+Additions beyond the reference (north star): episode batching, dtype, DP, encoder
+choice, relation-head variant, NOTA rate, L2 opt-in, LR-schedule choice.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+from dataclasses import dataclass, field
+from typing import Optional
+
+
+@dataclass
+class Config:
+    # ---------------- episode shape (train.py:11-12, :33) ----------------
+    model_name: str = "induction"
+    N: int = 5                 # ways
+    K: int = 2                 # shots
+    Q: int = 5                 # queries per class
+    # optional eval-time overrides (None -> same as train)
+    eval_N: Optional[int] = None
+    eval_K: Optional[int] = None
+    eval_Q: Optional[int] = None
+
+    # ---------------- data (train.py:24-27) ----------------
+    max_length: int = 37
+    train_file: str = "./data/train.json"
+    val_file: str = "./data/val.json"
+    word_vec_file: str = "./data/glove.6B.5d.json"
+    case_sensitive: bool = False
+    processed_dir: str = "_processed_data"
+    synthetic: bool = False            # synthetic tokens / random relations
+    synthetic_relations: int = 64
+    synthetic_instances: int = 700
+    synthetic_vocab: int = 400000
+    synthetic_word_dim: int = 5
+
+    # ---------------- model (model/base.py:12-27, train.py:31-37) ----------------
+    hidden_size: int = 20              # LSTM units per direction (u); BiLSTM out = 2u
+    pos_embedding_dim: int = 5         # fixed in reference (base.py:24)
+    init_std: float = 0.1              # tf.random_normal_initializer(stddev=0.1)
+    keep_prob: float = 0.9             # DropoutWrapper output_keep_prob (train)
+    routing_iters: int = 3             # dynamic_routing(iter_routing=3)
+    ntn_slices: int = 100              # neural_tensor_layer(out_size=100)
+    relation_head: str = "reference"   # "reference": W[h*N, N] mixes classes; "paper": per-pair W_r in R^h
+    encoder: str = "bilstm"            # "bilstm" | "bert"
+    lstm_skip_padding: bool = False    # parity: process all L steps
+    train_word_embedding: bool = False # only used when no pretrained table is given
+
+    # BERT encoder (north star); BERT-base defaults
+    bert_layers: int = 12
+    bert_hidden: int = 768
+    bert_heads: int = 12
+    bert_intermediate: int = 3072
+    bert_vocab: int = 30522
+    bert_max_position: int = 512
+
+    # ---------------- optimisation (model/base.py:94-99) ----------------
+    optimizer: str = "adam"            # "adam" (reference) | "adagrad" (paper 4.4)
+    learning_rate: float = 1e-3
+    decay_steps: int = 100
+    decay_rate: float = 0.9
+    staircase: bool = True
+    lr_schedule: str = "exponential"   # "exponential" (reference) | "constant"
+    adam_beta1: float = 0.9
+    adam_beta2: float = 0.999
+    adam_eps: float = 1e-8
+    adagrad_init_acc: float = 0.1
+    l2_lambda: float = 1e-5
+    use_l2: bool = False               # reference computes then discards it (graph.py:108-109)
+    loss_reduction: str = "mean"       # "mean" (reference) | "sum" (paper Eq.12)
+
+    # ---------------- loop cadence (model/base.py:115-116) ----------------
+    train_iter: int = 30000
+    val_iter: int = 1000
+    val_step: int = 2000
+    test_iter: int = 3000
+    log_every: int = 100
+    model_dir: str = "checkpoints/inductionNetwork_test"
+    ckpt_name: str = "inductionNetwork"
+    max_to_keep: int = 5
+    resume: bool = True
+
+    # ---------------- execution ----------------
+    episodes_per_step: int = 1         # B episodes per optimiser step (per rank)
+    dtype: str = "bf16"                # MFMA operand dtype on GPU: "bf16" | "fp32"
+    device: str = "auto"               # "auto" | "cuda" | "cpu"
+    seed: int = 12345
+    deterministic: bool = False
+    use_hip_graph: bool = False
+    nota_rate: float = 0.0             # FewRel 2.0 none-of-the-above probability per query
+    grad_check_finite: bool = True     # NaN/Inf guard on the loss
+    profile: bool = False
+
+    # ------------------------------------------------------------------
+    @property
+    def H(self) -> int:
+        return 2 * self.hidden_size
+
+    @property
+    def eN(self) -> int:
+        return self.eval_N or self.N
+
+    @property
+    def eK(self) -> int:
+        return self.eval_K or self.K
+
+    @property
+    def eQ(self) -> int:
+        return self.eval_Q or self.Q
+
+    def replace(self, **kw) -> "Config":
+        return dataclasses.replace(self, **kw)
+
+    def to_dict(self) -> dict:
+        return dataclasses.asdict(self)
+
+    def to_json(self) -> str:
+        return json.dumps(self.to_dict(), sort_keys=True)
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "Config":
+        names = {f.name for f in dataclasses.fields(cls)}
+        return cls(**{k: v for k, v in d.items() if k in names})
+
+    def validate(self) -> None:
+        if self.N < 1 or self.K < 1 or self.Q < 1:
+            raise ValueError("N, K, Q must be >= 1")
+        if self.hidden_size % 4 != 0:
+            raise ValueError("hidden_size must be a multiple of 4 (lane-ownership layout of the LSTM kernel)")
+        if self.relation_head not in ("reference", "paper"):
+            raise ValueError(f"unknown relation_head {self.relation_head}")
+        if self.dtype not in ("bf16", "fp32"):
+            raise ValueError(f"unknown dtype {self.dtype}")
+        if self.optimizer not in ("adam", "adagrad"):
+            raise ValueError(f"unknown optimizer {self.optimizer}")
+        if self.encoder not in ("bilstm", "bert"):
+            raise ValueError(f"unknown encoder {self.encoder}")
+
+
+def add_cli_args(p) -> None:
+    """Register every Config field as ``--field`` on an argparse parser."""
+    for f in dataclasses.fields(Config):
+        default = f.default if f.default is not dataclasses.MISSING else None
+        flag = "--" + f.name
+        if isinstance(default, bool):
+            p.add_argument(flag, type=lambda s: s.lower() in ("1", "true", "yes", "y"), default=None,
+                           metavar="BOOL")
+        elif default is None:
+            p.add_argument(flag, type=int if f.name.startswith("eval_") else str, default=None)
+        else:
+            p.add_argument(flag, type=type(default), default=None)
+
+
+def config_from_args(args, base: Optional[Config] = None) -> Config:
+    cfg = base or Config()
+    kw = {}
+    for f in dataclasses.fields(Config):
+        v = getattr(args, f.name, None)
+        if v is not None:
+            kw[f.name] = v
+    return cfg.replace(**kw)

@@ -1,0 +1,83 @@
+"""The Induction Network model (reference ``model/graph.py:15-109`` + ``model/base.py``).
+
+GPU path (``device.type == 'cuda'``): two fused autograd functions over hand-written gfx950 kernels
+  EncoderFn  -- embedding gather + BiLSTM + word-level self-attention  (ops/encoder.py)
+  HeadFn     -- dynamic routing + neural tensor layer + sigmoid         (ops/head.py)
+and no fallback: a missing kernel library raises.
+CPU path: the pure-PyTorch oracle (models/reference.py), used for plumbing runs and tests.
+
+N/K/Q are runtime arguments: only the reference head's ``w`` is N-dependent.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+from torch import nn
+
+from ..config import Config
+from . import reference as ref
+from .params import TF_NAMES, InductionParams
+
+GPU_SUPPORTED_U = (8, 20, 32)
+
+
+class InductionNetwork(nn.Module):
+    def __init__(self, cfg: Config, word_vec_mat: Optional[np.ndarray] = None, vocab_size: Optional[int] = None,
+                 seed: int = 0):
+        super().__init__()
+        cfg.validate()
+        self.cfg = cfg
+        self.params = InductionParams(cfg, word_vec_mat, vocab_size, seed)
+
+    # ------------------------------------------------------------------
+    def pdict(self) -> Dict[str, torch.Tensor]:
+        return {a: getattr(self.params, a) for a in TF_NAMES}
+
+    def check_gpu_config(self, N: int, Q: int, L: int) -> None:
+        u = self.cfg.hidden_size
+        din = self.params.input_dim
+        if u not in GPU_SUPPORTED_U:
+            raise NotImplementedError(f"GPU kernels are instantiated for hidden_size in {GPU_SUPPORTED_U}, got {u}")
+        if din > 64:
+            raise NotImplementedError(f"GPU LSTM kernel supports input dim <= 64, got {din}")
+        if L > 64:
+            raise NotImplementedError(f"GPU attention kernel supports max_length <= 64, got {L}")
+        if N > 16 or N * Q > 64:
+            raise NotImplementedError("GPU NTN kernel supports N <= 16 and N*Q <= 64")
+
+    def forward(self, inst: torch.Tensor, data: Tuple[torch.Tensor, ...], B: int, N: int, K: int, Q: int,
+                training: bool = True, dropout_seed: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+        """inst: int32 [B*(N*K+N*Q)] instance rows (episode layout, support first).
+        data: (word, pos1, pos2, mask) [NI, L] int32 on the same device.
+        Returns probs [B, N*Q, N] and alphas [B*(N*K+N*Q), L]."""
+        cfg = self.cfg
+        kp = cfg.keep_prob if training else 1.0
+        p = self.pdict()
+        if self.cfg.relation_head == "reference" and p["ntn_w"].shape[1] != N:
+            raise ValueError(f"reference relation head was built for N={p['ntn_w'].shape[1]}, got N={N} "
+                             "(use relation_head='paper' for N-independent scoring)")
+        if inst.is_cuda:
+            from ..ops.encoder import encode
+            from ..ops.head import head
+            word, pos1, pos2, mask = data
+            self.check_gpu_config(N, Q, word.shape[1])
+            meta = dict(U=cfg.hidden_size, bf16=(cfg.dtype == "bf16"), keep_prob=kp, seed=int(dropout_seed),
+                        word_grad=bool(isinstance(p["word_embedding"], nn.Parameter)
+                                       and p["word_embedding"].requires_grad))
+            e, alphas = encode(inst, data, p, meta)
+            probs = head(e, p, dict(E=B, N=N, K=K, Q=Q, iters=cfg.routing_iters,
+                                    paper=(cfg.relation_head == "paper")))
+            return probs, alphas
+        word, pos1, pos2, mask = (t[inst.long()] for t in data)
+        probs, alphas = ref.forward(p, word, pos1, pos2, mask, B, N, K, Q, cfg.routing_iters, cfg.relation_head,
+                                    kp, int(dropout_seed), bf16=False)
+        return probs, alphas.squeeze(-1)
+
+    # ------------------------------------------------------------------
+    def loss(self, probs: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        return ref.mse_loss(probs, labels.long(), self.cfg.loss_reduction)
+
+    def l2_value(self) -> torch.Tensor:
+        return sum((v.detach() ** 2).sum() / 2 for v in self.params.l2_vars()) * self.cfg.l2_lambda

@@ -1,0 +1,83 @@
+"""Sentence encoder on the GPU path: fused embedding + BiLSTM + self-attention pooling.
+
+One ``torch.autograd.Function`` spans the whole encoder so that the bf16 BiLSTM output never
+crosses an autograd boundary (its gradient stays fp32 inside ``backward``).
+
+forward:  lstm_fwd (gather + MFMA recurrence, both directions)  ->  attn_fwd (dropout regenerated
+          from the counter hash, MFMA projection, masked softmax, pooling)
+backward: attn_bwd (recompute projection, dH, dW1/db1/dw2 slabs)  ->  lstm_bwd (BPTT, dW/db/pos slabs)
+
+Reference layers: model/base.py:76-86 (embedding), model/graph.py:30-53 (BiLSTM + attention),
+model/layer_module.py:49-98 (self_attention).
+"""
+from __future__ import annotations
+
+import torch
+
+from ._ext import ops
+from .packing import lstm_shape, pack_attn, pack_lstm
+
+
+class EncoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, inst, word, pos1, pos2, mask, wemb, p1emb, p2emb, Kf, bf, Kb, bb, W1, b1, w2, meta):
+        """meta = dict(U, bf16, keep_prob, seed, word_grad, lstm_blocks, attn_blocks)."""
+        o = ops()
+        U, bf16 = meta["U"], meta["bf16"]
+        DIN = wemb.shape[1] + 2 * p1emb.shape[1]
+        sh = lstm_shape(U, DIN, bf16)
+        apack, a2pack = pack_lstm(Kf, Kb, U, DIN, bf16)
+        bias = torch.stack([bf.detach(), bb.detach()]).float().contiguous()
+        need_grad = ctx.needs_input_grad[5:15].count(True) > 0 if hasattr(ctx, "needs_input_grad") else True
+        hraw, cst = o.lstm_fwd(inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
+                               p2emb.detach().contiguous(), apack, bias, U, sh["NX"], bf16, bool(need_grad))
+        w1pack, w1tpack = pack_attn(W1, bf16)
+        kp = float(meta["keep_prob"])
+        e, alphas = o.attn_fwd(hraw, inst, mask, w1pack, b1.detach().contiguous(), w2.detach().reshape(-1).contiguous(),
+                               int(meta["seed"]), kp, U, bf16, int(meta.get("attn_blocks", 0)))
+        if need_grad:
+            ctx.save_for_backward(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hraw, cst,
+                                  w1pack, w1tpack, b1, w2, alphas)
+            ctx.meta = dict(meta, NX=sh["NX"], DIN=DIN)
+        ctx.mark_non_differentiable(alphas)
+        return e, alphas
+
+    @staticmethod
+    def backward(ctx, de, _dalpha):
+        o = ops()
+        (inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hraw, cst, w1pack, w1tpack, b1, w2,
+         alphas) = ctx.saved_tensors
+        m = ctx.meta
+        U, bf16, DIN = m["U"], m["bf16"], m["DIN"]
+        H2 = 2 * U
+        dH, aslab = o.attn_bwd(hraw, inst, w1pack, w1tpack, b1.detach().contiguous(),
+                               w2.detach().reshape(-1).contiguous(), int(m["seed"]), float(m["keep_prob"]),
+                               de.contiguous().float(), alphas, U, bf16, int(m.get("attn_blocks", 0)))
+        a = aslab.sum(0)
+        dW1 = a[: H2 * H2].view(H2, H2)
+        db1 = a[H2 * H2: H2 * H2 + H2]
+        dw2 = a[H2 * H2 + H2:].view(H2, 1)
+        word_grad = bool(m.get("word_grad", False))
+        dw_slab, dpos_slab, dwemb = o.lstm_bwd(inst, word, pos1, pos2, wemb.detach().contiguous(),
+                                               p1emb.detach().contiguous(), p2emb.detach().contiguous(), apack, a2pack,
+                                               bias, hraw, cst, dH, U, m["NX"], bf16, word_grad,
+                                               int(m.get("lstm_blocks", 0)))
+        D = dw_slab.sum(0)                         # [2, 4U, DIN+U+1]
+        dKf = D[0, :, : DIN + U].t().contiguous()
+        dKb = D[1, :, : DIN + U].t().contiguous()
+        dbf = D[0, :, DIN + U].contiguous()
+        dbb = D[1, :, DIN + U].contiguous()
+        P = dpos_slab.sum((0, 1))                  # [2 tables, 2L, PD]
+        dp1 = P[0][: p1emb.shape[0]]
+        dp2 = P[1][: p2emb.shape[0]]
+        return (None, None, None, None, None, dwemb if word_grad else None, dp1, dp2, dKf, dbf, dKb, dbb, dW1, db1,
+                dw2, None)
+
+
+def encode(inst, data, params, meta):
+    """data = (word, pos1, pos2, mask) device int32 arrays [NI, L]; returns (e [S, 2u], alphas [S, L])."""
+    word, pos1, pos2, mask = data
+    return EncoderFn.apply(inst, word, pos1, pos2, mask, params["word_embedding"], params["pos1_embedding"],
+                           params["pos2_embedding"], params["lstm_fw_kernel"], params["lstm_fw_bias"],
+                           params["lstm_bw_kernel"], params["lstm_bw_bias"], params["attn_kernel"],
+                           params["attn_bias"], params["attn_w2"], meta)

@@ -1,0 +1,133 @@
+"""Flat-buffer parameter store + fused optimizers (K10 of SURVEY 2.3).
+
+All trainable tensors are views into ONE contiguous fp32 buffer and their ``.grad`` are views into
+ONE contiguous fp32 gradient buffer. That single gradient buffer is the data-parallel all-reduce
+bucket (parallel/dp.py) and the fused optimizer updates the whole model with one kernel.
+
+Reference: model/base.py:94-99 -- ``tf.train.exponential_decay(1e-3, step, 100, 0.9, staircase=True)``
++ ``optimize_loss(..., optimizer="Adam")`` (TF1 Adam defaults, no clipping).
+On CPU the same math runs in torch (plumbing path, BASELINE config 1).
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+from typing import Dict, Optional
+
+import torch
+from torch import nn
+
+from ._ext import ops
+
+
+def lr_at(step: int, base: float, decay_steps: int, decay_rate: float, staircase: bool = True,
+          schedule: str = "exponential") -> float:
+    """tf.train.exponential_decay evaluated at ``global_step = step`` (before the increment)."""
+    if schedule == "constant":
+        return base
+    p = step / decay_steps
+    if staircase:
+        p = math.floor(p)
+    return base * decay_rate ** p
+
+
+class FlatParams:
+    """Re-homes the given parameters into one flat buffer (params and grads)."""
+
+    def __init__(self, named: "OrderedDict[str, nn.Parameter]"):
+        self.names = list(named.keys())
+        self.params = list(named.values())
+        self.shapes = [tuple(p.shape) for p in self.params]
+        self.numels = [p.numel() for p in self.params]
+        self.offsets = []
+        off = 0
+        for n in self.numels:
+            self.offsets.append(off)
+            off += n
+        self.numel = off
+        dev = self.params[0].device if self.params else torch.device("cpu")
+        self.flat = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for p, o, n in zip(self.params, self.offsets, self.numels):
+                self.flat[o:o + n].copy_(p.detach().reshape(-1))
+                p.data = self.flat[o:o + n].view(p.shape)
+                p.grad = self.grad[o:o + n].view(p.shape)
+
+    def view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
+        i = self.names.index(name)
+        return buf[self.offsets[i]:self.offsets[i] + self.numels[i]].view(self.shapes[i])
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+        # autograd may have replaced .grad with a fresh tensor (e.g. when a grad was None); re-home
+        for p, o, n in zip(self.params, self.offsets, self.numels):
+            g = p.grad
+            if g is None or g.data_ptr() != self.grad[o:o + n].data_ptr():
+                p.grad = self.grad[o:o + n].view(p.shape)
+
+    def sync_grads_into_flat(self) -> None:
+        """Copy any grad that autograd stored outside the flat buffer back into it."""
+        for p, o, n in zip(self.params, self.offsets, self.numels):
+            g = p.grad
+            if g is not None and g.data_ptr() != self.grad[o:o + n].data_ptr():
+                self.grad[o:o + n].copy_(g.reshape(-1))
+                p.grad = self.grad[o:o + n].view(p.shape)
+
+    def l2_mask(self, names) -> torch.Tensor:
+        m = torch.zeros(self.numel, dtype=torch.uint8, device=self.flat.device)
+        for nm in names:
+            i = self.names.index(nm)
+            m[self.offsets[i]:self.offsets[i] + self.numels[i]] = 1
+        return m
+
+
+class FusedOptimizer:
+    """Adam (TF1 form) or Adagrad over a FlatParams store; GPU -> one HIP kernel, CPU -> torch."""
+
+    def __init__(self, flat: FlatParams, kind: str = "adam", beta1: float = 0.9, beta2: float = 0.999,
+                 eps: float = 1e-8, adagrad_init: float = 0.1, l2: float = 0.0,
+                 l2_mask: Optional[torch.Tensor] = None):
+        self.flat = flat
+        self.kind = kind
+        self.b1, self.b2, self.eps = beta1, beta2, eps
+        self.l2 = float(l2)
+        self.l2_mask = l2_mask if (l2_mask is not None and self.l2 > 0) else None
+        self.t = 0  # number of applied updates (TF's beta powers = beta^t)
+        dev = flat.flat.device
+        if kind == "adam":
+            self.m = torch.zeros(flat.numel, dtype=torch.float32, device=dev)
+            self.v = torch.zeros(flat.numel, dtype=torch.float32, device=dev)
+        elif kind == "adagrad":
+            self.acc = torch.full((flat.numel,), adagrad_init, dtype=torch.float32, device=dev)
+        else:
+            raise ValueError(kind)
+
+    def state_tensors(self) -> Dict[str, torch.Tensor]:
+        if self.kind == "adam":
+            return {"m": self.m, "v": self.v}
+        return {"acc": self.acc}
+
+    def step(self, lr: float, grad_scale: float = 1.0) -> None:
+        self.t += 1
+        p, g = self.flat.flat, self.flat.grad
+        if p.is_cuda:
+            o = ops()
+            if self.kind == "adam":
+                lr_t = lr * math.sqrt(1 - self.b2 ** self.t) / (1 - self.b1 ** self.t)
+                o.adam_step(p, self.m, self.v, g, self.l2_mask, lr_t, self.b1, self.b2, self.eps, grad_scale, self.l2)
+            else:
+                o.adagrad_step(p, self.acc, g, self.l2_mask, lr, grad_scale, self.l2)
+            return
+        with torch.no_grad():
+            gg = g * grad_scale
+            if self.l2_mask is not None:
+                gg = gg + self.l2 * p * self.l2_mask.float()
+            if self.kind == "adam":
+                lr_t = lr * math.sqrt(1 - self.b2 ** self.t) / (1 - self.b1 ** self.t)
+                self.m.mul_(self.b1).add_(gg, alpha=1 - self.b1)
+                self.v.mul_(self.b2).addcmul_(gg, gg, value=1 - self.b2)
+                p.sub_(lr_t * self.m / (self.v.sqrt() + self.eps))
+            else:
+                self.acc.addcmul_(gg, gg)
+                p.sub_(lr * gg / self.acc.sqrt())

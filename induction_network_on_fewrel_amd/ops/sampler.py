@@ -1,0 +1,51 @@
+"""Device-resident episode sampling (HIP kernel ``ina.sample_episodes``).
+
+The dataset's id arrays live on the GPU (``DeviceDataset``); each step samples B episodes
+on-device and the encoder gathers tokens by instance index -- no per-step host sampling, no H2D
+copies (the reference samples on the host and feeds 5 numpy arrays per ``sess.run``,
+util/data_loader.py:259-309, model/base.py:143-152).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..data.fewrel import FewRelDataset
+from ._ext import ops
+
+
+class DeviceDataset:
+    def __init__(self, data: FewRelDataset, device):
+        self.data = data
+        self.device = torch.device(device)
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.int32), device=self.device)
+        self.word = t(data.data_word)
+        self.pos1 = t(data.data_pos1)
+        self.pos2 = t(data.data_pos2)
+        self.mask = t(data.data_mask)
+        self.scopes = t(data.scope_array())
+        self.L = data.max_length
+
+    def arrays(self):
+        return self.word, self.pos1, self.pos2, self.mask
+
+
+class DeviceEpisodeSampler:
+    def __init__(self, dd: DeviceDataset, seed: int = 0, nota_rate: float = 0.0):
+        self.dd = dd
+        self.seed = int(seed) & 0x7FFFFFFF
+        self.nota_rate = float(nota_rate)
+        self.calls = 0
+
+    def sample(self, B: int, N: int, K: int, Q: int):
+        """-> (idx int32 [B, N*K+N*Q], labels int32 [B, N*Q]) on the device."""
+        s = (self.seed * 1000003 + self.calls * 7919) & 0x7FFFFFFF
+        self.calls += 1
+        return ops().sample_episodes(self.dd.scopes, B, N, K, Q, s, self.nota_rate)
+
+    def state_dict(self):
+        return {"seed": self.seed, "calls": self.calls}
+
+    def load_state_dict(self, d):
+        self.seed = int(d["seed"])
+        self.calls = int(d["calls"])

@@ -1,0 +1,286 @@
+"""Numerics of every gfx950 kernel against the plain-PyTorch fp32 oracle (models/reference.py).
+
+fp32 mode uses the exact f32-input MFMA (v_mfma_f32_16x16x4_f32) and is checked tightly; bf16 mode
+is checked against the oracle with the same bf16 rounding points (``bf16=True``) and against the pure
+fp32 oracle with a looser bound.
+"""
+import numpy as np
+import pytest
+import torch
+
+from induction_network_on_fewrel_amd.config import Config
+from induction_network_on_fewrel_amd.data import EpisodeSampler, make_synthetic
+from induction_network_on_fewrel_amd.models import InductionNetwork
+from induction_network_on_fewrel_amd.models import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _problem(B=3, N=5, K=2, Q=5, L=37, u=20, dtype="fp32", seed=0, E=5, head="reference"):
+    cfg = Config(N=N, K=K, Q=Q, max_length=L, hidden_size=u, dtype=dtype, relation_head=head)
+    data = make_synthetic(num_relations=max(8, N + 2), instances_per_relation=40, max_length=L, vocab=1000,
+                          word_dim=E, seed=seed)
+    model = InductionNetwork(cfg, data.word_vec_mat, seed=seed).to(DEV)
+    g = torch.Generator().manual_seed(seed + 7)
+    with torch.no_grad():  # non-zero biases so bias paths are exercised
+        for name in ("lstm_fw_bias", "lstm_bw_bias", "attn_bias"):
+            t = getattr(model.params, name)
+            t.copy_((torch.randn(t.shape, generator=g) * 0.3).to(DEV))
+    idx, labels = EpisodeSampler(data, seed=seed).next_batch_indices(B, N, K, Q)
+    inst = torch.tensor(idx.reshape(-1), dtype=torch.int32, device=DEV)
+    from induction_network_on_fewrel_amd.ops.sampler import DeviceDataset
+    dd = DeviceDataset(data, DEV)
+    return cfg, data, model, dd, inst, torch.tensor(labels, device=DEV)
+
+
+def _relerr(a, b):
+    a = a.double()
+    b = b.double()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+def _gathered(dd, inst):
+    return [t[inst.long()] for t in dd.arrays()]
+
+
+def _unpack_cst(cst, S, L, U):
+    ntiles = cst.shape[0]
+    U4 = U // 4
+    out = torch.empty(ntiles * 16, L, 2 * U, device=cst.device)
+    for d in range(2):
+        c = cst[:, d]  # [tiles, L, U4, 64]
+        for m in range(U4):
+            for q in range(4):
+                # lane = q*16 + n  -> seq = tile*16 + n, unit = 4m + q
+                v = c[:, :, m, q * 16:(q + 1) * 16]  # [tiles, L, 16]
+                out[:, :, d * U + 4 * m + q] = v.permute(0, 2, 1).reshape(ntiles * 16, L)
+    return out[:S]
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_lstm_forward(dtype):
+    from induction_network_on_fewrel_amd.ops import ops
+    from induction_network_on_fewrel_amd.ops.packing import lstm_shape, pack_lstm
+    cfg, data, model, dd, inst, _ = _problem(dtype=dtype)
+    p = model.pdict()
+    bf16 = dtype == "bf16"
+    U = cfg.hidden_size
+    DIN = model.params.input_dim
+    sh = lstm_shape(U, DIN, bf16)
+    apack, _ = pack_lstm(p["lstm_fw_kernel"], p["lstm_bw_kernel"], U, DIN, bf16)
+    bias = torch.stack([p["lstm_fw_bias"], p["lstm_bw_bias"]]).detach().float().contiguous()
+    word, pos1, pos2, mask = dd.arrays()
+    hraw, cst = ops().lstm_fwd(inst, word, pos1, pos2, p["word_embedding"].detach(), p["pos1_embedding"].detach(),
+                               p["pos2_embedding"].detach(), apack, bias, U, sh["NX"], bf16, True)
+    torch.cuda.synchronize()
+    w, a1, a2, _ = _gathered(dd, inst)
+    with torch.no_grad():
+        x = ref.embed(p["word_embedding"], p["pos1_embedding"], p["pos2_embedding"], w.long(), a1.long(), a2.long())
+        hf, cf = ref.lstm_direction(x, p["lstm_fw_kernel"], p["lstm_fw_bias"], False, bf16)
+        hb, cb = ref.lstm_direction(x, p["lstm_bw_kernel"], p["lstm_bw_bias"], True, bf16)
+    tol = 2e-5 if not bf16 else 2e-2
+    S, L = inst.shape[0], word.shape[1]
+    ef = _relerr(hraw[..., :U].float(), hf)
+    eb = _relerr(hraw[..., U:].float(), hb)
+    c = _unpack_cst(cst, S, L, U)
+    ec = _relerr(c, torch.cat([cf, cb], -1))
+    print(f"lstm fwd {dtype}: h_fw {ef:.2e} h_bw {eb:.2e} c {ec:.2e}")
+    assert ef < tol and eb < tol and ec < tol
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("keep_prob", [1.0, 0.9])
+def test_attention_forward(dtype, keep_prob):
+    from induction_network_on_fewrel_amd.ops import ops
+    from induction_network_on_fewrel_amd.ops.packing import lstm_shape, pack_attn, pack_lstm
+    cfg, data, model, dd, inst, _ = _problem(dtype=dtype)
+    p = model.pdict()
+    bf16 = dtype == "bf16"
+    U = cfg.hidden_size
+    DIN = model.params.input_dim
+    apack, _ = pack_lstm(p["lstm_fw_kernel"], p["lstm_bw_kernel"], U, DIN, bf16)
+    bias = torch.stack([p["lstm_fw_bias"], p["lstm_bw_bias"]]).detach().float().contiguous()
+    word, pos1, pos2, mask = dd.arrays()
+    hraw, _ = ops().lstm_fwd(inst, word, pos1, pos2, p["word_embedding"].detach(), p["pos1_embedding"].detach(),
+                             p["pos2_embedding"].detach(), apack, bias, U, lstm_shape(U, DIN, bf16)["NX"], bf16, False)
+    w1p, _ = pack_attn(p["attn_kernel"], bf16)
+    seed = 1234
+    e, alphas = ops().attn_fwd(hraw, inst, mask, w1p, p["attn_bias"].detach().contiguous(),
+                               p["attn_w2"].detach().reshape(-1).contiguous(), seed, keep_prob, U, bf16, 0)
+    torch.cuda.synchronize()
+    S, L = hraw.shape[0], hraw.shape[1]
+    Hin = hraw.float()
+    if keep_prob < 1:
+        mf = ref.dropout_keep_mask(seed, 0, S, L, U, keep_prob, Hin.device)
+        mb = ref.dropout_keep_mask(seed, 1, S, L, U, keep_prob, Hin.device)
+        Hin = torch.cat([Hin[..., :U] * mf, Hin[..., U:] * mb], -1) / keep_prob
+    m01 = (mask[inst.long()] > 0)
+    with torch.no_grad():
+        e_ref, a_ref = ref.self_attention(Hin, m01, p["attn_kernel"], p["attn_bias"], p["attn_w2"], bf16)
+    ee = _relerr(e, e_ref)
+    ea = _relerr(alphas, a_ref.squeeze(-1))
+    print(f"attn fwd {dtype} kp={keep_prob}: e {ee:.2e} alpha {ea:.2e}")
+    tol = 1e-4 if not bf16 else 3e-2
+    assert ee < tol and ea < tol
+
+
+def _encoder_grads_ref(model, dd, inst, de, keep_prob, seed, bf16):
+    p = {k: v.detach().clone().requires_grad_(True) for k, v in model.pdict().items()}
+    p["word_embedding"].requires_grad_(False)
+    w, a1, a2, m = _gathered(dd, inst)
+    e, _ = ref.encode(p, w.long(), a1.long(), a2.long(), m, keep_prob, seed, bf16)
+    (e * de).sum().backward()
+    return e.detach(), {k: v.grad for k, v in p.items() if v.grad is not None}
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("keep_prob", [1.0, 0.9])
+def test_encoder_backward(dtype, keep_prob):
+    from induction_network_on_fewrel_amd.ops.encoder import encode
+    cfg, data, model, dd, inst, _ = _problem(dtype=dtype)
+    bf16 = dtype == "bf16"
+    seed = 99
+    meta = dict(U=cfg.hidden_size, bf16=bf16, keep_prob=keep_prob, seed=seed, word_grad=False)
+    p = model.pdict()
+    e, alphas = encode(inst, dd.arrays(), p, meta)
+    de = torch.randn_like(e)
+    (e * de).sum().backward()
+    torch.cuda.synchronize()
+    e_ref, g_ref = _encoder_grads_ref(model, dd, inst, de, keep_prob, seed, bf16=False)
+    tol_e = 1e-4 if not bf16 else 3e-2
+    tol_g = 2e-3 if not bf16 else 6e-2
+    ee = _relerr(e.detach(), e_ref)
+    print(f"encoder {dtype} kp={keep_prob}: e {ee:.2e}")
+    assert ee < tol_e
+    for k in ("pos1_embedding", "pos2_embedding", "lstm_fw_kernel", "lstm_fw_bias", "lstm_bw_kernel", "lstm_bw_bias",
+              "attn_kernel", "attn_bias", "attn_w2"):
+        g = getattr(model.params, k).grad
+        err = _relerr(g, g_ref[k])
+        print(f"  grad {k}: {err:.2e}")
+        assert err < tol_g, k
+
+
+@pytest.mark.parametrize("head", ["reference", "paper"])
+@pytest.mark.parametrize("shape", [(5, 2, 5), (5, 1, 5), (10, 5, 2), (3, 3, 5)])
+def test_head_forward_backward(head, shape):
+    from induction_network_on_fewrel_amd.ops.head import head as head_fn
+    N, K, Q = shape
+    B = 4
+    cfg, data, model, dd, inst, labels = _problem(B=B, N=N, K=K, Q=Q, head=head)
+    H = 2 * cfg.hidden_size
+    S = inst.shape[0]
+    torch.manual_seed(0)
+    e = (torch.randn(S, H, device=DEV) * 0.5).requires_grad_(True)
+    p = model.pdict()
+    probs = head_fn(e, p, dict(E=B, N=N, K=K, Q=Q, iters=3, paper=(head == "paper")))
+    dp = torch.randn_like(probs)
+    (probs * dp).sum().backward()
+    torch.cuda.synchronize()
+    # oracle with the kernels' bf16 rounding points
+    pr = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
+    er = e.detach().clone().requires_grad_(True)
+    ev = er.view(B, N * K + N * Q, H)
+    cls = ref.dynamic_routing(ev[:, : N * K].reshape(B, N, K, H), pr["W_s"], 3)
+    probs_r = ref.relation_probs(cls, ev[:, N * K:], pr["M"], pr["ntn_w"], pr["ntn_b"], head, bf16=True)
+    (probs_r * dp).sum().backward()
+    ep = _relerr(probs.detach(), probs_r.detach())
+    print(f"head {head} {shape}: probs {ep:.2e}")
+    assert ep < 2e-2
+    for k, t in (("e", (e.grad, er.grad)), ("W_s", (p["W_s"].grad, pr["W_s"].grad)), ("M", (p["M"].grad, pr["M"].grad)),
+                 ("w", (p["ntn_w"].grad, pr["ntn_w"].grad)), ("b", (p["ntn_b"].grad, pr["ntn_b"].grad))):
+        err = _relerr(*t)
+        print(f"  grad {k}: {err:.2e}")
+        assert err < 6e-2, k
+
+
+def test_routing_only_fp32():
+    """routing is fp32 VALU end to end: must match the oracle tightly."""
+    from induction_network_on_fewrel_amd.ops import ops
+    N, K, Q, B, H = 5, 3, 2, 6, 40
+    torch.manual_seed(1)
+    S = B * (N * K + N * Q)
+    e = torch.randn(S, H, device=DEV)
+    Ws = torch.randn(H, H, device=DEV) * 0.2
+    cls = ops().routing_fwd(e, Ws, B, N, K, Q, 3, 0)
+    ev = e.view(B, N * K + N * Q, H)
+    cls_r = ref.dynamic_routing(ev[:, : N * K].reshape(B, N, K, H), Ws, 3)
+    assert _relerr(cls, cls_r) < 1e-5
+    er = e.clone().requires_grad_(True)
+    Wr = Ws.clone().requires_grad_(True)
+    cr = ref.dynamic_routing(er.view(B, N * K + N * Q, H)[:, : N * K].reshape(B, N, K, H), Wr, 3)
+    dc = torch.randn_like(cr)
+    (cr * dc).sum().backward()
+    de = torch.zeros_like(e)
+    slab = ops().routing_bwd(e, Ws, dc.contiguous(), de, B, N, K, Q, 3, 0)
+    dWs = slab.sum(0)
+    sup_rows = torch.cat([torch.arange(b * (N * K + N * Q), b * (N * K + N * Q) + N * K) for b in range(B)]).to(DEV)
+    assert _relerr(de[sup_rows], er.grad[sup_rows]) < 1e-4
+    assert _relerr(dWs, Wr.grad) < 1e-4
+
+
+def test_adam_matches_tf_formula():
+    from induction_network_on_fewrel_amd.ops import ops
+    n = 10007
+    torch.manual_seed(0)
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    p0 = p.clone()
+    b1, b2, eps, lr = 0.9, 0.999, 1e-8, 1e-3
+    lr_t = lr * (1 - b2) ** 0.5 / (1 - b1)
+    ops().adam_step(p, m, v, g, None, lr_t, b1, b2, eps, 1.0, 0.0)
+    m_r = (1 - b1) * g
+    v_r = (1 - b2) * g * g
+    p_r = p0 - lr_t * m_r / (v_r.sqrt() + eps)
+    assert torch.allclose(p, p_r, atol=1e-7, rtol=1e-6)
+
+
+def test_device_sampler_layout():
+    from induction_network_on_fewrel_amd.ops.sampler import DeviceDataset, DeviceEpisodeSampler
+    data = make_synthetic(num_relations=12, instances_per_relation=30, max_length=20, vocab=100, seed=3)
+    dd = DeviceDataset(data, DEV)
+    s = DeviceEpisodeSampler(dd, seed=5, nota_rate=0.0)
+    N, K, Q, B = 5, 3, 4, 64
+    idx, lab = s.sample(B, N, K, Q)
+    idx, lab = idx.cpu().numpy(), lab.cpu().numpy()
+    rel = np.repeat(np.arange(12), 30)
+    for b in range(B):
+        sup = idx[b, : N * K].reshape(N, K)
+        cls = rel[sup]
+        assert (cls == cls[:, :1]).all()
+        assert len(set(cls[:, 0])) == N
+        qry = idx[b, N * K:]
+        assert len(set(np.concatenate([sup.ravel(), qry]))) == N * K + N * Q
+        assert (cls[lab[b], 0] == rel[qry]).all()
+        assert sorted(lab[b].tolist()) == sorted(np.repeat(np.arange(N), Q).tolist())
+    # NOTA
+    s2 = DeviceEpisodeSampler(dd, seed=6, nota_rate=0.5)
+    idx, lab = s2.sample(B, N, K, Q)
+    lab = lab.cpu().numpy()
+    assert (lab == N).mean() > 0.3
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_full_model_matches_oracle(dtype):
+    cfg, data, model, dd, inst, labels = _problem(dtype=dtype)
+    B, N, K, Q = 3, cfg.N, cfg.K, cfg.Q
+    probs, alphas = model(inst, dd.arrays(), B, N, K, Q, training=False)
+    loss = model.loss(probs, labels)
+    loss.backward()
+    torch.cuda.synchronize()
+    cpu_model = InductionNetwork(cfg, data.word_vec_mat, seed=0)
+    cpu_model.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
+    from induction_network_on_fewrel_amd.data.sampler import EpisodeSampler  # noqa: F401
+    cpu_arrays = tuple(t.cpu() for t in dd.arrays())
+    probs_c, _ = cpu_model(inst.cpu(), cpu_arrays, B, N, K, Q, training=False)
+    loss_c = cpu_model.loss(probs_c, labels.cpu())
+    loss_c.backward()
+    print(f"full {dtype}: loss gpu {loss.item():.6f} cpu {loss_c.item():.6f}")
+    assert abs(loss.item() - loss_c.item()) < (1e-3 if dtype == "fp32" else 2e-2) * max(1.0, abs(loss_c.item()))
+    for name, prm in model.params.trainable().items():
+        err = _relerr(prm.grad.cpu(), getattr(cpu_model.params, name).grad)
+        print(f"  grad {name}: {err:.2e}")
+        assert err < 8e-2, name
