@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node training episodes/sec of the Induction Network on MI355X.
+
+Metric / config (BASELINE.json): "episodes/sec (whole node)" on FewRel-shaped episodes,
+default 5-way 5-shot, Q=5, max_length 37, BiLSTM u=20 + self-attention, 3 routing iterations,
+NTN h=100, 5-d word table over a 400k vocabulary (the reference's train.py defaults), bf16 MFMA
+compute with fp32 master weights, Adam with the reference's staircase LR.
+Data: synthetic token sequences (64 relations x 700 instances, FewRel 1.0 train shape), random-init
+weights -- no dataset or checkpoint downloads are possible here.
+
+A timed step is the FULL training step: device episode sampling, forward, backward, RCCL
+all-reduce of the flat gradient (N > 1), fused Adam update. Weak scaling: episodes per GPU fixed.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--episodes-per-gpu B] [--shot K]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--episodes-per-gpu", type=int, default=2048)
+    ap.add_argument("--way", type=int, default=5)
+    ap.add_argument("--shot", type=int, default=5)
+    ap.add_argument("--query", type=int, default=5)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--hidden", type=int, default=20)
+    ap.add_argument("--profile-json", default="")
+    args = ap.parse_args()
+
+    import torch
+    from induction_network_on_fewrel_amd.config import Config
+    from induction_network_on_fewrel_amd.data import make_synthetic
+    from induction_network_on_fewrel_amd.parallel.dp import DistContext
+    from induction_network_on_fewrel_amd.runtime.trainer import Trainer
+
+    dist = DistContext.from_env("cuda")
+    world = dist.world
+    if world != args.gpus and dist.is_main:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    B = args.episodes_per_gpu
+    cfg = Config(N=args.way, K=args.shot, Q=args.query, max_length=37, hidden_size=args.hidden, dtype=args.dtype,
+                 episodes_per_step=B, seed=1234, resume=False, model_dir="/tmp/ina_bench",
+                 train_iter=args.steps + args.warmup)
+    data = make_synthetic(num_relations=64, instances_per_relation=700, max_length=37, vocab=400000, word_dim=5,
+                          seed=0)
+    tr = Trainer(cfg, data, None, device="cuda", dist_ctx=dist, log=False)
+    for _ in range(args.warmup):
+        tr.train_step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loss = acc = 0.0
+    for _ in range(args.steps):
+        loss, acc = tr.train_step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt = dist.max_scalar(dt)
+    in_sync = dist.params_in_sync(tr.flat.flat)
+    episodes = args.steps * B * world
+    value = episodes / dt
+    if dist.is_main:
+        out = {
+            "metric": "episodes/sec (whole node)",
+            "value": round(value, 2),
+            "unit": "episodes/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * dt / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (64 relations x 700 instances, L=37, 400k vocab, 5-d word table); random-init weights",
+            "config": {
+                "model": f"induction-network bilstm(u={args.hidden})+self-attn, routing x3, ntn h=100",
+                "episode": f"{args.way}-way {args.shot}-shot Q={args.query}",
+                "global_batch": B * world,
+                "episodes_per_gpu": B,
+                "seq_len": 37,
+                "sentences_per_step_per_gpu": B * args.way * (args.shot + args.query),
+                "parallelism": f"dp{world}",
+            },
+            "final_loss": round(loss, 6),
+            "params_in_sync": bool(in_sync),
+        }
+        print(json.dumps(out))
+        if args.profile_json:
+            with open(args.profile_json, "w") as fh:
+                json.dump(dict(out, timers=tr.timers), fh, indent=1)
+    dist.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,99 @@
+"""Checkpoint save / restore with the reference's layout and TF variable names.
+
+Reference (model/base.py:124,171-178): ``tf.train.Saver()`` (max_to_keep=5) saving to
+``<model_dir>/checkpoint/inductionNetwork-<global_step>`` plus the ``checkpoint`` state file, on best
+val accuracy; there is NO restore path in the reference (``curr_iter = 0``, :130). This module keeps
+the directory layout, the file stem and the state file, and the variable names/shapes of SURVEY 2.4
+as tensor keys (params, ``<var>/Adam``, ``<var>/Adam_1``, ``beta1_power``, ``beta2_power``,
+``global_step``), stored as safetensors + a JSON index (TF's binary bundle format is not
+reproducible without TensorFlow). Adds resume: params, optimizer moments, step, sampler/RNG state,
+best accuracy. Rank 0 writes; other ranks receive state by broadcast (parallel/dp.py).
+"""
+from __future__ import annotations
+
+import json
+import os
+import re
+from collections import OrderedDict
+from typing import Dict, Optional, Tuple
+
+import torch
+from safetensors.torch import load_file, save_file
+
+FORMAT = "ina-ckpt-v1"
+
+
+def ckpt_dir(model_dir: str) -> str:
+    return os.path.join(model_dir, "checkpoint")
+
+
+def _state_file(model_dir: str) -> str:
+    return os.path.join(ckpt_dir(model_dir), "checkpoint")
+
+
+def read_state(model_dir: str):
+    f = _state_file(model_dir)
+    if not os.path.exists(f):
+        return None, []
+    latest, allp = None, []
+    with open(f) as fh:
+        for line in fh:
+            m = re.match(r'\s*(\w+):\s*"(.*)"', line)
+            if not m:
+                continue
+            if m.group(1) == "model_checkpoint_path":
+                latest = m.group(2)
+            elif m.group(1) == "all_model_checkpoint_paths":
+                allp.append(m.group(2))
+    return latest, allp
+
+
+def _write_state(model_dir: str, latest: str, allp) -> None:
+    with open(_state_file(model_dir), "w") as fh:
+        fh.write(f'model_checkpoint_path: "{latest}"\n')
+        for p in allp:
+            fh.write(f'all_model_checkpoint_paths: "{p}"\n')
+
+
+def save(model_dir: str, name: str, step: int, tensors: "OrderedDict[str, torch.Tensor]", meta: dict,
+         max_to_keep: int = 5) -> str:
+    d = ckpt_dir(model_dir)
+    os.makedirs(d, exist_ok=True)
+    stem = f"{name}-{step}"
+    cpu = OrderedDict((k, v.detach().to("cpu").contiguous()) for k, v in tensors.items())
+    tmp = os.path.join(d, stem + ".safetensors.tmp")
+    save_file(cpu, tmp)
+    os.replace(tmp, os.path.join(d, stem + ".safetensors"))
+    index = dict(meta, format=FORMAT, global_step=int(step),
+                 variables={k: {"shape": list(v.shape), "dtype": str(v.dtype).replace("torch.", "")}
+                            for k, v in cpu.items()})
+    with open(os.path.join(d, stem + ".index.json"), "w") as fh:
+        json.dump(index, fh, indent=1, sort_keys=True)
+    _, allp = read_state(model_dir)
+    allp = [p for p in allp if p != stem] + [stem]
+    while len(allp) > max_to_keep:
+        old = allp.pop(0)
+        for ext in (".safetensors", ".index.json"):
+            try:
+                os.remove(os.path.join(d, old + ext))
+            except FileNotFoundError:
+                pass
+    _write_state(model_dir, stem, allp)
+    return os.path.join(d, stem)
+
+
+def latest(model_dir: str) -> Optional[str]:
+    stem, _ = read_state(model_dir)
+    if stem is None:
+        return None
+    p = os.path.join(ckpt_dir(model_dir), stem)
+    return p if os.path.exists(p + ".safetensors") else None
+
+
+def load(path_stem: str) -> Tuple[Dict[str, torch.Tensor], dict]:
+    tensors = load_file(path_stem + ".safetensors")
+    with open(path_stem + ".index.json") as fh:
+        meta = json.load(fh)
+    if meta.get("format") != FORMAT:
+        raise ValueError(f"unknown checkpoint format {meta.get('format')}")
+    return tensors, meta

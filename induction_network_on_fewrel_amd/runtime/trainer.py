@@ -1,0 +1,260 @@
+"""Episodic trainer / evaluator (reference ``Base.train`` / ``Base.eval``, model/base.py:115-208).
+
+Cadence kept from the reference: ``train_iter`` steps, running loss/acc printed every ``log_every``
+(100) steps and reset at ``it % val_step == 0``; validation every ``val_step`` (2000) steps over
+``val_iter`` (1000) episodes; checkpoint on best val accuracy; final "test" over ``test_iter`` (3000)
+episodes of the val loader (the reference has no test split).
+
+Fixes / additions (flagged in SURVEY 2.7): eval feeds the mask (#1) and is forward-only; resume from
+the latest checkpoint (5.4); B episodes per step; rank-folded samplers + flat-buffer all-reduce (DP);
+NaN/Inf loss guard; per-phase timers; JSONL + TensorBoard metrics; no per-step tensor printing (#11).
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from collections import OrderedDict
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..config import Config
+from ..data.fewrel import FewRelDataset
+from ..data.sampler import EpisodeSampler
+from ..models.induction import InductionNetwork
+from ..models import reference as ref
+from ..ops.optim import FlatParams, FusedOptimizer, lr_at
+from ..parallel.dp import DistContext
+from . import checkpoint as ckpt
+from .metrics import MetricsLogger
+
+
+class _HostEpisodes:
+    """CPU path: host sampler producing instance indices (same contract as the device sampler)."""
+
+    def __init__(self, data: FewRelDataset, seed: int, nota_rate: float):
+        self.data = data
+        self.s = EpisodeSampler(data, seed=seed, nota_rate=nota_rate)
+        self.arrays = tuple(torch.as_tensor(a) for a in (data.data_word, data.data_pos1, data.data_pos2,
+                                                          data.data_mask))
+
+    def sample(self, B, N, K, Q):
+        idx, lab = self.s.next_batch_indices(B, N, K, Q)
+        return torch.as_tensor(idx.astype(np.int32)), torch.as_tensor(lab.astype(np.int32))
+
+    def state_dict(self):
+        return {"bitgen": self.s.rng.bit_generator.state}
+
+    def load_state_dict(self, d):
+        self.s.rng.bit_generator.state = d["bitgen"]
+
+
+class Trainer:
+    def __init__(self, cfg: Config, train_data: FewRelDataset, val_data: Optional[FewRelDataset] = None,
+                 device: str = "auto", dist_ctx: Optional[DistContext] = None, log: bool = True):
+        cfg.validate()
+        self.cfg = cfg
+        self.dist = dist_ctx or DistContext.from_env(device if device != "auto" else cfg.device)
+        if device not in ("auto", None) and self.dist.world == 1:
+            self.dist.device = torch.device(device)
+        self.device = self.dist.device
+        self.train_data = train_data
+        self.val_data = val_data if val_data is not None else train_data
+        wv = train_data.word_vec_mat
+        vocab = None if wv is not None else int(max(train_data.data_word.max(), 1) + 1)
+        self.model = InductionNetwork(cfg, wv, vocab_size=vocab, seed=cfg.seed).to(self.device)
+        self.flat = FlatParams(self.model.params.trainable())
+        if self.dist.world > 1:
+            self.dist.broadcast_(self.flat.flat, 0)
+        l2_names = [n for n, p in self.model.params.trainable().items()
+                    if any(p is q for q in self.model.params.l2_vars())]
+        self.opt = FusedOptimizer(self.flat, cfg.optimizer, cfg.adam_beta1, cfg.adam_beta2, cfg.adam_eps,
+                                  cfg.adagrad_init_acc, l2=cfg.l2_lambda if cfg.use_l2 else 0.0,
+                                  l2_mask=self.flat.l2_mask(l2_names) if cfg.use_l2 else None)
+        self.global_step = 0
+        self.best_acc = 0.0
+        self.skipped_steps = 0
+        rank_seed = cfg.seed * 1009 + 7919 * self.dist.rank
+        self.train_eps = self._make_sampler(train_data, rank_seed, cfg.nota_rate)
+        self.val_eps = self._make_sampler(self.val_data, rank_seed + 1, cfg.nota_rate)
+        self.log = MetricsLogger(cfg.model_dir, enabled=log and self.dist.is_main)
+        self.timers = {"sample": 0.0, "fwd_bwd": 0.0, "allreduce": 0.0, "optim": 0.0}
+        if cfg.resume:
+            self.maybe_resume()
+
+    # ------------------------------------------------------------------ plumbing
+    def _make_sampler(self, data: FewRelDataset, seed: int, nota: float):
+        if self.device.type == "cuda":
+            from ..ops.sampler import DeviceDataset, DeviceEpisodeSampler
+            dd = DeviceDataset(data, self.device)
+            s = DeviceEpisodeSampler(dd, seed=seed, nota_rate=nota)
+            s.arrays = dd.arrays()
+            return s
+        return _HostEpisodes(data, seed, nota)
+
+    def _sync(self):
+        if self.device.type == "cuda" and self.cfg.profile:
+            torch.cuda.synchronize()
+
+    def dropout_seed(self) -> int:
+        return (self.cfg.seed * 2654435761 + self.global_step * 97 + self.dist.rank * 7919) & 0x7FFFFFFF
+
+    # ------------------------------------------------------------------ steps
+    def train_step(self) -> Tuple[float, float]:
+        cfg = self.cfg
+        B, N, K, Q = cfg.episodes_per_step, cfg.N, cfg.K, cfg.Q
+        t0 = time.perf_counter()
+        idx, labels = self.train_eps.sample(B, N, K, Q)
+        self._sync()
+        t1 = time.perf_counter()
+        self.flat.zero_grad()
+        probs, _ = self.model(idx.view(-1), self.train_eps.arrays, B, N, K, Q, training=True,
+                              dropout_seed=self.dropout_seed())
+        loss = self.model.loss(probs, labels)
+        loss.backward()
+        self.flat.sync_grads_into_flat()
+        with torch.no_grad():
+            acc_t = ref.accuracy(probs.detach(), labels.long())
+        self._sync()
+        t2 = time.perf_counter()
+        if self.dist.world > 1:
+            self.dist.allreduce_buckets_(self.flat.grad)
+        self._sync()
+        t3 = time.perf_counter()
+        lr = lr_at(self.global_step, cfg.learning_rate, cfg.decay_steps, cfg.decay_rate, cfg.staircase,
+                   cfg.lr_schedule)
+        loss_v = float(loss.detach())
+        if cfg.grad_check_finite and not math.isfinite(loss_v):
+            self.skipped_steps += 1
+        else:
+            self.opt.step(lr, grad_scale=1.0 / self.dist.world)
+        self.global_step += 1
+        self._sync()
+        t4 = time.perf_counter()
+        self.timers["sample"] += t1 - t0
+        self.timers["fwd_bwd"] += t2 - t1
+        self.timers["allreduce"] += t3 - t2
+        self.timers["optim"] += t4 - t3
+        self._last_lr = lr
+        return loss_v, float(acc_t)
+
+    @torch.no_grad()
+    def evaluate(self, iters: int, N: Optional[int] = None, K: Optional[int] = None, Q: Optional[int] = None,
+                 batch: Optional[int] = None, sampler=None, nota_threshold: Optional[float] = None) -> float:
+        """Mean over episodes of per-episode accuracy (model/base.py:186-208), mask fed (fix #1)."""
+        cfg = self.cfg
+        N, K, Q = N or cfg.eN, K or cfg.eK, Q or cfg.eQ
+        B = batch or max(1, min(cfg.episodes_per_step, iters))
+        s = sampler or self.val_eps
+        done, acc_sum = 0, 0.0
+        while done < iters:
+            b = min(B, iters - done)
+            idx, labels = s.sample(b, N, K, Q)
+            probs, _ = self.model(idx.view(-1), s.arrays, b, N, K, Q, training=False)
+            pred = ref.predict(probs, nota_threshold)
+            acc_sum += float((pred == labels.long()).float().mean(-1).sum())
+            done += b
+        acc = acc_sum / max(1, done)
+        return self.dist.mean_scalars([acc])[0]
+
+    # ------------------------------------------------------------------ loop
+    def train(self) -> float:
+        cfg = self.cfg
+        self.log.print(f"{cfg.N}-way-{cfg.K}-shot Few-Shot Relation Classification")
+        self.log.print(f"Model: {cfg.model_name}  world={self.dist.world}  device={self.device}  "
+                       f"episodes/step/rank={cfg.episodes_per_step}")
+        it_loss = it_acc = it_n = 0.0
+        start = self.global_step
+        t_start = time.time()
+        for it in range(start, cfg.train_iter):
+            loss, acc = self.train_step()
+            it_loss += loss
+            it_acc += acc
+            it_n += 1
+            self.log.log(self.global_step, "train", loss=loss, accuracy=acc, learning_rate=self._last_lr)
+            if it % cfg.log_every == 0:
+                el = time.time() - t_start
+                eps = (it - start + 1) * cfg.episodes_per_step * self.dist.world / max(el, 1e-9)
+                self.log.print(f"[train] step:{it + 1:4} | loss: {it_loss / it_n:2.6f}, accuracy: "
+                               f"{100 * it_acc / it_n:3.2f}% | {eps:.1f} episodes/s")
+                self.log.flush()
+            if it % cfg.val_step == 0:
+                it_loss = it_acc = it_n = 0.0
+            if (it + 1) % cfg.val_step == 0:
+                acc_val = self.evaluate(cfg.val_iter)
+                self.log.log(self.global_step, "val", accuracy=acc_val)
+                self.log.print(f"[EVAL] step {it + 1} accuracy: {100 * acc_val:.2f}%")
+                if acc_val > self.best_acc:
+                    self.best_acc = acc_val
+                    self.log.print(f"Best checkpoint.[EVAL] accuracy :{acc_val}")
+                    self.save()
+        self.log.print("\n####################\n")
+        self.log.print("Finish training :" + cfg.ckpt_name)
+        test_acc = self.evaluate(cfg.test_iter)
+        self.log.log(self.global_step, "test", accuracy=test_acc)
+        self.log.print(f"Test accuracy: {test_acc}")
+        self.log.close()
+        return test_acc
+
+    # ------------------------------------------------------------------ checkpoint
+    def state_tensors(self) -> "OrderedDict[str, torch.Tensor]":
+        p = self.model.params
+        out = OrderedDict(p.tf_state())
+        names = list(self.flat.names)
+        st = self.opt.state_tensors()
+        for i, attr in enumerate(names):
+            tf = p.tf_name(attr)
+            if self.opt.kind == "adam":
+                out[tf + "/Adam"] = self.flat.view(st["m"], attr)
+                out[tf + "/Adam_1"] = self.flat.view(st["v"], attr)
+            else:
+                out[tf + "/Adagrad"] = self.flat.view(st["acc"], attr)
+        if self.opt.kind == "adam":
+            out["beta1_power"] = torch.tensor(self.cfg.adam_beta1 ** (self.opt.t + 1), dtype=torch.float32)
+            out["beta2_power"] = torch.tensor(self.cfg.adam_beta2 ** (self.opt.t + 1), dtype=torch.float32)
+        out["global_step"] = torch.tensor(self.global_step, dtype=torch.int64)
+        return out
+
+    def save(self) -> Optional[str]:
+        if not self.dist.is_main:
+            return None
+        meta = {"best_acc": self.best_acc, "optimizer_t": self.opt.t, "config": self.cfg.to_dict(),
+                "train_sampler": self.train_eps.state_dict(), "skipped_steps": self.skipped_steps,
+                "world_size": self.dist.world}
+        return ckpt.save(self.cfg.model_dir, self.cfg.ckpt_name, self.global_step, self.state_tensors(), meta,
+                         self.cfg.max_to_keep)
+
+    def load(self, stem: str) -> None:
+        tensors, meta = ckpt.load(stem)
+        p = self.model.params
+        p.load_tf_state(tensors, strict=False)
+        st = self.opt.state_tensors()
+        with torch.no_grad():
+            for attr in self.flat.names:
+                tf = p.tf_name(attr)
+                if self.opt.kind == "adam" and tf + "/Adam" in tensors:
+                    self.flat.view(st["m"], attr).copy_(tensors[tf + "/Adam"])
+                    self.flat.view(st["v"], attr).copy_(tensors[tf + "/Adam_1"])
+                elif self.opt.kind == "adagrad" and tf + "/Adagrad" in tensors:
+                    self.flat.view(st["acc"], attr).copy_(tensors[tf + "/Adagrad"])
+        self.global_step = int(tensors["global_step"].item()) if "global_step" in tensors else int(meta["global_step"])
+        self.opt.t = int(meta.get("optimizer_t", self.global_step))
+        self.best_acc = float(meta.get("best_acc", 0.0))
+        self.skipped_steps = int(meta.get("skipped_steps", 0))
+        if "train_sampler" in meta and meta.get("world_size", 1) == self.dist.world:
+            try:
+                self.train_eps.load_state_dict(meta["train_sampler"])
+            except Exception:
+                pass
+        if self.dist.world > 1:
+            self.dist.broadcast_(self.flat.flat, 0)
+
+    def maybe_resume(self) -> bool:
+        stem = ckpt.latest(self.cfg.model_dir)
+        if stem is None:
+            return False
+        self.load(stem)
+        self.log.print(f"resumed from {stem} at step {self.global_step}")
+        return True
