@@ -11,94 +11,7 @@
 
 #include <tuple>
 
-namespace ina {
-struct LstmArgs {
-  const int* inst;
-  int S;
-  const int* word;
-  const int* pos1;
-  const int* pos2;
-  int L;
-  const float* wemb;
-  int E;
-  const float* p1emb;
-  const float* p2emb;
-  int PD;
-  const void* apack;
-  const void* a2pack;
-  const float* bias;
-  void* hraw;
-  float* cst;
-  const float* dH;
-  float* dw_slab;
-  float* dpos_slab;
-  float* dwemb;
-  int bwd_blocks;
-};
-int lstm_fwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
-int lstm_bwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
-bool lstm_supported(int U, int NX);
-size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD);
-
-struct AttnArgs {
-  const void* hraw;
-  const int* inst;
-  const int* mask;
-  int S, L;
-  const void* w1pack;
-  const void* w1tpack;
-  const float* b1;
-  const float* w2;
-  uint32_t seed, thr;
-  float inv_kp;
-  int drop;
-  float* e;
-  float* alphas;
-  const float* de;
-  float* dHraw;
-  float* slab;
-  int blocks;
-};
-int attn_fwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st);
-int attn_bwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st);
-
-int routing_fwd(const float* e, const float* Ws, int E, int N, int K, int Q, int R, int H, float* cls, int blocks,
-                hipStream_t st);
-int routing_bwd(const float* e, const float* Ws, int E, int N, int K, int Q, int R, int H, const float* dcls, float* de,
-                float* slab, int blocks, hipStream_t st);
-size_t routing_lds_bytes(int N, int K, int H, int R, bool bwd);
-
-struct NtnArgs {
-  const float* cls;
-  const float* e;
-  int E, N, K, Q, H, h;
-  const void* mpack;
-  const void* m2pack;
-  const void* wpack;
-  const void* wtpack;
-  const float* wvec;
-  const float* bias;
-  float* probs;
-  const float* dz;
-  float* dcls;
-  float* de;
-  void* dp_out;
-  float* dw_slab;
-  int blocks;
-  int paper;
-};
-int ntn_fwd(const NtnArgs& a, hipStream_t st);
-int ntn_bwd(const NtnArgs& a, hipStream_t st);
-
-int adam_step(float* p, float* m, float* v, const float* g, const unsigned char* l2mask, long n, float lr_t, float b1,
-              float b2, float eps, float gscale, float l2, hipStream_t st);
-int adagrad_step(float* p, float* acc, const float* g, const unsigned char* l2mask, long n, float lr, float gscale,
-                 float l2, hipStream_t st);
-int slab_reduce(const float* slabs, long nslab, long len, float* out, int accumulate, hipStream_t st);
-bool sampler_supported(int N, int K, int Q);
-int sample_episodes(const int* scopes, int R, int E, int N, int K, int Q, uint32_t seed, float nota_rate, int* idx,
-                    int* lab, hipStream_t st);
-}  // namespace ina
+#include "ina_launch.h"
 
 namespace {
 
@@ -118,11 +31,20 @@ void check_launch(int rc, const char* what) {
   TORCH_CHECK(rc == 0, "ina: ", what, " launch failed / unsupported configuration (rc=", rc, ")");
 }
 int64_t frag_elems(bool bf16) { return bf16 ? 8 : 1; }
+uint32_t keep_threshold(double kp) {
+  const double t = kp * 4294967296.0;
+  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
+
 
 // ------------------------------------------------------------------ LSTM
-std::tuple<Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& word, const Tensor& pos1, const Tensor& pos2,
-                                    const Tensor& wemb, const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack,
-                                    const Tensor& bias, int64_t U, int64_t NX, bool bf16, bool store_c) {
+// Returns (hlane, cst, hnat): hlane = raw recurrent h and cst = cell states, both in the
+// lane-native tile layout [ceil(S/16), 2, L, U/4, 64] (only when store_c: the backward needs them);
+// hnat = the DropoutWrapper output in natural layout [S, L, 2U] (the attention input).
+std::tuple<Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
+                                            const Tensor& pos2, const Tensor& wemb, const Tensor& p1emb,
+                                            const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U,
+                                            int64_t NX, bool bf16, bool store_c, int64_t seed, double keep_prob) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -142,10 +64,13 @@ std::tuple<Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& word, cons
   TORCH_CHECK(apack.numel() == 2 * U4 * NKS * 64 * KPL, "ina.lstm_fwd: apack has ", apack.numel(), " elems, expected ",
               2 * U4 * NKS * 64 * KPL);
   TORCH_CHECK(L * 2 * 16 * (int64_t)sizeof(int) * 4 <= 64 * 1024, "ina.lstm_fwd: L too large for the id stage");
-  auto hraw = at::empty({S, L, 2 * U}, word.options().dtype(bf16 ? at::kBFloat16 : at::kFloat));
+  const bool drop = keep_prob < 1.0;
+  auto hopt = word.options().dtype(bf16 ? at::kBFloat16 : at::kFloat);
   const int64_t ntiles = (S + 15) / 16;
+  auto hlane = store_c ? at::empty({ntiles, 2, L, U4, 64}, hopt) : at::empty({0}, hopt);
+  auto hnat = at::empty({S, L, 2 * U}, hopt);
   Tensor cst = store_c ? at::empty({ntiles, 2, L, U4, 64}, wemb.options()) : at::empty({0}, wemb.options());
-  if (S == 0) return {hraw, cst};
+  if (S == 0) return {hlane, cst, hnat};
   ina::LstmArgs a{};
   a.inst = inst.data_ptr<int>();
   a.S = (int)S;
@@ -160,17 +85,23 @@ std::tuple<Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& word, cons
   a.PD = (int)PD;
   a.apack = apack.data_ptr();
   a.bias = bias.data_ptr<float>();
-  a.hraw = hraw.data_ptr();
+  a.hraw = store_c ? hlane.data_ptr() : nullptr;
   a.cst = store_c ? cst.data_ptr<float>() : nullptr;
+  a.hdrop = hnat.data_ptr();
+  a.seed = (uint32_t)seed;
+  a.thr = keep_threshold(keep_prob);
+  a.inv_kp = (float)(1.0 / keep_prob);
+  a.drop = drop ? 1 : 0;
   check_launch(ina::lstm_fwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_fwd");
-  return {hraw, cst};
+  return {hlane, cst, hnat};
 }
 
 std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
                                             const Tensor& pos2, const Tensor& wemb, const Tensor& p1emb,
                                             const Tensor& p2emb, const Tensor& apack, const Tensor& a2pack,
                                             const Tensor& bias, const Tensor& hraw, const Tensor& cst, const Tensor& dH,
-                                            int64_t U, int64_t NX, bool bf16, bool word_grad, int64_t blocks) {
+                                            int64_t U, int64_t NX, bool bf16, bool word_grad, int64_t blocks,
+                                            int64_t seed, double keep_prob) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -188,8 +119,8 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   const int64_t S = inst.size(0), L = word.size(1), E = wemb.size(1), PD = p1emb.size(1);
   const int64_t DIN = E + 2 * PD, NF = DIN + U + 1, U4 = U / 4, KPL = frag_elems(bf16);
   TORCH_CHECK(DIN <= 4 * NX, "ina.lstm_bwd: input dim too large");
-  TORCH_CHECK(hraw.size(0) == S && hraw.size(1) == L && hraw.size(2) == 2 * U, "ina.lstm_bwd: hraw shape");
-  TORCH_CHECK(dH.sizes() == hraw.sizes(), "ina.lstm_bwd: dH shape");
+  TORCH_CHECK(hraw.numel() == ((S + 15) / 16) * 2 * L * U4 * 64, "ina.lstm_bwd: hlane shape");
+  TORCH_CHECK(dH.size(0) == S && dH.size(1) == L && dH.size(2) == 2 * U, "ina.lstm_bwd: dH shape");
   TORCH_CHECK(cst.numel() == ((S + 15) / 16) * 2 * L * U4 * 64, "ina.lstm_bwd: cst shape");
   const int64_t NSLOT = U4 + NX;
   TORCH_CHECK(a2pack.numel() == 2 * ((NSLOT + 3) / 4) * ((4 * U4 + KPL - 1) / KPL) * 64 * KPL, "ina.lstm_bwd: a2pack");
@@ -228,19 +159,18 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   a.dpos_slab = dpos_slab.data_ptr<float>();
   a.dwemb = word_grad ? dwemb.data_ptr<float>() : nullptr;
   a.bwd_blocks = (int)blocks;
+  a.seed = (uint32_t)seed;
+  a.thr = keep_threshold(keep_prob);
+  a.inv_kp = (float)(1.0 / keep_prob);
+  a.drop = keep_prob < 1.0 ? 1 : 0;
   check_launch(ina::lstm_bwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_bwd");
   return {dw_slab, dpos_slab, dwemb};
 }
 
 // ------------------------------------------------------------------ attention
-uint32_t keep_threshold(double kp) {
-  const double t = kp * 4294967296.0;
-  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
-}
 
 std::tuple<Tensor, Tensor> attn_fwd(const Tensor& hraw, const Tensor& inst, const Tensor& mask, const Tensor& w1pack,
-                                    const Tensor& b1, const Tensor& w2, int64_t seed, double keep_prob, int64_t U,
-                                    bool bf16, int64_t blocks) {
+                                    const Tensor& b1, const Tensor& w2, int64_t U, bool bf16, int64_t blocks) {
   check(hraw, "hraw", bf16 ? at::kBFloat16 : at::kFloat);
   check(inst, "inst", at::kInt);
   check(mask, "mask", at::kInt);
@@ -265,10 +195,6 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& hraw, const Tensor& inst, cons
   a.w1pack = w1pack.data_ptr();
   a.b1 = b1.data_ptr<float>();
   a.w2 = w2.data_ptr<float>();
-  a.seed = (uint32_t)seed;
-  a.thr = keep_threshold(keep_prob);
-  a.inv_kp = (float)(1.0 / keep_prob);
-  a.drop = keep_prob < 1.0 ? 1 : 0;
   a.e = e.data_ptr<float>();
   a.alphas = alphas.data_ptr<float>();
   if (blocks <= 0) blocks = 2048;
@@ -278,8 +204,8 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& hraw, const Tensor& inst, cons
 }
 
 std::tuple<Tensor, Tensor> attn_bwd(const Tensor& hraw, const Tensor& inst, const Tensor& w1pack, const Tensor& w1tpack,
-                                    const Tensor& b1, const Tensor& w2, int64_t seed, double keep_prob,
-                                    const Tensor& de, const Tensor& alphas, int64_t U, bool bf16, int64_t blocks) {
+                                    const Tensor& b1, const Tensor& w2, const Tensor& de, const Tensor& alphas,
+                                    int64_t U, bool bf16, int64_t blocks) {
   check(hraw, "hraw", bf16 ? at::kBFloat16 : at::kFloat);
   check(inst, "inst", at::kInt);
   check(w1pack, "w1pack", bf16 ? at::kBFloat16 : at::kFloat);
@@ -310,10 +236,6 @@ std::tuple<Tensor, Tensor> attn_bwd(const Tensor& hraw, const Tensor& inst, cons
   a.w1tpack = w1tpack.data_ptr();
   a.b1 = b1.data_ptr<float>();
   a.w2 = w2.data_ptr<float>();
-  a.seed = (uint32_t)seed;
-  a.thr = keep_threshold(keep_prob);
-  a.inv_kp = (float)(1.0 / keep_prob);
-  a.drop = keep_prob < 1.0 ? 1 : 0;
   a.de = de.data_ptr<float>();
   a.alphas = alphas.data_ptr<float>();
   a.dHraw = dH.data_ptr<float>();

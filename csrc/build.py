@@ -64,12 +64,12 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
     bsrc = os.path.join(CSRC, "bindings.cpp")
     bobj = os.path.join(OUT_DIR, "bindings.o")
     objs.append(bobj)
-    if _newer(bobj, [bsrc, __file__]):
+    if _newer(bobj, [bsrc, *headers, __file__]):
         cxx = shutil.which("g++") or "c++"
         cmd = [cxx, "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
                "-D_GLIBCXX_USE_CXX11_ABI=1", "-I/opt/rocm/include"]
         cmd += ["-I" + p for p in inc]
-        cmd += ["-I" + sysconfig.get_paths()["include"], "-c", bsrc, "-o", bobj]
+        cmd += ["-I" + sysconfig.get_paths()["include"], "-I" + os.path.join(CSRC, "include"), "-c", bsrc, "-o", bobj]
         tasks.append(cmd)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         for out in ex.map(_run, tasks):

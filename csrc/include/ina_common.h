@@ -37,11 +37,14 @@ INA_DEVICE f32x4_t mfma_f32(float a, float b, const f32x4_t& c) {
 }
 
 // ------------------------------------------------------------------ math
-INA_DEVICE float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// v_rcp_f32 (1 ulp) instead of the IEEE division sequence (div_scale/div_fmas/div_fixup): the
+// activations sit on the recurrence's dependency chain, so instruction latency is what matters.
+INA_DEVICE float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+INA_DEVICE float sigmoidf_(float x) { return fast_rcp(1.0f + __expf(-x)); }
 INA_DEVICE float tanhf_(float x) {
-  // tanh(x) = 1 - 2/(exp(2x)+1); saturates cleanly at +-1, abs err ~1e-7
-  float e = __expf(2.0f * x);
-  return 1.0f - 2.0f / (e + 1.0f);
+  // tanh(x) = 1 - 2/(exp(2x)+1); saturates cleanly at +-1, abs err ~2e-7
+  const float e = __expf(2.0f * x);
+  return 1.0f - 2.0f * fast_rcp(e + 1.0f);
 }
 
 // ------------------------------------------------------------------ RNG
@@ -54,11 +57,20 @@ INA_DEVICE uint32_t hash_u32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
-// Dropout keep decision for element `idx` of direction `dir` (reference.py::dropout_keep_mask).
+// Dropout: keep element `idx` (flat (seq*L + t)*U + unit) of direction `dir` iff
+// mix(idx * C1 + salt(seed, dir)) < thr.  Bit-identical to models/reference.py::dropout_keep_mask.
+INA_DEVICE uint32_t dropout_salt(uint32_t seed, uint32_t dir) {
+  return seed * 0x2545F491u + dir * 0x3C6EF372u + 0x1234567u;
+}
+INA_DEVICE bool dropout_keep_salted(uint32_t salt, uint32_t idx, uint32_t thr) {
+  uint32_t x = idx * 0x6C8E9CF5u + salt;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  return x < thr;
+}
 INA_DEVICE bool dropout_keep(uint32_t seed, uint32_t dir, uint32_t idx, uint32_t thr) {
-  uint32_t salt = seed * 0x9E37u + dir * 0x3C6EF372u + 0x1234567u;
-  uint32_t h = hash_u32(hash_u32(idx ^ salt) + (seed & 0x7FFFFFFFu));
-  return h < thr;
+  return dropout_keep_salted(dropout_salt(seed, dir), idx, thr);
 }
 
 // ------------------------------------------------------------------ reductions

@@ -5,8 +5,8 @@
 //   score  = x_proj @ W_a2                W_a2 [2u, 1]
 //   alphas = softmax_t(score + (1 - (mask>0)) * -2^31)
 //   e      = sum_t alphas_t * H_t
-// H is the BiLSTM output *after* the DropoutWrapper output dropout; the dropout mask is
-// regenerated here from the counter-based hash (no mask tensor is stored).
+// H is the BiLSTM output *after* the DropoutWrapper output dropout, applied once by lstm_fwd
+// (which stores the dropped copy); lstm_bwd re-applies the mask to the dH this kernel returns.
 //
 // One wave processes one sentence at a time (grid-stride).  The projection is computed
 // transposed, P^T[j, tok] = W1^T[j, i] H^T[i, tok], with v_mfma_f32_16x16x32_bf16 (or the f32
@@ -16,6 +16,7 @@
 // layout and feeds it straight back as the B operand of dH^T = W1 dP^T; dW1 = H^T dP is
 // accumulated with MFMAs after a wave-private LDS transpose (tokens become the K dimension).
 #include "ina_common.h"
+#include "ina_launch.h"
 
 using namespace ina;
 
@@ -71,25 +72,32 @@ INA_DEVICE int feat_of(int v, int q) {
   return 4 * v + q;
 }
 
-// Load the dropout-applied H values of token `tok` for lane group q: out fp32 values (hv) and
-// the MFMA B fragments (rounded for bf16).
+// Load the (already dropout-applied, by lstm_fwd) H values of token `tok` for lane group q.  Every
+// load is unconditional (clamped address + select): a lane-dependent branch around a load makes
+// hipcc wait vmcnt(0) per element and serialises the L2 round trips.
 template <int U, int NT, bool BF16>
-INA_DEVICE void load_h(const typename FT<BF16>::elem* __restrict__ hraw, long seq, int tok, int L, int q,
-                       uint32_t seed, uint32_t thr, float inv_kp, bool drop, float* hv) {
+INA_DEVICE void load_h(const typename FT<BF16>::elem* hraw, long seq, int tok, int L, int q, float* hv) {
   using Sh = AShape<U, NT, BF16>;
+  constexpr int H2 = Sh::H2;
+  const bool tv = tok < L;
+  const long row = (seq * L + (tv ? tok : L - 1)) * H2;
+  if constexpr (BF16) {
 #pragma unroll
-  for (int v = 0; v < Sh::NV; ++v) {
-    const int k = feat_of<BF16>(v, q);
-    float x = 0.f;
-    if (tok < L && k < Sh::H2) {
-      x = ld_elem(hraw + (seq * L + tok) * Sh::H2 + k);
-      if (drop) {
-        const int dirn = k >= U ? 1 : 0;
-        const uint32_t idx = (uint32_t)((seq * L + tok) * U + (k - dirn * U));
-        x = dropout_keep(seed, dirn, idx, thr) ? x * inv_kp : 0.f;
-      }
+    for (int ks = 0; ks < Sh::NKS; ++ks) {
+      const int k0 = 32 * ks + 8 * q;
+      const bool ok = tv && (k0 < H2);
+      const u16x8_t v = *reinterpret_cast<const u16x8_t*>(hraw + row + (ok ? k0 : 0));
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) hv[ks * 8 + jj] = ok ? bf2f(v[jj]) : 0.f;
     }
-    hv[v] = x;
+  } else {
+#pragma unroll
+    for (int v = 0; v < Sh::NV; ++v) {
+      const int k = feat_of<BF16>(v, q);
+      const bool ok = tv && (k < H2);
+      const float x = ld_elem(hraw + row + (ok ? k : 0));
+      hv[v] = ok ? x : 0.f;
+    }
   }
 }
 
@@ -98,9 +106,9 @@ INA_DEVICE void load_h(const typename FT<BF16>::elem* __restrict__ hraw, long se
 // ------------------------------------------------------------------------------------------
 template <int U, int NT, bool BF16>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(
-    const typename FT<BF16>::elem* __restrict__ hraw, const int* __restrict__ inst, const int* __restrict__ maskarr,
+    const typename FT<BF16>::elem* hraw, const int* __restrict__ inst, const int* __restrict__ maskarr,
     int S, int L, const typename FT<BF16>::frag* __restrict__ w1pack, const float* __restrict__ b1,
-    const float* __restrict__ w2, uint32_t seed, uint32_t thr, float inv_kp, int drop, float* __restrict__ e_out,
+    const float* __restrict__ w2, float* __restrict__ e_out,
     float* __restrict__ alphas) {
   using Sh = AShape<U, NT, BF16>;
   using frag = typename FT<BF16>::frag;
@@ -124,17 +132,18 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
     }
   for (int s = gw; s < S; s += nw) {
     const long row = (long)inst[s] * L;
-    float hv[NT][NV];
+    // pass 1: scores (projection + tanh + w2 dot), one token tile at a time
     float score[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int tok = 16 * nt + n;
-      load_h<U, NT, BF16>(hraw, s, tok, L, q, seed, thr, inv_kp, drop != 0, hv[nt]);
+      float hv[NV];
+      load_h<U, NT, BF16>(hraw, s, tok, L, q, hv);
       frag B[NKS];
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
 #pragma unroll
-        for (int j = 0; j < KPL; ++j) fset(B[ks], j, rnd(hv[nt][ks * KPL + j], BF16));
+        for (int j = 0; j < KPL; ++j) fset(B[ks], j, rnd(hv[ks * KPL + j], BF16));
       }
       float sp = 0.f;
 #pragma unroll
@@ -146,12 +155,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
         for (int r = 0; r < 4; ++r) sp += wj[m][r] * tanhf_(acc[r]);
       }
       sp = cross_group_sum(sp);
-      float v = -INFINITY;
-      if (tok < L) {
-        const float m01 = maskarr[row + tok] > 0 ? 1.f : 0.f;
-        v = sp + (1.f - m01) * -2147483648.f;
-      }
-      score[nt] = v;
+      const int mk = maskarr[row + (tok < L ? tok : L - 1)];
+      const float m01 = mk > 0 ? 1.f : 0.f;
+      score[nt] = (tok < L) ? sp + (1.f - m01) * -2147483648.f : -INFINITY;
     }
     float mx = -INFINITY;
 #pragma unroll
@@ -165,15 +171,20 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
     }
     sum = group16_sum(sum);
     const float inv = 1.f / sum;
+    asm volatile("" ::: "memory");  // keep pass-2 loads as re-reads (no CSE across passes)
+    // pass 2: pooling (H re-read from L1/L2)
     float ev[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) ev[v] = 0.f;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
+      const int tok = 16 * nt + n;
       const float a = p[nt] * inv;
-      if (q == 0 && 16 * nt + n < L) alphas[(long)s * L + 16 * nt + n] = a;
+      if (q == 0 && tok < L) alphas[(long)s * L + tok] = a;
+      float hv[NV];
+      load_h<U, NT, BF16>(hraw, s, tok, L, q, hv);
 #pragma unroll
-      for (int v = 0; v < NV; ++v) ev[v] += a * hv[nt][v];
+      for (int v = 0; v < NV; ++v) ev[v] += a * hv[v];
     }
 #pragma unroll
     for (int v = 0; v < NV; ++v) ev[v] = group16_sum(ev[v]);
@@ -191,10 +202,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
 // slab per block: [dW1 (H2*H2, row i, col j) | db1 (H2) | dw2 (H2)]
 template <int U, int NT, bool BF16>
 __global__ __launch_bounds__(256) void attn_bwd_kernel(
-    const typename FT<BF16>::elem* __restrict__ hraw, const int* __restrict__ inst, int S, int L,
+    const typename FT<BF16>::elem* hraw, const int* __restrict__ inst, int S, int L,
     const typename FT<BF16>::frag* __restrict__ w1pack, const typename FT<BF16>::frag* __restrict__ w1tpack,
-    const float* __restrict__ b1, const float* __restrict__ w2, uint32_t seed, uint32_t thr, float inv_kp,
-    int drop, const float* __restrict__ de, const float* __restrict__ alphas, float* __restrict__ dHraw,
+    const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ de,
+    const float* __restrict__ alphas, float* __restrict__ dHraw,
     float* __restrict__ slab) {
   using Sh = AShape<U, NT, BF16>;
   using frag = typename FT<BF16>::frag;
@@ -237,54 +248,77 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int k = feat_of<BF16>(v, q);
-      dev[v] = k < H2 ? de[(long)s * H2 + k] : 0.f;
+      const float x = de[(long)s * H2 + (k < H2 ? k : 0)];
+      dev[v] = k < H2 ? x : 0.f;
     }
-    float hv[NT][NV], pr[NT][MT][4], al[NT], da[NT];
+    float dei[MT][4];
 #pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * m + 4 * q + r;
+        const float x = de[(long)s * H2 + (i < H2 ? i : 0)];
+        dei[m][r] = i < H2 ? x : 0.f;
+      }
+    // pass 1: d(alpha)_t = de . H_t and the softmax-backward dot sum_t alpha_t d(alpha)_t
+    float al[NT], da[NT];
+#pragma unroll 1
     for (int nt = 0; nt < NT; ++nt) {
       const int tok = 16 * nt + n;
-      load_h<U, NT, BF16>(hraw, s, tok, L, q, seed, thr, inv_kp, drop != 0, hv[nt]);
+      float hv[NV];
+      load_h<U, NT, BF16>(hraw, s, tok, L, q, hv);
+      const float av = alphas[(long)s * L + (tok < L ? tok : L - 1)];
+      float d = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) d += dev[v] * hv[v];
+      d = cross_group_sum(d);
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        if (j == nt) {  // compile-time register index (no scratch)
+          al[j] = tok < L ? av : 0.f;
+          da[j] = d;
+        }
+    }
+    float sd = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) sd += al[nt] * da[nt];
+    sd = group16_sum(sd);
+    asm volatile("" ::: "memory");  // keep pass-2 loads as re-reads (no CSE across passes)
+    // pass 2: recompute the projection per token tile, form dP, dH, and stage dW1 operands
+#pragma unroll 1
+    for (int nt = 0; nt < NT; ++nt) {
+      const int tok = 16 * nt + n;
+      float alv = al[0], dav = da[0];
+#pragma unroll
+      for (int j = 1; j < NT; ++j)
+        if (j == nt) {
+          alv = al[j];
+          dav = da[j];
+        }
+      float hv[NV];
+      load_h<U, NT, BF16>(hraw, s, tok, L, q, hv);
       frag B[NKS];
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
 #pragma unroll
-        for (int j = 0; j < KPL; ++j) {
-          const float hr = rnd(hv[nt][ks * KPL + j], BF16);
-          fset(B[ks], j, hr);
-        }
+        for (int j = 0; j < KPL; ++j) fset(B[ks], j, rnd(hv[ks * KPL + j], BF16));
       }
+      const float ds = alv * (dav - sd);
+      float dp[MT][4];
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         f32x4_t acc = {bj[m][0], bj[m][1], bj[m][2], bj[m][3]};
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) acc = mma(w1pack[(m * NKS + ks) * 64 + lane], B[ks], acc);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) pr[nt][m][r] = tanhf_(acc[r]);
-      }
-      al[nt] = tok < L ? alphas[(long)s * L + tok] : 0.f;
-      float d = 0.f;
-#pragma unroll
-      for (int v = 0; v < NV; ++v) d += dev[v] * hv[nt][v];
-      da[nt] = cross_group_sum(d);
-    }
-    float sd = 0.f;
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) sd += al[nt] * da[nt];
-    sd = group16_sum(sd);
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int tok = 16 * nt + n;
-      const float ds = al[nt] * (da[nt] - sd);
-      float dp[MT][4];
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
         for (int r = 0; r < 4; ++r) {
-          dp[m][r] = ds * wj[m][r] * (1.f - pr[nt][m][r] * pr[nt][m][r]);
-          dw2a[m][r] += ds * pr[nt][m][r];
+          const float pr = tanhf_(acc[r]);
+          dp[m][r] = ds * wj[m][r] * (1.f - pr * pr);
+          dw2a[m][r] += ds * pr;
           db1a[m][r] += dp[m][r];
         }
-      // dH^T = W1 dP^T  (+ alpha * de)
+      }
+      // dH^T = W1 dP^T  (+ alpha * de), dropout mask re-applied
       frag B2[NKS2];
 #pragma unroll
       for (int ks = 0; ks < NKS2; ++ks) {
@@ -304,27 +338,22 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
         f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < NKS2; ++ks) acc = mma(w1tpack[(m * NKS2 + ks) * 64 + lane], B2[ks], acc);
-        if (tok < L) {
+        if (tok < L && 16 * m + 4 * q < H2) {
+          f32x4_t g;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int i = 16 * m + 4 * q + r;
-            if (i < H2) {
-              float g = acc[r] + al[nt] * de[(long)s * H2 + i];
-              if (drop) {
-                const int dirn = i >= U ? 1 : 0;
-                const uint32_t idx = (uint32_t)(((long)s * L + tok) * U + (i - dirn * U));
-                g = dropout_keep(seed, dirn, idx, thr) ? g * inv_kp : 0.f;
-              }
-              dHraw[((long)s * L + tok) * H2 + i] = g;
-            }
+            (void)i;
+            g[r] = acc[r] + alv * dei[m][r];
           }
+          *reinterpret_cast<f32x4_t*>(dHraw + ((long)s * L + tok) * H2 + 16 * m + 4 * q) = g;
         }
       }
       // stage H (MFMA operand values) and dP for the dW1 MFMA; tokens are the K dimension
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
         const int k = feat_of<BF16>(v, q);
-        if (k < ROWS) HT[k * RS + tok] = cvt_elem(hv[nt][v], (elem*)nullptr);
+        if (k < ROWS) HT[k * RS + tok] = cvt_elem(hv[v], (elem*)nullptr);
       }
 #pragma unroll
       for (int m = 0; m < MT; ++m)
@@ -393,25 +422,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
 // ------------------------------------------------------------------------------------------
 namespace ina {
 
-struct AttnArgs {
-  const void* hraw;
-  const int* inst;
-  const int* mask;
-  int S, L;
-  const void* w1pack;
-  const void* w1tpack;
-  const float* b1;
-  const float* w2;
-  uint32_t seed, thr;
-  float inv_kp;
-  int drop;
-  float* e;
-  float* alphas;
-  const float* de;
-  float* dHraw;
-  float* slab;
-  int blocks;
-};
+
 
 size_t attn_bwd_lds_bytes(int U, int NT, bool bf16) {
   const int H2 = 2 * U, MT = (H2 + 15) / 16;
@@ -426,7 +437,7 @@ static int attn_fwd_t(const AttnArgs& a, hipStream_t st) {
   using F = FT<BF16>;
   hipLaunchKernelGGL((attn_fwd_kernel<U, NT, BF16>), dim3(a.blocks), dim3(256), 0, st,
                      (const typename F::elem*)a.hraw, a.inst, a.mask, a.S, a.L, (const typename F::frag*)a.w1pack,
-                     a.b1, a.w2, a.seed, a.thr, a.inv_kp, a.drop, a.e, a.alphas);
+                     a.b1, a.w2, a.e, a.alphas);
   INA_CHECK_LAUNCH();
   return 0;
 }
@@ -436,8 +447,7 @@ static int attn_bwd_t(const AttnArgs& a, hipStream_t st) {
   const size_t lds = attn_bwd_lds_bytes(U, NT, BF16);
   hipLaunchKernelGGL((attn_bwd_kernel<U, NT, BF16>), dim3(a.blocks), dim3(256), lds, st,
                      (const typename F::elem*)a.hraw, a.inst, a.S, a.L, (const typename F::frag*)a.w1pack,
-                     (const typename F::frag*)a.w1tpack, a.b1, a.w2, a.seed, a.thr, a.inv_kp, a.drop, a.de,
-                     a.alphas, a.dHraw, a.slab);
+                     (const typename F::frag*)a.w1tpack, a.b1, a.w2, a.de, a.alphas, a.dHraw, a.slab);
   INA_CHECK_LAUNCH();
   return 0;
 }

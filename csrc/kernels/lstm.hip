@@ -14,6 +14,7 @@
 // The backward reuses the same trick for d[x;h] = W dG, and transposes (dG, XH) through
 // wave-private LDS every 2 steps to accumulate dW with MFMAs (32 samples per K-step).
 #include "ina_common.h"
+#include "ina_launch.h"
 
 using namespace ina;
 
@@ -70,13 +71,31 @@ INA_DEVICE float to_elem(float v, float*) { return v; }
 INA_DEVICE float from_elem(unsigned short v) { return bf2f(v); }
 INA_DEVICE float from_elem(float v) { return v; }
 
-// x feature f of token (wid, p1, p2); 0 beyond DIN.
-INA_DEVICE float gather_x(int f, int wid, int p1, int p2, const float* __restrict__ wemb, int E,
-                          const float* __restrict__ p1emb, const float* __restrict__ p2emb, int PD) {
-  if (f < E) return wemb[(long)wid * E + f];
-  if (f < E + PD) return p1emb[p1 * PD + (f - E)];
-  if (f < E + 2 * PD) return p2emb[p2 * PD + (f - E - PD)];
-  return 0.f;
+// Per-lane source of x feature f (loop invariant): word / pos1 / pos2 table column, or none.
+// The per-step gather is then ONE unconditional load per feature (no lane-dependent branch
+// around a load: hipcc would wait vmcnt(0) per element and serialise the L2 round trips).
+struct XSrc {
+  const float* base;
+  int stride, col, sel;  // sel: 0 word, 1 pos1, 2 pos2, 3 none
+};
+INA_DEVICE XSrc make_xsrc(int f, const float* __restrict__ wemb, int E, const float* __restrict__ p1emb,
+                          const float* __restrict__ p2emb, int PD) {
+  XSrc s;
+  if (f < E) {
+    s.base = wemb; s.stride = E; s.col = f; s.sel = 0;
+  } else if (f < E + PD) {
+    s.base = p1emb; s.stride = PD; s.col = f - E; s.sel = 1;
+  } else if (f < E + 2 * PD) {
+    s.base = p2emb; s.stride = PD; s.col = f - E - PD; s.sel = 2;
+  } else {
+    s.base = wemb; s.stride = 0; s.col = 0; s.sel = 3;
+  }
+  return s;
+}
+INA_DEVICE float gather_x(const XSrc& s, int wid, int p1, int p2) {
+  const int row = s.sel == 0 ? wid : (s.sel == 1 ? p1 : (s.sel == 2 ? p2 : 0));
+  const float v = s.base[(long)row * s.stride + s.col];
+  return s.sel == 3 ? 0.f : v;
 }
 
 INA_DEVICE void wave_lds_sync() {
@@ -95,7 +114,8 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(
     const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
     const float* __restrict__ p1emb, const float* __restrict__ p2emb, int PD,
     const typename FragT<BF16>::type* __restrict__ apack, const float* __restrict__ bias,
-    typename FragT<BF16>::elem* __restrict__ hout, float* __restrict__ cst) {
+    typename FragT<BF16>::elem* __restrict__ hlane, float* __restrict__ cst, typename FragT<BF16>::elem* __restrict__ hnat,
+    uint32_t seed, uint32_t thr, float inv_kp, int drop) {
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
   constexpr int U4 = Sh::U4, KPL = Sh::KPL, NKS = Sh::NKS, NMT = Sh::NMT;
@@ -122,6 +142,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(
   if (tile >= ntiles) return;
   const int seq = tile * 16 + n;
   const bool valid = seq < S;
+  const uint32_t salt = dropout_salt(seed, (uint32_t)dir);
 
   frag A[NMT][NKS];
   const frag* ap = apack + (size_t)dir * NMT * NKS * 64;
@@ -139,11 +160,13 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(
 #pragma unroll
   for (int m = 0; m < U4; ++m) h[m] = c[m] = 0.f;
 
+  XSrc xs[NX];
+#pragma unroll
+  for (int xi = 0; xi < NX; ++xi) xs[xi] = make_xsrc(4 * xi + q, wemb, E, p1emb, p2emb, PD);
   auto load_x = [&](int t, float* xv) {
     int2 id = ids[n * L + t];
 #pragma unroll
-    for (int xi = 0; xi < NX; ++xi)
-      xv[xi] = gather_x(4 * xi + q, id.x, id.y & 0xffff, id.y >> 16, wemb, E, p1emb, p2emb, PD);
+    for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(xs[xi], id.x, id.y & 0xffff, id.y >> 16);
   };
   float xv[NX], xn[NX];
   load_x(dir ? L - 1 : 0, xv);
@@ -176,9 +199,24 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(
       h[m] = hv;
     }
     if (valid) {
+      // natural-layout copy for the attention layer; dropout (DropoutWrapper output) applied here
       const long o = ((long)seq * L + t) * (2 * U) + dir * U + q;
+      if (drop) {
+        const uint32_t base = (uint32_t)(((long)seq * L + t) * U + q);
 #pragma unroll
-      for (int m = 0; m < U4; ++m) hout[o + 4 * m] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
+        for (int m = 0; m < U4; ++m) {
+          const bool keep = dropout_keep_salted(salt, base + 4 * m, thr);
+          hnat[o + 4 * m] = to_elem(keep ? h[m] * inv_kp : 0.f, (typename FragT<BF16>::elem*)nullptr);
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < U4; ++m) hnat[o + 4 * m] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
+      }
+    }
+    if (hlane) {  // raw recurrent h for the backward, lane-native (coalesced 128-B rows)
+      typename FragT<BF16>::elem* hp = hlane + (((size_t)tile * 2 + dir) * L + t) * U4 * 64 + lane;
+#pragma unroll
+      for (int m = 0; m < U4; ++m) hp[m * 64] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
     }
     if (cst) {
       float* cp = cst + (((size_t)tile * 2 + dir) * L + t) * U4 * 64 + lane;
@@ -203,7 +241,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
     const typename FragT<BF16>::type* __restrict__ apack, const typename FragT<BF16>::type* __restrict__ a2pack,
     const float* __restrict__ bias, const typename FragT<BF16>::elem* __restrict__ hraw,
     const float* __restrict__ cst, const float* __restrict__ dH, float* __restrict__ dw_slab,
-    float* __restrict__ dpos_slab, float* __restrict__ dwemb) {
+    float* __restrict__ dpos_slab, float* __restrict__ dwemb, uint32_t seed, uint32_t thr, float inv_kp, int drop) {
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
   using elem = typename FragT<BF16>::elem;
@@ -255,35 +293,68 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
 #pragma unroll
     for (int b = 0; b < FTMAX; ++b) accw[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  XSrc xs[NX];
+#pragma unroll
+  for (int xi = 0; xi < NX; ++xi) xs[xi] = make_xsrc(4 * xi + q, wemb, E, p1emb, p2emb, PD);
+
   for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const int tile = g * 4 + wave;
     if (tile >= ntiles) continue;  // no block-level barrier inside the group loop
     const int seq = tile * 16 + n;
     const bool valid = seq < S;
-    const long rowbase = valid ? (long)inst[seq] * L : 0;
+    const long seqc = valid ? seq : S - 1;  // clamped row for unconditional loads
+    const long rowbase = (long)inst[seqc] * L;
     const float* cbase = cst + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
-    float dh_rec[U4], dc_rec[U4], ccur[U4];
-#pragma unroll
-    for (int m = 0; m < U4; ++m) {
-      dh_rec[m] = dc_rec[m] = 0.f;
-      ccur[m] = cbase[((size_t)(dir ? 0 : L - 1) * U4 + m) * 64];
+    const elem* hbase = hraw + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
+    const uint32_t dsalt = dropout_salt(seed, (uint32_t)dir);
+    auto tof = [&](int tau) { return dir ? (L - 1 - tau) : tau; };  // processing step -> time
+    // software pipeline: ids two steps ahead, everything else one step ahead
+    int wid_c, p1_c, p2_c, wid_n, p1_n, p2_n;
+    {
+      const int t0 = tof(L - 1), t1 = tof(L >= 2 ? L - 2 : 0);
+      wid_c = word[rowbase + t0]; p1_c = pos1[rowbase + t0]; p2_c = pos2[rowbase + t0];
+      wid_n = word[rowbase + t1]; p1_n = pos1[rowbase + t1]; p2_n = pos2[rowbase + t1];
     }
-    for (int tau = L - 1; tau >= 0; --tau) {
-      const int t = dir ? (L - 1 - tau) : tau;
-      const int tp = dir ? t + 1 : t - 1;  // time index of the previous processing step
-      const bool has_prev = tau > 0;
-      // ---- loads
-      const int wid = word[rowbase + t];
-      const int p1 = pos1[rowbase + t], p2 = pos2[rowbase + t];
-      float xv[NX];
+    float xv[NX], hp[U4], cprev[U4], ccur[U4], dhin[U4];
+    {
+      const int t = tof(L - 1), tp = tof(L >= 2 ? L - 2 : 0);
 #pragma unroll
-      for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(4 * xi + q, wid, p1, p2, wemb, E, p1emb, p2emb, PD);
-      float hp[U4], cprev[U4], dhin[U4];
+      for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(xs[xi], wid_c, p1_c, p2_c);
 #pragma unroll
       for (int m = 0; m < U4; ++m) {
-        cprev[m] = has_prev ? cbase[((size_t)tp * U4 + m) * 64] : 0.f;
-        hp[m] = (has_prev && valid) ? from_elem(hraw[((long)seq * L + tp) * (2 * U) + dir * U + 4 * m + q]) : 0.f;
-        dhin[m] = valid ? dH[((long)seq * L + t) * (2 * U) + dir * U + 4 * m + q] : 0.f;
+        ccur[m] = cbase[((size_t)t * U4 + m) * 64];
+        const float cp = cbase[((size_t)tp * U4 + m) * 64];
+        cprev[m] = L >= 2 ? cp : 0.f;
+        const float hv = from_elem(hbase[((size_t)tp * U4 + m) * 64]);
+        hp[m] = (L >= 2 && valid) ? hv : 0.f;
+        const float dv = dH[(seqc * L + t) * (2 * U) + dir * U + 4 * m + q];
+        const bool keep = !drop || dropout_keep_salted(dsalt, (uint32_t)((seqc * L + t) * U + 4 * m + q), thr);
+        dhin[m] = (valid && keep) ? dv * inv_kp : 0.f;
+      }
+    }
+    float dh_rec[U4], dc_rec[U4];
+#pragma unroll
+    for (int m = 0; m < U4; ++m) dh_rec[m] = dc_rec[m] = 0.f;
+    for (int tau = L - 1; tau >= 0; --tau) {
+      const int wid = wid_c, p1 = p1_c, p2 = p2_c;
+      // ---- prefetch step tau-1 (x, h_{tau-2}, c_{tau-2}, dH_{tau-1}) and ids of tau-2
+      const int taun = tau >= 1 ? tau - 1 : 0;
+      const int taunn = tau >= 2 ? tau - 2 : 0;
+      const bool n_has_prev = tau >= 2;
+      const int tn = tof(taun), tnp = tof(taunn), tnn = tof(taunn);
+      const int wid_nn = word[rowbase + tnn], p1_nn = pos1[rowbase + tnn], p2_nn = pos2[rowbase + tnn];
+      float xv_n[NX], hp_n[U4], cprev_n[U4], dhin_n[U4];
+#pragma unroll
+      for (int xi = 0; xi < NX; ++xi) xv_n[xi] = gather_x(xs[xi], wid_n, p1_n, p2_n);
+#pragma unroll
+      for (int m = 0; m < U4; ++m) {
+        const float cp = cbase[((size_t)tnp * U4 + m) * 64];
+        cprev_n[m] = n_has_prev ? cp : 0.f;
+        const float hv = from_elem(hbase[((size_t)tnp * U4 + m) * 64]);
+        hp_n[m] = (n_has_prev && valid) ? hv : 0.f;
+        const float dv = dH[(seqc * L + tn) * (2 * U) + dir * U + 4 * m + q];
+        const bool keep = !drop || dropout_keep_salted(dsalt, (uint32_t)((seqc * L + tn) * U + 4 * m + q), thr);
+        dhin_n[m] = (valid && keep) ? dv * inv_kp : 0.f;
       }
       // ---- recompute gates
       frag B[NKS];
@@ -317,7 +388,6 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
         dg[m][1] = dj * (1.f - jg * jg);
         dg[m][2] = df * fg * (1.f - fg);
         dg[m][3] = d_o * og * (1.f - og);
-        ccur[m] = cprev[m];
       }
       // ---- d[x;h] = W dG
       frag B2[NKS2];
@@ -345,15 +415,11 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
       if (valid) {
 #pragma unroll
         for (int xi = 0; xi < NX; ++xi) {
-          const int f = 4 * xi + q;
           const float v = dslot[U4 + xi];
-          if (f < E) {
-            if (dwemb) atomicAdd(&dwemb[(long)wid * E + f], v);
-          } else if (f < E + PD) {
-            atomicAdd(&dpos_lds[p1 * PD + (f - E)], v);
-          } else if (f < E + 2 * PD) {
-            atomicAdd(&dpos_lds[(P2 + p2) * PD + (f - E - PD)], v);
-          }
+          const int sel = xs[xi].sel;
+          if (sel == 1) atomicAdd(&dpos_lds[p1 * PD + xs[xi].col], v);
+          if (sel == 2) atomicAdd(&dpos_lds[(P2 + p2) * PD + xs[xi].col], v);
+          if (sel == 0 && dwemb) atomicAdd(&dwemb[(long)wid * E + xs[xi].col], v);
         }
       }
       // ---- stage (dG, XH) for the dW MFMA: sample column = n + 16 * (tau & 1)
@@ -404,7 +470,6 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
           }
         }
         wave_lds_sync();
-        // clear the sample columns so a half-filled tail chunk contributes nothing stale
 #pragma unroll
         for (int m = 0; m < U4; ++m)
 #pragma unroll
@@ -414,6 +479,18 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
           }
         wave_lds_sync();
       }
+      // ---- rotate the pipeline
+#pragma unroll
+      for (int m = 0; m < U4; ++m) {
+        ccur[m] = cprev[m];
+        cprev[m] = cprev_n[m];
+        hp[m] = hp_n[m];
+        dhin[m] = dhin_n[m];
+      }
+#pragma unroll
+      for (int xi = 0; xi < NX; ++xi) xv[xi] = xv_n[xi];
+      wid_c = wid_n; p1_c = p1_n; p2_c = p2_n;
+      wid_n = wid_nn; p1_n = p1_nn; p2_n = p2_nn;
     }
   }
   // ---- reduce dW across the 4 waves through LDS (reuse the transpose region as f32)
@@ -443,29 +520,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
 // ------------------------------------------------------------------------------------------
 namespace ina {
 
-struct LstmArgs {
-  const int* inst;
-  int S;
-  const int* word;
-  const int* pos1;
-  const int* pos2;
-  int L;
-  const float* wemb;
-  int E;
-  const float* p1emb;
-  const float* p2emb;
-  int PD;
-  const void* apack;
-  const void* a2pack;
-  const float* bias;
-  void* hraw;
-  float* cst;
-  const float* dH;
-  float* dw_slab;
-  float* dpos_slab;
-  float* dwemb;
-  int bwd_blocks;
-};
+
 
 size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD) {
   const int KPL = bf16 ? 8 : 1;
@@ -495,7 +550,7 @@ static int launch_fwd_t(const LstmArgs& a, hipStream_t st) {
   size_t lds = (size_t)4 * 16 * a.L * sizeof(int2);
   hipLaunchKernelGGL((lstm_fwd_kernel<U, NX, BF16>), grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1,
                      a.pos2, a.L, a.wemb, a.E, a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, a.bias,
-                     (elem*)a.hraw, a.cst);
+                     (elem*)a.hraw, a.cst, (elem*)a.hdrop, a.seed, a.thr, a.inv_kp, a.drop);
   INA_CHECK_LAUNCH();
   return 0;
 }
@@ -514,7 +569,8 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   }
   hipLaunchKernelGGL(kfn, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, (const frag*)a.a2pack, a.bias,
-                     (const elem*)a.hraw, a.cst, a.dH, a.dw_slab, a.dpos_slab, a.dwemb);
+                     (const elem*)a.hraw, a.cst, a.dH, a.dw_slab, a.dpos_slab, a.dwemb, a.seed, a.thr, a.inv_kp,
+                     a.drop);
   INA_CHECK_LAUNCH();
   return 0;
 }

@@ -18,6 +18,7 @@
 // The backward recomputes P/T and produces dC, dQ (registers, summed over slices), the per-episode
 // dw contribution and dP (bf16, for the dM = C^T dP reduction GEMM across episodes).
 #include "ina_common.h"
+#include "ina_launch.h"
 
 using namespace ina;
 
@@ -348,25 +349,7 @@ __global__ __launch_bounds__(256) void ntn_bwd_kernel(
 // ------------------------------------------------------------------------------------------
 namespace ina {
 
-struct NtnArgs {
-  const float* cls;
-  const float* e;
-  int E, N, K, Q, H, h;
-  const void* mpack;
-  const void* m2pack;
-  const void* wpack;
-  const void* wtpack;
-  const float* wvec;
-  const float* bias;
-  float* probs;
-  const float* dz;
-  float* dcls;
-  float* de;
-  void* dp_out;
-  float* dw_slab;
-  int blocks;
-  int paper;
-};
+
 
 template <int MTH, int QT, bool P>
 static int ntn_fwd_t(const NtnArgs& a, hipStream_t st) {

@@ -50,12 +50,17 @@ def hash_u32(x: torch.Tensor) -> torch.Tensor:
 
 def dropout_keep_mask(seed: int, direction: int, S: int, L: int, u: int, keep_prob: float,
                       device=None) -> torch.Tensor:
-    """Bernoulli(keep_prob) mask [S, L, u] for one LSTM direction's outputs (float 0/1)."""
+    """Bernoulli(keep_prob) mask [S, L, u] for one LSTM direction's outputs (float 0/1).
+    Same integer recipe as ``dropout_keep_salted`` in csrc/include/ina_common.h (products are
+    reduced mod 2^32 after every multiply; all factors < 2^32 so int64 never overflows)."""
     idx = torch.arange(S * L * u, dtype=torch.int64, device=device)
-    salt = ((seed & _M32) * 0x9E37 + direction * 0x3C6EF372 + 0x1234567) & _M32
-    h = hash_u32(hash_u32(idx ^ salt) + (seed & 0x7FFFFFFF))
-    thr = int(keep_prob * 4294967296.0)
-    return (h < thr).to(torch.float32).view(S, L, u)
+    salt = ((seed & 0x7FFFFFFF) * 0x2545F491 + direction * 0x3C6EF372 + 0x1234567) & _M32
+    x = (idx * 0x6C8E9CF5 + salt) & _M32
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    thr = min(int(keep_prob * 4294967296.0), 0xFFFFFFFF)
+    return (x < thr).to(torch.float32).view(S, L, u)
 
 
 # ------------------------------------------------------------------ encoder

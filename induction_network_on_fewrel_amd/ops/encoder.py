@@ -3,9 +3,10 @@
 One ``torch.autograd.Function`` spans the whole encoder so that the bf16 BiLSTM output never
 crosses an autograd boundary (its gradient stays fp32 inside ``backward``).
 
-forward:  lstm_fwd (gather + MFMA recurrence, both directions)  ->  attn_fwd (dropout regenerated
-          from the counter hash, MFMA projection, masked softmax, pooling)
-backward: attn_bwd (recompute projection, dH, dW1/db1/dw2 slabs)  ->  lstm_bwd (BPTT, dW/db/pos slabs)
+forward:  lstm_fwd (gather + MFMA recurrence, both directions; applies the output dropout once and
+          stores the dropped copy)  ->  attn_fwd (MFMA projection, masked softmax, pooling)
+backward: attn_bwd (recompute projection, dH, dW1/db1/dw2 slabs)  ->  lstm_bwd (re-applies the dropout
+          mask from the counter hash, BPTT, dW/db/pos slabs)
 
 Reference layers: model/base.py:76-86 (embedding), model/graph.py:30-53 (BiLSTM + attention),
 model/layer_module.py:49-98 (self_attention).
@@ -29,15 +30,16 @@ class EncoderFn(torch.autograd.Function):
         apack, a2pack = pack_lstm(Kf, Kb, U, DIN, bf16)
         bias = torch.stack([bf.detach(), bb.detach()]).float().contiguous()
         need_grad = ctx.needs_input_grad[5:15].count(True) > 0 if hasattr(ctx, "needs_input_grad") else True
-        hraw, cst = o.lstm_fwd(inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
-                               p2emb.detach().contiguous(), apack, bias, U, sh["NX"], bf16, bool(need_grad))
-        w1pack, w1tpack = pack_attn(W1, bf16)
         kp = float(meta["keep_prob"])
-        e, alphas = o.attn_fwd(hraw, inst, mask, w1pack, b1.detach().contiguous(), w2.detach().reshape(-1).contiguous(),
-                               int(meta["seed"]), kp, U, bf16, int(meta.get("attn_blocks", 0)))
+        hlane, cst, hnat = o.lstm_fwd(inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
+                                      p2emb.detach().contiguous(), apack, bias, U, sh["NX"], bf16, bool(need_grad),
+                                      int(meta["seed"]), kp)
+        w1pack, w1tpack = pack_attn(W1, bf16)
+        e, alphas = o.attn_fwd(hnat, inst, mask, w1pack, b1.detach().contiguous(),
+                               w2.detach().reshape(-1).contiguous(), U, bf16, int(meta.get("attn_blocks", 0)))
         if need_grad:
-            ctx.save_for_backward(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hraw, cst,
-                                  w1pack, w1tpack, b1, w2, alphas)
+            ctx.save_for_backward(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst,
+                                  w1pack, w1tpack, b1, w2, alphas, hnat)
             ctx.meta = dict(meta, NX=sh["NX"], DIN=DIN)
         ctx.mark_non_differentiable(alphas)
         return e, alphas
@@ -45,14 +47,14 @@ class EncoderFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, de, _dalpha):
         o = ops()
-        (inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hraw, cst, w1pack, w1tpack, b1, w2,
-         alphas) = ctx.saved_tensors
+        (inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst, w1pack, w1tpack, b1, w2,
+         alphas, hnat) = ctx.saved_tensors
         m = ctx.meta
         U, bf16, DIN = m["U"], m["bf16"], m["DIN"]
         H2 = 2 * U
-        dH, aslab = o.attn_bwd(hraw, inst, w1pack, w1tpack, b1.detach().contiguous(),
-                               w2.detach().reshape(-1).contiguous(), int(m["seed"]), float(m["keep_prob"]),
-                               de.contiguous().float(), alphas, U, bf16, int(m.get("attn_blocks", 0)))
+        dH, aslab = o.attn_bwd(hnat, inst, w1pack, w1tpack, b1.detach().contiguous(),
+                               w2.detach().reshape(-1).contiguous(), de.contiguous().float(), alphas, U, bf16,
+                               int(m.get("attn_blocks", 0)))
         a = aslab.sum(0)
         dW1 = a[: H2 * H2].view(H2, H2)
         db1 = a[H2 * H2: H2 * H2 + H2]
@@ -60,8 +62,8 @@ class EncoderFn(torch.autograd.Function):
         word_grad = bool(m.get("word_grad", False))
         dw_slab, dpos_slab, dwemb = o.lstm_bwd(inst, word, pos1, pos2, wemb.detach().contiguous(),
                                                p1emb.detach().contiguous(), p2emb.detach().contiguous(), apack, a2pack,
-                                               bias, hraw, cst, dH, U, m["NX"], bf16, word_grad,
-                                               int(m.get("lstm_blocks", 0)))
+                                               bias, hlane, cst, dH, U, m["NX"], bf16, word_grad,
+                                               int(m.get("lstm_blocks", 0)), int(m["seed"]), float(m["keep_prob"]))
         D = dw_slab.sum(0)                         # [2, 4U, DIN+U+1]
         dKf = D[0, :, : DIN + U].t().contiguous()
         dKb = D[1, :, : DIN + U].t().contiguous()

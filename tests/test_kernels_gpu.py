@@ -72,8 +72,9 @@ def test_lstm_forward(dtype):
     apack, _ = pack_lstm(p["lstm_fw_kernel"], p["lstm_bw_kernel"], U, DIN, bf16)
     bias = torch.stack([p["lstm_fw_bias"], p["lstm_bw_bias"]]).detach().float().contiguous()
     word, pos1, pos2, mask = dd.arrays()
-    hraw, cst = ops().lstm_fwd(inst, word, pos1, pos2, p["word_embedding"].detach(), p["pos1_embedding"].detach(),
-                               p["pos2_embedding"].detach(), apack, bias, U, sh["NX"], bf16, True)
+    hlane, cst, hraw = ops().lstm_fwd(inst, word, pos1, pos2, p["word_embedding"].detach(),
+                                      p["pos1_embedding"].detach(), p["pos2_embedding"].detach(), apack, bias, U,
+                                      sh["NX"], bf16, True, 0, 1.0)
     torch.cuda.synchronize()
     w, a1, a2, _ = _gathered(dd, inst)
     with torch.no_grad():
@@ -86,8 +87,10 @@ def test_lstm_forward(dtype):
     eb = _relerr(hraw[..., U:].float(), hb)
     c = _unpack_cst(cst, S, L, U)
     ec = _relerr(c, torch.cat([cf, cb], -1))
-    print(f"lstm fwd {dtype}: h_fw {ef:.2e} h_bw {eb:.2e} c {ec:.2e}")
-    assert ef < tol and eb < tol and ec < tol
+    hl = _unpack_cst(hlane.float(), S, L, U)
+    eh = _relerr(hl, hraw.float())
+    print(f"lstm fwd {dtype}: h_fw {ef:.2e} h_bw {eb:.2e} c {ec:.2e} hlane {eh:.2e}")
+    assert ef < tol and eb < tol and ec < tol and eh == 0.0
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
@@ -103,12 +106,14 @@ def test_attention_forward(dtype, keep_prob):
     apack, _ = pack_lstm(p["lstm_fw_kernel"], p["lstm_bw_kernel"], U, DIN, bf16)
     bias = torch.stack([p["lstm_fw_bias"], p["lstm_bw_bias"]]).detach().float().contiguous()
     word, pos1, pos2, mask = dd.arrays()
-    hraw, _ = ops().lstm_fwd(inst, word, pos1, pos2, p["word_embedding"].detach(), p["pos1_embedding"].detach(),
-                             p["pos2_embedding"].detach(), apack, bias, U, lstm_shape(U, DIN, bf16)["NX"], bf16, False)
-    w1p, _ = pack_attn(p["attn_kernel"], bf16)
     seed = 1234
-    e, alphas = ops().attn_fwd(hraw, inst, mask, w1p, p["attn_bias"].detach().contiguous(),
-                               p["attn_w2"].detach().reshape(-1).contiguous(), seed, keep_prob, U, bf16, 0)
+    hlane, _, hdrop = ops().lstm_fwd(inst, word, pos1, pos2, p["word_embedding"].detach(),
+                                     p["pos1_embedding"].detach(), p["pos2_embedding"].detach(), apack, bias, U,
+                                     lstm_shape(U, DIN, bf16)["NX"], bf16, True, seed, keep_prob)
+    hraw = _unpack_cst(hlane.float(), inst.shape[0], word.shape[1], U)
+    w1p, _ = pack_attn(p["attn_kernel"], bf16)
+    e, alphas = ops().attn_fwd(hdrop, inst, mask, w1p, p["attn_bias"].detach().contiguous(),
+                               p["attn_w2"].detach().reshape(-1).contiguous(), U, bf16, 0)
     torch.cuda.synchronize()
     S, L = hraw.shape[0], hraw.shape[1]
     Hin = hraw.float()
