@@ -302,7 +302,8 @@ Tensor ntn_fwd(const Tensor& cls, const Tensor& e, const Tensor& mpack, const Te
   TORCH_CHECK(N <= 16 && N * Q <= 64, "ina.ntn_fwd: needs N <= 16 and N*Q <= 64");
   TORCH_CHECK(MTH == 1 || MTH == 3 || MTH == 4, "ina.ntn_fwd: unsupported H ", H);
   TORCH_CHECK(cls.numel() == E * N * H, "ina.ntn_fwd: cls shape");
-  TORCH_CHECK(mpack.numel() == h * MTH * NKA * 64 * 8, "ina.ntn_fwd: mpack size");
+  const int64_t hp = 2 * ((h + 1) / 2);  // packs are padded to an even number of slices
+  TORCH_CHECK(mpack.numel() == hp * MTH * NKA * 64 * 8, "ina.ntn_fwd: mpack size");
   if (paper) {
     check(wvec, "wvec", at::kFloat);
     TORCH_CHECK(wvec.numel() == h, "ina.ntn_fwd: paper head w must be [h]");
@@ -328,8 +329,8 @@ Tensor ntn_fwd(const Tensor& cls, const Tensor& e, const Tensor& mpack, const Te
   a.bias = bias.data_ptr<float>();
   a.probs = probs.data_ptr<float>();
   a.paper = paper ? 1 : 0;
-  if (blocks <= 0) blocks = 2048;
-  a.blocks = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (E + 3) / 4));
+  if (blocks <= 0) blocks = 1024;  // workgroups of 8 episodes (grid-stride beyond)
+  a.blocks = (int)std::max<int64_t>(1, blocks);
   check_launch(ina::ntn_fwd(a, cur_stream()), "ntn_fwd");
   return probs;
 }
@@ -351,12 +352,13 @@ std::tuple<Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tensor& e, c
   TORCH_CHECK(H % 4 == 0, "ina.ntn_bwd: H must be a multiple of 4");
   TORCH_CHECK(dz.numel() == E * N * Q * N, "ina.ntn_bwd: dz shape");
   TORCH_CHECK(de.sizes() == e.sizes(), "ina.ntn_bwd: de shape");
-  TORCH_CHECK(m2pack.numel() == h * MTH * NKB * 64 * 8, "ina.ntn_bwd: m2pack size");
+  const int64_t hp = 2 * ((h + 1) / 2);
+  TORCH_CHECK(m2pack.numel() == hp * MTH * NKB * 64 * 8 && mpack.numel() == m2pack.numel(), "ina.ntn_bwd: pack size");
   if (paper) {
     check(wvec, "wvec", at::kFloat);
   } else {
     check(wtpack, "wtpack", at::kBFloat16);
-    TORCH_CHECK(wtpack.numel() == h * 64 * 8, "ina.ntn_bwd: wtpack size");
+    TORCH_CHECK(wtpack.numel() == hp * 64 * 8, "ina.ntn_bwd: wtpack size");
   }
   auto dcls = at::empty({E, N, H}, e.options());
   auto dp = at::empty({E * N, h * H}, e.options().dtype(at::kBFloat16));
@@ -381,8 +383,8 @@ std::tuple<Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tensor& e, c
   a.dp_out = dp.data_ptr();
   a.dw_slab = dw.data_ptr<float>();
   a.paper = paper ? 1 : 0;
-  if (blocks <= 0) blocks = 2048;
-  a.blocks = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (E + 3) / 4));
+  if (blocks <= 0) blocks = 1024;
+  a.blocks = (int)std::max<int64_t>(1, blocks);
   check_launch(ina::ntn_bwd(a, cur_stream()), "ntn_bwd");
   return {dcls, dp, dw};
 }

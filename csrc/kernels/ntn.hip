@@ -17,6 +17,10 @@
 // ("kmap32").  Every memory operand that meets such a fragment is packed with the same map.
 // The backward recomputes P/T and produces dC, dQ (registers, summed over slices), the per-episode
 // dw contribution and dP (bf16, for the dM = C^T dP reduction GEMM across episodes).
+//
+// A workgroup is 8 waves = 8 episodes; the packed M / w fragments of each slice pair are staged ONCE
+// per workgroup into LDS (double buffered, one barrier per pair) and shared by the 8 episodes, so the
+// L2 traffic for M is 1/8 of a wave-per-episode design (which measured 76 % SQ_WAIT_ANY).
 #include "ina_common.h"
 #include "ina_launch.h"
 
@@ -41,28 +45,65 @@ constexpr f32x4_t Z4 = {0.f, 0.f, 0.f, 0.f};
 
 }  // namespace
 
+
+constexpr int NTN_WAVES = 8;
+constexpr int NTN_THREADS = NTN_WAVES * 64;
+
+// Stage slice pair p straight into LDS with global_load_lds (16 B / lane, one 1-KiB fragment per wave
+// instruction, no staging registers).  Staged pair layout (fragments of 64 lanes x 16 B):
+// [mpack: 2*MTH*NKA][m2pack: 2*MTH*NKB (backward only)][w: NSW].  The host pads every packed array to
+// an even number of slices, so no lane needs a bounds check.
+INA_DEVICE void glds16(const u16x8_t* gsrc_lane, u16x8_t* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc_lane,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+template <int MTH, int NSW, bool WITH_M2>
+INA_DEVICE void ntn_stage(u16x8_t* buf, int p, const u16x8_t* __restrict__ mpack, const u16x8_t* __restrict__ m2pack,
+                          const u16x8_t* __restrict__ wsrc, int w_per_pair) {
+  constexpr int NKA = (MTH + 1) / 2, NKB = (MTH + 1) / 2;
+  constexpr int F1 = 2 * MTH * NKA, F2 = WITH_M2 ? 2 * MTH * NKB : 0, FR = F1 + F2 + NSW;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int f = wave; f < FR; f += NTN_WAVES) {
+    const u16x8_t* src;
+    if (f < F1)
+      src = mpack + ((long)2 * p * MTH * NKA + f) * 64;
+    else if (f < F1 + F2)
+      src = m2pack + ((long)2 * p * MTH * NKB + (f - F1)) * 64;
+    else
+      src = wsrc + ((long)p * w_per_pair + (f - F1 - F2)) * 64;
+    glds16(src + lane, buf + f * 64);
+  }
+}
+INA_DEVICE void stage_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // ------------------------------------------------------------------------------------------
 template <int MTH, int QT, bool PAPER>
-__global__ __launch_bounds__(256) void ntn_fwd_kernel(const float* __restrict__ cls, const float* __restrict__ e, int E,
-                                                      int N, int K, int Q, int H, int h,
-                                                      const u16x8_t* __restrict__ mpack,
-                                                      const u16x8_t* __restrict__ wpack,
-                                                      const float* __restrict__ wvec, const float* __restrict__ bias,
-                                                      float* __restrict__ probs) {
+__global__ __launch_bounds__(NTN_THREADS) void ntn_fwd_kernel(const float* __restrict__ cls, const float* __restrict__ e,
+                                                              int E, int N, int K, int Q, int H, int h,
+                                                              const u16x8_t* __restrict__ mpack,
+                                                              const u16x8_t* __restrict__ wpack,
+                                                              const float* __restrict__ wvec,
+                                                              const float* __restrict__ bias, float* __restrict__ probs) {
   constexpr int NKA = (MTH + 1) / 2;  // K steps over a (32 each)
   constexpr int NKB = (MTH + 1) / 2;  // K steps over b (pairs of accumulator tiles)
-  const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15;
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  constexpr int NSW = PAPER ? 0 : 1;
+  constexpr int FR = 2 * MTH * NKA + NSW;
+  extern __shared__ __attribute__((aligned(16))) u16x8_t ntn_lds[];
+  const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15, wave = threadIdx.x >> 6;
   const int NQ = N * Q;
-  for (int ep = gw; ep < E; ep += nw) {
-    const long rq0 = (long)ep * (N * K + NQ) + N * K;
+  const int npair = (h + 1) / 2;
+  for (int g = blockIdx.x; g * NTN_WAVES < E; g += gridDim.x) {
+    const int ep = g * NTN_WAVES + wave;
+    const bool act = ep < E;
+    const int epc = act ? ep : E - 1;
+    const long rq0 = (long)epc * (N * K + NQ) + N * K;
     u16x8_t Cf[NKA];
 #pragma unroll
     for (int ka = 0; ka < NKA; ++ka)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int a = 32 * ka + 8 * q + j;
-        Cf[ka][j] = (n < N && a < H) ? f2bf(cls[((long)ep * N + n) * H + a]) : (unsigned short)0;
+        Cf[ka][j] = (n < N && a < H) ? f2bf(cls[((long)epc * N + n) * H + a]) : (unsigned short)0;
       }
     u16x8_t Qf[QT][NKB];
 #pragma unroll
@@ -77,61 +118,69 @@ __global__ __launch_bounds__(256) void ntn_fwd_kernel(const float* __restrict__ 
     f32x4_t Lg[QT];
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) Lg[qt] = Z4;
-    const int npair = (h + 1) / 2;
+    __syncthreads();  // previous group's readers are done with buffer 0
+    ntn_stage<MTH, NSW, false>(ntn_lds, 0, mpack, nullptr, wpack, 1);
+    stage_wait();
+    __syncthreads();
     for (int p = 0; p < npair; ++p) {
-      f32x4_t V[2][QT];
+      const u16x8_t* buf = ntn_lds + (p & 1) * FR * 64;
+      if (p + 1 < npair) ntn_stage<MTH, NSW, false>(ntn_lds + ((p + 1) & 1) * FR * 64, p + 1, mpack, nullptr, wpack, 1);
+      if (act) {
+        f32x4_t V[2][QT];
 #pragma unroll
-      for (int sl = 0; sl < 2; ++sl) {
-        const int s = 2 * p + sl;
-        if (s >= h) {
+        for (int sl = 0; sl < 2; ++sl) {
+          const int s = 2 * p + sl;
+          f32x4_t PT[2 * NKB];
 #pragma unroll
-          for (int qt = 0; qt < QT; ++qt) V[sl][qt] = Z4;
-          continue;
-        }
-        f32x4_t PT[2 * NKB];
+          for (int mb = 0; mb < 2 * NKB; ++mb) {
+            PT[mb] = Z4;
+            if (mb < MTH) {
 #pragma unroll
-        for (int mb = 0; mb < 2 * NKB; ++mb) {
-          PT[mb] = Z4;
-          if (mb < MTH) {
+              for (int ka = 0; ka < NKA; ++ka)
+                PT[mb] = mfma_bf16(buf[((sl * MTH + mb) * NKA + ka) * 64 + lane], Cf[ka], PT[mb]);
+            }
+          }
+          u16x8_t PTf[NKB];
 #pragma unroll
-            for (int ka = 0; ka < NKA; ++ka) PT[mb] = mfma_bf16(mpack[((s * MTH + mb) * NKA + ka) * 64 + lane], Cf[ka], PT[mb]);
+          for (int kb = 0; kb < NKB; ++kb) PTf[kb] = pack2(PT[2 * kb], PT[2 * kb + 1]);
+#pragma unroll
+          for (int qt = 0; qt < QT; ++qt) {
+            f32x4_t T = Z4;
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) T = mfma_bf16(PTf[kb], Qf[qt][kb], T);
+            if (PAPER) {
+              const float ws = s < h ? wvec[s < h ? s : 0] : 0.f;
+              const f32x4_t Rl = relu4(T);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) Lg[qt][r] += ws * Rl[r];
+            } else {
+              V[sl][qt] = relu4(T);  // zero M for s >= h -> T = 0
+            }
           }
         }
-        u16x8_t PTf[NKB];
+        if (!PAPER) {
+          const u16x8_t wf = buf[(2 * MTH * NKA) * 64 + lane];
 #pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) PTf[kb] = pack2(PT[2 * kb], PT[2 * kb + 1]);
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-          f32x4_t T = Z4;
-#pragma unroll
-          for (int kb = 0; kb < NKB; ++kb) T = mfma_bf16(PTf[kb], Qf[qt][kb], T);
-          if (PAPER) {
-            const float ws = wvec[s];
-            const f32x4_t R = relu4(T);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) Lg[qt][r] += ws * R[r];
-          } else {
-            V[sl][qt] = relu4(T);
-          }
+          for (int qt = 0; qt < QT; ++qt) Lg[qt] = mfma_bf16(pack2(V[0][qt], V[1][qt]), wf, Lg[qt]);
         }
       }
-      if (!PAPER) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) Lg[qt] = mfma_bf16(pack2(V[0][qt], V[1][qt]), wpack[p * 64 + lane], Lg[qt]);
-      }
+      stage_wait();
+      __syncthreads();
     }
+    if (act) {
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt)
+      for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (PAPER) {  // rows c, cols query
-          const int c = 4 * q + r, qi = 16 * qt + n;
-          if (c < N && qi < NQ) probs[((long)ep * NQ + qi) * N + c] = sigmoidf_(Lg[qt][r] + bias[0]);
-        } else {      // rows query, cols c'
-          const int qi = 16 * qt + 4 * q + r, c = n;
-          if (c < N && qi < NQ) probs[((long)ep * NQ + qi) * N + c] = sigmoidf_(Lg[qt][r] + bias[c]);
+        for (int r = 0; r < 4; ++r) {
+          if (PAPER) {  // rows c, cols query
+            const int c = 4 * q + r, qi = 16 * qt + n;
+            if (c < N && qi < NQ) probs[((long)ep * NQ + qi) * N + c] = sigmoidf_(Lg[qt][r] + bias[0]);
+          } else {      // rows query, cols c'
+            const int qi = 16 * qt + 4 * q + r, c = n;
+            if (c < N && qi < NQ) probs[((long)ep * NQ + qi) * N + c] = sigmoidf_(Lg[qt][r] + bias[c]);
+          }
         }
-      }
+    }
   }
 }
 
@@ -139,26 +188,33 @@ __global__ __launch_bounds__(256) void ntn_fwd_kernel(const float* __restrict__ 
 // Outputs: dcls [E,N,H]; de query rows [S,H]; dp_out bf16 [E*N][h*H] (col s*H + b);
 //          dw_slab [E][h][N][N] (reference head) or [E][h] (paper head).
 template <int MTH, int QT, bool PAPER>
-__global__ __launch_bounds__(256) void ntn_bwd_kernel(
+__global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
     const float* __restrict__ cls, const float* __restrict__ e, int E, int N, int K, int Q, int H, int h,
     const u16x8_t* __restrict__ mpack, const u16x8_t* __restrict__ m2pack, const u16x8_t* __restrict__ wtpack,
     const float* __restrict__ wvec, const float* __restrict__ dz, float* __restrict__ dcls, float* __restrict__ de,
     unsigned short* __restrict__ dp_out, float* __restrict__ dw_slab) {
   constexpr int NKA = (MTH + 1) / 2, NKB = (MTH + 1) / 2, KQ = (QT + 1) / 2;
-  const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15;
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  constexpr int NSW = PAPER ? 0 : 2;
+  constexpr int F1 = 2 * MTH * NKA, F2 = 2 * MTH * NKB;
+  constexpr int FR = F1 + F2 + NSW;
+  extern __shared__ __attribute__((aligned(16))) u16x8_t ntn_lds[];
+  const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15, wave = threadIdx.x >> 6;
   const int NQ = N * Q;
   const long hH = (long)h * H;
-  for (int ep = gw; ep < E; ep += nw) {
-    const long rq0 = (long)ep * (N * K + NQ) + N * K;
-    const float* dze = dz + (long)ep * NQ * N;
+  const int npair = (h + 1) / 2;
+  for (int g = blockIdx.x; g * NTN_WAVES < E; g += gridDim.x) {
+    const int ep = g * NTN_WAVES + wave;
+    const bool act = ep < E;
+    const int epc = act ? ep : E - 1;
+    const long rq0 = (long)epc * (N * K + NQ) + N * K;
+    const float* dze = dz + (long)epc * NQ * N;
     u16x8_t Cf[NKA];
 #pragma unroll
     for (int ka = 0; ka < NKA; ++ka)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int a = 32 * ka + 8 * q + j;
-        Cf[ka][j] = (n < N && a < H) ? f2bf(cls[((long)ep * N + n) * H + a]) : (unsigned short)0;
+        Cf[ka][j] = (n < N && a < H) ? f2bf(cls[((long)epc * N + n) * H + a]) : (unsigned short)0;
       }
     u16x8_t Qf[QT][NKB];
 #pragma unroll
@@ -213,156 +269,177 @@ __global__ __launch_bounds__(256) void ntn_bwd_kernel(
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt) dQT[m][qt] = Z4;
     }
-    const int npair = (h + 1) / 2;
+    __syncthreads();
+    ntn_stage<MTH, NSW, true>(ntn_lds, 0, mpack, m2pack, wtpack, 2);
+    stage_wait();
+    __syncthreads();
     for (int p = 0; p < npair; ++p) {
-      f32x4_t Ps[2][MTH], dTs[2][QT];
+      const u16x8_t* buf = ntn_lds + (p & 1) * FR * 64;
+      if (p + 1 < npair) ntn_stage<MTH, NSW, true>(ntn_lds + ((p + 1) & 1) * FR * 64, p + 1, mpack, m2pack, wtpack, 2);
+      if (act) {
+        f32x4_t Ps[2][MTH], dTs[2][QT];
 #pragma unroll
-      for (int sl = 0; sl < 2; ++sl) {
-        const int s = 2 * p + sl;
+        for (int sl = 0; sl < 2; ++sl) {
+          const int s = 2 * p + sl;
 #pragma unroll
-        for (int m = 0; m < MTH; ++m) Ps[sl][m] = Z4;
+          for (int m = 0; m < MTH; ++m) Ps[sl][m] = Z4;
 #pragma unroll
-        for (int qt = 0; qt < QT; ++qt) dTs[sl][qt] = Z4;
-        if (s >= h) continue;
-        // P^T (rows b, cols c) and P (rows c, cols b) from the same fragments (operand swap)
-        f32x4_t PT[2 * NKB];
+          for (int qt = 0; qt < QT; ++qt) dTs[sl][qt] = Z4;
+          if (s >= h) continue;
+          // P^T (rows b, cols c) and P (rows c, cols b) from the same fragments (operand swap)
+          f32x4_t PT[2 * NKB];
 #pragma unroll
-        for (int mb = 0; mb < 2 * NKB; ++mb) {
-          PT[mb] = Z4;
-          if (mb < MTH) {
+          for (int mb = 0; mb < 2 * NKB; ++mb) {
+            PT[mb] = Z4;
+            if (mb < MTH) {
 #pragma unroll
-            for (int ka = 0; ka < NKA; ++ka) {
-              const u16x8_t mf = mpack[((s * MTH + mb) * NKA + ka) * 64 + lane];
-              PT[mb] = mfma_bf16(mf, Cf[ka], PT[mb]);
-              Ps[sl][mb] = mfma_bf16(Cf[ka], mf, Ps[sl][mb]);
+              for (int ka = 0; ka < NKA; ++ka) {
+                const u16x8_t mf = buf[((sl * MTH + mb) * NKA + ka) * 64 + lane];
+                PT[mb] = mfma_bf16(mf, Cf[ka], PT[mb]);
+                Ps[sl][mb] = mfma_bf16(Cf[ka], mf, Ps[sl][mb]);
+              }
             }
           }
-        }
-        u16x8_t PTf[NKB];
+          u16x8_t PTf[NKB];
 #pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) PTf[kb] = pack2(PT[2 * kb], PT[2 * kb + 1]);
-        u16x8_t wt;
-        float ws = 0.f;
-        if (PAPER) {
-          ws = wvec[s];
-        } else {
-          wt = wtpack[(long)s * 64 + lane];
-        }
-        f32x4_t VT[2 * KQ], dTT[2 * KQ];
-#pragma unroll
-        for (int i = 0; i < 2 * KQ; ++i) VT[i] = dTT[i] = Z4;
-        float dwp = 0.f;
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-          f32x4_t T = Z4, TT = Z4;
-#pragma unroll
-          for (int kb = 0; kb < NKB; ++kb) {
-            T = mfma_bf16(PTf[kb], Qf[qt][kb], T);    // rows c, cols query
-            TT = mfma_bf16(Qf[qt][kb], PTf[kb], TT);  // rows query, cols c
-          }
-          f32x4_t dV, dVT;
+          for (int kb = 0; kb < NKB; ++kb) PTf[kb] = pack2(PT[2 * kb], PT[2 * kb + 1]);
+          u16x8_t wt = {0, 0, 0, 0, 0, 0, 0, 0};
+          float ws = 0.f;
           if (PAPER) {
+            ws = wvec[s];
+          } else {
+            wt = buf[(F1 + F2 + sl) * 64 + lane];
+          }
+          f32x4_t VT[2 * KQ], dTT[2 * KQ];
+#pragma unroll
+          for (int i = 0; i < 2 * KQ; ++i) VT[i] = dTT[i] = Z4;
+          float dwp = 0.f;
+#pragma unroll
+          for (int qt = 0; qt < QT; ++qt) {
+            f32x4_t T = Z4, TT = Z4;
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) {
+              T = mfma_bf16(PTf[kb], Qf[qt][kb], T);    // rows c, cols query
+              TT = mfma_bf16(Qf[qt][kb], PTf[kb], TT);  // rows query, cols c
+            }
+            f32x4_t dV, dVT;
+            if (PAPER) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                dV[r] = ws * dzC[qt][r];
+                dVT[r] = ws * dzR[qt][r];
+                dwp += fmaxf(TT[r], 0.f) * dzR[qt][r];
+              }
+            } else {
+              dV = mfma_bf16(wt, dzA[qt], Z4);   // rows c, cols query
+              dVT = mfma_bf16(dzA[qt], wt, Z4);  // rows query, cols c
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              dV[r] = ws * dzC[qt][r];
-              dVT[r] = ws * dzR[qt][r];
-              dwp += fmaxf(TT[r], 0.f) * dzR[qt][r];
+              dTs[sl][qt][r] = T[r] > 0.f ? dV[r] : 0.f;
+              dTT[qt][r] = TT[r] > 0.f ? dVT[r] : 0.f;
             }
+            VT[qt] = relu4(TT);
+          }
+          // per-episode dw contribution
+          if (PAPER) {
+            dwp = wave_sum(dwp);
+            if (lane == 0) dw_slab[(long)ep * h + s] = dwp;
           } else {
-            dV = mfma_bf16(wt, dzA[qt], Z4);   // rows c, cols query
-            dVT = mfma_bf16(dzA[qt], wt, Z4);  // rows query, cols c
+            f32x4_t dw = Z4;
+#pragma unroll
+            for (int kq = 0; kq < KQ; ++kq) dw = mfma_bf16(pack2(VT[2 * kq], VT[2 * kq + 1]), dzB[kq], dw);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int c = 4 * q + r;
+              if (c < N && n < N) dw_slab[(((long)ep * h + s) * N + c) * N + n] = dw[r];
+            }
           }
+          // dP^T[b, c] = sum_q Q[q, b] dT[c, q]
+          f32x4_t dPT[2 * NKB];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            dTs[sl][qt][r] = T[r] > 0.f ? dV[r] : 0.f;
-            dTT[qt][r] = TT[r] > 0.f ? dVT[r] : 0.f;
+          for (int mb = 0; mb < 2 * NKB; ++mb) {
+            dPT[mb] = Z4;
+            if (mb < MTH) {
+#pragma unroll
+              for (int kq = 0; kq < KQ; ++kq)
+                dPT[mb] = mfma_bf16(QTf[mb][kq], pack2(dTT[2 * kq], dTT[2 * kq + 1]), dPT[mb]);
+            }
           }
-          VT[qt] = relu4(TT);
-        }
-        // per-episode dw contribution
-        if (PAPER) {
-          dwp = wave_sum(dwp);
-          if (lane == 0) dw_slab[(long)ep * h + s] = dwp;
-        } else {
-          f32x4_t dw = Z4;
+          // dC^T[a, c] += sum_b M[a, b, s] dP[c, b]
 #pragma unroll
-          for (int kq = 0; kq < KQ; ++kq) dw = mfma_bf16(pack2(VT[2 * kq], VT[2 * kq + 1]), dzB[kq], dw);
+          for (int kb = 0; kb < NKB; ++kb) {
+            const u16x8_t dPf = pack2(dPT[2 * kb], dPT[2 * kb + 1]);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int c = 4 * q + r;
-            if (c < N && n < N) dw_slab[(((long)ep * h + s) * N + c) * N + n] = dw[r];
+            for (int ma = 0; ma < MTH; ++ma)
+              dCT[ma] = mfma_bf16(buf[(F1 + (sl * MTH + ma) * NKB + kb) * 64 + lane], dPf, dCT[ma]);
           }
-        }
-        // dP^T[b, c] = sum_q Q[q, b] dT[c, q]
-        f32x4_t dPT[2 * NKB];
+          // dP -> bf16 [E*N][h*H] for the dM reduction GEMM
+          if (n < N) {
 #pragma unroll
-        for (int mb = 0; mb < 2 * NKB; ++mb) {
-          dPT[mb] = Z4;
-          if (mb < MTH) {
-#pragma unroll
-            for (int kq = 0; kq < KQ; ++kq) dPT[mb] = mfma_bf16(QTf[mb][kq], pack2(dTT[2 * kq], dTT[2 * kq + 1]), dPT[mb]);
-          }
-        }
-        // dC^T[a, c] += sum_b M[a, b, s] dP[c, b]
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) {
-          const u16x8_t dPf = pack2(dPT[2 * kb], dPT[2 * kb + 1]);
-#pragma unroll
-          for (int ma = 0; ma < MTH; ++ma) dCT[ma] = mfma_bf16(m2pack[((s * MTH + ma) * NKB + kb) * 64 + lane], dPf, dCT[ma]);
-        }
-        // dP -> bf16 [E*N][h*H] for the dM reduction GEMM
-        if (n < N) {
-#pragma unroll
-          for (int mb = 0; mb < MTH; ++mb) {
-            const int b0 = 16 * mb + 4 * q;
-            if (b0 < H) {
-              u16x4_t v = {f2bf(dPT[mb][0]), f2bf(dPT[mb][1]), f2bf(dPT[mb][2]), f2bf(dPT[mb][3])};
-              *reinterpret_cast<u16x4_t*>(dp_out + ((long)ep * N + n) * hH + (long)s * H + b0) = v;
+            for (int mb = 0; mb < MTH; ++mb) {
+              const int b0 = 16 * mb + 4 * q;
+              if (b0 < H) {
+                u16x4_t v = {f2bf(dPT[mb][0]), f2bf(dPT[mb][1]), f2bf(dPT[mb][2]), f2bf(dPT[mb][3])};
+                *reinterpret_cast<u16x4_t*>(dp_out + ((long)ep * N + n) * hH + (long)s * H + b0) = v;
+              }
             }
           }
         }
-      }
-      // dQ^T[b, q] += sum_{s in pair, c} P_s[c, b] dT_s[c, q]
+        // dQ^T[b, q] += sum_{s in pair, c} P_s[c, b] dT_s[c, q]
 #pragma unroll
-      for (int nb = 0; nb < MTH; ++nb) {
-        const u16x8_t Pf = pack2(Ps[0][nb], Ps[1][nb]);
+        for (int nb = 0; nb < MTH; ++nb) {
+          const u16x8_t Pf = pack2(Ps[0][nb], Ps[1][nb]);
 #pragma unroll
-        for (int qt = 0; qt < QT; ++qt) dQT[nb][qt] = mfma_bf16(Pf, pack2(dTs[0][qt], dTs[1][qt]), dQT[nb][qt]);
+          for (int qt = 0; qt < QT; ++qt) dQT[nb][qt] = mfma_bf16(Pf, pack2(dTs[0][qt], dTs[1][qt]), dQT[nb][qt]);
+        }
       }
+      stage_wait();
+      __syncthreads();
     }
-    // write dC (rows a, cols c) and dQ (rows b, cols query)
+    if (act) {
 #pragma unroll
-    for (int ma = 0; ma < MTH; ++ma) {
-      const int a0 = 16 * ma + 4 * q;
-      if (n < N && a0 < H) *reinterpret_cast<f32x4_t*>(dcls + ((long)ep * N + n) * H + a0) = dCT[ma];
-    }
-#pragma unroll
-    for (int nb = 0; nb < MTH; ++nb)
-#pragma unroll
-      for (int qt = 0; qt < QT; ++qt) {
-        const int b0 = 16 * nb + 4 * q, qi = 16 * qt + n;
-        if (qi < NQ && b0 < H) *reinterpret_cast<f32x4_t*>(de + (rq0 + qi) * H + b0) = dQT[nb][qt];
+      for (int ma = 0; ma < MTH; ++ma) {
+        const int a0 = 16 * ma + 4 * q;
+        if (n < N && a0 < H) *reinterpret_cast<f32x4_t*>(dcls + ((long)ep * N + n) * H + a0) = dCT[ma];
       }
+#pragma unroll
+      for (int nb = 0; nb < MTH; ++nb)
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+          const int b0 = 16 * nb + 4 * q, qi = 16 * qt + n;
+          if (qi < NQ && b0 < H) *reinterpret_cast<f32x4_t*>(de + (rq0 + qi) * H + b0) = dQT[nb][qt];
+        }
+    }
   }
 }
 
 // ------------------------------------------------------------------------------------------
 namespace ina {
 
-
+static size_t ntn_lds_bytes(int MTH, bool paper, bool bwd) {
+  const int NKA = (MTH + 1) / 2;
+  const int fr = bwd ? (4 * MTH * NKA + (paper ? 0 : 2)) : (2 * MTH * NKA + (paper ? 0 : 1));
+  return (size_t)2 * fr * 64 * 16;
+}
 
 template <int MTH, int QT, bool P>
 static int ntn_fwd_t(const NtnArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((ntn_fwd_kernel<MTH, QT, P>), dim3(a.blocks), dim3(256), 0, st, a.cls, a.e, a.E, a.N, a.K, a.Q, a.H,
-                     a.h, (const u16x8_t*)a.mpack, (const u16x8_t*)a.wpack, a.wvec, a.bias, a.probs);
+  const int groups = (a.E + NTN_WAVES - 1) / NTN_WAVES;
+  const int blocks = groups < a.blocks ? groups : a.blocks;
+  hipLaunchKernelGGL((ntn_fwd_kernel<MTH, QT, P>), dim3(blocks), dim3(NTN_THREADS), ntn_lds_bytes(MTH, P, false), st,
+                     a.cls, a.e, a.E, a.N, a.K, a.Q, a.H, a.h, (const u16x8_t*)a.mpack, (const u16x8_t*)a.wpack,
+                     a.wvec, a.bias, a.probs);
   INA_CHECK_LAUNCH();
   return 0;
 }
 template <int MTH, int QT, bool P>
 static int ntn_bwd_t(const NtnArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((ntn_bwd_kernel<MTH, QT, P>), dim3(a.blocks), dim3(256), 0, st, a.cls, a.e, a.E, a.N, a.K, a.Q, a.H,
-                     a.h, (const u16x8_t*)a.mpack, (const u16x8_t*)a.m2pack, (const u16x8_t*)a.wtpack, a.wvec, a.dz,
-                     a.dcls, a.de, (unsigned short*)a.dp_out, a.dw_slab);
+  const int groups = (a.E + NTN_WAVES - 1) / NTN_WAVES;
+  const int blocks = groups < a.blocks ? groups : a.blocks;
+  hipLaunchKernelGGL((ntn_bwd_kernel<MTH, QT, P>), dim3(blocks), dim3(NTN_THREADS), ntn_lds_bytes(MTH, P, true), st,
+                     a.cls, a.e, a.E, a.N, a.K, a.Q, a.H, a.h, (const u16x8_t*)a.mpack, (const u16x8_t*)a.m2pack,
+                     (const u16x8_t*)a.wtpack, a.wvec, a.dz, a.dcls, a.de, (unsigned short*)a.dp_out, a.dw_slab);
   INA_CHECK_LAUNCH();
   return 0;
 }

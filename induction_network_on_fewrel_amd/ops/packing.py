@@ -136,11 +136,14 @@ def _kmap32(q: int, j: int) -> int:
 
 @lru_cache(maxsize=None)
 def _ntn_m_idx(H: int, h: int):
+    """Packed M fragments for h_pad = 2*ceil(h/2) slices (the pad slice is zero): the NTN kernels
+    stage whole slice pairs with global_load_lds and need no per-lane bounds checks."""
     MTH = (H + 15) // 16
     NKA = (MTH + 1) // 2
     Z = H * H * h
-    mp = np.empty((h, MTH, NKA, 64, 8), dtype=np.int64)
-    m2 = np.empty((h, MTH, NKA, 64, 8), dtype=np.int64)
+    hp = 2 * ((h + 1) // 2)
+    mp = np.full((hp, MTH, NKA, 64, 8), Z, dtype=np.int64)
+    m2 = np.full((hp, MTH, NKA, 64, 8), Z, dtype=np.int64)
     ls = np.arange(64)
     js = np.arange(8)
     for s in range(h):
@@ -162,7 +165,7 @@ def _ntn_w_idx(h: int, N: int):
     Z = h * N * N
     npair = (h + 1) // 2
     wp = np.empty((npair, 64, 8), dtype=np.int64)
-    wt = np.empty((h, 64, 8), dtype=np.int64)
+    wt = np.full((2 * npair, 64, 8), Z, dtype=np.int64)
     for p in range(npair):
         for l in range(64):
             for j in range(8):
