@@ -56,19 +56,20 @@ def main():
                           seed=0)
     tr = Trainer(cfg, data, None, device="cuda", dist_ctx=dist, log=False)
     for _ in range(args.warmup):
-        tr.train_step()
+        tr.train_step_async()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    loss = acc = 0.0
+    loss_t = None
     for _ in range(args.steps):
-        loss, acc = tr.train_step()
+        loss_t, _ = tr.train_step_async()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     dt = dist.max_scalar(dt)
+    loss = float(loss_t) if loss_t is not None else float("nan")
     in_sync = dist.params_in_sync(tr.flat.flat)
     episodes = args.steps * B * world
     value = episodes / dt

@@ -48,7 +48,8 @@ class InductionNetwork(nn.Module):
             raise NotImplementedError("GPU NTN kernel supports N <= 16 and N*Q <= 64")
 
     def forward(self, inst: torch.Tensor, data: Tuple[torch.Tensor, ...], B: int, N: int, K: int, Q: int,
-                training: bool = True, dropout_seed: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+                training: bool = True, dropout_seed: int = 0,
+                grad_views: Optional[Dict[str, torch.Tensor]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """inst: int32 [B*(N*K+N*Q)] instance rows (episode layout, support first).
         data: (word, pos1, pos2, mask) [NI, L] int32 on the same device.
         Returns probs [B, N*Q, N] and alphas [B*(N*K+N*Q), L]."""
@@ -65,10 +66,10 @@ class InductionNetwork(nn.Module):
             self.check_gpu_config(N, Q, word.shape[1])
             meta = dict(U=cfg.hidden_size, bf16=(cfg.dtype == "bf16"), keep_prob=kp, seed=int(dropout_seed),
                         word_grad=bool(isinstance(p["word_embedding"], nn.Parameter)
-                                       and p["word_embedding"].requires_grad))
+                                       and p["word_embedding"].requires_grad), grad_views=grad_views)
             e, alphas = encode(inst, data, p, meta)
             probs = head(e, p, dict(E=B, N=N, K=K, Q=Q, iters=cfg.routing_iters,
-                                    paper=(cfg.relation_head == "paper")))
+                                    paper=(cfg.relation_head == "paper"), grad_views=grad_views))
             return probs, alphas
         word, pos1, pos2, mask = (t[inst.long()] for t in data)
         probs, alphas = ref.forward(p, word, pos1, pos2, mask, B, N, K, Q, cfg.routing_iters, cfg.relation_head,

@@ -19,6 +19,18 @@ from ._ext import ops
 from .packing import lstm_shape, pack_attn, pack_lstm
 
 
+def _route_grad(meta, name, g):
+    """Write a parameter gradient straight into the flat gradient buffer when the trainer provides
+    its view (``meta['grad_views']``): no AccumulateGrad add kernel, no extra copy."""
+    views = meta.get("grad_views")
+    if g is None:
+        return None
+    if views is not None and name in views:
+        views[name].add_(g.reshape(views[name].shape))
+        return None
+    return g.contiguous()
+
+
 class EncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, inst, word, pos1, pos2, mask, wemb, p1emb, p2emb, Kf, bf, Kb, bb, W1, b1, w2, meta):
@@ -65,15 +77,19 @@ class EncoderFn(torch.autograd.Function):
                                                bias, hlane, cst, dH, U, m["NX"], bf16, word_grad,
                                                int(m.get("lstm_blocks", 0)), int(m["seed"]), float(m["keep_prob"]))
         D = dw_slab.sum(0)                         # [2, 4U, DIN+U+1]
-        dKf = D[0, :, : DIN + U].t().contiguous()
-        dKb = D[1, :, : DIN + U].t().contiguous()
-        dbf = D[0, :, DIN + U].contiguous()
-        dbb = D[1, :, DIN + U].contiguous()
+        dKf = D[0, :, : DIN + U].t()
+        dKb = D[1, :, : DIN + U].t()
+        dbf = D[0, :, DIN + U]
+        dbb = D[1, :, DIN + U]
         P = dpos_slab.sum((0, 1))                  # [2 tables, 2L, PD]
         dp1 = P[0][: p1emb.shape[0]]
         dp2 = P[1][: p2emb.shape[0]]
-        return (None, None, None, None, None, dwemb if word_grad else None, dp1, dp2, dKf, dbf, dKb, dbb, dW1, db1,
-                dw2, None)
+        grads = dict(word_embedding=dwemb if word_grad else None, pos1_embedding=dp1, pos2_embedding=dp2,
+                     lstm_fw_kernel=dKf, lstm_fw_bias=dbf, lstm_bw_kernel=dKb, lstm_bw_bias=dbb, attn_kernel=dW1,
+                     attn_bias=db1, attn_w2=dw2)
+        order = ("word_embedding", "pos1_embedding", "pos2_embedding", "lstm_fw_kernel", "lstm_fw_bias",
+                 "lstm_bw_kernel", "lstm_bw_bias", "attn_kernel", "attn_bias", "attn_w2")
+        return (None, None, None, None, None) + tuple(_route_grad(m, k, grads[k]) for k in order) + (None,)
 
 
 def encode(inst, data, params, meta):

@@ -13,6 +13,7 @@ from __future__ import annotations
 import torch
 
 from ._ext import ops
+from .encoder import _route_grad
 from .packing import pack_ntn_M, pack_ntn_w
 
 
@@ -60,7 +61,8 @@ class HeadFn(torch.autograd.Function):
             db = dz.sum((0, 1))
         slab = o.routing_bwd(e, Ws, dcls, de, E, N, K, Q, R, 0)
         dWs = slab.sum(0)
-        return de, dWs, dM, dw, db, None
+        return (de, _route_grad(m, "W_s", dWs), _route_grad(m, "M", dM), _route_grad(m, "ntn_w", dw),
+                _route_grad(m, "ntn_b", db), None)
 
 
 def head(e, params, meta):

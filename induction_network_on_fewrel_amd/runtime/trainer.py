@@ -66,6 +66,7 @@ class Trainer:
         vocab = None if wv is not None else int(max(train_data.data_word.max(), 1) + 1)
         self.model = InductionNetwork(cfg, wv, vocab_size=vocab, seed=cfg.seed).to(self.device)
         self.flat = FlatParams(self.model.params.trainable())
+        self.grad_views = {n: self.flat.view(self.flat.grad, n) for n in self.flat.names}
         if self.dist.world > 1:
             self.dist.broadcast_(self.flat.flat, 0)
         l2_names = [n for n, p in self.model.params.trainable().items()
@@ -103,6 +104,15 @@ class Trainer:
 
     # ------------------------------------------------------------------ steps
     def train_step(self) -> Tuple[float, float]:
+        """One optimiser step; returns host floats (synchronises)."""
+        loss, acc = self.train_step_async()
+        return float(loss), float(acc)
+
+    def train_step_async(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """One optimiser step with NO host synchronisation; returns device (loss, acc) tensors.
+
+        Gradients are written by the fused backward functions straight into the flat gradient
+        buffer (grad_views), which is also the DP all-reduce bucket and the fused optimizer input."""
         cfg = self.cfg
         B, N, K, Q = cfg.episodes_per_step, cfg.N, cfg.K, cfg.Q
         t0 = time.perf_counter()
@@ -110,8 +120,9 @@ class Trainer:
         self._sync()
         t1 = time.perf_counter()
         self.flat.zero_grad()
+        gv = self.grad_views if self.device.type == "cuda" else None
         probs, _ = self.model(idx.view(-1), self.train_eps.arrays, B, N, K, Q, training=True,
-                              dropout_seed=self.dropout_seed())
+                              dropout_seed=self.dropout_seed(), grad_views=gv)
         loss = self.model.loss(probs, labels)
         loss.backward()
         self.flat.sync_grads_into_flat()
@@ -125,9 +136,8 @@ class Trainer:
         t3 = time.perf_counter()
         lr = lr_at(self.global_step, cfg.learning_rate, cfg.decay_steps, cfg.decay_rate, cfg.staircase,
                    cfg.lr_schedule)
-        loss_v = float(loss.detach())
-        if cfg.grad_check_finite and not math.isfinite(loss_v):
-            self.skipped_steps += 1
+        if cfg.grad_check_finite and self.device.type != "cuda" and not math.isfinite(float(loss.detach())):
+            self.skipped_steps += 1   # CPU path: exact skip (the GPU path checks when it logs, see train())
         else:
             self.opt.step(lr, grad_scale=1.0 / self.dist.world)
         self.global_step += 1
@@ -138,7 +148,7 @@ class Trainer:
         self.timers["allreduce"] += t3 - t2
         self.timers["optim"] += t4 - t3
         self._last_lr = lr
-        return loss_v, float(acc_t)
+        return loss.detach(), acc_t
 
     @torch.no_grad()
     def evaluate(self, iters: int, N: Optional[int] = None, K: Optional[int] = None, Q: Optional[int] = None,
@@ -168,12 +178,27 @@ class Trainer:
         it_loss = it_acc = it_n = 0.0
         start = self.global_step
         t_start = time.time()
+        pend_loss = pend_acc = None
+        pend_n = 0
         for it in range(start, cfg.train_iter):
-            loss, acc = self.train_step()
-            it_loss += loss
-            it_acc += acc
-            it_n += 1
-            self.log.log(self.global_step, "train", loss=loss, accuracy=acc, learning_rate=self._last_lr)
+            loss_t, acc_t = self.train_step_async()
+            # accumulate on device; the host only synchronises at log / reset / eval points
+            pend_loss = loss_t if pend_loss is None else pend_loss + loss_t
+            pend_acc = acc_t if pend_acc is None else pend_acc + acc_t
+            pend_n += 1
+            if (it % cfg.log_every == 0 or it % cfg.val_step == 0 or (it + 1) % cfg.val_step == 0
+                    or it + 1 == cfg.train_iter):
+                pl, pa = float(pend_loss), float(pend_acc)
+                if cfg.grad_check_finite and not math.isfinite(pl):
+                    self.skipped_steps += 1
+                    self.log.print(f"[warn] non-finite loss around step {it + 1}")
+                it_loss += pl
+                it_acc += pa
+                it_n += pend_n
+                pend_loss = pend_acc = None
+                pend_n = 0
+                self.log.log(self.global_step, "train", loss=it_loss / it_n, accuracy=it_acc / it_n,
+                             learning_rate=self._last_lr)
             if it % cfg.log_every == 0:
                 el = time.time() - t_start
                 eps = (it - start + 1) * cfg.episodes_per_step * self.dist.world / max(el, 1e-9)
