@@ -1,0 +1,114 @@
+"""Runtime: optimizer math, LR schedule, checkpoint layout + resume, metrics event files, trainer."""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from induction_network_on_fewrel_amd.config import Config
+from induction_network_on_fewrel_amd.data import make_synthetic
+from induction_network_on_fewrel_amd.ops.optim import FlatParams, FusedOptimizer, lr_at
+from induction_network_on_fewrel_amd.runtime import checkpoint as ckpt
+from induction_network_on_fewrel_amd.runtime.metrics import EventWriter, crc32c, read_events
+
+
+def test_lr_staircase_matches_tf_exponential_decay():
+    assert lr_at(0, 1e-3, 100, 0.9) == 1e-3
+    assert lr_at(99, 1e-3, 100, 0.9) == 1e-3
+    assert abs(lr_at(100, 1e-3, 100, 0.9) - 9e-4) < 1e-12
+    assert abs(lr_at(10000, 1e-3, 100, 0.9) - 1e-3 * 0.9 ** 100) < 1e-15   # the reference's LR collapse
+    assert abs(lr_at(150, 1e-3, 100, 0.9, staircase=False) - 1e-3 * 0.9 ** 1.5) < 1e-12
+
+
+def test_fused_adam_cpu_matches_tf1_adam():
+    p = torch.nn.Parameter(torch.randn(50))
+    flat = FlatParams({"x": p})
+    opt = FusedOptimizer(flat, "adam")
+    ref_p = p.detach().clone()
+    m = torch.zeros(50)
+    v = torch.zeros(50)
+    for t in range(1, 6):
+        g = torch.randn(50)
+        flat.grad.copy_(g)
+        opt.step(1e-2)
+        m = 0.9 * m + 0.1 * g
+        v = 0.999 * v + 0.001 * g * g
+        lr_t = 1e-2 * math.sqrt(1 - 0.999 ** t) / (1 - 0.9 ** t)
+        ref_p = ref_p - lr_t * m / (v.sqrt() + 1e-8)
+    assert torch.allclose(p.detach(), ref_p, atol=1e-6)
+
+
+def test_flat_params_are_views():
+    a = torch.nn.Parameter(torch.ones(3, 2))
+    b = torch.nn.Parameter(torch.zeros(4))
+    flat = FlatParams({"a": a, "b": b})
+    flat.flat.fill_(2.0)
+    assert float(a.sum()) == 12 and float(b.sum()) == 8
+    (a.sum() * 3 + b.sum()).backward()
+    flat.sync_grads_into_flat()
+    assert torch.allclose(flat.grad, torch.tensor([3.0] * 6 + [1.0] * 4))
+
+
+def test_checkpoint_layout_and_rotation(tmp_path):
+    md = str(tmp_path / "m")
+    for step in (10, 20, 30):
+        ckpt.save(md, "inductionNetwork", step, {"W_s": torch.ones(2, 2) * step, "global_step": torch.tensor(step)},
+                  {"best_acc": step / 100}, max_to_keep=2)
+    d = os.path.join(md, "checkpoint")
+    files = sorted(os.listdir(d))
+    assert files == ["checkpoint", "inductionNetwork-20.index.json", "inductionNetwork-20.safetensors",
+                     "inductionNetwork-30.index.json", "inductionNetwork-30.safetensors"]
+    with open(os.path.join(d, "checkpoint")) as fh:
+        txt = fh.read()
+    assert 'model_checkpoint_path: "inductionNetwork-30"' in txt
+    t, meta = ckpt.load(ckpt.latest(md))
+    assert float(t["W_s"][0, 0]) == 30 and meta["best_acc"] == 0.3 and meta["variables"]["W_s"]["shape"] == [2, 2]
+
+
+def test_event_file_roundtrip(tmp_path):
+    assert crc32c(b"123456789") == 0xE3069283   # CRC-32C check value
+    w = EventWriter(str(tmp_path))
+    w.scalars(1, {"loss": 0.5, "accuracy": 0.25})
+    w.scalars(2, {"loss": 0.25})
+    w.close()
+    ev = read_events(w.path)
+    assert ev[1][0] == 1 and abs(ev[1][1]["loss"] - 0.5) < 1e-7 and abs(ev[1][1]["accuracy"] - 0.25) < 1e-7
+    assert ev[2] == (2, {"loss": 0.25})
+
+
+def _trainer(tmp_path, B=4, **kw):
+    from induction_network_on_fewrel_amd.runtime.trainer import Trainer
+    data = make_synthetic(num_relations=10, instances_per_relation=40, vocab=500, seed=0)
+    cfg = Config(N=5, K=2, Q=3, episodes_per_step=B, model_dir=str(tmp_path / "run"), seed=3, **kw)
+    return Trainer(cfg, data, None, device="cpu", log=False)
+
+
+def test_checkpoint_resume_is_bitwise(tmp_path):
+    tr = _trainer(tmp_path, resume=False)
+    for _ in range(3):
+        tr.train_step()
+    tr.save()
+    ref_losses = [tr.train_step()[0] for _ in range(2)]
+    ref_params = tr.flat.flat.clone()
+    tr2 = _trainer(tmp_path, resume=True)
+    assert tr2.global_step == 3
+    losses = [tr2.train_step()[0] for _ in range(2)]
+    assert losses == ref_losses
+    assert torch.equal(tr2.flat.flat, ref_params)
+    names = set(ckpt.load(ckpt.latest(str(tmp_path / "run")))[0].keys())
+    assert {"M", "M/Adam", "M/Adam_1", "beta1_power", "beta2_power", "global_step", "embedding/Variable"} <= names
+
+
+@pytest.mark.slow
+def test_training_learns_on_synthetic(tmp_path):
+    """The model has a long MSE plateau (~0.16) before it separates classes; ~500 episodes-steps of
+    8 episodes at lr 1e-2 get it well above chance on the synthetic trigger-token task."""
+    tr = _trainer(tmp_path, B=8, resume=False, learning_rate=1e-2, lr_schedule="constant", keep_prob=1.0)
+    first = [tr.train_step()[0] for _ in range(5)]
+    for _ in range(560):
+        tr.train_step()
+    last = [tr.train_step()[0] for _ in range(5)]
+    acc = tr.evaluate(60)
+    assert np.mean(last) < np.mean(first)
+    assert acc > 0.3   # chance = 0.2

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Train / evaluate the Induction Network (CLI-compatible with the reference ``train.py``).
+
+Reference: ``python train.py [model_name=induction] [N=5] [K=2]`` with Q=5, max_length=37,
+hidden_size=20, ``./data/glove.6B.5d.json`` and ``checkpoints/inductionNetwork_test``
+(train.py:10-39). The same positional form works here; every Config field is also a ``--flag``.
+
+Examples
+  python train.py induction 5 2                          # reference defaults (needs data files)
+  python train.py induction 5 1 --synthetic true         # synthetic FewRel-shaped data
+  python train.py induction 5 5 --val_file data/val.json --split_val true   # relation-disjoint val split
+  torchrun --nproc-per-node 8 --master-addr 127.0.0.1 train.py induction 5 5 --episodes_per_step 64
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from induction_network_on_fewrel_amd.config import Config, add_cli_args, config_from_args  # noqa: E402
+
+
+def build_parser():
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("pos_model_name", nargs="?", default=None)
+    p.add_argument("pos_N", nargs="?", type=int, default=None)
+    p.add_argument("pos_K", nargs="?", type=int, default=None)
+    add_cli_args(p)
+    p.add_argument("--split_val", type=lambda s: s.lower() in ("1", "true", "yes"), default=False,
+                   help="train.json is absent: split val.json's relations into disjoint train/val halves")
+    p.add_argument("--eval_only", type=lambda s: s.lower() in ("1", "true", "yes"), default=False)
+    p.add_argument("--vocab_from_data", type=lambda s: s.lower() in ("1", "true", "yes"), default=False,
+                   help="no GloVe file: build a random word table from the data's tokens")
+    return p
+
+
+def load_data(cfg: Config, args):
+    from induction_network_on_fewrel_amd.data import FewRelDataset, make_synthetic, vocab_from_fewrel
+    if cfg.synthetic:
+        tr = make_synthetic(cfg.synthetic_relations, cfg.synthetic_instances, cfg.max_length, cfg.synthetic_vocab,
+                            cfg.synthetic_word_dim, seed=cfg.seed)
+        va = make_synthetic(max(cfg.N + 1, 16), cfg.synthetic_instances, cfg.max_length, cfg.synthetic_vocab,
+                            cfg.synthetic_word_dim, seed=cfg.seed + 1)
+        va.word_vec_mat = tr.word_vec_mat
+        return tr, va
+    wv = cfg.word_vec_file
+    if args.vocab_from_data or not os.path.exists(wv):
+        src = cfg.val_file if args.split_val or not os.path.exists(cfg.train_file) else cfg.train_file
+        wv = os.path.join(cfg.processed_dir, "vocab_from_data.json")
+        if not os.path.exists(wv):
+            os.makedirs(cfg.processed_dir, exist_ok=True)
+            with open(wv, "w") as fh:
+                json.dump(vocab_from_fewrel(src, dim=cfg.synthetic_word_dim, seed=cfg.seed), fh)
+    if args.split_val or not os.path.exists(cfg.train_file):
+        full = FewRelDataset.from_json(cfg.val_file, wv, cfg.max_length, cfg.case_sensitive,
+                                       processed_dir=cfg.processed_dir)
+        rels = full.relations()
+        half = len(rels) // 2
+        return full.subset_relations(rels[:half], "train_split"), full.subset_relations(rels[half:], "val_split")
+    tr = FewRelDataset.from_json(cfg.train_file, wv, cfg.max_length, cfg.case_sensitive, processed_dir=cfg.processed_dir)
+    va = FewRelDataset.from_json(cfg.val_file, wv, cfg.max_length, cfg.case_sensitive, processed_dir=cfg.processed_dir)
+    return tr, va
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    cfg = config_from_args(args, Config())
+    pos = {}
+    if args.pos_model_name is not None:
+        pos["model_name"] = args.pos_model_name
+    if args.pos_N is not None:
+        pos["N"] = args.pos_N
+    if args.pos_K is not None:
+        pos["K"] = args.pos_K
+    cfg = cfg.replace(**pos)
+    cfg.validate()
+    if cfg.model_name != "induction":
+        raise SystemExit(f"unknown model {cfg.model_name!r} (only 'induction')")
+    from induction_network_on_fewrel_amd.runtime.trainer import Trainer
+    tr_data, va_data = load_data(cfg, args)
+    trainer = Trainer(cfg, tr_data, va_data, device=cfg.device)
+    if args.eval_only:
+        acc = trainer.evaluate(cfg.test_iter)
+        if trainer.dist.is_main:
+            print(json.dumps({"eval_accuracy": acc, "episodes": cfg.test_iter, "N": cfg.eN, "K": cfg.eK}))
+    else:
+        trainer.train()
+    trainer.dist.destroy()
+
+
+if __name__ == "__main__":
+    main()
