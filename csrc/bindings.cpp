@@ -68,8 +68,15 @@ std::tuple<Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& wo
   auto hopt = word.options().dtype(bf16 ? at::kBFloat16 : at::kFloat);
   const int64_t ntiles = (S + 15) / 16;
   auto hlane = store_c ? at::empty({ntiles, 2, L, U4, 64}, hopt) : at::empty({0}, hopt);
-  auto hnat = at::empty({S, L, 2 * U}, hopt);
-  Tensor cst = store_c ? at::empty({ntiles, 2, L, U4, 64}, wemb.options()) : at::empty({0}, wemb.options());
+  // hnat is allocated with 16 * ntiles rows so the kernel stores padding rows unconditionally
+  // (no lane-divergent store branch); callers see the first S rows.
+  auto hnat_full = at::empty({ntiles * 16, L, 2 * U}, hopt);
+  auto hnat = hnat_full.narrow(0, 0, S);
+  auto copt = wemb.options().dtype(bf16 ? at::kHalf : at::kFloat);   // fp16 cell states in bf16 mode
+  Tensor cst = store_c ? at::empty({ntiles, 2, L, U4, 64}, copt) : at::empty({0}, copt);
+  TORCH_CHECK(ntiles * 16 * L * 2 * U < (1LL << 31) && ntiles * 2 * L * U4 * 64 < (1LL << 32),
+              "ina.lstm_fwd: batch too large for 32-bit offsets (split the episode batch)");
+  TORCH_CHECK(wemb.size(0) < (1 << 24) && 2 * L < (1 << 16), "ina.lstm_fwd: table rows exceed 24-bit indexing");
   if (S == 0) return {hlane, cst, hnat};
   ina::LstmArgs a{};
   a.inst = inst.data_ptr<int>();
@@ -86,7 +93,7 @@ std::tuple<Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& wo
   a.apack = apack.data_ptr();
   a.bias = bias.data_ptr<float>();
   a.hraw = store_c ? hlane.data_ptr() : nullptr;
-  a.cst = store_c ? cst.data_ptr<float>() : nullptr;
+  a.cst = store_c ? cst.data_ptr() : nullptr;
   a.hdrop = hnat.data_ptr();
   a.seed = (uint32_t)seed;
   a.thr = keep_threshold(keep_prob);
@@ -110,8 +117,8 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   check(p1emb, "p1emb", at::kFloat);
   check(p2emb, "p2emb", at::kFloat);
   check(bias, "bias", at::kFloat);
-  check(cst, "cst", at::kFloat);
-  check(dH, "dH", at::kFloat);
+  check(cst, "cst", bf16 ? at::kHalf : at::kFloat);
+  check(dH, "dH", bf16 ? at::kBFloat16 : at::kFloat);
   check(apack, "apack", bf16 ? at::kBFloat16 : at::kFloat);
   check(a2pack, "a2pack", bf16 ? at::kBFloat16 : at::kFloat);
   check(hraw, "hraw", bf16 ? at::kBFloat16 : at::kFloat);
@@ -153,8 +160,8 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   a.a2pack = a2pack.data_ptr();
   a.bias = bias.data_ptr<float>();
   a.hraw = hraw.data_ptr();
-  a.cst = cst.data_ptr<float>();
-  a.dH = dH.data_ptr<float>();
+  a.cst = cst.data_ptr();
+  a.dH = dH.data_ptr();
   a.dw_slab = dw_slab.data_ptr<float>();
   a.dpos_slab = dpos_slab.data_ptr<float>();
   a.dwemb = word_grad ? dwemb.data_ptr<float>() : nullptr;
@@ -221,7 +228,7 @@ std::tuple<Tensor, Tensor> attn_bwd(const Tensor& hraw, const Tensor& inst, cons
   TORCH_CHECK(NT >= 1 && NT <= 4, "ina.attn_bwd: L must be <= 64");
   if (blocks <= 0) blocks = 1024;
   blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, (S + 3) / 4));
-  auto dH = at::empty({S, L, H2}, de.options());
+  auto dH = at::empty({S, L, H2}, de.options().dtype(bf16 ? at::kBFloat16 : at::kFloat));
   auto slab = at::empty({blocks, H2 * H2 + 2 * H2}, de.options());
   if (S == 0) {
     slab.zero_();
@@ -238,7 +245,7 @@ std::tuple<Tensor, Tensor> attn_bwd(const Tensor& hraw, const Tensor& inst, cons
   a.w2 = w2.data_ptr<float>();
   a.de = de.data_ptr<float>();
   a.alphas = alphas.data_ptr<float>();
-  a.dHraw = dH.data_ptr<float>();
+  a.dHraw = dH.data_ptr();
   a.slab = slab.data_ptr<float>();
   a.blocks = (int)blocks;
   check_launch(ina::attn_bwd(a, (int)U, (int)NT, bf16, cur_stream()), "attn_bwd");

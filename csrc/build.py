@@ -19,8 +19,13 @@ import sysconfig
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "csrc")
-OUT_DIR = os.path.join(ROOT, "build", "obj")
-LIB = os.path.join(ROOT, "induction_network_on_fewrel_amd", "_ina_kernels.so")
+# Experiment variants: INA_BUILD_TAG=<tag> INA_VARIANT_FLAGS="-DX=1" builds variants/_ina_kernels_<tag>.so
+# (load it with INA_KERNEL_LIB=<path>); the default build is the in-tree package library.
+_TAG = os.environ.get("INA_BUILD_TAG", "")
+_VFLAGS = os.environ.get("INA_VARIANT_FLAGS", "").split()
+OUT_DIR = os.path.join(ROOT, "build", "obj" + (f"_{_TAG}" if _TAG else ""))
+LIB = (os.path.join(ROOT, "variants", f"_ina_kernels_{_TAG}.so") if _TAG
+       else os.path.join(ROOT, "induction_network_on_fewrel_amd", "_ina_kernels.so"))
 ARCH = os.environ.get("INA_OFFLOAD_ARCH", "gfx950")
 
 
@@ -49,6 +54,7 @@ def _run(cmd):
 def build(verbose: bool = False, jobs: int = 0) -> str:
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     os.makedirs(OUT_DIR, exist_ok=True)
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
     headers = glob.glob(os.path.join(CSRC, "include", "*.h"))
     kernels = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     inc, tlib = _torch_paths()
@@ -59,7 +65,7 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
         obj = os.path.join(OUT_DIR, os.path.basename(src) + ".o")
         objs.append(obj)
         if _newer(obj, [src, *headers, __file__]):
-            tasks.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
+            tasks.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", *_VFLAGS,
                           "-I" + os.path.join(CSRC, "include"), "-c", src, "-o", obj])
     bsrc = os.path.join(CSRC, "bindings.cpp")
     bobj = os.path.join(OUT_DIR, "bindings.o")

@@ -23,8 +23,8 @@ struct LstmArgs {
   const void* a2pack;
   const float* bias;
   void* hraw;
-  float* cst;
-  const float* dH;
+  void* cst;        // bf16 mode: fp16 cell states; fp32 mode: fp32
+  const void* dH;   // bf16 mode: bf16; fp32 mode: fp32
   float* dw_slab;
   float* dpos_slab;
   float* dwemb;
@@ -51,7 +51,7 @@ struct AttnArgs {
   float* e;
   float* alphas;
   const float* de;
-  float* dHraw;
+  void* dHraw;      // bf16 mode: bf16; fp32 mode: fp32
   float* slab;
   int blocks;
 };

@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
     const typename FT<BF16>::elem* hraw, const int* __restrict__ inst, int S, int L,
     const typename FT<BF16>::frag* __restrict__ w1pack, const typename FT<BF16>::frag* __restrict__ w1tpack,
     const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ de,
-    const float* __restrict__ alphas, float* __restrict__ dHraw,
+    const float* __restrict__ alphas, typename FT<BF16>::elem* __restrict__ dHraw,
     float* __restrict__ slab) {
   using Sh = AShape<U, NT, BF16>;
   using frag = typename FT<BF16>::frag;
@@ -346,7 +346,15 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
             (void)i;
             g[r] = acc[r] + alv * dei[m][r];
           }
-          *reinterpret_cast<f32x4_t*>(dHraw + ((long)s * L + tok) * H2 + 16 * m + 4 * q) = g;
+          elem* dst = dHraw + ((long)s * L + tok) * H2 + 16 * m + 4 * q;
+          if constexpr (BF16) {  // bf16 dH: halves the largest backward stream (read back by lstm_bwd)
+            uint2 pk;
+            pk.x = (uint32_t)f2bf(g[0]) | ((uint32_t)f2bf(g[1]) << 16);
+            pk.y = (uint32_t)f2bf(g[2]) | ((uint32_t)f2bf(g[3]) << 16);
+            *reinterpret_cast<uint2*>(dst) = pk;
+          } else {
+            *reinterpret_cast<f32x4_t*>(dst) = g;
+          }
         }
       }
       // stage H (MFMA operand values) and dP for the dW1 MFMA; tokens are the K dimension
@@ -447,7 +455,7 @@ static int attn_bwd_t(const AttnArgs& a, hipStream_t st) {
   const size_t lds = attn_bwd_lds_bytes(U, NT, BF16);
   hipLaunchKernelGGL((attn_bwd_kernel<U, NT, BF16>), dim3(a.blocks), dim3(256), lds, st,
                      (const typename F::elem*)a.hraw, a.inst, a.S, a.L, (const typename F::frag*)a.w1pack,
-                     (const typename F::frag*)a.w1tpack, a.b1, a.w2, a.de, a.alphas, a.dHraw, a.slab);
+                     (const typename F::frag*)a.w1tpack, a.b1, a.w2, a.de, a.alphas, (typename F::elem*)a.dHraw, a.slab);
   INA_CHECK_LAUNCH();
   return 0;
 }

@@ -18,6 +18,10 @@
 
 using namespace ina;
 
+#ifndef INA_FWD_PIPE
+#define INA_FWD_PIPE 1
+#endif
+
 namespace {
 
 template <int U, int NX, bool BF16>
@@ -71,31 +75,60 @@ INA_DEVICE float to_elem(float v, float*) { return v; }
 INA_DEVICE float from_elem(unsigned short v) { return bf2f(v); }
 INA_DEVICE float from_elem(float v) { return v; }
 
-// Per-lane source of x feature f (loop invariant): word / pos1 / pos2 table column, or none.
-// The per-step gather is then ONE unconditional load per feature (no lane-dependent branch
-// around a load: hipcc would wait vmcnt(0) per element and serialise the L2 round trips).
+// Cell-state stash element: fp16 in bf16 mode (|c| <= L since |c_t - f c_{t-1}| < 1, far inside
+// fp16 range; 11-bit mantissa), fp32 in the exact fp32 mode.
+template <bool BF16>
+struct CT {
+  using type = float;
+};
+template <>
+struct CT<true> {
+  using type = _Float16;
+};
+INA_DEVICE float from_c(_Float16 v) { return (float)v; }
+INA_DEVICE float from_c(float v) { return v; }
+
+// lanes whose bit is set in the wave-uniform mask m take b, the others a (one v_cndmask with an
+// SGPR-pair condition; the masks are ballots computed once per kernel).
+INA_DEVICE uint32_t lane_sel(uint64_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+  return r;
+}
+
+// Per-lane source of x feature f = 4 xi + q (loop invariant): word / pos1 / pos2 table column, or
+// none (f >= DIN).  The per-step gather is ONE unconditional load per feature: the row offset is
+// picked with SGPR-mask selects (no lane-dependent branch around a load: hipcc would wait vmcnt(0)
+// per element and serialise the L2 round trips).  "none" lanes load a finite word-table value that
+// meets only zero weight rows (the packs are zero-padded past DIN) and is never staged for dW.
 struct XSrc {
   const float* base;
-  int stride, col, sel;  // sel: 0 word, 1 pos1, 2 pos2, 3 none
+  int col;
+  int sel;               // 0 word, 1 pos1, 2 pos2, 3 none
+  uint64_t mp1, mp2;     // wave-uniform lane masks
 };
 INA_DEVICE XSrc make_xsrc(int f, const float* __restrict__ wemb, int E, const float* __restrict__ p1emb,
                           const float* __restrict__ p2emb, int PD) {
   XSrc s;
-  if (f < E) {
-    s.base = wemb; s.stride = E; s.col = f; s.sel = 0;
-  } else if (f < E + PD) {
-    s.base = p1emb; s.stride = PD; s.col = f - E; s.sel = 1;
-  } else if (f < E + 2 * PD) {
-    s.base = p2emb; s.stride = PD; s.col = f - E - PD; s.sel = 2;
-  } else {
-    s.base = wemb; s.stride = 0; s.col = 0; s.sel = 3;
-  }
+  s.sel = f < E ? 0 : (f < E + PD ? 1 : (f < E + 2 * PD ? 2 : 3));
+  s.base = s.sel == 1 ? p1emb : (s.sel == 2 ? p2emb : wemb);
+  s.col = s.sel == 0 ? f : (s.sel == 1 ? f - E : (s.sel == 2 ? f - E - PD : 0));
+  s.mp1 = __ballot(s.sel == 1);
+  s.mp2 = __ballot(s.sel == 2);
   return s;
 }
-INA_DEVICE float gather_x(const XSrc& s, int wid, int p1, int p2) {
-  const int row = s.sel == 0 ? wid : (s.sel == 1 ? p1 : (s.sel == 2 ? p2 : 0));
-  const float v = s.base[(long)row * s.stride + s.col];
-  return s.sel == 3 ? 0.f : v;
+// element offsets of the step's token row in each table (24-bit multiplies: rows < 2^24 checked
+// on the host)
+struct XRow {
+  uint32_t w, p1, p2;
+};
+INA_DEVICE XRow xrow(int wid, int p1, int p2, int E, int PD) {
+  return XRow{(uint32_t)__umul24(wid, E), (uint32_t)__umul24(p1, PD), (uint32_t)__umul24(p2, PD)};
+}
+INA_DEVICE float gather_x(const XSrc& s, const XRow& r) {
+  uint32_t off = lane_sel(s.mp1, r.w, r.p1);
+  off = lane_sel(s.mp2, off, r.p2) + s.col;
+  return s.base[off];
 }
 
 INA_DEVICE void wave_lds_sync() {
@@ -108,16 +141,19 @@ INA_DEVICE void wave_lds_sync() {
 // ------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------
-template <int U, int NX, bool BF16>
+// DROP / STORE are compile-time so the step loop has no branches: the waitcnt pass can then count
+// the stores issued after each prefetch and wait only for the prefetched loads.
+template <int U, int NX, bool BF16, bool DROP, bool STORE>
 __global__ __launch_bounds__(256) void lstm_fwd_kernel(
     const int* __restrict__ inst, int S, const int* __restrict__ word, const int* __restrict__ pos1,
     const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
     const float* __restrict__ p1emb, const float* __restrict__ p2emb, int PD,
     const typename FragT<BF16>::type* __restrict__ apack, const float* __restrict__ bias,
-    typename FragT<BF16>::elem* __restrict__ hlane, float* __restrict__ cst, typename FragT<BF16>::elem* __restrict__ hnat,
-    uint32_t seed, uint32_t thr, float inv_kp, int drop) {
+    typename FragT<BF16>::elem* __restrict__ hlane, typename CT<BF16>::type* __restrict__ cst,
+    typename FragT<BF16>::elem* __restrict__ hnat, uint32_t seed, uint32_t thr, float inv_kp, int drop) {
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
+  using celem = typename CT<BF16>::type;
   constexpr int U4 = Sh::U4, KPL = Sh::KPL, NKS = Sh::NKS, NMT = Sh::NMT;
   extern __shared__ __attribute__((aligned(16))) int2 ids_all[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -140,8 +176,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(
   }
   wave_lds_sync();
   if (tile >= ntiles) return;
-  const int seq = tile * 16 + n;
-  const bool valid = seq < S;
+  const int seq = tile * 16 + n;  // rows >= S are padding rows of hnat (allocated to 16 * ntiles)
   const uint32_t salt = dropout_salt(seed, (uint32_t)dir);
 
   frag A[NMT][NKS];
@@ -164,15 +199,14 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(
 #pragma unroll
   for (int xi = 0; xi < NX; ++xi) xs[xi] = make_xsrc(4 * xi + q, wemb, E, p1emb, p2emb, PD);
   auto load_x = [&](int t, float* xv) {
-    int2 id = ids[n * L + t];
+    const int2 id = ids[n * L + t];
+    const XRow r = xrow(id.x, id.y & 0xffff, id.y >> 16, E, PD);
 #pragma unroll
-    for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(xs[xi], id.x, id.y & 0xffff, id.y >> 16);
+    for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(xs[xi], r);
   };
-  float xv[NX], xn[NX];
-  load_x(dir ? L - 1 : 0, xv);
-  for (int tau = 0; tau < L; ++tau) {
+  // one recurrence step at processing index tau with input features xv
+  auto step = [&](const int tau, const float* xv) __attribute__((always_inline)) {
     const int t = dir ? (L - 1 - tau) : tau;
-    if (tau + 1 < L) load_x(dir ? (L - 2 - tau) : (tau + 1), xn);
     frag B[NKS];
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
@@ -198,34 +232,72 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(
       if (BF16) hv = round_bf(hv);  // the stored / recurrent operand value
       h[m] = hv;
     }
-    if (valid) {
-      // natural-layout copy for the attention layer; dropout (DropoutWrapper output) applied here
-      const long o = ((long)seq * L + t) * (2 * U) + dir * U + q;
-      if (drop) {
-        const uint32_t base = (uint32_t)(((long)seq * L + t) * U + q);
+    {
+      // natural-layout copy for the attention layer; dropout (DropoutWrapper output) applied here.
+      // 32-bit offsets (S * L * 2U < 2^31 checked on the host); padding rows are stored too.
+      typename FragT<BF16>::elem* hn = hnat + (((uint32_t)seq * L + t) * (2 * U) + dir * U + q);
+      if constexpr (DROP) {
+        const uint32_t base = ((uint32_t)seq * L + t) * U + q;
 #pragma unroll
         for (int m = 0; m < U4; ++m) {
           const bool keep = dropout_keep_salted(salt, base + 4 * m, thr);
-          hnat[o + 4 * m] = to_elem(keep ? h[m] * inv_kp : 0.f, (typename FragT<BF16>::elem*)nullptr);
+          hn[4 * m] = to_elem(keep ? h[m] * inv_kp : 0.f, (typename FragT<BF16>::elem*)nullptr);
         }
       } else {
 #pragma unroll
-        for (int m = 0; m < U4; ++m) hnat[o + 4 * m] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
+        for (int m = 0; m < U4; ++m) hn[4 * m] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
       }
     }
-    if (hlane) {  // raw recurrent h for the backward, lane-native (coalesced 128-B rows)
-      typename FragT<BF16>::elem* hp = hlane + (((size_t)tile * 2 + dir) * L + t) * U4 * 64 + lane;
+    if constexpr (STORE) {  // raw recurrent h for the backward, lane-native (coalesced 128-B rows)
+      typename FragT<BF16>::elem* hp = hlane + ((uint32_t)((tile * 2 + dir) * L + t) * U4) * 64 + lane;
 #pragma unroll
       for (int m = 0; m < U4; ++m) hp[m * 64] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
     }
-    if (cst) {
-      float* cp = cst + (((size_t)tile * 2 + dir) * L + t) * U4 * 64 + lane;
+    if constexpr (STORE) {
+      celem* cp = cst + ((uint32_t)((tile * 2 + dir) * L + t) * U4) * 64 + lane;
 #pragma unroll
-      for (int m = 0; m < U4; ++m) cp[m * 64] = c[m];
+      for (int m = 0; m < U4; ++m) cp[m * 64] = (celem)c[m];
     }
+  };
+  // two-step unrolled loop with ping-pong x buffers: the gather for step tau+1 is issued before
+  // step tau's math and consumed one step later (no register copies).  The loop body is ONE basic
+  // block (odd-L tail peeled, prefetch index clamped) so LLVM cannot sink the prefetch loads down
+  // to their uses.
+  auto tof = [&](int tau) { return dir ? (L - 1 - tau) : tau; };
+  float xa[NX], xb[NX];
+#if INA_FWD_PIPE == 0
+  // simple loop: prefetch x_{tau+1}, copy at the end of the step
+  load_x(tof(0), xa);
+  for (int tau = 0; tau < L; ++tau) {
+    load_x(tof(min(tau + 1, L - 1)), xb);
+    step(tau, xa);
 #pragma unroll
-    for (int xi = 0; xi < NX; ++xi) xv[xi] = xn[xi];
+    for (int xi = 0; xi < NX; ++xi) xa[xi] = xb[xi];
   }
+#else
+  // sched_barrier pins each prefetch ahead of the step it overlaps (the machine scheduler would
+  // otherwise sink the loads next to their uses to save registers)
+  auto pair = [&](int tau) __attribute__((always_inline)) {
+    load_x(tof(tau + 1), xb);
+    __builtin_amdgcn_sched_barrier(0);
+    step(tau, xa);
+    __builtin_amdgcn_sched_barrier(0);
+    load_x(tof(min(tau + 2, L - 1)), xa);
+    __builtin_amdgcn_sched_barrier(0);
+    step(tau + 1, xb);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  load_x(tof(0), xa);
+  int tau = 0;
+  // first pair peeled: the loop header is then entered with the same outstanding-VMEM state from
+  // the preheader and the latch, so the waitcnt pass can count precisely.
+  if (L >= 2) {
+    pair(0);
+    tau = 2;
+  }
+  for (; tau + 1 < L; tau += 2) pair(tau);
+  if (tau < L) step(tau, xa);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -240,7 +312,8 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
     const float* __restrict__ p1emb, const float* __restrict__ p2emb, int PD,
     const typename FragT<BF16>::type* __restrict__ apack, const typename FragT<BF16>::type* __restrict__ a2pack,
     const float* __restrict__ bias, const typename FragT<BF16>::elem* __restrict__ hraw,
-    const float* __restrict__ cst, const float* __restrict__ dH, float* __restrict__ dw_slab,
+    const typename CT<BF16>::type* __restrict__ cst, const typename FragT<BF16>::elem* __restrict__ dH,
+    float* __restrict__ dw_slab,
     float* __restrict__ dpos_slab, float* __restrict__ dwemb, uint32_t seed, uint32_t thr, float inv_kp, int drop) {
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
@@ -304,7 +377,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
     const bool valid = seq < S;
     const long seqc = valid ? seq : S - 1;  // clamped row for unconditional loads
     const long rowbase = (long)inst[seqc] * L;
-    const float* cbase = cst + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
+    const typename CT<BF16>::type* cbase = cst + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
     const elem* hbase = hraw + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
     const uint32_t dsalt = dropout_salt(seed, (uint32_t)dir);
     auto tof = [&](int tau) { return dir ? (L - 1 - tau) : tau; };  // processing step -> time
@@ -319,15 +392,15 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
     {
       const int t = tof(L - 1), tp = tof(L >= 2 ? L - 2 : 0);
 #pragma unroll
-      for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(xs[xi], wid_c, p1_c, p2_c);
+      for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(xs[xi], xrow(wid_c, p1_c, p2_c, E, PD));
 #pragma unroll
       for (int m = 0; m < U4; ++m) {
-        ccur[m] = cbase[((size_t)t * U4 + m) * 64];
-        const float cp = cbase[((size_t)tp * U4 + m) * 64];
+        ccur[m] = from_c(cbase[((size_t)t * U4 + m) * 64]);
+        const float cp = from_c(cbase[((size_t)tp * U4 + m) * 64]);
         cprev[m] = L >= 2 ? cp : 0.f;
         const float hv = from_elem(hbase[((size_t)tp * U4 + m) * 64]);
         hp[m] = (L >= 2 && valid) ? hv : 0.f;
-        const float dv = dH[(seqc * L + t) * (2 * U) + dir * U + 4 * m + q];
+        const float dv = from_elem(dH[(seqc * L + t) * (2 * U) + dir * U + 4 * m + q]);
         const bool keep = !drop || dropout_keep_salted(dsalt, (uint32_t)((seqc * L + t) * U + 4 * m + q), thr);
         dhin[m] = (valid && keep) ? dv * inv_kp : 0.f;
       }
@@ -345,14 +418,14 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
       const int wid_nn = word[rowbase + tnn], p1_nn = pos1[rowbase + tnn], p2_nn = pos2[rowbase + tnn];
       float xv_n[NX], hp_n[U4], cprev_n[U4], dhin_n[U4];
 #pragma unroll
-      for (int xi = 0; xi < NX; ++xi) xv_n[xi] = gather_x(xs[xi], wid_n, p1_n, p2_n);
+      for (int xi = 0; xi < NX; ++xi) xv_n[xi] = gather_x(xs[xi], xrow(wid_n, p1_n, p2_n, E, PD));
 #pragma unroll
       for (int m = 0; m < U4; ++m) {
-        const float cp = cbase[((size_t)tnp * U4 + m) * 64];
+        const float cp = from_c(cbase[((size_t)tnp * U4 + m) * 64]);
         cprev_n[m] = n_has_prev ? cp : 0.f;
         const float hv = from_elem(hbase[((size_t)tnp * U4 + m) * 64]);
         hp_n[m] = (n_has_prev && valid) ? hv : 0.f;
-        const float dv = dH[(seqc * L + tn) * (2 * U) + dir * U + 4 * m + q];
+        const float dv = from_elem(dH[(seqc * L + tn) * (2 * U) + dir * U + 4 * m + q]);
         const bool keep = !drop || dropout_keep_salted(dsalt, (uint32_t)((seqc * L + tn) * U + 4 * m + q), thr);
         dhin_n[m] = (valid && keep) ? dv * inv_kp : 0.f;
       }
@@ -548,9 +621,12 @@ static int launch_fwd_t(const LstmArgs& a, hipStream_t st) {
   const int ntiles = (a.S + 15) / 16;
   dim3 grid((ntiles + 3) / 4, 2);
   size_t lds = (size_t)4 * 16 * a.L * sizeof(int2);
-  hipLaunchKernelGGL((lstm_fwd_kernel<U, NX, BF16>), grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1,
-                     a.pos2, a.L, a.wemb, a.E, a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, a.bias,
-                     (elem*)a.hraw, a.cst, (elem*)a.hdrop, a.seed, a.thr, a.inv_kp, a.drop);
+  const bool store = a.hraw != nullptr && a.cst != nullptr;
+  auto kern = a.drop ? (store ? lstm_fwd_kernel<U, NX, BF16, true, true> : lstm_fwd_kernel<U, NX, BF16, true, false>)
+                     : (store ? lstm_fwd_kernel<U, NX, BF16, false, true> : lstm_fwd_kernel<U, NX, BF16, false, false>);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
+                     a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, a.bias, (elem*)a.hraw,
+                     (typename CT<BF16>::type*)a.cst, (elem*)a.hdrop, a.seed, a.thr, a.inv_kp, a.drop);
   INA_CHECK_LAUNCH();
   return 0;
 }
@@ -569,7 +645,7 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   }
   hipLaunchKernelGGL(kfn, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, (const frag*)a.a2pack, a.bias,
-                     (const elem*)a.hraw, a.cst, a.dH, a.dw_slab, a.dpos_slab, a.dwemb, a.seed, a.thr, a.inv_kp,
+                     (const elem*)a.hraw, (const typename CT<BF16>::type*)a.cst, (const elem*)a.dH, a.dw_slab, a.dpos_slab, a.dwemb, a.seed, a.thr, a.inv_kp,
                      a.drop);
   INA_CHECK_LAUNCH();
   return 0;

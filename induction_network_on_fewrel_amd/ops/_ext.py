@@ -11,7 +11,9 @@ import threading
 
 import torch
 
-_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_ina_kernels.so")
+# INA_KERNEL_LIB selects an experiment build (csrc/build.py with INA_BUILD_TAG); default: in-tree.
+_LIB = os.environ.get("INA_KERNEL_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                        "_ina_kernels.so")
 _lock = threading.Lock()
 _loaded = False
 _error = None
