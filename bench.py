@@ -11,6 +11,9 @@ weights -- no dataset or checkpoint downloads are possible here.
 A timed step is the FULL training step: device episode sampling, forward, backward, RCCL
 all-reduce of the flat gradient (N > 1), fused Adam update. Weak scaling: episodes per GPU fixed.
 
+BERT configuration (BASELINE.json "FewRel 10-way 5-shot with BERT-base encoder"):
+  python bench.py --encoder bert   (10-way 5-shot Q=5, BERT-base 12x768, L=128, 8 episodes/GPU)
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--episodes-per-gpu B] [--shot K]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
@@ -29,10 +32,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--episodes-per-gpu", type=int, default=2048)
-    ap.add_argument("--way", type=int, default=5)
+    ap.add_argument("--encoder", default="bilstm", choices=["bilstm", "bert"])
+    ap.add_argument("--episodes-per-gpu", type=int, default=0, help="default 2048 (bilstm) / 8 (bert)")
+    ap.add_argument("--way", type=int, default=0, help="default 5 (bilstm) / 10 (bert)")
     ap.add_argument("--shot", type=int, default=5)
     ap.add_argument("--query", type=int, default=5)
+    ap.add_argument("--bert-layers", type=int, default=12)
+    ap.add_argument("--bert-len", type=int, default=128)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--hidden", type=int, default=20)
     ap.add_argument("--profile-json", default="")
@@ -48,12 +54,28 @@ def main():
     world = dist.world
     if world != args.gpus and dist.is_main:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    B = args.episodes_per_gpu
+    bert = args.encoder == "bert"
+    B = args.episodes_per_gpu or (8 if bert else 2048)
+    args.way = args.way or (10 if bert else 5)
     cfg = Config(N=args.way, K=args.shot, Q=args.query, max_length=37, hidden_size=args.hidden, dtype=args.dtype,
                  episodes_per_step=B, seed=1234, resume=False, model_dir="/tmp/ina_bench",
                  train_iter=args.steps + args.warmup)
+    if bert:
+        cfg = cfg.replace(encoder="bert", bert_layers=args.bert_layers, bert_max_length=args.bert_len,
+                          relation_head="reference")
     data = make_synthetic(num_relations=64, instances_per_relation=700, max_length=37, vocab=400000, word_dim=5,
                           seed=0)
+    if bert:   # random token ids over the BERT vocabulary, full-length sequences (worst case for L)
+        import numpy as np
+        from induction_network_on_fewrel_amd.data.bert_tokenize import synthetic_features
+        f = synthetic_features(data, cfg.bert_vocab, cfg.bert_max_length)
+        rng = np.random.default_rng(0)
+        n = f["ids"].shape[0]
+        f["ids"][:, 1:-1] = rng.integers(9, cfg.bert_vocab, (n, cfg.bert_max_length - 2), dtype=np.int32)
+        f["mask"][:] = 1
+        f["ids"][:, -1] = 3
+        f["length"][:] = cfg.bert_max_length
+        data.bert = f
     tr = Trainer(cfg, data, None, device="cuda", dist_ctx=dist, log=False)
     for _ in range(args.warmup):
         tr.train_step_async()
@@ -86,13 +108,17 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
-            "data": "synthetic (64 relations x 700 instances, L=37, 400k vocab, 5-d word table); random-init weights",
+            "data": ("synthetic (64 relations x 700 instances, " +
+                     (f"L={cfg.bert_max_length} full-length token ids over a {cfg.bert_vocab} vocab"
+                      if bert else "L=37, 400k vocab, 5-d word table") + "); random-init weights"),
             "config": {
-                "model": f"induction-network bilstm(u={args.hidden})+self-attn, routing x3, ntn h=100",
+                "model": (f"induction-network bert-base({cfg.bert_layers}x{cfg.bert_hidden}, {cfg.bert_heads} heads)"
+                          f"+entity-pool->{cfg.bert_out_dim}, routing x3, ntn h=100" if bert else
+                          f"induction-network bilstm(u={args.hidden})+self-attn, routing x3, ntn h=100"),
                 "episode": f"{args.way}-way {args.shot}-shot Q={args.query}",
                 "global_batch": B * world,
                 "episodes_per_gpu": B,
-                "seq_len": 37,
+                "seq_len": cfg.bert_max_length if bert else 37,
                 "sentences_per_step_per_gpu": B * args.way * (args.shot + args.query),
                 "parallelism": f"dp{world}",
             },

@@ -1,0 +1,287 @@
+// Torch op registrations of the BERT encoder kernels (csrc/kernels/bert.hip), namespace torch.ops.ina.
+// Host-side validation of every shape / dtype the kernel grids assume happens here, before launch.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+#include <torch/library.h>
+
+#include <tuple>
+
+#include "ina_launch.h"
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void chk(const Tensor& t, const char* name, at::ScalarType dt) {
+  TORCH_CHECK(t.is_cuda(), "ina.bert: ", name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), "ina.bert: ", name, " must be contiguous");
+  TORCH_CHECK(t.scalar_type() == dt, "ina.bert: ", name, " has dtype ", t.scalar_type(), ", expected ", dt);
+}
+void launched(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, "ina.bert: ", what, " launch failed / unsupported configuration (rc=", rc, ")");
+}
+uint32_t thr_of(double kp) {
+  const double t = kp * 4294967296.0;
+  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
+// same recipe as dropout_salt() in ina_common.h / models/bert.py::keep_mask
+uint32_t salt_of(int64_t seed, int64_t stream_id) {
+  return (uint32_t)((uint32_t)(seed & 0x7FFFFFFF) * 0x2545F491u + (uint32_t)stream_id * 0x3C6EF372u + 0x1234567u);
+}
+void check_hd(int64_t HD) {
+  TORCH_CHECK(HD % 256 == 0 && HD >= 256 && HD <= 1024, "ina.bert: hidden width must be 256/512/768/1024, got ",
+              HD);
+}
+
+// ------------------------------------------------------------------ embeddings + LN
+std::tuple<Tensor, Tensor> bert_embed_ln_fwd(const Tensor& inst, const Tensor& ids, const Tensor& wemb,
+                                             const Tensor& pemb, const Tensor& temb, const Tensor& gamma,
+                                             const Tensor& beta, int64_t seed, double p) {
+  chk(inst, "inst", at::kInt);
+  chk(ids, "ids", at::kInt);
+  for (auto* t : {&wemb, &pemb, &temb, &gamma, &beta}) chk(*t, "table", at::kFloat);
+  const int64_t S = inst.size(0), L = ids.size(1), HD = wemb.size(1);
+  check_hd(HD);
+  TORCH_CHECK(pemb.size(0) >= L && pemb.size(1) == HD && temb.size(1) == HD, "ina.bert_embed_ln_fwd: tables");
+  TORCH_CHECK(gamma.numel() == HD && beta.numel() == HD, "ina.bert_embed_ln_fwd: LN params");
+  TORCH_CHECK(S * L * HD < (1LL << 32), "ina.bert_embed_ln_fwd: batch too large");
+  auto y = at::empty({S * L, HD}, wemb.options().dtype(at::kBFloat16));
+  auto stats = at::empty({S * L, 2}, wemb.options());
+  if (S == 0) return {y, stats};
+  ina::BertEmbArgs a{};
+  a.inst = inst.data_ptr<int>();
+  a.ids = ids.data_ptr<int>();
+  a.S = (int)S;
+  a.L = (int)L;
+  a.HD = (int)HD;
+  a.wemb = wemb.data_ptr<float>();
+  a.pemb = pemb.data_ptr<float>();
+  a.temb = temb.data_ptr<float>();
+  a.gamma = gamma.data_ptr<float>();
+  a.beta = beta.data_ptr<float>();
+  a.y = y.data_ptr();
+  a.stats = stats.data_ptr<float>();
+  a.salt = salt_of(seed, 16);
+  a.thr = thr_of(1.0 - p);
+  a.inv_kp = (float)(1.0 / (1.0 - p));
+  a.drop = p > 0.0 ? 1 : 0;
+  launched(ina::embed_ln_fwd(a, stream()), "embed_ln_fwd");
+  return {y, stats};
+}
+
+std::tuple<Tensor, Tensor> bert_embed_ln_bwd(const Tensor& dy, const Tensor& inst, const Tensor& ids,
+                                             const Tensor& wemb, const Tensor& pemb, const Tensor& temb,
+                                             const Tensor& gamma, const Tensor& stats, int64_t seed, double p,
+                                             int64_t blocks) {
+  chk(dy, "dy", at::kBFloat16);
+  chk(inst, "inst", at::kInt);
+  chk(ids, "ids", at::kInt);
+  for (auto* t : {&wemb, &pemb, &temb, &gamma, &stats}) chk(*t, "table", at::kFloat);
+  const int64_t S = inst.size(0), L = ids.size(1), HD = wemb.size(1);
+  check_hd(HD);
+  TORCH_CHECK(dy.size(0) == S * L && dy.size(1) == HD && stats.size(0) == S * L, "ina.bert_embed_ln_bwd: shapes");
+  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks > 0 ? blocks : 1024, (S * L + 3) / 4));
+  auto dx = at::empty({S * L, HD}, wemb.options());
+  auto slab = at::zeros({blocks, 2, HD}, wemb.options());
+  if (S == 0) return {dx, slab};
+  ina::BertEmbArgs a{};
+  a.inst = inst.data_ptr<int>();
+  a.ids = ids.data_ptr<int>();
+  a.S = (int)S;
+  a.L = (int)L;
+  a.HD = (int)HD;
+  a.blocks = (int)blocks;
+  a.wemb = wemb.data_ptr<float>();
+  a.pemb = pemb.data_ptr<float>();
+  a.temb = temb.data_ptr<float>();
+  a.gamma = gamma.data_ptr<float>();
+  a.stats = stats.data_ptr<float>();
+  a.dy = dy.data_ptr();
+  a.dx = dx.data_ptr<float>();
+  a.slab = slab.data_ptr<float>();
+  a.salt = salt_of(seed, 16);
+  a.thr = thr_of(1.0 - p);
+  a.inv_kp = (float)(1.0 / (1.0 - p));
+  a.drop = p > 0.0 ? 1 : 0;
+  launched(ina::embed_ln_bwd(a, stream()), "embed_ln_bwd");
+  return {dx, slab};
+}
+
+// ------------------------------------------------------------------ residual + dropout + LN
+std::tuple<Tensor, Tensor> bert_ln_res_fwd(const Tensor& a_, const Tensor& res, const Tensor& gamma,
+                                           const Tensor& beta, int64_t seed, int64_t stream_id, double p) {
+  chk(a_, "a", at::kBFloat16);
+  chk(res, "res", at::kBFloat16);
+  chk(gamma, "gamma", at::kFloat);
+  chk(beta, "beta", at::kFloat);
+  const int64_t T = a_.size(0), HD = a_.size(1);
+  check_hd(HD);
+  TORCH_CHECK(res.sizes() == a_.sizes() && gamma.numel() == HD && beta.numel() == HD, "ina.bert_ln_res_fwd: shapes");
+  TORCH_CHECK(T * HD < (1LL << 32), "ina.bert_ln_res_fwd: batch too large");
+  auto y = at::empty_like(a_);
+  auto stats = at::empty({T, 2}, gamma.options());
+  if (T == 0) return {y, stats};
+  ina::BertLnArgs a{};
+  a.a = a_.data_ptr();
+  a.res = res.data_ptr();
+  a.gamma = gamma.data_ptr<float>();
+  a.beta = beta.data_ptr<float>();
+  a.y = y.data_ptr();
+  a.stats = stats.data_ptr<float>();
+  a.T = (int)T;
+  a.HD = (int)HD;
+  a.salt = salt_of(seed, stream_id);
+  a.thr = thr_of(1.0 - p);
+  a.inv_kp = (float)(1.0 / (1.0 - p));
+  a.drop = p > 0.0 ? 1 : 0;
+  launched(ina::ln_res_fwd(a, stream()), "ln_res_fwd");
+  return {y, stats};
+}
+
+std::tuple<Tensor, Tensor, Tensor> bert_ln_res_bwd(const Tensor& dy, const Tensor& a_, const Tensor& res,
+                                                   const Tensor& gamma, const Tensor& stats, int64_t seed,
+                                                   int64_t stream_id, double p, int64_t blocks) {
+  chk(dy, "dy", at::kBFloat16);
+  chk(a_, "a", at::kBFloat16);
+  chk(res, "res", at::kBFloat16);
+  chk(gamma, "gamma", at::kFloat);
+  chk(stats, "stats", at::kFloat);
+  const int64_t T = a_.size(0), HD = a_.size(1);
+  check_hd(HD);
+  TORCH_CHECK(dy.sizes() == a_.sizes() && res.sizes() == a_.sizes() && stats.size(0) == T,
+              "ina.bert_ln_res_bwd: shapes");
+  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks > 0 ? blocks : 1024, (T + 3) / 4));
+  auto dres = at::empty_like(a_);
+  auto da = at::empty_like(a_);
+  auto slab = at::zeros({blocks, 2, HD}, gamma.options());
+  if (T == 0) return {dres, da, slab};
+  ina::BertLnArgs a{};
+  a.a = a_.data_ptr();
+  a.res = res.data_ptr();
+  a.gamma = gamma.data_ptr<float>();
+  a.stats = stats.data_ptr<float>();
+  a.dy = dy.data_ptr();
+  a.dres = dres.data_ptr();
+  a.da = da.data_ptr();
+  a.slab = slab.data_ptr<float>();
+  a.T = (int)T;
+  a.HD = (int)HD;
+  a.blocks = (int)blocks;
+  a.salt = salt_of(seed, stream_id);
+  a.thr = thr_of(1.0 - p);
+  a.inv_kp = (float)(1.0 / (1.0 - p));
+  a.drop = p > 0.0 ? 1 : 0;
+  launched(ina::ln_res_bwd(a, stream()), "ln_res_bwd");
+  return {dres, da, slab};
+}
+
+// ------------------------------------------------------------------ bias + GELU
+Tensor bert_bias_gelu_fwd(const Tensor& x, const Tensor& b) {
+  chk(x, "x", at::kBFloat16);
+  chk(b, "b", at::kFloat);
+  const int64_t T = x.size(0), I = x.size(1);
+  TORCH_CHECK(I % 8 == 0 && b.numel() == I, "ina.bert_bias_gelu_fwd: I must be a multiple of 8 and b [I]");
+  auto y = at::empty_like(x);
+  if (T == 0) return y;
+  launched(ina::bias_gelu_fwd(x.data_ptr(), b.data_ptr<float>(), y.data_ptr(), T, (int)I, stream()), "bias_gelu_fwd");
+  return y;
+}
+
+std::tuple<Tensor, Tensor> bert_bias_gelu_bwd(const Tensor& dy, const Tensor& x, const Tensor& b, int64_t blocks) {
+  chk(dy, "dy", at::kBFloat16);
+  chk(x, "x", at::kBFloat16);
+  chk(b, "b", at::kFloat);
+  const int64_t T = x.size(0), I = x.size(1);
+  TORCH_CHECK(dy.sizes() == x.sizes() && I % 8 == 0 && I / 8 <= 1024 && b.numel() == I,
+              "ina.bert_bias_gelu_bwd: shapes");
+  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks > 0 ? blocks : 1024, T));
+  auto dx = at::empty_like(x);
+  auto slab = at::zeros({blocks, I}, b.options());
+  if (T == 0) return {dx, slab};
+  launched(ina::bias_gelu_bwd(dy.data_ptr(), x.data_ptr(), b.data_ptr<float>(), dx.data_ptr(),
+                              slab.data_ptr<float>(), (int)T, (int)I, (int)blocks, stream()),
+           "bias_gelu_bwd");
+  return {dx, slab};
+}
+
+// ------------------------------------------------------------------ fused attention
+void mha_checks(const Tensor& qkv, const Tensor& inst, const Tensor& mask, int64_t L, int64_t nh) {
+  chk(qkv, "qkv", at::kBFloat16);
+  chk(inst, "inst", at::kInt);
+  chk(mask, "mask", at::kInt);
+  TORCH_CHECK(ina::mha_lp((int)L) > 0, "ina.bert_mha: L must be <= 128, got ", L);
+  TORCH_CHECK(mask.size(1) == L, "ina.bert_mha: mask must be [NI, L]");
+  TORCH_CHECK(qkv.size(0) == inst.size(0) * L && qkv.size(1) == 3 * 64 * nh, "ina.bert_mha: qkv must be [S*L, 3*nh*64]");
+  TORCH_CHECK(inst.size(0) * nh * L * L < (1LL << 32), "ina.bert_mha: dropout index range");
+}
+
+std::tuple<Tensor, Tensor> bert_mha_fwd(const Tensor& qkv, const Tensor& inst, const Tensor& mask, int64_t L,
+                                        int64_t nh, int64_t seed, int64_t stream_id, double p) {
+  mha_checks(qkv, inst, mask, L, nh);
+  const int64_t S = inst.size(0);
+  const int LP = ina::mha_lp((int)L);
+  auto ctx = at::empty({S * L, 64 * nh}, qkv.options());
+  auto lse = at::empty({S, nh, LP}, qkv.options().dtype(at::kFloat));
+  if (S == 0) return {ctx, lse};
+  ina::BertMhaArgs a{};
+  a.qkv = qkv.data_ptr();
+  a.inst = inst.data_ptr<int>();
+  a.mask = mask.data_ptr<int>();
+  a.S = (int)S;
+  a.L = (int)L;
+  a.nh = (int)nh;
+  a.ctx = ctx.data_ptr();
+  a.lse = lse.data_ptr<float>();
+  a.salt = salt_of(seed, stream_id);
+  a.thr = thr_of(1.0 - p);
+  a.inv_kp = (float)(1.0 / (1.0 - p));
+  a.drop = p > 0.0 ? 1 : 0;
+  launched(ina::mha_fwd(a, stream()), "mha_fwd");
+  return {ctx, lse};
+}
+
+Tensor bert_mha_bwd(const Tensor& qkv, const Tensor& ctx, const Tensor& dctx, const Tensor& lse, const Tensor& inst,
+                    const Tensor& mask, int64_t L, int64_t nh, int64_t seed, int64_t stream_id, double p) {
+  mha_checks(qkv, inst, mask, L, nh);
+  chk(ctx, "ctx", at::kBFloat16);
+  chk(dctx, "dctx", at::kBFloat16);
+  chk(lse, "lse", at::kFloat);
+  const int64_t S = inst.size(0);
+  TORCH_CHECK(ctx.size(0) == S * L && ctx.size(1) == 64 * nh && dctx.sizes() == ctx.sizes(), "ina.bert_mha_bwd: ctx");
+  TORCH_CHECK(lse.numel() == S * nh * ina::mha_lp((int)L), "ina.bert_mha_bwd: lse");
+  auto dqkv = at::empty_like(qkv);
+  if (S == 0) return dqkv;
+  ina::BertMhaArgs a{};
+  a.qkv = qkv.data_ptr();
+  a.inst = inst.data_ptr<int>();
+  a.mask = mask.data_ptr<int>();
+  a.S = (int)S;
+  a.L = (int)L;
+  a.nh = (int)nh;
+  a.ctx = ctx.data_ptr();
+  a.lse = lse.data_ptr<float>();
+  a.dctx = dctx.data_ptr();
+  a.dqkv = dqkv.data_ptr();
+  a.salt = salt_of(seed, stream_id);
+  a.thr = thr_of(1.0 - p);
+  a.inv_kp = (float)(1.0 / (1.0 - p));
+  a.drop = p > 0.0 ? 1 : 0;
+  launched(ina::mha_bwd(a, stream()), "mha_bwd");
+  return dqkv;
+}
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(ina, m) {
+  m.def("bert_embed_ln_fwd", &bert_embed_ln_fwd);
+  m.def("bert_embed_ln_bwd", &bert_embed_ln_bwd);
+  m.def("bert_ln_res_fwd", &bert_ln_res_fwd);
+  m.def("bert_ln_res_bwd", &bert_ln_res_bwd);
+  m.def("bert_bias_gelu_fwd", &bert_bias_gelu_fwd);
+  m.def("bert_bias_gelu_bwd", &bert_bias_gelu_bwd);
+  m.def("bert_mha_fwd", &bert_mha_fwd);
+  m.def("bert_mha_bwd", &bert_mha_bwd);
+}

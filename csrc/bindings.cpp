@@ -264,7 +264,7 @@ Tensor routing_fwd(const Tensor& e, const Tensor& Ws, int64_t E, int64_t N, int6
   check_episode_rows(e, E, N, K, Q, "ina.routing_fwd");
   const int64_t H = e.size(1);
   TORCH_CHECK(Ws.size(0) == H && Ws.size(1) == H, "ina.routing_fwd: W_s must be [H, H]");
-  TORCH_CHECK(ina::routing_lds_bytes((int)N, (int)K, (int)H, (int)R, false) <= 64 * 1024, "ina.routing_fwd: N*K too large");
+  TORCH_CHECK(ina::routing_lds_bytes((int)N, (int)K, (int)H, (int)R, false) <= 160 * 1024, "ina.routing_fwd: N*K too large");
   auto cls = at::empty({E, N, H}, e.options());
   if (E == 0) return cls;
   if (blocks <= 0) blocks = 4096;
@@ -285,7 +285,7 @@ Tensor routing_bwd(const Tensor& e, const Tensor& Ws, const Tensor& dcls, Tensor
   const int64_t H = e.size(1);
   TORCH_CHECK(de.sizes() == e.sizes(), "ina.routing_bwd: de shape");
   TORCH_CHECK(dcls.numel() == E * N * H, "ina.routing_bwd: dcls shape");
-  TORCH_CHECK(ina::routing_lds_bytes((int)N, (int)K, (int)H, (int)R, true) <= 64 * 1024, "ina.routing_bwd: N*K too large");
+  TORCH_CHECK(ina::routing_lds_bytes((int)N, (int)K, (int)H, (int)R, true) <= 160 * 1024, "ina.routing_bwd: N*K too large");
   if (blocks <= 0) blocks = 2048;
   blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, std::max<int64_t>(E, 1)));
   auto slab = at::zeros({blocks, H, H}, e.options());

@@ -67,16 +67,17 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
         if _newer(obj, [src, *headers, __file__]):
             tasks.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", *_VFLAGS,
                           "-I" + os.path.join(CSRC, "include"), "-c", src, "-o", obj])
-    bsrc = os.path.join(CSRC, "bindings.cpp")
-    bobj = os.path.join(OUT_DIR, "bindings.o")
-    objs.append(bobj)
-    if _newer(bobj, [bsrc, *headers, __file__]):
-        cxx = shutil.which("g++") or "c++"
-        cmd = [cxx, "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
-               "-D_GLIBCXX_USE_CXX11_ABI=1", "-I/opt/rocm/include"]
-        cmd += ["-I" + p for p in inc]
-        cmd += ["-I" + sysconfig.get_paths()["include"], "-I" + os.path.join(CSRC, "include"), "-c", bsrc, "-o", bobj]
-        tasks.append(cmd)
+    for bsrc in sorted(glob.glob(os.path.join(CSRC, "*.cpp"))):   # host-only torch bindings (g++)
+        bobj = os.path.join(OUT_DIR, os.path.basename(bsrc) + ".o")
+        objs.append(bobj)
+        if _newer(bobj, [bsrc, *headers, __file__]):
+            cxx = shutil.which("g++") or "c++"
+            cmd = [cxx, "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
+                   "-D_GLIBCXX_USE_CXX11_ABI=1", "-I/opt/rocm/include"]
+            cmd += ["-I" + p for p in inc]
+            cmd += ["-I" + sysconfig.get_paths()["include"], "-I" + os.path.join(CSRC, "include"), "-c", bsrc, "-o",
+                    bobj]
+            tasks.append(cmd)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         for out in ex.map(_run, tasks):
             if verbose and out.strip():

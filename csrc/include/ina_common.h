@@ -101,6 +101,11 @@ INA_DEVICE float cross_group_sum(float v) {
   v += __shfl_xor(v, 32, 64);
   return v;
 }
+INA_DEVICE float cross_group_max(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  v = fmaxf(v, __shfl_xor(v, 32, 64));
+  return v;
+}
 
 }  // namespace ina
 

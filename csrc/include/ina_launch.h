@@ -94,4 +94,66 @@ int slab_reduce(const float* slabs, long nslab, long len, float* out, int accumu
 bool sampler_supported(int N, int K, int Q);
 int sample_episodes(const int* scopes, int R, int E, int N, int K, int Q, uint32_t seed, float nota_rate, int* idx,
                     int* lab, hipStream_t st);
+
+// ---------------------------------------------------------------- BERT (csrc/kernels/bert.hip)
+struct BertLnArgs {          // y = LN(res + dropout(a)); HD = 256 * {1..4}
+  const void* a;
+  const void* res;
+  const float* gamma;
+  const float* beta;
+  void* y;
+  float* stats;              // [T, 2] mean, rstd
+  const void* dy;
+  void* dres;
+  void* da;
+  float* slab;               // [blocks, 2, HD]
+  int T, HD, blocks;
+  uint32_t salt, thr;
+  float inv_kp;
+  int drop;
+};
+int ln_res_fwd(const BertLnArgs& a, hipStream_t st);
+int ln_res_bwd(const BertLnArgs& a, hipStream_t st);
+
+struct BertEmbArgs {         // y = dropout(LN(word[ids[inst[s], t]] + pos[t] + type[0]))
+  const int* inst;
+  const int* ids;            // [NI, L]
+  int S, L, HD, blocks;
+  const float* wemb;
+  const float* pemb;
+  const float* temb;
+  const float* gamma;
+  const float* beta;
+  void* y;
+  float* stats;
+  const void* dy;
+  float* dx;                 // [S*L, HD] fp32
+  float* slab;
+  uint32_t salt, thr;
+  float inv_kp;
+  int drop;
+};
+int embed_ln_fwd(const BertEmbArgs& a, hipStream_t st);
+int embed_ln_bwd(const BertEmbArgs& a, hipStream_t st);
+
+int bias_gelu_fwd(const void* x, const float* b, void* y, long T, int I, hipStream_t st);
+int bias_gelu_bwd(const void* dy, const void* x, const float* b, void* dx, float* slab, int T, int I, int blocks,
+                  hipStream_t st);
+
+struct BertMhaArgs {         // fused attention, head dim 64, L <= 128
+  const void* qkv;           // [S*L, 3*nh*64] bf16
+  const int* inst;
+  const int* mask;           // [NI, L] int32 key mask
+  int S, L, nh;
+  void* ctx;                 // [S*L, nh*64] bf16
+  float* lse;                // [S, nh, LP]
+  const void* dctx;
+  void* dqkv;
+  uint32_t salt, thr;
+  float inv_kp;
+  int drop;
+};
+int mha_lp(int L);
+int mha_fwd(const BertMhaArgs& a, hipStream_t st);
+int mha_bwd(const BertMhaArgs& a, hipStream_t st);
 }  // namespace ina

@@ -1,0 +1,787 @@
+// BERT encoder kernels for gfx950 (north-star BERT path; BASELINE config
+// "FewRel 10-way 5-shot with BERT-base encoder").  The reference has no BERT; the math is standard
+// post-LN BERT and the oracle is models/bert.py.
+//
+//  * embed_ln     : x = word[id] + pos[t] + type[0];  y = LN(x) (+ hidden dropout)      fwd / bwd
+//  * ln_res       : y = LN(res + dropout(a))  (attention-output and FFN-output sublayers)  fwd / bwd
+//  * bias_gelu    : y = gelu(x + b)  (erf form), db summed per block                        fwd / bwd
+//  * mha          : fused multi-head attention for one (sequence, head) per workgroup with the
+//                   whole sequence (L <= 128) resident in LDS; MFMA 16x16x32 bf16 for all
+//                   products; softmax in registers; attention-probability dropout from the
+//                   counter hash; backward recomputes P from the saved log-sum-exp.
+//
+// Row kernels (LN, embed) put one row on one wave: lane l owns columns 256c + 4l .. +3 (c < NCH),
+// 8-byte bf16 loads/stores, wave-shuffle reductions; hidden width HD = 256 * NCH.
+//
+// MHA layouts (lane l: n = l & 15, g = l >> 4; MFMA C[row 4g + r][col n]):
+//  forward ("query on the lane"): S^T = K Q^T tiles (A = K rows from LDS, B = the query's 16-B
+//    row slices kept in registers), so the softmax over keys is in-register + a 4-lane-group
+//    shuffle; O^T = V^T P^T takes the P^T accumulators directly as the B operand (kmap key order)
+//    and V^T from LDS.
+//  backward ("key on the lane"): each wave owns key tiles; S = Q K^T and dP = dO V^T have the key
+//    on the lane, so dV^T = dO^T P' and dK^T = Q^T dS take P'/dS accumulators as B operands (q in
+//    kmap order, dO^T / Q^T from LDS); dS crosses LDS once for dQ^T = K^T dS^T.
+#include "ina_common.h"
+#include "ina_launch.h"
+
+using namespace ina;
+
+namespace {
+
+constexpr float LN_EPS = 1e-12f;
+constexpr float LOG2E = 1.4426950408889634f;
+
+INA_DEVICE void ld4(const unsigned short* p, float* v) {
+  const u16x4_t x = *reinterpret_cast<const u16x4_t*>(p);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = bf2f(x[r]);
+}
+INA_DEVICE void st4(unsigned short* p, const float* v) {
+  u16x4_t x;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) x[r] = f2bf(v[r]);
+  *reinterpret_cast<u16x4_t*>(p) = x;
+}
+INA_DEVICE float4 ld4f(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// --------------------------------------------------------------------------------------------
+// LN(res + dropout(a))
+// --------------------------------------------------------------------------------------------
+template <int NCH>
+__global__ __launch_bounds__(256) void ln_res_fwd_kernel(const unsigned short* __restrict__ a,
+                                                         const unsigned short* __restrict__ res,
+                                                         const float* __restrict__ gam, const float* __restrict__ bet,
+                                                         unsigned short* __restrict__ y, float* __restrict__ stats,
+                                                         int T, uint32_t salt, uint32_t thr, float inv_kp, int drop) {
+  constexpr int HD = 256 * NCH;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= T) return;
+  const size_t base = (size_t)row * HD;
+  float x[NCH][4];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = 256 * c + 4 * lane;
+    float av[4], rv[4];
+    ld4(a + base + col, av);
+    ld4(res + base + col, rv);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = av[r];
+      if (drop) v = dropout_keep_salted(salt, (uint32_t)(base + col + r), thr) ? v * inv_kp : 0.f;
+      x[c][r] = v + rv[r];
+      s += x[c][r];
+    }
+  }
+  const float mean = wave_sum(s) * (1.f / HD);
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float d = x[c][r] - mean;
+      q += d * d;
+    }
+  const float rstd = rsqrtf(wave_sum(q) * (1.f / HD) + LN_EPS);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = 256 * c + 4 * lane;
+    const float4 gv = ld4f(gam + col), bv = ld4f(bet + col);
+    float o[4] = {(x[c][0] - mean) * rstd * gv.x + bv.x, (x[c][1] - mean) * rstd * gv.y + bv.y,
+                  (x[c][2] - mean) * rstd * gv.z + bv.z, (x[c][3] - mean) * rstd * gv.w + bv.w};
+    st4(y + base + col, o);
+  }
+  if (lane == 0) {
+    stats[2 * row] = mean;
+    stats[2 * row + 1] = rstd;
+  }
+}
+
+// dres = dLN/dx (bf16), da = dres * dropout mask / kp (bf16), slab[block] = [dgamma | dbeta]
+template <int NCH>
+__global__ __launch_bounds__(256) void ln_res_bwd_kernel(
+    const unsigned short* __restrict__ dy, const unsigned short* __restrict__ a, const unsigned short* __restrict__ res,
+    const float* __restrict__ gam, const float* __restrict__ stats, unsigned short* __restrict__ dres,
+    unsigned short* __restrict__ da, float* __restrict__ slab, int T, uint32_t salt, uint32_t thr, float inv_kp,
+    int drop) {
+  constexpr int HD = 256 * NCH;
+  __shared__ float red[4][2][HD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float dg[NCH][4], db[NCH][4];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dg[c][r] = db[c][r] = 0.f;
+  for (int row = blockIdx.x * 4 + wave; row < T; row += gridDim.x * 4) {
+    const size_t base = (size_t)row * HD;
+    const float mean = stats[2 * row], rstd = stats[2 * row + 1];
+    float xh[NCH][4], dyg[NCH][4], dyv[NCH][4];
+    bool keep[NCH][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = 256 * c + 4 * lane;
+      float av[4], rv[4];
+      ld4(a + base + col, av);
+      ld4(res + base + col, rv);
+      ld4(dy + base + col, dyv[c]);
+      const float4 gv = ld4f(gam + col);
+      const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        keep[c][r] = !drop || dropout_keep_salted(salt, (uint32_t)(base + col + r), thr);
+        const float v = drop ? (keep[c][r] ? av[r] * inv_kp : 0.f) : av[r];
+        xh[c][r] = (v + rv[r] - mean) * rstd;
+        dyg[c][r] = dyv[c][r] * gg[r];
+        s1 += dyg[c][r];
+        s2 += dyg[c][r] * xh[c][r];
+        dg[c][r] += dyv[c][r] * xh[c][r];
+        db[c][r] += dyv[c][r];
+      }
+    }
+    const float m1 = wave_sum(s1) * (1.f / HD), m2 = wave_sum(s2) * (1.f / HD);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = 256 * c + 4 * lane;
+      float dx[4], dav[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dx[r] = rstd * (dyg[c][r] - m1 - xh[c][r] * m2);
+        dav[r] = drop ? (keep[c][r] ? dx[r] * inv_kp : 0.f) : dx[r];
+      }
+      st4(dres + base + col, dx);
+      st4(da + base + col, dav);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      red[wave][0][256 * c + 4 * lane + r] = dg[c][r];
+      red[wave][1][256 * c + 4 * lane + r] = db[c][r];
+    }
+  __syncthreads();
+  float* out = slab + (size_t)blockIdx.x * 2 * HD;
+  for (int i = threadIdx.x; i < 2 * HD; i += 256) {
+    const int k = i / HD, col = i - k * HD;
+    out[i] = red[0][k][col] + red[1][k][col] + red[2][k][col] + red[3][k][col];
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// embeddings: x = word[id] + pos[t] + type[0];  y = dropout(LN(x))
+// --------------------------------------------------------------------------------------------
+template <int NCH>
+__global__ __launch_bounds__(256) void embed_ln_fwd_kernel(
+    const int* __restrict__ inst, const int* __restrict__ ids_all, int S, int L, const float* __restrict__ wemb,
+    const float* __restrict__ pemb, const float* __restrict__ temb, const float* __restrict__ gam,
+    const float* __restrict__ bet, unsigned short* __restrict__ y, float* __restrict__ stats, uint32_t salt,
+    uint32_t thr, float inv_kp, int drop) {
+  constexpr int HD = 256 * NCH;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= S * L) return;
+  const int s = row / L, t = row - s * L;
+  const int id = ids_all[(size_t)inst[s] * L + t];
+  const size_t base = (size_t)row * HD;
+  float x[NCH][4];
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = 256 * c + 4 * lane;
+    const float4 w = ld4f(wemb + (size_t)id * HD + col), p = ld4f(pemb + (size_t)t * HD + col),
+                 ty = ld4f(temb + col);
+    x[c][0] = w.x + p.x + ty.x;
+    x[c][1] = w.y + p.y + ty.y;
+    x[c][2] = w.z + p.z + ty.z;
+    x[c][3] = w.w + p.w + ty.w;
+    sum += x[c][0] + x[c][1] + x[c][2] + x[c][3];
+  }
+  const float mean = wave_sum(sum) * (1.f / HD);
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) q += (x[c][r] - mean) * (x[c][r] - mean);
+  const float rstd = rsqrtf(wave_sum(q) * (1.f / HD) + LN_EPS);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = 256 * c + 4 * lane;
+    const float4 gv = ld4f(gam + col), bv = ld4f(bet + col);
+    const float gg[4] = {gv.x, gv.y, gv.z, gv.w}, bb[4] = {bv.x, bv.y, bv.z, bv.w};
+    float o[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      o[r] = (x[c][r] - mean) * rstd * gg[r] + bb[r];
+      if (drop) o[r] = dropout_keep_salted(salt, (uint32_t)(base + col + r), thr) ? o[r] * inv_kp : 0.f;
+    }
+    st4(y + base + col, o);
+  }
+  if (lane == 0) {
+    stats[2 * row] = mean;
+    stats[2 * row + 1] = rstd;
+  }
+}
+
+// dx (fp32 [T, HD], the gradient of the summed embedding; the caller scatters it into the word /
+// position / type tables) and slab[block] = [dgamma | dbeta]
+template <int NCH>
+__global__ __launch_bounds__(256) void embed_ln_bwd_kernel(
+    const unsigned short* __restrict__ dy, const int* __restrict__ inst, const int* __restrict__ ids_all, int S,
+    int L, const float* __restrict__ wemb, const float* __restrict__ pemb, const float* __restrict__ temb,
+    const float* __restrict__ gam, const float* __restrict__ stats, float* __restrict__ dx, float* __restrict__ slab,
+    uint32_t salt, uint32_t thr, float inv_kp, int drop) {
+  constexpr int HD = 256 * NCH;
+  __shared__ float red[4][2][HD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float dg[NCH][4], db[NCH][4];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dg[c][r] = db[c][r] = 0.f;
+  const int T = S * L;
+  for (int row = blockIdx.x * 4 + wave; row < T; row += gridDim.x * 4) {
+    const int s = row / L, t = row - s * L;
+    const int id = ids_all[(size_t)inst[s] * L + t];
+    const size_t base = (size_t)row * HD;
+    const float mean = stats[2 * row], rstd = stats[2 * row + 1];
+    float xh[NCH][4], dyg[NCH][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = 256 * c + 4 * lane;
+      const float4 w = ld4f(wemb + (size_t)id * HD + col), p = ld4f(pemb + (size_t)t * HD + col),
+                   ty = ld4f(temb + col), gv = ld4f(gam + col);
+      const float xv[4] = {w.x + p.x + ty.x, w.y + p.y + ty.y, w.z + p.z + ty.z, w.w + p.w + ty.w};
+      const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+      float dyv[4];
+      ld4(dy + base + col, dyv);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (drop) dyv[r] = dropout_keep_salted(salt, (uint32_t)(base + col + r), thr) ? dyv[r] * inv_kp : 0.f;
+        xh[c][r] = (xv[r] - mean) * rstd;
+        dyg[c][r] = dyv[r] * gg[r];
+        s1 += dyg[c][r];
+        s2 += dyg[c][r] * xh[c][r];
+        dg[c][r] += dyv[r] * xh[c][r];
+        db[c][r] += dyv[r];
+      }
+    }
+    const float m1 = wave_sum(s1) * (1.f / HD), m2 = wave_sum(s2) * (1.f / HD);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = 256 * c + 4 * lane;
+      float4 o;
+      o.x = rstd * (dyg[c][0] - m1 - xh[c][0] * m2);
+      o.y = rstd * (dyg[c][1] - m1 - xh[c][1] * m2);
+      o.z = rstd * (dyg[c][2] - m1 - xh[c][2] * m2);
+      o.w = rstd * (dyg[c][3] - m1 - xh[c][3] * m2);
+      *reinterpret_cast<float4*>(dx + base + col) = o;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      red[wave][0][256 * c + 4 * lane + r] = dg[c][r];
+      red[wave][1][256 * c + 4 * lane + r] = db[c][r];
+    }
+  __syncthreads();
+  float* out = slab + (size_t)blockIdx.x * 2 * HD;
+  for (int i = threadIdx.x; i < 2 * HD; i += 256) {
+    const int k = i / HD, col = i - k * HD;
+    out[i] = red[0][k][col] + red[1][k][col] + red[2][k][col] + red[3][k][col];
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// bias + GELU (erf form)
+// --------------------------------------------------------------------------------------------
+INA_DEVICE float gelu_f(float u) { return 0.5f * u * (1.f + erff(u * 0.70710678118654752f)); }
+INA_DEVICE float gelu_grad(float u) {
+  return 0.5f * (1.f + erff(u * 0.70710678118654752f)) + u * 0.3989422804014327f * __expf(-0.5f * u * u);
+}
+
+// x, y: [T, I] bf16 row-major; I % 8 == 0.  Grid-stride over 8-element chunks.
+__global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const unsigned short* __restrict__ x,
+                                                            const float* __restrict__ b,
+                                                            unsigned short* __restrict__ y, long nchunks, int I) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nchunks; i += (long)gridDim.x * 256) {
+    const long e0 = i * 8;
+    const int col = (int)(e0 % I);
+    const u16x8_t v = *reinterpret_cast<const u16x8_t*>(x + e0);
+    const float4 b0 = ld4f(b + col), b1 = ld4f(b + col + 4);
+    const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    u16x8_t o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(gelu_f(bf2f(v[j]) + bb[j]));
+    *reinterpret_cast<u16x8_t*>(y + e0) = o;
+  }
+}
+
+// dx = dy * gelu'(x + b); slab[block][I] = column sums of dx over the block's rows.
+// Thread t owns column chunks t, t + 256, ... (< I/8, at most CPT of them); blocks stride rows.
+template <int CPT>
+__global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const unsigned short* __restrict__ dy,
+                                                            const unsigned short* __restrict__ x,
+                                                            const float* __restrict__ b, unsigned short* __restrict__ dx,
+                                                            float* __restrict__ slab, int T, int I) {
+  const int nch = I / 8;
+  float acc[CPT][8];
+  float bb[CPT][8];
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int ch = threadIdx.x + 256 * k;
+    const int col = (ch < nch ? ch : 0) * 8;
+    const float4 b0 = ld4f(b + col), b1 = ld4f(b + col + 4);
+    bb[k][0] = b0.x; bb[k][1] = b0.y; bb[k][2] = b0.z; bb[k][3] = b0.w;
+    bb[k][4] = b1.x; bb[k][5] = b1.y; bb[k][6] = b1.z; bb[k][7] = b1.w;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+  }
+  for (int row = blockIdx.x; row < T; row += gridDim.x) {
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int ch = threadIdx.x + 256 * k;
+      if (ch < nch) {
+        const size_t e0 = (size_t)row * I + ch * 8;
+        const u16x8_t gv = *reinterpret_cast<const u16x8_t*>(dy + e0);
+        const u16x8_t xv = *reinterpret_cast<const u16x8_t*>(x + e0);
+        u16x8_t o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = bf2f(gv[j]) * gelu_grad(bf2f(xv[j]) + bb[k][j]);
+          o[j] = f2bf(d);
+          acc[k][j] += d;
+        }
+        *reinterpret_cast<u16x8_t*>(dx + e0) = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int ch = threadIdx.x + 256 * k;
+    if (ch < nch) {
+      float* o = slab + (size_t)blockIdx.x * I + ch * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = acc[k][j];
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// fused multi-head attention, head dim 64, L <= 128
+// --------------------------------------------------------------------------------------------
+constexpr int HDIM = 64;
+constexpr int KSTR = HDIM + 8;  // LDS row stride (bf16) of row-major [key][d] images
+
+INA_DEVICE u16x8_t ld8(const unsigned short* p) { return *reinterpret_cast<const u16x8_t*>(p); }
+INA_DEVICE u16x4_t ld4h(const unsigned short* p) { return *reinterpret_cast<const u16x4_t*>(p); }
+INA_DEVICE u16x8_t cat44(const u16x4_t& a, const u16x4_t& b) {
+  return u16x8_t{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+INA_DEVICE u16x8_t zero8() { return u16x8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
+
+// qkv: [T, 3*HDm] bf16, HDm = nh*64; token row of (s, t) = s*L + t.  ctx: [T, HDm] bf16.
+// lse: [S, nh, LP] fp32 (log2-domain log-sum-exp of the scaled scores).  mask_all: [NI, L] int.
+template <int LP>
+__global__ __launch_bounds__(256) void mha_fwd_kernel(const unsigned short* __restrict__ qkv,
+                                                      const int* __restrict__ inst, const int* __restrict__ mask_all,
+                                                      int S, int L, int nh, unsigned short* __restrict__ ctx,
+                                                      float* __restrict__ lse, uint32_t salt, uint32_t thr,
+                                                      float inv_kp, int drop) {
+  constexpr int NT = LP / 16;        // key / query tiles
+  constexpr int VSTR = LP + 8;       // V^T row stride
+  __shared__ __attribute__((aligned(16))) unsigned short Ks[LP * KSTR];
+  __shared__ __attribute__((aligned(16))) unsigned short Vt[HDIM * VSTR];
+  __shared__ float madd[LP];
+  const int s = blockIdx.x / nh, hh = blockIdx.x - s * nh;
+  const int HDm = nh * HDIM, ROW = 3 * HDm;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const size_t tok0 = (size_t)s * L;
+  const unsigned short* kbase = qkv + tok0 * ROW + HDm + hh * HDIM;
+  const unsigned short* vbase = qkv + tok0 * ROW + 2 * HDm + hh * HDIM;
+  // stage K rows and V^T (rows >= L are zero), key mask
+  for (int i = threadIdx.x; i < LP * 8; i += 256) {
+    const int k = i >> 3, c = (i & 7) * 8;
+    const bool ok = k < L;
+    const size_t off = (size_t)(ok ? k : 0) * ROW + c;
+    u16x8_t kv = ld8(kbase + off), vv = ld8(vbase + off);
+    if (!ok) kv = vv = zero8();
+    *reinterpret_cast<u16x8_t*>(&Ks[k * KSTR + c]) = kv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Vt[(c + j) * VSTR + k] = vv[j];
+  }
+  const int* mrow = mask_all + (size_t)inst[s] * L;
+  for (int k = threadIdx.x; k < LP; k += 256) madd[k] = (k < L && mrow[k < L ? k : 0] > 0) ? 0.f : -INFINITY;
+  __syncthreads();
+  const float c2 = 0.125f * LOG2E;  // 1/sqrt(64) in the log2 domain
+#pragma unroll 1
+  for (int qt = wave; qt < NT; qt += 4) {
+    const int q = 16 * qt + n;
+    const bool qok = q < L;
+    const unsigned short* qrow = qkv + (tok0 + (qok ? q : 0)) * ROW + hh * HDIM;
+    u16x8_t qf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qf[ks] = ld8(qrow + 32 * ks + 8 * g);
+      if (!qok) qf[ks] = zero8();
+    }
+    float sc[NT][4];
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) {
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        acc = mfma_bf16(ld8(&Ks[(16 * kt + n) * KSTR + 32 * ks + 8 * g]), qf[ks], acc);
+      const float4 ma = *reinterpret_cast<const float4*>(&madd[16 * kt + 4 * g]);
+      sc[kt][0] = acc[0] * c2 + ma.x;
+      sc[kt][1] = acc[1] * c2 + ma.y;
+      sc[kt][2] = acc[2] * c2 + ma.z;
+      sc[kt][3] = acc[3] * c2 + ma.w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) m = fmaxf(m, sc[kt][r]);
+    }
+    m = cross_group_max(m);
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sc[kt][r] = exp2f(sc[kt][r] - m);
+        l += sc[kt][r];
+      }
+    l = cross_group_sum(l);
+    const float inv_l = 1.f / l;
+    if (drop) {
+      const uint32_t rowidx = ((uint32_t)(s * nh + hh) * L + q) * L;
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = 16 * kt + 4 * g + r;
+          sc[kt][r] = dropout_keep_salted(salt, rowidx + key, thr) ? sc[kt][r] * inv_kp : 0.f;
+        }
+    }
+    // O^T = V^T P^T: B operand = P^T accumulators (k-step ks2 covers key tiles 2ks2, 2ks2+1)
+    u16x8_t pf[NT / 2];
+#pragma unroll
+    for (int k2 = 0; k2 < NT / 2; ++k2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf[k2][j] = f2bf(sc[2 * k2 + (j >> 2)][j & 3]);
+    unsigned short* orow = ctx + (tok0 + (qok ? q : 0)) * HDm + hh * HDIM;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+      const unsigned short* vr = &Vt[(16 * dt + n) * VSTR];
+#pragma unroll
+      for (int k2 = 0; k2 < NT / 2; ++k2)
+        acc = mfma_bf16(cat44(ld4h(vr + 32 * k2 + 4 * g), ld4h(vr + 32 * k2 + 16 + 4 * g)), pf[k2], acc);
+      if (qok) {
+        float o[4] = {acc[0] * inv_l, acc[1] * inv_l, acc[2] * inv_l, acc[3] * inv_l};
+        st4(orow + 16 * dt + 4 * g, o);
+      }
+    }
+    if (g == 0) lse[((size_t)s * nh + hh) * LP + q] = m + __log2f(l);
+  }
+}
+
+// dqkv: [T, 3*HDm] bf16 (dQ | dK | dV), fully written (rows of tokens < L).
+template <int LP>
+__global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __restrict__ qkv,
+                                                      const unsigned short* __restrict__ ctx,
+                                                      const unsigned short* __restrict__ dctx,
+                                                      const float* __restrict__ lse, const int* __restrict__ inst,
+                                                      const int* __restrict__ mask_all, int S, int L, int nh,
+                                                      unsigned short* __restrict__ dqkv, uint32_t salt, uint32_t thr,
+                                                      float inv_kp, int drop) {
+  constexpr int NT = LP / 16;
+  constexpr int TSTR = LP + 8;       // row stride of the [d][q] / [d][key] transposed images
+  constexpr int SSTR = LP + 8;       // row stride of dS [q][key]
+  // region A: Q^T and dO^T (phase 1), then K^T (phase 2)
+  __shared__ __attribute__((aligned(16))) unsigned short TA[2 * HDIM * TSTR];
+  __shared__ __attribute__((aligned(16))) unsigned short dSl[LP * SSTR];
+  __shared__ float delta[LP];
+  __shared__ float madd[LP];
+  unsigned short* Qt = TA;
+  unsigned short* dOt = TA + HDIM * TSTR;
+  unsigned short* Kt = TA;
+  const int s = blockIdx.x / nh, hh = blockIdx.x - s * nh;
+  const int HDm = nh * HDIM, ROW = 3 * HDm;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const size_t tok0 = (size_t)s * L;
+  const unsigned short* qb = qkv + tok0 * ROW + hh * HDIM;
+  const unsigned short* kb = qb + HDm;
+  const unsigned short* vb = qb + 2 * HDm;
+  const unsigned short* ob = ctx + tok0 * HDm + hh * HDIM;
+  const unsigned short* gb = dctx + tok0 * HDm + hh * HDIM;
+  const float* lrow = lse + ((size_t)s * nh + hh) * LP;
+  // phase 0: Q^T, dO^T images; delta = rowsum(dO * O); key mask
+  for (int i = threadIdx.x; i < LP * 8; i += 256) {
+    const int q = i >> 3, c = (i & 7) * 8;
+    const bool ok = q < L;
+    const size_t qo = (size_t)(ok ? q : 0) * ROW + c, oo = (size_t)(ok ? q : 0) * HDm + c;
+    u16x8_t qv = ld8(qb + qo), dv = ld8(gb + oo);
+    if (!ok) qv = dv = zero8();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      Qt[(c + j) * TSTR + q] = qv[j];
+      dOt[(c + j) * TSTR + q] = dv[j];
+    }
+  }
+  for (int q = wave; q < LP; q += 4) {   // one wave per query row: 64 lanes = 64 d
+    const bool ok = q < L;
+    const size_t oo = (size_t)(ok ? q : 0) * HDm + lane;
+    float d = bf2f(gb[oo]) * bf2f(ob[oo]);
+    d = wave_sum(d);
+    if (lane == 0) delta[q] = ok ? d : 0.f;
+  }
+  const int* mrow = mask_all + (size_t)inst[s] * L;
+  for (int k = threadIdx.x; k < LP; k += 256) madd[k] = (k < L && mrow[k < L ? k : 0] > 0) ? 0.f : -INFINITY;
+  __syncthreads();
+  const float c2 = 0.125f * LOG2E;
+  const float scale = 0.125f;
+  // phase 1: each wave owns key tiles kt = wave, wave + 4
+#pragma unroll 1
+  for (int kt = wave; kt < NT; kt += 4) {
+    const int key = 16 * kt + n;
+    const bool kok = key < L;
+    u16x8_t kf[2], vf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      kf[ks] = ld8(kb + (size_t)(kok ? key : 0) * ROW + 32 * ks + 8 * g);
+      vf[ks] = ld8(vb + (size_t)(kok ? key : 0) * ROW + 32 * ks + 8 * g);
+      if (!kok) kf[ks] = vf[ks] = zero8();
+    }
+    const float ma = madd[key];
+    f32x4_t dV[4], dK[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dV[dt] = dK[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int qp = 0; qp < NT / 2; ++qp) {
+      float pp[2][4], ds[2][4];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int qt = 2 * qp + h2;
+        const int qa = 16 * qt + n;   // A-operand row (query) of this lane
+        const bool qaok = qa < L;
+        f32x4_t sacc = {0.f, 0.f, 0.f, 0.f}, pacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          u16x8_t qa8 = ld8(qb + (size_t)(qaok ? qa : 0) * ROW + 32 * ks + 8 * g);
+          u16x8_t ga8 = ld8(gb + (size_t)(qaok ? qa : 0) * HDm + 32 * ks + 8 * g);
+          if (!qaok) qa8 = ga8 = zero8();
+          sacc = mfma_bf16(qa8, kf[ks], sacc);
+          pacc = mfma_bf16(ga8, vf[ks], pacc);
+        }
+        const float4 lq = *reinterpret_cast<const float4*>(&lrow[16 * qt + 4 * g]);
+        const float4 dq = *reinterpret_cast<const float4*>(&delta[16 * qt + 4 * g]);
+        const float lqa[4] = {lq.x, lq.y, lq.z, lq.w}, dqa[4] = {dq.x, dq.y, dq.z, dq.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = 16 * qt + 4 * g + r;
+          const float p = (q < L) ? exp2f(sacc[r] * c2 + ma - lqa[r]) : 0.f;
+          float z = 1.f;
+          if (drop) z = dropout_keep_salted(salt, ((uint32_t)(s * nh + hh) * L + q) * L + key, thr) ? inv_kp : 0.f;
+          const float dp = pacc[r] * z;
+          pp[h2][r] = p * z;
+          ds[h2][r] = p * (dp - dqa[r]);
+        }
+      }
+      u16x8_t pf, sf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pf[j] = f2bf(pp[j >> 2][j & 3]);
+        sf[j] = f2bf(ds[j >> 2][j & 3]);
+      }
+      // dS -> LDS for the dQ phase: dSl[q][key]
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dSl[(32 * qp + 16 * (j >> 2) + 4 * g + (j & 3)) * SSTR + key] = sf[j];
+      // dV^T += dO^T P' ; dK^T += Q^T dS   (A rows = d, k = query in kmap order)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const unsigned short* gr = &dOt[(16 * dt + n) * TSTR + 32 * qp];
+        const unsigned short* qr = &Qt[(16 * dt + n) * TSTR + 32 * qp];
+        dV[dt] = mfma_bf16(cat44(ld4h(gr + 4 * g), ld4h(gr + 16 + 4 * g)), pf, dV[dt]);
+        dK[dt] = mfma_bf16(cat44(ld4h(qr + 4 * g), ld4h(qr + 16 + 4 * g)), sf, dK[dt]);
+      }
+    }
+    // outputs: dK^T / dV^T tiles -> rows of dqkv (lane: key = 16kt + n, d = 16dt + 4g + r)
+    if (kok) {
+      unsigned short* dk = dqkv + (tok0 + key) * ROW + HDm + hh * HDIM;
+      unsigned short* dv = dk + HDm;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        float a[4] = {dK[dt][0] * scale, dK[dt][1] * scale, dK[dt][2] * scale, dK[dt][3] * scale};
+        float b[4] = {dV[dt][0], dV[dt][1], dV[dt][2], dV[dt][3]};
+        st4(dk + 16 * dt + 4 * g, a);
+        st4(dv + 16 * dt + 4 * g, b);
+      }
+    }
+  }
+  __syncthreads();
+  // phase 2: K^T image into region A, then dQ^T = K^T dS^T per query tile
+  for (int i = threadIdx.x; i < LP * 8; i += 256) {
+    const int k = i >> 3, c = (i & 7) * 8;
+    const bool ok = k < L;
+    u16x8_t kv = ld8(kb + (size_t)(ok ? k : 0) * ROW + c);
+    if (!ok) kv = zero8();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Kt[(c + j) * TSTR + k] = kv[j];
+  }
+  __syncthreads();
+  for (int qt = wave; qt < NT; qt += 4) {
+    const int q = 16 * qt + n;
+    f32x4_t acc[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k2 = 0; k2 < NT / 2; ++k2) {
+      const u16x8_t bs = ld8(&dSl[q * SSTR + 32 * k2 + 8 * g]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma_bf16(ld8(&Kt[(16 * dt + n) * TSTR + 32 * k2 + 8 * g]), bs, acc[dt]);
+    }
+    if (q < L) {
+      unsigned short* dq = dqkv + (tok0 + q) * ROW + hh * HDIM;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        float a[4] = {acc[dt][0] * scale, acc[dt][1] * scale, acc[dt][2] * scale, acc[dt][3] * scale};
+        st4(dq + 16 * dt + 4 * g, a);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// --------------------------------------------------------------------------------------------
+// launchers
+// --------------------------------------------------------------------------------------------
+namespace ina {
+
+#define INA_NCH_DISPATCH(HD, CALL) \
+  switch ((HD) / 256) {            \
+    case 1: CALL(1); break;        \
+    case 2: CALL(2); break;        \
+    case 3: CALL(3); break;        \
+    case 4: CALL(4); break;        \
+    default: return -1;            \
+  }
+
+int ln_res_fwd(const BertLnArgs& a, hipStream_t st) {
+  const int grid = (a.T + 3) / 4;
+#define CALL(NC)                                                                                               \
+  hipLaunchKernelGGL(ln_res_fwd_kernel<NC>, dim3(grid), dim3(256), 0, st, (const unsigned short*)a.a,         \
+                     (const unsigned short*)a.res, a.gamma, a.beta, (unsigned short*)a.y, a.stats, a.T, a.salt, \
+                     a.thr, a.inv_kp, a.drop)
+  INA_NCH_DISPATCH(a.HD, CALL)
+#undef CALL
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ln_res_bwd(const BertLnArgs& a, hipStream_t st) {
+#define CALL(NC)                                                                                                 \
+  hipLaunchKernelGGL(ln_res_bwd_kernel<NC>, dim3(a.blocks), dim3(256), 0, st, (const unsigned short*)a.dy,      \
+                     (const unsigned short*)a.a, (const unsigned short*)a.res, a.gamma, a.stats,                \
+                     (unsigned short*)a.dres, (unsigned short*)a.da, a.slab, a.T, a.salt, a.thr, a.inv_kp, a.drop)
+  INA_NCH_DISPATCH(a.HD, CALL)
+#undef CALL
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int embed_ln_fwd(const BertEmbArgs& a, hipStream_t st) {
+  const int grid = (a.S * a.L + 3) / 4;
+#define CALL(NC)                                                                                               \
+  hipLaunchKernelGGL(embed_ln_fwd_kernel<NC>, dim3(grid), dim3(256), 0, st, a.inst, a.ids, a.S, a.L, a.wemb,  \
+                     a.pemb, a.temb, a.gamma, a.beta, (unsigned short*)a.y, a.stats, a.salt, a.thr, a.inv_kp, \
+                     a.drop)
+  INA_NCH_DISPATCH(a.HD, CALL)
+#undef CALL
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int embed_ln_bwd(const BertEmbArgs& a, hipStream_t st) {
+#define CALL(NC)                                                                                                \
+  hipLaunchKernelGGL(embed_ln_bwd_kernel<NC>, dim3(a.blocks), dim3(256), 0, st, (const unsigned short*)a.dy,  \
+                     a.inst, a.ids, a.S, a.L, a.wemb, a.pemb, a.temb, a.gamma, a.stats, a.dx, a.slab, a.salt, \
+                     a.thr, a.inv_kp, a.drop)
+  INA_NCH_DISPATCH(a.HD, CALL)
+#undef CALL
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int bias_gelu_fwd(const void* x, const float* b, void* y, long T, int I, hipStream_t st) {
+  const long nchunks = T * (long)I / 8;
+  long grid = (nchunks + 255) / 256;
+  if (grid > 65536) grid = 65536;
+  hipLaunchKernelGGL(bias_gelu_fwd_kernel, dim3((unsigned)grid), dim3(256), 0, st, (const unsigned short*)x, b,
+                     (unsigned short*)y, nchunks, I);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int bias_gelu_bwd(const void* dy, const void* x, const float* b, void* dx, float* slab, int T, int I, int blocks,
+                  hipStream_t st) {
+  const int nch = I / 8;
+  if (nch <= 256) {
+    hipLaunchKernelGGL(bias_gelu_bwd_kernel<1>, dim3(blocks), dim3(256), 0, st, (const unsigned short*)dy,
+                       (const unsigned short*)x, b, (unsigned short*)dx, slab, T, I);
+  } else if (nch <= 512) {
+    hipLaunchKernelGGL(bias_gelu_bwd_kernel<2>, dim3(blocks), dim3(256), 0, st, (const unsigned short*)dy,
+                       (const unsigned short*)x, b, (unsigned short*)dx, slab, T, I);
+  } else if (nch <= 1024) {
+    hipLaunchKernelGGL(bias_gelu_bwd_kernel<4>, dim3(blocks), dim3(256), 0, st, (const unsigned short*)dy,
+                       (const unsigned short*)x, b, (unsigned short*)dx, slab, T, I);
+  } else {
+    return -1;
+  }
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int mha_lp(int L) { return L <= 32 ? 32 : (L <= 64 ? 64 : (L <= 96 ? 96 : (L <= 128 ? 128 : -1))); }
+
+int mha_fwd(const BertMhaArgs& a, hipStream_t st) {
+  const dim3 grid(a.S * a.nh);
+#define CALL(LP)                                                                                          \
+  hipLaunchKernelGGL(mha_fwd_kernel<LP>, grid, dim3(256), 0, st, (const unsigned short*)a.qkv, a.inst,   \
+                     a.mask, a.S, a.L, a.nh, (unsigned short*)a.ctx, a.lse, a.salt, a.thr, a.inv_kp, a.drop)
+  switch (mha_lp(a.L)) {
+    case 32: CALL(32); break;
+    case 64: CALL(64); break;
+    case 96: CALL(96); break;
+    case 128: CALL(128); break;
+    default: return -1;
+  }
+#undef CALL
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int mha_bwd(const BertMhaArgs& a, hipStream_t st) {
+  const dim3 grid(a.S * a.nh);
+#define CALL(LP)                                                                                              \
+  hipLaunchKernelGGL(mha_bwd_kernel<LP>, grid, dim3(256), 0, st, (const unsigned short*)a.qkv,               \
+                     (const unsigned short*)a.ctx, (const unsigned short*)a.dctx, a.lse, a.inst, a.mask, a.S, \
+                     a.L, a.nh, (unsigned short*)a.dqkv, a.salt, a.thr, a.inv_kp, a.drop)
+  switch (mha_lp(a.L)) {
+    case 32: CALL(32); break;
+    case 64: CALL(64); break;
+    case 96: CALL(96); break;
+    case 128: CALL(128); break;
+    default: return -1;
+  }
+#undef CALL
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace ina

@@ -213,6 +213,9 @@ template <int H>
 static int rt_fwd_t(const float* e, const float* Ws, int E, int N, int K, int Q, int R, float* cls, int blocks,
                     hipStream_t st) {
   const size_t lds = routing_lds_bytes(N, K, H, R, false);
+  if (lds > 64 * 1024)   // large N*K (e.g. 10-way 5-shot at H=64): opt in to the full 160 KB LDS
+    (void)hipFuncSetAttribute((const void*)routing_fwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
   hipLaunchKernelGGL((routing_fwd_kernel<H>), dim3(blocks), dim3(64), lds, st, e, Ws, E, N, K, Q, R, cls);
   INA_CHECK_LAUNCH();
   return 0;
@@ -221,6 +224,9 @@ template <int H>
 static int rt_bwd_t(const float* e, const float* Ws, int E, int N, int K, int Q, int R, const float* dcls, float* de,
                     float* slab, int blocks, hipStream_t st) {
   const size_t lds = routing_lds_bytes(N, K, H, R, true);
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)routing_bwd_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
   hipLaunchKernelGGL((routing_bwd_kernel<H>), dim3(blocks), dim3(64), lds, st, e, Ws, E, N, K, Q, R, dcls, de, slab);
   INA_CHECK_LAUNCH();
   return 0;

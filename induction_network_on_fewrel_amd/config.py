@@ -63,6 +63,13 @@ class Config:
     bert_intermediate: int = 3072
     bert_vocab: int = 30522
     bert_max_position: int = 512
+    bert_max_length: int = 128         # tokens per sentence incl. [CLS]/[SEP]/entity markers
+    bert_pool: str = "entity"          # "entity": concat([E1], [E2]) states | "cls"
+    bert_out_dim: int = 64             # sentence-vector width fed to routing / NTN (fused kernels: 16/40/64)
+    bert_dropout: float = 0.1          # hidden dropout (embeddings, attention output, FFN output)
+    bert_attn_dropout: float = 0.1     # attention-probability dropout
+    bert_vocab_file: str = ""          # WordPiece vocab.txt; empty = word-level vocab from the data
+    bert_checkpoint: str = ""          # local HF checkpoint dir (model.safetensors / pytorch_model.bin)
 
     # ---------------- optimisation (model/base.py:94-99) ----------------
     optimizer: str = "adam"            # "adam" (reference) | "adagrad" (paper 4.4)
@@ -145,6 +152,13 @@ class Config:
             raise ValueError(f"unknown optimizer {self.optimizer}")
         if self.encoder not in ("bilstm", "bert"):
             raise ValueError(f"unknown encoder {self.encoder}")
+        if self.encoder == "bert":
+            if self.bert_hidden % self.bert_heads != 0 or self.bert_hidden // self.bert_heads != 64:
+                raise ValueError("BERT heads must be 64 wide (bert_hidden = 64 * bert_heads)")
+            if self.bert_pool not in ("entity", "cls"):
+                raise ValueError(f"unknown bert_pool {self.bert_pool}")
+            if self.bert_max_length > min(128, self.bert_max_position):
+                raise ValueError("bert_max_length must be <= 128 (fused attention keeps the sequence in LDS)")
 
 
 def add_cli_args(p) -> None:

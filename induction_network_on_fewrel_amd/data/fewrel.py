@@ -47,6 +47,8 @@ class FewRelDataset:
         self.word2id = word2id
         self.name = name
         self.max_length = int(self.data_word.shape[1])
+        # optional BERT input features (data/bert_tokenize.py): ids / mask / e1 / e2 / length
+        self.bert: Optional[Dict[str, np.ndarray]] = None
 
     # ------------------------------------------------------------------ info
     @property
@@ -73,9 +75,12 @@ class FewRelDataset:
             scope[r] = [i, i + (e - b)]
             i += e - b
         idx = np.concatenate(idx)
-        return FewRelDataset(self.data_word[idx], self.data_pos1[idx], self.data_pos2[idx],
-                             self.data_mask[idx], self.data_length[idx], scope,
-                             self.word_vec_mat, self.word2id, name or self.name)
+        out = FewRelDataset(self.data_word[idx], self.data_pos1[idx], self.data_pos2[idx],
+                            self.data_mask[idx], self.data_length[idx], scope,
+                            self.word_vec_mat, self.word2id, name or self.name)
+        if self.bert is not None:
+            out.bert = {k: v[idx] for k, v in self.bert.items()}
+        return out
 
     # -------------------------------------------------------------- tensorise
     @staticmethod

@@ -1,0 +1,168 @@
+"""BERT sentence encoder for the Induction Network (north-star addition).
+
+The reference has no BERT (its encoder is the BiLSTM of model/graph.py:30-53); this module adds the
+"FewRel 10-way 5-shot with BERT-base encoder" configuration of BASELINE.json.  Architecture =
+BERT (post-LN transformer, GELU FFN) with HuggingFace parameter names and layouts (Linear weights
+``[out, in]``), so a local HF checkpoint directory can be loaded by name (``load_hf_state``).
+The sentence vector is pooled at the entity-start markers (concat of the [E1] and [E2] states) or
+at [CLS], then projected to ``bert_out_dim`` -- the width the induction (routing) and relation
+(NTN) heads run at (their fused kernels are instantiated for H in {16, 40, 64}).
+
+This file holds the parameter table and the pure-PyTorch oracle (CPU path + kernel tests).  The
+GPU path (ops/bert.py) runs the same math on hand-written gfx950 kernels (fused attention,
+residual+dropout+LayerNorm, bias+GELU, embedding+LayerNorm) and hipBLASLt GEMMs.
+
+Dropout uses the counter hash of models/reference.py (bit-identical to the kernels):
+stream 16 = embedding output, 17 + 3*layer + {0: attention probs, 1: attention output,
+2: FFN output}.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+from typing import Dict, List, Tuple
+
+import torch
+
+from .reference import _M32
+
+LN_EPS = 1e-12
+
+
+def param_specs(cfg) -> "OrderedDict[str, Tuple[tuple, str]]":
+    """HF name -> (shape, init) in flat-buffer order.  q/k/v weights (and biases) are adjacent so the
+    flat bf16 copy exposes them as one [3*Hd, Hd] QKV matrix without a concat."""
+    Hd, I, P = cfg.bert_hidden, cfg.bert_intermediate, cfg.bert_max_position
+    V = cfg.bert_vocab
+    sp = OrderedDict()
+    e = "bert.embeddings."
+    sp[e + "word_embeddings.weight"] = ((V, Hd), "normal")
+    sp[e + "position_embeddings.weight"] = ((P, Hd), "normal")
+    sp[e + "token_type_embeddings.weight"] = ((2, Hd), "normal")
+    sp[e + "LayerNorm.weight"] = ((Hd,), "ones")
+    sp[e + "LayerNorm.bias"] = ((Hd,), "zeros")
+    for i in range(cfg.bert_layers):
+        p = f"bert.encoder.layer.{i}."
+        for n in ("query", "key", "value"):
+            sp[p + f"attention.self.{n}.weight"] = ((Hd, Hd), "normal")
+        for n in ("query", "key", "value"):
+            sp[p + f"attention.self.{n}.bias"] = ((Hd,), "zeros")
+        sp[p + "attention.output.dense.weight"] = ((Hd, Hd), "normal")
+        sp[p + "attention.output.dense.bias"] = ((Hd,), "zeros")
+        sp[p + "attention.output.LayerNorm.weight"] = ((Hd,), "ones")
+        sp[p + "attention.output.LayerNorm.bias"] = ((Hd,), "zeros")
+        sp[p + "intermediate.dense.weight"] = ((I, Hd), "normal")
+        sp[p + "intermediate.dense.bias"] = ((I,), "zeros")
+        sp[p + "output.dense.weight"] = ((Hd, I), "normal")
+        sp[p + "output.dense.bias"] = ((Hd,), "zeros")
+        sp[p + "output.LayerNorm.weight"] = ((Hd,), "ones")
+        sp[p + "output.LayerNorm.bias"] = ((Hd,), "zeros")
+    pool = 2 * Hd if cfg.bert_pool == "entity" else Hd
+    sp["bert_proj/kernel"] = ((pool, cfg.bert_out_dim), "glorot")
+    sp["bert_proj/bias"] = ((cfg.bert_out_dim,), "zeros")
+    return sp
+
+
+def attr_of(name: str) -> str:
+    return "bert__" + name.replace(".", "__").replace("/", "__")
+
+
+def init_tensor(shape, kind: str, gen: torch.Generator) -> torch.Tensor:
+    if kind == "normal":
+        return torch.randn(shape, generator=gen) * 0.02
+    if kind == "ones":
+        return torch.ones(shape)
+    if kind == "zeros":
+        return torch.zeros(shape)
+    if kind == "glorot":
+        lim = math.sqrt(6.0 / (shape[0] + shape[1]))
+        return (torch.rand(shape, generator=gen) * 2 - 1) * lim
+    raise ValueError(kind)
+
+
+# ------------------------------------------------------------------ dropout (hash shared with HIP)
+def keep_mask(seed: int, stream: int, numel: int, keep_prob: float, device=None) -> torch.Tensor:
+    """Bernoulli(keep_prob) float mask over flat indices 0..numel-1 (idx taken mod 2^32)."""
+    idx = torch.arange(numel, dtype=torch.int64, device=device) & _M32
+    salt = ((seed & 0x7FFFFFFF) * 0x2545F491 + stream * 0x3C6EF372 + 0x1234567) & _M32
+    x = ((idx * 0x6C8E9CF5) & _M32) + salt
+    x = x & _M32
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    thr = min(int(keep_prob * 4294967296.0), 0xFFFFFFFF)
+    return (x < thr).to(torch.float32)
+
+
+def _dropout(x: torch.Tensor, seed: int, stream: int, p: float, training: bool) -> torch.Tensor:
+    if not training or p <= 0.0:
+        return x
+    kp = 1.0 - p
+    m = keep_mask(seed, stream, x.numel(), kp, x.device).view_as(x)
+    return x * m / kp
+
+
+# ------------------------------------------------------------------ oracle layers
+def gelu(x: torch.Tensor) -> torch.Tensor:
+    return 0.5 * x * (1.0 + torch.erf(x / math.sqrt(2.0)))
+
+
+def layer_norm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    mu = x.mean(-1, keepdim=True)
+    var = ((x - mu) ** 2).mean(-1, keepdim=True)
+    return (x - mu) / torch.sqrt(var + LN_EPS) * g + b
+
+
+def attention(q, k, v, mask, nh: int, seed: int, stream: int, p: float, training: bool):
+    """q/k/v [S, L, Hd]; mask [S, L] (1 = real key).  Dropout index ((s*nh+h)*L + i)*L + j."""
+    S, L, Hd = q.shape
+    d = Hd // nh
+    qh = q.view(S, L, nh, d).transpose(1, 2)
+    kh = k.view(S, L, nh, d).transpose(1, 2)
+    vh = v.view(S, L, nh, d).transpose(1, 2)
+    sc = qh @ kh.transpose(-1, -2) / math.sqrt(d)
+    sc = sc.masked_fill(mask[:, None, None, :] == 0, float("-inf"))
+    pr = torch.softmax(sc, -1)
+    pr = _dropout(pr, seed, stream, p, training)
+    return (pr @ vh).transpose(1, 2).reshape(S, L, Hd)
+
+
+def encode_ref(p: Dict[str, torch.Tensor], ids, mask, e1, e2, cfg, training: bool = False,
+               seed: int = 0) -> torch.Tensor:
+    """Pure-PyTorch BERT encoder + pooling + projection -> [S, bert_out_dim] (fp32)."""
+    S, L = ids.shape
+    pd, ad = cfg.bert_dropout, cfg.bert_attn_dropout
+    e = "bert.embeddings."
+    x = (p[e + "word_embeddings.weight"][ids.long()] + p[e + "position_embeddings.weight"][:L][None]
+         + p[e + "token_type_embeddings.weight"][0][None, None])
+    x = layer_norm(x, p[e + "LayerNorm.weight"], p[e + "LayerNorm.bias"])
+    x = _dropout(x, seed, 16, pd, training)
+    for i in range(cfg.bert_layers):
+        pre = f"bert.encoder.layer.{i}."
+        a = pre + "attention."
+        q = x @ p[a + "self.query.weight"].t() + p[a + "self.query.bias"]
+        k = x @ p[a + "self.key.weight"].t() + p[a + "self.key.bias"]
+        v = x @ p[a + "self.value.weight"].t() + p[a + "self.value.bias"]
+        c = attention(q, k, v, mask, cfg.bert_heads, seed, 17 + 3 * i, ad, training)
+        o = c @ p[a + "output.dense.weight"].t() + p[a + "output.dense.bias"]
+        o = _dropout(o, seed, 18 + 3 * i, pd, training)
+        x = layer_norm(x + o, p[a + "output.LayerNorm.weight"], p[a + "output.LayerNorm.bias"])
+        h = gelu(x @ p[pre + "intermediate.dense.weight"].t() + p[pre + "intermediate.dense.bias"])
+        o = h @ p[pre + "output.dense.weight"].t() + p[pre + "output.dense.bias"]
+        o = _dropout(o, seed, 19 + 3 * i, pd, training)
+        x = layer_norm(x + o, p[pre + "output.LayerNorm.weight"], p[pre + "output.LayerNorm.bias"])
+    return pool_project(p, x, e1, e2, cfg.bert_pool)
+
+
+def pool_project(p, x, e1, e2, pool: str) -> torch.Tensor:
+    S = x.shape[0]
+    ar = torch.arange(S, device=x.device)
+    if pool == "entity":
+        v = torch.cat([x[ar, e1.long()], x[ar, e2.long()]], -1)
+    else:
+        v = x[:, 0]
+    return v.float() @ p["bert_proj/kernel"].float() + p["bert_proj/bias"].float()
+
+
+def hf_names(cfg) -> List[str]:
+    return [n for n in param_specs(cfg) if n.startswith("bert.")]

@@ -18,7 +18,7 @@ from torch import nn
 
 from ..config import Config
 from . import reference as ref
-from .params import TF_NAMES, InductionParams
+from .params import InductionParams
 
 GPU_SUPPORTED_U = (8, 20, 32)
 
@@ -33,7 +33,11 @@ class InductionNetwork(nn.Module):
 
     # ------------------------------------------------------------------
     def pdict(self) -> Dict[str, torch.Tensor]:
-        return {a: getattr(self.params, a) for a in TF_NAMES}
+        return {a: getattr(self.params, a) for a in self.params.names()}
+
+    def bert_pdict(self) -> Dict[str, torch.Tensor]:
+        """HF name -> tensor view of the BERT encoder + projection parameters."""
+        return {n: getattr(self.params, a) for a, n in self.params.names().items() if a.startswith("bert__")}
 
     def check_gpu_config(self, N: int, Q: int, L: int) -> None:
         u = self.cfg.hidden_size
@@ -59,6 +63,8 @@ class InductionNetwork(nn.Module):
         if self.cfg.relation_head == "reference" and p["ntn_w"].shape[1] != N:
             raise ValueError(f"reference relation head was built for N={p['ntn_w'].shape[1]}, got N={N} "
                              "(use relation_head='paper' for N-independent scoring)")
+        if cfg.encoder == "bert":
+            return self._forward_bert(inst, data, B, N, K, Q, training, dropout_seed, grad_views, p)
         if inst.is_cuda:
             from ..ops.encoder import encode
             from ..ops.head import head
@@ -75,6 +81,26 @@ class InductionNetwork(nn.Module):
         probs, alphas = ref.forward(p, word, pos1, pos2, mask, B, N, K, Q, cfg.routing_iters, cfg.relation_head,
                                     kp, int(dropout_seed), bf16=False)
         return probs, alphas.squeeze(-1)
+
+    def _forward_bert(self, inst, data, B, N, K, Q, training, dropout_seed, grad_views, p):
+        """BERT encoder (data = (ids, mask, e1, e2) [NI, Lb] int32) + the same induction/relation head.
+        Returns probs and the [CLS]-row attention-free placeholder alphas (None)."""
+        cfg = self.cfg
+        if inst.is_cuda:
+            from ..ops.bert import bert_encode
+            from ..ops.head import head
+            e = bert_encode(self, inst, data, training, int(dropout_seed), grad_views)
+            H = e.shape[1]
+            if H not in (16, 40, 64) or N > 16 or N * Q > 64:
+                raise NotImplementedError("GPU head kernels support H in {16,40,64}, N <= 16, N*Q <= 64")
+            probs = head(e, p, dict(E=B, N=N, K=K, Q=Q, iters=cfg.routing_iters,
+                                    paper=(cfg.relation_head == "paper"), grad_views=grad_views))
+            return probs, None
+        from . import bert as Bm
+        ids, mask, e1, e2 = (t[inst.long()] for t in data)
+        e = Bm.encode_ref(self.bert_pdict(), ids, mask, e1, e2, cfg, training, int(dropout_seed))
+        probs = ref.head_forward(p, e, B, N, K, Q, cfg.routing_iters, cfg.relation_head)
+        return probs, None
 
     # ------------------------------------------------------------------
     def loss(self, probs: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:

@@ -102,36 +102,52 @@ class InductionParams(nn.Module):
         super().__init__()
         self.cfg = cfg
         gen = torch.Generator().manual_seed(seed)
-        L, u, pd = cfg.max_length, cfg.hidden_size, cfg.pos_embedding_dim
-        H = 2 * u
         h = cfg.ntn_slices
         N = cfg.N
-        if word_vec_mat is not None:
-            wv = torch.as_tensor(np.asarray(word_vec_mat, dtype=np.float32))
-            self.pretrained = True
-            if cfg.train_word_embedding:
-                self.word_embedding = nn.Parameter(wv.clone())
-            else:
-                self.register_buffer("word_embedding", wv.clone())
+        # attr -> checkpoint name, in flat-buffer order
+        self._names: "OrderedDict[str, str]" = OrderedDict()
+        self.pretrained = False
+        if cfg.encoder == "bert":
+            from . import bert as B
+            for name, (shape, kind) in B.param_specs(cfg).items():
+                a = B.attr_of(name)
+                setattr(self, a, nn.Parameter(B.init_tensor(shape, kind, gen)))
+                self._names[a] = name
+            H = cfg.bert_out_dim
+            self.word_dim = cfg.bert_hidden
+            self.input_dim = cfg.bert_hidden
         else:
-            if vocab_size is None:
-                raise ValueError("need word_vec_mat or vocab_size")
-            self.pretrained = False
-            self.word_embedding = nn.Parameter(normal_(torch.empty(vocab_size, cfg.synthetic_word_dim), gen,
-                                                       cfg.init_std))
-        E = self.word_embedding.shape[1]
-        self.word_dim = E
-        D = E + 2 * pd
-        self.input_dim = D
-        self.pos1_embedding = nn.Parameter(normal_(torch.empty(2 * L, pd), gen, cfg.init_std))
-        self.pos2_embedding = nn.Parameter(normal_(torch.empty(2 * L, pd), gen, cfg.init_std))
-        self.lstm_fw_kernel = nn.Parameter(glorot_uniform_(torch.empty(D + u, 4 * u), gen))
-        self.lstm_fw_bias = nn.Parameter(torch.zeros(4 * u))
-        self.lstm_bw_kernel = nn.Parameter(glorot_uniform_(torch.empty(D + u, 4 * u), gen))
-        self.lstm_bw_bias = nn.Parameter(torch.zeros(4 * u))
-        self.attn_kernel = nn.Parameter(glorot_uniform_(torch.empty(H, H), gen))
-        self.attn_bias = nn.Parameter(torch.zeros(H))
-        self.attn_w2 = nn.Parameter(glorot_normal_(torch.empty(H, 1), gen))
+            L, u, pd = cfg.max_length, cfg.hidden_size, cfg.pos_embedding_dim
+            H = 2 * u
+            if word_vec_mat is not None:
+                wv = torch.as_tensor(np.asarray(word_vec_mat, dtype=np.float32))
+                self.pretrained = True
+                if cfg.train_word_embedding:
+                    self.word_embedding = nn.Parameter(wv.clone())
+                else:
+                    self.register_buffer("word_embedding", wv.clone())
+            else:
+                if vocab_size is None:
+                    raise ValueError("need word_vec_mat or vocab_size")
+                self.word_embedding = nn.Parameter(normal_(torch.empty(vocab_size, cfg.synthetic_word_dim), gen,
+                                                           cfg.init_std))
+            E = self.word_embedding.shape[1]
+            self.word_dim = E
+            D = E + 2 * pd
+            self.input_dim = D
+            self.pos1_embedding = nn.Parameter(normal_(torch.empty(2 * L, pd), gen, cfg.init_std))
+            self.pos2_embedding = nn.Parameter(normal_(torch.empty(2 * L, pd), gen, cfg.init_std))
+            self.lstm_fw_kernel = nn.Parameter(glorot_uniform_(torch.empty(D + u, 4 * u), gen))
+            self.lstm_fw_bias = nn.Parameter(torch.zeros(4 * u))
+            self.lstm_bw_kernel = nn.Parameter(glorot_uniform_(torch.empty(D + u, 4 * u), gen))
+            self.lstm_bw_bias = nn.Parameter(torch.zeros(4 * u))
+            self.attn_kernel = nn.Parameter(glorot_uniform_(torch.empty(H, H), gen))
+            self.attn_bias = nn.Parameter(torch.zeros(H))
+            self.attn_w2 = nn.Parameter(glorot_normal_(torch.empty(H, 1), gen))
+            for a in list(TF_NAMES)[:10]:
+                self._names[a] = ("embedding/Variable" if self.pretrained else "word_embedding") \
+                    if a == "word_embedding" else TF_NAMES[a]
+        self.head_dim = H
         self.W_s = nn.Parameter(glorot_normal_(torch.empty(H, H), gen))
         self.M = nn.Parameter(glorot_normal_(torch.empty(H, H, h), gen))
         if cfg.relation_head == "reference":
@@ -140,23 +156,26 @@ class InductionParams(nn.Module):
         else:
             self.ntn_w = nn.Parameter(glorot_normal_(torch.empty(h, 1), gen))
             self.ntn_b = nn.Parameter(glorot_normal_(torch.empty(1), gen))
+        for a in ("W_s", "M", "ntn_w", "ntn_b"):
+            self._names[a] = TF_NAMES[a]
 
     # ------------------------------------------------------------ naming
+    def names(self) -> "OrderedDict[str, str]":
+        """attr -> checkpoint name (TF1 names for the BiLSTM model, HF names for BERT)."""
+        return self._names
+
     def tf_name(self, attr: str) -> str:
-        if attr == "word_embedding":
-            return "embedding/Variable" if self.pretrained else "word_embedding"
-        return TF_NAMES[attr]
+        return self._names[attr]
 
     def tf_state(self) -> "OrderedDict[str, torch.Tensor]":
         out = OrderedDict()
-        for attr in TF_NAMES:
-            out[self.tf_name(attr)] = getattr(self, attr).detach()
+        for attr, name in self._names.items():
+            out[name] = getattr(self, attr).detach()
         return out
 
     def load_tf_state(self, state: Dict[str, torch.Tensor], strict: bool = True) -> None:
         with torch.no_grad():
-            for attr in TF_NAMES:
-                name = self.tf_name(attr)
+            for attr, name in self._names.items():
                 if name not in state:
                     if strict:
                         raise KeyError(f"missing {name} in checkpoint")
@@ -170,7 +189,7 @@ class InductionParams(nn.Module):
     def trainable(self) -> "OrderedDict[str, nn.Parameter]":
         """Ordered (attr -> Parameter) of trainable tensors (the flat-buffer order)."""
         out = OrderedDict()
-        for attr in TF_NAMES:
+        for attr in self._names:
             t = getattr(self, attr)
             if isinstance(t, nn.Parameter) and t.requires_grad:
                 out[attr] = t
@@ -183,7 +202,8 @@ class InductionParams(nn.Module):
         out = []
         for a, p in self.trainable().items():
             n = self.tf_name(a)
-            if "bias" in n or "word_embedding" in n or "pos1_embedding" in n or "pos2_embedding" in n:
+            if ("bias" in n or "word_embedding" in n or "pos1_embedding" in n or "pos2_embedding" in n
+                    or "embeddings" in n or "LayerNorm" in n):
                 continue
             out.append(p)
         return out

@@ -187,10 +187,15 @@ def forward(p: Dict[str, torch.Tensor], word, pos1, pos2, mask, B: int, N: int, 
             bf16: bool = False):
     """Episode batch forward. Row layout per episode: [support N*K ; query N*Q]."""
     e, alphas = encode(p, word, pos1, pos2, mask, keep_prob, dropout_seed, bf16)
+    return head_forward(p, e, B, N, K, Q, routing_iters, head, bf16), alphas
+
+
+def head_forward(p: Dict[str, torch.Tensor], e, B: int, N: int, K: int, Q: int, routing_iters: int = 3,
+                 head: str = "reference", bf16: bool = False):
+    """Routing + relation head over sentence vectors e [B*(N*K+N*Q), H] -> probs [B, N*Q, N]."""
     H = e.shape[-1]
     e = e.view(B, N * K + N * Q, H)
     sup = e[:, : N * K].reshape(B, N, K, H)
     qry = e[:, N * K:]
     cls = dynamic_routing(sup, p["W_s"], routing_iters)
-    probs = relation_probs(cls, qry, p["M"], p["ntn_w"], p["ntn_b"], head, bf16)
-    return probs, alphas
+    return relation_probs(cls, qry, p["M"], p["ntn_w"], p["ntn_b"], head, bf16)

@@ -1,0 +1,229 @@
+"""BERT encoder on the GPU path: hand-written gfx950 kernels + hipBLASLt GEMMs (bf16).
+
+Per layer (post-LN BERT, models/bert.py is the oracle):
+    qkv = x Wqkv^T + bqkv            torch.addmm (bf16 -> hipBLASLt); Wqkv is ONE [3Hd, Hd] view of the
+                                     flat bf16 weight copy (q/k/v are adjacent in the flat buffer)
+    ctx = MHA(qkv)                   ina.bert_mha_fwd / _bwd   (fused, sequence in LDS, MFMA)
+    x1  = LN(x + drop(ctx Wo^T+bo))  addmm + ina.bert_ln_res_fwd / _bwd
+    h   = gelu(x1 W1^T + b1)         mm + ina.bert_bias_gelu_fwd / _bwd
+    x2  = LN(x1 + drop(h W2^T+b2))   addmm + ina.bert_ln_res_fwd / _bwd
+Embeddings: ina.bert_embed_ln_fwd / _bwd (gather by instance index, no host copies); the word-table
+gradient is scattered with index_add_ straight into the flat gradient buffer.
+
+Weights: the encoder layers' fp32 masters are cast to bf16 ONCE per step as one contiguous region of
+the flat parameter buffer (``_CastRegion``); its backward adds the bf16 weight gradients into the
+matching region of the flat gradient buffer.  LayerNorm / GELU-bias / embedding tables stay fp32.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+
+from ._ext import ops
+from .encoder import _route_grad
+
+
+def _contiguous_region(ts: List[torch.Tensor]) -> Optional[torch.Tensor]:
+    """A 1-D view spanning ts if they are back-to-back in one storage (flat buffer), else None."""
+    base = ts[0]
+    off = base.storage_offset()
+    total = 0
+    for t in ts:
+        if (t.untyped_storage().data_ptr() != base.untyped_storage().data_ptr() or t.storage_offset() != off + total
+                or not t.is_contiguous()):
+            return None
+        total += t.numel()
+    return torch.as_strided(base.detach(), (total,), (1,), off)
+
+
+class _CastRegion(torch.autograd.Function):
+    """bf16 copy of a list of fp32 params as one flat tensor.  Backward: add into the flat gradient
+    region (trainer path) or return per-parameter slices (plain autograd)."""
+
+    @staticmethod
+    def forward(ctx, region, grad_region, shapes, *params):
+        ctx.grad_region = grad_region
+        ctx.shapes = shapes
+        src = region if region is not None else torch.cat([p.detach().reshape(-1) for p in params])
+        return src.to(torch.bfloat16)
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.grad_region is not None:
+            ctx.grad_region.add_(g.float())
+            return (None, None, None) + (None,) * len(ctx.shapes)
+        out, o = [], 0
+        for shp in ctx.shapes:
+            n = 1
+            for d in shp:
+                n *= d
+            out.append(g[o:o + n].float().view(shp))
+            o += n
+        return (None, None, None) + tuple(out)
+
+
+class _Embed(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, inst, ids, wemb, pemb, temb, gamma, beta, seed, p, meta):
+        y, stats = ops().bert_embed_ln_fwd(inst, ids, wemb.detach(), pemb.detach(), temb.detach(), gamma.detach(),
+                                           beta.detach(), seed, p)
+        ctx.save_for_backward(inst, ids, wemb, pemb, temb, gamma, stats)
+        ctx.cfg = (seed, p, meta)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        inst, ids, wemb, pemb, temb, gamma, stats = ctx.saved_tensors
+        seed, p, meta = ctx.cfg
+        dx, slab = ops().bert_embed_ln_bwd(dy.contiguous(), inst, ids, wemb.detach(), pemb.detach(), temb.detach(),
+                                           gamma.detach(), stats, seed, p, 0)
+        S, L = inst.shape[0], ids.shape[1]
+        HD = wemb.shape[1]
+        rows = ids[inst.long()].reshape(-1).long()
+        names = meta["names"]
+        views = meta.get("grad_views")
+        if views is not None and names["word"] in views:
+            views[names["word"]].index_add_(0, rows, dx)
+            dw = None
+        else:
+            dw = torch.zeros_like(wemb).index_add_(0, rows, dx) if wemb.requires_grad else None
+        dpos_L = dx.view(S, L, HD).sum(0)
+        dpos = torch.zeros_like(pemb)
+        dpos[:L] = dpos_L
+        dtype = torch.zeros_like(temb)
+        dtype[0] = dpos_L.sum(0)
+        sl = slab.sum(0)
+        return (None, None, dw, _route_grad(meta, names["pos"], dpos), _route_grad(meta, names["type"], dtype),
+                _route_grad(meta, names["gamma"], sl[0]), _route_grad(meta, names["beta"], sl[1]), None, None, None)
+
+
+class _LnRes(torch.autograd.Function):
+    """y = LN(res + dropout(a))."""
+
+    @staticmethod
+    def forward(ctx, a, res, gamma, beta, seed, stream, p, meta, gname, bname):
+        y, stats = ops().bert_ln_res_fwd(a.contiguous(), res.contiguous(), gamma.detach(), beta.detach(), seed,
+                                         stream, p)
+        ctx.save_for_backward(a, res, gamma, stats)
+        ctx.cfg = (seed, stream, p, meta, gname, bname)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        a, res, gamma, stats = ctx.saved_tensors
+        seed, stream, p, meta, gname, bname = ctx.cfg
+        dres, da, slab = ops().bert_ln_res_bwd(dy.contiguous(), a.contiguous(), res.contiguous(), gamma.detach(),
+                                               stats, seed, stream, p, 0)
+        sl = slab.sum(0)
+        return (da, dres, _route_grad(meta, gname, sl[0]), _route_grad(meta, bname, sl[1]), None, None, None, None,
+                None, None)
+
+
+class _BiasGelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, b, meta, bname):
+        y = ops().bert_bias_gelu_fwd(x.contiguous(), b.detach())
+        ctx.save_for_backward(x, b)
+        ctx.cfg = (meta, bname)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, b = ctx.saved_tensors
+        meta, bname = ctx.cfg
+        dx, slab = ops().bert_bias_gelu_bwd(dy.contiguous(), x, b.detach(), 0)
+        return dx, _route_grad(meta, bname, slab.sum(0)), None, None
+
+
+class _Mha(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, inst, mask, L, nh, seed, stream, p):
+        qkv = qkv.contiguous()
+        out, lse = ops().bert_mha_fwd(qkv, inst, mask, L, nh, seed, stream, p)
+        ctx.save_for_backward(qkv, out, lse, inst, mask)
+        ctx.cfg = (L, nh, seed, stream, p)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse, inst, mask = ctx.saved_tensors
+        L, nh, seed, stream, p = ctx.cfg
+        dqkv = ops().bert_mha_bwd(qkv, out, dout.contiguous(), lse, inst, mask, L, nh, seed, stream, p)
+        return dqkv, None, None, None, None, None, None, None
+
+
+def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
+                grad_views: Optional[Dict[str, torch.Tensor]] = None) -> torch.Tensor:
+    """GPU BERT encoder + pooling + projection -> sentence vectors [S, bert_out_dim] fp32."""
+    cfg = model.cfg
+    ids, mask, e1, e2 = data
+    prm = model.params
+    names = prm.names()                      # attr -> HF name
+    by_name = {n: a for a, n in names.items()}
+    P = lambda n: getattr(prm, by_name[n])  # noqa: E731
+    S, L = inst.shape[0], ids.shape[1]
+    Hd, nh, nl = cfg.bert_hidden, cfg.bert_heads, cfg.bert_layers
+    pd = cfg.bert_dropout if training else 0.0
+    pa = cfg.bert_attn_dropout if training else 0.0
+    seed = int(seed) & 0x7FFFFFFF
+    meta = {"grad_views": grad_views}
+    # ---- bf16 weight region: all encoder layers (contiguous in the flat buffer)
+    layer_names = [n for n in names.values() if n.startswith("bert.encoder.layer.")]
+    lparams = [P(n) for n in layer_names]
+    region = _contiguous_region(lparams)
+    grad_region = None
+    if region is not None and grad_views is not None:
+        g0 = grad_views.get(by_name[layer_names[0]])
+        if g0 is not None:
+            grad_region = torch.as_strided(g0, (region.numel(),), (1,), g0.storage_offset())
+    wb = _CastRegion.apply(region, grad_region, [tuple(p.shape) for p in lparams], *lparams)
+    offs, o = {}, 0
+    for n, p in zip(layer_names, lparams):
+        offs[n] = (o, p.numel(), tuple(p.shape))
+        o += p.numel()
+
+    def W(n):
+        off, cnt, shp = offs[n]
+        return wb.narrow(0, off, cnt).view(shp)
+
+    def span(n0, count_names):
+        off = offs[n0][0]
+        cnt = sum(offs[m][1] for m in count_names)
+        return wb.narrow(0, off, cnt)
+
+    # ---- embeddings
+    e = "bert.embeddings."
+    emb_names = {"word": by_name[e + "word_embeddings.weight"], "pos": by_name[e + "position_embeddings.weight"],
+                 "type": by_name[e + "token_type_embeddings.weight"], "gamma": by_name[e + "LayerNorm.weight"],
+                 "beta": by_name[e + "LayerNorm.bias"]}
+    x = _Embed.apply(inst, ids, P(e + "word_embeddings.weight"), P(e + "position_embeddings.weight"),
+                     P(e + "token_type_embeddings.weight"), P(e + "LayerNorm.weight"), P(e + "LayerNorm.bias"),
+                     seed, pd, dict(meta, names=emb_names))
+    # ---- layers
+    for i in range(nl):
+        pre = f"bert.encoder.layer.{i}."
+        a = pre + "attention."
+        qn = [a + f"self.{k}.weight" for k in ("query", "key", "value")]
+        bn = [a + f"self.{k}.bias" for k in ("query", "key", "value")]
+        Wqkv = span(qn[0], qn).view(3 * Hd, Hd)
+        bqkv = span(bn[0], bn)
+        qkv = torch.addmm(bqkv, x, Wqkv.t())
+        ctx = _Mha.apply(qkv, inst, mask, L, nh, seed, 17 + 3 * i, pa)
+        o = torch.addmm(W(a + "output.dense.bias"), ctx, W(a + "output.dense.weight").t())
+        x = _LnRes.apply(o, x, P(a + "output.LayerNorm.weight"), P(a + "output.LayerNorm.bias"), seed, 18 + 3 * i, pd,
+                         meta, by_name[a + "output.LayerNorm.weight"], by_name[a + "output.LayerNorm.bias"])
+        hpre = torch.mm(x, W(pre + "intermediate.dense.weight").t())
+        h = _BiasGelu.apply(hpre, P(pre + "intermediate.dense.bias"), meta, by_name[pre + "intermediate.dense.bias"])
+        o = torch.addmm(W(pre + "output.dense.bias"), h, W(pre + "output.dense.weight").t())
+        x = _LnRes.apply(o, x, P(pre + "output.LayerNorm.weight"), P(pre + "output.LayerNorm.bias"), seed, 19 + 3 * i,
+                         pd, meta, by_name[pre + "output.LayerNorm.weight"], by_name[pre + "output.LayerNorm.bias"])
+    # ---- pooling + projection (fp32)
+    xs = x.view(S, L, Hd)
+    ar = torch.arange(S, device=x.device)
+    if cfg.bert_pool == "entity":
+        ie = inst.long()
+        v = torch.cat([xs[ar, e1[ie].long()], xs[ar, e2[ie].long()]], -1)
+    else:
+        v = xs[:, 0]
+    return torch.addmm(P("bert_proj/bias"), v.float(), P("bert_proj/kernel"))

@@ -25,8 +25,13 @@ class DeviceDataset:
         self.mask = t(data.data_mask)
         self.scopes = t(data.scope_array())
         self.L = data.max_length
+        self.bert = ({k: t(data.bert[k]) for k in ("ids", "mask", "e1", "e2")} if data.bert is not None else None)
 
-    def arrays(self):
+    def arrays(self, encoder: str = "bilstm"):
+        if encoder == "bert":
+            if self.bert is None:
+                raise ValueError("dataset has no BERT features (data/bert_tokenize.py)")
+            return self.bert["ids"], self.bert["mask"], self.bert["e1"], self.bert["e2"]
         return self.word, self.pos1, self.pos2, self.mask
 
 

@@ -34,11 +34,16 @@ from .metrics import MetricsLogger
 class _HostEpisodes:
     """CPU path: host sampler producing instance indices (same contract as the device sampler)."""
 
-    def __init__(self, data: FewRelDataset, seed: int, nota_rate: float):
+    def __init__(self, data: FewRelDataset, seed: int, nota_rate: float, encoder: str = "bilstm"):
         self.data = data
         self.s = EpisodeSampler(data, seed=seed, nota_rate=nota_rate)
-        self.arrays = tuple(torch.as_tensor(a) for a in (data.data_word, data.data_pos1, data.data_pos2,
-                                                          data.data_mask))
+        if encoder == "bert":
+            if data.bert is None:
+                raise ValueError("dataset has no BERT features (data/bert_tokenize.py)")
+            self.arrays = tuple(torch.as_tensor(data.bert[k]) for k in ("ids", "mask", "e1", "e2"))
+        else:
+            self.arrays = tuple(torch.as_tensor(a) for a in (data.data_word, data.data_pos1, data.data_pos2,
+                                                              data.data_mask))
 
     def sample(self, B, N, K, Q):
         idx, lab = self.s.next_batch_indices(B, N, K, Q)
@@ -62,6 +67,11 @@ class Trainer:
         self.device = self.dist.device
         self.train_data = train_data
         self.val_data = val_data if val_data is not None else train_data
+        if cfg.encoder == "bert":
+            from ..data.bert_tokenize import synthetic_features
+            for d in {id(self.train_data): self.train_data, id(self.val_data): self.val_data}.values():
+                if d.bert is None:   # e.g. synthetic data: fold its word ids into the BERT vocabulary
+                    d.bert = synthetic_features(d, cfg.bert_vocab, cfg.bert_max_length)
         wv = train_data.word_vec_mat
         vocab = None if wv is not None else int(max(train_data.data_word.max(), 1) + 1)
         self.model = InductionNetwork(cfg, wv, vocab_size=vocab, seed=cfg.seed).to(self.device)
@@ -91,9 +101,9 @@ class Trainer:
             from ..ops.sampler import DeviceDataset, DeviceEpisodeSampler
             dd = DeviceDataset(data, self.device)
             s = DeviceEpisodeSampler(dd, seed=seed, nota_rate=nota)
-            s.arrays = dd.arrays()
+            s.arrays = dd.arrays(self.cfg.encoder)
             return s
-        return _HostEpisodes(data, seed, nota)
+        return _HostEpisodes(data, seed, nota, self.cfg.encoder)
 
     def _sync(self):
         if self.device.type == "cuda" and self.cfg.profile:

@@ -1,0 +1,150 @@
+"""BERT gfx950 kernels vs the fp32 PyTorch oracle (models/bert.py), forward and backward."""
+import math
+
+import pytest
+import torch
+
+from induction_network_on_fewrel_amd.models import bert as B
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda")
+
+
+def _ops():
+    from induction_network_on_fewrel_amd.ops._ext import ops
+    return ops()
+
+
+def _close(a, b, rtol=3e-2):
+    """max |a - b| relative to max |b| (bf16 storage / MFMA inputs vs the fp32 oracle)."""
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err / scale < rtol, f"max err {err} vs scale {scale}"
+
+
+@pytest.mark.parametrize("HD", [256, 768])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_ln_res(HD, p):
+    torch.manual_seed(0)
+    T = 70
+    a = torch.randn(T, HD, device=dev).bfloat16()
+    res = torch.randn(T, HD, device=dev).bfloat16()
+    g = (torch.rand(HD, device=dev) + 0.5)
+    b = torch.randn(HD, device=dev) * 0.1
+    seed, stream = 11, 18
+    y, stats = _ops().bert_ln_res_fwd(a, res, g, b, seed, stream, p)
+    af, rf = a.float().requires_grad_(), res.float().requires_grad_()
+    gf, bf = g.clone().requires_grad_(), b.clone().requires_grad_()
+    ref = B.layer_norm(rf + B._dropout(af, seed, stream, p, True), gf, bf)
+    _close(y, ref)
+    dy = torch.randn(T, HD, device=dev).bfloat16()
+    ref.backward(dy.float())
+    dres, da, slab = _ops().bert_ln_res_bwd(dy, a, res, g, stats, seed, stream, p, 7)
+    _close(dres, rf.grad)
+    _close(da, af.grad)
+    sl = slab.sum(0)
+    _close(sl[0], gf.grad, rtol=1e-2)
+    _close(sl[1], bf.grad, rtol=1e-2)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_embed_ln(p):
+    torch.manual_seed(1)
+    NI, L, HD, V = 9, 20, 512, 300
+    ids = torch.randint(0, V, (NI, L), device=dev, dtype=torch.int32)
+    inst = torch.tensor([3, 0, 8, 3], device=dev, dtype=torch.int32)
+    w = torch.randn(V, HD, device=dev) * 0.1
+    pe = torch.randn(40, HD, device=dev) * 0.1
+    te = torch.randn(2, HD, device=dev) * 0.1
+    g = torch.rand(HD, device=dev) + 0.5
+    b = torch.randn(HD, device=dev) * 0.1
+    y, stats = _ops().bert_embed_ln_fwd(inst, ids, w, pe, te, g, b, 5, p)
+    rows = ids[inst.long()].long()
+    wf = w.clone().requires_grad_()
+    gf = g.clone().requires_grad_()
+    x = wf[rows] + pe[:L][None] + te[0][None, None]
+    ref = B._dropout(B.layer_norm(x, gf, b), 5, 16, p, True).reshape(-1, HD)
+    _close(y, ref)
+    dy = torch.randn(4 * L, HD, device=dev).bfloat16()
+    ref.backward(dy.float())
+    dx, slab = _ops().bert_embed_ln_bwd(dy, inst, ids, w, pe, te, g, stats, 5, p, 3)
+    dw = torch.zeros_like(w).index_add_(0, rows.reshape(-1), dx)
+    _close(dw, wf.grad)
+    _close(slab.sum(0)[0], gf.grad, rtol=1e-2)
+
+
+def test_bias_gelu():
+    torch.manual_seed(2)
+    T, I = 333, 3072
+    x = torch.randn(T, I, device=dev).bfloat16()
+    b = torch.randn(I, device=dev) * 0.3
+    y = _ops().bert_bias_gelu_fwd(x, b)
+    xf, bf = x.float().requires_grad_(), b.clone().requires_grad_()
+    ref = B.gelu(xf + bf)
+    _close(y, ref, rtol=1e-2)
+    dy = torch.randn(T, I, device=dev).bfloat16()
+    ref.backward(dy.float())
+    dx, slab = _ops().bert_bias_gelu_bwd(dy, x, b, 64)
+    _close(dx, xf.grad, rtol=1e-2)
+    _close(slab.sum(0), bf.grad, rtol=1e-2)
+
+
+@pytest.mark.parametrize("L", [20, 37, 64, 100, 128])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_mha(L, p):
+    torch.manual_seed(3)
+    S, nh = 5, 2
+    Hd = 64 * nh
+    NI = 7
+    mask_all = torch.zeros(NI, L, dtype=torch.int32, device=dev)
+    for i in range(NI):
+        mask_all[i, : max(1, L - 3 * i)] = 1
+    inst = torch.tensor([6, 0, 2, 2, 5], device=dev, dtype=torch.int32)
+    qkv = torch.randn(S * L, 3 * Hd, device=dev).bfloat16()
+    seed, stream = 9, 20
+    ctx, lse = _ops().bert_mha_fwd(qkv, inst, mask_all, L, nh, seed, stream, p)
+    qf = qkv.float().requires_grad_()
+    q, k, v = qf.view(S, L, 3, Hd).unbind(2)
+    ref = B.attention(q, k, v, mask_all[inst.long()], nh, seed, stream, p, True).reshape(S * L, Hd)
+    _close(ctx, ref)
+    dctx = torch.randn(S * L, Hd, device=dev).bfloat16()
+    ref.backward(dctx.float())
+    dqkv = _ops().bert_mha_bwd(qkv, ctx, dctx, lse, inst, mask_all, L, nh, seed, stream, p)
+    for part in range(3):
+        _close(dqkv.view(S * L, 3, Hd)[:, part], qf.grad.view(S * L, 3, Hd)[:, part])
+
+
+def test_bert_encoder_end_to_end():
+    """ops.bert.bert_encode (kernels + hipBLASLt GEMMs) vs encode_ref: forward and parameter grads."""
+    from induction_network_on_fewrel_amd.config import Config
+    from induction_network_on_fewrel_amd.models import InductionNetwork
+    from induction_network_on_fewrel_amd.ops.bert import bert_encode
+    cfg = Config(encoder="bert", bert_layers=2, bert_hidden=256, bert_heads=4, bert_intermediate=512, bert_vocab=400,
+                 bert_max_position=64, bert_max_length=40, bert_out_dim=64, bert_dropout=0.1, bert_attn_dropout=0.1)
+    torch.manual_seed(4)
+    m = InductionNetwork(cfg, None, vocab_size=10).to(dev)
+    NI, L = 12, 40
+    ids = torch.randint(9, 400, (NI, L), device=dev, dtype=torch.int32)
+    mask = torch.ones(NI, L, device=dev, dtype=torch.int32)
+    for i in range(NI):
+        mask[i, 10 + 2 * i:] = 0
+        ids[i, 10 + 2 * i:] = 0
+    e1 = torch.randint(1, 8, (NI,), device=dev, dtype=torch.int32)
+    e2 = torch.randint(1, 8, (NI,), device=dev, dtype=torch.int32)
+    inst = torch.tensor([0, 3, 5, 7, 11, 2], device=dev, dtype=torch.int32)
+    out = bert_encode(m, inst, (ids, mask, e1, e2), True, 77)
+    p = m.bert_pdict()
+    ref = B.encode_ref(p, ids[inst.long()], mask[inst.long()], e1[inst.long()], e2[inst.long()], cfg, True, 77)
+    _close(out, ref, rtol=5e-2)
+    w = torch.randn_like(ref)
+    (out * w).sum().backward()
+    got = {n: t.grad.clone() for n, t in p.items() if t.grad is not None}
+    for t in p.values():
+        t.grad = None
+    (ref * w).sum().backward()
+    for n in ("bert.encoder.layer.0.attention.self.query.weight", "bert.encoder.layer.1.output.dense.weight",
+              "bert.encoder.layer.1.output.LayerNorm.weight", "bert.embeddings.position_embeddings.weight",
+              "bert.embeddings.word_embeddings.weight", "bert.encoder.layer.0.intermediate.dense.bias"):
+        assert n in got, n
+        _close(got[n], p[n].grad, rtol=8e-2)

@@ -31,6 +31,8 @@ def build_parser():
     p.add_argument("--split_val", type=lambda s: s.lower() in ("1", "true", "yes"), default=False,
                    help="train.json is absent: split val.json's relations into disjoint train/val halves")
     p.add_argument("--eval_only", type=lambda s: s.lower() in ("1", "true", "yes"), default=False)
+    p.add_argument("--train_relations", type=int, default=0,
+                   help="with --split_val: how many of val.json's relations train (default: half)")
     p.add_argument("--vocab_from_data", type=lambda s: s.lower() in ("1", "true", "yes"), default=False,
                    help="no GloVe file: build a random word table from the data's tokens")
     return p
@@ -57,11 +59,25 @@ def load_data(cfg: Config, args):
         full = FewRelDataset.from_json(cfg.val_file, wv, cfg.max_length, cfg.case_sensitive,
                                        processed_dir=cfg.processed_dir)
         rels = full.relations()
-        half = len(rels) // 2
-        return full.subset_relations(rels[:half], "train_split"), full.subset_relations(rels[half:], "val_split")
+        half = args.train_relations or len(rels) // 2
+        tr, va = full.subset_relations(rels[:half], "train_split"), full.subset_relations(rels[half:], "val_split")
+        return _with_bert(cfg, tr, va, cfg.val_file, full, rels, half)
     tr = FewRelDataset.from_json(cfg.train_file, wv, cfg.max_length, cfg.case_sensitive, processed_dir=cfg.processed_dir)
     va = FewRelDataset.from_json(cfg.val_file, wv, cfg.max_length, cfg.case_sensitive, processed_dir=cfg.processed_dir)
+    if cfg.encoder == "bert":
+        from induction_network_on_fewrel_amd.data.bert_tokenize import features_from_json
+        tr.bert, vocab = features_from_json(cfg.train_file, cfg.bert_max_length, vocab_file=cfg.bert_vocab_file)
+        va.bert, _ = features_from_json(cfg.val_file, cfg.bert_max_length, vocab=vocab)
     return tr, va
+
+
+def _with_bert(cfg, tr, va, path, full, rels, half):
+    """BERT features for a relation split of one JSON file (same instance order as the split)."""
+    if cfg.encoder != "bert":
+        return tr, va
+    from induction_network_on_fewrel_amd.data.bert_tokenize import features_from_json
+    full.bert, _ = features_from_json(path, cfg.bert_max_length, vocab_file=cfg.bert_vocab_file)
+    return full.subset_relations(rels[:half], "train_split"), full.subset_relations(rels[half:], "val_split")
 
 
 def main(argv=None):
