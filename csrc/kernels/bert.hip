@@ -404,15 +404,26 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const unsigned short* __re
   const unsigned short* kbase = qkv + tok0 * ROW + HDm + hh * HDIM;
   const unsigned short* vbase = qkv + tok0 * ROW + 2 * HDm + hh * HDIM;
   // stage K rows and V^T (rows >= L are zero), key mask
-  for (int i = threadIdx.x; i < LP * 8; i += 256) {
-    const int k = i >> 3, c = (i & 7) * 8;
-    const bool ok = k < L;
-    const size_t off = (size_t)(ok ? k : 0) * ROW + c;
-    u16x8_t kv = ld8(kbase + off), vv = ld8(vbase + off);
-    if (!ok) kv = vv = zero8();
-    *reinterpret_cast<u16x8_t*>(&Ks[k * KSTR + c]) = kv;
+  {
+    constexpr int NU = LP * 8 / 256;
+    u16x8_t kv[NU], vv[NU];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) Vt[(c + j) * VSTR + k] = vv[j];
+    for (int u = 0; u < NU; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int k = i >> 3, c = (i & 7) * 8;
+      const size_t off = (size_t)(k < L ? k : 0) * ROW + c;
+      kv[u] = ld8(kbase + off);
+      vv[u] = ld8(vbase + off);
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int k = i >> 3, c = (i & 7) * 8;
+      if (k >= L) kv[u] = vv[u] = zero8();
+      *reinterpret_cast<u16x8_t*>(&Ks[k * KSTR + c]) = kv[u];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Vt[(c + j) * VSTR + k] = vv[u][j];
+    }
   }
   const int* mrow = mask_all + (size_t)inst[s] * L;
   for (int k = threadIdx.x; k < LP; k += 256) madd[k] = (k < L && mrow[k < L ? k : 0] > 0) ? 0.f : -INFINITY;
@@ -506,6 +517,7 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
   __shared__ __attribute__((aligned(16))) unsigned short dSl[LP * SSTR];
   __shared__ float delta[LP];
   __shared__ float madd[LP];
+  __shared__ float lsel[LP];
   unsigned short* Qt = TA;
   unsigned short* dOt = TA + HDIM * TSTR;
   unsigned short* Kt = TA;
@@ -520,28 +532,45 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
   const unsigned short* ob = ctx + tok0 * HDm + hh * HDIM;
   const unsigned short* gb = dctx + tok0 * HDm + hh * HDIM;
   const float* lrow = lse + ((size_t)s * nh + hh) * LP;
-  // phase 0: Q^T, dO^T images; delta = rowsum(dO * O); key mask
-  for (int i = threadIdx.x; i < LP * 8; i += 256) {
-    const int q = i >> 3, c = (i & 7) * 8;
-    const bool ok = q < L;
-    const size_t qo = (size_t)(ok ? q : 0) * ROW + c, oo = (size_t)(ok ? q : 0) * HDm + c;
-    u16x8_t qv = ld8(qb + qo), dv = ld8(gb + oo);
-    if (!ok) qv = dv = zero8();
+  // phase 0: Q^T, dO^T images; delta = rowsum(dO * O); key mask.  All loads of a thread are issued
+  // before any is consumed (one memory latency per phase, not one per row).
+  {
+    constexpr int NU = LP * 8 / 256;
+    u16x8_t qv[NU], dv[NU], ov[NU];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      Qt[(c + j) * TSTR + q] = qv[j];
-      dOt[(c + j) * TSTR + q] = dv[j];
+    for (int u = 0; u < NU; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int q = i >> 3, c = (i & 7) * 8;
+      const int qc = q < L ? q : 0;
+      qv[u] = ld8(qb + (size_t)qc * ROW + c);
+      dv[u] = ld8(gb + (size_t)qc * HDm + c);
+      ov[u] = ld8(ob + (size_t)qc * HDm + c);
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int q = i >> 3, c = (i & 7) * 8;
+      const bool ok = q < L;
+      float d = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d += bf2f(dv[u][j]) * bf2f(ov[u][j]);
+      d += __shfl_xor(d, 1, 64);   // the 8 chunks of row q sit on 8 consecutive lanes
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      if ((i & 7) == 0) delta[q] = ok ? d : 0.f;
+      if (!ok) qv[u] = dv[u] = zero8();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        Qt[(c + j) * TSTR + q] = qv[u][j];
+        dOt[(c + j) * TSTR + q] = dv[u][j];
+      }
     }
   }
-  for (int q = wave; q < LP; q += 4) {   // one wave per query row: 64 lanes = 64 d
-    const bool ok = q < L;
-    const size_t oo = (size_t)(ok ? q : 0) * HDm + lane;
-    float d = bf2f(gb[oo]) * bf2f(ob[oo]);
-    d = wave_sum(d);
-    if (lane == 0) delta[q] = ok ? d : 0.f;
-  }
   const int* mrow = mask_all + (size_t)inst[s] * L;
-  for (int k = threadIdx.x; k < LP; k += 256) madd[k] = (k < L && mrow[k < L ? k : 0] > 0) ? 0.f : -INFINITY;
+  for (int k = threadIdx.x; k < LP; k += 256) {
+    madd[k] = (k < L && mrow[k < L ? k : 0] > 0) ? 0.f : -INFINITY;
+    lsel[k] = lrow[k];
+  }
   __syncthreads();
   const float c2 = 0.125f * LOG2E;
   const float scale = 0.125f;
@@ -561,24 +590,40 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
     f32x4_t dV[4], dK[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dV[dt] = dK[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // A operands (Q and dO rows of the lane's query) of the next q-tile pair are loaded while the
+    // current pair is processed
+    u16x8_t qa8[2][2], ga8[2][2];
+    auto load_pair = [&](int qp, u16x8_t (&qd)[2][2], u16x8_t (&gd)[2][2]) {
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int qa = 32 * qp + 16 * h2 + n;
+        const int qc = qa < L ? qa : 0;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          qd[h2][ks] = ld8(qb + (size_t)qc * ROW + 32 * ks + 8 * g);
+          gd[h2][ks] = ld8(gb + (size_t)qc * HDm + 32 * ks + 8 * g);
+        }
+      }
+    };
+    load_pair(0, qa8, ga8);
 #pragma unroll 1
     for (int qp = 0; qp < NT / 2; ++qp) {
+      u16x8_t qn8[2][2], gn8[2][2];
+      load_pair(qp + 1 < NT / 2 ? qp + 1 : qp, qn8, gn8);
       float pp[2][4], ds[2][4];
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         const int qt = 2 * qp + h2;
-        const int qa = 16 * qt + n;   // A-operand row (query) of this lane
-        const bool qaok = qa < L;
+        const bool qaok = 16 * qt + n < L;
         f32x4_t sacc = {0.f, 0.f, 0.f, 0.f}, pacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          u16x8_t qa8 = ld8(qb + (size_t)(qaok ? qa : 0) * ROW + 32 * ks + 8 * g);
-          u16x8_t ga8 = ld8(gb + (size_t)(qaok ? qa : 0) * HDm + 32 * ks + 8 * g);
-          if (!qaok) qa8 = ga8 = zero8();
-          sacc = mfma_bf16(qa8, kf[ks], sacc);
-          pacc = mfma_bf16(ga8, vf[ks], pacc);
+          const u16x8_t qv = qaok ? qa8[h2][ks] : zero8();
+          const u16x8_t gv = qaok ? ga8[h2][ks] : zero8();
+          sacc = mfma_bf16(qv, kf[ks], sacc);
+          pacc = mfma_bf16(gv, vf[ks], pacc);
         }
-        const float4 lq = *reinterpret_cast<const float4*>(&lrow[16 * qt + 4 * g]);
+        const float4 lq = *reinterpret_cast<const float4*>(&lsel[16 * qt + 4 * g]);
         const float4 dq = *reinterpret_cast<const float4*>(&delta[16 * qt + 4 * g]);
         const float lqa[4] = {lq.x, lq.y, lq.z, lq.w}, dqa[4] = {dq.x, dq.y, dq.z, dq.w};
 #pragma unroll
@@ -609,6 +654,13 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
         dV[dt] = mfma_bf16(cat44(ld4h(gr + 4 * g), ld4h(gr + 16 + 4 * g)), pf, dV[dt]);
         dK[dt] = mfma_bf16(cat44(ld4h(qr + 4 * g), ld4h(qr + 16 + 4 * g)), sf, dK[dt]);
       }
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          qa8[h2][ks] = qn8[h2][ks];
+          ga8[h2][ks] = gn8[h2][ks];
+        }
     }
     // outputs: dK^T / dV^T tiles -> rows of dqkv (lane: key = 16kt + n, d = 16dt + 4g + r)
     if (kok) {
@@ -625,13 +677,23 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
   }
   __syncthreads();
   // phase 2: K^T image into region A, then dQ^T = K^T dS^T per query tile
-  for (int i = threadIdx.x; i < LP * 8; i += 256) {
-    const int k = i >> 3, c = (i & 7) * 8;
-    const bool ok = k < L;
-    u16x8_t kv = ld8(kb + (size_t)(ok ? k : 0) * ROW + c);
-    if (!ok) kv = zero8();
+  {
+    constexpr int NU = LP * 8 / 256;
+    u16x8_t kv[NU];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) Kt[(c + j) * TSTR + k] = kv[j];
+    for (int u = 0; u < NU; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int k = i >> 3, c = (i & 7) * 8;
+      kv[u] = ld8(kb + (size_t)(k < L ? k : 0) * ROW + c);
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int k = i >> 3, c = (i & 7) * 8;
+      if (k >= L) kv[u] = zero8();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Kt[(c + j) * TSTR + k] = kv[u][j];
+    }
   }
   __syncthreads();
   for (int qt = wave; qt < NT; qt += 4) {

@@ -11,8 +11,9 @@ Embeddings: ina.bert_embed_ln_fwd / _bwd (gather by instance index, no host copi
 gradient is scattered with index_add_ straight into the flat gradient buffer.
 
 Weights: the encoder layers' fp32 masters are cast to bf16 ONCE per step as one contiguous region of
-the flat parameter buffer (``_CastRegion``); its backward adds the bf16 weight gradients into the
-matching region of the flat gradient buffer.  LayerNorm / GELU-bias / embedding tables stay fp32.
+the flat parameter buffer (outside autograd).  ``_Linear`` computes dW / db with fp32-output GEMMs and
+adds them straight into the flat gradient buffer (no bf16 weight-gradient tensors, no autograd slice
+accumulation).  LayerNorm / GELU-bias / embedding tables stay fp32.
 """
 from __future__ import annotations
 
@@ -37,30 +38,58 @@ def _contiguous_region(ts: List[torch.Tensor]) -> Optional[torch.Tensor]:
     return torch.as_strided(base.detach(), (total,), (1,), off)
 
 
-class _CastRegion(torch.autograd.Function):
-    """bf16 copy of a list of fp32 params as one flat tensor.  Backward: add into the flat gradient
-    region (trainer path) or return per-parameter slices (plain autograd)."""
+def _wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """dW = dy^T x in fp32.  K = tokens is the long dimension and the output has few 256x256 tiles, so
+    the reduction is split by hand into 16 K-chunks (one batched GEMM, fp32 out) + a sum: 1.4-3x the
+    plain GEMM at the BERT-base shapes (tools/gemm_bench.py, profiles/r1_gemm_bench.log)."""
+    T, o = dy.shape
+    i = x.shape[1]
+    nc = 16
+    if T % nc != 0 or T < 4096:
+        return torch.mm(dy.t(), x, out_dtype=torch.float32)
+    part = torch.bmm(dy.view(nc, T // nc, o).transpose(1, 2), x.view(nc, T // nc, i), out_dtype=torch.float32)
+    return part.sum(0)
+
+
+class _Linear(torch.autograd.Function):
+    """y = x W^T (+ b) with bf16 operands taken from the per-step bf16 weight copy.
+
+    W may be the row-concatenation of several fp32 parameters (fused QKV).  Backward computes dW and
+    db in fp32 (hipBLASLt bf16 GEMM with fp32 output) and either adds them straight into the flat
+    gradient buffer spans (trainer path) or returns them per parameter (plain autograd)."""
 
     @staticmethod
-    def forward(ctx, region, grad_region, shapes, *params):
-        ctx.grad_region = grad_region
-        ctx.shapes = shapes
-        src = region if region is not None else torch.cat([p.detach().reshape(-1) for p in params])
-        return src.to(torch.bfloat16)
+    def forward(ctx, x, Wb, bb, gW, gb, nw, *params):
+        y = torch.addmm(bb, x, Wb.t()) if bb is not None else torch.mm(x, Wb.t())
+        ctx.save_for_backward(x, Wb)
+        ctx.cfg = (gW, gb, nw, [tuple(p.shape) for p in params], bb is not None)
+        return y
 
     @staticmethod
-    def backward(ctx, g):
-        if ctx.grad_region is not None:
-            ctx.grad_region.add_(g.float())
-            return (None, None, None) + (None,) * len(ctx.shapes)
-        out, o = [], 0
-        for shp in ctx.shapes:
-            n = 1
-            for d in shp:
-                n *= d
-            out.append(g[o:o + n].float().view(shp))
-            o += n
-        return (None, None, None) + tuple(out)
+    def backward(ctx, dy):
+        x, Wb = ctx.saved_tensors
+        gW, gb, nw, shapes, has_b = ctx.cfg
+        dy = dy.contiguous()
+        dx = torch.mm(dy, Wb)
+        dW = _wgrad(dy, x)
+        db = dy.sum(0, dtype=torch.float32) if has_b else None
+        outs = [None] * len(shapes)
+        if gW is not None:
+            gW.add_(dW.view(gW.shape))
+        else:
+            o = 0
+            for i in range(nw):
+                outs[i] = dW[o:o + shapes[i][0]]
+                o += shapes[i][0]
+        if has_b:
+            if gb is not None:
+                gb.add_(db)
+            else:
+                o = 0
+                for i in range(nw, len(shapes)):
+                    outs[i] = db[o:o + shapes[i][0]]
+                    o += shapes[i][0]
+        return (dx, None, None, None, None, None) + tuple(outs)
 
 
 class _Embed(torch.autograd.Function):
@@ -168,29 +197,35 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
     pa = cfg.bert_attn_dropout if training else 0.0
     seed = int(seed) & 0x7FFFFFFF
     meta = {"grad_views": grad_views}
-    # ---- bf16 weight region: all encoder layers (contiguous in the flat buffer)
+    # ---- bf16 weight copy of all encoder layers: ONE cast of a contiguous flat-buffer region
     layer_names = [n for n in names.values() if n.startswith("bert.encoder.layer.")]
     lparams = [P(n) for n in layer_names]
-    region = _contiguous_region(lparams)
-    grad_region = None
-    if region is not None and grad_views is not None:
-        g0 = grad_views.get(by_name[layer_names[0]])
-        if g0 is not None:
-            grad_region = torch.as_strided(g0, (region.numel(),), (1,), g0.storage_offset())
-    wb = _CastRegion.apply(region, grad_region, [tuple(p.shape) for p in lparams], *lparams)
+    with torch.no_grad():
+        region = _contiguous_region(lparams)
+        wb = (region if region is not None else torch.cat([p.detach().reshape(-1) for p in lparams])).to(torch.bfloat16)
     offs, o = {}, 0
     for n, p in zip(layer_names, lparams):
-        offs[n] = (o, p.numel(), tuple(p.shape))
+        offs[n] = (o, p.numel())
         o += p.numel()
 
-    def W(n):
-        off, cnt, shp = offs[n]
-        return wb.narrow(0, off, cnt).view(shp)
+    def wspan(ns, shape):
+        return wb.narrow(0, offs[ns[0]][0], sum(offs[m][1] for m in ns)).view(shape)
 
-    def span(n0, count_names):
-        off = offs[n0][0]
-        cnt = sum(offs[m][1] for m in count_names)
-        return wb.narrow(0, off, cnt)
+    def gspan(ns):
+        """fp32 view of the flat gradient over consecutive params ns (trainer path) or None."""
+        if grad_views is None:
+            return None
+        g0 = grad_views.get(by_name[ns[0]])
+        if g0 is None:
+            return None
+        cnt = sum(offs[m][1] for m in ns)
+        return torch.as_strided(g0, (cnt,), (1,), g0.storage_offset())
+
+    def linear(x, wn, bn, out_dim, in_dim):
+        Wb = wspan(wn, (out_dim, in_dim))
+        bb = wspan(bn, (out_dim,)) if bn else None
+        return _Linear.apply(x, Wb, bb, gspan(wn), gspan(bn) if bn else None, len(wn),
+                             *[P(n) for n in wn], *[P(n) for n in (bn or [])])
 
     # ---- embeddings
     e = "bert.embeddings."
@@ -206,16 +241,15 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
         a = pre + "attention."
         qn = [a + f"self.{k}.weight" for k in ("query", "key", "value")]
         bn = [a + f"self.{k}.bias" for k in ("query", "key", "value")]
-        Wqkv = span(qn[0], qn).view(3 * Hd, Hd)
-        bqkv = span(bn[0], bn)
-        qkv = torch.addmm(bqkv, x, Wqkv.t())
+        qkv = linear(x, qn, bn, 3 * Hd, Hd)
         ctx = _Mha.apply(qkv, inst, mask, L, nh, seed, 17 + 3 * i, pa)
-        o = torch.addmm(W(a + "output.dense.bias"), ctx, W(a + "output.dense.weight").t())
+        o = linear(ctx, [a + "output.dense.weight"], [a + "output.dense.bias"], Hd, Hd)
         x = _LnRes.apply(o, x, P(a + "output.LayerNorm.weight"), P(a + "output.LayerNorm.bias"), seed, 18 + 3 * i, pd,
                          meta, by_name[a + "output.LayerNorm.weight"], by_name[a + "output.LayerNorm.bias"])
-        hpre = torch.mm(x, W(pre + "intermediate.dense.weight").t())
+        I = cfg.bert_intermediate
+        hpre = linear(x, [pre + "intermediate.dense.weight"], None, I, Hd)
         h = _BiasGelu.apply(hpre, P(pre + "intermediate.dense.bias"), meta, by_name[pre + "intermediate.dense.bias"])
-        o = torch.addmm(W(pre + "output.dense.bias"), h, W(pre + "output.dense.weight").t())
+        o = linear(h, [pre + "output.dense.weight"], [pre + "output.dense.bias"], Hd, I)
         x = _LnRes.apply(o, x, P(pre + "output.LayerNorm.weight"), P(pre + "output.LayerNorm.bias"), seed, 19 + 3 * i,
                          pd, meta, by_name[pre + "output.LayerNorm.weight"], by_name[pre + "output.LayerNorm.bias"])
     # ---- pooling + projection (fp32)
