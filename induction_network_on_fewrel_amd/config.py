@@ -105,6 +105,10 @@ class Config:
     deterministic: bool = False
     use_hip_graph: bool = False
     nota_rate: float = 0.0             # FewRel 2.0 none-of-the-above probability per query
+    eval_nota_rate: float = -1.0       # NOTA rate of val/test episodes (-1: same as nota_rate)
+    nota_threshold: float = -1.0       # best-score threshold for predicting NOTA (-1: tuned on val when NOTA > 0)
+    eval_batch: int = 0                # episodes per eval forward (0: episodes_per_step); sized for HBM
+    test_file: str = ""                # final test set (e.g. another domain for FewRel 2.0 DA); empty = val
     grad_check_finite: bool = True     # NaN/Inf guard on the loss
     profile: bool = False
 

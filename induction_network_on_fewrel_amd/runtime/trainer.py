@@ -58,7 +58,8 @@ class _HostEpisodes:
 
 class Trainer:
     def __init__(self, cfg: Config, train_data: FewRelDataset, val_data: Optional[FewRelDataset] = None,
-                 device: str = "auto", dist_ctx: Optional[DistContext] = None, log: bool = True):
+                 device: str = "auto", dist_ctx: Optional[DistContext] = None, log: bool = True,
+                 test_data: Optional[FewRelDataset] = None):
         cfg.validate()
         self.cfg = cfg
         self.dist = dist_ctx or DistContext.from_env(device if device != "auto" else cfg.device)
@@ -67,9 +68,11 @@ class Trainer:
         self.device = self.dist.device
         self.train_data = train_data
         self.val_data = val_data if val_data is not None else train_data
+        self.test_data = test_data
         if cfg.encoder == "bert":
             from ..data.bert_tokenize import synthetic_features
-            for d in {id(self.train_data): self.train_data, id(self.val_data): self.val_data}.values():
+            ds = [self.train_data, self.val_data] + ([test_data] if test_data is not None else [])
+            for d in {id(x): x for x in ds}.values():
                 if d.bert is None:   # e.g. synthetic data: fold its word ids into the BERT vocabulary
                     d.bert = synthetic_features(d, cfg.bert_vocab, cfg.bert_max_length)
         wv = train_data.word_vec_mat
@@ -89,7 +92,9 @@ class Trainer:
         self.skipped_steps = 0
         rank_seed = cfg.seed * 1009 + 7919 * self.dist.rank
         self.train_eps = self._make_sampler(train_data, rank_seed, cfg.nota_rate)
-        self.val_eps = self._make_sampler(self.val_data, rank_seed + 1, cfg.nota_rate)
+        self.eval_nota = cfg.nota_rate if cfg.eval_nota_rate < 0 else cfg.eval_nota_rate
+        self.val_eps = self._make_sampler(self.val_data, rank_seed + 1, self.eval_nota)
+        self.nota_threshold: Optional[float] = cfg.nota_threshold if cfg.nota_threshold >= 0 else None
         self.log = MetricsLogger(cfg.model_dir, enabled=log and self.dist.is_main)
         self.timers = {"sample": 0.0, "fwd_bwd": 0.0, "allreduce": 0.0, "optim": 0.0}
         if cfg.resume:
@@ -166,8 +171,10 @@ class Trainer:
         """Mean over episodes of per-episode accuracy (model/base.py:186-208), mask fed (fix #1)."""
         cfg = self.cfg
         N, K, Q = N or cfg.eN, K or cfg.eK, Q or cfg.eQ
-        B = batch or max(1, min(cfg.episodes_per_step, iters))
+        B = batch or cfg.eval_batch or max(1, min(cfg.episodes_per_step, iters))
         s = sampler or self.val_eps
+        if nota_threshold is None:
+            nota_threshold = self.nota_threshold
         done, acc_sum = 0, 0.0
         while done < iters:
             b = min(B, iters - done)
@@ -227,8 +234,22 @@ class Trainer:
                     self.save()
         self.log.print("\n####################\n")
         self.log.print("Finish training :" + cfg.ckpt_name)
-        test_acc = self.evaluate(cfg.test_iter)
-        self.log.log(self.global_step, "test", accuracy=test_acc)
+        if self.eval_nota > 0.0 and self.nota_threshold is None:
+            from .evaluate import collect_probs, select_nota_threshold
+            tp, tl = collect_probs(self, self.val_eps, min(cfg.val_iter, 1000), cfg.eN, cfg.eK, cfg.eQ,
+                                   cfg.eval_batch or None)
+            self.nota_threshold = select_nota_threshold(tp, tl, cfg.eN)
+            self.log.print(f"NOTA threshold (tuned on val): {self.nota_threshold:.2f}")
+        if self.test_data is not None:   # e.g. another domain (FewRel 2.0 DA) or a held-out split
+            from .evaluate import evaluate_dataset
+            rep = evaluate_dataset(self, self.test_data, cfg.test_iter, cfg.eN, cfg.eK, cfg.eQ, self.eval_nota,
+                                   self.nota_threshold, cfg.eval_batch or None)
+            test_acc = rep.accuracy
+            self.log.log(self.global_step, "test", **{k: v for k, v in rep.to_dict().items()
+                                                      if isinstance(v, float) and v == v})
+        else:
+            test_acc = self.evaluate(cfg.test_iter)
+            self.log.log(self.global_step, "test", accuracy=test_acc)
         self.log.print(f"Test accuracy: {test_acc}")
         self.log.close()
         return test_acc

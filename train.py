@@ -71,6 +71,20 @@ def load_data(cfg: Config, args):
     return tr, va
 
 
+def load_test(cfg: Config, tr):
+    """A separate test file (e.g. another domain, FewRel 2.0 DA) tensorised with the training vocabulary."""
+    from induction_network_on_fewrel_amd.data import FewRelDataset
+    if tr.word2id is None:
+        raise SystemExit("--test_file needs a vocabulary-backed training set (not --synthetic)")
+    te = FewRelDataset.from_fewrel_json_with_vocab(cfg.test_file, tr.word2id, tr.word_vec_mat, cfg.max_length,
+                                                   cfg.case_sensitive)
+    if cfg.encoder == "bert":
+        from induction_network_on_fewrel_amd.data.bert_tokenize import features_from_json
+        te.bert, _ = features_from_json(cfg.test_file, cfg.bert_max_length, vocab=getattr(tr, "bert_vocab", None),
+                                        vocab_file=cfg.bert_vocab_file)
+    return te
+
+
 def _with_bert(cfg, tr, va, path, full, rels, half):
     """BERT features for a relation split of one JSON file (same instance order as the split)."""
     if cfg.encoder != "bert":
@@ -96,7 +110,8 @@ def main(argv=None):
         raise SystemExit(f"unknown model {cfg.model_name!r} (only 'induction')")
     from induction_network_on_fewrel_amd.runtime.trainer import Trainer
     tr_data, va_data = load_data(cfg, args)
-    trainer = Trainer(cfg, tr_data, va_data, device=cfg.device)
+    te_data = load_test(cfg, tr_data) if cfg.test_file else None
+    trainer = Trainer(cfg, tr_data, va_data, device=cfg.device, test_data=te_data)
     if args.eval_only:
         acc = trainer.evaluate(cfg.test_iter)
         if trainer.dist.is_main:
