@@ -109,6 +109,7 @@ class Config:
     nota_threshold: float = -1.0       # best-score threshold for predicting NOTA (-1: tuned on val when NOTA > 0)
     eval_batch: int = 0                # episodes per eval forward (0: episodes_per_step); sized for HBM
     test_file: str = ""                # final test set (e.g. another domain for FewRel 2.0 DA); empty = val
+    test_best: bool = False            # final test from the best-val checkpoint (reference: the last weights)
     grad_check_finite: bool = True     # NaN/Inf guard on the loss
     profile: bool = False
 

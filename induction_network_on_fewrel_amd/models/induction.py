@@ -53,7 +53,7 @@ class InductionNetwork(nn.Module):
 
     def forward(self, inst: torch.Tensor, data: Tuple[torch.Tensor, ...], B: int, N: int, K: int, Q: int,
                 training: bool = True, dropout_seed: int = 0,
-                grad_views: Optional[Dict[str, torch.Tensor]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                grad_views: Optional[Dict[str, torch.Tensor]] = None, overlap=None) -> Tuple[torch.Tensor, torch.Tensor]:
         """inst: int32 [B*(N*K+N*Q)] instance rows (episode layout, support first).
         data: (word, pos1, pos2, mask) [NI, L] int32 on the same device.
         Returns probs [B, N*Q, N] and alphas [B*(N*K+N*Q), L]."""
@@ -64,7 +64,7 @@ class InductionNetwork(nn.Module):
             raise ValueError(f"reference relation head was built for N={p['ntn_w'].shape[1]}, got N={N} "
                              "(use relation_head='paper' for N-independent scoring)")
         if cfg.encoder == "bert":
-            return self._forward_bert(inst, data, B, N, K, Q, training, dropout_seed, grad_views, p)
+            return self._forward_bert(inst, data, B, N, K, Q, training, dropout_seed, grad_views, p, overlap)
         if inst.is_cuda:
             from ..ops.encoder import encode
             from ..ops.head import head
@@ -82,14 +82,14 @@ class InductionNetwork(nn.Module):
                                     kp, int(dropout_seed), bf16=False)
         return probs, alphas.squeeze(-1)
 
-    def _forward_bert(self, inst, data, B, N, K, Q, training, dropout_seed, grad_views, p):
+    def _forward_bert(self, inst, data, B, N, K, Q, training, dropout_seed, grad_views, p, overlap=None):
         """BERT encoder (data = (ids, mask, e1, e2) [NI, Lb] int32) + the same induction/relation head.
         Returns probs and the [CLS]-row attention-free placeholder alphas (None)."""
         cfg = self.cfg
         if inst.is_cuda:
             from ..ops.bert import bert_encode
             from ..ops.head import head
-            e = bert_encode(self, inst, data, training, int(dropout_seed), grad_views)
+            e = bert_encode(self, inst, data, training, int(dropout_seed), grad_views, overlap)
             H = e.shape[1]
             if H not in (16, 40, 64) or N > 16 or N * Q > 64:
                 raise NotImplementedError("GPU head kernels support H in {16,40,64}, N <= 16, N*Q <= 64")

@@ -59,16 +59,16 @@ class _Linear(torch.autograd.Function):
     gradient buffer spans (trainer path) or returns them per parameter (plain autograd)."""
 
     @staticmethod
-    def forward(ctx, x, Wb, bb, gW, gb, nw, *params):
+    def forward(ctx, x, Wb, bb, gW, gb, nw, on_done, *params):
         y = torch.addmm(bb, x, Wb.t()) if bb is not None else torch.mm(x, Wb.t())
         ctx.save_for_backward(x, Wb)
-        ctx.cfg = (gW, gb, nw, [tuple(p.shape) for p in params], bb is not None)
+        ctx.cfg = (gW, gb, nw, [tuple(p.shape) for p in params], bb is not None, on_done)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, Wb = ctx.saved_tensors
-        gW, gb, nw, shapes, has_b = ctx.cfg
+        gW, gb, nw, shapes, has_b, on_done = ctx.cfg
         dy = dy.contiguous()
         dx = torch.mm(dy, Wb)
         dW = _wgrad(dy, x)
@@ -89,7 +89,9 @@ class _Linear(torch.autograd.Function):
                 for i in range(nw, len(shapes)):
                     outs[i] = db[o:o + shapes[i][0]]
                     o += shapes[i][0]
-        return (dx, None, None, None, None, None) + tuple(outs)
+        if on_done is not None:   # last backward op of a layer: its gradient bucket is final
+            on_done()
+        return (dx, None, None, None, None, None, None) + tuple(outs)
 
 
 class _Embed(torch.autograd.Function):
@@ -182,9 +184,22 @@ class _Mha(torch.autograd.Function):
         return dqkv, None, None, None, None, None, None, None
 
 
+def layer_spans(model, flat_names, offsets, numels):
+    """Flat-buffer (offset, numel) of each encoder layer's parameters (the DP overlap buckets)."""
+    names = model.params.names()
+    spans = []
+    for i in range(model.cfg.bert_layers):
+        pre = f"bert.encoder.layer.{i}."
+        idx = [k for k, a in enumerate(flat_names) if names[a].startswith(pre)]
+        spans.append((offsets[idx[0]], sum(numels[k] for k in idx)))
+    return spans
+
+
 def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
-                grad_views: Optional[Dict[str, torch.Tensor]] = None) -> torch.Tensor:
-    """GPU BERT encoder + pooling + projection -> sentence vectors [S, bert_out_dim] fp32."""
+                grad_views: Optional[Dict[str, torch.Tensor]] = None, overlap=None) -> torch.Tensor:
+    """GPU BERT encoder + pooling + projection -> sentence vectors [S, bert_out_dim] fp32.
+    ``overlap`` (parallel/dp.py::OverlapAllReduce over layer_spans) gets ``ready(i)`` when layer i's
+    gradients are final, so DP all-reduces run under the rest of backward."""
     cfg = model.cfg
     ids, mask, e1, e2 = data
     prm = model.params
@@ -221,11 +236,14 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
         cnt = sum(offs[m][1] for m in ns)
         return torch.as_strided(g0, (cnt,), (1,), g0.storage_offset())
 
-    def linear(x, wn, bn, out_dim, in_dim):
+    def linear(x, wn, bn, out_dim, in_dim, on_done=None):
         Wb = wspan(wn, (out_dim, in_dim))
         bb = wspan(bn, (out_dim,)) if bn else None
-        return _Linear.apply(x, Wb, bb, gspan(wn), gspan(bn) if bn else None, len(wn),
+        return _Linear.apply(x, Wb, bb, gspan(wn), gspan(bn) if bn else None, len(wn), on_done,
                              *[P(n) for n in wn], *[P(n) for n in (bn or [])])
+
+    # DP overlap: the QKV projection's backward is the last backward op of layer i -> bucket i is final
+    layer_ready = (lambda i: (lambda: overlap.ready(i))) if overlap is not None else (lambda i: None)
 
     # ---- embeddings
     e = "bert.embeddings."
@@ -241,7 +259,7 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
         a = pre + "attention."
         qn = [a + f"self.{k}.weight" for k in ("query", "key", "value")]
         bn = [a + f"self.{k}.bias" for k in ("query", "key", "value")]
-        qkv = linear(x, qn, bn, 3 * Hd, Hd)
+        qkv = linear(x, qn, bn, 3 * Hd, Hd, layer_ready(i))
         ctx = _Mha.apply(qkv, inst, mask, L, nh, seed, 17 + 3 * i, pa)
         o = linear(ctx, [a + "output.dense.weight"], [a + "output.dense.bias"], Hd, Hd)
         x = _LnRes.apply(o, x, P(a + "output.LayerNorm.weight"), P(a + "output.LayerNorm.bias"), seed, 18 + 3 * i, pd,

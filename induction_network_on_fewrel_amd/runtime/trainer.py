@@ -136,8 +136,14 @@ class Trainer:
         t1 = time.perf_counter()
         self.flat.zero_grad()
         gv = self.grad_views if self.device.type == "cuda" else None
+        ov = None
+        if self.dist.world > 1 and cfg.encoder == "bert" and self.device.type == "cuda":
+            # per-layer buckets all-reduced under the rest of backward (~28 MB fp32 each at BERT-base)
+            from ..ops.bert import layer_spans
+            ov = self.dist.overlap(self.flat.grad, layer_spans(self.model, self.flat.names, self.flat.offsets,
+                                                               self.flat.numels))
         probs, _ = self.model(idx.view(-1), self.train_eps.arrays, B, N, K, Q, training=True,
-                              dropout_seed=self.dropout_seed(), grad_views=gv)
+                              dropout_seed=self.dropout_seed(), grad_views=gv, overlap=ov)
         loss = self.model.loss(probs, labels)
         loss.backward()
         self.flat.sync_grads_into_flat()
@@ -145,7 +151,9 @@ class Trainer:
             acc_t = ref.accuracy(probs.detach(), labels.long())
         self._sync()
         t2 = time.perf_counter()
-        if self.dist.world > 1:
+        if ov is not None:
+            ov.finish()
+        elif self.dist.world > 1:
             self.dist.allreduce_buckets_(self.flat.grad)
         self._sync()
         t3 = time.perf_counter()
@@ -234,6 +242,12 @@ class Trainer:
                     self.save()
         self.log.print("\n####################\n")
         self.log.print("Finish training :" + cfg.ckpt_name)
+        if cfg.test_best and self.best_acc > 0.0:
+            best = ckpt.latest(cfg.model_dir)   # saved only on improvement -> latest = best
+            if best is not None:
+                step = self.global_step
+                self.load(best)
+                self.log.print(f"test from best checkpoint {best} (val acc {self.best_acc:.4f}; trained {step} steps)")
         if self.eval_nota > 0.0 and self.nota_threshold is None:
             from .evaluate import collect_probs, select_nota_threshold
             tp, tl = collect_probs(self, self.val_eps, min(cfg.val_iter, 1000), cfg.eN, cfg.eK, cfg.eQ,

@@ -46,7 +46,16 @@ def _worker(rank, world, port, out_dir):
     for _ in range(3):
         tr.train_step()
     in_sync = tr.dist.params_in_sync(tr.flat.flat)
-    torch.save({"ok_sum": ok_sum, "in_sync": in_sync, "idx": idx}, os.path.join(out_dir, f"r{rank}.pt"))
+    # 3) backward-overlapped bucket all-reduce: buckets launched out of order + the uncovered rest
+    buf = torch.arange(20, dtype=torch.float32) * (rank + 1)
+    ov = dist.overlap(buf, [(2, 5), (10, 4)])
+    ov.ready(1)
+    ov.ready(0)
+    ov.ready(1)          # idempotent
+    ov.finish()
+    ok_overlap = torch.equal(buf, torch.arange(20, dtype=torch.float32) * sum(r + 1 for r in range(world)))
+    torch.save({"ok_sum": ok_sum, "in_sync": in_sync, "idx": idx, "ok_overlap": ok_overlap},
+               os.path.join(out_dir, f"r{rank}.pt"))
     dist.destroy()
 
 
@@ -58,4 +67,5 @@ def test_dp_gloo_world2(tmp_path):
     r = [torch.load(tmp_path / f"r{i}.pt", weights_only=True) for i in range(world)]
     assert all(x["ok_sum"] for x in r)
     assert all(x["in_sync"] for x in r)
+    assert all(x["ok_overlap"] for x in r)
     assert not torch.equal(r[0]["idx"], r[1]["idx"])   # rank-folded sampling
