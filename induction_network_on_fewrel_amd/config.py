@@ -111,7 +111,9 @@ class Config:
     test_file: str = ""                # final test set (e.g. another domain for FewRel 2.0 DA); empty = val
     test_best: bool = False            # final test from the best-val checkpoint (reference: the last weights)
     grad_check_finite: bool = True     # NaN/Inf guard on the loss
-    profile: bool = False
+    profile: bool = False              # per-phase GPU time (HIP events) into metrics.jsonl at log points
+    watchdog_s: float = 0.0            # abort (traceback + exit) if one train step takes longer (0 = off)
+    save_every: int = 0                # periodic checkpoints for restart-resume (reference: best-val only)
 
     # ------------------------------------------------------------------
     @property

@@ -11,8 +11,10 @@ NaN/Inf loss guard; per-phase timers; JSONL + TensorBoard metrics; no per-step t
 """
 from __future__ import annotations
 
+import faulthandler
 import math
 import os
+import sys
 import time
 from collections import OrderedDict
 from typing import Optional, Tuple
@@ -96,7 +98,12 @@ class Trainer:
         self.val_eps = self._make_sampler(self.val_data, rank_seed + 1, self.eval_nota)
         self.nota_threshold: Optional[float] = cfg.nota_threshold if cfg.nota_threshold >= 0 else None
         self.log = MetricsLogger(cfg.model_dir, enabled=log and self.dist.is_main)
-        self.timers = {"sample": 0.0, "fwd_bwd": 0.0, "allreduce": 0.0, "optim": 0.0}
+        self.timers = {"sample": 0.0, "fwd_bwd": 0.0, "allreduce": 0.0, "optim": 0.0}   # host (launch) time
+        self.gpu_phase_ms = {k: 0.0 for k in self.timers}                                # HIP-event time
+        self._pending_events = []
+        # fault injection (tests / chaos runs): raise at a given global step on a given rank
+        self._fault_step = int(os.environ.get("INA_FAULT_STEP", "-1"))
+        self._fault_rank = int(os.environ.get("INA_FAULT_RANK", "0"))
         if cfg.resume:
             self.maybe_resume()
 
@@ -111,8 +118,23 @@ class Trainer:
         return _HostEpisodes(data, seed, nota, self.cfg.encoder)
 
     def _sync(self):
+        """Phase boundary: with ``profile`` on a GPU, record a HIP event (no host synchronisation)."""
         if self.device.type == "cuda" and self.cfg.profile:
-            torch.cuda.synchronize()
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ev
+        return None
+
+    def drain_phase_events(self) -> dict:
+        """Accumulate the recorded phase events into ``gpu_phase_ms`` (call at a sync point)."""
+        for evs in self._pending_events:
+            if any(e is None for e in evs):
+                continue
+            evs[-1].synchronize()
+            for k, a, b in zip(("sample", "fwd_bwd", "allreduce", "optim"), evs[:-1], evs[1:]):
+                self.gpu_phase_ms[k] += a.elapsed_time(b)
+        self._pending_events = []
+        return dict(self.gpu_phase_ms)
 
     def dropout_seed(self) -> int:
         return (self.cfg.seed * 2654435761 + self.global_step * 97 + self.dist.rank * 7919) & 0x7FFFFFFF
@@ -130,9 +152,12 @@ class Trainer:
         buffer (grad_views), which is also the DP all-reduce bucket and the fused optimizer input."""
         cfg = self.cfg
         B, N, K, Q = cfg.episodes_per_step, cfg.N, cfg.K, cfg.Q
+        if self.global_step == self._fault_step and self.dist.rank == self._fault_rank:
+            raise RuntimeError(f"injected fault at step {self.global_step} on rank {self.dist.rank} (INA_FAULT_STEP)")
         t0 = time.perf_counter()
+        e0 = self._sync()
         idx, labels = self.train_eps.sample(B, N, K, Q)
-        self._sync()
+        e1 = self._sync()
         t1 = time.perf_counter()
         self.flat.zero_grad()
         gv = self.grad_views if self.device.type == "cuda" else None
@@ -149,13 +174,13 @@ class Trainer:
         self.flat.sync_grads_into_flat()
         with torch.no_grad():
             acc_t = ref.accuracy(probs.detach(), labels.long())
-        self._sync()
+        e2 = self._sync()
         t2 = time.perf_counter()
         if ov is not None:
             ov.finish()
         elif self.dist.world > 1:
             self.dist.allreduce_buckets_(self.flat.grad)
-        self._sync()
+        e3 = self._sync()
         t3 = time.perf_counter()
         lr = lr_at(self.global_step, cfg.learning_rate, cfg.decay_steps, cfg.decay_rate, cfg.staircase,
                    cfg.lr_schedule)
@@ -164,7 +189,9 @@ class Trainer:
         else:
             self.opt.step(lr, grad_scale=1.0 / self.dist.world)
         self.global_step += 1
-        self._sync()
+        e4 = self._sync()
+        if e0 is not None:
+            self._pending_events.append((e0, e1, e2, e3, e4))
         t4 = time.perf_counter()
         self.timers["sample"] += t1 - t0
         self.timers["fwd_bwd"] += t2 - t1
@@ -205,8 +232,14 @@ class Trainer:
         t_start = time.time()
         pend_loss = pend_acc = None
         pend_n = 0
+        if cfg.watchdog_s > 0:
+            self.log.print(f"watchdog: abort if a step exceeds {cfg.watchdog_s:.0f}s")
         for it in range(start, cfg.train_iter):
+            if cfg.watchdog_s > 0:   # hung collective / kernel -> traceback + exit (launcher restarts, resume)
+                faulthandler.dump_traceback_later(cfg.watchdog_s, repeat=False, file=sys.stderr, exit=True)
             loss_t, acc_t = self.train_step_async()
+            if cfg.save_every > 0 and self.global_step % cfg.save_every == 0:
+                self.save()
             # accumulate on device; the host only synchronises at log / reset / eval points
             pend_loss = loss_t if pend_loss is None else pend_loss + loss_t
             pend_acc = acc_t if pend_acc is None else pend_acc + acc_t
@@ -224,6 +257,10 @@ class Trainer:
                 pend_n = 0
                 self.log.log(self.global_step, "train", loss=it_loss / it_n, accuracy=it_acc / it_n,
                              learning_rate=self._last_lr)
+                if cfg.profile and self.device.type == "cuda":
+                    self.log.log(self.global_step, "profile", **{f"gpu_{k}_ms": v for k, v in
+                                                                 self.drain_phase_events().items()},
+                                 **{f"host_{k}_s": v for k, v in self.timers.items()})
             if it % cfg.log_every == 0:
                 el = time.time() - t_start
                 eps = (it - start + 1) * cfg.episodes_per_step * self.dist.world / max(el, 1e-9)
@@ -233,6 +270,8 @@ class Trainer:
             if it % cfg.val_step == 0:
                 it_loss = it_acc = it_n = 0.0
             if (it + 1) % cfg.val_step == 0:
+                if cfg.watchdog_s > 0:
+                    faulthandler.cancel_dump_traceback_later()   # evaluation is not a train step
                 acc_val = self.evaluate(cfg.val_iter)
                 self.log.log(self.global_step, "val", accuracy=acc_val)
                 self.log.print(f"[EVAL] step {it + 1} accuracy: {100 * acc_val:.2f}%")
@@ -240,6 +279,8 @@ class Trainer:
                     self.best_acc = acc_val
                     self.log.print(f"Best checkpoint.[EVAL] accuracy :{acc_val}")
                     self.save()
+        if cfg.watchdog_s > 0:
+            faulthandler.cancel_dump_traceback_later()
         self.log.print("\n####################\n")
         self.log.print("Finish training :" + cfg.ckpt_name)
         if cfg.test_best and self.best_acc > 0.0:

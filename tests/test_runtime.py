@@ -112,3 +112,23 @@ def test_training_learns_on_synthetic(tmp_path):
     acc = tr.evaluate(60)
     assert np.mean(last) < np.mean(first)
     assert acc > 0.3   # chance = 0.2
+
+
+def test_fault_injection_then_resume(tmp_path):
+    """Failure detection / restart: a rank dies mid-run (INA_FAULT_STEP), the relaunch resumes from the
+    last periodic checkpoint and finishes."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = [sys.executable, os.path.join(root, "train.py"), "induction", "5", "1", "--synthetic", "true",
+            "--synthetic_relations", "8", "--synthetic_instances", "20", "--synthetic_vocab", "300",
+            "--train_iter", "8", "--val_step", "100", "--val_iter", "2", "--test_iter", "2", "--log_every", "1",
+            "--save_every", "2", "--device", "cpu", "--watchdog_s", "600", "--model_dir", str(tmp_path / "ck")]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", INA_FAULT_STEP="5")
+    r = subprocess.run(args, capture_output=True, text=True, timeout=600, env=env, cwd=tmp_path)
+    assert r.returncode != 0 and "injected fault at step 5" in r.stderr
+    env.pop("INA_FAULT_STEP")
+    r = subprocess.run(args, capture_output=True, text=True, timeout=600, env=env, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "resumed from" in r.stdout and "inductionNetwork-4" in r.stdout
+    assert "Test accuracy" in r.stdout
