@@ -132,6 +132,85 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
     }
   for (int s = gw; s < S; s += nw) {
     const long row = (long)inst[s] * L;
+    if constexpr (BF16) {
+      // all of the sentence's loads first (H tiles stay in registers for scores AND pooling)
+      u16x8_t hf[NT][NKS];
+      int mk[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int tok = 16 * nt + n;
+        const bool tv = tok < L;
+        const size_t hrow = ((size_t)s * L + (tv ? tok : L - 1)) * H2;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          const int k0 = 32 * ks + 8 * q;
+          const bool ok = tv && (k0 < H2);
+          const u16x8_t v = *reinterpret_cast<const u16x8_t*>(hraw + hrow + (ok ? k0 : 0));
+          hf[nt][ks] = ok ? v : u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+        mk[nt] = maskarr[row + (tv ? tok : L - 1)];
+      }
+      float score[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int tok = 16 * nt + n;
+        float sp = 0.f;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          f32x4_t acc = {bj[m][0], bj[m][1], bj[m][2], bj[m][3]};
+#pragma unroll
+          for (int ks = 0; ks < NKS; ++ks) acc = mma(A[m][ks], hf[nt][ks], acc);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sp += wj[m][r] * tanhf_(acc[r]);
+        }
+        sp = cross_group_sum(sp);
+        const float m01 = mk[nt] > 0 ? 1.f : 0.f;
+        score[nt] = (tok < L) ? sp + (1.f - m01) * -2147483648.f : -INFINITY;
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) mx = fmaxf(mx, score[nt]);
+      mx = group16_max(mx);
+      float p[NT], sum = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        p[nt] = (16 * nt + n < L) ? __expf(score[nt] - mx) : 0.f;
+        sum += p[nt];
+      }
+      sum = group16_sum(sum);
+      const float inv = 1.f / sum;
+      float ev[NKS][8];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ev[ks][j] = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int tok = 16 * nt + n;
+        const float a = p[nt] * inv;
+        if (q == 0 && tok < L) alphas[(long)s * L + tok] = a;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ev[ks][j] += a * bf2f(hf[nt][ks][j]);
+      }
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ev[ks][j] = group16_sum(ev[ks][j]);
+      if (n == 0) {
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          const int k0 = 32 * ks + 8 * q;
+          if (k0 < H2) {
+            float4* o = reinterpret_cast<float4*>(e_out + (long)s * H2 + k0);
+            o[0] = make_float4(ev[ks][0], ev[ks][1], ev[ks][2], ev[ks][3]);
+            o[1] = make_float4(ev[ks][4], ev[ks][5], ev[ks][6], ev[ks][7]);
+          }
+        }
+      }
+      continue;
+    }
     // pass 1: scores (projection + tanh + w2 dot), one token tile at a time
     float score[NT];
 #pragma unroll
@@ -428,6 +507,239 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// bf16 backward, v2: 8-wave workgroups, weight fragments shared in LDS, every load of a sentence
+// issued up front (H tiles kept in registers for both passes), d(alpha) from the same registers,
+// dW1 accumulated in 32-token K-steps through a small wave-private LDS transpose.
+// slab per block: [dW1 (H2*H2, row i, col j) | db1 (H2) | dw2 (H2)]
+constexpr int AB2_WAVES = 4;
+
+template <int U, int NT>
+__host__ __device__ constexpr int ab2_rows() { return ((2 * U + 15) / 16) * 16; }
+constexpr int AB2_RS = 40;   // staging row stride (32 tokens + 8 pad), bf16 elements
+
+template <int U, int NT>
+__global__ __launch_bounds__(256) void attn_bwd2_kernel(
+    const unsigned short* __restrict__ hraw, int S, int L, const u16x8_t* __restrict__ w1pack,
+    const u16x8_t* __restrict__ w1tpack, const float* __restrict__ b1, const float* __restrict__ w2,
+    const float* __restrict__ de, const float* __restrict__ alphas, unsigned short* __restrict__ dHraw,
+    float* __restrict__ slab) {
+  using Sh = AShape<U, NT, true>;
+  constexpr int H2 = Sh::H2, NKS = Sh::NKS, MT = Sh::MT, NKS2 = Sh::NKS2;
+  constexpr int ROWS = MT * 16;
+  constexpr int NA = MT * NKS * 64, NA2 = MT * NKS2 * 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane >> 4, n = lane & 15;
+  const int gw = blockIdx.x * AB2_WAVES + wave, nw = gridDim.x * AB2_WAVES;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  u16x8_t* lA = reinterpret_cast<u16x8_t*>(smem);
+  u16x8_t* lAT = lA + NA;
+  float* lbw = reinterpret_cast<float*>(lAT + NA2);           // [b1 | w2] padded to ROWS each
+  unsigned short* stg = reinterpret_cast<unsigned short*>(lbw + 2 * ROWS) + (size_t)wave * 2 * ROWS * AB2_RS;
+  unsigned short* HT = stg;                                    // [feature i][token col]
+  unsigned short* DPT = stg + ROWS * AB2_RS;                   // [j][token col]
+  for (int i = threadIdx.x; i < NA; i += 256) lA[i] = w1pack[i];
+  for (int i = threadIdx.x; i < NA2; i += 256) lAT[i] = w1tpack[i];
+  for (int i = threadIdx.x; i < ROWS; i += 256) {
+    lbw[i] = i < H2 ? b1[i] : 0.f;
+    lbw[ROWS + i] = i < H2 ? w2[i] : 0.f;
+  }
+  for (int i = lane; i < 2 * ROWS * AB2_RS; i += 64) stg[i] = 0;
+  __syncthreads();
+
+  f32x4_t accW[MT][MT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < MT; ++b) accW[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float dw2a[MT][4], db1a[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dw2a[m][r] = db1a[m][r] = 0.f;
+  int tc = 0;  // tiles staged by this wave (column half = tc & 1)
+
+  auto flush = [&]() {
+    wave_lds_sync();
+    u16x8_t fb[MT];
+#pragma unroll
+    for (int b = 0; b < MT; ++b) fb[b] = *reinterpret_cast<const u16x8_t*>(&DPT[(16 * b + n) * AB2_RS + 8 * q]);
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+      const u16x8_t fa = *reinterpret_cast<const u16x8_t*>(&HT[(16 * a + n) * AB2_RS + 8 * q]);
+#pragma unroll
+      for (int b = 0; b < MT; ++b) accW[a][b] = mfma_bf16(fa, fb[b], accW[a][b]);
+    }
+    wave_lds_sync();
+  };
+
+  for (int s = gw; s < S; s += nw) {
+    // ---- every load of the sentence first: H tiles (bf16 MFMA operands), de, alphas
+    u16x8_t hf[NT][NKS];
+    float al[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int tok = 16 * nt + n;
+      const bool tv = tok < L;
+      const size_t row = ((size_t)s * L + (tv ? tok : L - 1)) * H2;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int k0 = 32 * ks + 8 * q;
+        const bool ok = tv && (k0 < H2);
+        const u16x8_t v = *reinterpret_cast<const u16x8_t*>(hraw + row + (ok ? k0 : 0));
+        hf[nt][ks] = ok ? v : u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+      const float a = alphas[(size_t)s * L + (tv ? tok : L - 1)];
+      al[nt] = tv ? a : 0.f;
+    }
+    float dev[NKS][8];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int k0 = 32 * ks + 8 * q;
+      const bool ok = k0 < H2;
+      const float4 a = *reinterpret_cast<const float4*>(de + (size_t)s * H2 + (ok ? k0 : 0));
+      const float4 b = *reinterpret_cast<const float4*>(de + (size_t)s * H2 + (ok ? k0 : 0) + 4);
+      const float z = ok ? 1.f : 0.f;
+      dev[ks][0] = a.x * z; dev[ks][1] = a.y * z; dev[ks][2] = a.z * z; dev[ks][3] = a.w * z;
+      dev[ks][4] = b.x * z; dev[ks][5] = b.y * z; dev[ks][6] = b.z * z; dev[ks][7] = b.w * z;
+    }
+    float dei[MT][4];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int i0 = 16 * m + 4 * q;
+      const bool ok = i0 < H2;
+      const float4 a = *reinterpret_cast<const float4*>(de + (size_t)s * H2 + (ok ? i0 : 0));
+      dei[m][0] = ok ? a.x : 0.f; dei[m][1] = ok ? a.y : 0.f; dei[m][2] = ok ? a.z : 0.f; dei[m][3] = ok ? a.w : 0.f;
+    }
+    // ---- pass A (registers only): d(alpha)_t = de . H_t, sd = sum_t alpha_t d(alpha)_t
+    float da[NT];
+    float sd = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      float d = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d += dev[ks][j] * bf2f(hf[nt][ks][j]);
+      da[nt] = cross_group_sum(d);
+      sd += al[nt] * da[nt];
+    }
+    sd = group16_sum(sd);
+    // ---- pass B per token tile (not unrolled: one tile's temporaries live at a time; the tile's
+    // registers are picked with compile-time selects, so no scratch indexing)
+#pragma unroll 1
+    for (int nt = 0; nt < NT; ++nt) {
+      asm volatile("" ::: "memory");   // re-read the LDS weight fragments per tile (no hoisting)
+      u16x8_t ht[NKS];
+      float alv = al[0], dav = da[0];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) ht[ks] = hf[0][ks];
+#pragma unroll
+      for (int j = 1; j < NT; ++j)
+        if (j == nt) {
+          alv = al[j];
+          dav = da[j];
+#pragma unroll
+          for (int ks = 0; ks < NKS; ++ks) ht[ks] = hf[j][ks];
+        }
+      const int tok = 16 * nt + n;
+      const float ds = alv * (dav - sd);
+      float dp[MT][4];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const float4 bj = *reinterpret_cast<const float4*>(&lbw[16 * m + 4 * q]);
+        const float4 wj = *reinterpret_cast<const float4*>(&lbw[ROWS + 16 * m + 4 * q]);
+        f32x4_t acc = {bj.x, bj.y, bj.z, bj.w};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) acc = mfma_bf16(lA[(m * NKS + ks) * 64 + lane], ht[ks], acc);
+        const float wv[4] = {wj.x, wj.y, wj.z, wj.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pr = tanhf_(acc[r]);
+          dp[m][r] = ds * wv[r] * (1.f - pr * pr);
+          dw2a[m][r] += ds * pr;
+          db1a[m][r] += dp[m][r];
+        }
+      }
+      u16x8_t B2[NKS2];
+#pragma unroll
+      for (int ks = 0; ks < NKS2; ++ks) {
+        B2[ks] = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int idx = ks * 8 + j;
+          if (idx < 4 * MT) B2[ks][j] = f2bf(dp[idx >> 2][idx & 3]);
+        }
+      }
+      unsigned short* dst = dHraw + ((size_t)s * L + (tok < L ? tok : 0)) * H2;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NKS2; ++ks) acc = mfma_bf16(lAT[(m * NKS2 + ks) * 64 + lane], B2[ks], acc);
+        if (tok < L && 16 * m + 4 * q < H2) {
+          uint2 pk;
+          pk.x = (uint32_t)f2bf(acc[0] + alv * dei[m][0]) | ((uint32_t)f2bf(acc[1] + alv * dei[m][1]) << 16);
+          pk.y = (uint32_t)f2bf(acc[2] + alv * dei[m][2]) | ((uint32_t)f2bf(acc[3] + alv * dei[m][3]) << 16);
+          *reinterpret_cast<uint2*>(dst + 16 * m + 4 * q) = pk;
+        }
+      }
+      // stage this tile's H (features) and dP columns for the dW1 K-step
+      const int col = 16 * (tc & 1) + n;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 32 * ks + 8 * q + j;
+          if (k < ROWS) HT[k * AB2_RS + col] = ht[ks][j];
+        }
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) DPT[(16 * m + 4 * q + r) * AB2_RS + col] = f2bf(dp[m][r]);
+      if (tc & 1) flush();
+      ++tc;
+    }
+  }
+  if (tc & 1) {   // half-filled last K-step: clear the other half, then flush
+#pragma unroll
+    for (int k = 0; k < ROWS; k += 4) {
+      HT[(k + q) * AB2_RS + 16 + n] = 0;
+      DPT[(k + q) * AB2_RS + 16 + n] = 0;
+    }
+    flush();
+  }
+  // ---- workgroup reduction into the slab (reuse the packs' LDS as fp32 after a barrier)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  const int NS = H2 * H2 + 2 * H2;
+  for (int i = threadIdx.x; i < NS; i += 256) red[i] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < MT; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * a + 4 * q + r, j = 16 * b + n;
+        if (i < H2 && j < H2) atomicAdd(&red[i * H2 + j], accW[a][b][r]);
+      }
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * m + 4 * q + r;
+      const float d1 = group16_sum(db1a[m][r]);
+      const float d2 = group16_sum(dw2a[m][r]);
+      if (n == 0 && j < H2) {
+        atomicAdd(&red[H2 * H2 + j], d1);
+        atomicAdd(&red[H2 * H2 + H2 + j], d2);
+      }
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NS; i += 256) slab[(size_t)blockIdx.x * NS + i] = red[i];
+}
+
+// ------------------------------------------------------------------------------------------
 namespace ina {
 
 
@@ -449,9 +761,29 @@ static int attn_fwd_t(const AttnArgs& a, hipStream_t st) {
   INA_CHECK_LAUNCH();
   return 0;
 }
+size_t attn_bwd2_lds_bytes(int U, int NT) {
+  const int H2 = 2 * U, MT = (H2 + 15) / 16, ROWS = MT * 16;
+  const int NKS = ((H2 + 31) / 32), NKS2 = (4 * MT + 7) / 8;
+  size_t b = (size_t)(MT * NKS * 64 + MT * NKS2 * 64) * 16 + (size_t)2 * ROWS * 4 +
+             (size_t)AB2_WAVES * 2 * ROWS * AB2_RS * 2;
+  const size_t r = (size_t)(H2 * H2 + 2 * H2) * 4;
+  return b > r ? b : r;
+}
+
 template <int U, int NT, bool BF16>
 static int attn_bwd_t(const AttnArgs& a, hipStream_t st) {
   using F = FT<BF16>;
+  if constexpr (BF16) {
+    const size_t lds2 = attn_bwd2_lds_bytes(U, NT);
+    if (lds2 > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<U, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+    hipLaunchKernelGGL((attn_bwd2_kernel<U, NT>), dim3(a.blocks), dim3(256), lds2, st,
+                       (const unsigned short*)a.hraw, a.S, a.L, (const u16x8_t*)a.w1pack,
+                       (const u16x8_t*)a.w1tpack, a.b1, a.w2, a.de, a.alphas, (unsigned short*)a.dHraw, a.slab);
+    INA_CHECK_LAUNCH();
+    return 0;
+  }
   const size_t lds = attn_bwd_lds_bytes(U, NT, BF16);
   hipLaunchKernelGGL((attn_bwd_kernel<U, NT, BF16>), dim3(a.blocks), dim3(256), lds, st,
                      (const typename F::elem*)a.hraw, a.inst, a.S, a.L, (const typename F::frag*)a.w1pack,
