@@ -41,7 +41,7 @@ uint32_t keep_threshold(double kp) {
 // Returns (hlane, cst, hnat): hlane = raw recurrent h and cst = cell states, both in the
 // lane-native tile layout [ceil(S/16), 2, L, U/4, 64] (only when store_c: the backward needs them);
 // hnat = the DropoutWrapper output in natural layout [S, L, 2U] (the attention input).
-std::tuple<Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
+std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
                                             const Tensor& pos2, const Tensor& wemb, const Tensor& p1emb,
                                             const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U,
                                             int64_t NX, bool bf16, bool store_c, int64_t seed, double keep_prob) {
@@ -77,7 +77,10 @@ std::tuple<Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& wo
   TORCH_CHECK(ntiles * 16 * L * 2 * U < (1LL << 31) && ntiles * 2 * L * U4 * 64 < (1LL << 32),
               "ina.lstm_fwd: batch too large for 32-bit offsets (split the episode batch)");
   TORCH_CHECK(wemb.size(0) < (1 << 24) && 2 * L < (1 << 16), "ina.lstm_fwd: table rows exceed 24-bit indexing");
-  if (S == 0) return {hlane, cst, hnat};
+  // dropout keep bits for the backward (one byte per lane-step), only when both are needed
+  Tensor dmask = (store_c && drop) ? at::empty({ntiles, 2, L, 64}, word.options().dtype(at::kByte))
+                                   : at::empty({0}, word.options().dtype(at::kByte));
+  if (S == 0) return {hlane, cst, hnat, dmask};
   ina::LstmArgs a{};
   a.inst = inst.data_ptr<int>();
   a.S = (int)S;
@@ -95,20 +98,21 @@ std::tuple<Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& wo
   a.hraw = store_c ? hlane.data_ptr() : nullptr;
   a.cst = store_c ? cst.data_ptr() : nullptr;
   a.hdrop = hnat.data_ptr();
+  a.dmask = (store_c && drop) ? dmask.data_ptr<uint8_t>() : nullptr;
   a.seed = (uint32_t)seed;
   a.thr = keep_threshold(keep_prob);
   a.inv_kp = (float)(1.0 / keep_prob);
   a.drop = drop ? 1 : 0;
   check_launch(ina::lstm_fwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_fwd");
-  return {hlane, cst, hnat};
+  return {hlane, cst, hnat, dmask};
 }
 
 std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
                                             const Tensor& pos2, const Tensor& wemb, const Tensor& p1emb,
                                             const Tensor& p2emb, const Tensor& apack, const Tensor& a2pack,
                                             const Tensor& bias, const Tensor& hraw, const Tensor& cst, const Tensor& dH,
-                                            int64_t U, int64_t NX, bool bf16, bool word_grad, int64_t blocks,
-                                            int64_t seed, double keep_prob) {
+                                            const Tensor& dmask, int64_t U, int64_t NX, bool bf16, bool word_grad,
+                                            int64_t blocks, int64_t seed, double keep_prob) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -129,6 +133,11 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   TORCH_CHECK(hraw.numel() == ((S + 15) / 16) * 2 * L * U4 * 64, "ina.lstm_bwd: hlane shape");
   TORCH_CHECK(dH.size(0) == S && dH.size(1) == L && dH.size(2) == 2 * U, "ina.lstm_bwd: dH shape");
   TORCH_CHECK(cst.numel() == ((S + 15) / 16) * 2 * L * U4 * 64, "ina.lstm_bwd: cst shape");
+  const bool drop_ = keep_prob < 1.0;
+  if (drop_) {
+    check(dmask, "dmask", at::kByte);
+    TORCH_CHECK(dmask.numel() == ((S + 15) / 16) * 2 * L * 64, "ina.lstm_bwd: dmask (from lstm_fwd) shape");
+  }
   const int64_t NSLOT = U4 + NX;
   TORCH_CHECK(a2pack.numel() == 2 * ((NSLOT + 3) / 4) * ((4 * U4 + KPL - 1) / KPL) * 64 * KPL, "ina.lstm_bwd: a2pack");
   TORCH_CHECK(ina::lstm_bwd_lds_bytes((int)U, (int)NX, bf16, (int)L, (int)PD) <= 160 * 1024, "ina.lstm_bwd: LDS budget");
@@ -165,6 +174,7 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   a.dw_slab = dw_slab.data_ptr<float>();
   a.dpos_slab = dpos_slab.data_ptr<float>();
   a.dwemb = word_grad ? dwemb.data_ptr<float>() : nullptr;
+  a.dmask = drop_ ? dmask.data_ptr<uint8_t>() : nullptr;
   a.bwd_blocks = (int)blocks;
   a.seed = (uint32_t)seed;
   a.thr = keep_threshold(keep_prob);

@@ -30,6 +30,7 @@ struct LstmArgs {
   float* dwemb;
   int bwd_blocks;
   void* hdrop;
+  unsigned char* dmask;  // [tiles][2][L][64] dropout keep bits (bit m = unit 4m+q), written by fwd, read by bwd
   uint32_t seed, thr;
   float inv_kp;
   int drop;

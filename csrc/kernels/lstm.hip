@@ -144,13 +144,14 @@ INA_DEVICE void wave_lds_sync() {
 // DROP / STORE are compile-time so the step loop has no branches: the waitcnt pass can then count
 // the stores issued after each prefetch and wait only for the prefetched loads.
 template <int U, int NX, bool BF16, bool DROP, bool STORE>
-__global__ __launch_bounds__(256) void lstm_fwd_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void lstm_fwd_kernel(
     const int* __restrict__ inst, int S, const int* __restrict__ word, const int* __restrict__ pos1,
     const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
     const float* __restrict__ p1emb, const float* __restrict__ p2emb, int PD,
     const typename FragT<BF16>::type* __restrict__ apack, const float* __restrict__ bias,
     typename FragT<BF16>::elem* __restrict__ hlane, typename CT<BF16>::type* __restrict__ cst,
-    typename FragT<BF16>::elem* __restrict__ hnat, uint32_t seed, uint32_t thr, float inv_kp, int drop) {
+    typename FragT<BF16>::elem* __restrict__ hnat, unsigned char* __restrict__ dmask, uint32_t seed, uint32_t thr,
+    float inv_kp, int drop) {
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
   using celem = typename CT<BF16>::type;
@@ -238,10 +239,15 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(
       typename FragT<BF16>::elem* hn = hnat + (((uint32_t)seq * L + t) * (2 * U) + dir * U + q);
       if constexpr (DROP) {
         const uint32_t base = ((uint32_t)seq * L + t) * U + q;
+        uint32_t bits = 0;
 #pragma unroll
         for (int m = 0; m < U4; ++m) {
           const bool keep = dropout_keep_salted(salt, base + 4 * m, thr);
+          bits |= keep ? (1u << m) : 0u;
           hn[4 * m] = to_elem(keep ? h[m] * inv_kp : 0.f, (typename FragT<BF16>::elem*)nullptr);
+        }
+        if constexpr (STORE) {   // the backward re-applies the mask from these bits (no re-hashing)
+          if constexpr (U4 <= 8) dmask[(uint32_t)((tile * 2 + dir) * L + t) * 64 + lane] = (unsigned char)bits;
         }
       } else {
 #pragma unroll
@@ -314,7 +320,8 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
     const float* __restrict__ bias, const typename FragT<BF16>::elem* __restrict__ hraw,
     const typename CT<BF16>::type* __restrict__ cst, const typename FragT<BF16>::elem* __restrict__ dH,
     float* __restrict__ dw_slab,
-    float* __restrict__ dpos_slab, float* __restrict__ dwemb, uint32_t seed, uint32_t thr, float inv_kp, int drop) {
+    float* __restrict__ dpos_slab, float* __restrict__ dwemb, const unsigned char* __restrict__ dmask, uint32_t seed,
+    uint32_t thr, float inv_kp, int drop) {
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
   using elem = typename FragT<BF16>::elem;
@@ -360,6 +367,11 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
   for (int i = lane; i < 32; i += 64) xhT[(DIN + U) * RS + i] = to_elem(1.f, (elem*)nullptr);
   __syncthreads();
 
+  float bm[NMT][4];   // gate biases of the lane's units (registers, not per-step LDS reads)
+#pragma unroll
+  for (int m = 0; m < NMT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bm[m][r] = lbias[r * U + 4 * m + q];
   f32x4_t accw[GT][FTMAX];
 #pragma unroll
   for (int a = 0; a < GT; ++a)
@@ -379,7 +391,6 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
     const long rowbase = (long)inst[seqc] * L;
     const typename CT<BF16>::type* cbase = cst + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
     const elem* hbase = hraw + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
-    const uint32_t dsalt = dropout_salt(seed, (uint32_t)dir);
     auto tof = [&](int tau) { return dir ? (L - 1 - tau) : tau; };  // processing step -> time
     // software pipeline: ids two steps ahead, everything else one step ahead
     int wid_c, p1_c, p2_c, wid_n, p1_n, p2_n;
@@ -389,8 +400,10 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
       wid_n = word[rowbase + t1]; p1_n = pos1[rowbase + t1]; p2_n = pos2[rowbase + t1];
     }
     float xv[NX], hp[U4], cprev[U4], ccur[U4], dhin[U4];
+    const unsigned char* mbase = dmask + (size_t)(tile * 2 + dir) * L * 64 + lane;   // fwd keep bits
     {
       const int t = tof(L - 1), tp = tof(L >= 2 ? L - 2 : 0);
+      const uint32_t bits = drop ? (uint32_t)mbase[(size_t)t * 64] : 0xFFu;
 #pragma unroll
       for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(xs[xi], xrow(wid_c, p1_c, p2_c, E, PD));
 #pragma unroll
@@ -401,13 +414,21 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
         const float hv = from_elem(hbase[((size_t)tp * U4 + m) * 64]);
         hp[m] = (L >= 2 && valid) ? hv : 0.f;
         const float dv = from_elem(dH[(seqc * L + t) * (2 * U) + dir * U + 4 * m + q]);
-        const bool keep = !drop || dropout_keep_salted(dsalt, (uint32_t)((seqc * L + t) * U + 4 * m + q), thr);
+        const bool keep = (bits >> m) & 1u;
         dhin[m] = (valid && keep) ? dv * inv_kp : 0.f;
       }
     }
     float dh_rec[U4], dc_rec[U4];
 #pragma unroll
     for (int m = 0; m < U4; ++m) dh_rec[m] = dc_rec[m] = 0.f;
+    if (L & 1) {
+      // odd L: the tile's first dW chunk {L, L-1} is half filled; clear the dG columns of the missing
+      // step (they still hold the previous tile's last chunk)
+#pragma unroll
+      for (int m = 0; m < U4; ++m)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) dgT[(g4 * U + 4 * m + q) * RS + n + 16] = to_elem(0.f, (elem*)nullptr);
+    }
     for (int tau = L - 1; tau >= 0; --tau) {
       const int wid = wid_c, p1 = p1_c, p2 = p2_c;
       // ---- prefetch step tau-1 (x, h_{tau-2}, c_{tau-2}, dH_{tau-1}) and ids of tau-2
@@ -417,6 +438,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
       const int tn = tof(taun), tnp = tof(taunn), tnn = tof(taunn);
       const int wid_nn = word[rowbase + tnn], p1_nn = pos1[rowbase + tnn], p2_nn = pos2[rowbase + tnn];
       float xv_n[NX], hp_n[U4], cprev_n[U4], dhin_n[U4];
+      const uint32_t bits_n = drop ? (uint32_t)mbase[(size_t)tn * 64] : 0xFFu;
 #pragma unroll
       for (int xi = 0; xi < NX; ++xi) xv_n[xi] = gather_x(xs[xi], xrow(wid_n, p1_n, p2_n, E, PD));
 #pragma unroll
@@ -426,7 +448,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
         const float hv = from_elem(hbase[((size_t)tnp * U4 + m) * 64]);
         hp_n[m] = (n_has_prev && valid) ? hv : 0.f;
         const float dv = from_elem(dH[(seqc * L + tn) * (2 * U) + dir * U + 4 * m + q]);
-        const bool keep = !drop || dropout_keep_salted(dsalt, (uint32_t)((seqc * L + tn) * U + 4 * m + q), thr);
+        const bool keep = (bits_n >> m) & 1u;
         dhin_n[m] = (valid && keep) ? dv * inv_kp : 0.f;
       }
       // ---- recompute gates
@@ -446,8 +468,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
       float dg[U4][4];
 #pragma unroll
       for (int m = 0; m < NMT; ++m) {
-        f32x4_t acc = {lbias[0 * U + 4 * m + q], lbias[1 * U + 4 * m + q], lbias[2 * U + 4 * m + q],
-                       lbias[3 * U + 4 * m + q]};
+        f32x4_t acc = {bm[m][0], bm[m][1], bm[m][2], bm[m][3]};
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) acc = mma(lA[(m * NKS + ks) * 64 + lane], B[ks], acc);
         const float ig = sigmoidf_(acc[0]), jg = tanhf_(acc[1]), fg = sigmoidf_(acc[2] + 1.0f),
@@ -542,15 +563,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
             }
           }
         }
-        wave_lds_sync();
-#pragma unroll
-        for (int m = 0; m < U4; ++m)
-#pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) {
-            dgT[(g4 * U + 4 * m + q) * RS + n] = to_elem(0.f, (elem*)nullptr);
-            dgT[(g4 * U + 4 * m + q) * RS + n + 16] = to_elem(0.f, (elem*)nullptr);
-          }
-        wave_lds_sync();
+        wave_lds_sync();   // every later chunk rewrites both column halves: no clearing needed
       }
       // ---- rotate the pipeline
 #pragma unroll
@@ -626,7 +639,7 @@ static int launch_fwd_t(const LstmArgs& a, hipStream_t st) {
                      : (store ? lstm_fwd_kernel<U, NX, BF16, false, true> : lstm_fwd_kernel<U, NX, BF16, false, false>);
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, a.bias, (elem*)a.hraw,
-                     (typename CT<BF16>::type*)a.cst, (elem*)a.hdrop, a.seed, a.thr, a.inv_kp, a.drop);
+                     (typename CT<BF16>::type*)a.cst, (elem*)a.hdrop, a.dmask, a.seed, a.thr, a.inv_kp, a.drop);
   INA_CHECK_LAUNCH();
   return 0;
 }
@@ -645,7 +658,7 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   }
   hipLaunchKernelGGL(kfn, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, (const frag*)a.a2pack, a.bias,
-                     (const elem*)a.hraw, (const typename CT<BF16>::type*)a.cst, (const elem*)a.dH, a.dw_slab, a.dpos_slab, a.dwemb, a.seed, a.thr, a.inv_kp,
+                     (const elem*)a.hraw, (const typename CT<BF16>::type*)a.cst, (const elem*)a.dH, a.dw_slab, a.dpos_slab, a.dwemb, a.dmask, a.seed, a.thr, a.inv_kp,
                      a.drop);
   INA_CHECK_LAUNCH();
   return 0;

@@ -43,7 +43,7 @@ class EncoderFn(torch.autograd.Function):
         bias = torch.stack([bf.detach(), bb.detach()]).float().contiguous()
         need_grad = ctx.needs_input_grad[5:15].count(True) > 0 if hasattr(ctx, "needs_input_grad") else True
         kp = float(meta["keep_prob"])
-        hlane, cst, hnat = o.lstm_fwd(inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
+        hlane, cst, hnat, dmask = o.lstm_fwd(inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
                                       p2emb.detach().contiguous(), apack, bias, U, sh["NX"], bf16, bool(need_grad),
                                       int(meta["seed"]), kp)
         w1pack, w1tpack = pack_attn(W1, bf16)
@@ -51,7 +51,7 @@ class EncoderFn(torch.autograd.Function):
                                w2.detach().reshape(-1).contiguous(), U, bf16, int(meta.get("attn_blocks", 0)))
         if need_grad:
             ctx.save_for_backward(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst,
-                                  w1pack, w1tpack, b1, w2, alphas, hnat)
+                                  w1pack, w1tpack, b1, w2, alphas, hnat, dmask)
             ctx.meta = dict(meta, NX=sh["NX"], DIN=DIN)
         ctx.mark_non_differentiable(alphas)
         return e, alphas
@@ -60,7 +60,7 @@ class EncoderFn(torch.autograd.Function):
     def backward(ctx, de, _dalpha):
         o = ops()
         (inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst, w1pack, w1tpack, b1, w2,
-         alphas, hnat) = ctx.saved_tensors
+         alphas, hnat, dmask) = ctx.saved_tensors
         m = ctx.meta
         U, bf16, DIN = m["U"], m["bf16"], m["DIN"]
         H2 = 2 * U
@@ -74,7 +74,7 @@ class EncoderFn(torch.autograd.Function):
         word_grad = bool(m.get("word_grad", False))
         dw_slab, dpos_slab, dwemb = o.lstm_bwd(inst, word, pos1, pos2, wemb.detach().contiguous(),
                                                p1emb.detach().contiguous(), p2emb.detach().contiguous(), apack, a2pack,
-                                               bias, hlane, cst, dH, U, m["NX"], bf16, word_grad,
+                                               bias, hlane, cst, dH, dmask, U, m["NX"], bf16, word_grad,
                                                int(m.get("lstm_blocks", 0)), int(m["seed"]), float(m["keep_prob"]))
         D = dw_slab.sum(0)                         # [2, 4U, DIN+U+1]
         dKf = D[0, :, : DIN + U].t()

@@ -72,7 +72,7 @@ def test_lstm_forward(dtype):
     apack, _ = pack_lstm(p["lstm_fw_kernel"], p["lstm_bw_kernel"], U, DIN, bf16)
     bias = torch.stack([p["lstm_fw_bias"], p["lstm_bw_bias"]]).detach().float().contiguous()
     word, pos1, pos2, mask = dd.arrays()
-    hlane, cst, hraw = ops().lstm_fwd(inst, word, pos1, pos2, p["word_embedding"].detach(),
+    hlane, cst, hraw, _ = ops().lstm_fwd(inst, word, pos1, pos2, p["word_embedding"].detach(),
                                       p["pos1_embedding"].detach(), p["pos2_embedding"].detach(), apack, bias, U,
                                       sh["NX"], bf16, True, 0, 1.0)
     torch.cuda.synchronize()
@@ -107,7 +107,7 @@ def test_attention_forward(dtype, keep_prob):
     bias = torch.stack([p["lstm_fw_bias"], p["lstm_bw_bias"]]).detach().float().contiguous()
     word, pos1, pos2, mask = dd.arrays()
     seed = 1234
-    hlane, _, hdrop = ops().lstm_fwd(inst, word, pos1, pos2, p["word_embedding"].detach(),
+    hlane, _, hdrop, _ = ops().lstm_fwd(inst, word, pos1, pos2, p["word_embedding"].detach(),
                                      p["pos1_embedding"].detach(), p["pos2_embedding"].detach(), apack, bias, U,
                                      lstm_shape(U, DIN, bf16)["NX"], bf16, True, seed, keep_prob)
     hraw = _unpack_cst(hlane.float(), inst.shape[0], word.shape[1], U)

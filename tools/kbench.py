@@ -68,7 +68,7 @@ def main():
         return ts[len(ts) // 2], out
 
     res = {"tag": args.tag, "S": S}
-    t, (hlane, cst, hnat) = timed(lambda: o.lstm_fwd(inst, word, pos1, pos2, wemb, p1, p2, apack, bias, U, sh["NX"],
+    t, (hlane, cst, hnat, dmask) = timed(lambda: o.lstm_fwd(inst, word, pos1, pos2, wemb, p1, p2, apack, bias, U, sh["NX"],
                                                        True, True, 7, 0.9))
     res["lstm_fwd"] = t
     t, _ = timed(lambda: o.lstm_fwd(inst, word, pos1, pos2, wemb, p1, p2, apack, bias, U, sh["NX"], True, False, 7,
@@ -78,7 +78,7 @@ def main():
     res["attn_fwd"] = t
     t, (dH, aslab) = timed(lambda: o.attn_bwd(hnat, inst, w1pack, w1tpack, b1, w2, de, alphas, U, True, 0))
     res["attn_bwd"] = t
-    t, _ = timed(lambda: o.lstm_bwd(inst, word, pos1, pos2, wemb, p1, p2, apack, a2pack, bias, hlane, cst, dH, U,
+    t, _ = timed(lambda: o.lstm_bwd(inst, word, pos1, pos2, wemb, p1, p2, apack, a2pack, bias, hlane, cst, dH, dmask, U,
                                     sh["NX"], True, False, 0, 7, 0.9))
     res["lstm_bwd"] = t
     res["encoder_total"] = res["lstm_fwd"] + res["attn_fwd"] + res["attn_bwd"] + res["lstm_bwd"]
