@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--bert-len", type=int, default=128)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--hidden", type=int, default=20)
+    ap.add_argument("--word-dim", type=int, default=5, help="5 = reference train.py; paper config: --hidden 128 --word-dim 300")
     ap.add_argument("--profile-json", default="")
     args = ap.parse_args()
 
@@ -63,8 +64,8 @@ def main():
     if bert:
         cfg = cfg.replace(encoder="bert", bert_layers=args.bert_layers, bert_max_length=args.bert_len,
                           relation_head="reference")
-    data = make_synthetic(num_relations=64, instances_per_relation=700, max_length=37, vocab=400000, word_dim=5,
-                          seed=0)
+    data = make_synthetic(num_relations=64, instances_per_relation=700, max_length=37, vocab=400000,
+                          word_dim=args.word_dim, seed=0)
     if bert:   # random token ids over the BERT vocabulary, full-length sequences (worst case for L)
         import numpy as np
         from induction_network_on_fewrel_amd.data.bert_tokenize import synthetic_features
@@ -110,7 +111,7 @@ def main():
             "dtype": args.dtype,
             "data": ("synthetic (64 relations x 700 instances, " +
                      (f"L={cfg.bert_max_length} full-length token ids over a {cfg.bert_vocab} vocab"
-                      if bert else "L=37, 400k vocab, 5-d word table") + "); random-init weights"),
+                      if bert else f"L=37, 400k vocab, {args.word_dim}-d word table") + "); random-init weights"),
             "config": {
                 "model": (f"induction-network bert-base({cfg.bert_layers}x{cfg.bert_hidden}, {cfg.bert_heads} heads)"
                           f"+entity-pool->{cfg.bert_out_dim}, routing x3, ntn h=100" if bert else

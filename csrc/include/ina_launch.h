@@ -96,6 +96,29 @@ bool sampler_supported(int N, int K, int Q);
 int sample_episodes(const int* scopes, int R, int E, int N, int K, int Q, uint32_t seed, float nota_rate, int* idx,
                     int* lab, hipStream_t st);
 
+// ---------------------------------------------------------------- wide BiLSTM cell (lstm_wide.hip)
+struct LstmWideArgs {
+  int S, L, U;
+  const float* gx;    // [2][S][L][4U] fp32
+  const float* gh;    // [2][S][4U]
+  float* c;           // [2][S][U]
+  void* hcur;         // [2][S][U] bf16
+  void* hall;         // [2][S][L][U] bf16
+  float* call;        // [2][S][L][U]
+  void* acts;         // [2][S][L][4U] bf16
+  void* hout;         // [S][L][2U] bf16
+  const void* dH;     // [S][L][2U] bf16
+  const float* dhrec; // [2][S][U]
+  float* dcrec;       // [2][S][U]
+  void* dG;           // [2][S][L][4U] bf16
+  void* dGcur;        // [2][S][4U] bf16
+  uint32_t salt0, salt1, thr;
+  float inv_kp;
+  int drop;
+};
+int lstm_wide_fwd_step(const LstmWideArgs& a, int tau, hipStream_t st);
+int lstm_wide_bwd_step(const LstmWideArgs& a, int tau, hipStream_t st);
+
 // ---------------------------------------------------------------- BERT (csrc/kernels/bert.hip)
 struct BertLnArgs {          // y = LN(res + dropout(a)); HD = 256 * {1..4}
   const void* a;

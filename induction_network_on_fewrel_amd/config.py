@@ -54,6 +54,7 @@ class Config:
     relation_head: str = "reference"   # "reference": W[h*N, N] mixes classes; "paper": per-pair W_r in R^h
     encoder: str = "bilstm"            # "bilstm" | "bert"
     lstm_skip_padding: bool = False    # parity: process all L steps
+    lstm_impl: str = "auto"            # GPU BiLSTM: "fused" (lane-ownership kernel, u<=32) | "wide" (GEMM + cell kernels) | "auto"
     train_word_embedding: bool = False # only used when no pretrained table is given
 
     # BERT encoder (north star); BERT-base defaults

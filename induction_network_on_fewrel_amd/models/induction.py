@@ -20,7 +20,7 @@ from ..config import Config
 from . import reference as ref
 from .params import InductionParams
 
-GPU_SUPPORTED_U = (8, 20, 32)
+GPU_SUPPORTED_U = (8, 20, 32)   # fused BiLSTM kernel instantiations; other widths use ops/wide.py
 
 
 class InductionNetwork(nn.Module):
@@ -38,6 +38,25 @@ class InductionNetwork(nn.Module):
     def bert_pdict(self) -> Dict[str, torch.Tensor]:
         """HF name -> tensor view of the BERT encoder + projection parameters."""
         return {n: getattr(self.params, a) for a, n in self.params.names().items() if a.startswith("bert__")}
+
+    def use_fused_lstm(self, L: int) -> bool:
+        """Fused lane-ownership BiLSTM+attention kernels (u in GPU_SUPPORTED_U, input <= 64, L <= 64) or
+        the wide GEMM path (``lstm_impl`` forces either)."""
+        impl = self.cfg.lstm_impl
+        ok = self.cfg.hidden_size in GPU_SUPPORTED_U and self.params.input_dim <= 64 and L <= 64
+        if impl == "fused" and not ok:
+            raise NotImplementedError(f"fused BiLSTM kernels need u in {GPU_SUPPORTED_U}, input dim <= 64, L <= 64")
+        return ok if impl == "auto" else impl == "fused"
+
+    def _head(self, e, p, B, N, K, Q, grad_views):
+        """Fused routing + NTN kernels when instantiated for (H, N, Q), else the GEMM formulation."""
+        cfg = self.cfg
+        H = e.shape[1]
+        if H in (16, 40, 64) and N <= 16 and N * Q <= 64:
+            from ..ops.head import head
+            return head(e, p, dict(E=B, N=N, K=K, Q=Q, iters=cfg.routing_iters,
+                                   paper=(cfg.relation_head == "paper"), grad_views=grad_views))
+        return ref.head_forward(p, e.float(), B, N, K, Q, cfg.routing_iters, cfg.relation_head)
 
     def check_gpu_config(self, N: int, Q: int, L: int) -> None:
         u = self.cfg.hidden_size
@@ -66,17 +85,17 @@ class InductionNetwork(nn.Module):
         if cfg.encoder == "bert":
             return self._forward_bert(inst, data, B, N, K, Q, training, dropout_seed, grad_views, p, overlap)
         if inst.is_cuda:
-            from ..ops.encoder import encode
-            from ..ops.head import head
             word, pos1, pos2, mask = data
-            self.check_gpu_config(N, Q, word.shape[1])
-            meta = dict(U=cfg.hidden_size, bf16=(cfg.dtype == "bf16"), keep_prob=kp, seed=int(dropout_seed),
-                        word_grad=bool(isinstance(p["word_embedding"], nn.Parameter)
-                                       and p["word_embedding"].requires_grad), grad_views=grad_views)
-            e, alphas = encode(inst, data, p, meta)
-            probs = head(e, p, dict(E=B, N=N, K=K, Q=Q, iters=cfg.routing_iters,
-                                    paper=(cfg.relation_head == "paper"), grad_views=grad_views))
-            return probs, alphas
+            if self.use_fused_lstm(word.shape[1]):
+                from ..ops.encoder import encode
+                meta = dict(U=cfg.hidden_size, bf16=(cfg.dtype == "bf16"), keep_prob=kp, seed=int(dropout_seed),
+                            word_grad=bool(isinstance(p["word_embedding"], nn.Parameter)
+                                           and p["word_embedding"].requires_grad), grad_views=grad_views)
+                e, alphas = encode(inst, data, p, meta)
+            else:   # wide layers (e.g. the paper's u=128, E=300): GEMM + fused-cell path
+                from ..ops.wide import encode_wide
+                e, alphas = encode_wide(inst, data, p, cfg.hidden_size, kp, int(dropout_seed))
+            return self._head(e, p, B, N, K, Q, grad_views), alphas
         word, pos1, pos2, mask = (t[inst.long()] for t in data)
         probs, alphas = ref.forward(p, word, pos1, pos2, mask, B, N, K, Q, cfg.routing_iters, cfg.relation_head,
                                     kp, int(dropout_seed), bf16=False)
@@ -88,14 +107,8 @@ class InductionNetwork(nn.Module):
         cfg = self.cfg
         if inst.is_cuda:
             from ..ops.bert import bert_encode
-            from ..ops.head import head
             e = bert_encode(self, inst, data, training, int(dropout_seed), grad_views, overlap)
-            H = e.shape[1]
-            if H not in (16, 40, 64) or N > 16 or N * Q > 64:
-                raise NotImplementedError("GPU head kernels support H in {16,40,64}, N <= 16, N*Q <= 64")
-            probs = head(e, p, dict(E=B, N=N, K=K, Q=Q, iters=cfg.routing_iters,
-                                    paper=(cfg.relation_head == "paper"), grad_views=grad_views))
-            return probs, None
+            return self._head(e, p, B, N, K, Q, grad_views), None
         from . import bert as Bm
         ids, mask, e1, e2 = (t[inst.long()] for t in data)
         e = Bm.encode_ref(self.bert_pdict(), ids, mask, e1, e2, cfg, training, int(dropout_seed))

@@ -1,0 +1,64 @@
+"""Wide-layer GPU path (ops/wide.py + lstm_wide.hip): the paper configuration (u=128, 50-d words,
+H=256 head) and the wide path forced at u=20 against the fused kernels and the fp32 oracle."""
+import pytest
+import torch
+
+from induction_network_on_fewrel_amd.config import Config
+from induction_network_on_fewrel_amd.data import EpisodeSampler, make_synthetic
+from induction_network_on_fewrel_amd.models import InductionNetwork
+from induction_network_on_fewrel_amd.models import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _relerr(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+def _setup(u, E, impl, kp_train=True, N=5, K=2, Q=3, B=3, L=37):
+    cfg = Config(N=N, K=K, Q=Q, max_length=L, hidden_size=u, lstm_impl=impl, relation_head="reference")
+    data = make_synthetic(num_relations=10, instances_per_relation=30, max_length=L, vocab=800, word_dim=E, seed=1)
+    torch.manual_seed(0)
+    model = InductionNetwork(cfg, data.word_vec_mat, seed=3).to(DEV)
+    with torch.no_grad():
+        for n in ("lstm_fw_bias", "lstm_bw_bias", "attn_bias"):
+            getattr(model.params, n).copy_(torch.randn_like(getattr(model.params, n)) * 0.3)
+    idx, lab = EpisodeSampler(data, seed=2).next_batch_indices(B, N, K, Q)
+    inst = torch.tensor(idx.reshape(-1), dtype=torch.int32, device=DEV)
+    arrays = tuple(torch.as_tensor(a).to(DEV) for a in (data.data_word, data.data_pos1, data.data_pos2,
+                                                        data.data_mask))
+    return cfg, model, inst, arrays, torch.tensor(lab, device=DEV), (B, N, K, Q)
+
+
+@pytest.mark.parametrize("keep_prob", [1.0, 0.9])
+def test_paper_config_forward_backward_vs_oracle(keep_prob):
+    cfg, model, inst, arrays, lab, (B, N, K, Q) = _setup(128, 50, "auto")
+    cfg.keep_prob = keep_prob
+    assert not model.use_fused_lstm(37)
+    probs, _ = model(inst, arrays, B, N, K, Q, training=True, dropout_seed=5)
+    loss = model.loss(probs, lab)
+    loss.backward()
+    got = {k: v.grad.clone() for k, v in model.pdict().items() if v.grad is not None}
+    # fp32 oracle on the same device, same dropout masks (counter hash)
+    p = {k: v.detach().clone().requires_grad_(v.requires_grad) for k, v in model.pdict().items()}
+    w, a1, a2, m = (t[inst.long()] for t in arrays)
+    pr, _ = ref.forward(p, w.long(), a1.long(), a2.long(), m, B, N, K, Q, 3, "reference", keep_prob, 5, bf16=False)
+    model.loss(pr, lab).backward()
+    assert _relerr(probs.detach(), pr.detach()) < 3e-2
+    for k in ("lstm_fw_kernel", "lstm_bw_bias", "pos1_embedding", "attn_kernel", "W_s", "M"):
+        assert _relerr(got[k], p[k].grad) < 8e-2, k
+
+
+def test_wide_matches_fused_at_u20():
+    outs = []
+    for impl in ("fused", "wide"):
+        cfg, model, inst, arrays, lab, (B, N, K, Q) = _setup(20, 5, impl)
+        probs, _ = model(inst, arrays, B, N, K, Q, training=True, dropout_seed=9)
+        model.loss(probs, lab).backward()
+        outs.append((probs.detach(), model.params.lstm_fw_kernel.grad.clone(), model.params.attn_kernel.grad.clone()))
+    (p0, g0, a0), (p1, g1, a1) = outs
+    assert _relerr(p1, p0) < 2e-2
+    assert _relerr(g1, g0) < 6e-2
+    assert _relerr(a1, a0) < 6e-2
