@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--hidden", type=int, default=20)
     ap.add_argument("--word-dim", type=int, default=5, help="5 = reference train.py; paper config: --hidden 128 --word-dim 300")
     ap.add_argument("--profile-json", default="")
+    ap.add_argument("--graph", type=int, default=0, help="capture the BiLSTM train step as a hipGraph (1/0)")
     args = ap.parse_args()
 
     import torch
@@ -60,7 +61,7 @@ def main():
     args.way = args.way or (10 if bert else 5)
     cfg = Config(N=args.way, K=args.shot, Q=args.query, max_length=37, hidden_size=args.hidden, dtype=args.dtype,
                  episodes_per_step=B, seed=1234, resume=False, model_dir="/tmp/ina_bench",
-                 train_iter=args.steps + args.warmup)
+                 train_iter=args.steps + args.warmup, use_hip_graph=bool(args.graph) and not bert)
     if bert:
         cfg = cfg.replace(encoder="bert", bert_layers=args.bert_layers, bert_max_length=args.bert_len,
                           relation_head="reference")

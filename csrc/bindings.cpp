@@ -30,6 +30,17 @@ void check(const Tensor& t, const char* name, at::ScalarType dt) {
 void check_launch(int rc, const char* what) {
   TORCH_CHECK(rc == 0, "ina: ", what, " launch failed / unsupported configuration (rc=", rc, ")");
 }
+const float* dev_float(const std::optional<Tensor>& t, const char* name) {
+  if (!t.has_value() || !t->defined() || t->numel() == 0) return nullptr;
+  check(*t, name, at::kFloat);
+  return t->data_ptr<float>();
+}
+const int* dev_int(const std::optional<Tensor>& t, const char* name) {
+  if (!t.has_value() || !t->defined() || t->numel() == 0) return nullptr;
+  check(*t, name, at::kInt);
+  return t->data_ptr<int>();
+}
+
 int64_t frag_elems(bool bf16) { return bf16 ? 8 : 1; }
 uint32_t keep_threshold(double kp) {
   const double t = kp * 4294967296.0;
@@ -44,7 +55,8 @@ uint32_t keep_threshold(double kp) {
 std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
                                             const Tensor& pos2, const Tensor& wemb, const Tensor& p1emb,
                                             const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U,
-                                            int64_t NX, bool bf16, bool store_c, int64_t seed, double keep_prob) {
+                                            int64_t NX, bool bf16, bool store_c, int64_t seed, double keep_prob,
+                                            const std::optional<Tensor>& seed_dev) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -99,6 +111,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Te
   a.cst = store_c ? cst.data_ptr() : nullptr;
   a.hdrop = hnat.data_ptr();
   a.dmask = (store_c && drop) ? dmask.data_ptr<uint8_t>() : nullptr;
+  a.seed_dev = dev_int(seed_dev, "seed_dev");
   a.seed = (uint32_t)seed;
   a.thr = keep_threshold(keep_prob);
   a.inv_kp = (float)(1.0 / keep_prob);
@@ -410,7 +423,7 @@ std::tuple<Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tensor& e, c
 
 // ------------------------------------------------------------------ optim / misc
 void adam_step(Tensor p, Tensor m, Tensor v, const Tensor& g, const std::optional<Tensor>& l2mask, double lr_t,
-               double b1, double b2, double eps, double gscale, double l2) {
+               double b1, double b2, double eps, double gscale, double l2, const std::optional<Tensor>& lr_dev) {
   check(p, "p", at::kFloat);
   check(m, "m", at::kFloat);
   check(v, "v", at::kFloat);
@@ -425,12 +438,13 @@ void adam_step(Tensor p, Tensor m, Tensor v, const Tensor& g, const std::optiona
   }
   if (n == 0) return;
   check_launch(ina::adam_step(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), g.data_ptr<float>(), mk, n,
-                              (float)lr_t, (float)b1, (float)b2, (float)eps, (float)gscale, (float)l2, cur_stream()),
+                              (float)lr_t, (float)b1, (float)b2, (float)eps, (float)gscale, (float)l2,
+                              dev_float(lr_dev, "lr_dev"), cur_stream()),
                "adam_step");
 }
 
 void adagrad_step(Tensor p, Tensor acc, const Tensor& g, const std::optional<Tensor>& l2mask, double lr, double gscale,
-                  double l2) {
+                  double l2, const std::optional<Tensor>& lr_dev) {
   check(p, "p", at::kFloat);
   check(acc, "acc", at::kFloat);
   check(g, "g", at::kFloat);
@@ -443,7 +457,7 @@ void adagrad_step(Tensor p, Tensor acc, const Tensor& g, const std::optional<Ten
   }
   if (n == 0) return;
   check_launch(ina::adagrad_step(p.data_ptr<float>(), acc.data_ptr<float>(), g.data_ptr<float>(), mk, n, (float)lr,
-                                 (float)gscale, (float)l2, cur_stream()),
+                                 (float)gscale, (float)l2, dev_float(lr_dev, "lr_dev"), cur_stream()),
                "adagrad_step");
 }
 
@@ -458,7 +472,7 @@ void slab_reduce(const Tensor& slabs, Tensor out, bool accumulate) {
 }
 
 std::tuple<Tensor, Tensor> sample_episodes(const Tensor& scopes, int64_t E, int64_t N, int64_t K, int64_t Q, int64_t seed,
-                                           double nota_rate) {
+                                           double nota_rate, const std::optional<Tensor>& seed_dev) {
   check(scopes, "scopes", at::kInt);
   TORCH_CHECK(scopes.dim() == 2 && scopes.size(1) == 2, "ina.sample_episodes: scopes must be [R, 2]");
   const int64_t R = scopes.size(0);
@@ -468,12 +482,25 @@ std::tuple<Tensor, Tensor> sample_episodes(const Tensor& scopes, int64_t E, int6
   auto lab = at::empty({E, N * Q}, scopes.options());
   if (E == 0) return {idx, lab};
   check_launch(ina::sample_episodes(scopes.data_ptr<int>(), (int)R, (int)E, (int)N, (int)K, (int)Q, (uint32_t)seed,
-                                    (float)nota_rate, idx.data_ptr<int>(), lab.data_ptr<int>(), cur_stream()),
+                                    (float)nota_rate, idx.data_ptr<int>(), lab.data_ptr<int>(),
+                                    dev_int(seed_dev, "seed_dev"), cur_stream()),
                "sample_episodes");
   return {idx, lab};
 }
 
-int64_t abi_version() { return 1; }
+// per-step control block for HIP-graph replay (see optim.hip::step_control_kernel)
+void step_control(Tensor ctl, Tensor lrt, int64_t seedA, int64_t seedB, double lr0, double decay_steps,
+                  double decay_rate, bool staircase, bool constant, bool adam, double b1, double b2) {
+  check(ctl, "ctl", at::kInt);
+  check(lrt, "lrt", at::kFloat);
+  TORCH_CHECK(ctl.numel() >= 5 && lrt.numel() >= 1, "ina.step_control: ctl needs 5 ints, lrt 1 float");
+  check_launch(ina::step_control(ctl.data_ptr<int>(), lrt.data_ptr<float>(), (long long)seedA, (long long)seedB, lr0,
+                                 decay_steps, decay_rate, staircase ? 1 : 0, constant ? 1 : 0, adam ? 1 : 0, b1, b2,
+                                 cur_stream()),
+               "step_control");
+}
+
+int64_t abi_version() { return 2; }
 
 }  // namespace
 
@@ -491,4 +518,5 @@ TORCH_LIBRARY(ina, m) {
   m.def("adagrad_step", &adagrad_step);
   m.def("slab_reduce", &slab_reduce);
   m.def("sample_episodes", &sample_episodes);
+  m.def("step_control", &step_control);
 }

@@ -31,6 +31,7 @@ struct LstmArgs {
   int bwd_blocks;
   void* hdrop;
   unsigned char* dmask;  // [tiles][2][L][64] dropout keep bits (bit m = unit 4m+q), written by fwd, read by bwd
+  const int* seed_dev;   // optional device-resident dropout seed (overrides seed; HIP-graph replay)
   uint32_t seed, thr;
   float inv_kp;
   int drop;
@@ -88,13 +89,15 @@ int ntn_fwd(const NtnArgs& a, hipStream_t st);
 int ntn_bwd(const NtnArgs& a, hipStream_t st);
 
 int adam_step(float* p, float* m, float* v, const float* g, const unsigned char* l2mask, long n, float lr_t, float b1,
-              float b2, float eps, float gscale, float l2, hipStream_t st);
+              float b2, float eps, float gscale, float l2, const float* lr_dev, hipStream_t st);
 int adagrad_step(float* p, float* acc, const float* g, const unsigned char* l2mask, long n, float lr, float gscale,
-                 float l2, hipStream_t st);
+                 float l2, const float* lr_dev, hipStream_t st);
+int step_control(int* ctl, float* lrt, long long seedA, long long seedB, double lr0, double decay_steps,
+                 double decay_rate, int staircase, int constant, int adam, double b1, double b2, hipStream_t st);
 int slab_reduce(const float* slabs, long nslab, long len, float* out, int accumulate, hipStream_t st);
 bool sampler_supported(int N, int K, int Q);
 int sample_episodes(const int* scopes, int R, int E, int N, int K, int Q, uint32_t seed, float nota_rate, int* idx,
-                    int* lab, hipStream_t st);
+                    int* lab, const int* seed_dev, hipStream_t st);
 
 // ---------------------------------------------------------------- wide BiLSTM cell (lstm_wide.hip)
 struct LstmWideArgs {

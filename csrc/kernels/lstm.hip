@@ -151,7 +151,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     const typename FragT<BF16>::type* __restrict__ apack, const float* __restrict__ bias,
     typename FragT<BF16>::elem* __restrict__ hlane, typename CT<BF16>::type* __restrict__ cst,
     typename FragT<BF16>::elem* __restrict__ hnat, unsigned char* __restrict__ dmask, uint32_t seed, uint32_t thr,
-    float inv_kp, int drop) {
+    float inv_kp, int drop, const int* __restrict__ seed_dev) {
+  if (seed_dev) seed = (uint32_t)seed_dev[0];   // device-resident dropout seed (HIP-graph replay)
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
   using celem = typename CT<BF16>::type;
@@ -639,7 +640,7 @@ static int launch_fwd_t(const LstmArgs& a, hipStream_t st) {
                      : (store ? lstm_fwd_kernel<U, NX, BF16, false, true> : lstm_fwd_kernel<U, NX, BF16, false, false>);
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, a.bias, (elem*)a.hraw,
-                     (typename CT<BF16>::type*)a.cst, (elem*)a.hdrop, a.dmask, a.seed, a.thr, a.inv_kp, a.drop);
+                     (typename CT<BF16>::type*)a.cst, (elem*)a.hdrop, a.dmask, a.seed, a.thr, a.inv_kp, a.drop, a.seed_dev);
   INA_CHECK_LAUNCH();
   return 0;
 }

@@ -11,7 +11,8 @@
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                                                    const float* __restrict__ g, const unsigned char* __restrict__ l2mask,
                                                    long n, float lr_t, float b1, float b2, float eps, float gscale,
-                                                   float l2) {
+                                                   float l2, const float* __restrict__ lr_dev) {
+  if (lr_dev) lr_t = lr_dev[0];   // device-resident schedule (HIP-graph replay)
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float gi = g[i] * gscale;
@@ -28,7 +29,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
 __global__ __launch_bounds__(256) void adagrad_kernel(float* __restrict__ p, float* __restrict__ acc,
                                                       const float* __restrict__ g,
                                                       const unsigned char* __restrict__ l2mask, long n, float lr,
-                                                      float gscale, float l2) {
+                                                      float gscale, float l2, const float* __restrict__ lr_dev) {
+  if (lr_dev) lr = lr_dev[0];
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float gi = g[i] * gscale;
@@ -38,6 +40,32 @@ __global__ __launch_bounds__(256) void adagrad_kernel(float* __restrict__ p, flo
     acc[i] = a;
     p[i] = pi - lr * gi * rsqrtf(a);
   }
+}
+
+// Per-step control block for HIP-graph replay: a captured step cannot take new scalar kernel
+// arguments, so the per-step values are computed on the device by the graph's first kernel from
+// counters that live in device memory (the same formulas as the host: runtime/trainer.py
+// dropout_seed, ops/sampler.py seeds, ops/optim.py lr_at + TF1 Adam bias correction).
+// ctl: [0] dropout seed, [1] sampler seed, [2] global step, [3] sampler calls, [4] optimizer t
+// lrt: [0] learning rate for the optimizer kernel (Adam: bias-corrected lr_t)
+__global__ void step_control_kernel(int* __restrict__ ctl, float* __restrict__ lrt, long long seedA, long long seedB,
+                                    double lr0, double decay_steps, double decay_rate, int staircase, int constant,
+                                    int adam, double b1, double b2) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const long long step = ctl[2], calls = ctl[3];
+  const long long t = (long long)ctl[4] + 1;
+  ctl[0] = (int)((seedA + step * 97LL) & 0x7FFFFFFFLL);
+  ctl[1] = (int)((seedB + calls * 7919LL) & 0x7FFFFFFFLL);
+  double lr = lr0;
+  if (!constant) {
+    const double e = staircase ? floor((double)step / decay_steps) : (double)step / decay_steps;
+    lr = lr0 * pow(decay_rate, e);
+  }
+  if (adam) lr = lr * sqrt(1.0 - pow(b2, (double)t)) / (1.0 - pow(b1, (double)t));
+  lrt[0] = (float)lr;
+  ctl[2] = (int)(step + 1);
+  ctl[3] = (int)(calls + 1);
+  ctl[4] = (int)t;
 }
 
 // Sum `nslab` contiguous slabs of length `len` (fp32) into out (out = sum, or out += sum).
@@ -61,16 +89,24 @@ static int grid_for(long n) {
 }
 
 int adam_step(float* p, float* m, float* v, const float* g, const unsigned char* l2mask, long n, float lr_t, float b1,
-              float b2, float eps, float gscale, float l2, hipStream_t st) {
+              float b2, float eps, float gscale, float l2, const float* lr_dev, hipStream_t st) {
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, m, v, g, l2mask, n, lr_t, b1, b2, eps, gscale,
-                     l2);
+                     l2, lr_dev);
   INA_CHECK_LAUNCH();
   return 0;
 }
 
 int adagrad_step(float* p, float* acc, const float* g, const unsigned char* l2mask, long n, float lr, float gscale,
-                 float l2, hipStream_t st) {
-  hipLaunchKernelGGL(adagrad_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, acc, g, l2mask, n, lr, gscale, l2);
+                 float l2, const float* lr_dev, hipStream_t st) {
+  hipLaunchKernelGGL(adagrad_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, acc, g, l2mask, n, lr, gscale, l2, lr_dev);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int step_control(int* ctl, float* lrt, long long seedA, long long seedB, double lr0, double decay_steps,
+                 double decay_rate, int staircase, int constant, int adam, double b1, double b2, hipStream_t st) {
+  hipLaunchKernelGGL(step_control_kernel, dim3(1), dim3(64), 0, st, ctl, lrt, seedA, seedB, lr0, decay_steps, decay_rate,
+                     staircase, constant, adam, b1, b2);
   INA_CHECK_LAUNCH();
   return 0;
 }

@@ -32,7 +32,9 @@ constexpr int MAXNQ = 512;  // N * Q
 
 __global__ __launch_bounds__(64) void sample_episodes_kernel(const int* __restrict__ scopes, int R, int E, int N, int K,
                                                              int Q, uint32_t seed, float nota_rate,
-                                                             int* __restrict__ idx_out, int* __restrict__ lab_out) {
+                                                             int* __restrict__ idx_out, int* __restrict__ lab_out,
+                                                             const int* __restrict__ seed_dev) {
+  if (seed_dev) seed = (uint32_t)seed_dev[0];   // device-resident seed (HIP-graph replay)
   const int ep = blockIdx.x * blockDim.x + threadIdx.x;
   if (ep >= E) return;
   Rng rng{hash_u32(seed * 0x85EBCA77u + 0x27D4EB2Fu) ^ hash_u32((uint32_t)ep + 0x165667B1u), 0u};
@@ -107,9 +109,9 @@ namespace ina {
 bool sampler_supported(int N, int K, int Q) { return N <= MAXN && K + Q <= MAXKQ && N * Q <= MAXNQ; }
 
 int sample_episodes(const int* scopes, int R, int E, int N, int K, int Q, uint32_t seed, float nota_rate, int* idx,
-                    int* lab, hipStream_t st) {
+                    int* lab, const int* seed_dev, hipStream_t st) {
   hipLaunchKernelGGL(sample_episodes_kernel, dim3((E + 63) / 64), dim3(64), 0, st, scopes, R, E, N, K, Q, seed,
-                     nota_rate, idx, lab);
+                     nota_rate, idx, lab, seed_dev);
   INA_CHECK_LAUNCH();
   return 0;
 }

@@ -72,7 +72,8 @@ class InductionNetwork(nn.Module):
 
     def forward(self, inst: torch.Tensor, data: Tuple[torch.Tensor, ...], B: int, N: int, K: int, Q: int,
                 training: bool = True, dropout_seed: int = 0,
-                grad_views: Optional[Dict[str, torch.Tensor]] = None, overlap=None) -> Tuple[torch.Tensor, torch.Tensor]:
+                grad_views: Optional[Dict[str, torch.Tensor]] = None, overlap=None,
+                seed_dev: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """inst: int32 [B*(N*K+N*Q)] instance rows (episode layout, support first).
         data: (word, pos1, pos2, mask) [NI, L] int32 on the same device.
         Returns probs [B, N*Q, N] and alphas [B*(N*K+N*Q), L]."""
@@ -90,7 +91,8 @@ class InductionNetwork(nn.Module):
                 from ..ops.encoder import encode
                 meta = dict(U=cfg.hidden_size, bf16=(cfg.dtype == "bf16"), keep_prob=kp, seed=int(dropout_seed),
                             word_grad=bool(isinstance(p["word_embedding"], nn.Parameter)
-                                           and p["word_embedding"].requires_grad), grad_views=grad_views)
+                                           and p["word_embedding"].requires_grad), grad_views=grad_views,
+                            seed_dev=seed_dev)
                 e, alphas = encode(inst, data, p, meta)
             else:   # wide layers (e.g. the paper's u=128, E=300): GEMM + fused-cell path
                 from ..ops.wide import encode_wide

@@ -45,7 +45,7 @@ class EncoderFn(torch.autograd.Function):
         kp = float(meta["keep_prob"])
         hlane, cst, hnat, dmask = o.lstm_fwd(inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
                                       p2emb.detach().contiguous(), apack, bias, U, sh["NX"], bf16, bool(need_grad),
-                                      int(meta["seed"]), kp)
+                                      int(meta["seed"]), kp, meta.get("seed_dev"))
         w1pack, w1tpack = pack_attn(W1, bf16)
         e, alphas = o.attn_fwd(hnat, inst, mask, w1pack, b1.detach().contiguous(),
                                w2.detach().reshape(-1).contiguous(), U, bf16, int(meta.get("attn_blocks", 0)))

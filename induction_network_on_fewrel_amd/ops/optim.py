@@ -108,16 +108,19 @@ class FusedOptimizer:
             return {"m": self.m, "v": self.v}
         return {"acc": self.acc}
 
-    def step(self, lr: float, grad_scale: float = 1.0) -> None:
+    def step(self, lr: float, grad_scale: float = 1.0, lr_dev: Optional[torch.Tensor] = None) -> None:
+        """``lr_dev``: device scalar holding the (bias-corrected for Adam) rate, overriding ``lr``
+        (HIP-graph replay: written by ina.step_control inside the captured step)."""
         self.t += 1
         p, g = self.flat.flat, self.flat.grad
         if p.is_cuda:
             o = ops()
             if self.kind == "adam":
                 lr_t = lr * math.sqrt(1 - self.b2 ** self.t) / (1 - self.b1 ** self.t)
-                o.adam_step(p, self.m, self.v, g, self.l2_mask, lr_t, self.b1, self.b2, self.eps, grad_scale, self.l2)
+                o.adam_step(p, self.m, self.v, g, self.l2_mask, lr_t, self.b1, self.b2, self.eps, grad_scale, self.l2,
+                            lr_dev)
             else:
-                o.adagrad_step(p, self.acc, g, self.l2_mask, lr, grad_scale, self.l2)
+                o.adagrad_step(p, self.acc, g, self.l2_mask, lr, grad_scale, self.l2, lr_dev)
             return
         with torch.no_grad():
             gg = g * grad_scale

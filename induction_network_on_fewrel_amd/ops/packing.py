@@ -9,6 +9,19 @@ from __future__ import annotations
 
 from functools import lru_cache
 
+_DEV_CACHE = {}
+
+
+def _on(t: torch.Tensor, dev) -> torch.Tensor:
+    """Device copy of a cached (lru_cache'd, hence immortal) host index tensor, made once: no per-step
+    host-to-device copies (and HIP-graph capturable)."""
+    key = (id(t), str(dev))
+    v = _DEV_CACHE.get(key)
+    if v is None:
+        v = t.to(dev)
+        _DEV_CACHE[key] = v
+    return v
+
 import numpy as np
 import torch
 
@@ -76,7 +89,7 @@ def pack_lstm(Wf: torch.Tensor, Wb: torch.Tensor, U: int, DIN: int, bf16: bool):
     """-> (apack [2, NMT, NKS, 64, KPL], a2pack [2, NMT2, NKS2, 64, KPL]) in bf16 or fp32."""
     fi, bi = _lstm_idx(U, DIN, bf16)
     dev = Wf.device
-    fi, bi = fi.to(dev), bi.to(dev)
+    fi, bi = _on(fi, dev), _on(bi, dev)
     dt = torch.bfloat16 if bf16 else torch.float32
     outs_f, outs_b = [], []
     for W in (Wf, Wb):
@@ -126,7 +139,7 @@ def pack_attn(W1: torch.Tensor, bf16: bool):
     dev = W1.device
     We = torch.cat([W1.detach().float().reshape(-1), W1.new_zeros(1, dtype=torch.float32)])
     dt = torch.bfloat16 if bf16 else torch.float32
-    return We[pi.to(dev)].to(dt).contiguous(), We[ti.to(dev)].to(dt).contiguous()
+    return We[_on(pi, dev)].to(dt).contiguous(), We[_on(ti, dev)].to(dt).contiguous()
 
 
 # ------------------------------------------------------------------ NTN (bf16 only)
@@ -187,11 +200,11 @@ def pack_ntn_M(M: torch.Tensor):
     mi, m2i = _ntn_m_idx(H, h)
     dev = M.device
     Me = torch.cat([M.detach().float().reshape(-1), M.new_zeros(1, dtype=torch.float32)])
-    return Me[mi.to(dev)].to(torch.bfloat16).contiguous(), Me[m2i.to(dev)].to(torch.bfloat16).contiguous()
+    return Me[_on(mi, dev)].to(torch.bfloat16).contiguous(), Me[_on(m2i, dev)].to(torch.bfloat16).contiguous()
 
 
 def pack_ntn_w(w: torch.Tensor, h: int, N: int):
     wi, wti = _ntn_w_idx(h, N)
     dev = w.device
     we = torch.cat([w.detach().float().reshape(-1), w.new_zeros(1, dtype=torch.float32)])
-    return we[wi.to(dev)].to(torch.bfloat16).contiguous(), we[wti.to(dev)].to(torch.bfloat16).contiguous()
+    return we[_on(wi, dev)].to(torch.bfloat16).contiguous(), we[_on(wti, dev)].to(torch.bfloat16).contiguous()

@@ -42,11 +42,16 @@ class DeviceEpisodeSampler:
         self.nota_rate = float(nota_rate)
         self.calls = 0
 
-    def sample(self, B: int, N: int, K: int, Q: int):
-        """-> (idx int32 [B, N*K+N*Q], labels int32 [B, N*Q]) on the device."""
+    def sample(self, B: int, N: int, K: int, Q: int, seed_dev=None):
+        """-> (idx int32 [B, N*K+N*Q], labels int32 [B, N*Q]) on the device.  ``seed_dev`` (int32
+        device scalar) replaces the host seed (HIP-graph replay; runtime/graph.py)."""
         s = (self.seed * 1000003 + self.calls * 7919) & 0x7FFFFFFF
         self.calls += 1
-        return ops().sample_episodes(self.dd.scopes, B, N, K, Q, s, self.nota_rate)
+        return ops().sample_episodes(self.dd.scopes, B, N, K, Q, s, self.nota_rate, seed_dev)
+
+    def seed_base(self) -> int:
+        """seed(calls) = (seed_base + calls * 7919) mod 2^31 (the device step-control formula)."""
+        return (self.seed * 1000003) & 0x7FFFFFFF
 
     def state_dict(self):
         return {"seed": self.seed, "calls": self.calls}

@@ -101,6 +101,7 @@ class Trainer:
         self.timers = {"sample": 0.0, "fwd_bwd": 0.0, "allreduce": 0.0, "optim": 0.0}   # host (launch) time
         self.gpu_phase_ms = {k: 0.0 for k in self.timers}                                # HIP-event time
         self._pending_events = []
+        self._graph = None   # runtime/graph.py::GraphedTrainStep when cfg.use_hip_graph
         # fault injection (tests / chaos runs): raise at a given global step on a given rank
         self._fault_step = int(os.environ.get("INA_FAULT_STEP", "-1"))
         self._fault_rank = int(os.environ.get("INA_FAULT_RANK", "0"))
@@ -152,6 +153,14 @@ class Trainer:
         buffer (grad_views), which is also the DP all-reduce bucket and the fused optimizer input."""
         cfg = self.cfg
         B, N, K, Q = cfg.episodes_per_step, cfg.N, cfg.K, cfg.Q
+        if (cfg.use_hip_graph and self.device.type == "cuda" and cfg.encoder == "bilstm"
+                and self.global_step != self._fault_step):
+            if self._graph is None:
+                from .graph import GraphedTrainStep
+                self._graph = GraphedTrainStep(self)   # first step eager (warm-up) + capture, then replays
+            self._last_lr = lr_at(self.global_step, cfg.learning_rate, cfg.decay_steps, cfg.decay_rate,
+                                  cfg.staircase, cfg.lr_schedule)
+            return self._graph.step()
         if self.global_step == self._fault_step and self.dist.rank == self._fault_rank:
             raise RuntimeError(f"injected fault at step {self.global_step} on rank {self.dist.rank} (INA_FAULT_STEP)")
         t0 = time.perf_counter()

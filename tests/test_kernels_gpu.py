@@ -74,7 +74,7 @@ def test_lstm_forward(dtype):
     word, pos1, pos2, mask = dd.arrays()
     hlane, cst, hraw, _ = ops().lstm_fwd(inst, word, pos1, pos2, p["word_embedding"].detach(),
                                       p["pos1_embedding"].detach(), p["pos2_embedding"].detach(), apack, bias, U,
-                                      sh["NX"], bf16, True, 0, 1.0)
+                                      sh["NX"], bf16, True, 0, 1.0, None)
     torch.cuda.synchronize()
     w, a1, a2, _ = _gathered(dd, inst)
     with torch.no_grad():
@@ -109,7 +109,7 @@ def test_attention_forward(dtype, keep_prob):
     seed = 1234
     hlane, _, hdrop, _ = ops().lstm_fwd(inst, word, pos1, pos2, p["word_embedding"].detach(),
                                      p["pos1_embedding"].detach(), p["pos2_embedding"].detach(), apack, bias, U,
-                                     lstm_shape(U, DIN, bf16)["NX"], bf16, True, seed, keep_prob)
+                                     lstm_shape(U, DIN, bf16)["NX"], bf16, True, seed, keep_prob, None)
     hraw = _unpack_cst(hlane.float(), inst.shape[0], word.shape[1], U)
     w1p, _ = pack_attn(p["attn_kernel"], bf16)
     e, alphas = ops().attn_fwd(hdrop, inst, mask, w1p, p["attn_bias"].detach().contiguous(),
@@ -238,7 +238,7 @@ def test_adam_matches_tf_formula():
     p0 = p.clone()
     b1, b2, eps, lr = 0.9, 0.999, 1e-8, 1e-3
     lr_t = lr * (1 - b2) ** 0.5 / (1 - b1)
-    ops().adam_step(p, m, v, g, None, lr_t, b1, b2, eps, 1.0, 0.0)
+    ops().adam_step(p, m, v, g, None, lr_t, b1, b2, eps, 1.0, 0.0, None)
     m_r = (1 - b1) * g
     v_r = (1 - b2) * g * g
     p_r = p0 - lr_t * m_r / (v_r.sqrt() + eps)
@@ -291,3 +291,21 @@ def test_full_model_matches_oracle(dtype):
         err = _relerr(prm.grad.cpu(), getattr(cpu_model.params, name).grad)
         print(f"  grad {name}: {err:.2e}")
         assert err < 8e-2, name
+
+
+def test_hip_graph_step_matches_eager(tmp_path):
+    """runtime/graph.py: the captured train step (device-resident seeds / LR) follows the eager
+    trajectory (same episodes, dropout masks and Adam updates)."""
+    from induction_network_on_fewrel_amd.runtime.trainer import Trainer
+    data = make_synthetic(num_relations=12, instances_per_relation=40, vocab=500, seed=0)
+    runs = []
+    for graph in (False, True):
+        cfg = Config(N=5, K=2, Q=3, episodes_per_step=16, model_dir=str(tmp_path / f"g{int(graph)}"), seed=4,
+                     resume=False, use_hip_graph=graph, learning_rate=1e-2)
+        tr = Trainer(cfg, data, None, device="cuda", log=False)
+        losses = [float(tr.train_step()[0]) for _ in range(6)]
+        runs.append((losses, tr.flat.flat.detach().clone(), tr.global_step, tr.opt.t, tr.train_eps.calls))
+    (l0, p0, s0, t0, c0), (l1, p1, s1, t1, c1) = runs
+    assert (s0, t0, c0) == (s1, t1, c1) == (6, 6, 6)
+    assert max(abs(a - b) for a, b in zip(l0, l1)) < 1e-4
+    assert _relerr(p1, p0) < 1e-4

@@ -69,10 +69,10 @@ def main():
 
     res = {"tag": args.tag, "S": S}
     t, (hlane, cst, hnat, dmask) = timed(lambda: o.lstm_fwd(inst, word, pos1, pos2, wemb, p1, p2, apack, bias, U, sh["NX"],
-                                                       True, True, 7, 0.9))
+                                                       True, True, 7, 0.9, None))
     res["lstm_fwd"] = t
     t, _ = timed(lambda: o.lstm_fwd(inst, word, pos1, pos2, wemb, p1, p2, apack, bias, U, sh["NX"], True, False, 7,
-                                    1.0))
+                                    1.0, None))
     res["lstm_fwd_infer"] = t
     t, (e, alphas) = timed(lambda: o.attn_fwd(hnat, inst, mask, w1pack, b1, w2, U, True, 0))
     res["attn_fwd"] = t
