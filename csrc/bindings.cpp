@@ -292,8 +292,8 @@ Tensor routing_fwd(const Tensor& e, const Tensor& Ws, int64_t E, int64_t N, int6
   TORCH_CHECK(ina::routing_lds_bytes((int)N, (int)K, (int)H, (int)R, false) <= 160 * 1024, "ina.routing_fwd: N*K too large");
   auto cls = at::empty({E, N, H}, e.options());
   if (E == 0) return cls;
-  if (blocks <= 0) blocks = 4096;
-  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, E));
+  if (blocks <= 0) blocks = 8192;   // work items = (episode, class) pairs
+  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, E * N));
   check_launch(ina::routing_fwd(e.data_ptr<float>(), Ws.data_ptr<float>(), (int)E, (int)N, (int)K, (int)Q, (int)R,
                                 (int)H, cls.data_ptr<float>(), (int)blocks, cur_stream()),
                "routing_fwd");
@@ -311,8 +311,8 @@ Tensor routing_bwd(const Tensor& e, const Tensor& Ws, const Tensor& dcls, Tensor
   TORCH_CHECK(de.sizes() == e.sizes(), "ina.routing_bwd: de shape");
   TORCH_CHECK(dcls.numel() == E * N * H, "ina.routing_bwd: dcls shape");
   TORCH_CHECK(ina::routing_lds_bytes((int)N, (int)K, (int)H, (int)R, true) <= 160 * 1024, "ina.routing_bwd: N*K too large");
-  if (blocks <= 0) blocks = 2048;
-  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, std::max<int64_t>(E, 1)));
+  if (blocks <= 0) blocks = 4096;   // work items = (episode, class) pairs; slab per block
+  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, std::max<int64_t>(E * N, 1)));
   auto slab = at::zeros({blocks, H, H}, e.options());
   if (E == 0) return slab;
   check_launch(ina::routing_bwd(e.data_ptr<float>(), Ws.data_ptr<float>(), (int)E, (int)N, (int)K, (int)Q, (int)R,

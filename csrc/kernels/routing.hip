@@ -8,10 +8,11 @@
 //   return c        (the last b update is unused)
 //   squash(v) = v * n/(1+n) / sqrt(n + 1e-9),  n = |v|^2
 //
-// One wave per episode, lane = feature column h (H <= 64).  The backward recomputes the
-// forward keeping every iteration's (d, c_hat, c, n) in wave-private LDS, then runs the exact
-// reverse-mode recurrence through all iterations (softmax / squash / agreement update), and
-// accumulates dW_s = S^T dE_hat in registers across the episodes the wave visits.
+// One wave per (episode, class) work item (classes route independently; W_s is the only shared
+// operand), lane = feature column h (H <= 64).  The backward recomputes the forward keeping every
+// iteration's (d, c_hat, c, n) in wave-private LDS, then runs the exact reverse-mode recurrence
+// through all iterations (softmax / squash / agreement update), and accumulates dW_s = S^T dE_hat
+// in registers across the work items the wave visits.
 #include "ina_common.h"
 
 using namespace ina;
@@ -31,54 +32,56 @@ INA_DEVICE float squash_scale_grad(float n) {
   return (n + 2e-9f - n * n) / (2.f * r * r * r * onep * onep);
 }
 
-// per-wave LDS carve (floats): sup[NK*H] eh[NK*H] deh[NK*H] chat[R*N*H] cv[R*N*H] d[R*NK] n2[R*N] b[NK] gb[NK] dd[NK]
+// per-wave LDS carve (floats), ONE class of one episode per work item:
+//   sup[K*H] eh[K*H] deh[K*H] chat[R*H] cv[R*H] d[R*K] n2[R] b[K] gb[K] dd[K]
+// (routing is independent across the N classes of an episode: the only shared operand is W_s, so
+// the work is split per (episode, class) -- N times more waves, N times shorter serial chains)
 __host__ __device__ inline size_t rt_wave_floats(int N, int K, int H, int R) {
-  const int NK = N * K;
-  return (size_t)3 * NK * H + (size_t)2 * R * N * H + (size_t)R * NK + R * N + 3 * NK;
+  (void)N;
+  return (size_t)3 * K * H + (size_t)2 * R * H + (size_t)R * K + R + 3 * K;
 }
 
 template <int H>
-INA_DEVICE void routing_forward(const float* __restrict__ e, long sup_row0, int N, int K, int R, const float* ws_col,
+INA_DEVICE void routing_forward(const float* __restrict__ e, long sup_row0, int K, int R, const float* ws_col,
                                 float* sup, float* eh, float* chat_s, float* cv_s, float* d_s, float* n2_s, float* b,
                                 int lane) {
-  const int NK = N * K;
   const int h = lane;
   if (h < H)
-    for (int ck = 0; ck < NK; ++ck) sup[ck * H + h] = e[(sup_row0 + ck) * H + h];
+    for (int k = 0; k < K; ++k) sup[k * H + h] = e[(sup_row0 + k) * H + h];
   wave_lds_sync();
-  for (int ck = 0; ck < NK; ++ck) {
+  for (int k = 0; k < K; ++k) {
     float acc = 0.f;
 #pragma unroll
-    for (int a = 0; a < H; ++a) acc += sup[ck * H + a] * ws_col[a];
-    if (h < H) eh[ck * H + h] = acc;
-    if (lane == 0) b[ck] = 0.f;
+    for (int a = 0; a < H; ++a) acc += sup[k * H + a] * ws_col[a];
+    if (h < H) eh[k * H + h] = acc;
+    if (lane == 0) b[k] = 0.f;
   }
   wave_lds_sync();
   for (int r = 0; r < R; ++r) {
-    for (int c = 0; c < N; ++c) {
-      float mx = -INFINITY;
-      for (int k = 0; k < K; ++k) mx = fmaxf(mx, b[c * K + k]);
-      float den = 0.f;
-      for (int k = 0; k < K; ++k) den += __expf(b[c * K + k] - mx);
-      float ch = 0.f;
+    float mx = -INFINITY;
+    for (int k = 0; k < K; ++k) mx = fmaxf(mx, b[k]);
+    float den = 0.f;
+    for (int k = 0; k < K; ++k) den += __expf(b[k] - mx);
+    const float inv = 1.f / den;
+    float ch = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float dk = __expf(b[k] - mx) * inv;
+      if (lane == 0) d_s[r * K + k] = dk;
+      ch += dk * (h < H ? eh[k * H + h] : 0.f);
+    }
+    const float n2 = wave_sum(h < H ? ch * ch : 0.f);
+    const float cvh = ch * squash_scale(n2);
+    if (h < H) {
+      chat_s[r * H + h] = ch;
+      cv_s[r * H + h] = cvh;
+    }
+    if (lane == 0) n2_s[r] = n2;
+    if (r + 1 < R) {   // the last agreement update is unused (reference quirk)
       for (int k = 0; k < K; ++k) {
-        const float dk = __expf(b[c * K + k] - mx) / den;
-        if (lane == 0) d_s[r * NK + c * K + k] = dk;
-        ch += dk * (h < H ? eh[(c * K + k) * H + h] : 0.f);
+        const float ag = wave_sum(h < H ? eh[k * H + h] * cvh : 0.f);
+        if (lane == 0) b[k] += ag;
       }
-      const float n2 = wave_sum(h < H ? ch * ch : 0.f);
-      const float cvh = ch * squash_scale(n2);
-      if (h < H) {
-        chat_s[(r * N + c) * H + h] = ch;
-        cv_s[(r * N + c) * H + h] = cvh;
-      }
-      if (lane == 0) n2_s[r * N + c] = n2;
-      for (int k = 0; k < K; ++k) {
-        const float ag = wave_sum(h < H ? eh[(c * K + k) * H + h] * cvh : 0.f);
-        wave_lds_sync();
-        if (lane == 0) b[c * K + k] += ag;
-        wave_lds_sync();
-      }
+      wave_lds_sync();
     }
   }
 }
@@ -90,23 +93,23 @@ __global__ __launch_bounds__(64) void routing_fwd_kernel(const float* __restrict
                                                          int N, int K, int Q, int R, float* __restrict__ cls) {
   extern __shared__ __attribute__((aligned(16))) float rsm[];
   const int lane = threadIdx.x;
-  const int NK = N * K;
   float* sup = rsm;
-  float* eh = sup + NK * H;
-  float* deh = eh + NK * H;
-  float* chat = deh + NK * H;
-  float* cv = chat + R * N * H;
-  float* d = cv + R * N * H;
-  float* n2 = d + R * NK;
-  float* b = n2 + R * N;
+  float* eh = sup + K * H;
+  float* deh = eh + K * H;
+  float* chat = deh + K * H;
+  float* cv = chat + R * H;
+  float* d = cv + R * H;
+  float* n2 = d + R * K;
+  float* b = n2 + R;
   float ws_col[H];
 #pragma unroll
   for (int a = 0; a < H; ++a) ws_col[a] = lane < H ? Ws[a * H + lane] : 0.f;
-  for (int ep = blockIdx.x; ep < E; ep += gridDim.x) {
-    const long row0 = (long)ep * (NK + N * Q);
-    routing_forward<H>(e, row0, N, K, R, ws_col, sup, eh, chat, cv, d, n2, b, lane);
-    if (lane < H)
-      for (int c = 0; c < N; ++c) cls[((long)ep * N + c) * H + lane] = cv[((R - 1) * N + c) * H + lane];
+  const int NK = N * K;
+  for (int w = blockIdx.x; w < E * N; w += gridDim.x) {
+    const int ep = w / N, c = w - ep * N;
+    const long row0 = (long)ep * (NK + N * Q) + (long)c * K;
+    routing_forward<H>(e, row0, K, R, ws_col, sup, eh, chat, cv, d, n2, b, lane);
+    if (lane < H) cls[((long)ep * N + c) * H + lane] = cv[(R - 1) * H + lane];
     wave_lds_sync();
   }
 }
@@ -118,80 +121,81 @@ __global__ __launch_bounds__(64) void routing_bwd_kernel(const float* __restrict
                                                          float* __restrict__ de, float* __restrict__ dws_slab) {
   extern __shared__ __attribute__((aligned(16))) float rsm[];
   const int lane = threadIdx.x, h = lane;
-  const int NK = N * K;
   float* sup = rsm;
-  float* eh = sup + NK * H;
-  float* deh = eh + NK * H;
-  float* chat = deh + NK * H;
-  float* cv = chat + R * N * H;
-  float* d = cv + R * N * H;
-  float* n2 = d + R * NK;
-  float* b = n2 + R * N;
-  float* gb = b + NK;
-  float* dd = gb + NK;
-  float* wsl = dd + NK;  // [H][H] W_s row-major (for dS = dE_hat W_s^T)
+  float* eh = sup + K * H;
+  float* deh = eh + K * H;
+  float* chat = deh + K * H;
+  float* cv = chat + R * H;
+  float* d = cv + R * H;
+  float* n2 = d + R * K;
+  float* b = n2 + R;
+  float* gb = b + K;
+  float* dd = gb + K;
+  float* wst = dd + K;  // [H][H] W_s^T (wst[h*H + a] = W_s[a][h]): dS reads are lane-contiguous
   float ws_col[H], dws[H];
 #pragma unroll
   for (int a = 0; a < H; ++a) {
     ws_col[a] = lane < H ? Ws[a * H + lane] : 0.f;
     dws[a] = 0.f;
   }
-  for (int i = lane; i < H * H; i += 64) wsl[i] = Ws[i];
+  for (int i = lane; i < H * H; i += 64) {
+    const int a = i / H, hh = i - a * H;
+    wst[hh * H + a] = Ws[i];
+  }
   wave_lds_sync();
-  for (int ep = blockIdx.x; ep < E; ep += gridDim.x) {
-    const long row0 = (long)ep * (NK + N * Q);
-    routing_forward<H>(e, row0, N, K, R, ws_col, sup, eh, chat, cv, d, n2, b, lane);
-    for (int ck = 0; ck < NK; ++ck) {
-      if (h < H) deh[ck * H + h] = 0.f;
-      if (lane == 0) gb[ck] = 0.f;
+  const int NK = N * K;
+  for (int w = blockIdx.x; w < E * N; w += gridDim.x) {
+    const int ep = w / N, c = w - ep * N;
+    const long row0 = (long)ep * (NK + N * Q) + (long)c * K;
+    routing_forward<H>(e, row0, K, R, ws_col, sup, eh, chat, cv, d, n2, b, lane);
+    for (int k = 0; k < K; ++k) {
+      if (h < H) deh[k * H + h] = 0.f;
+      if (lane == 0) gb[k] = 0.f;
     }
     wave_lds_sync();
     for (int r = R - 1; r >= 0; --r) {
-      for (int c = 0; c < N; ++c) {
-        // gradient into c_r: from the output (last iteration) and from b_{r+1} = b_r + e_hat . c_r
-        float dc = (r == R - 1 && h < H) ? dcls[((long)ep * N + c) * H + h] : 0.f;
-        const float cvh = h < H ? cv[(r * N + c) * H + h] : 0.f;
-        for (int k = 0; k < K; ++k) {
-          const float g = gb[c * K + k];
-          if (h < H) {
-            dc += g * eh[(c * K + k) * H + h];
-            deh[(c * K + k) * H + h] += g * cvh;
-          }
+      // gradient into c_r: from the output (last iteration) and from b_{r+1} = b_r + e_hat . c_r
+      float dc = (r == R - 1 && h < H) ? dcls[((long)ep * N + c) * H + h] : 0.f;
+      const float cvh = h < H ? cv[r * H + h] : 0.f;
+      for (int k = 0; k < K; ++k) {
+        const float g = gb[k];
+        if (h < H) {
+          dc += g * eh[k * H + h];
+          deh[k * H + h] += g * cvh;
         }
-        // squash backward
-        const float ch = h < H ? chat[(r * N + c) * H + h] : 0.f;
-        const float nn = n2[r * N + c];
-        const float dot = wave_sum(ch * dc);
-        const float dch = squash_scale(nn) * dc + 2.f * ch * dot * squash_scale_grad(nn);
-        // c_hat = sum_k d_k e_hat_k
-        float sdd = 0.f;
-        for (int k = 0; k < K; ++k) {
-          const float ehv = h < H ? eh[(c * K + k) * H + h] : 0.f;
-          const float ddk = wave_sum(ehv * dch);
-          const float dk = d[r * NK + c * K + k];
-          if (h < H) deh[(c * K + k) * H + h] += dk * dch;
-          if (lane == 0) dd[c * K + k] = ddk;
-          sdd += dk * ddk;
-        }
-        wave_lds_sync();
-        // softmax backward; gb accumulates dL/db_r (identity path from b_{r+1} already inside)
-        if (lane == 0)
-          for (int k = 0; k < K; ++k) gb[c * K + k] += d[r * NK + c * K + k] * (dd[c * K + k] - sdd);
-        wave_lds_sync();
       }
+      // squash backward
+      const float ch = h < H ? chat[r * H + h] : 0.f;
+      const float nn = n2[r];
+      const float dot = wave_sum(ch * dc);
+      const float dch = squash_scale(nn) * dc + 2.f * ch * dot * squash_scale_grad(nn);
+      // c_hat = sum_k d_k e_hat_k
+      float sdd = 0.f;
+      for (int k = 0; k < K; ++k) {
+        const float ehv = h < H ? eh[k * H + h] : 0.f;
+        const float ddk = wave_sum(ehv * dch);
+        const float dk = d[r * K + k];
+        if (h < H) deh[k * H + h] += dk * dch;
+        if (lane == 0) dd[k] = ddk;
+        sdd += dk * ddk;
+      }
+      wave_lds_sync();
+      // softmax backward; gb accumulates dL/db_r (identity path from b_{r+1} already inside)
+      if (lane == 0)
+        for (int k = 0; k < K; ++k) gb[k] += d[r * K + k] * (dd[k] - sdd);
+      wave_lds_sync();
     }
-    wave_lds_sync();
-    // dS = dE_hat W_s^T  (lane = a),  dW_s[a][h] += sum_ck S[ck][a] dE_hat[ck][h]  (lane = h)
-    for (int ck = 0; ck < NK; ++ck) {
+    // dS = dE_hat W_s^T  (lane = a),  dW_s[a][h] += sum_k S[k][a] dE_hat[k][h]  (lane = h)
+    for (int k = 0; k < K; ++k) {
       if (lane < H) {
         float acc = 0.f;
 #pragma unroll
-        for (int hh = 0; hh < H; ++hh) acc += deh[ck * H + hh] * wsl[lane * H + hh];
-        de[(row0 + ck) * H + lane] = acc;
+        for (int hh = 0; hh < H; ++hh) acc += deh[k * H + hh] * wst[hh * H + lane];
+        de[(row0 + k) * H + lane] = acc;
       }
-      const float dv = h < H ? deh[ck * H + h] : 0.f;
+      const float dv = h < H ? deh[k * H + h] : 0.f;
 #pragma unroll
-      for (int a = 0; a < H; ++a) dws[a] += sup[ck * H + a] * dv;
+      for (int a = 0; a < H; ++a) dws[a] += sup[k * H + a] * dv;
     }
     wave_lds_sync();
   }
