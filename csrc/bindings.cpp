@@ -159,7 +159,13 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, ngroups));
   auto opt = wemb.options();
   auto dw_slab = at::empty({blocks, 2, 4 * U, NF}, opt);
-  auto dpos_slab = at::empty({blocks, 2, 2, 2 * L, PD}, opt);
+  // bf16: pos gradients leave lstm_bwd as per-token rows and pos_grad reduces them -> [pblocks, 1, 2, 2L, PD]
+  const int64_t ntiles = (S + 15) / 16;
+  const int64_t pitems = ntiles * ((L + 1) / 2);
+  const int64_t pblocks = std::max<int64_t>(1, std::min<int64_t>(1024, (pitems + 31) / 32));
+  if (bf16) TORCH_CHECK(2 * PD <= 16 && 2 * L <= 128, "ina.lstm_bwd: bf16 path needs pos_dim <= 8 and L <= 64");
+  auto dpos_slab = bf16 ? at::empty({pblocks, 1, 2, 2 * L, PD}, opt) : at::empty({blocks, 2, 2, 2 * L, PD}, opt);
+  Tensor dxp = bf16 ? at::empty({2, ntiles, L, 2 * PD, 16}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
   Tensor dwemb = word_grad ? at::zeros_like(wemb) : at::empty({0}, opt);
   if (S == 0) {
     dw_slab.zero_();
@@ -193,7 +199,9 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   a.thr = keep_threshold(keep_prob);
   a.inv_kp = (float)(1.0 / keep_prob);
   a.drop = keep_prob < 1.0 ? 1 : 0;
+  a.dxp = bf16 ? dxp.data_ptr() : nullptr;
   check_launch(ina::lstm_bwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_bwd");
+  if (bf16) check_launch(ina::pos_grad(a, (int)pblocks, dpos_slab.data_ptr<float>(), cur_stream()), "pos_grad");
   return {dw_slab, dpos_slab, dwemb};
 }
 

@@ -32,12 +32,15 @@ struct LstmArgs {
   void* hdrop;
   unsigned char* dmask;  // [tiles][2][L][64] dropout keep bits (bit m = unit 4m+q), written by fwd, read by bwd
   const int* seed_dev;   // optional device-resident dropout seed (overrides seed; HIP-graph replay)
+  void* dxp;             // bf16 bwd: pos-feature gradients [2 dir][tiles][L][2PD][16] (reduced by pos_grad)
   uint32_t seed, thr;
   float inv_kp;
   int drop;
 };
 int lstm_fwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
 int lstm_bwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
+// bf16 mode: reduce a.dxp into slab [blocks][2 tables][2L][PD] (needs 2L <= 128, 2PD <= 16)
+int pos_grad(const LstmArgs& a, int blocks, float* slab, hipStream_t st);
 bool lstm_supported(int U, int NX);
 size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD);
 

@@ -16,6 +16,7 @@
 #include "ina_common.h"
 #include "ina_launch.h"
 
+
 using namespace ina;
 
 #ifndef INA_FWD_PIPE
@@ -200,6 +201,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   XSrc xs[NX];
 #pragma unroll
   for (int xi = 0; xi < NX; ++xi) xs[xi] = make_xsrc(4 * xi + q, wemb, E, p1emb, p2emb, PD);
+  int pofs[NX];   // lane's element offset inside a dxp [NPF][16] step block (pos features only)
+#pragma unroll
+  for (int xi = 0; xi < NX; ++xi) pofs[xi] = (4 * xi + q - E) * 16 + n;
   auto load_x = [&](int t, float* xv) {
     const int2 id = ids[n * L + t];
     const XRow r = xrow(id.x, id.y & 0xffff, id.y >> 16, E, PD);
@@ -322,7 +326,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
     const typename CT<BF16>::type* __restrict__ cst, const typename FragT<BF16>::elem* __restrict__ dH,
     float* __restrict__ dw_slab,
     float* __restrict__ dpos_slab, float* __restrict__ dwemb, const unsigned char* __restrict__ dmask, uint32_t seed,
-    uint32_t thr, float inv_kp, int drop) {
+    uint32_t thr, float inv_kp, int drop, unsigned short* __restrict__ dxp) {
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
   using elem = typename FragT<BF16>::elem;
@@ -357,11 +361,13 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
     off += xp > red ? xp : red;
   }
   off = (off + 15) & ~(size_t)15;
-  float* dpos_lds = reinterpret_cast<float*>(smem + off);
+  float* dpos_lds = reinterpret_cast<float*>(smem + off);   // [2 tables][2L][PD]
   for (int i = threadIdx.x; i < NA; i += 256) lA[i] = apack[(size_t)dir * NA + i];
   for (int i = threadIdx.x; i < NA2; i += 256) lA2[i] = a2pack[(size_t)dir * NA2 + i];
   for (int i = threadIdx.x; i < 4 * U; i += 256) lbias[i] = bias[dir * 4 * U + i];
-  for (int i = threadIdx.x; i < 2 * P2 * PD; i += 256) dpos_lds[i] = 0.f;
+  if constexpr (!BF16)
+    for (int i = threadIdx.x; i < 2 * P2 * PD; i += 256) dpos_lds[i] = 0.f;
+  const int NPF = 2 * PD;   // pos features (bf16 mode: exported to dxp, reduced by pos_grad_kernel)
   // zero the wave's transpose buffers once (pad rows / columns stay zero; bias row = 1)
   for (int i = lane; i < XROWS * RS; i += 64) dgT[i] = to_elem(0.f, (elem*)nullptr);
   wave_lds_sync();
@@ -382,6 +388,9 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
   XSrc xs[NX];
 #pragma unroll
   for (int xi = 0; xi < NX; ++xi) xs[xi] = make_xsrc(4 * xi + q, wemb, E, p1emb, p2emb, PD);
+  int pofs[NX];   // lane's element offset inside a dxp [NPF][16] step block (pos features only)
+#pragma unroll
+  for (int xi = 0; xi < NX; ++xi) pofs[xi] = (4 * xi + q - E) * 16 + n;
 
   for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const int tile = g * 4 + wave;
@@ -506,15 +515,28 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
       }
 #pragma unroll
       for (int m = 0; m < U4; ++m) dh_rec[m] = dslot[m];
-      // x-feature gradients -> pos tables (LDS atomics) / word table (global atomics)
-      if (valid) {
+      // x-feature gradients of the pos features.  bf16: plain coalesced stores into dxp (rows of 16
+      // sequences per feature); pos_grad_kernel reduces them with one-hot MFMAs -- per-element LDS
+      // float atomics here sat on the recurrence's critical path (~20% of this kernel).  fp32: LDS
+      // atomics into the block's pos tables.
+      if constexpr (BF16) {
+        unsigned short* drow = dxp + (((size_t)dir * ntiles + tile) * L + tof(tau)) * NPF * 16;
+#pragma unroll
+        for (int xi = 0; xi < NX; ++xi)
+          if ((uint32_t)(xs[xi].sel - 1) < 2u) drow[pofs[xi]] = f2bf(valid ? dslot[U4 + xi] : 0.f);
+      } else {
 #pragma unroll
         for (int xi = 0; xi < NX; ++xi) {
-          const float v = dslot[U4 + xi];
-          const int sel = xs[xi].sel;
-          if (sel == 1) atomicAdd(&dpos_lds[p1 * PD + xs[xi].col], v);
-          if (sel == 2) atomicAdd(&dpos_lds[(P2 + p2) * PD + xs[xi].col], v);
-          if (sel == 0 && dwemb) atomicAdd(&dwemb[(long)wid * E + xs[xi].col], v);
+          const uint32_t i1 = (uint32_t)(p1 * PD + xs[xi].col), i2 = (uint32_t)((P2 + p2) * PD + xs[xi].col);
+          if (valid && (uint32_t)(xs[xi].sel - 1) < 2u) atomicAdd(&dpos_lds[lane_sel(xs[xi].mp2, i1, i2)], dslot[U4 + xi]);
+        }
+      }
+      // word table (global atomics, only when trained)
+      if (dwemb) {
+        if (valid) {
+#pragma unroll
+          for (int xi = 0; xi < NX; ++xi)
+            if (xs[xi].sel == 0) atomicAdd(&dwemb[(long)wid * E + xs[xi].col], dslot[U4 + xi]);
         }
       }
       // ---- stage (dG, XH) for the dW MFMA: sample column = n + 16 * (tau & 1)
@@ -541,11 +563,9 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
           for (int a = 0; a < GT; ++a) {
             const u16x8_t fa = *reinterpret_cast<const u16x8_t*>(&dgT[(a * 16 + n) * RS + 8 * q]);
 #pragma unroll
-            for (int b = 0; b < FTMAX; ++b) {
-              if (b < FT) {
-                const u16x8_t fb = *reinterpret_cast<const u16x8_t*>(&xhT[(b * 16 + n) * RS + 8 * q]);
-                accw[a][b] = mfma_bf16(fa, fb, accw[a][b]);
-              }
+            for (int b = 0; b < FTMAX; ++b) {   // rows >= NF of xhT are zero: no runtime bound needed
+              const u16x8_t fb = *reinterpret_cast<const u16x8_t*>(&xhT[(b * 16 + n) * RS + 8 * q]);
+              accw[a][b] = mfma_bf16(fa, fb, accw[a][b]);
             }
           }
         } else {
@@ -556,10 +576,8 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
               const float fa = dgT[(a * 16 + n) * RS + 4 * kk + q];
 #pragma unroll
               for (int b = 0; b < FTMAX; ++b) {
-                if (b < FT) {
-                  const float fb = xhT[(b * 16 + n) * RS + 4 * kk + q];
-                  accw[a][b] = mfma_f32(fa, fb, accw[a][b]);
-                }
+                const float fb = xhT[(b * 16 + n) * RS + 4 * kk + q];
+                accw[a][b] = mfma_f32(fa, fb, accw[a][b]);
               }
             }
           }
@@ -598,8 +616,93 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
   __syncthreads();
   float* slab = dw_slab + ((size_t)blockIdx.x * 2 + dir) * REDN;
   for (int i = threadIdx.x; i < REDN; i += 256) slab[i] = red[i];
-  float* ps = dpos_slab + ((size_t)blockIdx.x * 2 + dir) * 2 * P2 * PD;
-  for (int i = threadIdx.x; i < 2 * P2 * PD; i += 256) ps[i] = dpos_lds[i];
+  if constexpr (!BF16) {
+    float* ps = dpos_slab + ((size_t)blockIdx.x * 2 + dir) * 2 * P2 * PD;
+    for (int i = threadIdx.x; i < 2 * P2 * PD; i += 256) ps[i] = dpos_lds[i];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// pos-table gradients (bf16 mode): dpos_tb[p][c] = sum over (s, t) with pos_tb[s][t] == p of
+// dx[s][t][c], both directions.  As a GEMM: D[p][c] += OneHot[p][sample] * DX[sample][c] with
+// K = 32 samples (2 steps x 16 sequences of a tile) per v_mfma_f32_16x16x32_bf16; the one-hot A
+// fragments are built in registers from the gathered position ids (shared by the two directions
+// and, per position tile, by both tables' columns).  NPT = position tiles (2L <= 16 * NPT).
+// ------------------------------------------------------------------------------------------
+template <int NPT>
+__global__ __launch_bounds__(256) void pos_grad_kernel(const unsigned short* __restrict__ dxp,
+                                                       const int* __restrict__ inst, int S,
+                                                       const int* __restrict__ pos1, const int* __restrict__ pos2,
+                                                       int L, int PD, float* __restrict__ slab) {
+  __shared__ float red[4][2 * 16 * NPT * 8];   // per-wave partials (summed in fixed order: deterministic)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, kg = lane >> 4;
+  const int ntiles = (S + 15) / 16, npairs = (L + 1) / 2, NPF = 2 * PD, P2 = 2 * L;
+  const long items = (long)ntiles * npairs;
+  const size_t dstride = (size_t)ntiles * L * NPF * 16;   // one direction of dxp
+  const int half = (kg & 1) * 8, sstep = kg >> 1;         // fragment k = 8 kg + e <-> (step, seq)
+  f32x4_t acc[2][NPT];
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int pt = 0; pt < NPT; ++pt) acc[tb][pt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (long it = (long)blockIdx.x * 4 + wave; it < items; it += (long)gridDim.x * 4) {
+    const int tile = (int)(it / npairs), pr = (int)(it - (long)tile * npairs);
+    const int t = 2 * pr + sstep;
+    const bool tv = t < L;
+    const int tc = tv ? t : L - 1;
+    // B = dx[sample][feature i16] for the lane's 8 samples (one 16-byte load per direction)
+    u16x8_t b0 = {0, 0, 0, 0, 0, 0, 0, 0}, b1 = b0;
+    if (tv && i16 < NPF) {
+      const size_t o = (((size_t)tile * L + t) * NPF + i16) * 16 + half;
+      b0 = *reinterpret_cast<const u16x8_t*>(dxp + o);
+      b1 = *reinterpret_cast<const u16x8_t*>(dxp + dstride + o);
+    }
+    // position ids of the lane's 8 samples; hit = position tile of the sample if it lands on the
+    // lane's A row (p % 16 == i16), else -1
+    int h1[8], h2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      int sq = tile * 16 + half + e;
+      sq = sq < S ? sq : S - 1;   // padded sequences carry dx == 0
+      const long r = (long)inst[sq] * L + tc;
+      const int v1 = pos1[r], v2 = pos2[r];
+      h1[e] = (v1 & 15) == i16 ? (v1 >> 4) : -1;
+      h2[e] = (v2 & 15) == i16 ? (v2 >> 4) : -1;
+    }
+#pragma unroll
+    for (int pt = 0; pt < NPT; ++pt) {
+      u16x8_t a1, a2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        a1[e] = h1[e] == pt ? (unsigned short)0x3F80 : (unsigned short)0;
+        a2[e] = h2[e] == pt ? (unsigned short)0x3F80 : (unsigned short)0;
+      }
+      acc[0][pt] = mfma_bf16(a1, b0, acc[0][pt]);
+      acc[0][pt] = mfma_bf16(a1, b1, acc[0][pt]);
+      acc[1][pt] = mfma_bf16(a2, b0, acc[1][pt]);
+      acc[1][pt] = mfma_bf16(a2, b1, acc[1][pt]);
+    }
+  }
+  // D[row = 4 kg + r][col = i16] of tile pt = (position pt*16 + row, feature column i16); table tb
+  // owns columns [tb*PD, tb*PD + PD)
+  // (every (table, p, c) is owned by exactly one lane of the wave)
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb) {
+    const int c = i16 - tb * PD;
+    if (c >= 0 && c < PD) {
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int p = pt * 16 + 4 * kg + r;
+          if (p < P2) red[wave][(tb * P2 + p) * PD + c] = acc[tb][pt][r];
+        }
+    }
+  }
+  __syncthreads();
+  float* out = slab + (size_t)blockIdx.x * 2 * P2 * PD;
+  for (int i = threadIdx.x; i < 2 * P2 * PD; i += 256) out[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -624,7 +727,7 @@ size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD) {
   const size_t red = (size_t)4 * U * (4 * NX + U + 1) * 4;
   off += xp > red ? xp : red;
   off = (off + 15) & ~(size_t)15;
-  off += (size_t)2 * 2 * L * PD * 4;
+  if (!bf16) off += (size_t)2 * 2 * L * PD * 4;   // block pos tables (bf16 mode: pos_grad_kernel)
   return off;
 }
 
@@ -660,7 +763,7 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(kfn, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, (const frag*)a.a2pack, a.bias,
                      (const elem*)a.hraw, (const typename CT<BF16>::type*)a.cst, (const elem*)a.dH, a.dw_slab, a.dpos_slab, a.dwemb, a.dmask, a.seed, a.thr, a.inv_kp,
-                     a.drop);
+                     a.drop, (unsigned short*)a.dxp);
   INA_CHECK_LAUNCH();
   return 0;
 }
@@ -683,6 +786,24 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
 
 int lstm_fwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st) { INA_LSTM_DISPATCH(launch_fwd_t) }
 int lstm_bwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st) { INA_LSTM_DISPATCH(launch_bwd_t) }
+
+int pos_grad(const LstmArgs& a, int blocks, float* slab, hipStream_t st) {
+  const int P2 = 2 * a.L;
+  dim3 grid(blocks), block(256);
+  const int* inst = a.inst;
+  const auto* dxp = (const unsigned short*)a.dxp;
+  if (P2 <= 48) {
+    hipLaunchKernelGGL(pos_grad_kernel<3>, grid, block, 0, st, dxp, inst, a.S, a.pos1, a.pos2, a.L, a.PD, slab);
+  } else if (P2 <= 80) {
+    hipLaunchKernelGGL(pos_grad_kernel<5>, grid, block, 0, st, dxp, inst, a.S, a.pos1, a.pos2, a.L, a.PD, slab);
+  } else if (P2 <= 128) {
+    hipLaunchKernelGGL(pos_grad_kernel<8>, grid, block, 0, st, dxp, inst, a.S, a.pos1, a.pos2, a.L, a.PD, slab);
+  } else {
+    return -1;
+  }
+  INA_CHECK_LAUNCH();
+  return 0;
+}
 
 bool lstm_supported(int U, int NX) {
   return (U == 20 || U == 32 || U == 8) && (NX == 4 || NX == 16);

@@ -40,12 +40,14 @@ class InductionNetwork(nn.Module):
         return {n: getattr(self.params, a) for a, n in self.params.names().items() if a.startswith("bert__")}
 
     def use_fused_lstm(self, L: int) -> bool:
-        """Fused lane-ownership BiLSTM+attention kernels (u in GPU_SUPPORTED_U, input <= 64, L <= 64) or
-        the wide GEMM path (``lstm_impl`` forces either)."""
+        """Fused lane-ownership BiLSTM+attention kernels (u in GPU_SUPPORTED_U, input <= 64, L <= 64,
+        pos dim <= 8) or the wide GEMM path (``lstm_impl`` forces either)."""
         impl = self.cfg.lstm_impl
-        ok = self.cfg.hidden_size in GPU_SUPPORTED_U and self.params.input_dim <= 64 and L <= 64
+        ok = (self.cfg.hidden_size in GPU_SUPPORTED_U and self.params.input_dim <= 64 and L <= 64
+              and self.cfg.pos_embedding_dim <= 8)
         if impl == "fused" and not ok:
-            raise NotImplementedError(f"fused BiLSTM kernels need u in {GPU_SUPPORTED_U}, input dim <= 64, L <= 64")
+            raise NotImplementedError(f"fused BiLSTM kernels need u in {GPU_SUPPORTED_U}, input dim <= 64, L <= 64, "
+                                      "pos dim <= 8")
         return ok if impl == "auto" else impl == "fused"
 
     def _head(self, e, p, B, N, K, Q, grad_views):
