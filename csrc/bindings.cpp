@@ -165,7 +165,8 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   const int64_t pblocks = std::max<int64_t>(1, std::min<int64_t>(1024, (pitems + 31) / 32));
   if (bf16) TORCH_CHECK(2 * PD <= 16 && 2 * L <= 128, "ina.lstm_bwd: bf16 path needs pos_dim <= 8 and L <= 64");
   auto dpos_slab = bf16 ? at::empty({pblocks, 1, 2, 2 * L, PD}, opt) : at::empty({blocks, 2, 2, 2 * L, PD}, opt);
-  Tensor dxp = bf16 ? at::empty({2, ntiles, L, 2 * PD, 16}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
+  // [2 dir][tiles][L][2PD][16] bf16 dx of the pos features, then [tiles][L][16] u16 position ids
+  Tensor dxp = bf16 ? at::empty({(2 * 2 * PD + 1) * ntiles * L * 16}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
   Tensor dwemb = word_grad ? at::zeros_like(wemb) : at::empty({0}, opt);
   if (S == 0) {
     dw_slab.zero_();

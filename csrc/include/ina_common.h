@@ -107,6 +107,18 @@ INA_DEVICE float cross_group_max(float v) {
   return v;
 }
 
+// Deterministic workgroup reduction: the waves add their contributions into a shared LDS buffer one
+// after another (wave 0 first), so the fp32 summation order never depends on scheduling (LDS float
+// atomics would).  body() does plain read-add-writes; within one wave every lane must own distinct
+// addresses.  Must be reached by every thread of the workgroup.
+template <class F>
+INA_DEVICE void ordered_wave_accumulate(int wave, int nwaves, F&& body) {
+  for (int w = 0; w < nwaves; ++w) {
+    if (wave == w) body();
+    __syncthreads();
+  }
+}
+
 }  // namespace ina
 
 #define INA_CHECK_LAUNCH()                                                        \

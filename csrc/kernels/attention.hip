@@ -481,28 +481,35 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
   const int NS = H2 * H2 + 2 * H2;
   for (int i = threadIdx.x; i < NS; i += 256) red[i] = 0.f;
   __syncthreads();
-#pragma unroll
-  for (int a = 0; a < MT; ++a)
-#pragma unroll
-    for (int b = 0; b < MT; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 16 * a + 4 * q + r, j = 16 * b + n;
-        if (i < H2 && j < H2) atomicAdd(&red[i * H2 + j], accW[a][b][r]);
-      }
+  float d1s[MT][4], d2s[MT][4];   // cross-lane sums first (every lane takes part in the shuffles)
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int j = 16 * m + 4 * q + r;
-      const float d1 = group16_sum(db1a[m][r]);
-      const float d2 = group16_sum(dw2a[m][r]);
-      if (n == 0 && j < H2) {
-        atomicAdd(&red[H2 * H2 + j], d1);
-        atomicAdd(&red[H2 * H2 + H2 + j], d2);
-      }
+      d1s[m][r] = group16_sum(db1a[m][r]);
+      d2s[m][r] = group16_sum(dw2a[m][r]);
     }
-  __syncthreads();
+  ordered_wave_accumulate(threadIdx.x >> 6, 4, [&] {   // 256-thread workgroups; deterministic order
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < MT; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 16 * a + 4 * q + r, j = 16 * b + n;
+          if (i < H2 && j < H2) red[i * H2 + j] += accW[a][b][r];
+        }
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = 16 * m + 4 * q + r;
+        if (n == 0 && j < H2) {
+          red[H2 * H2 + j] += d1s[m][r];
+          red[H2 * H2 + H2 + j] += d2s[m][r];
+        }
+      }
+  });
   for (int i = threadIdx.x; i < NS; i += 256) slab[(size_t)blockIdx.x * NS + i] = red[i];
 }
 
@@ -714,28 +721,35 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(
   const int NS = H2 * H2 + 2 * H2;
   for (int i = threadIdx.x; i < NS; i += 256) red[i] = 0.f;
   __syncthreads();
-#pragma unroll
-  for (int a = 0; a < MT; ++a)
-#pragma unroll
-    for (int b = 0; b < MT; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 16 * a + 4 * q + r, j = 16 * b + n;
-        if (i < H2 && j < H2) atomicAdd(&red[i * H2 + j], accW[a][b][r]);
-      }
+  float d1s[MT][4], d2s[MT][4];   // cross-lane sums first (every lane takes part in the shuffles)
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int j = 16 * m + 4 * q + r;
-      const float d1 = group16_sum(db1a[m][r]);
-      const float d2 = group16_sum(dw2a[m][r]);
-      if (n == 0 && j < H2) {
-        atomicAdd(&red[H2 * H2 + j], d1);
-        atomicAdd(&red[H2 * H2 + H2 + j], d2);
-      }
+      d1s[m][r] = group16_sum(db1a[m][r]);
+      d2s[m][r] = group16_sum(dw2a[m][r]);
     }
-  __syncthreads();
+  ordered_wave_accumulate(threadIdx.x >> 6, 4, [&] {   // 256-thread workgroups; deterministic order
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < MT; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 16 * a + 4 * q + r, j = 16 * b + n;
+          if (i < H2 && j < H2) red[i * H2 + j] += accW[a][b][r];
+        }
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = 16 * m + 4 * q + r;
+        if (n == 0 && j < H2) {
+          red[H2 * H2 + j] += d1s[m][r];
+          red[H2 * H2 + H2 + j] += d2s[m][r];
+        }
+      }
+  });
   for (int i = threadIdx.x; i < NS; i += 256) slab[(size_t)blockIdx.x * NS + i] = red[i];
 }
 

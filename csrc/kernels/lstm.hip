@@ -316,8 +316,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
 // ------------------------------------------------------------------------------------------
 // dW slab layout per (block, dir): D[gc][f], gc in [0, 4U), f in [0, DIN + U + 1) where
 // f < DIN are x features, DIN..DIN+U-1 the h units and DIN+U the bias.
+#ifndef INA_DH_LANE
+#define INA_DH_LANE 0   // timing experiment: dH read in the lane layout (wrong values)
+#endif
+// 2 waves/SIMD where the register set fits in 256 without spilling (the default u=20 / 5-d words
+// case); the wider instantiations keep 1 wave and no spills
+template <int U, int NX>
+struct BwdWaves {
+  static constexpr int value = (U <= 20 && NX == 4) ? 2 : 1;
+};
 template <int U, int NX, bool BF16>
-__global__ __launch_bounds__(256) void lstm_bwd_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U, NX>::value))) void lstm_bwd_kernel(
     const int* __restrict__ inst, int S, const int* __restrict__ word, const int* __restrict__ pos1,
     const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
     const float* __restrict__ p1emb, const float* __restrict__ p2emb, int PD,
@@ -423,7 +432,11 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
         cprev[m] = L >= 2 ? cp : 0.f;
         const float hv = from_elem(hbase[((size_t)tp * U4 + m) * 64]);
         hp[m] = (L >= 2 && valid) ? hv : 0.f;
+#if INA_DH_LANE
+        const float dv = from_elem(dH[(((size_t)tile * 2 + dir) * L + t) * U4 * 64 + m * 64 + lane]);
+#else
         const float dv = from_elem(dH[(seqc * L + t) * (2 * U) + dir * U + 4 * m + q]);
+#endif
         const bool keep = (bits >> m) & 1u;
         dhin[m] = (valid && keep) ? dv * inv_kp : 0.f;
       }
@@ -457,7 +470,11 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
         cprev_n[m] = n_has_prev ? cp : 0.f;
         const float hv = from_elem(hbase[((size_t)tnp * U4 + m) * 64]);
         hp_n[m] = (n_has_prev && valid) ? hv : 0.f;
+#if INA_DH_LANE
+        const float dv = from_elem(dH[(((size_t)tile * 2 + dir) * L + tn) * U4 * 64 + m * 64 + lane]);
+#else
         const float dv = from_elem(dH[(seqc * L + tn) * (2 * U) + dir * U + 4 * m + q]);
+#endif
         const bool keep = (bits_n >> m) & 1u;
         dhin_n[m] = (valid && keep) ? dv * inv_kp : 0.f;
       }
@@ -524,6 +541,10 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
 #pragma unroll
         for (int xi = 0; xi < NX; ++xi)
           if ((uint32_t)(xs[xi].sel - 1) < 2u) drow[pofs[xi]] = f2bf(valid ? dslot[U4 + xi] : 0.f);
+        // the token's position ids (p1 | p2 << 8) for the reduction, written once (direction 0)
+        if (dir == 0 && q == 0)
+          dxp[(size_t)2 * ntiles * L * NPF * 16 + ((size_t)tile * L + tof(tau)) * 16 + n] =
+              (unsigned short)(p1 | (p2 << 8));
       } else {
 #pragma unroll
         for (int xi = 0; xi < NX; ++xi) {
@@ -604,16 +625,17 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
   const int REDN = G4 * NF;
   for (int i = threadIdx.x; i < REDN; i += 256) red[i] = 0.f;
   __syncthreads();
+  ordered_wave_accumulate(wave, 4, [&] {   // deterministic summation order
 #pragma unroll
-  for (int a = 0; a < GT; ++a)
+    for (int a = 0; a < GT; ++a)
 #pragma unroll
-    for (int b = 0; b < FTMAX; ++b)
+      for (int b = 0; b < FTMAX; ++b)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gc = a * 16 + 4 * q + r, f = b * 16 + n;
-        if (b < FT && gc < G4 && f < NF) atomicAdd(&red[gc * NF + f], accw[a][b][r]);
-      }
-  __syncthreads();
+        for (int r = 0; r < 4; ++r) {
+          const int gc = a * 16 + 4 * q + r, f = b * 16 + n;
+          if (b < FT && gc < G4 && f < NF) red[gc * NF + f] += accw[a][b][r];
+        }
+  });
   float* slab = dw_slab + ((size_t)blockIdx.x * 2 + dir) * REDN;
   for (int i = threadIdx.x; i < REDN; i += 256) slab[i] = red[i];
   if constexpr (!BF16) {
@@ -626,58 +648,76 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(
 // pos-table gradients (bf16 mode): dpos_tb[p][c] = sum over (s, t) with pos_tb[s][t] == p of
 // dx[s][t][c], both directions.  As a GEMM: D[p][c] += OneHot[p][sample] * DX[sample][c] with
 // K = 32 samples (2 steps x 16 sequences of a tile) per v_mfma_f32_16x16x32_bf16; the one-hot A
-// fragments are built in registers from the gathered position ids (shared by the two directions
-// and, per position tile, by both tables' columns).  NPT = position tiles (2L <= 16 * NPT).
+// fragments are built in registers from the position ids lstm_bwd stored next to dx (shared by
+// the two directions and, per position tile, by both tables' columns).  NPT = position tiles
+// (2L <= 16 * NPT, ids < 256).
 // ------------------------------------------------------------------------------------------
 template <int NPT>
-__global__ __launch_bounds__(256) void pos_grad_kernel(const unsigned short* __restrict__ dxp,
-                                                       const int* __restrict__ inst, int S,
-                                                       const int* __restrict__ pos1, const int* __restrict__ pos2,
-                                                       int L, int PD, float* __restrict__ slab) {
+__global__ __launch_bounds__(256) void pos_grad_kernel(const unsigned short* __restrict__ dxp, int S, int L, int PD,
+                                                       float* __restrict__ slab) {
   __shared__ float red[4][2 * 16 * NPT * 8];   // per-wave partials (summed in fixed order: deterministic)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i16 = lane & 15, kg = lane >> 4;
   const int ntiles = (S + 15) / 16, npairs = (L + 1) / 2, NPF = 2 * PD, P2 = 2 * L;
   const long items = (long)ntiles * npairs;
   const size_t dstride = (size_t)ntiles * L * NPF * 16;   // one direction of dxp
+  const unsigned short* posb = dxp + 2 * dstride;         // [tiles][L][16] p1 | p2 << 8
   const int half = (kg & 1) * 8, sstep = kg >> 1;         // fragment k = 8 kg + e <-> (step, seq)
+  const int col = i16 < NPF ? i16 : NPF - 1;
   f32x4_t acc[2][NPT];
 #pragma unroll
   for (int tb = 0; tb < 2; ++tb)
 #pragma unroll
     for (int pt = 0; pt < NPT; ++pt) acc[tb][pt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  for (long it = (long)blockIdx.x * 4 + wave; it < items; it += (long)gridDim.x * 4) {
-    const int tile = (int)(it / npairs), pr = (int)(it - (long)tile * npairs);
+  const long stride = (long)gridDim.x * 4;
+  long it = (long)blockIdx.x * 4 + wave;
+  // three independent 16-byte loads per item (dx of both directions, position ids); software
+  // pipelined one item ahead
+  auto load = [&](long item, u16x8_t& b0, u16x8_t& b1, u16x8_t& pp, bool& zero) {
+    const long itc = item < items ? item : items - 1;
+    const int tile = (int)(itc / npairs), pr = (int)(itc - (long)tile * npairs);
     const int t = 2 * pr + sstep;
-    const bool tv = t < L;
-    const int tc = tv ? t : L - 1;
-    // B = dx[sample][feature i16] for the lane's 8 samples (one 16-byte load per direction)
-    u16x8_t b0 = {0, 0, 0, 0, 0, 0, 0, 0}, b1 = b0;
-    if (tv && i16 < NPF) {
-      const size_t o = (((size_t)tile * L + t) * NPF + i16) * 16 + half;
-      b0 = *reinterpret_cast<const u16x8_t*>(dxp + o);
-      b1 = *reinterpret_cast<const u16x8_t*>(dxp + dstride + o);
-    }
-    // position ids of the lane's 8 samples; hit = position tile of the sample if it lands on the
-    // lane's A row (p % 16 == i16), else -1
-    int h1[8], h2[8];
+    const int tc = t < L ? t : L - 1;
+    const size_t o = (((size_t)tile * L + tc) * NPF + col) * 16 + half;
+    b0 = *reinterpret_cast<const u16x8_t*>(dxp + o);
+    b1 = *reinterpret_cast<const u16x8_t*>(dxp + dstride + o);
+    pp = *reinterpret_cast<const u16x8_t*>(posb + ((size_t)tile * L + tc) * 16 + half);
+    zero = t >= L || i16 >= NPF;
+  };
+  u16x8_t nb0, nb1, npp;
+  bool nz;
+  load(it, nb0, nb1, npp, nz);
+  for (; it < items; it += stride) {
+    u16x8_t b0 = nb0, b1 = nb1, pp = npp;
+    const bool z = nz;
+    load(it + stride, nb0, nb1, npp, nz);
+    if (z) b0 = b1 = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    // one-hot A rows: element e of the lane's row p = pt*16 + i16 is 1 iff pos(e) == p.  Pair bits
+    // m = (1 << tile(e0)) | (1 << (16 + tile(e1))) for samples landing on row i16 (bit 15 / 31 =
+    // no hit, never a tile index); a tile's packed bf16 pair is then ((m >> pt) & 0x10001) * 0x3F80.
+    uint32_t m1[4], m2[4];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      int sq = tile * 16 + half + e;
-      sq = sq < S ? sq : S - 1;   // padded sequences carry dx == 0
-      const long r = (long)inst[sq] * L + tc;
-      const int v1 = pos1[r], v2 = pos2[r];
-      h1[e] = (v1 & 15) == i16 ? (v1 >> 4) : -1;
-      h2[e] = (v2 & 15) == i16 ? (v2 >> 4) : -1;
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t v0 = pp[2 * w], v1 = pp[2 * w + 1];
+      const uint32_t a0 = v0 & 0xFF, a1 = v1 & 0xFF, c0 = v0 >> 8, c1 = v1 >> 8;
+      const uint32_t ha0 = (a0 & 15) == (uint32_t)i16 ? (a0 >> 4) : 15u;
+      const uint32_t ha1 = (a1 & 15) == (uint32_t)i16 ? (a1 >> 4) : 15u;
+      const uint32_t hc0 = (c0 & 15) == (uint32_t)i16 ? (c0 >> 4) : 15u;
+      const uint32_t hc1 = (c1 & 15) == (uint32_t)i16 ? (c1 >> 4) : 15u;
+      m1[w] = (1u << ha0) | (1u << (16 + ha1));
+      m2[w] = (1u << hc0) | (1u << (16 + hc1));
     }
 #pragma unroll
     for (int pt = 0; pt < NPT; ++pt) {
-      u16x8_t a1, a2;
+      uint32_t w1[4], w2[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        a1[e] = h1[e] == pt ? (unsigned short)0x3F80 : (unsigned short)0;
-        a2[e] = h2[e] == pt ? (unsigned short)0x3F80 : (unsigned short)0;
+      for (int w = 0; w < 4; ++w) {
+        w1[w] = __umul24((m1[w] >> pt) & 0x10001u, 0x3F80u);
+        w2[w] = __umul24((m2[w] >> pt) & 0x10001u, 0x3F80u);
       }
+      u16x8_t a1, a2;
+      __builtin_memcpy(&a1, w1, 16);
+      __builtin_memcpy(&a2, w2, 16);
       acc[0][pt] = mfma_bf16(a1, b0, acc[0][pt]);
       acc[0][pt] = mfma_bf16(a1, b1, acc[0][pt]);
       acc[1][pt] = mfma_bf16(a2, b0, acc[1][pt]);
@@ -790,14 +830,13 @@ int lstm_bwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st) { INA_
 int pos_grad(const LstmArgs& a, int blocks, float* slab, hipStream_t st) {
   const int P2 = 2 * a.L;
   dim3 grid(blocks), block(256);
-  const int* inst = a.inst;
   const auto* dxp = (const unsigned short*)a.dxp;
   if (P2 <= 48) {
-    hipLaunchKernelGGL(pos_grad_kernel<3>, grid, block, 0, st, dxp, inst, a.S, a.pos1, a.pos2, a.L, a.PD, slab);
+    hipLaunchKernelGGL(pos_grad_kernel<3>, grid, block, 0, st, dxp, a.S, a.L, a.PD, slab);
   } else if (P2 <= 80) {
-    hipLaunchKernelGGL(pos_grad_kernel<5>, grid, block, 0, st, dxp, inst, a.S, a.pos1, a.pos2, a.L, a.PD, slab);
+    hipLaunchKernelGGL(pos_grad_kernel<5>, grid, block, 0, st, dxp, a.S, a.L, a.PD, slab);
   } else if (P2 <= 128) {
-    hipLaunchKernelGGL(pos_grad_kernel<8>, grid, block, 0, st, dxp, inst, a.S, a.pos1, a.pos2, a.L, a.PD, slab);
+    hipLaunchKernelGGL(pos_grad_kernel<8>, grid, block, 0, st, dxp, a.S, a.L, a.PD, slab);
   } else {
     return -1;
   }
