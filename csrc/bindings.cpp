@@ -322,8 +322,8 @@ Tensor routing_bwd(const Tensor& e, const Tensor& Ws, const Tensor& dcls, Tensor
   TORCH_CHECK(ina::routing_lds_bytes((int)N, (int)K, (int)H, (int)R, true) <= 160 * 1024, "ina.routing_bwd: N*K too large");
   if (blocks <= 0) blocks = 4096;   // work items = (episode, class) pairs; slab per block
   blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, std::max<int64_t>(E * N, 1)));
-  auto slab = at::zeros({blocks, H, H}, e.options());
-  if (E == 0) return slab;
+  auto slab = at::empty({blocks, H, H}, e.options());   // every block writes its whole slab
+  if (E == 0) return slab.zero_();
   check_launch(ina::routing_bwd(e.data_ptr<float>(), Ws.data_ptr<float>(), (int)E, (int)N, (int)K, (int)Q, (int)R,
                                 (int)H, dcls.data_ptr<float>(), de.data_ptr<float>(), slab.data_ptr<float>(),
                                 (int)blocks, cur_stream()),
@@ -379,7 +379,8 @@ Tensor ntn_fwd(const Tensor& cls, const Tensor& e, const Tensor& mpack, const Te
 std::tuple<Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tensor& e, const Tensor& mpack,
                                            const Tensor& m2pack, const Tensor& wtpack, const Tensor& wvec,
                                            const Tensor& dz, Tensor de, int64_t E, int64_t N, int64_t K, int64_t Q,
-                                           int64_t h, bool paper, int64_t blocks) {
+                                           int64_t h, bool paper, int64_t blocks,
+                                           const std::optional<Tensor>& gscale, const std::optional<Tensor>& cls_bf) {
   check(cls, "cls", at::kFloat);
   check(e, "e", at::kFloat);
   check(mpack, "mpack", at::kBFloat16);
@@ -424,6 +425,12 @@ std::tuple<Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tensor& e, c
   a.dp_out = dp.data_ptr();
   a.dw_slab = dw.data_ptr<float>();
   a.paper = paper ? 1 : 0;
+  a.gscale = dev_float(gscale, "gscale");
+  if (cls_bf.has_value() && cls_bf->defined()) {
+    check(*cls_bf, "cls_bf", at::kBFloat16);
+    TORCH_CHECK(cls_bf->numel() == E * N * H, "ina.ntn_bwd: cls_bf must be [E*N, H]");
+    a.cls_bf = cls_bf->data_ptr();
+  }
   if (blocks <= 0) blocks = 1024;
   a.blocks = (int)std::max<int64_t>(1, blocks);
   check_launch(ina::ntn_bwd(a, cur_stream()), "ntn_bwd");

@@ -87,8 +87,30 @@ struct NtnArgs {
   float* dw_slab;
   int blocks;
   int paper;
+  const float* gscale;   // bwd: optional device scalar multiplying dz (upstream loss gradient)
+  void* cls_bf;          // bwd: optional bf16 copy of cls [E*N][H] (operand of the dM GEMM)
 };
 int ntn_fwd(const NtnArgs& a, hipStream_t st);
+
+// step glue (glue.hip)
+constexpr int SLAB_MAX_JOBS = 8;
+struct SlabJobs {   // passed by value as a kernel argument (no per-step host->device copies)
+  const float* src[SLAB_MAX_JOBS];    // slab [nblk][n] fp32
+  const int* map[SLAB_MAX_JOBS];      // [n] destination index (-1 = skip)
+  const float* scale[SLAB_MAX_JOBS];  // optional device scalar multiplier
+  long n[SLAB_MAX_JOBS];
+  int nblk[SLAB_MAX_JOBS];
+  int nch[SLAB_MAX_JOBS];             // row chunks of the job (partial sums)
+  long wsbase[SLAB_MAX_JOBS];         // job's partials in the workspace: [nch][n]
+  long bbase[SLAB_MAX_JOBS + 1];      // prefix sums of ceil(n/64) * nch (partial-launch workgroups)
+  long fbase[SLAB_MAX_JOBS + 1];      // prefix sums of ceil(n/64) (finish-launch workgroups)
+  int njobs;
+};
+int gather_pack(const float* src, const int* idx, long nb, long ntot, void* outb, float* outf, hipStream_t st);
+int head_loss(const float* probs, const int* labels, long rows, int N, float scale, float* dz, float* out, float* part,
+              int blocks, hipStream_t st);
+int head_loss_part_floats();
+int slab_scatter(const SlabJobs& jobs, float* dst, float* ws, hipStream_t st);
 int ntn_bwd(const NtnArgs& a, hipStream_t st);
 
 int adam_step(float* p, float* m, float* v, const float* g, const unsigned char* l2mask, long n, float lr_t, float b1,

@@ -1,0 +1,216 @@
+// Step-glue kernels: everything between the model's big kernels that would otherwise be a string
+// of ~80 small PyTorch launches per training step (weight re-packing, loss / accuracy / loss
+// gradient, slab reductions, transposes and the adds into the flat gradient buffer).  At ~5 us of
+// GPU time per tiny launch those cost ~15% of the BiLSTM step; here they are 5 launches.
+//
+//  gather_pack : every per-step MFMA weight pack (LSTM gate/transpose packs, attention W1 packs,
+//                NTN M / w packs, stacked LSTM biases) in ONE gather from the flat parameter buffer
+//                with a precomputed int32 index (-1 -> 0); bf16 region then fp32 region.
+//  head_loss   : MSE loss vs one-hot labels (tf.one_hot semantics: NOTA -> zero row), accuracy
+//                (first-max argmax == label), the pre-sigmoid gradient dz = dL/dp * p(1-p) for the
+//                NTN backward and the bias gradient sum_rows dz.  Deterministic two-level reduce:
+//                per-block partials, then a one-block launch sums them in block order.
+//  slab_scatter: sum per-block gradient slabs over their blocks (chunked across workgroups, then
+//                the chunk partials summed in chunk order by a second launch) and ADD the
+//                result into the flat gradient at an int32 map (-1 = skip); transposes and pos-table
+//                crops are encoded in the maps.  Up to 8 slabs per launch.
+// Reference semantics: model/graph.py:88-95 (MSE on one-hot, accuracy), model/base.py (grads).
+#include "ina_common.h"
+#include "ina_launch.h"
+
+using namespace ina;
+
+namespace {
+
+__global__ __launch_bounds__(256) void gather_pack_kernel(const float* __restrict__ src, const int* __restrict__ idx,
+                                                          long nb, long ntot, unsigned short* __restrict__ outb,
+                                                          float* __restrict__ outf) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < ntot; i += (long)gridDim.x * 256) {
+    const int k = idx[i];
+    const float v = k >= 0 ? src[k] : 0.f;
+    if (i < nb)
+      outb[i] = f2bf(v);
+    else
+      outf[i - nb] = v;
+  }
+}
+
+constexpr int HL_NMAX = 16;
+constexpr int HL_PART = 2 + HL_NMAX;   // loss, correct, db[16]
+
+// rows = E * NQ; probs/dz [rows][N]; labels int32 [rows] (N = NOTA)
+__global__ __launch_bounds__(256) void head_loss_kernel(const float* __restrict__ probs,
+                                                        const int* __restrict__ labels, long rows, int N,
+                                                        float scale, float* __restrict__ dz,
+                                                        float* __restrict__ part) {
+  __shared__ float red[4][HL_PART];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float ls = 0.f, cor = 0.f, db[HL_NMAX];
+#pragma unroll
+  for (int c = 0; c < HL_NMAX; ++c) db[c] = 0.f;
+  for (long r = (long)blockIdx.x * 256 + threadIdx.x; r < rows; r += (long)gridDim.x * 256) {
+    const int lab = labels[r];
+    const float* pr = probs + r * N;
+    float best = -1.f;
+    int arg = 0;
+#pragma unroll
+    for (int c = 0; c < HL_NMAX; ++c) {
+      if (c < N) {
+        const float p = pr[c];
+        const float d = p - (c == lab ? 1.f : 0.f);
+        ls += d * d;
+        const float g = 2.f * scale * d * p * (1.f - p);
+        dz[r * N + c] = g;
+        db[c] += g;
+        if (p > best) {   // first maximum (torch.argmax)
+          best = p;
+          arg = c;
+        }
+      }
+    }
+    cor += (arg == lab) ? 1.f : 0.f;
+  }
+  ls = wave_sum(ls);
+  cor = wave_sum(cor);
+#pragma unroll
+  for (int c = 0; c < HL_NMAX; ++c) db[c] = wave_sum(db[c]);
+  if (lane == 0) {
+    red[wave][0] = ls;
+    red[wave][1] = cor;
+#pragma unroll
+    for (int c = 0; c < HL_NMAX; ++c) red[wave][2 + c] = db[c];
+  }
+  __syncthreads();
+  if (threadIdx.x < HL_PART)
+    part[(long)blockIdx.x * HL_PART + threadIdx.x] =
+        (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+// second launch (the kernel boundary orders it after every partial): block-order sums
+__global__ __launch_bounds__(64) void head_loss_finish_kernel(const float* __restrict__ part, int nblocks, long rows,
+                                                              int N, float scale, float* __restrict__ out) {
+  __shared__ float tot[HL_PART];
+  if (threadIdx.x < HL_PART) {
+    float s = 0.f;
+    for (int b = 0; b < nblocks; ++b) s += part[(long)b * HL_PART + threadIdx.x];
+    tot[threadIdx.x] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[0] = tot[0] * scale;
+    out[1] = tot[1] / (float)(rows > 0 ? rows : 1);
+    float t = 0.f;
+    for (int c = 0; c < N; ++c) {
+      out[2 + c] = tot[2 + c];
+      t += tot[2 + c];
+    }
+    out[2 + N] = t;
+  }
+}
+
+// slab_scatter: column sums of each job's [nblk][n] slab, added into dst at the job's map.
+// Launch 1 (slab_partial): workgroup = (job, 64-column group, chunk of rows); its 4 waves take
+// the chunk's rows round-robin (lanes = columns, coalesced 256-byte rows, 4 loads in flight per
+// lane) and combine in wave order -> ws[wsbase + chunk * n + col].  Launch 2 (slab_finish):
+// workgroup = (job, 64-column group); the waves split the chunk partials, combine in wave order,
+// scale, and add at the map.  Fixed summation order everywhere: deterministic.  (Two launches
+// rather than a last-block ticket: a device-scope fence per workgroup is an L2 write-back on
+// gfx950.)
+INA_DEVICE int find_job(const long* base, int njobs, long x) {
+  int j = 0;
+  while (j + 1 < njobs && x >= base[j + 1]) ++j;
+  return j;
+}
+
+__global__ __launch_bounds__(256) void slab_partial_kernel(SlabJobs jobs, float* __restrict__ ws) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long bid = blockIdx.x;
+  const int j = find_job(jobs.bbase, jobs.njobs, bid);
+  const long loc = bid - jobs.bbase[j];
+  const int ncol = (int)((jobs.n[j] + 63) / 64), nch = jobs.nch[j];
+  const int cg = (int)(loc % ncol), ch = (int)(loc / ncol);
+  const long n = jobs.n[j];
+  const long col = (long)cg * 64 + lane;
+  const int nb = jobs.nblk[j];
+  const int b0 = (int)(((long)nb * ch) / nch), b1 = (int)(((long)nb * (ch + 1)) / nch);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (col < n) {
+    const float* s = jobs.src[j] + col;
+    int b = b0 + wave;
+    for (; b + 12 < b1; b += 16) {
+      a0 += s[(long)b * n];
+      a1 += s[(long)(b + 4) * n];
+      a2 += s[(long)(b + 8) * n];
+      a3 += s[(long)(b + 12) * n];
+    }
+    for (; b < b1; b += 4) a0 += s[(long)b * n];
+  }
+  red[wave][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (wave == 0 && col < n)
+    ws[jobs.wsbase[j] + (long)ch * n + col] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+__global__ __launch_bounds__(256) void slab_finish_kernel(SlabJobs jobs, const float* __restrict__ ws,
+                                                          float* __restrict__ dst) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long bid = blockIdx.x;
+  const int j = find_job(jobs.fbase, jobs.njobs, bid);
+  const long n = jobs.n[j];
+  const long col = (bid - jobs.fbase[j]) * 64 + lane;
+  float a = 0.f;
+  if (col < n) {
+    const float* w = ws + jobs.wsbase[j] + col;
+    for (int c = wave; c < jobs.nch[j]; c += 4) a += w[(long)c * n];
+  }
+  red[wave][lane] = a;
+  __syncthreads();
+  if (wave == 0 && col < n) {
+    const int m = jobs.map[j][col];
+    if (m >= 0) {
+      float s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+      if (jobs.scale[j]) s *= jobs.scale[j][0];
+      dst[m] += s;
+    }
+  }
+}
+
+}  // namespace
+
+namespace ina {
+
+int gather_pack(const float* src, const int* idx, long nb, long ntot, void* outb, float* outf, hipStream_t st) {
+  if (ntot <= 0) return 0;
+  long g = (ntot + 255) / 256;
+  if (g > 2048) g = 2048;
+  hipLaunchKernelGGL(gather_pack_kernel, dim3((unsigned)g), dim3(256), 0, st, src, idx, nb, ntot,
+                     (unsigned short*)outb, outf);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int head_loss(const float* probs, const int* labels, long rows, int N, float scale, float* dz, float* out,
+              float* part, int blocks, hipStream_t st) {
+  if (N > HL_NMAX || rows <= 0) return -1;
+  hipLaunchKernelGGL(head_loss_kernel, dim3(blocks), dim3(256), 0, st, probs, labels, rows, N, scale, dz, part);
+  INA_CHECK_LAUNCH();
+  hipLaunchKernelGGL(head_loss_finish_kernel, dim3(1), dim3(64), 0, st, part, blocks, rows, N, scale, out);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int head_loss_part_floats() { return HL_PART; }
+
+int slab_scatter(const SlabJobs& jobs, float* dst, float* ws, hipStream_t st) {
+  const long nb1 = jobs.bbase[jobs.njobs], nb2 = jobs.fbase[jobs.njobs];
+  if (nb2 <= 0) return 0;
+  hipLaunchKernelGGL(slab_partial_kernel, dim3((unsigned)nb1), dim3(256), 0, st, jobs, ws);
+  INA_CHECK_LAUNCH();
+  hipLaunchKernelGGL(slab_finish_kernel, dim3((unsigned)nb2), dim3(256), 0, st, jobs, (const float*)ws, dst);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace ina

@@ -192,8 +192,10 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
     const float* __restrict__ cls, const float* __restrict__ e, int E, int N, int K, int Q, int H, int h,
     const u16x8_t* __restrict__ mpack, const u16x8_t* __restrict__ m2pack, const u16x8_t* __restrict__ wtpack,
     const float* __restrict__ wvec, const float* __restrict__ dz, float* __restrict__ dcls, float* __restrict__ de,
-    unsigned short* __restrict__ dp_out, float* __restrict__ dw_slab) {
+    unsigned short* __restrict__ dp_out, float* __restrict__ dw_slab, const float* __restrict__ gscale,
+    unsigned short* __restrict__ cls_bf) {
   constexpr int NKA = (MTH + 1) / 2, NKB = (MTH + 1) / 2, KQ = (QT + 1) / 2;
+  const float gs = gscale ? gscale[0] : 1.f;   // upstream scale of dz (loss.backward(g))
   constexpr int NSW = PAPER ? 0 : 2;
   constexpr int F1 = 2 * MTH * NKA, F2 = 2 * MTH * NKB;
   constexpr int FR = F1 + F2 + NSW;
@@ -215,6 +217,7 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
       for (int j = 0; j < 8; ++j) {
         const int a = 32 * ka + 8 * q + j;
         Cf[ka][j] = (n < N && a < H) ? f2bf(cls[((long)epc * N + n) * H + a]) : (unsigned short)0;
+        if (cls_bf && act && n < N && a < H) cls_bf[((long)ep * N + n) * H + a] = Cf[ka][j];
       }
     u16x8_t Qf[QT][NKB];
 #pragma unroll
@@ -245,14 +248,14 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int qi = 16 * qt + n, cp = 8 * q + j;
-        dzA[qt][j] = (qi < NQ && cp < N) ? f2bf(dze[qi * N + cp]) : (unsigned short)0;
+        dzA[qt][j] = (qi < NQ && cp < N) ? f2bf(gs * dze[qi * N + cp]) : (unsigned short)0;
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int c = 4 * q + r, qi = 16 * qt + n;
-        dzC[qt][r] = (c < N && qi < NQ) ? dze[qi * N + c] : 0.f;
+        dzC[qt][r] = (c < N && qi < NQ) ? gs * dze[qi * N + c] : 0.f;
         const int qr = 16 * qt + 4 * q + r;
-        dzR[qt][r] = (n < N && qr < NQ) ? dze[qr * N + n] : 0.f;
+        dzR[qt][r] = (n < N && qr < NQ) ? gs * dze[qr * N + n] : 0.f;
       }
     }
 #pragma unroll
@@ -260,7 +263,7 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int qi = 32 * kq + kmap32(q, j);
-        dzB[kq][j] = (qi < NQ && n < N) ? f2bf(dze[qi * N + n]) : (unsigned short)0;
+        dzB[kq][j] = (qi < NQ && n < N) ? f2bf(gs * dze[qi * N + n]) : (unsigned short)0;
       }
     f32x4_t dCT[MTH], dQT[MTH][QT];
 #pragma unroll
@@ -439,7 +442,8 @@ static int ntn_bwd_t(const NtnArgs& a, hipStream_t st) {
   const int blocks = groups < a.blocks ? groups : a.blocks;
   hipLaunchKernelGGL((ntn_bwd_kernel<MTH, QT, P>), dim3(blocks), dim3(NTN_THREADS), ntn_lds_bytes(MTH, P, true), st,
                      a.cls, a.e, a.E, a.N, a.K, a.Q, a.H, a.h, (const u16x8_t*)a.mpack, (const u16x8_t*)a.m2pack,
-                     (const u16x8_t*)a.wtpack, a.wvec, a.dz, a.dcls, a.de, (unsigned short*)a.dp_out, a.dw_slab);
+                     (const u16x8_t*)a.wtpack, a.wvec, a.dz, a.dcls, a.de, (unsigned short*)a.dp_out, a.dw_slab,
+                     a.gscale, (unsigned short*)a.cls_bf);
   INA_CHECK_LAUNCH();
   return 0;
 }

@@ -105,6 +105,7 @@ class Config:
     seed: int = 12345
     deterministic: bool = False
     use_hip_graph: bool = False        # replay the BiLSTM train step as one captured hipGraph (runtime/graph.py)
+    step_glue: bool = True             # GPU BiLSTM: one-launch packs / loss / gradient scatter (ops/glue.py)
     nota_rate: float = 0.0             # FewRel 2.0 none-of-the-above probability per query
     eval_nota_rate: float = -1.0       # NOTA rate of val/test episodes (-1: same as nota_rate)
     nota_threshold: float = -1.0       # best-score threshold for predicting NOTA (-1: tuned on val when NOTA > 0)

@@ -119,6 +119,42 @@ class InductionNetwork(nn.Module):
         probs = ref.head_forward(p, e, B, N, K, Q, cfg.routing_iters, cfg.relation_head)
         return probs, None
 
+    def forward_train(self, inst: torch.Tensor, data: Tuple[torch.Tensor, ...], B: int, N: int, K: int, Q: int,
+                      labels: torch.Tensor, dropout_seed: int = 0,
+                      grad_views: Optional[Dict[str, torch.Tensor]] = None, overlap=None,
+                      seed_dev: Optional[torch.Tensor] = None, glue=None):
+        """Training forward with the loss: -> (loss, accuracy, probs).
+
+        With a ``StepGlue`` on the fused GPU BiLSTM path this is the low-launch step (one pack
+        gather, encoder, routing/NTN/loss in one node; gradients queued for the glue's single
+        scatter-add -- the caller runs ``glue.flush()`` after backward).  Otherwise it is
+        forward + ``loss`` + ``accuracy`` (CPU, BERT, wide layers, GEMM-formulated head)."""
+        cfg = self.cfg
+        p = self.pdict()
+        H = 2 * cfg.hidden_size
+        fused = (glue is not None and inst.is_cuda and cfg.encoder == "bilstm" and grad_views is not None
+                 and self.use_fused_lstm(data[0].shape[1]) and H in (16, 40, 64) and N <= 16 and N * Q <= 64
+                 and not (cfg.relation_head == "reference" and p["ntn_w"].shape[1] != N))
+        if not fused:
+            probs, _ = self.forward(inst, data, B, N, K, Q, training=True, dropout_seed=dropout_seed,
+                                    grad_views=grad_views, overlap=overlap, seed_dev=seed_dev)
+            loss = self.loss(probs, labels)
+            with torch.no_grad():
+                acc = ref.accuracy(probs.detach(), labels.long())
+            return loss, acc, probs
+        from ..ops.encoder import encode
+        from ..ops.glue import lstm_din
+        from ..ops.head import head_loss
+        U, bf16 = cfg.hidden_size, cfg.dtype == "bf16"
+        paper = cfg.relation_head == "paper"
+        packs = glue.packs(p, U, lstm_din(p), bf16, (H, p["M"].shape[2], N, paper))
+        meta = dict(U=U, bf16=bf16, keep_prob=cfg.keep_prob, seed=int(dropout_seed),
+                    word_grad=bool(isinstance(p["word_embedding"], nn.Parameter) and p["word_embedding"].requires_grad),
+                    grad_views=grad_views, seed_dev=seed_dev, packs=packs, glue=glue, pdict=p)
+        e, _ = encode(inst, data, p, meta)
+        return head_loss(e, p, labels, dict(E=B, N=N, K=K, Q=Q, iters=cfg.routing_iters, paper=paper, glue=glue,
+                                            packs=packs, pdict=p, reduction=cfg.loss_reduction))
+
     # ------------------------------------------------------------------
     def loss(self, probs: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         return ref.mse_loss(probs, labels.long(), self.cfg.loss_reduction)

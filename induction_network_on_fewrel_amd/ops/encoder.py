@@ -39,14 +39,18 @@ class EncoderFn(torch.autograd.Function):
         U, bf16 = meta["U"], meta["bf16"]
         DIN = wemb.shape[1] + 2 * p1emb.shape[1]
         sh = lstm_shape(U, DIN, bf16)
-        apack, a2pack = pack_lstm(Kf, Kb, U, DIN, bf16)
-        bias = torch.stack([bf.detach(), bb.detach()]).float().contiguous()
+        pk = meta.get("packs")
+        if pk is not None:   # StepGlue: every pack of the step came from one gather launch
+            apack, a2pack, bias = pk["apack"], pk["a2pack"], pk["bias2"]
+        else:
+            apack, a2pack = pack_lstm(Kf, Kb, U, DIN, bf16)
+            bias = torch.stack([bf.detach(), bb.detach()]).float().contiguous()
         need_grad = ctx.needs_input_grad[5:15].count(True) > 0 if hasattr(ctx, "needs_input_grad") else True
         kp = float(meta["keep_prob"])
         hlane, cst, hnat, dmask = o.lstm_fwd(inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
                                       p2emb.detach().contiguous(), apack, bias, U, sh["NX"], bf16, bool(need_grad),
                                       int(meta["seed"]), kp, meta.get("seed_dev"))
-        w1pack, w1tpack = pack_attn(W1, bf16)
+        w1pack, w1tpack = (pk["w1pack"], pk["w1tpack"]) if pk is not None else pack_attn(W1, bf16)
         e, alphas = o.attn_fwd(hnat, inst, mask, w1pack, b1.detach().contiguous(),
                                w2.detach().reshape(-1).contiguous(), U, bf16, int(meta.get("attn_blocks", 0)))
         if need_grad:
@@ -54,6 +58,7 @@ class EncoderFn(torch.autograd.Function):
                                   w1pack, w1tpack, b1, w2, alphas, hnat, dmask)
             ctx.meta = dict(meta, NX=sh["NX"], DIN=DIN)
         ctx.mark_non_differentiable(alphas)
+        ctx.set_materialize_grads(False)   # no zero-fill launch for the alphas gradient
         return e, alphas
 
     @staticmethod
@@ -67,15 +72,26 @@ class EncoderFn(torch.autograd.Function):
         dH, aslab = o.attn_bwd(hnat, inst, w1pack, w1tpack, b1.detach().contiguous(),
                                w2.detach().reshape(-1).contiguous(), de.contiguous().float(), alphas, U, bf16,
                                int(m.get("attn_blocks", 0)))
-        a = aslab.sum(0)
-        dW1 = a[: H2 * H2].view(H2, H2)
-        db1 = a[H2 * H2: H2 * H2 + H2]
-        dw2 = a[H2 * H2 + H2:].view(H2, 1)
         word_grad = bool(m.get("word_grad", False))
         dw_slab, dpos_slab, dwemb = o.lstm_bwd(inst, word, pos1, pos2, wemb.detach().contiguous(),
                                                p1emb.detach().contiguous(), p2emb.detach().contiguous(), apack, a2pack,
                                                bias, hlane, cst, dH, dmask, U, m["NX"], bf16, word_grad,
                                                int(m.get("lstm_blocks", 0)), int(m["seed"]), float(m["keep_prob"]))
+        glue = m.get("glue")
+        if glue is not None:
+            # slabs -> flat gradient in the step's single slab_scatter_add launch (StepGlue.flush)
+            p = m["pdict"]
+            glue.add(aslab, glue.map_attn(p, H2), aslab.shape[0])
+            glue.add(dw_slab, glue.map_lstm_dw(p, U, DIN), dw_slab.shape[0])
+            L, PD = word.shape[1], p1emb.shape[1]
+            mp = glue.map_pos(p, L, PD)
+            glue.add(dpos_slab, mp, dpos_slab.numel() // mp.numel())
+            wg = _route_grad(m, "word_embedding", dwemb) if word_grad else None
+            return (None,) * 5 + (wg,) + (None,) * 10
+        a = aslab.sum(0)
+        dW1 = a[: H2 * H2].view(H2, H2)
+        db1 = a[H2 * H2: H2 * H2 + H2]
+        dw2 = a[H2 * H2 + H2:].view(H2, 1)
         D = dw_slab.sum(0)                         # [2, 4U, DIN+U+1]
         dKf = D[0, :, : DIN + U].t()
         dKb = D[1, :, : DIN + U].t()

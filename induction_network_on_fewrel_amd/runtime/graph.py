@@ -18,7 +18,6 @@ from __future__ import annotations
 
 import torch
 
-from ..models import reference as ref
 from ..ops._ext import ops
 
 
@@ -67,13 +66,12 @@ class GraphedTrainStep:
                        cfg.adam_beta1, cfg.adam_beta2)
         idx, labels = tr.train_eps.sample(B, N, K, Q, seed_dev=self.ctl[1:2])
         tr.flat.zero_grad()
-        probs, _ = tr.model(idx.view(-1), tr.train_eps.arrays, B, N, K, Q, training=True, dropout_seed=0,
-                            grad_views=tr.grad_views, seed_dev=self.ctl[0:1])
-        loss = tr.model.loss(probs, labels)
-        loss.backward()
+        loss, acc, _ = tr.model.forward_train(idx.view(-1), tr.train_eps.arrays, B, N, K, Q, labels, dropout_seed=0,
+                                              grad_views=tr.grad_views, seed_dev=self.ctl[0:1], glue=tr.glue)
+        torch.autograd.backward(loss, tr.glue.one if tr.glue is not None else None)
+        if tr.glue is not None:
+            tr.glue.flush()
         tr.flat.sync_grads_into_flat()
-        with torch.no_grad():
-            acc = ref.accuracy(probs.detach(), labels.long())
         if self.with_opt:
             tr.opt.step(0.0, grad_scale=1.0, lr_dev=self.lrt[0:1])
         return loss.detach(), acc

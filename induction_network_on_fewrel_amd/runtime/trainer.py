@@ -82,6 +82,10 @@ class Trainer:
         self.model = InductionNetwork(cfg, wv, vocab_size=vocab, seed=cfg.seed).to(self.device)
         self.flat = FlatParams(self.model.params.trainable())
         self.grad_views = {n: self.flat.view(self.flat.grad, n) for n in self.flat.names}
+        self.glue = None   # fused step plumbing (ops/glue.py): GPU BiLSTM path
+        if self.device.type == "cuda" and cfg.encoder == "bilstm" and cfg.step_glue:
+            from ..ops.glue import StepGlue
+            self.glue = StepGlue(self.flat)
         if self.dist.world > 1:
             self.dist.broadcast_(self.flat.flat, 0)
         l2_names = [n for n, p in self.model.params.trainable().items()
@@ -176,13 +180,13 @@ class Trainer:
             from ..ops.bert import layer_spans
             ov = self.dist.overlap(self.flat.grad, layer_spans(self.model, self.flat.names, self.flat.offsets,
                                                                self.flat.numels))
-        probs, _ = self.model(idx.view(-1), self.train_eps.arrays, B, N, K, Q, training=True,
-                              dropout_seed=self.dropout_seed(), grad_views=gv, overlap=ov)
-        loss = self.model.loss(probs, labels)
-        loss.backward()
+        loss, acc_t, _ = self.model.forward_train(idx.view(-1), self.train_eps.arrays, B, N, K, Q, labels,
+                                                  dropout_seed=self.dropout_seed(), grad_views=gv, overlap=ov,
+                                                  glue=self.glue)
+        torch.autograd.backward(loss, self.glue.one if self.glue is not None else None)
+        if self.glue is not None:
+            self.glue.flush()
         self.flat.sync_grads_into_flat()
-        with torch.no_grad():
-            acc_t = ref.accuracy(probs.detach(), labels.long())
         e2 = self._sync()
         t2 = time.perf_counter()
         if ov is not None:

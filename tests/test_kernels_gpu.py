@@ -309,3 +309,62 @@ def test_hip_graph_step_matches_eager(tmp_path):
     assert (s0, t0, c0) == (s1, t1, c1) == (6, 6, 6)
     assert max(abs(a - b) for a, b in zip(l0, l1)) < 1e-4
     assert _relerr(p1, p0) < 1e-4
+
+
+@pytest.mark.parametrize("head", ["reference", "paper"])
+def test_step_glue_matches_unfused(tmp_path, head):
+    """ops/glue.py: the low-launch step (one pack gather, fused loss node, one slab scatter-add)
+    produces the same losses, accuracies and parameter trajectory as the per-op path."""
+    from induction_network_on_fewrel_amd.runtime.trainer import Trainer
+    data = make_synthetic(num_relations=12, instances_per_relation=40, vocab=500, seed=0)
+    runs = []
+    for glue in (False, True):
+        cfg = Config(N=5, K=3, Q=4, episodes_per_step=24, model_dir=str(tmp_path / f"s{int(glue)}{head}"), seed=6,
+                     resume=False, step_glue=glue, relation_head=head, learning_rate=1e-3)
+        tr = Trainer(cfg, data, None, device="cuda", log=False)
+        assert (tr.glue is not None) == glue
+        hist = [tr.train_step() for _ in range(4)]
+        runs.append((hist, tr.flat.flat.detach().clone()))
+    (h0, p0), (h1, p1) = runs
+    for (l0, a0), (l1, a1) in zip(h0, h1):
+        assert abs(l0 - l1) < 1e-4 * max(1.0, abs(l0)), (l0, l1)
+        assert abs(a0 - a1) < 1e-6
+    assert _relerr(p1, p0) < 2e-3
+
+
+def test_step_glue_gradients_match_autograd():
+    """One fused step's flat gradient vs the per-op path's, before any optimizer update."""
+    from induction_network_on_fewrel_amd.ops.glue import StepGlue
+    from induction_network_on_fewrel_amd.ops.optim import FlatParams
+    data = make_synthetic(num_relations=10, instances_per_relation=30, vocab=400, seed=1)
+    B, N, K, Q = 12, 5, 2, 3
+    idx, lab = EpisodeSampler(data, seed=3).next_batch_indices(B, N, K, Q)
+    inst = torch.tensor(idx.reshape(-1), dtype=torch.int32, device="cuda")
+    labels = torch.tensor(lab, dtype=torch.int32, device="cuda")
+    arrays = tuple(torch.as_tensor(a).to("cuda") for a in (data.data_word, data.data_pos1, data.data_pos2,
+                                                           data.data_mask))
+    grads = []
+    for use in (False, True):
+        cfg = Config(N=N, K=K, Q=Q, max_length=data.data_word.shape[1])
+        torch.manual_seed(0)
+        model = InductionNetwork(cfg, data.word_vec_mat, seed=3).to("cuda")
+        flat = FlatParams(model.params.trainable())
+        views = {n: flat.view(flat.grad, n) for n in flat.names}
+        glue = StepGlue(flat) if use else None
+        flat.zero_grad()
+        loss, acc, probs = model.forward_train(inst, arrays, B, N, K, Q, labels, dropout_seed=11, grad_views=views,
+                                               glue=glue)
+        torch.autograd.backward(loss, glue.one if glue else None)
+        if glue:
+            assert glue.pending() == 7
+            glue.flush()
+        flat.sync_grads_into_flat()
+        grads.append((float(loss.detach()), float(acc), probs.detach().clone(), flat.grad.clone(), flat))
+    (l0, a0, pr0, g0, f0), (l1, a1, pr1, g1, _) = grads
+    assert abs(l0 - l1) < 1e-5 and abs(a0 - a1) < 1e-6
+    assert torch.equal(pr0, pr1)
+    # dz differs in the last fp32 bits (fused vs PyTorch elementwise), which can flip bf16 operand
+    # roundings inside the NTN / routing backward
+    for n in f0.names:
+        x, y = f0.view(g1, n), f0.view(g0, n)
+        assert _relerr(x, y) < 1e-2, (n, _relerr(x, y))

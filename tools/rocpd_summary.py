@@ -31,7 +31,23 @@ def main():
     ap.add_argument("--csv", default="")
     ap.add_argument("--md", default="")
     ap.add_argument("--steps", type=int, default=0, help="timed+warmup steps in the trace (per-step column)")
+    ap.add_argument("--sequence", default="", help="print the kernel sequence (start order, duration, gap) of the "
+                    "last full step delimited by this kernel-name substring (e.g. adam_kernel)")
     a = ap.parse_args()
+    if a.sequence:
+        c = sqlite3.connect(a.db)
+        ks = c.execute("select name, start, end from kernels order by start").fetchall()
+        marks = [i for i, k in enumerate(ks) if a.sequence in k[0]]
+        if len(marks) >= 2:
+            lo, hi = marks[-2] + 1, marks[-1] + 1
+            span = (ks[hi - 1][2] - ks[lo][1]) / 1e3
+            busy = sum(k[2] - k[1] for k in ks[lo:hi]) / 1e3
+            print(f"step: {hi - lo} kernels, span {span:.1f} us, kernel-busy {busy:.1f} us")
+            prev_end = ks[lo - 1][2]
+            for k in ks[lo:hi]:
+                print(f"{(k[2] - k[1]) / 1e3:9.2f} us  gap {(k[1] - prev_end) / 1e3:7.2f}  {short(k[0], 110)}")
+                prev_end = k[2]
+        return
     rows, tot = summary(a.db)
     hdr = ["kernel", "calls", "total_ms", "avg_us", "pct"] + (["ms_per_step"] if a.steps else [])
     lines = [f"total GPU kernel time: {tot:.3f} ms"]
