@@ -36,9 +36,10 @@ void gather_pack(const Tensor& src, const Tensor& idx, int64_t nb, Tensor out_bf
 }
 
 // probs [rows, N] fp32, labels int32 [rows]; writes dz [rows, N] and out [N + 3] =
-// (loss, accuracy, db[0..N), db_total); part: workspace [blocks * 18]
+// (loss, accuracy, db[0..N), db_total); part: workspace [blocks * 18].  ce: softmax cross-entropy
+// over the pre-sigmoid scores instead of the reference MSE
 void head_loss(const Tensor& probs, const Tensor& labels, double scale, Tensor dz, Tensor out, Tensor part,
-               int64_t blocks) {
+               int64_t blocks, bool ce) {
   const char* op = "ina.head_loss";
   need(probs, op, "probs", at::kFloat);
   need(labels, op, "labels", at::kInt);
@@ -50,7 +51,7 @@ void head_loss(const Tensor& probs, const Tensor& labels, double scale, Tensor d
   TORCH_CHECK(labels.numel() == rows && dz.numel() == probs.numel() && out.numel() >= N + 3, op, ": shapes");
   TORCH_CHECK(blocks >= 1 && part.numel() >= blocks * ina::head_loss_part_floats(), op, ": workspace too small");
   TORCH_CHECK(ina::head_loss(probs.data_ptr<float>(), labels.data_ptr<int>(), (long)rows, (int)N, (float)scale,
-                             dz.data_ptr<float>(), out.data_ptr<float>(), part.data_ptr<float>(), (int)blocks,
+                             ce ? 1 : 0, dz.data_ptr<float>(), out.data_ptr<float>(), part.data_ptr<float>(), (int)blocks,
                              stream()) == 0,
               op, ": launch failed");
 }

@@ -107,8 +107,8 @@ struct SlabJobs {   // passed by value as a kernel argument (no per-step host->d
   int njobs;
 };
 int gather_pack(const float* src, const int* idx, long nb, long ntot, void* outb, float* outf, hipStream_t st);
-int head_loss(const float* probs, const int* labels, long rows, int N, float scale, float* dz, float* out, float* part,
-              int blocks, hipStream_t st);
+int head_loss(const float* probs, const int* labels, long rows, int N, float scale, int ce, float* dz, float* out,
+              float* part, int blocks, hipStream_t st);
 int head_loss_part_floats();
 int slab_scatter(const SlabJobs& jobs, float* dst, float* ws, hipStream_t st);
 int ntn_bwd(const NtnArgs& a, hipStream_t st);

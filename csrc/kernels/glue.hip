@@ -38,10 +38,14 @@ __global__ __launch_bounds__(256) void gather_pack_kernel(const float* __restric
 constexpr int HL_NMAX = 16;
 constexpr int HL_PART = 2 + HL_NMAX;   // loss, correct, db[16]
 
-// rows = E * NQ; probs/dz [rows][N]; labels int32 [rows] (N = NOTA)
+constexpr float CE_ODDS_EPS = 1e-7f;   // models/reference.py::CE_ODDS_EPS
+
+// rows = E * NQ; probs/dz [rows][N]; labels int32 [rows] (N = NOTA).
+// ce = 0: MSE on the sigmoid scores vs one-hot (reference).  ce = 1: softmax cross-entropy over the
+// pre-sigmoid scores z = log p - log(1 - p) (models/reference.py::ce_loss); NOTA rows contribute 0.
 __global__ __launch_bounds__(256) void head_loss_kernel(const float* __restrict__ probs,
                                                         const int* __restrict__ labels, long rows, int N,
-                                                        float scale, float* __restrict__ dz,
+                                                        float scale, int ce, float* __restrict__ dz,
                                                         float* __restrict__ part) {
   __shared__ float red[4][HL_PART];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -53,22 +57,54 @@ __global__ __launch_bounds__(256) void head_loss_kernel(const float* __restrict_
     const float* pr = probs + r * N;
     float best = -1.f;
     int arg = 0;
+    float pv[HL_NMAX];
 #pragma unroll
     for (int c = 0; c < HL_NMAX; ++c) {
-      if (c < N) {
-        const float p = pr[c];
-        const float d = p - (c == lab ? 1.f : 0.f);
-        ls += d * d;
-        const float g = 2.f * scale * d * p * (1.f - p);
-        dz[r * N + c] = g;
-        db[c] += g;
-        if (p > best) {   // first maximum (torch.argmax)
-          best = p;
-          arg = c;
-        }
+      pv[c] = c < N ? pr[c] : 0.f;
+      if (c < N && pv[c] > best) {   // first maximum (torch.argmax)
+        best = pv[c];
+        arg = c;
       }
     }
     cor += (arg == lab) ? 1.f : 0.f;
+    if (ce) {
+      float z[HL_NMAX], zm = -INFINITY, zl = 0.f;
+#pragma unroll
+      for (int c = 0; c < HL_NMAX; ++c) {
+        z[c] = c < N ? logf(pv[c]) - logf(fmaxf(1.f - pv[c], CE_ODDS_EPS)) : -INFINITY;
+        zm = fmaxf(zm, z[c]);
+        if (c == lab) zl = z[c];
+      }
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < HL_NMAX; ++c) {
+        z[c] = c < N ? expf(z[c] - zm) : 0.f;
+        s += z[c];
+      }
+      const bool has = lab < N;
+      const float inv = 1.f / s;
+#pragma unroll
+      for (int c = 0; c < HL_NMAX; ++c) {
+        if (c < N) {
+          const float g = has ? scale * (z[c] * inv - (c == lab ? 1.f : 0.f)) : 0.f;
+          dz[r * N + c] = g;
+          db[c] += g;
+        }
+      }
+      if (has) ls += logf(s) + zm - zl;   // -log softmax_lab
+    } else {
+#pragma unroll
+      for (int c = 0; c < HL_NMAX; ++c) {
+        if (c < N) {
+          const float p = pv[c];
+          const float d = p - (c == lab ? 1.f : 0.f);
+          ls += d * d;
+          const float g = 2.f * scale * d * p * (1.f - p);
+          dz[r * N + c] = g;
+          db[c] += g;
+        }
+      }
+    }
   }
   ls = wave_sum(ls);
   cor = wave_sum(cor);
@@ -191,10 +227,10 @@ int gather_pack(const float* src, const int* idx, long nb, long ntot, void* outb
   return 0;
 }
 
-int head_loss(const float* probs, const int* labels, long rows, int N, float scale, float* dz, float* out,
+int head_loss(const float* probs, const int* labels, long rows, int N, float scale, int ce, float* dz, float* out,
               float* part, int blocks, hipStream_t st) {
   if (N > HL_NMAX || rows <= 0) return -1;
-  hipLaunchKernelGGL(head_loss_kernel, dim3(blocks), dim3(256), 0, st, probs, labels, rows, N, scale, dz, part);
+  hipLaunchKernelGGL(head_loss_kernel, dim3(blocks), dim3(256), 0, st, probs, labels, rows, N, scale, ce, dz, part);
   INA_CHECK_LAUNCH();
   hipLaunchKernelGGL(head_loss_finish_kernel, dim3(1), dim3(64), 0, st, part, blocks, rows, N, scale, out);
   INA_CHECK_LAUNCH();

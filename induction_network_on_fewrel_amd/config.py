@@ -86,6 +86,7 @@ class Config:
     l2_lambda: float = 1e-5
     use_l2: bool = False               # reference computes then discards it (graph.py:108-109)
     loss_reduction: str = "mean"       # "mean" (reference) | "sum" (paper Eq.12)
+    loss_type: str = "mse"             # "mse" on sigmoid scores (reference) | "ce": softmax over the N scores
 
     # ---------------- loop cadence (model/base.py:115-116) ----------------
     train_iter: int = 30000
@@ -157,6 +158,8 @@ class Config:
             raise ValueError(f"unknown relation_head {self.relation_head}")
         if self.dtype not in ("bf16", "fp32"):
             raise ValueError(f"unknown dtype {self.dtype}")
+        if self.loss_type not in ("mse", "ce"):
+            raise ValueError(f"unknown loss_type {self.loss_type}")
         if self.optimizer not in ("adam", "adagrad"):
             raise ValueError(f"unknown optimizer {self.optimizer}")
         if self.encoder not in ("bilstm", "bert"):

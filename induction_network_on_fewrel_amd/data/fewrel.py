@@ -21,7 +21,7 @@ from __future__ import annotations
 import json
 import os
 from collections import OrderedDict
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -66,11 +66,17 @@ class FewRelDataset:
         """[R, 2] int32 (begin, end) in relation order -- what the device sampler consumes."""
         return np.asarray([self.rel2scope[r] for r in self.rel2scope], dtype=np.int32).reshape(-1, 2)
 
-    def subset_relations(self, rels: List[str], name: Optional[str] = None) -> "FewRelDataset":
-        """Relation-disjoint split helper (train.json is absent: split val.json by relation)."""
+    def subset_relations(self, rels: List[str], name: Optional[str] = None,
+                         part: Optional[Tuple[float, float]] = None) -> "FewRelDataset":
+        """Relation-disjoint split helper (train.json is absent: split val.json by relation).
+        ``part=(lo, hi)`` keeps only instances [lo, hi) (fractions) of every relation's scope --
+        the instance-disjoint split (same relations, disjoint sentences)."""
         idx, scope, i = [], OrderedDict(), 0
         for r in rels:
             b, e = self.rel2scope[r]
+            if part is not None:
+                n = e - b
+                b, e = b + int(round(part[0] * n)), b + int(round(part[1] * n))
             idx.append(np.arange(b, e))
             scope[r] = [i, i + (e - b)]
             i += e - b

@@ -153,10 +153,13 @@ class InductionNetwork(nn.Module):
                     grad_views=grad_views, seed_dev=seed_dev, packs=packs, glue=glue, pdict=p)
         e, _ = encode(inst, data, p, meta)
         return head_loss(e, p, labels, dict(E=B, N=N, K=K, Q=Q, iters=cfg.routing_iters, paper=paper, glue=glue,
-                                            packs=packs, pdict=p, reduction=cfg.loss_reduction))
+                                            packs=packs, pdict=p, reduction=cfg.loss_reduction,
+                                            loss_type=cfg.loss_type))
 
     # ------------------------------------------------------------------
     def loss(self, probs: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        if self.cfg.loss_type == "ce":
+            return ref.ce_loss(probs, labels.long(), self.cfg.loss_reduction)
         return ref.mse_loss(probs, labels.long(), self.cfg.loss_reduction)
 
     def l2_value(self) -> torch.Tensor:

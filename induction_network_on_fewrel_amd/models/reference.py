@@ -169,6 +169,30 @@ def mse_loss(probs: torch.Tensor, labels: torch.Tensor, reduction: str = "mean")
     return d.mean() if reduction == "mean" else d.sum() / max(1, probs.shape[0])
 
 
+CE_ODDS_EPS = 1e-7   # 1 - p floor when recovering the logit from a saturated sigmoid (same in glue.hip)
+
+
+def relation_logits(probs: torch.Tensor) -> torch.Tensor:
+    """Pre-sigmoid relation scores z = log p - log(1 - p) (exact where 1 - p > CE_ODDS_EPS)."""
+    return torch.log(probs) - torch.log(torch.clamp(1.0 - probs, min=CE_ODDS_EPS))
+
+
+def ce_loss(probs: torch.Tensor, labels: torch.Tensor, reduction: str = "mean") -> torch.Tensor:
+    """Softmax cross-entropy over the N relation scores of each query (``loss_type='ce'``, an
+    opt-in alternative to the reference's MSE-on-sigmoid).  NOTA queries (label == N) carry no
+    class to score and contribute zero loss.  ``mean``: over the labelled queries; ``sum``: summed
+    and divided by the episode count (like ``mse_loss``)."""
+    N = probs.shape[-1]
+    z = relation_logits(probs).reshape(-1, N)
+    lab = labels.reshape(-1).long()
+    keep = lab < N
+    nll = torch.nn.functional.cross_entropy(z, torch.where(keep, lab, torch.zeros_like(lab)), reduction="none")
+    nll = nll * keep.to(nll.dtype)
+    if reduction == "mean":
+        return nll.sum() / max(1, int(lab.numel()))
+    return nll.sum() / max(1, probs.shape[0])
+
+
 def predict(probs: torch.Tensor, nota_threshold: Optional[float] = None) -> torch.Tensor:
     pred = probs.argmax(-1)
     if nota_threshold is not None:

@@ -98,10 +98,14 @@ class HeadLossFn(torch.autograd.Function):
             wvec = torch.empty(0, dtype=torch.float32, device=e.device)
         probs = o.ntn_fwd(cls, e, mpack, wpack, wvec, b.detach().float().contiguous(), E, N, K, Q, h, paper, 0)
         rows = E * N * Q
-        scale = 1.0 / (rows * N) if meta.get("reduction", "mean") == "mean" else 1.0 / max(1, E)
+        ce = meta.get("loss_type", "mse") == "ce"
+        if meta.get("reduction", "mean") == "mean":
+            scale = 1.0 / rows if ce else 1.0 / (rows * N)
+        else:
+            scale = 1.0 / max(1, E)
         dz = torch.empty_like(probs)
         out = torch.empty(N + 3, dtype=torch.float32, device=e.device)
-        o.head_loss(probs, labels.reshape(-1), scale, dz, out, glue.loss_part, _loss_blocks(glue, rows))
+        o.head_loss(probs, labels.reshape(-1), scale, dz, out, glue.loss_part, _loss_blocks(glue, rows), ce)
         ctx.save_for_backward(e, Wsd, cls, mpack, m2pack, wtpack, wvec, dz, out)
         ctx.meta = dict(meta, H=H, h=h)
         ctx.set_materialize_grads(False)   # no zero-fill launches for the non-differentiable outputs

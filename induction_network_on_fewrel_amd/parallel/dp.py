@@ -46,9 +46,11 @@ class DistContext:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29500")
             os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
-            backend = "nccl" if use_cuda else "gloo"
+            # INA_DIST_BACKEND=gloo: several ranks sharing ONE GPU (RCCL refuses duplicate devices) --
+            # the one-card rehearsal of the multi-rank GPU step (tests/test_dp_gpu.py)
+            backend = os.environ.get("INA_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
             kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
-            if use_cuda:
+            if use_cuda and backend == "nccl":
                 kw["device_id"] = dev
             if not dist.is_initialized():
                 dist.init_process_group(**kw)

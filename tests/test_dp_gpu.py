@@ -1,0 +1,44 @@
+"""Multi-rank GPU training step on ONE card: bench.py under torch.distributed.run, world_size 2.
+
+RCCL refuses two ranks on the same device, so the collective backend here is gloo
+(INA_DIST_BACKEND=gloo, CUDA tensors); everything else is the driver's 8-GPU path: one process per
+rank, rank-folded device sampling, the fused kernels writing the flat gradient, the bucketed
+all-reduce + 1/world scaling inside the timed step, the fused Adam, the MAX-over-ranks timing and
+the rank-0 JSON line.  The check is that parameters stay bitwise identical across ranks
+(``params_in_sync``) for the eager step and for the HIP-graph step (all-reduce outside the graph).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("graph", [0, 1])
+def test_bench_world2_one_gpu(graph):
+    env = dict(os.environ, INA_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "2", "--episodes-per-gpu", "64", "--graph", str(graph)]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout   # rank 0 prints exactly one JSON line
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 128
+    assert out["params_in_sync"] is True
+    assert out["final_loss"] == out["final_loss"] and out["value"] > 0

@@ -95,6 +95,23 @@ def test_mse_mean_onehot_and_nota():
     assert pred.tolist() == [[3, 0]]
 
 
+def test_ce_loss_on_presigmoid_scores_and_nota():
+    """loss_type='ce': softmax cross-entropy over the pre-sigmoid relation scores; NOTA rows add 0
+    (mean over all query rows); gradient wrt the logits = (softmax - onehot) / rows."""
+    z = torch.randn(2, 6, 3, dtype=torch.float64, requires_grad=True)
+    labels = torch.tensor([[0, 1, 2, 0, 1, 3], [2, 2, 1, 0, 3, 3]])
+    loss = ref.ce_loss(torch.sigmoid(z), labels)
+    keep = labels < 3
+    want = torch.nn.functional.cross_entropy(z[keep], labels[keep], reduction="sum") / labels.numel()
+    assert torch.allclose(loss, want)
+    loss.backward()
+    sm = torch.softmax(z.detach(), -1)
+    g = (sm - torch.nn.functional.one_hot(labels.clamp(max=2), 3)) * keep.unsqueeze(-1) / labels.numel()
+    assert torch.allclose(z.grad, g, atol=1e-7)
+    cfg = Config(loss_type="ce")
+    cfg.validate()
+
+
 def test_param_names_shapes_and_init():
     cfg = Config(N=5, K=2, Q=5, hidden_size=20, max_length=37)
     wv = np.random.randn(1002, 5).astype(np.float32)

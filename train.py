@@ -33,6 +33,11 @@ def build_parser():
     p.add_argument("--eval_only", type=lambda s: s.lower() in ("1", "true", "yes"), default=False)
     p.add_argument("--train_relations", type=int, default=0,
                    help="with --split_val: how many of val.json's relations train (default: half)")
+    p.add_argument("--split_mode", default="relation", choices=["relation", "instance"],
+                   help="with --split_val: 'relation' = disjoint relations (few-shot transfer); 'instance' = "
+                        "every relation in both halves, disjoint sentences (train_fraction of each relation)")
+    p.add_argument("--train_fraction", type=float, default=0.7,
+                   help="with --split_mode instance: leading fraction of each relation's instances that trains")
     p.add_argument("--vocab_from_data", type=lambda s: s.lower() in ("1", "true", "yes"), default=False,
                    help="no GloVe file: build a random word table from the data's tokens")
     return p
@@ -59,6 +64,12 @@ def load_data(cfg: Config, args):
         full = FewRelDataset.from_json(cfg.val_file, wv, cfg.max_length, cfg.case_sensitive,
                                        processed_dir=cfg.processed_dir)
         rels = full.relations()
+        if getattr(args, "split_mode", "relation") == "instance":
+            f = args.train_fraction
+            if cfg.encoder == "bert":
+                raise SystemExit("--split_mode instance is implemented for the BiLSTM encoder")
+            return (full.subset_relations(rels, "train_split", part=(0.0, f)),
+                    full.subset_relations(rels, "val_split", part=(f, 1.0)))
         half = args.train_relations or len(rels) // 2
         tr, va = full.subset_relations(rels[:half], "train_split"), full.subset_relations(rels[half:], "val_split")
         return _with_bert(cfg, tr, va, cfg.val_file, full, rels, half)
