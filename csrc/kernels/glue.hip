@@ -39,6 +39,7 @@ constexpr int HL_NMAX = 16;
 constexpr int HL_PART = 2 + HL_NMAX;   // loss, correct, db[16]
 
 constexpr float CE_ODDS_EPS = 1e-7f;   // models/reference.py::CE_ODDS_EPS
+constexpr float CE_P_MIN = 1e-30f;     // models/reference.py::CE_P_MIN (z >= -69: no -inf / NaN)
 
 // rows = E * NQ; probs/dz [rows][N]; labels int32 [rows] (N = NOTA).
 // ce = 0: MSE on the sigmoid scores vs one-hot (reference).  ce = 1: softmax cross-entropy over the
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(256) void head_loss_kernel(const float* __restrict_
       float z[HL_NMAX], zm = -INFINITY, zl = 0.f;
 #pragma unroll
       for (int c = 0; c < HL_NMAX; ++c) {
-        z[c] = c < N ? logf(pv[c]) - logf(fmaxf(1.f - pv[c], CE_ODDS_EPS)) : -INFINITY;
+        z[c] = c < N ? logf(fmaxf(pv[c], CE_P_MIN)) - logf(fmaxf(1.f - pv[c], CE_ODDS_EPS)) : -INFINITY;
         zm = fmaxf(zm, z[c]);
         if (c == lab) zl = z[c];
       }

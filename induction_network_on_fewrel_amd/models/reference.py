@@ -170,11 +170,13 @@ def mse_loss(probs: torch.Tensor, labels: torch.Tensor, reduction: str = "mean")
 
 
 CE_ODDS_EPS = 1e-7   # 1 - p floor when recovering the logit from a saturated sigmoid (same in glue.hip)
+CE_P_MIN = 1e-30     # p floor: z >= -69, never -inf (an underflowed sigmoid would give inf / NaN losses)
 
 
 def relation_logits(probs: torch.Tensor) -> torch.Tensor:
-    """Pre-sigmoid relation scores z = log p - log(1 - p) (exact where 1 - p > CE_ODDS_EPS)."""
-    return torch.log(probs) - torch.log(torch.clamp(1.0 - probs, min=CE_ODDS_EPS))
+    """Pre-sigmoid relation scores z = log p - log(1 - p), exact for z in [-69, 16.1]; outside it the
+    clamps saturate z (and stop its gradient): a score already that confident is not pushed further."""
+    return torch.log(torch.clamp(probs, min=CE_P_MIN)) - torch.log(torch.clamp(1.0 - probs, min=CE_ODDS_EPS))
 
 
 def ce_loss(probs: torch.Tensor, labels: torch.Tensor, reduction: str = "mean") -> torch.Tensor:
