@@ -8,8 +8,9 @@
 //                with a precomputed int32 index (-1 -> 0); bf16 region then fp32 region.
 //  head_loss   : MSE loss vs one-hot labels (tf.one_hot semantics: NOTA -> zero row), accuracy
 //                (first-max argmax == label), the pre-sigmoid gradient dz = dL/dp * p(1-p) for the
-//                NTN backward and the bias gradient sum_rows dz.  Deterministic two-level reduce:
-//                per-block partials, then a one-block launch sums them in block order.
+//                NTN backward and the bias gradient sum_rows dz (loss_type ce: softmax cross-entropy
+//                over the relation scores instead).  Deterministic two-level reduce: per-block
+//                partials, then a one-block launch sums them with a fixed shuffle tree.
 //  slab_scatter: sum per-block gradient slabs over their blocks (chunked across workgroups, then
 //                the chunk partials summed in chunk order by a second launch) and ADD the
 //                result into the flat gradient at an int32 map (-1 = skip); transposes and pos-table
@@ -123,14 +124,18 @@ __global__ __launch_bounds__(256) void head_loss_kernel(const float* __restrict_
         (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 
-// second launch (the kernel boundary orders it after every partial): block-order sums
-__global__ __launch_bounds__(64) void head_loss_finish_kernel(const float* __restrict__ part, int nblocks, long rows,
-                                                              int N, float scale, float* __restrict__ out) {
+// second launch (the kernel boundary orders it after every partial): per column, lane b loads block
+// b's partial (nblocks <= 64: ONE load latency instead of a 64-long dependent chain) and a fixed
+// shuffle tree sums them -- deterministic
+__global__ __launch_bounds__(256) void head_loss_finish_kernel(const float* __restrict__ part, int nblocks, long rows,
+                                                               int N, float scale, float* __restrict__ out) {
   __shared__ float tot[HL_PART];
-  if (threadIdx.x < HL_PART) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int col = wave; col < HL_PART; col += 4) {
     float s = 0.f;
-    for (int b = 0; b < nblocks; ++b) s += part[(long)b * HL_PART + threadIdx.x];
-    tot[threadIdx.x] = s;
+    for (int b = lane; b < nblocks; b += 64) s += part[(long)b * HL_PART + col];
+    s = wave_sum(s);
+    if (lane == 0) tot[col] = s;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -233,7 +238,7 @@ int head_loss(const float* probs, const int* labels, long rows, int N, float sca
   if (N > HL_NMAX || rows <= 0) return -1;
   hipLaunchKernelGGL(head_loss_kernel, dim3(blocks), dim3(256), 0, st, probs, labels, rows, N, scale, ce, dz, part);
   INA_CHECK_LAUNCH();
-  hipLaunchKernelGGL(head_loss_finish_kernel, dim3(1), dim3(64), 0, st, part, blocks, rows, N, scale, out);
+  hipLaunchKernelGGL(head_loss_finish_kernel, dim3(1), dim3(256), 0, st, part, blocks, rows, N, scale, out);
   INA_CHECK_LAUNCH();
   return 0;
 }

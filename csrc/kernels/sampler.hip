@@ -25,92 +25,123 @@ struct Rng {
 };
 
 constexpr int MAXN = 32;    // ways
-constexpr int MAXKQ = 64;   // K + Q per class
+constexpr int MAXKQ = 64;   // K + Q per class (one lane per draw)
 constexpr int MAXNQ = 512;  // N * Q
+constexpr int SW = 4;       // episodes (waves) per workgroup
+constexpr int MAX_ROUNDS = 256;   // rejection rounds: an exit every wave reaches (host checks spans >= K + Q)
+
+INA_DEVICE uint32_t stream_key(uint32_t ekey, uint32_t id) { return hash_u32(ekey ^ ((id + 1u) * 0x632BE5ABu)); }
+
+INA_DEVICE void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
 }  // namespace
 
-__global__ __launch_bounds__(64) void sample_episodes_kernel(const int* __restrict__ scopes, int R, int E, int N, int K,
-                                                             int Q, uint32_t seed, float nota_rate,
-                                                             int* __restrict__ idx_out, int* __restrict__ lab_out,
-                                                             const int* __restrict__ seed_dev) {
+// One wave per episode (the first version ran one THREAD per episode: 32 waves for 2048 episodes and
+// the pick / query arrays in scratch).  Lanes work in parallel wherever the draws are independent:
+//   classes  : lane i holds class i; a wave-uniform rejection loop (ballot duplicate test);
+//   instances: per class, lane j draws pick j from its own counter stream; lanes that collide with a
+//              lower lane redraw (ballot) -- K + Q distinct instances in a few rounds;
+//   NOTA     : per query, lane-parallel;
+//   query permutation: random 32-bit key per query, rank = #smaller keys (ties by index) -> scatter.
+__global__ __launch_bounds__(256) void sample_episodes_kernel(const int* __restrict__ scopes, int R, int E, int N, int K,
+                                                              int Q, uint32_t seed, float nota_rate,
+                                                              int* __restrict__ idx_out, int* __restrict__ lab_out,
+                                                              const int* __restrict__ seed_dev) {
+  __shared__ int s_q[SW][MAXNQ];
+  __shared__ int s_l[SW][MAXNQ];
+  __shared__ uint32_t s_key[SW][MAXNQ];
+  __shared__ int s_x[SW][64];
   if (seed_dev) seed = (uint32_t)seed_dev[0];   // device-resident seed (HIP-graph replay)
-  const int ep = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ep >= E) return;
-  Rng rng{hash_u32(seed * 0x85EBCA77u + 0x27D4EB2Fu) ^ hash_u32((uint32_t)ep + 0x165667B1u), 0u};
-  int cls[MAXN];
-  for (int i = 0; i < N; ++i) {
-    int c;
-    bool dup;
-    do {
-      c = (int)rng.below((uint32_t)R);
-      dup = false;
-      for (int j = 0; j < i; ++j) dup |= (cls[j] == c);
-    } while (dup);
-    cls[i] = c;
-  }
-  const int rowlen = N * K + N * Q;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ep = blockIdx.x * SW + w;
+  if (ep >= E) return;   // wave-level synchronisation only below
+  const uint32_t ekey = hash_u32(seed * 0x85EBCA77u + 0x27D4EB2Fu) ^ hash_u32((uint32_t)ep + 0x165667B1u);
+  const int NQ = N * Q, KQ = K + Q;
+  const int rowlen = N * K + NQ;
   int* row = idx_out + (long)ep * rowlen;
-  int* lab = lab_out + (long)ep * N * Q;
-  int qidx[MAXNQ], qlab[MAXNQ];
+  int* lab = lab_out + (long)ep * NQ;
+  // ---- N distinct classes (every lane runs the same stream: wave-uniform control flow)
+  Rng rc{ekey, 0u};
+  int my_cls = -1;
   for (int i = 0; i < N; ++i) {
-    const int b = scopes[2 * cls[i]], e = scopes[2 * cls[i] + 1];
-    const int span = e - b;
-    int pick[MAXKQ];
-    for (int j = 0; j < K + Q; ++j) {
-      int x;
-      bool dup;
-      do {
-        x = (int)rng.below((uint32_t)span);
-        dup = false;
-        for (int t = 0; t < j; ++t) dup |= (pick[t] == x);
-      } while (dup);
-      pick[j] = x;
+    int c = 0;
+    for (int round = 0; round < MAX_ROUNDS; ++round) {
+      c = (int)rc.below((uint32_t)R);
+      if (__ballot(lane < i && my_cls == c) == 0) break;
     }
-    for (int j = 0; j < K; ++j) row[i * K + j] = b + pick[j];
-    for (int j = 0; j < Q; ++j) {
-      qidx[i * Q + j] = b + pick[K + j];
-      qlab[i * Q + j] = i;
+    if (lane == i) my_cls = c;
+  }
+  // ---- K + Q distinct instances of each class
+  for (int i = 0; i < N; ++i) {
+    const int ci = __shfl(my_cls, i, 64);
+    const int b = scopes[2 * ci], span = scopes[2 * ci + 1] - b;
+    Rng ri{stream_key(ekey, (uint32_t)(i * 64 + lane)), 0u};
+    int x = 0;
+    bool need = lane < KQ;
+    for (int round = 0; round < MAX_ROUNDS; ++round) {
+      if (need) x = (int)ri.below((uint32_t)span);
+      s_x[w][lane] = x;
+      wave_lds_sync();
+      bool dup = false;
+      if (lane < KQ)
+        for (int k = 0; k < lane; ++k) dup |= (s_x[w][k] == x);
+      wave_lds_sync();
+      need = dup;
+      if (__ballot(need) == 0) break;
+    }
+    if (lane < K) row[i * K + lane] = b + x;
+    else if (lane < KQ) {
+      s_q[w][i * Q + lane - K] = b + x;
+      s_l[w][i * Q + lane - K] = i;
     }
   }
+  wave_lds_sync();
+  // ---- NOTA queries: an instance of a relation outside the episode, label N
   if (nota_rate > 0.f && R > N) {
-    for (int qq = 0; qq < N * Q; ++qq) {
-      if (rng.uniform() < nota_rate) {
-        int c;
-        bool in;
-        do {
-          c = (int)rng.below((uint32_t)R);
-          in = false;
-          for (int j = 0; j < N; ++j) in |= (cls[j] == c);
-        } while (in);
+    for (int qq = lane; qq < NQ; qq += 64) {
+      Rng rn{stream_key(ekey, (uint32_t)(MAXN * 64 + qq)), 0u};
+      if (rn.uniform() < nota_rate) {
+        int c = 0;
+        for (int round = 0; round < MAX_ROUNDS; ++round) {
+          c = (int)rn.below((uint32_t)R);
+          bool in = false;
+          for (int j = 0; j < N; ++j) in |= (__shfl(my_cls, j, 64) == c);
+          if (!in) break;
+        }
         const int b = scopes[2 * c], e = scopes[2 * c + 1];
-        qidx[qq] = b + (int)rng.below((uint32_t)(e - b));
-        qlab[qq] = N;
+        s_q[w][qq] = b + (int)rn.below((uint32_t)(e - b));
+        s_l[w][qq] = N;
       }
     }
   }
-  // Fisher-Yates permutation of the queries
-  for (int i = N * Q - 1; i > 0; --i) {
-    const int j = (int)rng.below((uint32_t)(i + 1));
-    const int ti = qidx[i], tl = qlab[i];
-    qidx[i] = qidx[j];
-    qlab[i] = qlab[j];
-    qidx[j] = ti;
-    qlab[j] = tl;
+  // ---- uniform random permutation of the queries: rank by random keys (ties broken by index)
+  for (int qq = lane; qq < NQ; qq += 64) {
+    Rng rk{stream_key(ekey, (uint32_t)(2 * MAXN * 64 + qq)), 0u};
+    s_key[w][qq] = rk.next();
   }
-  for (int i = 0; i < N * Q; ++i) {
-    row[N * K + i] = qidx[i];
-    lab[i] = qlab[i];
+  wave_lds_sync();
+  for (int qq = lane; qq < NQ; qq += 64) {
+    const uint32_t kq = s_key[w][qq];
+    int rank = 0;
+    for (int k = 0; k < NQ; ++k) {
+      const uint32_t kk = s_key[w][k];
+      rank += (kk < kq || (kk == kq && k < qq)) ? 1 : 0;
+    }
+    row[N * K + rank] = s_q[w][qq];
+    lab[rank] = s_l[w][qq];
   }
 }
 
 namespace ina {
 
-bool sampler_supported(int N, int K, int Q) { return N <= MAXN && K + Q <= MAXKQ && N * Q <= MAXNQ; }
+bool sampler_supported(int N, int K, int Q) { return N <= MAXN && N <= 64 && K + Q <= MAXKQ && N * Q <= MAXNQ; }
 
 int sample_episodes(const int* scopes, int R, int E, int N, int K, int Q, uint32_t seed, float nota_rate, int* idx,
                     int* lab, const int* seed_dev, hipStream_t st) {
-  hipLaunchKernelGGL(sample_episodes_kernel, dim3((E + 63) / 64), dim3(64), 0, st, scopes, R, E, N, K, Q, seed,
+  hipLaunchKernelGGL(sample_episodes_kernel, dim3((E + SW - 1) / SW), dim3(256), 0, st, scopes, R, E, N, K, Q, seed,
                      nota_rate, idx, lab, seed_dev);
   INA_CHECK_LAUNCH();
   return 0;

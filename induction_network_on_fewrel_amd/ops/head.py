@@ -125,13 +125,26 @@ class HeadLossFn(torch.autograd.Function):
         de = torch.empty_like(e)
         cls_bf = torch.empty(E * N, H, dtype=torch.bfloat16, device=e.device)
         dcls, dp, dw_slab = o.ntn_bwd(cls, e, mpack, m2pack, wtpack, wvec, dz, de, E, N, K, Q, h, paper, 0, g, cls_bf)
-        dMf = torch.mm(cls_bf.t(), dp, out_dtype=torch.float32)          # [H, h*H] (col s*H + b)
+        # dM = C^T dP over K = E*N rows: split-K as a batched GEMM [ns, H, h*H] (a plain [H=40] x
+        # [h*H=4000] GEMM has only ~63 output tiles -- a quarter of the CUs streaming the 82 MB dP); the
+        # ns partial slabs are summed by the glue's deterministic slab scatter-add
+        ns = _dm_splits(E * N)
+        dMf = torch.bmm(cls_bf.view(ns, -1, H).transpose(1, 2), dp.view(ns, -1, dp.shape[1]),
+                        out_dtype=torch.float32)                          # [ns, H, h*H] (col s*H + b)
         slab = o.routing_bwd(e, Ws, dcls, de, E, N, K, Q, R, 0)
         glue.add(dw_slab, glue.map_identity(p["ntn_w"]), E)
         glue.add(out[2 + N:3 + N] if paper else out[2:2 + N], glue.map_identity(p["ntn_b"]), 1, scale=g)
         glue.add(slab, glue.map_identity(p["W_s"]), slab.shape[0])
-        glue.add(dMf, glue.map_ntn_M(p["M"]), 1)
+        glue.add(dMf, glue.map_ntn_M(p["M"]), ns)
         return de, None, None, None, None, None, None
+
+
+def _dm_splits(rows: int) -> int:
+    """Split-K factor of the dM GEMM: >= 1024 (episode, class) rows per split, dividing ``rows``."""
+    for ns in (8, 4, 2):
+        if rows % ns == 0 and rows // ns >= 1024:
+            return ns
+    return 1
 
 
 def _loss_blocks(glue, rows: int) -> int:

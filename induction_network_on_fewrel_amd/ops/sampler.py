@@ -23,7 +23,10 @@ class DeviceDataset:
         self.pos1 = t(data.data_pos1)
         self.pos2 = t(data.data_pos2)
         self.mask = t(data.data_mask)
-        self.scopes = t(data.scope_array())
+        sc = data.scope_array()
+        self.scopes = t(sc)
+        self.min_span = int((sc[:, 1] - sc[:, 0]).min()) if len(sc) else 0
+        self.num_relations = int(len(sc))
         self.L = data.max_length
         self.bert = ({k: t(data.bert[k]) for k in ("ids", "mask", "e1", "e2")} if data.bert is not None else None)
 
@@ -45,6 +48,10 @@ class DeviceEpisodeSampler:
     def sample(self, B: int, N: int, K: int, Q: int, seed_dev=None):
         """-> (idx int32 [B, N*K+N*Q], labels int32 [B, N*Q]) on the device.  ``seed_dev`` (int32
         device scalar) replaces the host seed (HIP-graph replay; runtime/graph.py)."""
+        if K + Q > self.dd.min_span or N > self.dd.num_relations:
+            # the kernel's rejection loops need K + Q distinct instances per relation and N relations
+            raise ValueError(f"episode {N}-way K+Q={K + Q} needs >= {N} relations with >= {K + Q} instances "
+                             f"each (have {self.dd.num_relations}, smallest {self.dd.min_span})")
         s = (self.seed * 1000003 + self.calls * 7919) & 0x7FFFFFFF
         self.calls += 1
         return ops().sample_episodes(self.dd.scopes, B, N, K, Q, s, self.nota_rate, seed_dev)
