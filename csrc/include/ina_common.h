@@ -74,38 +74,65 @@ INA_DEVICE bool dropout_keep(uint32_t seed, uint32_t dir, uint32_t idx, uint32_t
 }
 
 // ------------------------------------------------------------------ reductions
-INA_DEVICE float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// Cross-lane data movement without the LDS pipe: __shfl_xor lowers to ds_bpermute_b32 (an LDS
+// instruction with tens of cycles of latency plus an address VGPR); these use DPP lane permutes
+// inside a 16-lane row (folded into the v_add / v_max) and the gfx950 v_permlane16/32_swap row
+// exchanges across rows.  Every step combines symmetric pairs, so all lanes of the reduced group
+// end with bitwise the same value; the order is fixed (deterministic), not the xor-butterfly order.
+namespace dpp {
+constexpr int QUAD_XOR1 = 0xB1;         // quad_perm:[1,0,3,2]
+constexpr int QUAD_XOR2 = 0x4E;         // quad_perm:[2,3,0,1]
+constexpr int ROW_HALF_MIRROR = 0x141;  // lane i <- 7 - i within each 8
+constexpr int ROW_MIRROR = 0x140;       // lane i <- 15 - i within each 16
+template <int CTRL>
+INA_DEVICE float mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
 }
-INA_DEVICE float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+// permlane16_swap(x, x) -> (rows 0,0,2,2 ; rows 1,1,3,3); permlane32_swap(x, x) -> (lo,lo ; hi,hi)
+INA_DEVICE void swap16(float v, float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                  false, false);
+  a = __builtin_bit_cast(float, (unsigned)r[0]);
+  b = __builtin_bit_cast(float, (unsigned)r[1]);
 }
+INA_DEVICE void swap32(float v, float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                  false, false);
+  a = __builtin_bit_cast(float, (unsigned)r[0]);
+  b = __builtin_bit_cast(float, (unsigned)r[1]);
+}
+}  // namespace dpp
+
 // sum over the 16 lanes that share a lane group (same l>>4)
 INA_DEVICE float group16_sum(float v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v += dpp::mov<dpp::QUAD_XOR1>(v);
+  v += dpp::mov<dpp::QUAD_XOR2>(v);
+  v += dpp::mov<dpp::ROW_HALF_MIRROR>(v);
+  v += dpp::mov<dpp::ROW_MIRROR>(v);
   return v;
 }
 INA_DEVICE float group16_max(float v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  v = fmaxf(v, dpp::mov<dpp::QUAD_XOR1>(v));
+  v = fmaxf(v, dpp::mov<dpp::QUAD_XOR2>(v));
+  v = fmaxf(v, dpp::mov<dpp::ROW_HALF_MIRROR>(v));
+  v = fmaxf(v, dpp::mov<dpp::ROW_MIRROR>(v));
   return v;
 }
 // sum over the 4 lane groups (lanes n, n+16, n+32, n+48)
 INA_DEVICE float cross_group_sum(float v) {
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
+  float a, b;
+  dpp::swap16(v, a, b);
+  dpp::swap32(a + b, a, b);
+  return a + b;
 }
 INA_DEVICE float cross_group_max(float v) {
-  v = fmaxf(v, __shfl_xor(v, 16, 64));
-  v = fmaxf(v, __shfl_xor(v, 32, 64));
-  return v;
+  float a, b;
+  dpp::swap16(v, a, b);
+  dpp::swap32(fmaxf(a, b), a, b);
+  return fmaxf(a, b);
 }
+INA_DEVICE float wave_sum(float v) { return cross_group_sum(group16_sum(v)); }
+INA_DEVICE float wave_max(float v) { return cross_group_max(group16_max(v)); }
 
 // Deterministic workgroup reduction: the waves add their contributions into a shared LDS buffer one
 // after another (wave 0 first), so the fp32 summation order never depends on scheduling (LDS float

@@ -154,7 +154,7 @@ class InductionNetwork(nn.Module):
         e, _ = encode(inst, data, p, meta)
         return head_loss(e, p, labels, dict(E=B, N=N, K=K, Q=Q, iters=cfg.routing_iters, paper=paper, glue=glue,
                                             packs=packs, pdict=p, reduction=cfg.loss_reduction,
-                                            loss_type=cfg.loss_type))
+                                            loss_type=cfg.loss_type, overlap=overlap))
 
     # ------------------------------------------------------------------
     def loss(self, probs: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:

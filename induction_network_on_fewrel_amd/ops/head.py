@@ -136,6 +136,10 @@ class HeadLossFn(torch.autograd.Function):
         glue.add(out[2 + N:3 + N] if paper else out[2:2 + N], glue.map_identity(p["ntn_b"]), 1, scale=g)
         glue.add(slab, glue.map_identity(p["W_s"]), slab.shape[0])
         glue.add(dMf, glue.map_ntn_M(p["M"]), ns)
+        ov = m.get("overlap")
+        if ov is not None:   # DP: scatter the head's gradients now and start their all-reduce (bucket 0)
+            glue.flush()
+            ov.ready(0)
         return de, None, None, None, None, None, None
 
 

@@ -106,6 +106,7 @@ class Trainer:
         self.gpu_phase_ms = {k: 0.0 for k in self.timers}                                # HIP-event time
         self._pending_events = []
         self._graph = None   # runtime/graph.py::GraphedTrainStep when cfg.use_hip_graph
+        self._head_span = self._contiguous_span(("W_s", "M", "ntn_w", "ntn_b"))
         # fault injection (tests / chaos runs): raise at a given global step on a given rank
         self._fault_step = int(os.environ.get("INA_FAULT_STEP", "-1"))
         self._fault_rank = int(os.environ.get("INA_FAULT_RANK", "0"))
@@ -121,6 +122,14 @@ class Trainer:
             s.arrays = dd.arrays(self.cfg.encoder)
             return s
         return _HostEpisodes(data, seed, nota, self.cfg.encoder)
+
+    def _contiguous_span(self, names):
+        """(offset, numel) of parameters that are adjacent in the flat buffer, else None."""
+        idx = sorted(self.flat.names.index(n) for n in names if n in self.flat.names)
+        if not idx or idx != list(range(idx[0], idx[0] + len(idx))):
+            return None
+        off = self.flat.offsets[idx[0]]
+        return off, self.flat.offsets[idx[-1]] + self.flat.numels[idx[-1]] - off
 
     def _sync(self):
         """Phase boundary: with ``profile`` on a GPU, record a HIP event (no host synchronisation)."""
@@ -180,6 +189,10 @@ class Trainer:
             from ..ops.bert import layer_spans
             ov = self.dist.overlap(self.flat.grad, layer_spans(self.model, self.flat.names, self.flat.offsets,
                                                                self.flat.numels))
+        elif self.dist.world > 1 and self.glue is not None and self._head_span is not None:
+            # BiLSTM step: the relation head's gradients (W_s, M, w, b: ~94% of the parameters) are final
+            # after the head backward -> their all-reduce runs under the attention + BiLSTM backward
+            ov = self.dist.overlap(self.flat.grad, [self._head_span])
         loss, acc_t, _ = self.model.forward_train(idx.view(-1), self.train_eps.arrays, B, N, K, Q, labels,
                                                   dropout_seed=self.dropout_seed(), grad_views=gv, overlap=ov,
                                                   glue=self.glue)

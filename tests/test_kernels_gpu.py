@@ -334,7 +334,8 @@ def test_step_glue_matches_unfused(tmp_path, head, loss):
     (h0, p0), (h1, p1) = runs
     for (l0, a0), (l1, a1) in zip(h0, h1):
         assert abs(l0 - l1) < 1e-4 * max(1.0, abs(l0)), (l0, l1)
-        assert abs(a0 - a1) < 1e-6
+        # at most 2 of the 480 queries may flip on a near-tie (the two paths round differently)
+        assert abs(a0 - a1) <= 2.0 / (24 * 5 * 4) + 1e-6, (a0, a1)
     assert _relerr(p1, p0) < 2e-3
 
 
