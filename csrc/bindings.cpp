@@ -125,7 +125,7 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
                                             const Tensor& p2emb, const Tensor& apack, const Tensor& a2pack,
                                             const Tensor& bias, const Tensor& hraw, const Tensor& cst, const Tensor& dH,
                                             const Tensor& dmask, int64_t U, int64_t NX, bool bf16, bool word_grad,
-                                            int64_t blocks, int64_t seed, double keep_prob) {
+                                            int64_t blocks, int64_t seed, double keep_prob, bool pos_shift) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -164,7 +164,10 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   const int64_t pitems = ntiles * ((L + 1) / 2);
   const int64_t pblocks = std::max<int64_t>(1, std::min<int64_t>(1024, (pitems + 31) / 32));
   if (bf16) TORCH_CHECK(2 * PD <= 16 && 2 * L <= 128, "ina.lstm_bwd: bf16 path needs pos_dim <= 8 and L <= 64");
-  auto dpos_slab = bf16 ? at::empty({pblocks, 1, 2, 2 * L, PD}, opt) : at::empty({blocks, 2, 2, 2 * L, PD}, opt);
+  // pos_shift (caller-checked pos[s][t] = pos[s][0] + t, pos[s][0] <= L): per-sequence one-hot GEMM -> ONE slab
+  const bool shift = bf16 && pos_shift && (L + 1 + 15) / 16 <= 5;
+  auto dpos_slab = shift ? at::empty({1, 1, 2, 2 * L, PD}, opt)
+                         : (bf16 ? at::empty({pblocks, 1, 2, 2 * L, PD}, opt) : at::empty({blocks, 2, 2, 2 * L, PD}, opt));
   // [2 dir][tiles][L][2PD][16] bf16 dx of the pos features, then [tiles][L][16] u16 position ids
   Tensor dxp = bf16 ? at::empty({(2 * 2 * PD + 1) * ntiles * L * 16}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
   Tensor dwemb = word_grad ? at::zeros_like(wemb) : at::empty({0}, opt);
@@ -202,7 +205,13 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   a.drop = keep_prob < 1.0 ? 1 : 0;
   a.dxp = bf16 ? dxp.data_ptr() : nullptr;
   check_launch(ina::lstm_bwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_bwd");
-  if (bf16) check_launch(ina::pos_grad(a, (int)pblocks, dpos_slab.data_ptr<float>(), cur_stream()), "pos_grad");
+  if (shift) {
+    Tensor gpart = at::empty({(int64_t)ina::pos_shift_workspace_floats((int)S, (int)L, (int)PD, nullptr, nullptr)}, opt);
+    check_launch(ina::pos_grad_shift(a, gpart.data_ptr<float>(), dpos_slab.data_ptr<float>(), cur_stream()),
+                 "pos_grad_shift");
+  } else if (bf16) {
+    check_launch(ina::pos_grad(a, (int)pblocks, dpos_slab.data_ptr<float>(), cur_stream()), "pos_grad");
+  }
   return {dw_slab, dpos_slab, dwemb};
 }
 

@@ -41,6 +41,10 @@ int lstm_fwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
 int lstm_bwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
 // bf16 mode: reduce a.dxp into slab [blocks][2 tables][2L][PD] (needs 2L <= 128, 2PD <= 16)
 int pos_grad(const LstmArgs& a, int blocks, float* slab, hipStream_t st);
+// bf16 mode, position ids pos[s][t] = o_s + t (checked by the caller): the same reduction as a
+// per-sequence one-hot GEMM (gpart: pos_shift_workspace_floats floats) -> out [2 tables][2L][PD]
+size_t pos_shift_workspace_floats(int S, int L, int PD, int* nchunk, int* kps);
+int pos_grad_shift(const LstmArgs& a, float* gpart, float* out, hipStream_t st);
 bool lstm_supported(int U, int NX);
 size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD);
 

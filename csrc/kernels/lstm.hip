@@ -746,6 +746,109 @@ __global__ __launch_bounds__(256) void pos_grad_kernel(const unsigned short* __r
 }
 
 // ------------------------------------------------------------------------------------------
+// pos-table gradients, shifted-position form (bf16 mode).  FewRel position ids are a shifted arange
+// per sequence: pos[s][t] = o_s + t (o_s = L - entity index, model/base.py / util/data_loader.py:
+// pos = j - p + L), checked on the host (ops/sampler.py::DeviceDataset.pos_shift).  Then
+//   dpos[p][c] = sum_t G[p - t][t][c],   G[o][t][c] = sum_{s : o_s = o} dx[s][t][c]
+// and G is a GEMM with K = sequences and a per-SEQUENCE one-hot: one v_mfma_f32_16x16x32_bf16 covers
+// 32 sequences x 16 (t, c) columns, instead of 32 (sequence, step) samples x 16 positions in the
+// general kernel above -- ~37x fewer MFMAs and one-hot builds.  o_s <= L, so NRT = ceil((L+1)/16)
+// row tiles.  Stage 1 (this kernel): wave = (table, 16-column tile, chunk of K-steps), partial G per
+// chunk -> gpart[chunk][table][NRT*16][NT*16].  Stage 2 (pos_shift_finish): one workgroup per output
+// (table, p, c) sums chunks and the diagonal in a fixed order (deterministic).
+// ------------------------------------------------------------------------------------------
+template <int NRT>
+__global__ __launch_bounds__(256) void pos_shift_gemm_kernel(const unsigned short* __restrict__ dxp, int S, int L,
+                                                             int PD, int kps, float* __restrict__ gpart) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane >> 4, n = lane & 15;
+  const int ntiles = (S + 15) / 16, NPF = 2 * PD;
+  const int ncol = L * PD, NT = (ncol + 15) / 16;
+  const int gw = blockIdx.x * 4 + wave;   // (table, column tile)
+  if (gw >= 2 * NT) return;               // no workgroup barrier in this kernel
+  const int tb = gw / NT, nt = gw - tb * NT;
+  const int ci = nt * 16 + n;             // this lane's B column = (step t, feature c)
+  const bool cval = ci < ncol;
+  const int t = cval ? ci / PD : 0;
+  const int f = tb * PD + (cval ? ci - t * PD : 0);
+  const size_t dstride = (size_t)ntiles * L * NPF * 16;
+  const unsigned short* posb = dxp + 2 * dstride;   // [tiles][L][16] p1 | p2 << 8
+  const int half = (q & 1) * 8, sh = tb * 8;
+  const int ksteps = (ntiles + 1) / 2;   // 32 sequences (2 tiles) per K-step
+  const int k0 = blockIdx.y * kps, k1 = min(ksteps, k0 + kps);
+  f32x4_t acc[NRT];
+#pragma unroll
+  for (int pt = 0; pt < NRT; ++pt) acc[pt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // B fragment: lane (q, n) holds sequences 8(q&1)..+7 of tile 2ks + (q>>1) at column n (16 B, both
+  // directions); the one-hot A row n of tile pt marks the sequences whose offset is pt*16 + n
+  auto load = [&](int ks, u16x8_t& b0, u16x8_t& b1, u16x8_t& pp, bool& ok) {
+    const int tile = 2 * ks + (q >> 1);
+    ok = cval && tile < ntiles && ks < k1;
+    const int tl = tile < ntiles ? tile : ntiles - 1;
+    const size_t o = (((size_t)tl * L + t) * NPF + f) * 16 + half;
+    b0 = *reinterpret_cast<const u16x8_t*>(dxp + o);
+    b1 = *reinterpret_cast<const u16x8_t*>(dxp + dstride + o);
+    pp = *reinterpret_cast<const u16x8_t*>(posb + (size_t)tl * L * 16 + half);   // ids at t = 0
+  };
+  u16x8_t nb0, nb1, npp;
+  bool nok;
+  if (k0 < k1) load(k0, nb0, nb1, npp, nok);
+  for (int ks = k0; ks < k1; ++ks) {
+    u16x8_t b0 = nb0, b1 = nb1, pp = npp;
+    const bool ok = nok;
+    load(ks + 1, nb0, nb1, npp, nok);   // clamped addresses past the chunk: loaded, never used
+    if (!ok) b0 = b1 = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    // pair bits m = (1 << tile(o_2w)) | (1 << (16 + tile(o_2w+1))) for sequences whose offset lands on
+    // row n (15 = no hit, never a tile index); tile pt's packed bf16 pair = ((m >> pt) & 0x10001) * 0x3F80
+    uint32_t m[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t o0 = ((uint32_t)pp[2 * w] >> sh) & 0xFF, o1 = ((uint32_t)pp[2 * w + 1] >> sh) & 0xFF;
+      const uint32_t h0 = (o0 & 15) == (uint32_t)n ? (o0 >> 4) : 15u;
+      const uint32_t h1 = (o1 & 15) == (uint32_t)n ? (o1 >> 4) : 15u;
+      m[w] = (1u << h0) | (1u << (16 + h1));
+    }
+#pragma unroll
+    for (int pt = 0; pt < NRT; ++pt) {
+      uint32_t wv[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) wv[w] = __umul24((m[w] >> pt) & 0x10001u, 0x3F80u);
+      u16x8_t a;
+      __builtin_memcpy(&a, wv, 16);
+      acc[pt] = mfma_bf16(a, b0, acc[pt]);
+      acc[pt] = mfma_bf16(a, b1, acc[pt]);
+    }
+  }
+  // D[row = 4q + r][col = n] of tile pt = (offset pt*16 + 4q + r, column nt*16 + n)
+  float* g = gpart + ((size_t)blockIdx.y * 2 + tb) * (NRT * 16) * (NT * 16);
+#pragma unroll
+  for (int pt = 0; pt < NRT; ++pt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) g[(size_t)(pt * 16 + 4 * q + r) * (NT * 16) + nt * 16 + n] = acc[pt][r];
+}
+
+// out[tb][p][c] = sum_chunk sum_t gpart[chunk][tb][p - t][t * PD + c]   (one workgroup per output)
+__global__ __launch_bounds__(256) void pos_shift_finish_kernel(const float* __restrict__ gpart, int nchunk, int L,
+                                                               int PD, int rows, float* __restrict__ out) {
+  __shared__ float red[4];
+  const int P2 = 2 * L, NT = (L * PD + 15) / 16;
+  const int id = blockIdx.x;   // (tb * P2 + p) * PD + c
+  const int c = id % PD, p = (id / PD) % P2, tb = id / (PD * P2);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tlo = max(0, p - rows + 1), thi = min(L - 1, p);   // 0 <= p - t < rows
+  const int nt_ = thi >= tlo ? thi - tlo + 1 : 0;
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nchunk * nt_; i += 256) {
+    const int ch = i / nt_, t = tlo + (i - ch * nt_);
+    acc += gpart[(((size_t)ch * 2 + tb) * rows + (p - t)) * (NT * 16) + t * PD + c];
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) red[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[id] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
 namespace ina {
@@ -840,6 +943,37 @@ int pos_grad(const LstmArgs& a, int blocks, float* slab, hipStream_t st) {
   } else {
     return -1;
   }
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+size_t pos_shift_workspace_floats(int S, int L, int PD, int* nchunk, int* kps) {
+  const int ntiles = (S + 15) / 16, ksteps = (ntiles + 1) / 2;
+  const int NT = (L * PD + 15) / 16, NRT = (L + 1 + 15) / 16 <= 3 ? 3 : 5;
+  int nc = (4096 + 2 * NT - 1) / (2 * NT);      // ~4096 waves in flight
+  nc = nc < 1 ? 1 : (nc > ksteps ? ksteps : nc);
+  const int k = (ksteps + nc - 1) / nc;
+  nc = (ksteps + k - 1) / k;
+  if (nchunk) *nchunk = nc;
+  if (kps) *kps = k;
+  return (size_t)nc * 2 * NRT * 16 * NT * 16;
+}
+
+int pos_grad_shift(const LstmArgs& a, float* gpart, float* out, hipStream_t st) {
+  int nchunk = 0, kps = 0;
+  pos_shift_workspace_floats(a.S, a.L, a.PD, &nchunk, &kps);
+  const int NT = (a.L * a.PD + 15) / 16, NRT = (a.L + 1 + 15) / 16;
+  if (NRT > 5 || a.S <= 0) return -1;
+  const auto* dxp = (const unsigned short*)a.dxp;
+  dim3 grid((2 * NT + 3) / 4, nchunk), block(256);
+  if (NRT <= 3)
+    hipLaunchKernelGGL(pos_shift_gemm_kernel<3>, grid, block, 0, st, dxp, a.S, a.L, a.PD, kps, gpart);
+  else
+    hipLaunchKernelGGL(pos_shift_gemm_kernel<5>, grid, block, 0, st, dxp, a.S, a.L, a.PD, kps, gpart);
+  INA_CHECK_LAUNCH();
+  const int rows = (NRT <= 3 ? 3 : 5) * 16;
+  hipLaunchKernelGGL(pos_shift_finish_kernel, dim3(2 * 2 * a.L * a.PD), dim3(256), 0, st, gpart, nchunk, a.L, a.PD,
+                     rows, out);
   INA_CHECK_LAUNCH();
   return 0;
 }

@@ -76,7 +76,8 @@ class EncoderFn(torch.autograd.Function):
         dw_slab, dpos_slab, dwemb = o.lstm_bwd(inst, word, pos1, pos2, wemb.detach().contiguous(),
                                                p1emb.detach().contiguous(), p2emb.detach().contiguous(), apack, a2pack,
                                                bias, hlane, cst, dH, dmask, U, m["NX"], bf16, word_grad,
-                                               int(m.get("lstm_blocks", 0)), int(m["seed"]), float(m["keep_prob"]))
+                                               int(m.get("lstm_blocks", 0)), int(m["seed"]), float(m["keep_prob"]),
+                                               bool(m.get("pos_shift", False)))
         glue = m.get("glue")
         if glue is not None:
             # slabs -> flat gradient in the step's single slab_scatter_add launch (StepGlue.flush)
@@ -111,6 +112,8 @@ class EncoderFn(torch.autograd.Function):
 def encode(inst, data, params, meta):
     """data = (word, pos1, pos2, mask) device int32 arrays [NI, L]; returns (e [S, 2u], alphas [S, L])."""
     word, pos1, pos2, mask = data
+    # position ids known to be shifted aranges (ops/sampler.py::DeviceArrays): cheaper pos-table gradient
+    meta = dict(meta, pos_shift=bool(getattr(data, "pos_shift", False)))
     return EncoderFn.apply(inst, word, pos1, pos2, mask, params["word_embedding"], params["pos1_embedding"],
                            params["pos2_embedding"], params["lstm_fw_kernel"], params["lstm_fw_bias"],
                            params["lstm_bw_kernel"], params["lstm_bw_bias"], params["attn_kernel"],

@@ -14,6 +14,21 @@ from ..data.fewrel import FewRelDataset
 from ._ext import ops
 
 
+class DeviceArrays(tuple):
+    """(word, pos1, pos2, mask) device arrays; ``pos_shift`` = every sequence's position ids are a
+    shifted arange (pos[s][t] = pos[s][0] + t, 0 <= pos[s][0] <= L: FewRel's ``j - p + L``), which
+    lets the backward reduce the position-table gradients as a per-sequence one-hot GEMM."""
+    pos_shift = False
+
+
+def positions_are_shifted(pos: np.ndarray) -> bool:
+    if pos.ndim != 2 or pos.size == 0:
+        return False
+    L = pos.shape[1]
+    return bool((pos - pos[:, :1] == np.arange(L, dtype=pos.dtype)[None]).all() and (pos[:, 0] >= 0).all()
+                and (pos[:, 0] <= L).all())
+
+
 class DeviceDataset:
     def __init__(self, data: FewRelDataset, device):
         self.data = data
@@ -28,6 +43,7 @@ class DeviceDataset:
         self.min_span = int((sc[:, 1] - sc[:, 0]).min()) if len(sc) else 0
         self.num_relations = int(len(sc))
         self.L = data.max_length
+        self.pos_shift = positions_are_shifted(data.data_pos1) and positions_are_shifted(data.data_pos2)
         self.bert = ({k: t(data.bert[k]) for k in ("ids", "mask", "e1", "e2")} if data.bert is not None else None)
 
     def arrays(self, encoder: str = "bilstm"):
@@ -35,7 +51,9 @@ class DeviceDataset:
             if self.bert is None:
                 raise ValueError("dataset has no BERT features (data/bert_tokenize.py)")
             return self.bert["ids"], self.bert["mask"], self.bert["e1"], self.bert["e2"]
-        return self.word, self.pos1, self.pos2, self.mask
+        out = DeviceArrays((self.word, self.pos1, self.pos2, self.mask))
+        out.pos_shift = self.pos_shift
+        return out
 
 
 class DeviceEpisodeSampler:

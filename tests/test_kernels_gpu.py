@@ -167,6 +167,36 @@ def test_encoder_backward(dtype, keep_prob):
         assert err < tol_g, k
 
 
+@pytest.mark.parametrize("B", [3, 41])
+def test_pos_grad_shift_matches_general(B):
+    """pos-table gradient as a per-sequence one-hot GEMM (position ids = shifted aranges, FewRel's
+    j - p + L) == the general per-token one-hot reduction, on the same lstm_bwd dx rows."""
+    from induction_network_on_fewrel_amd.ops import ops
+    from induction_network_on_fewrel_amd.ops.packing import lstm_shape, pack_lstm
+    cfg, data, model, dd, inst, _ = _problem(B=B, dtype="bf16")
+    assert dd.pos_shift
+    p = model.pdict()
+    U = cfg.hidden_size
+    DIN = model.params.input_dim
+    NX = lstm_shape(U, DIN, True)["NX"]
+    apack, a2pack = pack_lstm(p["lstm_fw_kernel"], p["lstm_bw_kernel"], U, DIN, True)
+    bias = torch.stack([p["lstm_fw_bias"], p["lstm_bw_bias"]]).detach().float().contiguous()
+    word, pos1, pos2, _ = dd.arrays()
+    tabs = [p[k].detach().contiguous() for k in ("word_embedding", "pos1_embedding", "pos2_embedding")]
+    hlane, cst, hnat, dmask = ops().lstm_fwd(inst, word, pos1, pos2, *tabs, apack, bias, U, NX, True, True, 5, 0.9,
+                                             None)
+    dH = torch.randn(hnat.shape[0], hnat.shape[1], 2 * U, device=DEV).to(torch.bfloat16)[: inst.shape[0]].contiguous()
+    outs = []
+    for shift in (False, True):
+        _, dpos, _ = ops().lstm_bwd(inst, word, pos1, pos2, *tabs, apack, a2pack, bias, hlane, cst, dH, dmask, U, NX,
+                                    True, False, 0, 5, 0.9, shift)
+        outs.append(dpos.sum((0, 1)))
+    torch.cuda.synchronize()
+    err = _relerr(outs[1], outs[0])
+    print(f"pos grad shift vs general (B={B}): {err:.2e}")
+    assert outs[1].shape == outs[0].shape and err < 1e-5
+
+
 @pytest.mark.parametrize("head", ["reference", "paper"])
 @pytest.mark.parametrize("shape", [(5, 2, 5), (5, 1, 5), (10, 5, 2), (3, 3, 5)])
 def test_head_forward_backward(head, shape):

@@ -79,7 +79,7 @@ def main():
     t, (dH, aslab) = timed(lambda: o.attn_bwd(hnat, inst, w1pack, w1tpack, b1, w2, de, alphas, U, True, 0))
     res["attn_bwd"] = t
     t, _ = timed(lambda: o.lstm_bwd(inst, word, pos1, pos2, wemb, p1, p2, apack, a2pack, bias, hlane, cst, dH, dmask, U,
-                                    sh["NX"], True, False, 0, 7, 0.9))
+                                    sh["NX"], True, False, 0, 7, 0.9, False))
     res["lstm_bwd"] = t
     res["encoder_total"] = res["lstm_fwd"] + res["attn_fwd"] + res["attn_bwd"] + res["lstm_bwd"]
     print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in res.items()}))
