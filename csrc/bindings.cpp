@@ -49,14 +49,17 @@ uint32_t keep_threshold(double kp) {
 
 
 // ------------------------------------------------------------------ LSTM
-// Returns (hlane, cst, hnat): hlane = raw recurrent h and cst = cell states, both in the
+// Returns (hlane, cst, hnat, dmask, xg): hlane = raw recurrent h and cst = cell states, both in the
 // lane-native tile layout [ceil(S/16), 2, L, U/4, 64] (only when store_c: the backward needs them);
-// hnat = the DropoutWrapper output in natural layout [S, L, 2U] (the attention input).
-std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
+// hnat = the DropoutWrapper output in natural layout [S, L, 2U] (the attention input); dmask = the
+// dropout keep bits; xg (bf16 mode) = the gathered encoder input [tiles][L][64][NX] followed by the
+// position ids [tiles][L][16] (x_gather_kernel; an input of lstm_bwd).
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
                                             const Tensor& pos2, const Tensor& wemb, const Tensor& p1emb,
                                             const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U,
                                             int64_t NX, bool bf16, bool store_c, int64_t seed, double keep_prob,
-                                            const std::optional<Tensor>& seed_dev) {
+                                            const std::optional<Tensor>& seed_dev,
+                                            const std::optional<Tensor>& wrows) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -92,7 +95,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Te
   // dropout keep bits for the backward (one byte per lane-step), only when both are needed
   Tensor dmask = (store_c && drop) ? at::empty({ntiles, 2, L, 64}, word.options().dtype(at::kByte))
                                    : at::empty({0}, word.options().dtype(at::kByte));
-  if (S == 0) return {hlane, cst, hnat, dmask};
+  TORCH_CHECK(ntiles * L * (64 * NX + 16) < (1LL << 31), "ina.lstm_fwd: batch too large for the x rows");
+  Tensor xg = bf16 ? at::empty({ntiles * L * (64 * NX + 16)}, word.options().dtype(at::kBFloat16))
+                   : at::empty({0}, word.options().dtype(at::kBFloat16));
+  if (S == 0) return {hlane, cst, hnat, dmask, xg};
   ina::LstmArgs a{};
   a.inst = inst.data_ptr<int>();
   a.S = (int)S;
@@ -116,16 +122,26 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Te
   a.thr = keep_threshold(keep_prob);
   a.inv_kp = (float)(1.0 / keep_prob);
   a.drop = drop ? 1 : 0;
+  a.wrows = dev_float(wrows, "wrows");
+  if (a.wrows)
+    TORCH_CHECK(wrows->numel() == word.numel() * E && word.numel() < (1 << 24),
+                "ina.lstm_fwd: wrows must be [NI * L, E] with NI * L < 2^24");
+  if (bf16) {
+    a.xg = xg.data_ptr();
+    a.posb = reinterpret_cast<const unsigned short*>(xg.data_ptr<at::BFloat16>() + ntiles * L * 64 * NX);
+    check_launch(ina::x_gather(a, (int)NX, cur_stream()), "x_gather");
+  }
   check_launch(ina::lstm_fwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_fwd");
-  return {hlane, cst, hnat, dmask};
+  return {hlane, cst, hnat, dmask, xg};
 }
 
 std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
                                             const Tensor& pos2, const Tensor& wemb, const Tensor& p1emb,
                                             const Tensor& p2emb, const Tensor& apack, const Tensor& a2pack,
                                             const Tensor& bias, const Tensor& hraw, const Tensor& cst, const Tensor& dH,
-                                            const Tensor& dmask, int64_t U, int64_t NX, bool bf16, bool word_grad,
-                                            int64_t blocks, int64_t seed, double keep_prob, bool pos_shift) {
+                                            const Tensor& dmask, const Tensor& xg, int64_t U, int64_t NX, bool bf16,
+                                            bool word_grad, int64_t blocks, int64_t seed, double keep_prob,
+                                            bool pos_shift) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -168,8 +184,12 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   const bool shift = bf16 && pos_shift && (L + 1 + 15) / 16 <= 5;
   auto dpos_slab = shift ? at::empty({1, 1, 2, 2 * L, PD}, opt)
                          : (bf16 ? at::empty({pblocks, 1, 2, 2 * L, PD}, opt) : at::empty({blocks, 2, 2, 2 * L, PD}, opt));
-  // [2 dir][tiles][L][2PD][16] bf16 dx of the pos features, then [tiles][L][16] u16 position ids
-  Tensor dxp = bf16 ? at::empty({(2 * 2 * PD + 1) * ntiles * L * 16}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
+  // [2 dir][tiles][L][2PD][16] bf16 dx of the pos features
+  Tensor dxp = bf16 ? at::empty({2 * 2 * PD * ntiles * L * 16}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
+  if (bf16) {
+    check(xg, "xg", at::kBFloat16);
+    TORCH_CHECK(xg.numel() == ntiles * L * (64 * NX + 16), "ina.lstm_bwd: xg (from lstm_fwd) shape");
+  }
   Tensor dwemb = word_grad ? at::zeros_like(wemb) : at::empty({0}, opt);
   if (S == 0) {
     dw_slab.zero_();
@@ -204,6 +224,9 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   a.inv_kp = (float)(1.0 / keep_prob);
   a.drop = keep_prob < 1.0 ? 1 : 0;
   a.dxp = bf16 ? dxp.data_ptr() : nullptr;
+  a.xg = bf16 ? xg.data_ptr() : nullptr;
+  a.posb = bf16 ? reinterpret_cast<const unsigned short*>(xg.data_ptr<at::BFloat16>() + ntiles * L * 64 * NX)
+                : nullptr;
   check_launch(ina::lstm_bwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_bwd");
   if (shift) {
     Tensor gpart = at::empty({(int64_t)ina::pos_shift_workspace_floats((int)S, (int)L, (int)PD, nullptr, nullptr)}, opt);
@@ -525,7 +548,7 @@ void step_control(Tensor ctl, Tensor lrt, int64_t seedA, int64_t seedB, double l
                "step_control");
 }
 
-int64_t abi_version() { return 2; }
+int64_t abi_version() { return 3; }
 
 }  // namespace
 

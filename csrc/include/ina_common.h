@@ -46,6 +46,13 @@ INA_DEVICE float tanhf_(float x) {
   const float e = __expf(2.0f * x);
   return 1.0f - 2.0f * fast_rcp(e + 1.0f);
 }
+// Pre-scaled forms: the argument already carries the exp2 range factor, z = log2(e) x (sigmoid)
+// resp. z = 2 log2(e) x (tanh).  The LSTM kernels fold these factors into their gate weight rows
+// and biases once per kernel, so each activation on the recurrence is v_exp + v_add + v_rcp
+// (+ one v_fma for tanh): no per-step range multiply.
+constexpr float LOG2E_F = 1.44269504088896341f;
+INA_DEVICE float sigmoid_l2(float z) { return fast_rcp(1.0f + __builtin_amdgcn_exp2f(-z)); }
+INA_DEVICE float tanh_l2(float z) { return 1.0f - 2.0f * fast_rcp(__builtin_amdgcn_exp2f(z) + 1.0f); }
 
 // ------------------------------------------------------------------ RNG
 // Counter-based hash; bit-identical to models/reference.py::hash_u32.

@@ -33,10 +33,15 @@ struct LstmArgs {
   unsigned char* dmask;  // [tiles][2][L][64] dropout keep bits (bit m = unit 4m+q), written by fwd, read by bwd
   const int* seed_dev;   // optional device-resident dropout seed (overrides seed; HIP-graph replay)
   void* dxp;             // bf16 bwd: pos-feature gradients [2 dir][tiles][L][2PD][16] (reduced by pos_grad)
+  void* xg;              // bf16: x_gather output [tiles][L][64 lanes][NX] (input of lstm_fwd / lstm_bwd)
+  const unsigned short* posb;   // bf16: x_gather position ids [tiles][L][16] = pos1 | pos2 << 8
+  const float* wrows;    // optional [NI * L][E]: word rows per token (x_gather reads them directly)
   uint32_t seed, thr;
   float inv_kp;
   int drop;
 };
+// bf16 mode: gather every token's x features once into a.xg / a.posb (lstm.hip x_gather_kernel)
+int x_gather(const LstmArgs& a, int NX, hipStream_t st);
 int lstm_fwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
 int lstm_bwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
 // bf16 mode: reduce a.dxp into slab [blocks][2 tables][2L][PD] (needs 2L <= 128, 2PD <= 16)

@@ -13,6 +13,8 @@
 // units it owns (and x features 4xi+q): the recurrence h_t -> B operand never leaves the lane.
 // The backward reuses the same trick for d[x;h] = W dG, and transposes (dG, XH) through
 // wave-private LDS every 2 steps to accumulate dW with MFMAs (32 samples per K-step).
+#include <type_traits>
+
 #include "ina_common.h"
 #include "ina_launch.h"
 
@@ -21,6 +23,24 @@ using namespace ina;
 
 #ifndef INA_FWD_PIPE
 #define INA_FWD_PIPE 1
+#endif
+// bf16 forward: x-row ring depth (prefetch distance XG_RING - 1 steps)
+#ifndef XG_RING
+#define XG_RING 4
+#endif
+// timing experiments (wrong values): INA_EXP_ACT=1 VALU-only activations, INA_EXP_NOX=1 no x gathers,
+// INA_FWD_GATHER=1 bf16 forward gathers x per step itself, INA_SKIP_XG=1 no x_gather launch
+#ifndef INA_FWD_GATHER
+#define INA_FWD_GATHER 0
+#endif
+#ifndef INA_SKIP_XG
+#define INA_SKIP_XG 0
+#endif
+#ifndef INA_EXP_ACT
+#define INA_EXP_ACT 0
+#endif
+#ifndef INA_EXP_NOX
+#define INA_EXP_NOX 0
 #endif
 
 namespace {
@@ -132,12 +152,93 @@ INA_DEVICE float gather_x(const XSrc& s, const XRow& r) {
   return s.base[off];
 }
 
+// exp2 range factor of gate type g (i, j, f, o): the kernels scale their gate weight rows and biases
+// by it once (sigmoid_l2 / tanh_l2 in ina_common.h), and add the forget bias 1.0 to the f bias first.
+// Weight fragment row = lane & 15, gate type = row & 3 = lane & 3 (csrc/kernels header comment).
+INA_DEVICE float gate_scale(int g) { return g == 1 ? 2.f * LOG2E_F : LOG2E_F; }
+INA_DEVICE float gate_bias(float b, int g) { return (b + (g == 2 ? 1.f : 0.f)) * gate_scale(g); }
+INA_DEVICE u16x8_t fscale(u16x8_t a, float s) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = f2bf(bf2f(a[j]) * s);
+  return a;
+}
+INA_DEVICE float fscale(float a, float s) { return a * s; }
+
+template <int I, int N, class F>
+INA_DEVICE void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// s_waitcnt vmcnt(N) that the value d (an inline-asm load destination) depends on
+template <int N>
+INA_DEVICE void vm_wait(uint64_t& d) {
+  asm volatile("s_waitcnt vmcnt(%1)" : "+v"(d) : "n"(N) : "memory");
+}
+
 INA_DEVICE void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 
 }  // namespace
+
+// ------------------------------------------------------------------------------------------
+// encoder input gather (bf16 mode; K1 of SURVEY 2.3).  The recurrences used to gather their x
+// features per step (a random 20-byte word-table row per token, 2 directions x fwd + bwd = 4 times
+// per token, one step of prefetch): latency-bound on L2/MALL misses (kbench: 0.44 -> 0.29 ms
+// forward without the gathers).  This kernel gathers every token ONCE with full memory-level
+// parallelism (one thread per token) into the lane-ownership layout the recurrences consume as
+// one coalesced 8-byte load per lane-step:
+//   xg[tile][t][lane = 16 q + n][xi] = bf16 x feature 4 xi + q of sequence 16 tile + n at step t
+//                                      (0 past DIN and for padding sequences >= S)
+//   posb[tile][t][n] = pos1 | pos2 << 8 (position ids of the pos-table gradient kernels)
+// x enters the gate MFMAs as bf16 in this mode, so the values are exactly the ones the per-step
+// gather produced.
+// ------------------------------------------------------------------------------------------
+constexpr int XG_T = 16;   // steps per workgroup (16 sequences x 16 steps = 256 threads)
+template <int NX, bool DIRECT>
+__global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ inst, int S,
+                                                      const int* __restrict__ word, const int* __restrict__ pos1,
+                                                      const int* __restrict__ pos2, int L,
+                                                      const float* __restrict__ wemb, int E,
+                                                      const float* __restrict__ p1emb,
+                                                      const float* __restrict__ p2emb, int PD,
+                                                      unsigned short* __restrict__ xg,
+                                                      unsigned short* __restrict__ posb) {
+  // thread = one token (sequence n = tid & 15, step t0 + tid / 16): its id / row loads are runs along
+  // t (coalesced), and it writes its NX x 4 features as 4 lane-group chunks; for a fixed step the
+  // 16 sequences' chunks of one lane group are one contiguous 16 x 8-byte segment.
+  const int tile = blockIdx.x;
+  const int n = threadIdx.x & 15, t = blockIdx.y * XG_T + (threadIdx.x >> 4);
+  const int seq = tile * 16 + n;
+  const bool valid = seq < S;
+  const long r = (long)inst[valid ? seq : S - 1] * L + min(t, L - 1);   // clamped: unconditional loads
+  const int p1 = pos1[r], p2 = pos2[r];
+  const float* wrow = DIRECT ? wemb + r * E : wemb + (long)word[r] * E;
+  const float* p1row = p1emb + p1 * PD;
+  const float* p2row = p2emb + p2 * PD;
+  const int DIN = E + 2 * PD;
+  float x[4 * NX];
+#pragma unroll
+  for (int f = 0; f < 4 * NX; ++f)   // E, PD are kernel arguments: the source branches are uniform
+    x[f] = f < E ? wrow[f] : (f < E + PD ? p1row[f - E] : (f < DIN ? p2row[f - E - PD] : 0.f));
+  if (t >= L) return;
+  unsigned short* dst = xg + (size_t)(tile * L + t) * 64 * NX;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    unsigned short v[NX];
+#pragma unroll
+    for (int xi = 0; xi < NX; ++xi) v[xi] = f2bf(valid ? x[4 * xi + q] : 0.f);
+#pragma unroll
+    for (int c = 0; c < NX / 4; ++c)
+      *reinterpret_cast<u16x4_t*>(dst + (q * 16 + n) * NX + 4 * c) =
+          u16x4_t{v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
+  }
+  posb[(size_t)(tile * L + t) * 16 + n] = (unsigned short)(p1 | (p2 << 8));
+}
 
 // ------------------------------------------------------------------------------------------
 // forward
@@ -152,7 +253,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     const typename FragT<BF16>::type* __restrict__ apack, const float* __restrict__ bias,
     typename FragT<BF16>::elem* __restrict__ hlane, typename CT<BF16>::type* __restrict__ cst,
     typename FragT<BF16>::elem* __restrict__ hnat, unsigned char* __restrict__ dmask, uint32_t seed, uint32_t thr,
-    float inv_kp, int drop, const int* __restrict__ seed_dev) {
+    float inv_kp, int drop, const int* __restrict__ seed_dev, const unsigned short* __restrict__ xg) {
   if (seed_dev) seed = (uint32_t)seed_dev[0];   // device-resident dropout seed (HIP-graph replay)
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
@@ -165,19 +266,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   const int ntiles = (S + 15) / 16;
   const int tile = blockIdx.x * 4 + wave;
   int2* ids = ids_all + wave * 16 * L;
-  // stage (word, pos1 | pos2 << 16) of the wave's 16 sequences into LDS
-  for (int i = lane; i < 16 * L; i += 64) {
-    int sn = i / L, t = i - sn * L;
-    int sq = tile * 16 + sn;
-    int2 v = make_int2(0, 0);
-    if (tile < ntiles && sq < S) {
-      long r = (long)inst[sq] * L + t;
-      v.x = word[r];
-      v.y = pos1[r] | (pos2[r] << 16);
+  constexpr bool FG = !BF16 || INA_FWD_GATHER;   // gather x per step (fp32 mode)
+  if constexpr (FG) {
+    // fp32 mode gathers x per step: stage (word, pos1 | pos2 << 16) of the wave's 16 sequences into LDS
+    for (int i = lane; i < 16 * L; i += 64) {
+      int sn = i / L, t = i - sn * L;
+      int sq = tile * 16 + sn;
+      int2 v = make_int2(0, 0);
+      if (tile < ntiles && sq < S) {
+        long r = (long)inst[sq] * L + t;
+        v.x = word[r];
+        v.y = pos1[r] | (pos2[r] << 16);
+      }
+      ids[i] = v;
     }
-    ids[i] = v;
+    wave_lds_sync();
   }
-  wave_lds_sync();
   if (tile >= ntiles) return;
   const int seq = tile * 16 + n;  // rows >= S are padding rows of hnat (allocated to 16 * ntiles)
   const uint32_t salt = dropout_salt(seed, (uint32_t)dir);
@@ -187,12 +291,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
 #pragma unroll
   for (int m = 0; m < NMT; ++m)
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) A[m][ks] = ap[(m * NKS + ks) * 64 + lane];
-  float bm[NMT][4];
+    for (int ks = 0; ks < NKS; ++ks) A[m][ks] = fscale(ap[(m * NKS + ks) * 64 + lane], gate_scale(lane & 3));
+  float bm[NMT][4];   // pre-scaled gate biases (gate_bias)
 #pragma unroll
   for (int m = 0; m < NMT; ++m)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bm[m][r] = bias[dir * 4 * U + r * U + 4 * m + q];
+    for (int r = 0; r < 4; ++r) bm[m][r] = gate_bias(bias[dir * 4 * U + r * U + 4 * m + q], r);
 
   float h[U4], c[U4];
 #pragma unroll
@@ -205,10 +309,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
 #pragma unroll
   for (int xi = 0; xi < NX; ++xi) pofs[xi] = (4 * xi + q - E) * 16 + n;
   auto load_x = [&](int t, float* xv) {
-    const int2 id = ids[n * L + t];
-    const XRow r = xrow(id.x, id.y & 0xffff, id.y >> 16, E, PD);
+    if constexpr (!FG) {   // x_gather_kernel output: one coalesced 8-byte load per 4 features
+      const unsigned short* xp = xg + ((uint32_t)(tile * L + t) * 64 + lane) * NX;
 #pragma unroll
-    for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(xs[xi], r);
+      for (int c = 0; c < NX / 4; ++c) {
+        const u16x4_t v = *reinterpret_cast<const u16x4_t*>(xp + 4 * c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[4 * c + e] = bf2f(v[e]);
+      }
+    } else {
+      const int2 id = ids[n * L + t];
+      const XRow r = xrow(id.x, id.y & 0xffff, id.y >> 16, E, PD);
+#pragma unroll
+      for (int xi = 0; xi < NX; ++xi) xv[xi] = INA_EXP_NOX ? __int_as_float(r.w) : gather_x(xs[xi], r);
+    }
   };
   // one recurrence step at processing index tau with input features xv
   auto step = [&](const int tau, const float* xv) __attribute__((always_inline)) {
@@ -231,10 +345,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
       f32x4_t acc = {bm[m][0], bm[m][1], bm[m][2], bm[m][3]};
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) acc = mma(A[m][ks], B[ks], acc);
-      const float ig = sigmoidf_(acc[0]), jg = tanhf_(acc[1]), fg = sigmoidf_(acc[2] + 1.0f),
-                  og = sigmoidf_(acc[3]);
+#if INA_EXP_ACT
+      const float ig = fmaf(acc[0], 0.1f, 0.5f), jg = fmaf(acc[1], 0.1f, 0.f), fg = fmaf(acc[2], 0.1f, 0.5f),
+                  og = fmaf(acc[3], 0.1f, 0.5f);
       c[m] = c[m] * fg + ig * jg;
-      float hv = tanhf_(c[m]) * og;
+      float hv = fmaf(c[m], 0.1f, 0.f) * og;
+#else
+      const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
+      c[m] = c[m] * fg + ig * jg;
+      float hv = tanh_l2(c[m] * (2.f * LOG2E_F)) * og;
+#endif
       if (BF16) hv = round_bf(hv);  // the stored / recurrent operand value
       h[m] = hv;
     }
@@ -275,6 +395,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   // block (odd-L tail peeled, prefetch index clamped) so LLVM cannot sink the prefetch loads down
   // to their uses.
   auto tof = [&](int tau) { return dir ? (L - 1 - tau) : tau; };
+  if constexpr (!FG && NX == 4) {
+    // x rows (x_gather_kernel) stream from HBM.  A ring of R raw rows keeps R - 1 steps of prefetch
+    // in flight.  The loads are issued by inline asm and retired by explicit counted waits: the
+    // compiler's waitcnt pass merges the loop-header state conservatively and waited vmcnt(3) at the
+    // top of every body, i.e. for all of the previous steps' ~16 stores (store latency on the
+    // recurrence).  The count is exact because the step's VMEM stream is fixed at compile time:
+    // NST stores per step (hnat U4, hlane U4, cst U4, dmask 1; no compiler-visible loads in the loop).
+    // Order of VMEM ops: ld(0..R-2), then per step j: ld(j + R - 1), NST stores of step j; before
+    // step j's math the ops issued after ld(j) number R - 1 + min(j, R - 1) * NST.
+    constexpr int R = XG_RING;
+    constexpr int NST = U4 + (STORE ? 2 * U4 : 0) + ((DROP && STORE && U4 <= 8) ? 1 : 0);
+    auto ld = [&](int tau, uint64_t& d) __attribute__((always_inline)) {
+      const unsigned short* xp = xg + ((uint32_t)(tile * L + tof(min(tau, L - 1))) * 64 + lane) * NX;
+      asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(d) : "v"(xp) : "memory");
+    };
+    auto run = [&](int tau, uint64_t d) __attribute__((always_inline)) {
+      float xv[NX];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xv[e] = bf2f((unsigned short)(d >> (16 * e)));
+      step(tau, xv);
+    };
+    uint64_t xr[R];
+    // one body = R steps; FIRST: the peeled first body (the prologue loads precede it)
+    auto body = [&](int tau, auto first) __attribute__((always_inline)) {
+      static_for<0, R>([&](auto kc) __attribute__((always_inline)) {
+        constexpr int k = decltype(kc)::value;
+        constexpr int n = decltype(first)::value ? R - 1 + k * NST : (R - 1) * (NST + 1);
+        ld(tau + k + R - 1, xr[(k + R - 1) % R]);
+        vm_wait<(n < 63 ? n : 63)>(xr[k]);
+        __builtin_amdgcn_sched_barrier(0);
+        run(tau + k, xr[k]);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    };
+#pragma unroll
+    for (int k = 0; k < R - 1; ++k) ld(k, xr[k]);
+    int tau = 0;
+    if (L >= R) {
+      body(0, std::true_type{});
+      tau = R;
+      for (; tau + R - 1 < L; tau += R) body(tau, std::false_type{});
+    }
+    // tail (< R steps, no further loads): ops issued after ld(tau + k) >= R - 2 - k + k * NST
+    static_for<0, R - 1>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value;
+      constexpr int n = R - 2 - k + k * NST;
+      if (tau + k < L) {
+        vm_wait<(n < 63 ? n : 63)>(xr[k]);
+        run(tau + k, xr[k]);
+      }
+    });
+    return;
+  }
   float xa[NX], xb[NX];
 #if INA_FWD_PIPE == 0
   // simple loop: prefetch x_{tau+1}, copy at the end of the step
@@ -335,7 +508,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     const typename CT<BF16>::type* __restrict__ cst, const typename FragT<BF16>::elem* __restrict__ dH,
     float* __restrict__ dw_slab,
     float* __restrict__ dpos_slab, float* __restrict__ dwemb, const unsigned char* __restrict__ dmask, uint32_t seed,
-    uint32_t thr, float inv_kp, int drop, unsigned short* __restrict__ dxp) {
+    uint32_t thr, float inv_kp, int drop, unsigned short* __restrict__ dxp, const unsigned short* __restrict__ xg) {
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
   using elem = typename FragT<BF16>::elem;
@@ -371,9 +544,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   }
   off = (off + 15) & ~(size_t)15;
   float* dpos_lds = reinterpret_cast<float*>(smem + off);   // [2 tables][2L][PD]
-  for (int i = threadIdx.x; i < NA; i += 256) lA[i] = apack[(size_t)dir * NA + i];
+  // gate packs / biases pre-scaled as in the forward (fragment index i -> lane i & 63, gate i & 3);
+  // the transposed pack (d[x;h] = W dG) keeps the true weights
+  for (int i = threadIdx.x; i < NA; i += 256) lA[i] = fscale(apack[(size_t)dir * NA + i], gate_scale(i & 3));
   for (int i = threadIdx.x; i < NA2; i += 256) lA2[i] = a2pack[(size_t)dir * NA2 + i];
-  for (int i = threadIdx.x; i < 4 * U; i += 256) lbias[i] = bias[dir * 4 * U + i];
+  for (int i = threadIdx.x; i < 4 * U; i += 256) lbias[i] = gate_bias(bias[dir * 4 * U + i], i / U);
   if constexpr (!BF16)
     for (int i = threadIdx.x; i < 2 * P2 * PD; i += 256) dpos_lds[i] = 0.f;
   const int NPF = 2 * PD;   // pos features (bf16 mode: exported to dxp, reduced by pos_grad_kernel)
@@ -411,9 +586,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     const typename CT<BF16>::type* cbase = cst + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
     const elem* hbase = hraw + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
     auto tof = [&](int tau) { return dir ? (L - 1 - tau) : tau; };  // processing step -> time
-    // software pipeline: ids two steps ahead, everything else one step ahead
-    int wid_c, p1_c, p2_c, wid_n, p1_n, p2_n;
-    {
+    // bf16: x from the x_gather_kernel rows (one coalesced load per 4 features), no token ids
+    auto load_xg = [&](int t, float* xv) {
+      const unsigned short* xp = xg + ((uint32_t)(tile * L + t) * 64 + lane) * NX;
+#pragma unroll
+      for (int c = 0; c < NX / 4; ++c) {
+        const u16x4_t v = *reinterpret_cast<const u16x4_t*>(xp + 4 * c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[4 * c + e] = bf2f(v[e]);
+      }
+    };
+    // software pipeline (fp32 mode): ids two steps ahead, everything else one step ahead
+    int wid_c = 0, p1_c = 0, p2_c = 0, wid_n = 0, p1_n = 0, p2_n = 0;
+    if constexpr (!BF16) {
       const int t0 = tof(L - 1), t1 = tof(L >= 2 ? L - 2 : 0);
       wid_c = word[rowbase + t0]; p1_c = pos1[rowbase + t0]; p2_c = pos2[rowbase + t0];
       wid_n = word[rowbase + t1]; p1_n = pos1[rowbase + t1]; p2_n = pos2[rowbase + t1];
@@ -423,8 +608,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     {
       const int t = tof(L - 1), tp = tof(L >= 2 ? L - 2 : 0);
       const uint32_t bits = drop ? (uint32_t)mbase[(size_t)t * 64] : 0xFFu;
+      if constexpr (BF16) {
+        load_xg(t, xv);
+      } else {
 #pragma unroll
-      for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(xs[xi], xrow(wid_c, p1_c, p2_c, E, PD));
+        for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(xs[xi], xrow(wid_c, p1_c, p2_c, E, PD));
+      }
 #pragma unroll
       for (int m = 0; m < U4; ++m) {
         ccur[m] = from_c(cbase[((size_t)t * U4 + m) * 64]);
@@ -459,11 +648,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       const int taunn = tau >= 2 ? tau - 2 : 0;
       const bool n_has_prev = tau >= 2;
       const int tn = tof(taun), tnp = tof(taunn), tnn = tof(taunn);
-      const int wid_nn = word[rowbase + tnn], p1_nn = pos1[rowbase + tnn], p2_nn = pos2[rowbase + tnn];
+      int wid_nn = 0, p1_nn = 0, p2_nn = 0;
+      if constexpr (!BF16) {
+        wid_nn = word[rowbase + tnn];
+        p1_nn = pos1[rowbase + tnn];
+        p2_nn = pos2[rowbase + tnn];
+      }
       float xv_n[NX], hp_n[U4], cprev_n[U4], dhin_n[U4];
       const uint32_t bits_n = drop ? (uint32_t)mbase[(size_t)tn * 64] : 0xFFu;
+      if constexpr (BF16) {
+        load_xg(tn, xv_n);
+      } else {
 #pragma unroll
-      for (int xi = 0; xi < NX; ++xi) xv_n[xi] = gather_x(xs[xi], xrow(wid_n, p1_n, p2_n, E, PD));
+        for (int xi = 0; xi < NX; ++xi) xv_n[xi] = gather_x(xs[xi], xrow(wid_n, p1_n, p2_n, E, PD));
+      }
 #pragma unroll
       for (int m = 0; m < U4; ++m) {
         const float cp = from_c(cbase[((size_t)tnp * U4 + m) * 64]);
@@ -498,9 +696,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         f32x4_t acc = {bm[m][0], bm[m][1], bm[m][2], bm[m][3]};
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) acc = mma(lA[(m * NKS + ks) * 64 + lane], B[ks], acc);
-        const float ig = sigmoidf_(acc[0]), jg = tanhf_(acc[1]), fg = sigmoidf_(acc[2] + 1.0f),
-                    og = sigmoidf_(acc[3]);
-        const float tc = tanhf_(ccur[m]);
+        const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
+        const float tc = tanh_l2(ccur[m] * (2.f * LOG2E_F));
         const float dh = dh_rec[m] + dhin[m];
         const float dc = dc_rec[m] + dh * og * (1.f - tc * tc);
         const float di = dc * jg, dj = dc * ig, df = dc * cprev[m], d_o = dh * tc;
@@ -541,10 +738,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
 #pragma unroll
         for (int xi = 0; xi < NX; ++xi)
           if ((uint32_t)(xs[xi].sel - 1) < 2u) drow[pofs[xi]] = f2bf(valid ? dslot[U4 + xi] : 0.f);
-        // the token's position ids (p1 | p2 << 8) for the reduction, written once (direction 0)
-        if (dir == 0 && q == 0)
-          dxp[(size_t)2 * ntiles * L * NPF * 16 + ((size_t)tile * L + tof(tau)) * 16 + n] =
-              (unsigned short)(p1 | (p2 << 8));
+        // (the reduction's position ids come from x_gather_kernel's posb)
       } else {
 #pragma unroll
         for (int xi = 0; xi < NX; ++xi) {
@@ -555,9 +749,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       // word table (global atomics, only when trained)
       if (dwemb) {
         if (valid) {
+          const int wrow = BF16 ? word[rowbase + tof(tau)] : wid;   // bf16: not pipelined (trained words only)
 #pragma unroll
           for (int xi = 0; xi < NX; ++xi)
-            if (xs[xi].sel == 0) atomicAdd(&dwemb[(long)wid * E + xs[xi].col], dslot[U4 + xi]);
+            if (xs[xi].sel == 0) atomicAdd(&dwemb[(long)wrow * E + xs[xi].col], dslot[U4 + xi]);
         }
       }
       // ---- stage (dG, XH) for the dW MFMA: sample column = n + 16 * (tau & 1)
@@ -653,7 +848,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
 // (2L <= 16 * NPT, ids < 256).
 // ------------------------------------------------------------------------------------------
 template <int NPT>
-__global__ __launch_bounds__(256) void pos_grad_kernel(const unsigned short* __restrict__ dxp, int S, int L, int PD,
+__global__ __launch_bounds__(256) void pos_grad_kernel(const unsigned short* __restrict__ dxp,
+                                                       const unsigned short* __restrict__ posb, int S, int L, int PD,
                                                        float* __restrict__ slab) {
   __shared__ float red[4][2 * 16 * NPT * 8];   // per-wave partials (summed in fixed order: deterministic)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -661,7 +857,6 @@ __global__ __launch_bounds__(256) void pos_grad_kernel(const unsigned short* __r
   const int ntiles = (S + 15) / 16, npairs = (L + 1) / 2, NPF = 2 * PD, P2 = 2 * L;
   const long items = (long)ntiles * npairs;
   const size_t dstride = (size_t)ntiles * L * NPF * 16;   // one direction of dxp
-  const unsigned short* posb = dxp + 2 * dstride;         // [tiles][L][16] p1 | p2 << 8
   const int half = (kg & 1) * 8, sstep = kg >> 1;         // fragment k = 8 kg + e <-> (step, seq)
   const int col = i16 < NPF ? i16 : NPF - 1;
   f32x4_t acc[2][NPT];
@@ -758,7 +953,8 @@ __global__ __launch_bounds__(256) void pos_grad_kernel(const unsigned short* __r
 // (table, p, c) sums chunks and the diagonal in a fixed order (deterministic).
 // ------------------------------------------------------------------------------------------
 template <int NRT>
-__global__ __launch_bounds__(256) void pos_shift_gemm_kernel(const unsigned short* __restrict__ dxp, int S, int L,
+__global__ __launch_bounds__(256) void pos_shift_gemm_kernel(const unsigned short* __restrict__ dxp,
+                                                             const unsigned short* __restrict__ posb, int S, int L,
                                                              int PD, int kps, float* __restrict__ gpart) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = lane >> 4, n = lane & 15;
@@ -772,7 +968,6 @@ __global__ __launch_bounds__(256) void pos_shift_gemm_kernel(const unsigned shor
   const int t = cval ? ci / PD : 0;
   const int f = tb * PD + (cval ? ci - t * PD : 0);
   const size_t dstride = (size_t)ntiles * L * NPF * 16;
-  const unsigned short* posb = dxp + 2 * dstride;   // [tiles][L][16] p1 | p2 << 8
   const int half = (q & 1) * 8, sh = tb * 8;
   const int ksteps = (ntiles + 1) / 2;   // 32 sequences (2 tiles) per K-step
   const int k0 = blockIdx.y * kps, k1 = min(ksteps, k0 + kps);
@@ -880,13 +1075,14 @@ static int launch_fwd_t(const LstmArgs& a, hipStream_t st) {
   using elem = typename FragT<BF16>::elem;
   const int ntiles = (a.S + 15) / 16;
   dim3 grid((ntiles + 3) / 4, 2);
-  size_t lds = (size_t)4 * 16 * a.L * sizeof(int2);
+  size_t lds = (BF16 && !INA_FWD_GATHER) ? 0 : (size_t)4 * 16 * a.L * sizeof(int2);   // fp32: token ids
   const bool store = a.hraw != nullptr && a.cst != nullptr;
   auto kern = a.drop ? (store ? lstm_fwd_kernel<U, NX, BF16, true, true> : lstm_fwd_kernel<U, NX, BF16, true, false>)
                      : (store ? lstm_fwd_kernel<U, NX, BF16, false, true> : lstm_fwd_kernel<U, NX, BF16, false, false>);
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, a.bias, (elem*)a.hraw,
-                     (typename CT<BF16>::type*)a.cst, (elem*)a.hdrop, a.dmask, a.seed, a.thr, a.inv_kp, a.drop, a.seed_dev);
+                     (typename CT<BF16>::type*)a.cst, (elem*)a.hdrop, a.dmask, a.seed, a.thr, a.inv_kp, a.drop, a.seed_dev,
+                     (const unsigned short*)a.xg);
   INA_CHECK_LAUNCH();
   return 0;
 }
@@ -906,7 +1102,7 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(kfn, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, (const frag*)a.a2pack, a.bias,
                      (const elem*)a.hraw, (const typename CT<BF16>::type*)a.cst, (const elem*)a.dH, a.dw_slab, a.dpos_slab, a.dwemb, a.dmask, a.seed, a.thr, a.inv_kp,
-                     a.drop, (unsigned short*)a.dxp);
+                     a.drop, (unsigned short*)a.dxp, (const unsigned short*)a.xg);
   INA_CHECK_LAUNCH();
   return 0;
 }
@@ -935,11 +1131,11 @@ int pos_grad(const LstmArgs& a, int blocks, float* slab, hipStream_t st) {
   dim3 grid(blocks), block(256);
   const auto* dxp = (const unsigned short*)a.dxp;
   if (P2 <= 48) {
-    hipLaunchKernelGGL(pos_grad_kernel<3>, grid, block, 0, st, dxp, a.S, a.L, a.PD, slab);
+    hipLaunchKernelGGL(pos_grad_kernel<3>, grid, block, 0, st, dxp, a.posb, a.S, a.L, a.PD, slab);
   } else if (P2 <= 80) {
-    hipLaunchKernelGGL(pos_grad_kernel<5>, grid, block, 0, st, dxp, a.S, a.L, a.PD, slab);
+    hipLaunchKernelGGL(pos_grad_kernel<5>, grid, block, 0, st, dxp, a.posb, a.S, a.L, a.PD, slab);
   } else if (P2 <= 128) {
-    hipLaunchKernelGGL(pos_grad_kernel<8>, grid, block, 0, st, dxp, a.S, a.L, a.PD, slab);
+    hipLaunchKernelGGL(pos_grad_kernel<8>, grid, block, 0, st, dxp, a.posb, a.S, a.L, a.PD, slab);
   } else {
     return -1;
   }
@@ -967,13 +1163,38 @@ int pos_grad_shift(const LstmArgs& a, float* gpart, float* out, hipStream_t st) 
   const auto* dxp = (const unsigned short*)a.dxp;
   dim3 grid((2 * NT + 3) / 4, nchunk), block(256);
   if (NRT <= 3)
-    hipLaunchKernelGGL(pos_shift_gemm_kernel<3>, grid, block, 0, st, dxp, a.S, a.L, a.PD, kps, gpart);
+    hipLaunchKernelGGL(pos_shift_gemm_kernel<3>, grid, block, 0, st, dxp, a.posb, a.S, a.L, a.PD, kps, gpart);
   else
-    hipLaunchKernelGGL(pos_shift_gemm_kernel<5>, grid, block, 0, st, dxp, a.S, a.L, a.PD, kps, gpart);
+    hipLaunchKernelGGL(pos_shift_gemm_kernel<5>, grid, block, 0, st, dxp, a.posb, a.S, a.L, a.PD, kps, gpart);
   INA_CHECK_LAUNCH();
   const int rows = (NRT <= 3 ? 3 : 5) * 16;
   hipLaunchKernelGGL(pos_shift_finish_kernel, dim3(2 * 2 * a.L * a.PD), dim3(256), 0, st, gpart, nchunk, a.L, a.PD,
                      rows, out);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int x_gather(const LstmArgs& a, int NX, hipStream_t st) {
+  const int ntiles = (a.S + 15) / 16;
+  if (ntiles <= 0 || INA_SKIP_XG) return 0;
+  auto* xg = (unsigned short*)a.xg;
+  auto* posb = const_cast<unsigned short*>(a.posb);
+  const dim3 grid(ntiles, (a.L + XG_T - 1) / XG_T);
+  const float* wsrc = a.wrows ? a.wrows : a.wemb;
+#define INA_XG_LAUNCH(NXV, DIR)                                                                          \
+  hipLaunchKernelGGL((x_gather_kernel<NXV, DIR>), grid, dim3(256), 0, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, \
+                     wsrc, a.E, a.p1emb, a.p2emb, a.PD, xg, posb)
+  if (NX == 4 && a.wrows)
+    INA_XG_LAUNCH(4, true);
+  else if (NX == 4)
+    INA_XG_LAUNCH(4, false);
+  else if (NX == 16 && a.wrows)
+    INA_XG_LAUNCH(16, true);
+  else if (NX == 16)
+    INA_XG_LAUNCH(16, false);
+  else
+    return -1;
+#undef INA_XG_LAUNCH
   INA_CHECK_LAUNCH();
   return 0;
 }

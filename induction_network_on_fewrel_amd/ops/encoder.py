@@ -31,6 +31,30 @@ def _route_grad(meta, name, g):
     return g.contiguous()
 
 
+_WROWS: dict = {}
+
+
+def word_rows(word: torch.Tensor, wemb: torch.Tensor, fresh: bool):
+    """Word-table rows per dataset token, [NI * L, E] fp32, for lstm_fwd's x gather (the kernel then
+    reads one contiguous run per sequence instead of a random row of the 400k-row table per token).
+    A frozen table (the reference default, model/base.py:55-59) is gathered once per (ids, table
+    version); ``fresh`` (trained word table, updated in place by the fused optimizer) gathers every
+    step.  None when the token count exceeds the kernel's 24-bit row indexing."""
+    if word.numel() >= (1 << 24):
+        return None
+    key = (word.data_ptr(), word.numel(), wemb.data_ptr(), wemb.shape[0], wemb._version)
+    if not fresh:
+        hit = _WROWS.get(key)
+        if hit is not None:
+            return hit
+    rows = wemb.detach().float().index_select(0, word.reshape(-1).long()).contiguous()
+    if not fresh:
+        if len(_WROWS) >= 4:
+            _WROWS.pop(next(iter(_WROWS)))
+        _WROWS[key] = rows
+    return rows
+
+
 class EncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, inst, word, pos1, pos2, mask, wemb, p1emb, p2emb, Kf, bf, Kb, bb, W1, b1, w2, meta):
@@ -47,15 +71,16 @@ class EncoderFn(torch.autograd.Function):
             bias = torch.stack([bf.detach(), bb.detach()]).float().contiguous()
         need_grad = ctx.needs_input_grad[5:15].count(True) > 0 if hasattr(ctx, "needs_input_grad") else True
         kp = float(meta["keep_prob"])
-        hlane, cst, hnat, dmask = o.lstm_fwd(inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
+        hlane, cst, hnat, dmask, xg = o.lstm_fwd(inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
                                       p2emb.detach().contiguous(), apack, bias, U, sh["NX"], bf16, bool(need_grad),
-                                      int(meta["seed"]), kp, meta.get("seed_dev"))
+                                      int(meta["seed"]), kp, meta.get("seed_dev"),
+                                      word_rows(word, wemb, bool(meta.get("word_grad", False))) if bf16 else None)
         w1pack, w1tpack = (pk["w1pack"], pk["w1tpack"]) if pk is not None else pack_attn(W1, bf16)
         e, alphas = o.attn_fwd(hnat, inst, mask, w1pack, b1.detach().contiguous(),
                                w2.detach().reshape(-1).contiguous(), U, bf16, int(meta.get("attn_blocks", 0)))
         if need_grad:
             ctx.save_for_backward(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst,
-                                  w1pack, w1tpack, b1, w2, alphas, hnat, dmask)
+                                  w1pack, w1tpack, b1, w2, alphas, hnat, dmask, xg)
             ctx.meta = dict(meta, NX=sh["NX"], DIN=DIN)
         ctx.mark_non_differentiable(alphas)
         ctx.set_materialize_grads(False)   # no zero-fill launch for the alphas gradient
@@ -65,7 +90,7 @@ class EncoderFn(torch.autograd.Function):
     def backward(ctx, de, _dalpha):
         o = ops()
         (inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst, w1pack, w1tpack, b1, w2,
-         alphas, hnat, dmask) = ctx.saved_tensors
+         alphas, hnat, dmask, xg) = ctx.saved_tensors
         m = ctx.meta
         U, bf16, DIN = m["U"], m["bf16"], m["DIN"]
         H2 = 2 * U
@@ -75,7 +100,7 @@ class EncoderFn(torch.autograd.Function):
         word_grad = bool(m.get("word_grad", False))
         dw_slab, dpos_slab, dwemb = o.lstm_bwd(inst, word, pos1, pos2, wemb.detach().contiguous(),
                                                p1emb.detach().contiguous(), p2emb.detach().contiguous(), apack, a2pack,
-                                               bias, hlane, cst, dH, dmask, U, m["NX"], bf16, word_grad,
+                                               bias, hlane, cst, dH, dmask, xg, U, m["NX"], bf16, word_grad,
                                                int(m.get("lstm_blocks", 0)), int(m["seed"]), float(m["keep_prob"]),
                                                bool(m.get("pos_shift", False)))
         glue = m.get("glue")

@@ -48,6 +48,7 @@ def main():
     b1 = torch.zeros(2 * U, device=dev)
     w2 = (torch.randn(2 * U, generator=g) * 0.2).to(dev)
     sh = lstm_shape(U, DIN, True)
+    wrows = None if os.environ.get("KB_NO_WROWS") else wemb.index_select(0, word.reshape(-1).long()).contiguous()
     apack, a2pack = pack_lstm(Kf, Kb, U, DIN, True)
     w1pack, w1tpack = pack_attn(W1, True)
     de = (torch.randn(S, 2 * U, generator=g) * 1e-3).to(dev)
@@ -68,17 +69,17 @@ def main():
         return ts[len(ts) // 2], out
 
     res = {"tag": args.tag, "S": S}
-    t, (hlane, cst, hnat, dmask) = timed(lambda: o.lstm_fwd(inst, word, pos1, pos2, wemb, p1, p2, apack, bias, U, sh["NX"],
-                                                       True, True, 7, 0.9, None))
+    t, (hlane, cst, hnat, dmask, xg) = timed(lambda: o.lstm_fwd(inst, word, pos1, pos2, wemb, p1, p2, apack, bias, U, sh["NX"],
+                                                       True, True, 7, 0.9, None, wrows))
     res["lstm_fwd"] = t
     t, _ = timed(lambda: o.lstm_fwd(inst, word, pos1, pos2, wemb, p1, p2, apack, bias, U, sh["NX"], True, False, 7,
-                                    1.0, None))
+                                    1.0, None, wrows))
     res["lstm_fwd_infer"] = t
     t, (e, alphas) = timed(lambda: o.attn_fwd(hnat, inst, mask, w1pack, b1, w2, U, True, 0))
     res["attn_fwd"] = t
     t, (dH, aslab) = timed(lambda: o.attn_bwd(hnat, inst, w1pack, w1tpack, b1, w2, de, alphas, U, True, 0))
     res["attn_bwd"] = t
-    t, _ = timed(lambda: o.lstm_bwd(inst, word, pos1, pos2, wemb, p1, p2, apack, a2pack, bias, hlane, cst, dH, dmask, U,
+    t, _ = timed(lambda: o.lstm_bwd(inst, word, pos1, pos2, wemb, p1, p2, apack, a2pack, bias, hlane, cst, dH, dmask, xg, U,
                                     sh["NX"], True, False, 0, 7, 0.9, False))
     res["lstm_bwd"] = t
     res["encoder_total"] = res["lstm_fwd"] + res["attn_fwd"] + res["attn_bwd"] + res["lstm_bwd"]
