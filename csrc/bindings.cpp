@@ -82,13 +82,14 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, 
   const bool drop = keep_prob < 1.0;
   auto hopt = word.options().dtype(bf16 ? at::kBFloat16 : at::kFloat);
   const int64_t ntiles = (S + 15) / 16;
-  auto hlane = store_c ? at::empty({ntiles, 2, L, U4, 64}, hopt) : at::empty({0}, hopt);
+  // bf16: hlane holds h (bf16) | c (fp16) << 16 packed per dword and cst is empty
+  auto hlane = store_c ? at::empty({ntiles, 2, L, U4, 64}, bf16 ? word.options() : hopt) : at::empty({0}, hopt);
   // hnat is allocated with 16 * ntiles rows so the kernel stores padding rows unconditionally
   // (no lane-divergent store branch); callers see the first S rows.
   auto hnat_full = at::empty({ntiles * 16, L, 2 * U}, hopt);
   auto hnat = hnat_full.narrow(0, 0, S);
   auto copt = wemb.options().dtype(bf16 ? at::kHalf : at::kFloat);   // fp16 cell states in bf16 mode
-  Tensor cst = store_c ? at::empty({ntiles, 2, L, U4, 64}, copt) : at::empty({0}, copt);
+  Tensor cst = (store_c && !bf16) ? at::empty({ntiles, 2, L, U4, 64}, copt) : at::empty({0}, copt);
   TORCH_CHECK(ntiles * 16 * L * 2 * U < (1LL << 31) && ntiles * 2 * L * U4 * 64 < (1LL << 32),
               "ina.lstm_fwd: batch too large for 32-bit offsets (split the episode batch)");
   TORCH_CHECK(wemb.size(0) < (1 << 24) && 2 * L < (1 << 16), "ina.lstm_fwd: table rows exceed 24-bit indexing");
@@ -114,8 +115,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, 
   a.apack = apack.data_ptr();
   a.bias = bias.data_ptr<float>();
   a.hraw = store_c ? hlane.data_ptr() : nullptr;
-  a.cst = store_c ? cst.data_ptr() : nullptr;
-  a.hdrop = hnat.data_ptr();
+  a.cst = store_c ? (bf16 ? hlane.data_ptr() : cst.data_ptr()) : nullptr;   // bf16: unused (packed in hlane)
+  // bf16: the kernel writes the dropped h in its lane layout; h_natural transposes it into hnat
+  Tensor hl = bf16 ? at::empty({ntiles, 2, L, U4, 64}, hopt) : at::empty({0}, hopt);
+  a.hdrop = bf16 ? hl.data_ptr() : hnat.data_ptr();
   a.dmask = (store_c && drop) ? dmask.data_ptr<uint8_t>() : nullptr;
   a.seed_dev = dev_int(seed_dev, "seed_dev");
   a.seed = (uint32_t)seed;
@@ -132,6 +135,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, 
     check_launch(ina::x_gather(a, (int)NX, cur_stream()), "x_gather");
   }
   check_launch(ina::lstm_fwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_fwd");
+  if (bf16)
+    check_launch(ina::h_natural(hl.data_ptr(), (int)S, (int)L, (int)U, hnat_full.data_ptr(), cur_stream()), "h_natural");
   return {hlane, cst, hnat, dmask, xg};
 }
 
@@ -150,18 +155,18 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   check(p1emb, "p1emb", at::kFloat);
   check(p2emb, "p2emb", at::kFloat);
   check(bias, "bias", at::kFloat);
-  check(cst, "cst", bf16 ? at::kHalf : at::kFloat);
+  if (!bf16) check(cst, "cst", at::kFloat);   // bf16: the cell states are packed into hlane
   check(dH, "dH", bf16 ? at::kBFloat16 : at::kFloat);
   check(apack, "apack", bf16 ? at::kBFloat16 : at::kFloat);
   check(a2pack, "a2pack", bf16 ? at::kBFloat16 : at::kFloat);
-  check(hraw, "hraw", bf16 ? at::kBFloat16 : at::kFloat);
+  check(hraw, "hraw", bf16 ? at::kInt : at::kFloat);   // bf16: packed h | c << 16 (lstm_fwd)
   TORCH_CHECK(ina::lstm_supported((int)U, (int)NX), "ina.lstm_bwd: unsupported (U, NX)");
   const int64_t S = inst.size(0), L = word.size(1), E = wemb.size(1), PD = p1emb.size(1);
   const int64_t DIN = E + 2 * PD, NF = DIN + U + 1, U4 = U / 4, KPL = frag_elems(bf16);
   TORCH_CHECK(DIN <= 4 * NX, "ina.lstm_bwd: input dim too large");
   TORCH_CHECK(hraw.numel() == ((S + 15) / 16) * 2 * L * U4 * 64, "ina.lstm_bwd: hlane shape");
   TORCH_CHECK(dH.size(0) == S && dH.size(1) == L && dH.size(2) == 2 * U, "ina.lstm_bwd: dH shape");
-  TORCH_CHECK(cst.numel() == ((S + 15) / 16) * 2 * L * U4 * 64, "ina.lstm_bwd: cst shape");
+  TORCH_CHECK(bf16 || cst.numel() == ((S + 15) / 16) * 2 * L * U4 * 64, "ina.lstm_bwd: cst shape");
   const bool drop_ = keep_prob < 1.0;
   if (drop_) {
     check(dmask, "dmask", at::kByte);
@@ -212,7 +217,7 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   a.a2pack = a2pack.data_ptr();
   a.bias = bias.data_ptr<float>();
   a.hraw = hraw.data_ptr();
-  a.cst = cst.data_ptr();
+  a.cst = bf16 ? hraw.data_ptr() : cst.data_ptr();
   a.dH = dH.data_ptr();
   a.dw_slab = dw_slab.data_ptr<float>();
   a.dpos_slab = dpos_slab.data_ptr<float>();

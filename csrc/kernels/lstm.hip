@@ -28,21 +28,6 @@ using namespace ina;
 #ifndef XG_RING
 #define XG_RING 4
 #endif
-// timing experiments (wrong values): INA_EXP_ACT=1 VALU-only activations, INA_EXP_NOX=1 no x gathers,
-// INA_FWD_GATHER=1 bf16 forward gathers x per step itself, INA_SKIP_XG=1 no x_gather launch
-#ifndef INA_FWD_GATHER
-#define INA_FWD_GATHER 0
-#endif
-#ifndef INA_SKIP_XG
-#define INA_SKIP_XG 0
-#endif
-#ifndef INA_EXP_ACT
-#define INA_EXP_ACT 0
-#endif
-#ifndef INA_EXP_NOX
-#define INA_EXP_NOX 0
-#endif
-
 namespace {
 
 template <int U, int NX, bool BF16>
@@ -266,7 +251,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   const int ntiles = (S + 15) / 16;
   const int tile = blockIdx.x * 4 + wave;
   int2* ids = ids_all + wave * 16 * L;
-  constexpr bool FG = !BF16 || INA_FWD_GATHER;   // gather x per step (fp32 mode)
+  constexpr bool FG = !BF16;   // fp32 mode gathers x per step
   if constexpr (FG) {
     // fp32 mode gathers x per step: stage (word, pos1 | pos2 << 16) of the wave's 16 sequences into LDS
     for (int i = lane; i < 16 * L; i += 64) {
@@ -321,7 +306,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
       const int2 id = ids[n * L + t];
       const XRow r = xrow(id.x, id.y & 0xffff, id.y >> 16, E, PD);
 #pragma unroll
-      for (int xi = 0; xi < NX; ++xi) xv[xi] = INA_EXP_NOX ? __int_as_float(r.w) : gather_x(xs[xi], r);
+      for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(xs[xi], r);
     }
   };
   // one recurrence step at processing index tau with input features xv
@@ -345,23 +330,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
       f32x4_t acc = {bm[m][0], bm[m][1], bm[m][2], bm[m][3]};
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) acc = mma(A[m][ks], B[ks], acc);
-#if INA_EXP_ACT
-      const float ig = fmaf(acc[0], 0.1f, 0.5f), jg = fmaf(acc[1], 0.1f, 0.f), fg = fmaf(acc[2], 0.1f, 0.5f),
-                  og = fmaf(acc[3], 0.1f, 0.5f);
-      c[m] = c[m] * fg + ig * jg;
-      float hv = fmaf(c[m], 0.1f, 0.f) * og;
-#else
       const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
       c[m] = c[m] * fg + ig * jg;
       float hv = tanh_l2(c[m] * (2.f * LOG2E_F)) * og;
-#endif
       if (BF16) hv = round_bf(hv);  // the stored / recurrent operand value
       h[m] = hv;
     }
     {
-      // natural-layout copy for the attention layer; dropout (DropoutWrapper output) applied here.
+      // the attention layer's input, dropout (DropoutWrapper output) applied here.  bf16: lane layout
+      // [tile][dir][t][U4][64] (one coalesced 128-B store per unit slot; h_natural_kernel transposes
+      // it) -- the natural [seq][t][2U] rows took 16 scattered 8-byte pieces per store instruction
+      // and cost ~300 of this kernel's ~700 us (kbench A/B).  fp32: natural layout directly.
       // 32-bit offsets (S * L * 2U < 2^31 checked on the host); padding rows are stored too.
-      typename FragT<BF16>::elem* hn = hnat + (((uint32_t)seq * L + t) * (2 * U) + dir * U + q);
+      constexpr int HS = BF16 ? 64 : 4;   // element stride between the lane's unit slots
+      typename FragT<BF16>::elem* hn =
+          BF16 ? hnat + ((uint32_t)((tile * 2 + dir) * L + t) * U4) * 64 + lane
+               : hnat + (((uint32_t)seq * L + t) * (2 * U) + dir * U + q);
       if constexpr (DROP) {
         const uint32_t base = ((uint32_t)seq * L + t) * U + q;
         uint32_t bits = 0;
@@ -369,22 +353,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
         for (int m = 0; m < U4; ++m) {
           const bool keep = dropout_keep_salted(salt, base + 4 * m, thr);
           bits |= keep ? (1u << m) : 0u;
-          hn[4 * m] = to_elem(keep ? h[m] * inv_kp : 0.f, (typename FragT<BF16>::elem*)nullptr);
+          hn[HS * m] = to_elem(keep ? h[m] * inv_kp : 0.f, (typename FragT<BF16>::elem*)nullptr);
         }
         if constexpr (STORE) {   // the backward re-applies the mask from these bits (no re-hashing)
           if constexpr (U4 <= 8) dmask[(uint32_t)((tile * 2 + dir) * L + t) * 64 + lane] = (unsigned char)bits;
         }
       } else {
 #pragma unroll
-        for (int m = 0; m < U4; ++m) hn[4 * m] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
+        for (int m = 0; m < U4; ++m) hn[HS * m] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
       }
     }
-    if constexpr (STORE) {  // raw recurrent h for the backward, lane-native (coalesced 128-B rows)
+    if constexpr (STORE && BF16) {
+      // raw recurrent h (bf16) | cell state (fp16) << 16 for the backward, lane-native: ONE coalesced
+      // 256-B dword store per unit slot (stores are issue-bound here, not bandwidth-bound)
+      uint32_t* hp = reinterpret_cast<uint32_t*>(hlane) + ((uint32_t)((tile * 2 + dir) * L + t) * U4) * 64 + lane;
+#pragma unroll
+      for (int m = 0; m < U4; ++m)
+        hp[m * 64] = (uint32_t)f2bf(h[m]) | ((uint32_t)__builtin_bit_cast(unsigned short, (_Float16)c[m]) << 16);
+    } else if constexpr (STORE) {
+      // fp32 mode: raw h and c, lane-native (coalesced rows)
       typename FragT<BF16>::elem* hp = hlane + ((uint32_t)((tile * 2 + dir) * L + t) * U4) * 64 + lane;
 #pragma unroll
       for (int m = 0; m < U4; ++m) hp[m * 64] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
-    }
-    if constexpr (STORE) {
       celem* cp = cst + ((uint32_t)((tile * 2 + dir) * L + t) * U4) * 64 + lane;
 #pragma unroll
       for (int m = 0; m < U4; ++m) cp[m * 64] = (celem)c[m];
@@ -401,11 +391,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     // compiler's waitcnt pass merges the loop-header state conservatively and waited vmcnt(3) at the
     // top of every body, i.e. for all of the previous steps' ~16 stores (store latency on the
     // recurrence).  The count is exact because the step's VMEM stream is fixed at compile time:
-    // NST stores per step (hnat U4, hlane U4, cst U4, dmask 1; no compiler-visible loads in the loop).
+    // NST stores per step (hnat U4, packed h|c U4, dmask 1; no compiler-visible loads in the loop).
     // Order of VMEM ops: ld(0..R-2), then per step j: ld(j + R - 1), NST stores of step j; before
     // step j's math the ops issued after ld(j) number R - 1 + min(j, R - 1) * NST.
     constexpr int R = XG_RING;
-    constexpr int NST = U4 + (STORE ? 2 * U4 : 0) + ((DROP && STORE && U4 <= 8) ? 1 : 0);
+    constexpr int NST = U4 + (STORE ? U4 : 0) + ((DROP && STORE && U4 <= 8) ? 1 : 0);
     auto ld = [&](int tau, uint64_t& d) __attribute__((always_inline)) {
       const unsigned short* xp = xg + ((uint32_t)(tile * L + tof(min(tau, L - 1))) * 64 + lane) * NX;
       asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(d) : "v"(xp) : "memory");
@@ -482,6 +472,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   for (; tau + 1 < L; tau += 2) pair(tau);
   if (tau < L) step(tau, xa);
 #endif
+}
+
+// ------------------------------------------------------------------------------------------
+// bf16 forward output, lane layout [tile][dir][t][U4][64] -> natural rows [seq][t][2U] (the
+// attention input, model/graph.py:49 concat of the two directions).  One workgroup per 16-sequence
+// tile: the tile's contiguous input block lands in LDS by LDS-DMA; each sequence's output rows are
+// one contiguous run written with coalesced dwords (16 threads per sequence).
+// ------------------------------------------------------------------------------------------
+template <int U>
+__global__ __launch_bounds__(256) void h_natural_kernel(const unsigned short* __restrict__ hl, int L,
+                                                        unsigned short* __restrict__ hnat) {
+  constexpr int U4 = U / 4;
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds_h[];   // the tile's input block
+  const int tile = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // 1) the tile's contiguous input block [2][L][U4][64] -> LDS: 1-KB LDS-DMA pieces, all in flight
+  const int bytes = 2 * L * U4 * 64 * 2;
+  const char* src = reinterpret_cast<const char*>(hl) + (size_t)tile * bytes;
+  for (int k = wave; k * 1024 < bytes; k += 4) {
+    const int off = k * 1024 + lane * 16;
+    if (off < bytes)
+      __builtin_amdgcn_global_load_lds(src + off, reinterpret_cast<char*>(lds_h) + k * 1024, 16, 0, 0);
+  }
+  __syncthreads();
+  // 2) natural rows: thread (sequence n = tid / 16, part) writes dwords part, part + 16, ... of n's
+  //    contiguous run [L][2U] (dword = features (2p, 2p + 1) of one step)
+  const int n = threadIdx.x >> 4, part = threadIdx.x & 15;
+  uint32_t* dst = reinterpret_cast<uint32_t*>(hnat + ((size_t)tile * 16 + n) * L * 2 * U);
+  for (int i = part; i < L * U; i += 16) {
+    const int t = i / U, f = 2 * (i - t * U);
+    uint32_t v = 0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int fe = f + e, d = fe >= U ? 1 : 0, u = fe - d * U;
+      const uint32_t x = lds_h[((d * L + t) * U4 + (u >> 2)) * 64 + (u & 3) * 16 + n];
+      v |= x << (16 * e);
+    }
+    dst[i] = v;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -585,6 +614,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     const long rowbase = (long)inst[seqc] * L;
     const typename CT<BF16>::type* cbase = cst + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
     const elem* hbase = hraw + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
+    // bf16: packed h | c << 16 (one dword load per unit slot and step)
+    const uint32_t* pbase = reinterpret_cast<const uint32_t*>(hraw) + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
+    auto ld_hc = [&](int tt, int m, float& hv, float& cv) {
+      if constexpr (BF16) {
+        const uint32_t v = pbase[((size_t)tt * U4 + m) * 64];
+        hv = bf2f((unsigned short)(v & 0xFFFFu));
+        cv = (float)__builtin_bit_cast(_Float16, (unsigned short)(v >> 16));
+      } else {
+        hv = from_elem(hbase[((size_t)tt * U4 + m) * 64]);
+        cv = from_c(cbase[((size_t)tt * U4 + m) * 64]);
+      }
+    };
     auto tof = [&](int tau) { return dir ? (L - 1 - tau) : tau; };  // processing step -> time
     // bf16: x from the x_gather_kernel rows (one coalesced load per 4 features), no token ids
     auto load_xg = [&](int t, float* xv) {
@@ -616,10 +657,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       }
 #pragma unroll
       for (int m = 0; m < U4; ++m) {
-        ccur[m] = from_c(cbase[((size_t)t * U4 + m) * 64]);
-        const float cp = from_c(cbase[((size_t)tp * U4 + m) * 64]);
+        float hdummy, cp, hv;
+        ld_hc(t, m, hdummy, ccur[m]);
+        ld_hc(tp, m, hv, cp);
         cprev[m] = L >= 2 ? cp : 0.f;
-        const float hv = from_elem(hbase[((size_t)tp * U4 + m) * 64]);
         hp[m] = (L >= 2 && valid) ? hv : 0.f;
 #if INA_DH_LANE
         const float dv = from_elem(dH[(((size_t)tile * 2 + dir) * L + t) * U4 * 64 + m * 64 + lane]);
@@ -664,9 +705,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       }
 #pragma unroll
       for (int m = 0; m < U4; ++m) {
-        const float cp = from_c(cbase[((size_t)tnp * U4 + m) * 64]);
+        float hv, cp;
+        ld_hc(tnp, m, hv, cp);
         cprev_n[m] = n_has_prev ? cp : 0.f;
-        const float hv = from_elem(hbase[((size_t)tnp * U4 + m) * 64]);
         hp_n[m] = (n_has_prev && valid) ? hv : 0.f;
 #if INA_DH_LANE
         const float dv = from_elem(dH[(((size_t)tile * 2 + dir) * L + tn) * U4 * 64 + m * 64 + lane]);
@@ -1075,7 +1116,7 @@ static int launch_fwd_t(const LstmArgs& a, hipStream_t st) {
   using elem = typename FragT<BF16>::elem;
   const int ntiles = (a.S + 15) / 16;
   dim3 grid((ntiles + 3) / 4, 2);
-  size_t lds = (BF16 && !INA_FWD_GATHER) ? 0 : (size_t)4 * 16 * a.L * sizeof(int2);   // fp32: token ids
+  size_t lds = BF16 ? 0 : (size_t)4 * 16 * a.L * sizeof(int2);   // fp32: token ids
   const bool store = a.hraw != nullptr && a.cst != nullptr;
   auto kern = a.drop ? (store ? lstm_fwd_kernel<U, NX, BF16, true, true> : lstm_fwd_kernel<U, NX, BF16, true, false>)
                      : (store ? lstm_fwd_kernel<U, NX, BF16, false, true> : lstm_fwd_kernel<U, NX, BF16, false, false>);
@@ -1174,9 +1215,31 @@ int pos_grad_shift(const LstmArgs& a, float* gpart, float* out, hipStream_t st) 
   return 0;
 }
 
+int h_natural(const void* hl, int S, int L, int U, void* hnat, hipStream_t st) {
+  const int ntiles = (S + 15) / 16;
+  if (ntiles <= 0) return 0;
+  const size_t lds = ((size_t)2 * L * (U / 4) * 64 * sizeof(unsigned short) + 1023) & ~(size_t)1023;
+  if (lds > 160 * 1024) return -1;
+  const auto* in = (const unsigned short*)hl;
+  auto* out = (unsigned short*)hnat;
+#define INA_HN(UV)                                                                                     \
+  if (U == UV) {                                                                                       \
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)h_natural_kernel<UV>,                        \
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+    hipLaunchKernelGGL(h_natural_kernel<UV>, dim3(ntiles), dim3(256), lds, st, in, L, out);           \
+    INA_CHECK_LAUNCH();                                                                                \
+    return 0;                                                                                          \
+  }
+  INA_HN(20)
+  INA_HN(32)
+  INA_HN(8)
+#undef INA_HN
+  return -1;
+}
+
 int x_gather(const LstmArgs& a, int NX, hipStream_t st) {
   const int ntiles = (a.S + 15) / 16;
-  if (ntiles <= 0 || INA_SKIP_XG) return 0;
+  if (ntiles <= 0) return 0;
   auto* xg = (unsigned short*)a.xg;
   auto* posb = const_cast<unsigned short*>(a.posb);
   const dim3 grid(ntiles, (a.L + XG_T - 1) / XG_T);

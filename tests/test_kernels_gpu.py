@@ -45,6 +45,17 @@ def _gathered(dd, inst):
     return [t[inst.long()] for t in dd.arrays()]
 
 
+def _split_stash(hlane, cst):
+    """lstm_fwd's backward stash as float lane-layout (h, c): bf16 mode packs h (bf16) | c (fp16) << 16
+    into one int32 per slot (cst is empty); fp32 mode returns separate arrays."""
+    if hlane.dtype == torch.int32:
+        halves = hlane.view(torch.int16).view(*hlane.shape, 2)
+        h = halves[..., 0].contiguous().view(torch.bfloat16).float()
+        c = halves[..., 1].contiguous().view(torch.float16).float()
+        return h, c
+    return hlane.float(), (cst.float() if cst is not None else None)
+
+
 def _unpack_cst(cst, S, L, U):
     ntiles = cst.shape[0]
     U4 = U // 4
@@ -85,9 +96,10 @@ def test_lstm_forward(dtype):
     S, L = inst.shape[0], word.shape[1]
     ef = _relerr(hraw[..., :U].float(), hf)
     eb = _relerr(hraw[..., U:].float(), hb)
-    c = _unpack_cst(cst, S, L, U)
+    hs, cs = _split_stash(hlane, cst)
+    c = _unpack_cst(cs, S, L, U)
     ec = _relerr(c, torch.cat([cf, cb], -1))
-    hl = _unpack_cst(hlane.float(), S, L, U)
+    hl = _unpack_cst(hs, S, L, U)
     eh = _relerr(hl, hraw.float())
     print(f"lstm fwd {dtype}: h_fw {ef:.2e} h_bw {eb:.2e} c {ec:.2e} hlane {eh:.2e}")
     assert ef < tol and eb < tol and ec < tol and eh == 0.0
@@ -110,7 +122,7 @@ def test_attention_forward(dtype, keep_prob):
     hlane, _, hdrop, _, _ = ops().lstm_fwd(inst, word, pos1, pos2, p["word_embedding"].detach(),
                                      p["pos1_embedding"].detach(), p["pos2_embedding"].detach(), apack, bias, U,
                                      lstm_shape(U, DIN, bf16)["NX"], bf16, True, seed, keep_prob, None, None)
-    hraw = _unpack_cst(hlane.float(), inst.shape[0], word.shape[1], U)
+    hraw = _unpack_cst(_split_stash(hlane, None)[0], inst.shape[0], word.shape[1], U)
     w1p, _ = pack_attn(p["attn_kernel"], bf16)
     e, alphas = ops().attn_fwd(hdrop, inst, mask, w1p, p["attn_bias"].detach().contiguous(),
                                p["attn_w2"].detach().reshape(-1).contiguous(), U, bf16, 0)
