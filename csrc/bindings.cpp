@@ -125,10 +125,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, 
   a.thr = keep_threshold(keep_prob);
   a.inv_kp = (float)(1.0 / keep_prob);
   a.drop = drop ? 1 : 0;
-  a.wrows = dev_float(wrows, "wrows");
-  if (a.wrows)
-    TORCH_CHECK(wrows->numel() == word.numel() * E && word.numel() < (1 << 24),
-                "ina.lstm_fwd: wrows must be [NI * L, E] with NI * L < 2^24");
+  a.wrows = nullptr;
+  if (wrows.has_value() && wrows->defined() && wrows->numel() > 0) {
+    check(*wrows, "wrows", at::kBFloat16);
+    TORCH_CHECK(wrows->numel() == word.numel() * 8 && E <= 8, "ina.lstm_fwd: wrows must be bf16 [NI * L, 8] (E <= 8)");
+    a.wrows = wrows->data_ptr();
+  }
   if (bf16) {
     a.xg = xg.data_ptr();
     a.posb = reinterpret_cast<const unsigned short*>(xg.data_ptr<at::BFloat16>() + ntiles * L * 64 * NX);

@@ -35,7 +35,7 @@ struct LstmArgs {
   void* dxp;             // bf16 bwd: pos-feature gradients [2 dir][tiles][L][2PD][16] (reduced by pos_grad)
   void* xg;              // bf16: x_gather output [tiles][L][64 lanes][NX] (input of lstm_fwd / lstm_bwd)
   const unsigned short* posb;   // bf16: x_gather position ids [tiles][L][16] = pos1 | pos2 << 8
-  const float* wrows;    // optional [NI * L][E]: word rows per token (x_gather reads them directly)
+  const void* wrows;     // optional bf16 [NI * L][8]: word rows per token, zero padded (x_gather DIRECT)
   uint32_t seed, thr;
   float inv_kp;
   int drop;

@@ -188,11 +188,18 @@ template <int NX, bool DIRECT>
 __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ inst, int S,
                                                       const int* __restrict__ word, const int* __restrict__ pos1,
                                                       const int* __restrict__ pos2, int L,
-                                                      const float* __restrict__ wemb, int E,
+                                                      const float* __restrict__ wemb,
+                                                      const unsigned short* __restrict__ wrows, int E,
                                                       const float* __restrict__ p1emb,
                                                       const float* __restrict__ p2emb, int PD,
                                                       unsigned short* __restrict__ xg,
                                                       unsigned short* __restrict__ posb) {
+  // the two position tables ([2L, PD] each, tiny) in LDS: per-feature loads from them were most of
+  // this kernel's vector-memory instructions
+  __shared__ float ptab[2 * 128 * 8];
+  const int PT = 2 * L * PD;
+  for (int i = threadIdx.x; i < 2 * PT; i += 256) ptab[i] = i < PT ? p1emb[i] : p2emb[i - PT];
+  __syncthreads();
   // thread = one token (sequence n = tid & 15, step t0 + tid / 16): its id / row loads are runs along
   // t (coalesced), and it writes its NX x 4 features as 4 lane-group chunks; for a fixed step the
   // 16 sequences' chunks of one lane group are one contiguous 16 x 8-byte segment.
@@ -202,14 +209,20 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
   const bool valid = seq < S;
   const long r = (long)inst[valid ? seq : S - 1] * L + min(t, L - 1);   // clamped: unconditional loads
   const int p1 = pos1[r], p2 = pos2[r];
-  const float* wrow = DIRECT ? wemb + r * E : wemb + (long)word[r] * E;
-  const float* p1row = p1emb + p1 * PD;
-  const float* p2row = p2emb + p2 * PD;
+  const float* p1row = ptab + p1 * PD;
+  const float* p2row = ptab + PT + p2 * PD;
   const int DIN = E + 2 * PD;
+  // DIRECT: the token's word row as one 16-byte load of 8 bf16 (E <= 8, zero padded)
+  u16x8_t wr = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  if constexpr (DIRECT) wr = *reinterpret_cast<const u16x8_t*>(wrows + r * 8);
+  const float* wrow = wemb + (DIRECT ? 0 : (long)word[r] * E);
   float x[4 * NX];
 #pragma unroll
-  for (int f = 0; f < 4 * NX; ++f)   // E, PD are kernel arguments: the source branches are uniform
-    x[f] = f < E ? wrow[f] : (f < E + PD ? p1row[f - E] : (f < DIN ? p2row[f - E - PD] : 0.f));
+  for (int f = 0; f < 4 * NX; ++f) {   // E, PD are kernel arguments: the source branches are uniform
+    float wv = 0.f;
+    if (f < E) wv = DIRECT ? bf2f(wr[f < 8 ? f : 0]) : wrow[f];
+    x[f] = f < E ? wv : (f < E + PD ? p1row[f - E] : (f < DIN ? p2row[f - E - PD] : 0.f));
+  }
   if (t >= L) return;
   unsigned short* dst = xg + (size_t)(tile * L + t) * 64 * NX;
 #pragma unroll
@@ -1243,10 +1256,11 @@ int x_gather(const LstmArgs& a, int NX, hipStream_t st) {
   auto* xg = (unsigned short*)a.xg;
   auto* posb = const_cast<unsigned short*>(a.posb);
   const dim3 grid(ntiles, (a.L + XG_T - 1) / XG_T);
-  const float* wsrc = a.wrows ? a.wrows : a.wemb;
+  if (2 * a.L * a.PD > 128 * 8) return -1;   // pos tables staged in LDS
+  const auto* wr16 = (const unsigned short*)a.wrows;
 #define INA_XG_LAUNCH(NXV, DIR)                                                                          \
   hipLaunchKernelGGL((x_gather_kernel<NXV, DIR>), grid, dim3(256), 0, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, \
-                     wsrc, a.E, a.p1emb, a.p2emb, a.PD, xg, posb)
+                     a.wemb, wr16, a.E, a.p1emb, a.p2emb, a.PD, xg, posb)
   if (NX == 4 && a.wrows)
     INA_XG_LAUNCH(4, true);
   else if (NX == 4)

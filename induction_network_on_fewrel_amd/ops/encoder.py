@@ -35,19 +35,22 @@ _WROWS: dict = {}
 
 
 def word_rows(word: torch.Tensor, wemb: torch.Tensor, fresh: bool):
-    """Word-table rows per dataset token, [NI * L, E] fp32, for lstm_fwd's x gather (the kernel then
-    reads one contiguous run per sequence instead of a random row of the 400k-row table per token).
+    """Word-table rows per dataset token, bf16 [NI * L, 8] (zero padded; the gate MFMAs take x in bf16
+    anyway), for lstm_fwd's x gather: one 16-byte load per token from a per-instance contiguous run
+    instead of a random row of the 400k-row table.
     A frozen table (the reference default, model/base.py:55-59) is gathered once per (ids, table
     version); ``fresh`` (trained word table, updated in place by the fused optimizer) gathers every
-    step.  None when the token count exceeds the kernel's 24-bit row indexing."""
-    if word.numel() >= (1 << 24):
+    step.  None for word vectors wider than 8 (the kernel then gathers from the table itself)."""
+    if wemb.shape[1] > 8:
         return None
     key = (word.data_ptr(), word.numel(), wemb.data_ptr(), wemb.shape[0], wemb._version)
     if not fresh:
         hit = _WROWS.get(key)
         if hit is not None:
             return hit
-    rows = wemb.detach().float().index_select(0, word.reshape(-1).long()).contiguous()
+    E = wemb.shape[1]
+    rows = torch.nn.functional.pad(wemb.detach().float().index_select(0, word.reshape(-1).long()), (0, 8 - E))
+    rows = rows.to(torch.bfloat16).contiguous()
     if not fresh:
         if len(_WROWS) >= 4:
             _WROWS.pop(next(iter(_WROWS)))

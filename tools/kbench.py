@@ -48,7 +48,8 @@ def main():
     b1 = torch.zeros(2 * U, device=dev)
     w2 = (torch.randn(2 * U, generator=g) * 0.2).to(dev)
     sh = lstm_shape(U, DIN, True)
-    wrows = None if os.environ.get("KB_NO_WROWS") else wemb.index_select(0, word.reshape(-1).long()).contiguous()
+    from induction_network_on_fewrel_amd.ops.encoder import word_rows
+    wrows = None if os.environ.get("KB_NO_WROWS") else word_rows(word, wemb, True)
     apack, a2pack = pack_lstm(Kf, Kb, U, DIN, True)
     w1pack, w1tpack = pack_attn(W1, True)
     de = (torch.randn(S, 2 * U, generator=g) * 1e-3).to(dev)
