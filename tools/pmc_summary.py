@@ -19,7 +19,7 @@ def load(root):
 def main(root):
     vals, cnt = load(root)
     print(f"{'kernel':48s} {'VALU/wave':>9s} {'MFMA/w':>7s} {'LDS/w':>6s} {'VMRD/w':>7s} {'VMWR/w':>7s} "
-          f"{'wait%':>6s} {'waitI%':>6s} {'valu%':>6s} {'mfma%':>6s} {'ldsconf%':>8s}")
+          f"{'wait%':>6s} {'waitI%':>6s} {'valu%':>6s} {'mfma%':>6s} {'ldsconf%':>8s} {'rdMB':>7s} {'wrMB':>7s}")
     for k, v in sorted(vals.items()):
         wc = v.get("SQ_WAVE_CYCLES", 0) or 1
         waves = v.get("SQ_WAVES", 0)
@@ -34,8 +34,11 @@ def main(root):
         mfma = 100 * v.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (gui * 4 * 256 / max(1, cnt[k].get("GRBM_GUI_ACTIVE", 1)) * 1)
         lds = v.get("SQ_LDS_IDX_ACTIVE", 0) or 1
         ldsc = 100 * v.get("SQ_LDS_BANK_CONFLICT", 0) / lds
+        # HBM traffic per dispatch (FETCH_SIZE / WRITE_SIZE are KB summed over the dispatch's rows)
+        rd = v.get("FETCH_SIZE", 0) / max(1, cnt[k].get("FETCH_SIZE", 1)) / 1024
+        wr = v.get("WRITE_SIZE", 0) / max(1, cnt[k].get("WRITE_SIZE", 1)) / 1024
         print(f"{k:48s} {row[0]:9.3g} {row[1]:7.3g} {row[2]:6.3g} {row[3]:7.3g} {row[4]:7.3g} {wait:6.1f} {waiti:6.1f} "
-              f"{valu:6.1f} {mfma:6.1f} {ldsc:8.1f}")
+              f"{valu:6.1f} {mfma:6.1f} {ldsc:8.1f} {rd:7.1f} {wr:7.1f}")
     print("\nraw sums per kernel:")
     for k, v in sorted(vals.items()):
         print(k, {c: f"{x:.4g}" for c, x in sorted(v.items())})
