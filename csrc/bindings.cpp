@@ -82,8 +82,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, 
   const bool drop = keep_prob < 1.0;
   auto hopt = word.options().dtype(bf16 ? at::kBFloat16 : at::kFloat);
   const int64_t ntiles = (S + 15) / 16;
-  // bf16: hlane holds h (bf16) | c (fp16) << 16 packed per dword and cst is empty
-  auto hlane = store_c ? at::empty({ntiles, 2, L, U4, 64}, bf16 ? word.options() : hopt) : at::empty({0}, hopt);
+  // bf16: hlane = the step records [tiles][2][L][2][U4][64] (h slot bf16, c slot fp16 bits; always
+  // written -- the h slot is also the attention input) and cst is empty.  fp32: h / c stash (store_c)
+  auto hlane = bf16 ? at::empty({ntiles, 2, L, 2, U4, 64}, hopt)
+                    : (store_c ? at::empty({ntiles, 2, L, U4, 64}, hopt) : at::empty({0}, hopt));
   // hnat is allocated with 16 * ntiles rows so the kernel stores padding rows unconditionally
   // (no lane-divergent store branch); callers see the first S rows.
   auto hnat_full = at::empty({ntiles * 16, L, 2 * U}, hopt);
@@ -93,9 +95,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, 
   TORCH_CHECK(ntiles * 16 * L * 2 * U < (1LL << 31) && ntiles * 2 * L * U4 * 64 < (1LL << 32),
               "ina.lstm_fwd: batch too large for 32-bit offsets (split the episode batch)");
   TORCH_CHECK(wemb.size(0) < (1 << 24) && 2 * L < (1 << 16), "ina.lstm_fwd: table rows exceed 24-bit indexing");
-  // dropout keep bits for the backward (one byte per lane-step), only when both are needed
-  Tensor dmask = (store_c && drop) ? at::empty({ntiles, 2, L, 64}, word.options().dtype(at::kByte))
-                                   : at::empty({0}, word.options().dtype(at::kByte));
+  // dropout keep bits (one byte per lane-step): for the backward, and in bf16 mode for h_natural
+  const bool want_mask = drop && (store_c || bf16);
+  Tensor dmask = want_mask ? at::empty({ntiles, 2, L, 64}, word.options().dtype(at::kByte))
+                           : at::empty({0}, word.options().dtype(at::kByte));
   TORCH_CHECK(ntiles * L * (64 * NX + 16) < (1LL << 31), "ina.lstm_fwd: batch too large for the x rows");
   Tensor xg = bf16 ? at::empty({ntiles * L * (64 * NX + 16)}, word.options().dtype(at::kBFloat16))
                    : at::empty({0}, word.options().dtype(at::kBFloat16));
@@ -114,12 +117,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, 
   a.PD = (int)PD;
   a.apack = apack.data_ptr();
   a.bias = bias.data_ptr<float>();
+  // non-null hraw / cst select the stash-writing kernel (bf16: c slots of the step records)
   a.hraw = store_c ? hlane.data_ptr() : nullptr;
-  a.cst = store_c ? (bf16 ? hlane.data_ptr() : cst.data_ptr()) : nullptr;   // bf16: unused (packed in hlane)
-  // bf16: the kernel writes the dropped h in its lane layout; h_natural transposes it into hnat
-  Tensor hl = bf16 ? at::empty({ntiles, 2, L, U4, 64}, hopt) : at::empty({0}, hopt);
-  a.hdrop = bf16 ? hl.data_ptr() : hnat.data_ptr();
-  a.dmask = (store_c && drop) ? dmask.data_ptr<uint8_t>() : nullptr;
+  a.cst = store_c ? (bf16 ? hlane.data_ptr() : cst.data_ptr()) : nullptr;
+  // bf16: the kernel writes its step records (hlane); h_natural transposes the h slots into hnat
+  a.hdrop = bf16 ? hlane.data_ptr() : hnat.data_ptr();
+  a.dmask = want_mask ? dmask.data_ptr<uint8_t>() : nullptr;
   a.seed_dev = dev_int(seed_dev, "seed_dev");
   a.seed = (uint32_t)seed;
   a.thr = keep_threshold(keep_prob);
@@ -138,7 +141,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, 
   }
   check_launch(ina::lstm_fwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_fwd");
   if (bf16)
-    check_launch(ina::h_natural(hl.data_ptr(), (int)S, (int)L, (int)U, hnat_full.data_ptr(), cur_stream()), "h_natural");
+    check_launch(ina::h_natural(hlane.data_ptr(), drop ? dmask.data_ptr<uint8_t>() : nullptr, (float)(1.0 / keep_prob),
+                                (int)S, (int)L, (int)U, hnat_full.data_ptr(), cur_stream()),
+                 "h_natural");
   return {hlane, cst, hnat, dmask, xg};
 }
 
@@ -161,12 +166,12 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   check(dH, "dH", bf16 ? at::kBFloat16 : at::kFloat);
   check(apack, "apack", bf16 ? at::kBFloat16 : at::kFloat);
   check(a2pack, "a2pack", bf16 ? at::kBFloat16 : at::kFloat);
-  check(hraw, "hraw", bf16 ? at::kInt : at::kFloat);   // bf16: packed h | c << 16 (lstm_fwd)
+  check(hraw, "hraw", bf16 ? at::kBFloat16 : at::kFloat);   // bf16: lstm_fwd's step records
   TORCH_CHECK(ina::lstm_supported((int)U, (int)NX), "ina.lstm_bwd: unsupported (U, NX)");
   const int64_t S = inst.size(0), L = word.size(1), E = wemb.size(1), PD = p1emb.size(1);
   const int64_t DIN = E + 2 * PD, NF = DIN + U + 1, U4 = U / 4, KPL = frag_elems(bf16);
   TORCH_CHECK(DIN <= 4 * NX, "ina.lstm_bwd: input dim too large");
-  TORCH_CHECK(hraw.numel() == ((S + 15) / 16) * 2 * L * U4 * 64, "ina.lstm_bwd: hlane shape");
+  TORCH_CHECK(hraw.numel() == ((S + 15) / 16) * 2 * L * U4 * 64 * (bf16 ? 2 : 1), "ina.lstm_bwd: hlane shape");
   TORCH_CHECK(dH.size(0) == S && dH.size(1) == L && dH.size(2) == 2 * U, "ina.lstm_bwd: dH shape");
   TORCH_CHECK(bf16 || cst.numel() == ((S + 15) / 16) * 2 * L * U4 * 64, "ina.lstm_bwd: cst shape");
   const bool drop_ = keep_prob < 1.0;

@@ -43,8 +43,10 @@ struct LstmArgs {
 // bf16 mode: gather every token's x features once into a.xg / a.posb (lstm.hip x_gather_kernel)
 int x_gather(const LstmArgs& a, int NX, hipStream_t st);
 int lstm_fwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
-// bf16: lstm_fwd's lane-layout output [tiles][2][L][U/4][64] -> natural rows [16 * tiles][L][2U]
-int h_natural(const void* hl, int S, int L, int U, void* hnat, hipStream_t st);
+// bf16: the h slots of lstm_fwd's step records [tiles][2][L][2][U/4][64] -> natural rows
+// [16 * tiles][L][2U], with the dropout keep bits [tiles][2][L][64] applied when dmask is non-null
+int h_natural(const void* rec, const unsigned char* dmask, float inv_kp, int S, int L, int U, void* hnat,
+              hipStream_t st);
 int lstm_bwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
 // bf16 mode: reduce a.dxp into slab [blocks][2 tables][2L][PD] (needs 2L <= 128, 2PD <= 16)
 int pos_grad(const LstmArgs& a, int blocks, float* slab, hipStream_t st);

@@ -349,16 +349,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
       if (BF16) hv = round_bf(hv);  // the stored / recurrent operand value
       h[m] = hv;
     }
-    {
-      // the attention layer's input, dropout (DropoutWrapper output) applied here.  bf16: lane layout
-      // [tile][dir][t][U4][64] (one coalesced 128-B store per unit slot; h_natural_kernel transposes
-      // it) -- the natural [seq][t][2U] rows took 16 scattered 8-byte pieces per store instruction
-      // and cost ~300 of this kernel's ~700 us (kbench A/B).  fp32: natural layout directly.
-      // 32-bit offsets (S * L * 2U < 2^31 checked on the host); padding rows are stored too.
-      constexpr int HS = BF16 ? 64 : 4;   // element stride between the lane's unit slots
-      typename FragT<BF16>::elem* hn =
-          BF16 ? hnat + ((uint32_t)((tile * 2 + dir) * L + t) * U4) * 64 + lane
-               : hnat + (((uint32_t)seq * L + t) * (2 * U) + dir * U + q);
+    if constexpr (BF16) {
+      // bf16 step record [tile][dir][t][2][U4][64] (16-bit): slot 0 = the raw recurrent h (bf16), slot 1
+      // = the cell state (fp16, training only); every store is a coalesced 128-B lane-layout run off
+      // ONE address.  The h slot is both the backward's stash and the attention input:
+      // h_natural_kernel transposes it to natural rows and applies the DropoutWrapper mask from the
+      // keep bits stored here.  (Natural [seq][t][2U] rows from here scatter each store over 16 rows,
+      // ~300 us of ~550; a separate dropped copy costs 303 MB more on a write-bandwidth-bound kernel.)
+      // 32-bit offsets (checked on the host); padding rows are stored too.
+      typename FragT<BF16>::elem* rec = hnat + ((uint32_t)((tile * 2 + dir) * L + t) * (2 * U4)) * 64 + lane;
+#pragma unroll
+      for (int m = 0; m < U4; ++m) rec[m * 64] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
+      if constexpr (STORE) {
+#pragma unroll
+        for (int m = 0; m < U4; ++m) rec[(U4 + m) * 64] = __builtin_bit_cast(unsigned short, (_Float16)c[m]);
+      }
+      if constexpr (DROP) {
+        const uint32_t base = ((uint32_t)seq * L + t) * U + q;
+        uint32_t bits = 0;
+#pragma unroll
+        for (int m = 0; m < U4; ++m) bits |= dropout_keep_salted(salt, base + 4 * m, thr) ? (1u << m) : 0u;
+        dmask[(uint32_t)((tile * 2 + dir) * L + t) * 64 + lane] = (unsigned char)bits;
+      }
+    } else {
+      // fp32: the attention input (dropout applied) in natural rows, h / c stash in the lane layout
+      typename FragT<BF16>::elem* hn = hnat + (((uint32_t)seq * L + t) * (2 * U) + dir * U + q);
       if constexpr (DROP) {
         const uint32_t base = ((uint32_t)seq * L + t) * U + q;
         uint32_t bits = 0;
@@ -366,31 +381,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
         for (int m = 0; m < U4; ++m) {
           const bool keep = dropout_keep_salted(salt, base + 4 * m, thr);
           bits |= keep ? (1u << m) : 0u;
-          hn[HS * m] = to_elem(keep ? h[m] * inv_kp : 0.f, (typename FragT<BF16>::elem*)nullptr);
+          hn[4 * m] = to_elem(keep ? h[m] * inv_kp : 0.f, (typename FragT<BF16>::elem*)nullptr);
         }
         if constexpr (STORE) {   // the backward re-applies the mask from these bits (no re-hashing)
           if constexpr (U4 <= 8) dmask[(uint32_t)((tile * 2 + dir) * L + t) * 64 + lane] = (unsigned char)bits;
         }
       } else {
 #pragma unroll
-        for (int m = 0; m < U4; ++m) hn[HS * m] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
+        for (int m = 0; m < U4; ++m) hn[4 * m] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
       }
-    }
-    if constexpr (STORE && BF16) {
-      // raw recurrent h (bf16) | cell state (fp16) << 16 for the backward, lane-native: ONE coalesced
-      // 256-B dword store per unit slot (stores are issue-bound here, not bandwidth-bound)
-      uint32_t* hp = reinterpret_cast<uint32_t*>(hlane) + ((uint32_t)((tile * 2 + dir) * L + t) * U4) * 64 + lane;
+      if constexpr (STORE) {
+        typename FragT<BF16>::elem* hp = hlane + ((uint32_t)((tile * 2 + dir) * L + t) * U4) * 64 + lane;
 #pragma unroll
-      for (int m = 0; m < U4; ++m)
-        hp[m * 64] = (uint32_t)f2bf(h[m]) | ((uint32_t)__builtin_bit_cast(unsigned short, (_Float16)c[m]) << 16);
-    } else if constexpr (STORE) {
-      // fp32 mode: raw h and c, lane-native (coalesced rows)
-      typename FragT<BF16>::elem* hp = hlane + ((uint32_t)((tile * 2 + dir) * L + t) * U4) * 64 + lane;
+        for (int m = 0; m < U4; ++m) hp[m * 64] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
+        celem* cp = cst + ((uint32_t)((tile * 2 + dir) * L + t) * U4) * 64 + lane;
 #pragma unroll
-      for (int m = 0; m < U4; ++m) hp[m * 64] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
-      celem* cp = cst + ((uint32_t)((tile * 2 + dir) * L + t) * U4) * 64 + lane;
-#pragma unroll
-      for (int m = 0; m < U4; ++m) cp[m * 64] = (celem)c[m];
+        for (int m = 0; m < U4; ++m) cp[m * 64] = (celem)c[m];
+      }
     }
   };
   // two-step unrolled loop with ping-pong x buffers: the gather for step tau+1 is issued before
@@ -404,11 +411,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     // compiler's waitcnt pass merges the loop-header state conservatively and waited vmcnt(3) at the
     // top of every body, i.e. for all of the previous steps' ~16 stores (store latency on the
     // recurrence).  The count is exact because the step's VMEM stream is fixed at compile time:
-    // NST stores per step (hnat U4, packed h|c U4, dmask 1; no compiler-visible loads in the loop).
+    // NST stores per step (h U4, c U4 when STORE, keep bits 1 when DROP; no compiler-visible loads).
     // Order of VMEM ops: ld(0..R-2), then per step j: ld(j + R - 1), NST stores of step j; before
     // step j's math the ops issued after ld(j) number R - 1 + min(j, R - 1) * NST.
     constexpr int R = XG_RING;
-    constexpr int NST = U4 + (STORE ? U4 : 0) + ((DROP && STORE && U4 <= 8) ? 1 : 0);
+    constexpr int NST = U4 + (STORE ? U4 : 0) + (DROP ? 1 : 0);
     auto ld = [&](int tau, uint64_t& d) __attribute__((always_inline)) {
       const unsigned short* xp = xg + ((uint32_t)(tile * L + tof(min(tau, L - 1))) * 64 + lane) * NX;
       asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(d) : "v"(xp) : "memory");
@@ -494,23 +501,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
 // one contiguous run written with coalesced dwords (16 threads per sequence).
 // ------------------------------------------------------------------------------------------
 template <int U>
-__global__ __launch_bounds__(256) void h_natural_kernel(const unsigned short* __restrict__ hl, int L,
-                                                        unsigned short* __restrict__ hnat) {
-  constexpr int U4 = U / 4;
-  extern __shared__ __attribute__((aligned(16))) unsigned short lds_h[];   // the tile's input block
+__global__ __launch_bounds__(256) void h_natural_kernel(const unsigned short* __restrict__ rec,
+                                                        const unsigned char* __restrict__ dmask, int L,
+                                                        float inv_kp, unsigned short* __restrict__ hnat) {
+  constexpr int U4 = U / 4, PIECE = U4 * 64 * 2;   // bytes of one (dir, step) h slot
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds_h[];   // h [2][L][U4][64], keep bits
   const int tile = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // 1) the tile's contiguous input block [2][L][U4][64] -> LDS: 1-KB LDS-DMA pieces, all in flight
-  const int bytes = 2 * L * U4 * 64 * 2;
-  const char* src = reinterpret_cast<const char*>(hl) + (size_t)tile * bytes;
-  for (int k = wave; k * 1024 < bytes; k += 4) {
-    const int off = k * 1024 + lane * 16;
-    if (off < bytes)
-      __builtin_amdgcn_global_load_lds(src + off, reinterpret_cast<char*>(lds_h) + k * 1024, 16, 0, 0);
+  // 1) the h slots of the tile's step records ([2][L][2][U4][64]) and its keep bits [2][L][64] -> LDS
+  //    by LDS-DMA (16 B per lane, one piece per wave instruction), all in flight
+  const int hbytes = 2 * L * PIECE, hpad = (hbytes + 1023) & ~1023, mbytes = dmask ? 2 * L * 64 : 0;
+  const char* src = reinterpret_cast<const char*>(rec) + (size_t)tile * 2 * hbytes;
+  char* lds = reinterpret_cast<char*>(lds_h);
+  for (int k = wave; k < 2 * L; k += 4)
+    if (lane * 16 < PIECE)
+      __builtin_amdgcn_global_load_lds(src + (size_t)k * 2 * PIECE + lane * 16, lds + k * PIECE, 16, 0, 0);
+  if (dmask) {
+    const char* msrc = reinterpret_cast<const char*>(dmask) + (size_t)tile * mbytes;
+    for (int k = wave; k * 1024 < mbytes; k += 4) {
+      const int off = k * 1024 + lane * 16;
+      if (off < mbytes) __builtin_amdgcn_global_load_lds(msrc + off, lds + hpad + k * 1024, 16, 0, 0);
+    }
   }
   __syncthreads();
+  const unsigned char* keep = reinterpret_cast<const unsigned char*>(lds + hpad);
   // 2) natural rows: thread (sequence n = tid / 16, part) writes dwords part, part + 16, ... of n's
-  //    contiguous run [L][2U] (dword = features (2p, 2p + 1) of one step)
+  //    contiguous run [L][2U] (dword = features (2p, 2p + 1) of one step); DropoutWrapper output
+  //    keep ? bf16(h / keep_prob) : 0 (model/graph.py:36-38)
   const int n = threadIdx.x >> 4, part = threadIdx.x & 15;
   uint32_t* dst = reinterpret_cast<uint32_t*>(hnat + ((size_t)tile * 16 + n) * L * 2 * U);
   for (int i = part; i < L * U; i += 16) {
@@ -519,8 +536,10 @@ __global__ __launch_bounds__(256) void h_natural_kernel(const unsigned short* __
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int fe = f + e, d = fe >= U ? 1 : 0, u = fe - d * U;
-      const uint32_t x = lds_h[((d * L + t) * U4 + (u >> 2)) * 64 + (u & 3) * 16 + n];
-      v |= x << (16 * e);
+      const int li = (u & 3) * 16 + n;
+      unsigned short x = lds_h[((d * L + t) * U4 + (u >> 2)) * 64 + li];
+      if (dmask) x = ((keep[(d * L + t) * 64 + li] >> (u >> 2)) & 1u) ? f2bf(bf2f(x) * inv_kp) : (unsigned short)0;
+      v |= (uint32_t)x << (16 * e);
     }
     dst[i] = v;
   }
@@ -627,13 +646,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     const long rowbase = (long)inst[seqc] * L;
     const typename CT<BF16>::type* cbase = cst + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
     const elem* hbase = hraw + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
-    // bf16: packed h | c << 16 (one dword load per unit slot and step)
-    const uint32_t* pbase = reinterpret_cast<const uint32_t*>(hraw) + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
+    // bf16: the forward's step records [t][2][U4][64]: h slot, then c slot (fp16 bits)
+    const unsigned short* rbase = reinterpret_cast<const unsigned short*>(hraw) + ((size_t)tile * 2 + dir) * L * 2 * U4 * 64 + lane;
     auto ld_hc = [&](int tt, int m, float& hv, float& cv) {
       if constexpr (BF16) {
-        const uint32_t v = pbase[((size_t)tt * U4 + m) * 64];
-        hv = bf2f((unsigned short)(v & 0xFFFFu));
-        cv = (float)__builtin_bit_cast(_Float16, (unsigned short)(v >> 16));
+        hv = bf2f(rbase[((size_t)tt * 2 * U4 + m) * 64]);
+        cv = (float)__builtin_bit_cast(_Float16, rbase[((size_t)tt * 2 * U4 + U4 + m) * 64]);
       } else {
         hv = from_elem(hbase[((size_t)tt * U4 + m) * 64]);
         cv = from_c(cbase[((size_t)tt * U4 + m) * 64]);
@@ -1228,10 +1246,13 @@ int pos_grad_shift(const LstmArgs& a, float* gpart, float* out, hipStream_t st) 
   return 0;
 }
 
-int h_natural(const void* hl, int S, int L, int U, void* hnat, hipStream_t st) {
+int h_natural(const void* rec, const unsigned char* dmask, float inv_kp, int S, int L, int U, void* hnat,
+              hipStream_t st) {
   const int ntiles = (S + 15) / 16;
   if (ntiles <= 0) return 0;
-  const size_t lds = ((size_t)2 * L * (U / 4) * 64 * sizeof(unsigned short) + 1023) & ~(size_t)1023;
+  const size_t lds = (((size_t)2 * L * (U / 4) * 64 * sizeof(unsigned short) + 1023) & ~(size_t)1023) +
+                     (dmask ? (((size_t)2 * L * 64 + 1023) & ~(size_t)1023) : 0);
+  const auto* hl = rec;
   if (lds > 160 * 1024) return -1;
   const auto* in = (const unsigned short*)hl;
   auto* out = (unsigned short*)hnat;
@@ -1239,7 +1260,7 @@ int h_natural(const void* hl, int S, int L, int U, void* hnat, hipStream_t st) {
   if (U == UV) {                                                                                       \
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)h_natural_kernel<UV>,                        \
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
-    hipLaunchKernelGGL(h_natural_kernel<UV>, dim3(ntiles), dim3(256), lds, st, in, L, out);           \
+    hipLaunchKernelGGL(h_natural_kernel<UV>, dim3(ntiles), dim3(256), lds, st, in, dmask, L, inv_kp, out); \
     INA_CHECK_LAUNCH();                                                                                \
     return 0;                                                                                          \
   }

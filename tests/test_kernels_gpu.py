@@ -46,12 +46,11 @@ def _gathered(dd, inst):
 
 
 def _split_stash(hlane, cst):
-    """lstm_fwd's backward stash as float lane-layout (h, c): bf16 mode packs h (bf16) | c (fp16) << 16
-    into one int32 per slot (cst is empty); fp32 mode returns separate arrays."""
-    if hlane.dtype == torch.int32:
-        halves = hlane.view(torch.int16).view(*hlane.shape, 2)
-        h = halves[..., 0].contiguous().view(torch.bfloat16).float()
-        c = halves[..., 1].contiguous().view(torch.float16).float()
+    """lstm_fwd's backward stash as float lane-layout (h, c): bf16 mode keeps both in its step records
+    (h slot bf16, c slot fp16 bits; cst is empty); fp32 mode returns separate arrays."""
+    if hlane.dim() == 6:   # bf16 step records [tiles][2][L][2 slots][U4][64]: h (bf16), c (fp16 bits)
+        h = hlane[:, :, :, 0].contiguous().float()
+        c = hlane[:, :, :, 1].contiguous().view(torch.float16).float()
         return h, c
     return hlane.float(), (cst.float() if cst is not None else None)
 
