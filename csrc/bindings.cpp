@@ -54,12 +54,11 @@ uint32_t keep_threshold(double kp) {
 // hnat = the DropoutWrapper output in natural layout [S, L, 2U] (the attention input); dmask = the
 // dropout keep bits; xg (bf16 mode) = the gathered encoder input [tiles][L][64][NX] followed by the
 // position ids [tiles][L][16] (x_gather_kernel; an input of lstm_bwd).
-std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
-                                            const Tensor& pos2, const Tensor& wemb, const Tensor& p1emb,
-                                            const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U,
-                                            int64_t NX, bool bf16, bool store_c, int64_t seed, double keep_prob,
-                                            const std::optional<Tensor>& seed_dev,
-                                            const std::optional<Tensor>& wrows) {
+static std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd_impl(
+    const Tensor& inst, const Tensor& word, const Tensor& pos1, const Tensor& pos2, const Tensor& wemb,
+    const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U, int64_t NX, bool bf16,
+    bool store_c, int64_t seed, double keep_prob, const std::optional<Tensor>& seed_dev,
+    const std::optional<Tensor>& wrows, bool natural) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -140,11 +139,72 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, 
     check_launch(ina::x_gather(a, (int)NX, cur_stream()), "x_gather");
   }
   check_launch(ina::lstm_fwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_fwd");
-  if (bf16)
+  if (bf16 && natural)
     check_launch(ina::h_natural(hlane.data_ptr(), drop ? dmask.data_ptr<uint8_t>() : nullptr, (float)(1.0 / keep_prob),
                                 (int)S, (int)L, (int)U, hnat_full.data_ptr(), cur_stream()),
                  "h_natural");
   return {hlane, cst, hnat, dmask, xg};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
+                                            const Tensor& pos2, const Tensor& wemb, const Tensor& p1emb,
+                                            const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U,
+                                            int64_t NX, bool bf16, bool store_c, int64_t seed, double keep_prob,
+                                            const std::optional<Tensor>& seed_dev,
+                                            const std::optional<Tensor>& wrows) {
+  return lstm_fwd_impl(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, bias, U, NX, bf16, store_c, seed, keep_prob,
+                       seed_dev, wrows, true);
+}
+
+// bf16 encoder forward in three launches: x_gather, lstm_fwd, hnat_attn (the LSTM output transpose +
+// dropout fused with the self-attention forward, attention.hip).  Returns lstm_fwd's outputs plus
+// attn_fwd's (e, alphas).  Callers check hnat_attn_ok first (else lstm_fwd + attn_fwd).
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> lstm_attn_fwd(
+    const Tensor& inst, const Tensor& word, const Tensor& pos1, const Tensor& pos2, const Tensor& wemb,
+    const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U, int64_t NX,
+    bool store_c, int64_t seed, double keep_prob, const std::optional<Tensor>& seed_dev,
+    const std::optional<Tensor>& wrows, const Tensor& mask, const Tensor& w1pack, const Tensor& b1, const Tensor& w2) {
+  check(mask, "mask", at::kInt);
+  check(w1pack, "w1pack", at::kBFloat16);
+  check(b1, "b1", at::kFloat);
+  check(w2, "w2", at::kFloat);
+  const int64_t L = word.size(1), S = inst.size(0), NT = (L + 15) / 16;
+  TORCH_CHECK(mask.size(1) == L, "ina.lstm_attn_fwd: mask length");
+  TORCH_CHECK(b1.numel() == 2 * U && w2.numel() == 2 * U, "ina.lstm_attn_fwd: b1/w2 size");
+  TORCH_CHECK(NT >= 1 && NT <= 4, "ina.lstm_attn_fwd: L must be <= 64");
+  const int64_t H2 = 2 * U, MT = (H2 + 15) / 16, NKS = (H2 + 31) / 32;
+  TORCH_CHECK(w1pack.numel() == MT * NKS * 64 * 8, "ina.lstm_attn_fwd: w1pack size");
+  const bool drop = keep_prob < 1.0;
+  TORCH_CHECK(ina::hnat_attn_lds_bytes((int)U, (int)L, drop) <= 160 * 1024, "ina.lstm_attn_fwd: LDS budget");
+  auto r = lstm_fwd_impl(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, bias, U, NX, true, store_c, seed, keep_prob,
+                         seed_dev, wrows, false);
+  auto e = at::empty({S, 2 * U}, b1.options());
+  auto alphas = at::empty({S, L}, b1.options());
+  if (S == 0) return {std::get<0>(r), std::get<1>(r), std::get<2>(r), std::get<3>(r), std::get<4>(r), e, alphas};
+  const Tensor& hlane = std::get<0>(r);
+  const Tensor& hnat = std::get<2>(r);   // first S rows of the [16 * tiles] allocation
+  const Tensor& dmask = std::get<3>(r);
+  TORCH_CHECK(hlane.numel() == ((S + 15) / 16) * 2 * L * 2 * (U / 4) * 64, "ina.lstm_attn_fwd: step records");
+  TORCH_CHECK(!drop || dmask.numel() == ((S + 15) / 16) * 2 * L * 64, "ina.lstm_attn_fwd: keep bits");
+  ina::AttnArgs a{};
+  a.inst = inst.data_ptr<int>();
+  a.mask = mask.data_ptr<int>();
+  a.S = (int)S;
+  a.L = (int)L;
+  a.w1pack = w1pack.data_ptr();
+  a.b1 = b1.data_ptr<float>();
+  a.w2 = w2.data_ptr<float>();
+  a.e = e.data_ptr<float>();
+  a.alphas = alphas.data_ptr<float>();
+  check_launch(ina::hnat_attn(hlane.data_ptr(), drop ? dmask.data_ptr<uint8_t>() : nullptr, (float)(1.0 / keep_prob),
+                              hnat.data_ptr(), a, (int)U, cur_stream()),
+               "hnat_attn");
+  return {std::get<0>(r), std::get<1>(r), hnat, std::get<3>(r), std::get<4>(r), e, alphas};
+}
+
+bool hnat_attn_ok(int64_t U, int64_t L, double keep_prob) {
+  return (U == 8 || U == 20 || U == 32) && L >= 1 && L <= 64 &&
+         ina::hnat_attn_lds_bytes((int)U, (int)L, keep_prob < 1.0) <= 160 * 1024;
 }
 
 std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
@@ -568,6 +628,8 @@ TORCH_LIBRARY(ina, m) {
   m.def("abi_version", &abi_version);
   m.def("lstm_fwd", &lstm_fwd);
   m.def("lstm_bwd", &lstm_bwd);
+  m.def("lstm_attn_fwd", &lstm_attn_fwd);
+  m.def("hnat_attn_ok", &hnat_attn_ok);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("routing_fwd", &routing_fwd);

@@ -75,6 +75,10 @@ struct AttnArgs {
 };
 int attn_fwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st);
 int attn_bwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st);
+// bf16: lstm_fwd step records (+ keep bits) -> natural rows hnat AND the attention forward (e, alphas)
+size_t hnat_attn_lds_bytes(int U, int L, bool drop);
+int hnat_attn(const void* rec, const unsigned char* dmask, float inv_kp, void* hnat, const AttnArgs& a, int U,
+              hipStream_t st);
 
 int routing_fwd(const float* e, const float* Ws, int E, int N, int K, int Q, int R, int H, float* cls, int blocks,
                 hipStream_t st);

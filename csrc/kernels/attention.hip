@@ -101,6 +101,79 @@ INA_DEVICE void load_h(const typename FT<BF16>::elem* hraw, long seq, int tok, i
   }
 }
 
+// bf16 forward of one sentence from its H tiles (hf: token 16 * nt + n, features 32 * ks + 8 * q ..+7,
+// zero outside [L) x [2U)) and the mask ids of those tokens: projection (MFMA), tanh, w2 dot, masked
+// softmax over the tokens, pooling.  Shared by attn_fwd_kernel (H from global rows) and
+// hnat_attn_kernel (H from the LDS-transposed LSTM step records).
+template <int U, int NT>
+INA_DEVICE void attn_sentence_bf16(const u16x8_t (&hf)[NT][AShape<U, NT, true>::NKS], const int (&mk)[NT],
+                                   const u16x8_t (&A)[AShape<U, NT, true>::MT][AShape<U, NT, true>::NKS],
+                                   const float (&bj)[AShape<U, NT, true>::MT][4],
+                                   const float (&wj)[AShape<U, NT, true>::MT][4], long s, int L, int q, int n,
+                                   float* __restrict__ e_out, float* __restrict__ alphas) {
+  using Sh = AShape<U, NT, true>;
+  constexpr int H2 = Sh::H2, NKS = Sh::NKS, MT = Sh::MT;
+  float score[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int tok = 16 * nt + n;
+    float sp = 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      f32x4_t acc = {bj[m][0], bj[m][1], bj[m][2], bj[m][3]};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) acc = mma(A[m][ks], hf[nt][ks], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sp += wj[m][r] * tanhf_(acc[r]);
+    }
+    sp = cross_group_sum(sp);
+    const float m01 = mk[nt] > 0 ? 1.f : 0.f;
+    score[nt] = (tok < L) ? sp + (1.f - m01) * -2147483648.f : -INFINITY;
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) mx = fmaxf(mx, score[nt]);
+  mx = group16_max(mx);
+  float p[NT], sum = 0.f;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    p[nt] = (16 * nt + n < L) ? __expf(score[nt] - mx) : 0.f;
+    sum += p[nt];
+  }
+  sum = group16_sum(sum);
+  const float inv = 1.f / sum;
+  float ev[NKS][8];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ev[ks][j] = 0.f;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int tok = 16 * nt + n;
+    const float a = p[nt] * inv;
+    if (q == 0 && tok < L) alphas[(long)s * L + tok] = a;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ev[ks][j] += a * bf2f(hf[nt][ks][j]);
+  }
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ev[ks][j] = group16_sum(ev[ks][j]);
+  if (n == 0) {
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int k0 = 32 * ks + 8 * q;
+      if (k0 < H2) {
+        float4* o = reinterpret_cast<float4*>(e_out + (long)s * H2 + k0);
+        o[0] = make_float4(ev[ks][0], ev[ks][1], ev[ks][2], ev[ks][3]);
+        o[1] = make_float4(ev[ks][4], ev[ks][5], ev[ks][6], ev[ks][7]);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -150,65 +223,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
         }
         mk[nt] = maskarr[row + (tv ? tok : L - 1)];
       }
-      float score[NT];
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int tok = 16 * nt + n;
-        float sp = 0.f;
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          f32x4_t acc = {bj[m][0], bj[m][1], bj[m][2], bj[m][3]};
-#pragma unroll
-          for (int ks = 0; ks < NKS; ++ks) acc = mma(A[m][ks], hf[nt][ks], acc);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) sp += wj[m][r] * tanhf_(acc[r]);
-        }
-        sp = cross_group_sum(sp);
-        const float m01 = mk[nt] > 0 ? 1.f : 0.f;
-        score[nt] = (tok < L) ? sp + (1.f - m01) * -2147483648.f : -INFINITY;
-      }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) mx = fmaxf(mx, score[nt]);
-      mx = group16_max(mx);
-      float p[NT], sum = 0.f;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        p[nt] = (16 * nt + n < L) ? __expf(score[nt] - mx) : 0.f;
-        sum += p[nt];
-      }
-      sum = group16_sum(sum);
-      const float inv = 1.f / sum;
-      float ev[NKS][8];
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ev[ks][j] = 0.f;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int tok = 16 * nt + n;
-        const float a = p[nt] * inv;
-        if (q == 0 && tok < L) alphas[(long)s * L + tok] = a;
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) ev[ks][j] += a * bf2f(hf[nt][ks][j]);
-      }
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ev[ks][j] = group16_sum(ev[ks][j]);
-      if (n == 0) {
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          const int k0 = 32 * ks + 8 * q;
-          if (k0 < H2) {
-            float4* o = reinterpret_cast<float4*>(e_out + (long)s * H2 + k0);
-            o[0] = make_float4(ev[ks][0], ev[ks][1], ev[ks][2], ev[ks][3]);
-            o[1] = make_float4(ev[ks][4], ev[ks][5], ev[ks][6], ev[ks][7]);
-          }
-        }
-      }
+      attn_sentence_bf16<U, NT>(hf, mk, A, bj, wj, s, L, q, n, e_out, alphas);
       continue;
     }
     // pass 1: scores (projection + tanh + w2 dot), one token tile at a time
@@ -274,6 +289,113 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
         if (k < H2) e_out[(long)s * H2 + k] = ev[v];
       }
     }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// bf16 forward fused with the LSTM output transpose (replaces h_natural_kernel + attn_fwd_kernel).
+// Input: lstm_fwd's step records [tile][dir][t][2][U4][64] (16-bit; slot 0 = h of the 16 sequences
+// of the tile in the lane layout: unit 4m + (li >> 4) of sequence li & 15 at [m][li]) and the
+// DropoutWrapper keep bits [tile][dir][t][64] (bit m of byte li).  One 512-thread workgroup per tile:
+//   1) every thread loads 16-B chunks of the tile's h slots (+ the 8 keep bytes of each chunk) into
+//      registers, applies the dropout (model/graph.py:36-38: keep ? h / keep_prob : 0, bf16) and
+//      scatters the 8 values into the tile's natural rows [16][L][2U] in LDS (model/graph.py:49);
+//   2) the LDS rows -> HBM with 16-B stores (the tile's rows are one contiguous run of hnat, the
+//      backward's input);
+//   3) each wave pools 2 sentences from the LDS rows (attn_sentence_bf16: 16-B LDS reads); their
+//      instance ids and mask ids are loaded before the transpose.
+// LDS = the natural rows only (47 KB at L=37, u=20): 2 workgroups per CU.  Saves attn_fwd's 303 MB
+// re-read of the natural rows (default 5w5s, 2048 episodes) and a launch.
+// ------------------------------------------------------------------------------------------
+template <int U, int NT>
+__global__ __launch_bounds__(512) void hnat_attn_kernel(const unsigned short* __restrict__ rec,
+                                                        const unsigned char* __restrict__ dmask, int S, int L,
+                                                        float inv_kp, unsigned short* __restrict__ hnat,
+                                                        const int* __restrict__ inst, const int* __restrict__ maskarr,
+                                                        const u16x8_t* __restrict__ w1pack,
+                                                        const float* __restrict__ b1, const float* __restrict__ w2,
+                                                        float* __restrict__ e_out, float* __restrict__ alphas) {
+  using Sh = AShape<U, NT, true>;
+  constexpr int H2 = Sh::H2, NKS = Sh::NKS, MT = Sh::MT;
+  constexpr int U4 = U / 4, CPP = U4 * 64 / 8;   // 16-B chunks per (dir, step) h slot
+  extern __shared__ __attribute__((aligned(16))) unsigned short nat[];   // [16][L][2U] bf16
+  const int tile = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane >> 4, nl = lane & 15;
+  // sentence ids and mask ids first (their dependent loads overlap the transpose)
+  int mk[2][NT];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const long s = (long)tile * 16 + wave * 2 + j;
+    const long row = (long)inst[s < S ? s : S - 1] * L;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int tok = 16 * nt + nl;
+      mk[j][nt] = maskarr[row + (tok < L ? tok : L - 1)];
+    }
+  }
+  // 1) records -> registers -> dropout -> natural rows in LDS
+  const uint4* src = reinterpret_cast<const uint4*>(rec + (size_t)tile * 2 * L * 2 * U4 * 64);
+  const int nch = 2 * L * CPP;
+  for (int c = threadIdx.x; c < nch; c += 512) {
+    const int k = c / CPP, off = c - k * CPP;             // k = dir * L + t
+    const uint4 v = src[(size_t)k * 2 * CPP + off];      // h slot of record k (c slot skipped)
+    const int e0 = off * 8, m = e0 >> 6, li0 = e0 & 63;   // 8 lanes li0..li0+7: same m, r = li0 >> 4
+    const int r = li0 >> 4, n0 = li0 & 15;
+    const int d = k >= L ? 1 : 0, t = k - d * L;
+    const int col = d * U + 4 * m + r;
+    unsigned long long kb = ~0ull;
+    if (dmask) kb = *reinterpret_cast<const unsigned long long*>(dmask + ((size_t)tile * 2 * L + k) * 64 + li0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      unsigned short x = (unsigned short)(w[i >> 1] >> (16 * (i & 1)));
+      if (dmask) x = ((kb >> (8 * i + m)) & 1ull) ? f2bf(bf2f(x) * inv_kp) : (unsigned short)0;
+      nat[((n0 + i) * L + t) * H2 + col] = x;
+    }
+  }
+  u16x8_t A[MT][NKS];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) A[m][ks] = w1pack[(m * NKS + ks) * 64 + lane];
+  float bj[MT][4], wj[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * m + 4 * q + r;
+      bj[m][r] = j < H2 ? b1[j] : 0.f;
+      wj[m][r] = j < H2 ? w2[j] : 0.f;
+    }
+  __syncthreads();
+  // 2) the tile's rows are one contiguous run of hnat (padding rows of the last tile included)
+  {
+    const uint4* ls = reinterpret_cast<const uint4*>(nat);
+    uint4* dst = reinterpret_cast<uint4*>(hnat + (size_t)tile * 16 * L * H2);
+    for (int i = threadIdx.x; i < 16 * L * H2 / 8; i += 512) dst[i] = ls[i];
+  }
+  // 3) attention forward, 2 sentences per wave (unrolled: mk stays in registers)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = wave * 2 + j;
+    const long s = (long)tile * 16 + n;
+    if (s >= S) break;   // wave-uniform
+    u16x8_t hf[NT][NKS];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int tok = 16 * nt + nl;
+      const bool tv = tok < L;
+      const int hrow = (n * L + (tv ? tok : L - 1)) * H2;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int k0 = 32 * ks + 8 * q;
+        const bool ok = tv && (k0 < H2);
+        const u16x8_t v = *reinterpret_cast<const u16x8_t*>(nat + hrow + (ok ? k0 : 0));
+        hf[nt][ks] = ok ? v : u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+    attn_sentence_bf16<U, NT>(hf, mk[j], A, bj, wj, s, L, q, nl, e_out, alphas);
   }
 }
 
@@ -822,6 +944,40 @@ static int attn_bwd_t(const AttnArgs& a, hipStream_t st) {
     INA_ATTN_CASE(FN, 8) INA_ATTN_CASE(FN, 20) INA_ATTN_CASE(FN, 32) \
   }                                           \
   return -1;
+
+size_t hnat_attn_lds_bytes(int U, int L, bool) { return (size_t)16 * L * 2 * U * 2; }
+
+template <int U, int NT>
+static int hnat_attn_t(const void* rec, const unsigned char* dmask, float inv_kp, void* hnat, const AttnArgs& a,
+                       hipStream_t st) {
+  const size_t lds = hnat_attn_lds_bytes(U, a.L, dmask != nullptr);
+  if (lds > 160 * 1024) return -1;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)hnat_attn_kernel<U, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+  const int ntiles = (a.S + 15) / 16;
+  hipLaunchKernelGGL((hnat_attn_kernel<U, NT>), dim3(ntiles), dim3(512), lds, st, (const unsigned short*)rec, dmask,
+                     a.S, a.L, inv_kp, (unsigned short*)hnat, a.inst, a.mask, (const u16x8_t*)a.w1pack, a.b1, a.w2,
+                     a.e, a.alphas);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int hnat_attn(const void* rec, const unsigned char* dmask, float inv_kp, void* hnat, const AttnArgs& a, int U,
+              hipStream_t st) {
+  if (a.S <= 0) return 0;
+  const int NT = (a.L + 15) / 16;
+#define INA_HA(UV)                                                         \
+  if (U == UV) {                                                           \
+    if (NT == 1) return hnat_attn_t<UV, 1>(rec, dmask, inv_kp, hnat, a, st); \
+    if (NT == 2) return hnat_attn_t<UV, 2>(rec, dmask, inv_kp, hnat, a, st); \
+    if (NT == 3) return hnat_attn_t<UV, 3>(rec, dmask, inv_kp, hnat, a, st); \
+    if (NT == 4) return hnat_attn_t<UV, 4>(rec, dmask, inv_kp, hnat, a, st); \
+  }
+  INA_HA(8) INA_HA(20) INA_HA(32)
+#undef INA_HA
+  return -1;
+}
 
 int attn_fwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st) { INA_ATTN_DISPATCH(attn_fwd_t) }
 int attn_bwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st) { INA_ATTN_DISPATCH(attn_bwd_t) }

@@ -74,13 +74,19 @@ class EncoderFn(torch.autograd.Function):
             bias = torch.stack([bf.detach(), bb.detach()]).float().contiguous()
         need_grad = ctx.needs_input_grad[5:15].count(True) > 0 if hasattr(ctx, "needs_input_grad") else True
         kp = float(meta["keep_prob"])
-        hlane, cst, hnat, dmask, xg = o.lstm_fwd(inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
-                                      p2emb.detach().contiguous(), apack, bias, U, sh["NX"], bf16, bool(need_grad),
-                                      int(meta["seed"]), kp, meta.get("seed_dev"),
-                                      word_rows(word, wemb, bool(meta.get("word_grad", False))) if bf16 else None)
         w1pack, w1tpack = (pk["w1pack"], pk["w1tpack"]) if pk is not None else pack_attn(W1, bf16)
-        e, alphas = o.attn_fwd(hnat, inst, mask, w1pack, b1.detach().contiguous(),
-                               w2.detach().reshape(-1).contiguous(), U, bf16, int(meta.get("attn_blocks", 0)))
+        lstm_args = (inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
+                     p2emb.detach().contiguous(), apack, bias, U, sh["NX"])
+        tail = (int(meta["seed"]), kp, meta.get("seed_dev"),
+                word_rows(word, wemb, bool(meta.get("word_grad", False))) if bf16 else None)
+        b1c, w2c = b1.detach().contiguous(), w2.detach().reshape(-1).contiguous()
+        if bf16 and meta.get("fuse_hnat_attn", True) and o.hnat_attn_ok(U, word.shape[1], kp):
+            # LSTM output transpose + dropout fused with the attention forward (hnat_attn_kernel)
+            hlane, cst, hnat, dmask, xg, e, alphas = o.lstm_attn_fwd(*lstm_args, bool(need_grad), *tail,
+                                                                     mask, w1pack, b1c, w2c)
+        else:
+            hlane, cst, hnat, dmask, xg = o.lstm_fwd(*lstm_args, bf16, bool(need_grad), *tail)
+            e, alphas = o.attn_fwd(hnat, inst, mask, w1pack, b1c, w2c, U, bf16, int(meta.get("attn_blocks", 0)))
         if need_grad:
             ctx.save_for_backward(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst,
                                   w1pack, w1tpack, b1, w2, alphas, hnat, dmask, xg)

@@ -142,6 +142,38 @@ def test_attention_forward(dtype, keep_prob):
     assert ee < tol and ea < tol
 
 
+@pytest.mark.parametrize("keep_prob", [1.0, 0.9])
+@pytest.mark.parametrize("tail", [0, 5])
+def test_fused_hnat_attention_matches_unfused(keep_prob, tail):
+    """lstm_attn_fwd (transpose + dropout + attention in one kernel) == lstm_fwd + attn_fwd, bitwise."""
+    from induction_network_on_fewrel_amd.ops import ops
+    from induction_network_on_fewrel_amd.ops.packing import lstm_shape, pack_attn, pack_lstm
+    cfg, data, model, dd, inst, _ = _problem(dtype="bf16")
+    if tail:
+        inst = inst[: inst.shape[0] - tail].contiguous()   # a partial last 16-sequence tile
+    p = model.pdict()
+    U = cfg.hidden_size
+    DIN = model.params.input_dim
+    apack, _ = pack_lstm(p["lstm_fw_kernel"], p["lstm_bw_kernel"], U, DIN, True)
+    bias = torch.stack([p["lstm_fw_bias"], p["lstm_bw_bias"]]).detach().float().contiguous()
+    word, pos1, pos2, mask = dd.arrays()
+    assert ops().hnat_attn_ok(U, word.shape[1], keep_prob)
+    args = (inst, word, pos1, pos2, p["word_embedding"].detach(), p["pos1_embedding"].detach(),
+            p["pos2_embedding"].detach(), apack, bias, U, lstm_shape(U, DIN, True)["NX"])
+    w1p, _ = pack_attn(p["attn_kernel"], True)
+    b1 = p["attn_bias"].detach().contiguous()
+    w2 = p["attn_w2"].detach().reshape(-1).contiguous()
+    hl0, _, hn0, dm0, _ = ops().lstm_fwd(*args, True, True, 77, keep_prob, None, None)
+    e0, a0 = ops().attn_fwd(hn0, inst, mask, w1p, b1, w2, U, True, 0)
+    hl1, _, hn1, dm1, _, e1, a1 = ops().lstm_attn_fwd(*args, True, 77, keep_prob, None, None, mask, w1p, b1, w2)
+    torch.cuda.synchronize()
+    assert hn1.shape == hn0.shape and e1.shape == e0.shape and a1.shape == a0.shape
+    assert torch.equal(hl1, hl0) and torch.equal(dm1, dm0)
+    assert torch.equal(hn1, hn0), "natural rows differ"
+    assert torch.equal(e1, e0), (e1 - e0).abs().max()
+    assert torch.equal(a1, a0), (a1 - a0).abs().max()
+
+
 def _encoder_grads_ref(model, dd, inst, de, keep_prob, seed, bf16):
     p = {k: v.detach().clone().requires_grad_(True) for k, v in model.pdict().items()}
     p["word_embedding"].requires_grad_(False)
