@@ -297,9 +297,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
 // Input: lstm_fwd's step records [tile][dir][t][2][U4][64] (16-bit; slot 0 = h of the 16 sequences
 // of the tile in the lane layout: unit 4m + (li >> 4) of sequence li & 15 at [m][li]) and the
 // DropoutWrapper keep bits [tile][dir][t][64] (bit m of byte li).  One 512-thread workgroup per tile:
-//   1) every thread loads 16-B chunk pairs of the tile's h slots (+ their keep bytes) into
-//      registers, applies the dropout (model/graph.py:36-38: keep ? h / keep_prob : 0, bf16) and
-//      scatters them as dwords into the tile's natural rows [16][L][2U] in LDS (model/graph.py:49);
+//   1) every thread loads 4 16-B chunks (units 4m..4m+3) of the tile's h slots (+ their keep bytes)
+//      into registers, applies the dropout (model/graph.py:36-38: keep ? h / keep_prob : 0, bf16)
+//      and scatters them as 8-B pieces into the tile's natural rows [16][L][2U] in LDS
+//      (model/graph.py:49);
 //   2) the LDS rows -> HBM with 16-B stores (the tile's rows are one contiguous run of hnat, the
 //      backward's input);
 //   3) each wave pools 2 sentences from the LDS rows (attn_sentence_bf16: 16-B LDS reads); their
@@ -336,36 +337,37 @@ __global__ __launch_bounds__(512) void hnat_attn_kernel(const unsigned short* __
   }
   // 1) records -> registers -> dropout -> natural rows in LDS
   const uint4* src = reinterpret_cast<const uint4*>(rec + (size_t)tile * 2 * L * 2 * U4 * 64);
-  // a work item = the chunks of units (4m + r, 4m + r + 1), r even, of 8 sequences n0..n0+7: lanes
-  // li0 = 16r + n0 and li0 + 16 (chunks oa, oa + 2 of the slot); each sequence's two values form one
-  // dword of its natural row
-  const int nit = 2 * L * U4 * 4;
-  uint32_t* nat32 = reinterpret_cast<uint32_t*>(nat);
+  // a work item = the 4 chunks of units 4m .. 4m + 3 of 8 sequences n0..n0+7 (lanes 16r + n0, chunks
+  // 8m + 2r + n0 / 8 of the slot); each sequence's 4 values are one 8-B piece of its natural row
+  // (column d * U + 4m: 8-B aligned since U % 4 == 0)
+  const int nit = 2 * L * U4 * 2;
+  uint2* nat64 = reinterpret_cast<uint2*>(nat);
   for (int c = threadIdx.x; c < nit; c += 512) {
-    const int k = c / (U4 * 4), pc = c - k * (U4 * 4);   // k = dir * L + t
-    const int m = pc >> 2, p = pc & 3;
-    const int r = (p >> 1) * 2, n0 = (p & 1) * 8, li0 = 16 * r + n0;
-    const int oa = m * 8 + (li0 >> 3);
-    const uint4 va = src[(size_t)k * 2 * CPP + oa];       // h slot of record k (c slot skipped)
-    const uint4 vb = src[(size_t)k * 2 * CPP + oa + 2];
+    const int k = c / (U4 * 2), pc = c - k * (U4 * 2);   // k = dir * L + t
+    const int m = pc >> 1, n0 = (pc & 1) * 8;
+    const uint4* sk = src + (size_t)k * 2 * CPP + m * 8 + (n0 >> 3);   // h slot of record k
+    uint4 v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = sk[2 * r];
     const int d = k >= L ? 1 : 0, t = k - d * L;
-    const int col2 = (d * U + 4 * m + r) >> 1;
-    unsigned long long ka = ~0ull, kb = ~0ull;
+    const int col4 = (d * U + 4 * m) >> 2;
+    unsigned long long kb[4] = {~0ull, ~0ull, ~0ull, ~0ull};
     if (dmask) {
-      const unsigned char* kp = dmask + ((size_t)tile * 2 * L + k) * 64 + li0;
-      ka = *reinterpret_cast<const unsigned long long*>(kp);
-      kb = *reinterpret_cast<const unsigned long long*>(kp + 16);
+      const unsigned char* kp = dmask + ((size_t)tile * 2 * L + k) * 64 + n0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) kb[r] = *reinterpret_cast<const unsigned long long*>(kp + 16 * r);
     }
-    const uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wb[4] = {vb.x, vb.y, vb.z, vb.w};
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      unsigned short xa = (unsigned short)(wa[i >> 1] >> (16 * (i & 1)));
-      unsigned short xb = (unsigned short)(wb[i >> 1] >> (16 * (i & 1)));
-      if (dmask) {
-        xa = ((ka >> (8 * i + m)) & 1ull) ? f2bf(bf2f(xa) * inv_kp) : (unsigned short)0;
-        xb = ((kb >> (8 * i + m)) & 1ull) ? f2bf(bf2f(xb) * inv_kp) : (unsigned short)0;
+      uint32_t x[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t w = i < 2 ? v[r].x : i < 4 ? v[r].y : i < 6 ? v[r].z : v[r].w;
+        unsigned short h = (unsigned short)(w >> (16 * (i & 1)));
+        if (dmask) h = ((kb[r] >> (8 * i + m)) & 1ull) ? f2bf(bf2f(h) * inv_kp) : (unsigned short)0;
+        x[r] = h;
       }
-      nat32[((n0 + i) * L + t) * (H2 / 2) + col2] = (uint32_t)xa | ((uint32_t)xb << 16);
+      nat64[((n0 + i) * L + t) * (H2 / 4) + col4] = make_uint2(x[0] | (x[1] << 16), x[2] | (x[3] << 16));
     }
   }
   u16x8_t A[MT][NKS];
