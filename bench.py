@@ -44,6 +44,10 @@ def main():
     ap.add_argument("--word-dim", type=int, default=5, help="5 = reference train.py; paper config: --hidden 128 --word-dim 300")
     ap.add_argument("--profile-json", default="")
     ap.add_argument("--graph", type=int, default=0, help="capture the BiLSTM train step as a hipGraph (1/0)")
+    ap.add_argument("--mode", default="train", choices=["train", "eval"],
+                    help="eval: forward-only episodic evaluation (FewRel 2.0 style, dropout off, accuracy "
+                         "computed); a step = one batch of --episodes-per-gpu episodes (default 16384)")
+    ap.add_argument("--nota", type=float, default=0.0, help="eval: none-of-the-above query rate (FewRel 2.0)")
     args = ap.parse_args()
 
     import torch
@@ -57,11 +61,13 @@ def main():
     if world != args.gpus and dist.is_main:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     bert = args.encoder == "bert"
-    B = args.episodes_per_gpu or (8 if bert else 2048)
+    evalm = args.mode == "eval"
+    B = args.episodes_per_gpu or (8 if bert else (16384 if evalm else 2048))
     args.way = args.way or (10 if bert else 5)
     cfg = Config(N=args.way, K=args.shot, Q=args.query, max_length=37, hidden_size=args.hidden, dtype=args.dtype,
                  episodes_per_step=B, seed=1234, resume=False, model_dir="/tmp/ina_bench",
-                 train_iter=args.steps + args.warmup, use_hip_graph=bool(args.graph) and not bert)
+                 train_iter=args.steps + args.warmup, use_hip_graph=bool(args.graph) and not bert and not evalm,
+                 nota_rate=args.nota, eval_batch=B)
     if bert:
         cfg = cfg.replace(encoder="bert", bert_layers=args.bert_layers, bert_max_length=args.bert_len,
                           relation_head="reference")
@@ -79,15 +85,22 @@ def main():
         f["length"][:] = cfg.bert_max_length
         data.bert = f
     tr = Trainer(cfg, data, None, device="cuda", dist_ctx=dist, log=False)
+    if evalm:
+        tr.nota_threshold = 0.5 if args.nota > 0 else None
+
+        def step():
+            return tr.evaluate(B, batch=B), None
+    else:
+        step = tr.train_step_async
     for _ in range(args.warmup):
-        tr.train_step_async()
+        step()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     loss_t = None
     for _ in range(args.steps):
-        loss_t, _ = tr.train_step_async()
+        loss_t, _ = step()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
@@ -99,7 +112,7 @@ def main():
     value = episodes / dt
     if dist.is_main:
         out = {
-            "metric": "episodes/sec (whole node)",
+            "metric": "eval episodes/sec (whole node)" if evalm else "episodes/sec (whole node)",
             "value": round(value, 2),
             "unit": "episodes/s",
             "n_gpus": world,
@@ -123,8 +136,9 @@ def main():
                 "seq_len": cfg.bert_max_length if bert else 37,
                 "sentences_per_step_per_gpu": B * args.way * (args.shot + args.query),
                 "parallelism": f"dp{world}",
+                "mode": args.mode + (f", nota_rate={args.nota}" if evalm else ""),
             },
-            "final_loss": round(loss, 6),
+            ("eval_accuracy" if evalm else "final_loss"): round(loss, 6),
             "params_in_sync": bool(in_sync),
         }
         print(json.dumps(out))

@@ -158,7 +158,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, 
 
 // bf16 encoder forward in three launches: x_gather, lstm_fwd, hnat_attn (the LSTM output transpose +
 // dropout fused with the self-attention forward, attention.hip).  Returns lstm_fwd's outputs plus
-// attn_fwd's (e, alphas).  Callers check hnat_attn_ok first (else lstm_fwd + attn_fwd).
+// attn_fwd's (e, alphas).  Callers check hnat_attn_ok first (else lstm_fwd + attn_fwd).  With
+// store_c false (no backward) hnat is left unwritten.
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> lstm_attn_fwd(
     const Tensor& inst, const Tensor& word, const Tensor& pos1, const Tensor& pos2, const Tensor& wemb,
     const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U, int64_t NX,
@@ -196,8 +197,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> lstm_attn_fwd
   a.w2 = w2.data_ptr<float>();
   a.e = e.data_ptr<float>();
   a.alphas = alphas.data_ptr<float>();
+  // without a backward (store_c false) the natural rows are not needed: hnat is returned unwritten
   check_launch(ina::hnat_attn(hlane.data_ptr(), drop ? dmask.data_ptr<uint8_t>() : nullptr, (float)(1.0 / keep_prob),
-                              hnat.data_ptr(), a, (int)U, cur_stream()),
+                              store_c ? hnat.data_ptr() : nullptr, a, (int)U, cur_stream()),
                "hnat_attn");
   return {std::get<0>(r), std::get<1>(r), hnat, std::get<3>(r), std::get<4>(r), e, alphas};
 }

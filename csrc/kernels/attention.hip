@@ -385,8 +385,9 @@ __global__ __launch_bounds__(512) void hnat_attn_kernel(const unsigned short* __
       wj[m][r] = j < H2 ? w2[j] : 0.f;
     }
   __syncthreads();
-  // 2) the tile's rows are one contiguous run of hnat (padding rows of the last tile included)
-  {
+  // 2) the tile's rows are one contiguous run of hnat (padding rows of the last tile included);
+  //    skipped without a backward (hnat == nullptr: eval / serving)
+  if (hnat) {
     const uint4* ls = reinterpret_cast<const uint4*>(nat);
     uint4* dst = reinterpret_cast<uint4*>(hnat + (size_t)tile * 16 * L * H2);
     for (int i = threadIdx.x; i < 16 * L * H2 / 8; i += 512) dst[i] = ls[i];
