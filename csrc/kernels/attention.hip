@@ -105,11 +105,30 @@ INA_DEVICE void load_h(const typename FT<BF16>::elem* hraw, long seq, int tok, i
 // zero outside [L) x [2U)) and the mask ids of those tokens: projection (MFMA), tanh, w2 dot, masked
 // softmax over the tokens, pooling.  Shared by attn_fwd_kernel (H from global rows) and
 // hnat_attn_kernel (H from the LDS-transposed LSTM step records).
-template <int U, int NT>
+// Weight operands: register arrays (attn_fwd_kernel) or LDS (hnat_attn_kernel: registers kept for
+// occupancy), read through wa / wb / ww.
+template <int MT, int NKS>
+struct RegW {
+  const u16x8_t (&A)[MT][NKS];
+  const float (&bj)[MT][4];
+  const float (&wj)[MT][4];
+  INA_DEVICE u16x8_t wa(int m, int ks) const { return A[m][ks]; }
+  INA_DEVICE float wb(int m, int r) const { return bj[m][r]; }
+  INA_DEVICE float ww(int m, int r) const { return wj[m][r]; }
+};
+template <int MT, int NKS>
+struct LdsW {
+  const u16x8_t* lA;   // [MT * NKS][64]
+  const float* lbw;    // [b1 | w2], MT * 16 each
+  int lane, q;
+  INA_DEVICE u16x8_t wa(int m, int ks) const { return lA[(m * NKS + ks) * 64 + lane]; }
+  INA_DEVICE float wb(int m, int r) const { return lbw[16 * m + 4 * q + r]; }
+  INA_DEVICE float ww(int m, int r) const { return lbw[MT * 16 + 16 * m + 4 * q + r]; }
+};
+
+template <int U, int NT, typename W>
 INA_DEVICE void attn_sentence_bf16(const u16x8_t (&hf)[NT][AShape<U, NT, true>::NKS], const int (&mk)[NT],
-                                   const u16x8_t (&A)[AShape<U, NT, true>::MT][AShape<U, NT, true>::NKS],
-                                   const float (&bj)[AShape<U, NT, true>::MT][4],
-                                   const float (&wj)[AShape<U, NT, true>::MT][4], long s, int L, int q, int n,
+                                   const W& w, long s, int L, int q, int n,
                                    float* __restrict__ e_out, float* __restrict__ alphas) {
   using Sh = AShape<U, NT, true>;
   constexpr int H2 = Sh::H2, NKS = Sh::NKS, MT = Sh::MT;
@@ -118,13 +137,14 @@ INA_DEVICE void attn_sentence_bf16(const u16x8_t (&hf)[NT][AShape<U, NT, true>::
   for (int nt = 0; nt < NT; ++nt) {
     const int tok = 16 * nt + n;
     float sp = 0.f;
+    asm volatile("" ::: "memory");   // LdsW: re-read the weight fragments per token tile (no hoisting)
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      f32x4_t acc = {bj[m][0], bj[m][1], bj[m][2], bj[m][3]};
+      f32x4_t acc = {w.wb(m, 0), w.wb(m, 1), w.wb(m, 2), w.wb(m, 3)};
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) acc = mma(A[m][ks], hf[nt][ks], acc);
+      for (int ks = 0; ks < NKS; ++ks) acc = mma(w.wa(m, ks), hf[nt][ks], acc);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sp += wj[m][r] * tanhf_(acc[r]);
+      for (int r = 0; r < 4; ++r) sp += w.ww(m, r) * tanhf_(acc[r]);
     }
     sp = cross_group_sum(sp);
     const float m01 = mk[nt] > 0 ? 1.f : 0.f;
@@ -223,7 +243,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
         }
         mk[nt] = maskarr[row + (tv ? tok : L - 1)];
       }
-      attn_sentence_bf16<U, NT>(hf, mk, A, bj, wj, s, L, q, n, e_out, alphas);
+      attn_sentence_bf16<U, NT>(hf, mk, RegW<MT, NKS>{A, bj, wj}, s, L, q, n, e_out, alphas);
       continue;
     }
     // pass 1: scores (projection + tanh + w2 dot), one token tile at a time
@@ -309,7 +329,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
 // re-read of the natural rows (default 5w5s, 2048 episodes) and a launch.
 // ------------------------------------------------------------------------------------------
 template <int U, int NT>
-__global__ __launch_bounds__(512) void hnat_attn_kernel(const unsigned short* __restrict__ rec,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NT <= 3 ? 6 : 4))) void hnat_attn_kernel(const unsigned short* __restrict__ rec,
                                                         const unsigned char* __restrict__ dmask, int S, int L,
                                                         float inv_kp, unsigned short* __restrict__ hnat,
                                                         const int* __restrict__ inst, const int* __restrict__ maskarr,
@@ -370,20 +390,14 @@ __global__ __launch_bounds__(512) void hnat_attn_kernel(const unsigned short* __
       nat64[((n0 + i) * L + t) * (H2 / 4) + col4] = make_uint2(x[0] | (x[1] << 16), x[2] | (x[3] << 16));
     }
   }
-  u16x8_t A[MT][NKS];
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) A[m][ks] = w1pack[(m * NKS + ks) * 64 + lane];
-  float bj[MT][4], wj[MT][4];
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int j = 16 * m + 4 * q + r;
-      bj[m][r] = j < H2 ? b1[j] : 0.f;
-      wj[m][r] = j < H2 ? w2[j] : 0.f;
-    }
+  // W1 fragments and b1 / w2 staged in LDS (read per sentence: registers stay free for occupancy)
+  u16x8_t* lA = reinterpret_cast<u16x8_t*>(nat + 16 * L * H2);          // [MT * NKS][64]
+  float* lbw = reinterpret_cast<float*>(lA + MT * NKS * 64);             // [b1 | w2], MT * 16 each
+  for (int i = threadIdx.x; i < MT * NKS * 64; i += 512) lA[i] = w1pack[i];
+  for (int i = threadIdx.x; i < MT * 16; i += 512) {
+    lbw[i] = i < H2 ? b1[i] : 0.f;
+    lbw[MT * 16 + i] = i < H2 ? w2[i] : 0.f;
+  }
   __syncthreads();
   // 2) the tile's rows are one contiguous run of hnat (padding rows of the last tile included);
   //    skipped without a backward (hnat == nullptr: eval / serving)
@@ -392,8 +406,9 @@ __global__ __launch_bounds__(512) void hnat_attn_kernel(const unsigned short* __
     uint4* dst = reinterpret_cast<uint4*>(hnat + (size_t)tile * 16 * L * H2);
     for (int i = threadIdx.x; i < 16 * L * H2 / 8; i += 512) dst[i] = ls[i];
   }
-  // 3) attention forward, 2 sentences per wave (unrolled: mk stays in registers)
-#pragma unroll
+  // 3) attention forward, 2 sentences per wave (not unrolled; the sentence's mask ids are picked with
+  //    selects, so mk stays in registers)
+#pragma unroll 1
   for (int j = 0; j < 2; ++j) {
     const int n = wave * 2 + j;
     const long s = (long)tile * 16 + n;
@@ -412,7 +427,10 @@ __global__ __launch_bounds__(512) void hnat_attn_kernel(const unsigned short* __
         hf[nt][ks] = ok ? v : u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
       }
     }
-    attn_sentence_bf16<U, NT>(hf, mk[j], A, bj, wj, s, L, q, nl, e_out, alphas);
+    int mkj[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) mkj[nt] = j == 0 ? mk[0][nt] : mk[1][nt];
+    attn_sentence_bf16<U, NT>(hf, mkj, LdsW<MT, NKS>{lA, lbw, lane, q}, s, L, q, nl, e_out, alphas);
   }
 }
 
@@ -962,7 +980,10 @@ static int attn_bwd_t(const AttnArgs& a, hipStream_t st) {
   }                                           \
   return -1;
 
-size_t hnat_attn_lds_bytes(int U, int L, bool) { return (size_t)16 * L * 2 * U * 2; }
+size_t hnat_attn_lds_bytes(int U, int L, bool) {
+  const int H2 = 2 * U, MT = (H2 + 15) / 16, NKS = (H2 + 31) / 32;
+  return (size_t)16 * L * H2 * 2 + (size_t)MT * NKS * 64 * 16 + (size_t)2 * MT * 16 * 4;
+}
 
 template <int U, int NT>
 static int hnat_attn_t(const void* rec, const unsigned char* dmask, float inv_kp, void* hnat, const AttnArgs& a,
