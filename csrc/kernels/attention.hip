@@ -328,6 +328,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
 // LDS = the natural rows only (47 KB at L=37, u=20): 2 workgroups per CU.  Saves attn_fwd's 303 MB
 // re-read of the natural rows (default 5w5s, 2048 episodes) and a launch.
 // ------------------------------------------------------------------------------------------
+#ifndef INA_HA_PHASES
+#define INA_HA_PHASES 7   // timing experiments: bit 0 transpose, bit 1 natural-row write, bit 2 attention
+#endif
 template <int U, int NT>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NT <= 3 ? 6 : 4))) void hnat_attn_kernel(const unsigned short* __restrict__ rec,
                                                         const unsigned char* __restrict__ dmask, int S, int L,
@@ -362,7 +365,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NT <= 3 ? 6
   // (column d * U + 4m: 8-B aligned since U % 4 == 0)
   const int nit = 2 * L * U4 * 2;
   uint2* nat64 = reinterpret_cast<uint2*>(nat);
-  for (int c = threadIdx.x; c < nit; c += 512) {
+  for (int c = threadIdx.x; c < ((INA_HA_PHASES & 1) ? nit : 0); c += 512) {
     const int k = c / (U4 * 2), pc = c - k * (U4 * 2);   // k = dir * L + t
     const int m = pc >> 1, n0 = (pc & 1) * 8;
     const uint4* sk = src + (size_t)k * 2 * CPP + m * 8 + (n0 >> 3);   // h slot of record k
@@ -401,7 +404,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NT <= 3 ? 6
   __syncthreads();
   // 2) the tile's rows are one contiguous run of hnat (padding rows of the last tile included);
   //    skipped without a backward (hnat == nullptr: eval / serving)
-  if (hnat) {
+  if ((INA_HA_PHASES & 2) && hnat) {
     const uint4* ls = reinterpret_cast<const uint4*>(nat);
     uint4* dst = reinterpret_cast<uint4*>(hnat + (size_t)tile * 16 * L * H2);
     for (int i = threadIdx.x; i < 16 * L * H2 / 8; i += 512) dst[i] = ls[i];
@@ -412,7 +415,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NT <= 3 ? 6
   for (int j = 0; j < 2; ++j) {
     const int n = wave * 2 + j;
     const long s = (long)tile * 16 + n;
-    if (s >= S) break;   // wave-uniform
+    if (s >= S || !(INA_HA_PHASES & 4)) break;   // wave-uniform
     u16x8_t hf[NT][NKS];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
