@@ -41,6 +41,14 @@ const int* dev_int(const std::optional<Tensor>& t, const char* name) {
   return t->data_ptr<int>();
 }
 
+// the optimizer's device skip counter, required together with a guard flag
+int* guard_skips(const std::optional<Tensor>& guard, const std::optional<Tensor>& skips) {
+  if (!guard.has_value() || !guard->defined() || guard->numel() == 0) return nullptr;
+  TORCH_CHECK(skips.has_value() && skips->defined() && skips->numel() >= 1, "ina: a guard flag needs a skip counter");
+  check(*skips, "skips", at::kInt);
+  return skips->data_ptr<int>();
+}
+
 int64_t frag_elems(bool bf16) { return bf16 ? 8 : 1; }
 uint32_t keep_threshold(double kp) {
   const double t = kp * 4294967296.0;
@@ -545,7 +553,8 @@ std::tuple<Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tensor& e, c
 
 // ------------------------------------------------------------------ optim / misc
 void adam_step(Tensor p, Tensor m, Tensor v, const Tensor& g, const std::optional<Tensor>& l2mask, double lr_t,
-               double b1, double b2, double eps, double gscale, double l2, const std::optional<Tensor>& lr_dev) {
+               double b1, double b2, double eps, double gscale, double l2, const std::optional<Tensor>& lr_dev,
+               const std::optional<Tensor>& guard, const std::optional<Tensor>& skips) {
   check(p, "p", at::kFloat);
   check(m, "m", at::kFloat);
   check(v, "v", at::kFloat);
@@ -561,12 +570,14 @@ void adam_step(Tensor p, Tensor m, Tensor v, const Tensor& g, const std::optiona
   if (n == 0) return;
   check_launch(ina::adam_step(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), g.data_ptr<float>(), mk, n,
                               (float)lr_t, (float)b1, (float)b2, (float)eps, (float)gscale, (float)l2,
-                              dev_float(lr_dev, "lr_dev"), cur_stream()),
+                              dev_float(lr_dev, "lr_dev"), dev_float(guard, "guard"), guard_skips(guard, skips),
+                              cur_stream()),
                "adam_step");
 }
 
 void adagrad_step(Tensor p, Tensor acc, const Tensor& g, const std::optional<Tensor>& l2mask, double lr, double gscale,
-                  double l2, const std::optional<Tensor>& lr_dev) {
+                  double l2, const std::optional<Tensor>& lr_dev, const std::optional<Tensor>& guard,
+                  const std::optional<Tensor>& skips) {
   check(p, "p", at::kFloat);
   check(acc, "acc", at::kFloat);
   check(g, "g", at::kFloat);
@@ -579,8 +590,21 @@ void adagrad_step(Tensor p, Tensor acc, const Tensor& g, const std::optional<Ten
   }
   if (n == 0) return;
   check_launch(ina::adagrad_step(p.data_ptr<float>(), acc.data_ptr<float>(), g.data_ptr<float>(), mk, n, (float)lr,
-                                 (float)gscale, (float)l2, dev_float(lr_dev, "lr_dev"), cur_stream()),
+                                 (float)gscale, (float)l2, dev_float(lr_dev, "lr_dev"), dev_float(guard, "guard"),
+                                 guard_skips(guard, skips), cur_stream()),
                "adagrad_step");
+}
+
+// NaN/Inf guard: flag[0] = 1 when any element of g (or the loss scalar) is not finite; flag must be 0
+// before (it is the zeroed tail of the flat gradient buffer, ops/optim.py::FlatParams)
+void nonfinite_flag(const Tensor& g, const std::optional<Tensor>& loss, Tensor flag) {
+  check(g, "g", at::kFloat);
+  check(flag, "flag", at::kFloat);
+  TORCH_CHECK(flag.numel() >= 1, "ina.nonfinite_flag: flag needs 1 float");
+  const float* lp = dev_float(loss, "loss");
+  if (g.numel() == 0 && lp == nullptr) return;
+  check_launch(ina::nonfinite_flag(g.data_ptr<float>(), g.numel(), lp, flag.data_ptr<float>(), cur_stream()),
+               "nonfinite_flag");
 }
 
 void slab_reduce(const Tensor& slabs, Tensor out, bool accumulate) {
@@ -622,7 +646,7 @@ void step_control(Tensor ctl, Tensor lrt, int64_t seedA, int64_t seedB, double l
                "step_control");
 }
 
-int64_t abi_version() { return 3; }
+int64_t abi_version() { return 4; }
 
 }  // namespace
 
@@ -640,6 +664,7 @@ TORCH_LIBRARY(ina, m) {
   m.def("ntn_bwd", &ntn_bwd);
   m.def("adam_step", &adam_step);
   m.def("adagrad_step", &adagrad_step);
+  m.def("nonfinite_flag", &nonfinite_flag);
   m.def("slab_reduce", &slab_reduce);
   m.def("sample_episodes", &sample_episodes);
   m.def("step_control", &step_control);

@@ -131,9 +131,11 @@ int slab_scatter(const SlabJobs& jobs, float* dst, float* ws, hipStream_t st);
 int ntn_bwd(const NtnArgs& a, hipStream_t st);
 
 int adam_step(float* p, float* m, float* v, const float* g, const unsigned char* l2mask, long n, float lr_t, float b1,
-              float b2, float eps, float gscale, float l2, const float* lr_dev, hipStream_t st);
+              float b2, float eps, float gscale, float l2, const float* lr_dev, const float* guard, int* skips,
+              hipStream_t st);
 int adagrad_step(float* p, float* acc, const float* g, const unsigned char* l2mask, long n, float lr, float gscale,
-                 float l2, const float* lr_dev, hipStream_t st);
+                 float l2, const float* lr_dev, const float* guard, int* skips, hipStream_t st);
+int nonfinite_flag(const float* g, long n, const float* loss, float* flag, hipStream_t st);
 int step_control(int* ctl, float* lrt, long long seedA, long long seedB, double lr0, double decay_steps,
                  double decay_rate, int staircase, int constant, int adam, double b1, double b2, hipStream_t st);
 int slab_reduce(const float* slabs, long nslab, long len, float* out, int accumulate, hipStream_t st);

@@ -6,12 +6,39 @@
 //   m = b1 m + (1 - b1) g ;  v = b2 v + (1 - b2) g^2 ;  p -= lr_t * m / (sqrt(v) + eps)
 // Optional L2 (the reference's dead L2 term, opt-in): g += l2 * p where l2mask[i] != 0.
 // Adagrad (the paper's optimizer, TF1 form): acc += g^2 ; p -= lr * g / sqrt(acc).
+// NaN/Inf guard: nonfinite_flag_kernel sets *flag when any gradient (or the loss) is not finite; the
+// optimizer kernels then leave parameters and moments untouched and count the skip on the device
+// (no host synchronisation, works inside a captured hipGraph).  The flag lives in the tail of the
+// flat gradient buffer, so the per-step gradient zeroing clears it.
 #include "ina_common.h"
+
+__global__ __launch_bounds__(256) void nonfinite_flag_kernel(const float* __restrict__ g, long n,
+                                                             const float* __restrict__ loss, float* __restrict__ flag) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  bool bad = false;
+  const long n4 = n >> 2;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (long i = t0; i < n4; i += stride) {
+    const float4 x = g4[i];
+    // |x| <= FLT_MAX is false for NaN and +-Inf
+    bad |= !(fabsf(x.x) <= 3.402823466e38f) | !(fabsf(x.y) <= 3.402823466e38f) |
+           !(fabsf(x.z) <= 3.402823466e38f) | !(fabsf(x.w) <= 3.402823466e38f);
+  }
+  for (long i = (n4 << 2) + t0; i < n; i += stride) bad |= !(fabsf(g[i]) <= 3.402823466e38f);
+  if (loss && t0 == 0) bad |= !(fabsf(loss[0]) <= 3.402823466e38f);
+  if (bad) flag[0] = 1.f;   // benign race: every writer stores the same value
+}
 
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                                                    const float* __restrict__ g, const unsigned char* __restrict__ l2mask,
                                                    long n, float lr_t, float b1, float b2, float eps, float gscale,
-                                                   float l2, const float* __restrict__ lr_dev) {
+                                                   float l2, const float* __restrict__ lr_dev,
+                                                   const float* __restrict__ guard, int* __restrict__ skips) {
+  if (guard && guard[0] != 0.f) {   // non-finite step: no update; block 0 counts it
+    if (blockIdx.x == 0 && threadIdx.x == 0) skips[0] = skips[0] + 1;
+    return;
+  }
   if (lr_dev) lr_t = lr_dev[0];   // device-resident schedule (HIP-graph replay)
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -29,7 +56,12 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
 __global__ __launch_bounds__(256) void adagrad_kernel(float* __restrict__ p, float* __restrict__ acc,
                                                       const float* __restrict__ g,
                                                       const unsigned char* __restrict__ l2mask, long n, float lr,
-                                                      float gscale, float l2, const float* __restrict__ lr_dev) {
+                                                      float gscale, float l2, const float* __restrict__ lr_dev,
+                                                      const float* __restrict__ guard, int* __restrict__ skips) {
+  if (guard && guard[0] != 0.f) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) skips[0] = skips[0] + 1;
+    return;
+  }
   if (lr_dev) lr = lr_dev[0];
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -89,16 +121,26 @@ static int grid_for(long n) {
 }
 
 int adam_step(float* p, float* m, float* v, const float* g, const unsigned char* l2mask, long n, float lr_t, float b1,
-              float b2, float eps, float gscale, float l2, const float* lr_dev, hipStream_t st) {
+              float b2, float eps, float gscale, float l2, const float* lr_dev, const float* guard, int* skips,
+              hipStream_t st) {
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, m, v, g, l2mask, n, lr_t, b1, b2, eps, gscale,
-                     l2, lr_dev);
+                     l2, lr_dev, guard, skips);
   INA_CHECK_LAUNCH();
   return 0;
 }
 
 int adagrad_step(float* p, float* acc, const float* g, const unsigned char* l2mask, long n, float lr, float gscale,
-                 float l2, const float* lr_dev, hipStream_t st) {
-  hipLaunchKernelGGL(adagrad_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, acc, g, l2mask, n, lr, gscale, l2, lr_dev);
+                 float l2, const float* lr_dev, const float* guard, int* skips, hipStream_t st) {
+  hipLaunchKernelGGL(adagrad_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, acc, g, l2mask, n, lr, gscale, l2, lr_dev,
+                     guard, skips);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int nonfinite_flag(const float* g, long n, const float* loss, float* flag, hipStream_t st) {
+  long b = (n / 4 + 255) / 256;
+  b = b < 1 ? 1 : (b > 512 ? 512 : b);
+  hipLaunchKernelGGL(nonfinite_flag_kernel, dim3((int)b), dim3(256), 0, st, g, n, loss, flag);
   INA_CHECK_LAUNCH();
   return 0;
 }

@@ -33,17 +33,22 @@ def main(argv=None):
     p.add_argument("--settings", default="", help="comma list of N-K (default: the config's eval N/K)")
     p.add_argument("--nota_rates", default="0")
     p.add_argument("--iters", type=int, default=1000)
+    p.add_argument("--checkpoint", default="best", choices=["best", "latest"],
+                   help="best-val checkpoint (falls back to the latest) or the latest one")
     args = p.parse_args(argv)
     base = Config()
-    stem = ckpt.latest(args.model_dir or base.model_dir)
+    md = args.model_dir or base.model_dir
+    stem = (ckpt.best(md) if args.checkpoint == "best" else None) or ckpt.latest(md)
     if stem is not None:
         _, meta = ckpt.load(stem)
         base = Config.from_dict(meta.get("config", {}))
-    cfg = config_from_args(args, base).replace(resume=True, episodes_per_step=max(1, base.episodes_per_step))
+    cfg = config_from_args(args, base).replace(resume=False, episodes_per_step=max(1, base.episodes_per_step))
     tr_data, va_data = T.load_data(cfg, args)
     te = T.load_test(cfg, tr_data) if cfg.test_file else va_data
     trainer = Trainer(cfg, tr_data, va_data, device=cfg.device, log=False)
-    if stem is None:
+    if stem is not None:
+        trainer.load(stem)
+    else:
         print(json.dumps({"warning": "no checkpoint found; evaluating the random init"}), file=sys.stderr)
     settings = ([tuple(int(x) for x in s.split("-")) for s in args.settings.split(",") if s]
                 or [(cfg.eN, cfg.eK)])

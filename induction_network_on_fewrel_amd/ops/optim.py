@@ -47,7 +47,11 @@ class FlatParams:
         self.numel = off
         dev = self.params[0].device if self.params else torch.device("cpu")
         self.flat = torch.zeros(self.numel, dtype=torch.float32, device=dev)
-        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        # gradient storage = [grad (numel) | pad | NaN/Inf guard flag]: zero_grad clears the flag with the
+        # gradients in one fill (the flag word sits 16-B aligned behind the last gradient)
+        self._gstore = torch.zeros(self.numel + 8 - self.numel % 4, dtype=torch.float32, device=dev)
+        self.grad = self._gstore[:self.numel]
+        self.guard = self._gstore[-1:]
         with torch.no_grad():
             for p, o, n in zip(self.params, self.offsets, self.numels):
                 self.flat[o:o + n].copy_(p.detach().reshape(-1))
@@ -59,7 +63,7 @@ class FlatParams:
         return buf[self.offsets[i]:self.offsets[i] + self.numels[i]].view(self.shapes[i])
 
     def zero_grad(self) -> None:
-        self.grad.zero_()
+        self._gstore.zero_()
         # autograd may have replaced .grad with a fresh tensor (e.g. when a grad was None); re-home
         for p, o, n in zip(self.params, self.offsets, self.numels):
             g = p.grad
@@ -93,8 +97,10 @@ class FusedOptimizer:
         self.b1, self.b2, self.eps = beta1, beta2, eps
         self.l2 = float(l2)
         self.l2_mask = l2_mask if (l2_mask is not None and self.l2 > 0) else None
-        self.t = 0  # number of applied updates (TF's beta powers = beta^t)
+        self.t = 0  # number of optimizer steps (TF's beta powers = beta^t)
         dev = flat.flat.device
+        self.skips_host = 0   # steps skipped by the NaN/Inf guard (CPU path + restored from a checkpoint)
+        self.skips_dev = torch.zeros(1, dtype=torch.int32, device=dev) if dev.type == "cuda" else None
         if kind == "adam":
             self.m = torch.zeros(flat.numel, dtype=torch.float32, device=dev)
             self.v = torch.zeros(flat.numel, dtype=torch.float32, device=dev)
@@ -108,19 +114,43 @@ class FusedOptimizer:
             return {"m": self.m, "v": self.v}
         return {"acc": self.acc}
 
-    def step(self, lr: float, grad_scale: float = 1.0, lr_dev: Optional[torch.Tensor] = None) -> None:
+    def skipped(self) -> int:
+        """Steps the NaN/Inf guard skipped so far (reads the device counter: synchronises)."""
+        return self.skips_host + (int(self.skips_dev.item()) if self.skips_dev is not None else 0)
+
+    def set_skipped(self, n: int) -> None:
+        self.skips_host = int(n)
+        if self.skips_dev is not None:
+            self.skips_dev.zero_()
+
+    def step(self, lr: float, grad_scale: float = 1.0, lr_dev: Optional[torch.Tensor] = None,
+             check_finite: bool = False, loss: Optional[torch.Tensor] = None) -> None:
         """``lr_dev``: device scalar holding the (bias-corrected for Adam) rate, overriding ``lr``
-        (HIP-graph replay: written by ina.step_control inside the captured step)."""
+        (HIP-graph replay: written by ina.step_control inside the captured step).
+
+        ``check_finite``: skip the whole update (parameters and moments untouched) when any gradient
+        -- or ``loss``, a scalar -- is NaN/Inf.  On the GPU the decision is made on the device
+        (``ina.nonfinite_flag`` -> guard word in the gradient buffer tail -> the optimizer kernel), so
+        the step stays asynchronous / graph-capturable; skips are counted in ``skips_dev``.  Under DP
+        pass the all-reduced gradients and no loss, so every rank takes the same decision."""
         self.t += 1
         p, g = self.flat.flat, self.flat.grad
         if p.is_cuda:
             o = ops()
+            guard = None
+            if check_finite:
+                guard = self.flat.guard
+                o.nonfinite_flag(g, loss.detach().reshape(1).float() if loss is not None else None, guard)
             if self.kind == "adam":
                 lr_t = lr * math.sqrt(1 - self.b2 ** self.t) / (1 - self.b1 ** self.t)
                 o.adam_step(p, self.m, self.v, g, self.l2_mask, lr_t, self.b1, self.b2, self.eps, grad_scale, self.l2,
-                            lr_dev)
+                            lr_dev, guard, self.skips_dev)
             else:
-                o.adagrad_step(p, self.acc, g, self.l2_mask, lr, grad_scale, self.l2, lr_dev)
+                o.adagrad_step(p, self.acc, g, self.l2_mask, lr, grad_scale, self.l2, lr_dev, guard, self.skips_dev)
+            return
+        if check_finite and (not bool(torch.isfinite(g).all())
+                             or (loss is not None and not bool(torch.isfinite(loss.detach()).all()))):
+            self.skips_host += 1
             return
         with torch.no_grad():
             gg = g * grad_scale

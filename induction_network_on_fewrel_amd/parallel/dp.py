@@ -109,6 +109,14 @@ class DistContext:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return [float(v) / self.world for v in t.tolist()]
 
+    def all_gather_objects(self, obj) -> list:
+        """Every rank's ``obj`` (picklable, small), in rank order, on every rank."""
+        if not self.initialized:
+            return [obj]
+        out = [None] * self.world
+        dist.all_gather_object(out, obj)
+        return out
+
     def params_in_sync(self, flat: torch.Tensor) -> bool:
         """Max-abs difference of the flat parameters across ranks is zero."""
         if not self.initialized:

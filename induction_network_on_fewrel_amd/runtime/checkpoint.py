@@ -55,8 +55,25 @@ def _write_state(model_dir: str, latest: str, allp) -> None:
             fh.write(f'all_model_checkpoint_paths: "{p}"\n')
 
 
+def _best_file(model_dir: str) -> str:
+    return os.path.join(ckpt_dir(model_dir), "best_checkpoint")
+
+
+def best_stem(model_dir: str) -> Optional[str]:
+    """Stem recorded by the last ``save(..., best=True)`` (kept out of the max_to_keep rotation)."""
+    f = _best_file(model_dir)
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        m = re.match(r'\s*model_checkpoint_path:\s*"(.*)"', fh.read())
+    return m.group(1) if m else None
+
+
 def save(model_dir: str, name: str, step: int, tensors: "OrderedDict[str, torch.Tensor]", meta: dict,
-         max_to_keep: int = 5) -> str:
+         max_to_keep: int = 5, best: bool = False) -> str:
+    """Write ``<model_dir>/checkpoint/<name>-<step>`` and rotate to ``max_to_keep``.  ``best=True`` also
+    points ``best_checkpoint`` at it; the best checkpoint is never rotated away (a periodic or resumed
+    checkpoint can be newer, so "latest" is not "best")."""
     d = ckpt_dir(model_dir)
     os.makedirs(d, exist_ok=True)
     stem = f"{name}-{step}"
@@ -69,10 +86,17 @@ def save(model_dir: str, name: str, step: int, tensors: "OrderedDict[str, torch.
                             for k, v in cpu.items()})
     with open(os.path.join(d, stem + ".index.json"), "w") as fh:
         json.dump(index, fh, indent=1, sort_keys=True)
+    if best:
+        with open(_best_file(model_dir) + ".tmp", "w") as fh:
+            fh.write(f'model_checkpoint_path: "{stem}"\n')
+        os.replace(_best_file(model_dir) + ".tmp", _best_file(model_dir))
+    keep = best_stem(model_dir)
     _, allp = read_state(model_dir)
     allp = [p for p in allp if p != stem] + [stem]
     while len(allp) > max_to_keep:
         old = allp.pop(0)
+        if old == keep:
+            continue   # dropped from the rotation list, file kept
         for ext in (".safetensors", ".index.json"):
             try:
                 os.remove(os.path.join(d, old + ext))
@@ -84,6 +108,15 @@ def save(model_dir: str, name: str, step: int, tensors: "OrderedDict[str, torch.
 
 def latest(model_dir: str) -> Optional[str]:
     stem, _ = read_state(model_dir)
+    if stem is None:
+        return None
+    p = os.path.join(ckpt_dir(model_dir), stem)
+    return p if os.path.exists(p + ".safetensors") else None
+
+
+def best(model_dir: str) -> Optional[str]:
+    """Path stem of the best-val checkpoint, if one was recorded and still exists."""
+    stem = best_stem(model_dir)
     if stem is None:
         return None
     p = os.path.join(ckpt_dir(model_dir), stem)

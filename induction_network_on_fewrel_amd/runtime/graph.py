@@ -73,14 +73,14 @@ class GraphedTrainStep:
             tr.glue.flush()
         tr.flat.sync_grads_into_flat()
         if self.with_opt:
-            tr.opt.step(0.0, grad_scale=1.0, lr_dev=self.lrt[0:1])
+            tr.opt.step(0.0, grad_scale=1.0, lr_dev=self.lrt[0:1], check_finite=cfg.grad_check_finite, loss=loss)
         return loss.detach(), acc
 
     def _after_eager_or_replay(self):
         tr = self.tr
         if not self.with_opt:
             tr.dist.allreduce_buckets_(tr.flat.grad)
-            tr.opt.step(0.0, grad_scale=1.0 / tr.dist.world, lr_dev=self.lrt[0:1])
+            tr.opt.step(0.0, grad_scale=1.0 / tr.dist.world, lr_dev=self.lrt[0:1], check_finite=tr.cfg.grad_check_finite)
         tr.global_step += 1
 
     def step(self):

@@ -12,7 +12,6 @@ NaN/Inf loss guard; per-phase timers; JSONL + TensorBoard metrics; no per-step t
 from __future__ import annotations
 
 import faulthandler
-import math
 import os
 import sys
 import time
@@ -95,7 +94,6 @@ class Trainer:
                                   l2_mask=self.flat.l2_mask(l2_names) if cfg.use_l2 else None)
         self.global_step = 0
         self.best_acc = 0.0
-        self.skipped_steps = 0
         rank_seed = cfg.seed * 1009 + 7919 * self.dist.rank
         self.train_eps = self._make_sampler(train_data, rank_seed, cfg.nota_rate)
         self.eval_nota = cfg.nota_rate if cfg.eval_nota_rate < 0 else cfg.eval_nota_rate
@@ -149,6 +147,11 @@ class Trainer:
                 self.gpu_phase_ms[k] += a.elapsed_time(b)
         self._pending_events = []
         return dict(self.gpu_phase_ms)
+
+    @property
+    def skipped_steps(self) -> int:
+        """Optimizer steps skipped by the NaN/Inf guard (synchronises on the GPU)."""
+        return self.opt.skipped()
 
     def dropout_seed(self) -> int:
         return (self.cfg.seed * 2654435761 + self.global_step * 97 + self.dist.rank * 7919) & 0x7FFFFFFF
@@ -210,10 +213,10 @@ class Trainer:
         t3 = time.perf_counter()
         lr = lr_at(self.global_step, cfg.learning_rate, cfg.decay_steps, cfg.decay_rate, cfg.staircase,
                    cfg.lr_schedule)
-        if cfg.grad_check_finite and self.device.type != "cuda" and not math.isfinite(float(loss.detach())):
-            self.skipped_steps += 1   # CPU path: exact skip (the GPU path checks when it logs, see train())
-        else:
-            self.opt.step(lr, grad_scale=1.0 / self.dist.world)
+        # NaN/Inf guard: the update is skipped on the device when a gradient / the loss is not finite
+        # (DP: only the all-reduced gradients are checked, so every rank takes the same decision)
+        self.opt.step(lr, grad_scale=1.0 / self.dist.world, check_finite=cfg.grad_check_finite,
+                      loss=loss if self.dist.world == 1 else None)
         self.global_step += 1
         e4 = self._sync()
         if e0 is not None:
@@ -258,6 +261,7 @@ class Trainer:
         t_start = time.time()
         pend_loss = pend_acc = None
         pend_n = 0
+        seen_skips = self.skipped_steps if cfg.grad_check_finite else 0
         if cfg.watchdog_s > 0:
             self.log.print(f"watchdog: abort if a step exceeds {cfg.watchdog_s:.0f}s")
         for it in range(start, cfg.train_iter):
@@ -266,16 +270,21 @@ class Trainer:
             loss_t, acc_t = self.train_step_async()
             if cfg.save_every > 0 and self.global_step % cfg.save_every == 0:
                 self.save()
-            # accumulate on device; the host only synchronises at log / reset / eval points
-            pend_loss = loss_t if pend_loss is None else pend_loss + loss_t
-            pend_acc = acc_t if pend_acc is None else pend_acc + acc_t
+            # accumulate on device; the host only synchronises at log / reset / eval points.  The first
+            # term is cloned: with use_hip_graph loss_t/acc_t are the graph's static outputs, which the
+            # next replay overwrites
+            pend_loss = loss_t.clone() if pend_loss is None else pend_loss + loss_t
+            pend_acc = acc_t.clone() if pend_acc is None else pend_acc + acc_t
             pend_n += 1
             if (it % cfg.log_every == 0 or it % cfg.val_step == 0 or (it + 1) % cfg.val_step == 0
                     or it + 1 == cfg.train_iter):
                 pl, pa = float(pend_loss), float(pend_acc)
-                if cfg.grad_check_finite and not math.isfinite(pl):
-                    self.skipped_steps += 1
-                    self.log.print(f"[warn] non-finite loss around step {it + 1}")
+                if cfg.grad_check_finite:
+                    sk = self.skipped_steps
+                    if sk > seen_skips:
+                        self.log.print(f"[warn] {sk - seen_skips} step(s) with non-finite gradients/loss up to step "
+                                       f"{it + 1}: update skipped (parameters and optimizer moments unchanged)")
+                        seen_skips = sk
                 it_loss += pl
                 it_acc += pa
                 it_n += pend_n
@@ -304,13 +313,13 @@ class Trainer:
                 if acc_val > self.best_acc:
                     self.best_acc = acc_val
                     self.log.print(f"Best checkpoint.[EVAL] accuracy :{acc_val}")
-                    self.save()
+                    self.save(best=True)
         if cfg.watchdog_s > 0:
             faulthandler.cancel_dump_traceback_later()
         self.log.print("\n####################\n")
         self.log.print("Finish training :" + cfg.ckpt_name)
         if cfg.test_best and self.best_acc > 0.0:
-            best = ckpt.latest(cfg.model_dir)   # saved only on improvement -> latest = best
+            best = ckpt.best(cfg.model_dir)   # the best-val pointer, not the newest (periodic) checkpoint
             if best is not None:
                 step = self.global_step
                 self.load(best)
@@ -354,14 +363,17 @@ class Trainer:
         out["global_step"] = torch.tensor(self.global_step, dtype=torch.int64)
         return out
 
-    def save(self) -> Optional[str]:
+    def save(self, best: bool = False) -> Optional[str]:
+        """Collective under DP (every rank calls it at the same step): each rank's own sampler state is
+        gathered, then rank 0 writes.  ``best``: this is the best-val checkpoint (``test_best``)."""
+        samplers = self.dist.all_gather_objects(self.train_eps.state_dict())
+        skipped = self.skipped_steps
         if not self.dist.is_main:
             return None
         meta = {"best_acc": self.best_acc, "optimizer_t": self.opt.t, "config": self.cfg.to_dict(),
-                "train_sampler": self.train_eps.state_dict(), "skipped_steps": self.skipped_steps,
-                "world_size": self.dist.world}
+                "train_samplers": samplers, "skipped_steps": skipped, "world_size": self.dist.world}
         return ckpt.save(self.cfg.model_dir, self.cfg.ckpt_name, self.global_step, self.state_tensors(), meta,
-                         self.cfg.max_to_keep)
+                         self.cfg.max_to_keep, best=best)
 
     def load(self, stem: str) -> None:
         tensors, meta = ckpt.load(stem)
@@ -379,14 +391,26 @@ class Trainer:
         self.global_step = int(tensors["global_step"].item()) if "global_step" in tensors else int(meta["global_step"])
         self.opt.t = int(meta.get("optimizer_t", self.global_step))
         self.best_acc = float(meta.get("best_acc", 0.0))
-        self.skipped_steps = int(meta.get("skipped_steps", 0))
-        if "train_sampler" in meta and meta.get("world_size", 1) == self.dist.world:
-            try:
-                self.train_eps.load_state_dict(meta["train_sampler"])
-            except Exception:
-                pass
+        self.opt.set_skipped(int(meta.get("skipped_steps", 0)))
+        self._restore_sampler(meta)
         if self.dist.world > 1:
             self.dist.broadcast_(self.flat.flat, 0)
+
+    def _restore_sampler(self, meta: dict) -> None:
+        """Each rank restores ITS OWN sampler state (rank-folded seed), so the DP ranks keep drawing
+        different episodes after a restart.  With a different world size the per-rank streams do not
+        map onto the new ranks: keep the fresh rank-folded seeds and only carry the call counter of the
+        device sampler forward (new episodes, no replay of the pre-restart ones)."""
+        states = meta.get("train_samplers")
+        if states is None:   # older single-state checkpoints: rank 0's state -> counter only
+            states = [meta["train_sampler"]] if "train_sampler" in meta else []
+            same_world = False
+        else:
+            same_world = len(states) == self.dist.world
+        if same_world:
+            self.train_eps.load_state_dict(states[self.dist.rank])
+        elif states and "calls" in states[0] and hasattr(self.train_eps, "calls"):
+            self.train_eps.calls = int(states[0]["calls"])
 
     def maybe_resume(self) -> bool:
         stem = ckpt.latest(self.cfg.model_dir)

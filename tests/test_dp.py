@@ -59,6 +59,43 @@ def _worker(rank, world, port, out_dir):
     dist.destroy()
 
 
+def _resume_worker(rank, world, port, out_dir):
+    """Save (collective) after 2 steps, continue 1 step, then a fresh trainer resumes from the
+    checkpoint: every rank must continue ITS OWN episode stream (advisor finding: rank 0's sampler
+    state used to be loaded on every rank, collapsing DP to one rank's episodes)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from induction_network_on_fewrel_amd.config import Config
+    from induction_network_on_fewrel_amd.data import make_synthetic
+    from induction_network_on_fewrel_amd.parallel.dp import DistContext
+    from induction_network_on_fewrel_amd.runtime.trainer import Trainer
+    dist = DistContext.from_env("cpu")
+    data = make_synthetic(num_relations=10, instances_per_relation=30, vocab=300, seed=0)
+    cfg = Config(N=5, K=2, Q=2, episodes_per_step=2, model_dir=os.path.join(out_dir, "m"), resume=False, seed=5)
+    tr = Trainer(cfg, data, None, device="cpu", dist_ctx=dist, log=False)
+    for _ in range(2):
+        tr.train_step()
+    tr.save()
+    cont = tr.train_eps.sample(2, 5, 2, 2)[0]           # what this rank draws next without a restart
+    tr2 = Trainer(cfg.replace(resume=True), data, None, device="cpu", dist_ctx=dist, log=False)
+    resumed = tr2.train_eps.sample(2, 5, 2, 2)[0]
+    torch.save({"cont": cont, "resumed": resumed, "step": tr2.global_step}, os.path.join(out_dir, f"res{rank}.pt"))
+    dist.destroy()
+
+
+@pytest.mark.slow
+def test_dp_resume_keeps_per_rank_samplers(tmp_path):
+    world = 2
+    mp.start_processes(_resume_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    r = [torch.load(tmp_path / f"res{i}.pt", weights_only=True) for i in range(world)]
+    assert all(x["step"] == 2 for x in r)
+    for x in r:
+        assert torch.equal(x["resumed"], x["cont"])          # each rank continues its own stream
+    assert not torch.equal(r[0]["resumed"], r[1]["resumed"])  # ranks still draw different episodes
+
+
 @pytest.mark.slow
 def test_dp_gloo_world2(tmp_path):
     world = 2

@@ -69,11 +69,12 @@ def _unpack_cst(cst, S, L, U):
     return out[:S]
 
 
+@pytest.mark.parametrize("u", [8, 20, 32])
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_lstm_forward(dtype):
+def test_lstm_forward(dtype, u):
     from induction_network_on_fewrel_amd.ops import ops
     from induction_network_on_fewrel_amd.ops.packing import lstm_shape, pack_lstm
-    cfg, data, model, dd, inst, _ = _problem(dtype=dtype)
+    cfg, data, model, dd, inst, _ = _problem(dtype=dtype, u=u)
     p = model.pdict()
     bf16 = dtype == "bf16"
     U = cfg.hidden_size
@@ -184,11 +185,12 @@ def _encoder_grads_ref(model, dd, inst, de, keep_prob, seed, bf16):
     return e.detach(), {k: v.grad for k, v in p.items() if v.grad is not None}
 
 
+@pytest.mark.parametrize("u", [8, 20, 32])
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 @pytest.mark.parametrize("keep_prob", [1.0, 0.9])
-def test_encoder_backward(dtype, keep_prob):
+def test_encoder_backward(dtype, keep_prob, u):
     from induction_network_on_fewrel_amd.ops.encoder import encode
-    cfg, data, model, dd, inst, _ = _problem(dtype=dtype)
+    cfg, data, model, dd, inst, _ = _problem(dtype=dtype, u=u)
     bf16 = dtype == "bf16"
     seed = 99
     meta = dict(U=cfg.hidden_size, bf16=bf16, keep_prob=keep_prob, seed=seed, word_grad=False)
@@ -351,11 +353,44 @@ def test_adam_matches_tf_formula():
     p0 = p.clone()
     b1, b2, eps, lr = 0.9, 0.999, 1e-8, 1e-3
     lr_t = lr * (1 - b2) ** 0.5 / (1 - b1)
-    ops().adam_step(p, m, v, g, None, lr_t, b1, b2, eps, 1.0, 0.0, None)
+    ops().adam_step(p, m, v, g, None, lr_t, b1, b2, eps, 1.0, 0.0, None, None, None)
     m_r = (1 - b1) * g
     v_r = (1 - b2) * g * g
     p_r = p0 - lr_t * m_r / (v_r.sqrt() + eps)
     assert torch.allclose(p, p_r, atol=1e-7, rtol=1e-6)
+
+
+@pytest.mark.parametrize("kind", ["adam", "adagrad"])
+def test_nonfinite_guard_skips_update_on_device(kind):
+    """A NaN / Inf gradient (or loss) skips the fused optimizer step on the device: parameters and
+    moments stay bitwise unchanged and the device skip counter advances (no host sync in the step)."""
+    from induction_network_on_fewrel_amd.ops.optim import FlatParams, FusedOptimizer
+    torch.manual_seed(0)
+    prm = torch.nn.Parameter(torch.randn(10007, device=DEV))
+    flat = FlatParams({"x": prm})
+    opt = FusedOptimizer(flat, kind)
+    st = lambda: [t.clone() for t in [flat.flat] + list(opt.state_tensors().values())]
+    flat.zero_grad()
+    flat.grad.copy_(torch.randn(10007, device=DEV))
+    opt.step(1e-2, check_finite=True, loss=torch.tensor(0.5, device=DEV))
+    before = st()
+    assert opt.skipped() == 0 and not torch.equal(before[0], prm.detach() * 0)
+    for bad_at, val in ((10006, float("nan")), (17, float("inf")), (None, None)):
+        flat.zero_grad()
+        flat.grad.copy_(torch.randn(10007, device=DEV))
+        loss = torch.tensor(0.25, device=DEV)
+        if bad_at is not None:
+            flat.grad[bad_at] = val
+        else:
+            loss.fill_(float("nan"))   # finite gradients, non-finite loss
+        opt.step(1e-2, check_finite=True, loss=loss)
+        torch.cuda.synchronize()
+        assert all(torch.equal(a, b) for a, b in zip(st(), before))
+    assert opt.skipped() == 3
+    flat.zero_grad()                   # the guard word is cleared with the gradients
+    flat.grad.copy_(torch.randn(10007, device=DEV))
+    opt.step(1e-2, check_finite=True, loss=torch.tensor(0.5, device=DEV))
+    assert opt.skipped() == 3 and not torch.equal(flat.flat, before[0])
 
 
 def test_device_sampler_layout():
@@ -383,9 +418,10 @@ def test_device_sampler_layout():
     assert (lab == N).mean() > 0.3
 
 
+@pytest.mark.parametrize("u", [8, 20, 32])
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_full_model_matches_oracle(dtype):
-    cfg, data, model, dd, inst, labels = _problem(dtype=dtype)
+def test_full_model_matches_oracle(dtype, u):
+    cfg, data, model, dd, inst, labels = _problem(dtype=dtype, u=u)
     B, N, K, Q = 3, cfg.N, cfg.K, cfg.Q
     probs, alphas = model(inst, dd.arrays(), B, N, K, Q, training=False)
     loss = model.loss(probs, labels)

@@ -66,6 +66,48 @@ def test_checkpoint_layout_and_rotation(tmp_path):
     assert float(t["W_s"][0, 0]) == 30 and meta["best_acc"] == 0.3 and meta["variables"]["W_s"]["shape"] == [2, 2]
 
 
+def test_best_checkpoint_survives_rotation_and_newer_saves(tmp_path):
+    md = str(tmp_path / "m")
+    t = lambda step: {"W_s": torch.ones(2, 2) * step, "global_step": torch.tensor(step)}
+    ckpt.save(md, "inductionNetwork", 2, t(2), {}, max_to_keep=2, best=True)
+    for step in (4, 6, 8):   # periodic checkpoints after the best one
+        ckpt.save(md, "inductionNetwork", step, t(step), {}, max_to_keep=2)
+    assert ckpt.latest(md).endswith("inductionNetwork-8")
+    assert ckpt.best(md).endswith("inductionNetwork-2")
+    assert float(ckpt.load(ckpt.best(md))[0]["W_s"][0, 0]) == 2
+    files = sorted(os.listdir(os.path.join(md, "checkpoint")))
+    assert "inductionNetwork-4.safetensors" not in files and "inductionNetwork-2.safetensors" in files
+
+
+def test_test_best_loads_best_not_latest(tmp_path):
+    """test_best with periodic saves: the final test must run on the best-val weights."""
+    tr = _trainer(tmp_path, resume=False, save_every=1, train_iter=4, val_step=2, val_iter=2, test_iter=2,
+                  test_best=True, log_every=1)
+    accs = iter([0.9, 0.1])   # val at step 2 is the best, val at step 4 is worse
+    tr.evaluate = lambda iters, **kw: next(accs, 0.5)
+    loaded = []
+    orig = tr.load
+    tr.load = lambda stem: (loaded.append(stem), orig(stem))
+    tr.train()
+    assert loaded and loaded[0].endswith("inductionNetwork-2"), loaded
+
+
+def test_nonfinite_gradient_skips_update_cpu():
+    p = torch.nn.Parameter(torch.randn(10))
+    flat = FlatParams({"x": p})
+    opt = FusedOptimizer(flat, "adam")
+    flat.grad.copy_(torch.randn(10))
+    opt.step(1e-2, check_finite=True)
+    p1, m1, v1 = flat.flat.clone(), opt.m.clone(), opt.v.clone()
+    flat.grad[3] = float("nan")
+    opt.step(1e-2, check_finite=True)
+    assert torch.equal(flat.flat, p1) and torch.equal(opt.m, m1) and torch.equal(opt.v, v1)
+    assert opt.skipped() == 1
+    flat.grad.fill_(0.5)
+    opt.step(1e-2, check_finite=True, loss=torch.tensor(float("inf")))
+    assert opt.skipped() == 2 and torch.equal(flat.flat, p1)
+
+
 def test_event_file_roundtrip(tmp_path):
     assert crc32c(b"123456789") == 0xE3069283   # CRC-32C check value
     w = EventWriter(str(tmp_path))
