@@ -24,10 +24,6 @@ using namespace ina;
 #ifndef INA_FWD_PIPE
 #define INA_FWD_PIPE 1
 #endif
-// bf16 forward: x-row ring depth (prefetch distance XG_RING - 1 steps)
-#ifndef XG_RING
-#define XG_RING 4
-#endif
 namespace {
 
 template <int U, int NX, bool BF16>
@@ -148,20 +144,6 @@ INA_DEVICE u16x8_t fscale(u16x8_t a, float s) {
   return a;
 }
 INA_DEVICE float fscale(float a, float s) { return a * s; }
-
-template <int I, int N, class F>
-INA_DEVICE void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
-}
-
-// s_waitcnt vmcnt(N) that the value d (an inline-asm load destination) depends on
-template <int N>
-INA_DEVICE void vm_wait(uint64_t& d) {
-  asm volatile("s_waitcnt vmcnt(%1)" : "+v"(d) : "n"(N) : "memory");
-}
 
 INA_DEVICE void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -405,59 +387,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   // block (odd-L tail peeled, prefetch index clamped) so LLVM cannot sink the prefetch loads down
   // to their uses.
   auto tof = [&](int tau) { return dir ? (L - 1 - tau) : tau; };
-  if constexpr (!FG && NX == 4) {
-    // x rows (x_gather_kernel) stream from HBM.  A ring of R raw rows keeps R - 1 steps of prefetch
-    // in flight.  The loads are issued by inline asm and retired by explicit counted waits: the
-    // compiler's waitcnt pass merges the loop-header state conservatively and waited vmcnt(3) at the
-    // top of every body, i.e. for all of the previous steps' ~16 stores (store latency on the
-    // recurrence).  The count is exact because the step's VMEM stream is fixed at compile time:
-    // NST stores per step (h U4, c U4 when STORE, keep bits 1 when DROP; no compiler-visible loads).
-    // Order of VMEM ops: ld(0..R-2), then per step j: ld(j + R - 1), NST stores of step j; before
-    // step j's math the ops issued after ld(j) number R - 1 + min(j, R - 1) * NST.
-    constexpr int R = XG_RING;
-    constexpr int NST = U4 + (STORE ? U4 : 0) + (DROP ? 1 : 0);
-    auto ld = [&](int tau, uint64_t& d) __attribute__((always_inline)) {
-      const unsigned short* xp = xg + ((uint32_t)(tile * L + tof(min(tau, L - 1))) * 64 + lane) * NX;
-      asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(d) : "v"(xp) : "memory");
-    };
-    auto run = [&](int tau, uint64_t d) __attribute__((always_inline)) {
-      float xv[NX];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) xv[e] = bf2f((unsigned short)(d >> (16 * e)));
-      step(tau, xv);
-    };
-    uint64_t xr[R];
-    // one body = R steps; FIRST: the peeled first body (the prologue loads precede it)
-    auto body = [&](int tau, auto first) __attribute__((always_inline)) {
-      static_for<0, R>([&](auto kc) __attribute__((always_inline)) {
-        constexpr int k = decltype(kc)::value;
-        constexpr int n = decltype(first)::value ? R - 1 + k * NST : (R - 1) * (NST + 1);
-        ld(tau + k + R - 1, xr[(k + R - 1) % R]);
-        vm_wait<(n < 63 ? n : 63)>(xr[k]);
-        __builtin_amdgcn_sched_barrier(0);
-        run(tau + k, xr[k]);
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    };
-#pragma unroll
-    for (int k = 0; k < R - 1; ++k) ld(k, xr[k]);
-    int tau = 0;
-    if (L >= R) {
-      body(0, std::true_type{});
-      tau = R;
-      for (; tau + R - 1 < L; tau += R) body(tau, std::false_type{});
-    }
-    // tail (< R steps, no further loads): ops issued after ld(tau + k) >= R - 2 - k + k * NST
-    static_for<0, R - 1>([&](auto kc) __attribute__((always_inline)) {
-      constexpr int k = decltype(kc)::value;
-      constexpr int n = R - 2 - k + k * NST;
-      if (tau + k < L) {
-        vm_wait<(n < 63 ? n : 63)>(xr[k]);
-        run(tau + k, xr[k]);
-      }
-    });
-    return;
-  }
+  // (Round 1 streamed the bf16 x rows through an inline-asm load ring retired by hand-counted
+  // `s_waitcnt vmcnt(n)` waits.  It was removed: at u=8 it returned stale x values in 8 of 12
+  // back-to-back runs (tools/dbg/u8_repro2.py; profiles/r2_v1), i.e. the count of VMEM ops retiring
+  // after a load is not a safe completion bound, and an inline-asm load destination is invisible to
+  // the register allocator (a spilled / copied in-flight destination corrupts state).  The loads
+  // below are compiler-visible; the waitcnt pass inserts the waits.)
   float xa[NX], xb[NX];
 #if INA_FWD_PIPE == 0
   // simple loop: prefetch x_{tau+1}, copy at the end of the step

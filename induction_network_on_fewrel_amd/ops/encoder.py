@@ -13,6 +13,8 @@ model/layer_module.py:49-98 (self_attention).
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from ._ext import ops
@@ -43,18 +45,20 @@ def word_rows(word: torch.Tensor, wemb: torch.Tensor, fresh: bool):
     step.  None for word vectors wider than 8 (the kernel then gathers from the table itself)."""
     if wemb.shape[1] > 8:
         return None
-    key = (word.data_ptr(), word.numel(), wemb.data_ptr(), wemb.shape[0], wemb._version)
+    # keyed by tensor identity (weak references), not data_ptr: a freed tensor's address is reused
+    # by the caching allocator, and a data_ptr key would then hand back another table's rows
+    key = (id(word), id(wemb), wemb._version)
     if not fresh:
         hit = _WROWS.get(key)
-        if hit is not None:
-            return hit
+        if hit is not None and hit[0]() is word and hit[1]() is wemb:
+            return hit[2]
     E = wemb.shape[1]
     rows = torch.nn.functional.pad(wemb.detach().float().index_select(0, word.reshape(-1).long()), (0, 8 - E))
     rows = rows.to(torch.bfloat16).contiguous()
     if not fresh:
         if len(_WROWS) >= 4:
             _WROWS.pop(next(iter(_WROWS)))
-        _WROWS[key] = rows
+        _WROWS[key] = (weakref.ref(word), weakref.ref(wemb), rows)
     return rows
 
 
