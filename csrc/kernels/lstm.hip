@@ -389,7 +389,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   auto tof = [&](int tau) { return dir ? (L - 1 - tau) : tau; };
   // (Round 1 streamed the bf16 x rows through an inline-asm load ring retired by hand-counted
   // `s_waitcnt vmcnt(n)` waits.  It was removed: at u=8 it returned stale x values in 8 of 12
-  // back-to-back runs (tools/dbg/u8_repro2.py; profiles/r2_v1), i.e. the count of VMEM ops retiring
+  // back-to-back runs (tools/dbg/u8_repro2.py; profiles/r2_v2), i.e. the count of VMEM ops retiring
   // after a load is not a safe completion bound, and an inline-asm load destination is invisible to
   // the register allocator (a spilled / copied in-flight destination corrupts state).  The loads
   // below are compiler-visible; the waitcnt pass inserts the waits.)
