@@ -33,6 +33,7 @@ def make_synthetic(num_relations: int = 64, instances_per_relation: int = 700, m
     tot = R * I
     unk, blank = vocab, vocab + 1
     max_len = min(max_len, L)
+    min_len = max(1, min(min_len, max_len))
     lengths = rng.integers(min_len, max_len + 1, size=tot).astype(np.int32)
     word = rng.integers(0, vocab, size=(tot, L)).astype(np.int32)
     # a sprinkle of OOV tokens, like real text
