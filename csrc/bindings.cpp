@@ -89,11 +89,9 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd_impl(
   const bool drop = keep_prob < 1.0;
   auto hopt = word.options().dtype(bf16 ? at::kBFloat16 : at::kFloat);
   const int64_t ntiles = (S + 15) / 16;
-  // bf16: hlane = the step-PAIR records [tiles][2][P = ceil(L/2)][2][U4][64][2 steps] (h slot bf16, c
-  // slot fp16 bits; always written -- the h slot is also the attention input) and cst is empty.
-  // fp32: h / c stash (store_c)
-  const int64_t P = (L + 1) / 2;
-  auto hlane = bf16 ? at::empty({ntiles, 2, P, 2, U4, 64, 2}, hopt)
+  // bf16: hlane = the step records [tiles][2][L][2][U4][64] (h slot bf16, c slot fp16 bits; always
+  // written -- the h slot is also the attention input) and cst is empty.  fp32: h / c stash (store_c)
+  auto hlane = bf16 ? at::empty({ntiles, 2, L, 2, U4, 64}, hopt)
                     : (store_c ? at::empty({ntiles, 2, L, U4, 64}, hopt) : at::empty({0}, hopt));
   // hnat is allocated with 16 * ntiles rows so the kernel stores padding rows unconditionally
   // (no lane-divergent store branch); callers see the first S rows.
@@ -104,11 +102,9 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd_impl(
   TORCH_CHECK(ntiles * 16 * L * 2 * U < (1LL << 31) && ntiles * 2 * L * U4 * 64 < (1LL << 32),
               "ina.lstm_fwd: batch too large for 32-bit offsets (split the episode batch)");
   TORCH_CHECK(wemb.size(0) < (1 << 24) && 2 * L < (1 << 16), "ina.lstm_fwd: table rows exceed 24-bit indexing");
-  // dropout keep bits (one byte per lane-step; bf16: [tiles][2][P][64][2 steps]): for the backward,
-  // and in bf16 mode for the natural-row transpose
+  // dropout keep bits (one byte per lane-step): for the backward, and in bf16 mode for h_natural
   const bool want_mask = drop && (store_c || bf16);
-  Tensor dmask = want_mask ? (bf16 ? at::empty({ntiles, 2, P, 64, 2}, word.options().dtype(at::kByte))
-                                   : at::empty({ntiles, 2, L, 64}, word.options().dtype(at::kByte)))
+  Tensor dmask = want_mask ? at::empty({ntiles, 2, L, 64}, word.options().dtype(at::kByte))
                            : at::empty({0}, word.options().dtype(at::kByte));
   TORCH_CHECK(ntiles * L * (64 * NX + 16) < (1LL << 31), "ina.lstm_fwd: batch too large for the x rows");
   Tensor xg = bf16 ? at::empty({ntiles * L * (64 * NX + 16)}, word.options().dtype(at::kBFloat16))
@@ -197,9 +193,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> lstm_attn_fwd
   const Tensor& hlane = std::get<0>(r);
   const Tensor& hnat = std::get<2>(r);   // first S rows of the [16 * tiles] allocation
   const Tensor& dmask = std::get<3>(r);
-  const int64_t P2 = 2 * ((L + 1) / 2);   // steps of the pair records
-  TORCH_CHECK(hlane.numel() == ((S + 15) / 16) * 2 * P2 * 2 * (U / 4) * 64, "ina.lstm_attn_fwd: step records");
-  TORCH_CHECK(!drop || dmask.numel() == ((S + 15) / 16) * 2 * P2 * 64, "ina.lstm_attn_fwd: keep bits");
+  TORCH_CHECK(hlane.numel() == ((S + 15) / 16) * 2 * L * 2 * (U / 4) * 64, "ina.lstm_attn_fwd: step records");
+  TORCH_CHECK(!drop || dmask.numel() == ((S + 15) / 16) * 2 * L * 64, "ina.lstm_attn_fwd: keep bits");
   ina::AttnArgs a{};
   a.inst = inst.data_ptr<int>();
   a.mask = mask.data_ptr<int>();
@@ -246,14 +241,13 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   const int64_t S = inst.size(0), L = word.size(1), E = wemb.size(1), PD = p1emb.size(1);
   const int64_t DIN = E + 2 * PD, NF = DIN + U + 1, U4 = U / 4, KPL = frag_elems(bf16);
   TORCH_CHECK(DIN <= 4 * NX, "ina.lstm_bwd: input dim too large");
-  const int64_t LS = bf16 ? 2 * ((L + 1) / 2) : L;   // bf16: step-pair records (h and c slots)
-  TORCH_CHECK(hraw.numel() == ((S + 15) / 16) * 2 * LS * U4 * 64 * (bf16 ? 2 : 1), "ina.lstm_bwd: hlane shape");
+  TORCH_CHECK(hraw.numel() == ((S + 15) / 16) * 2 * L * U4 * 64 * (bf16 ? 2 : 1), "ina.lstm_bwd: hlane shape");
   TORCH_CHECK(dH.size(0) == S && dH.size(1) == L && dH.size(2) == 2 * U, "ina.lstm_bwd: dH shape");
   TORCH_CHECK(bf16 || cst.numel() == ((S + 15) / 16) * 2 * L * U4 * 64, "ina.lstm_bwd: cst shape");
   const bool drop_ = keep_prob < 1.0;
   if (drop_) {
     check(dmask, "dmask", at::kByte);
-    TORCH_CHECK(dmask.numel() == ((S + 15) / 16) * 2 * LS * 64, "ina.lstm_bwd: dmask (from lstm_fwd) shape");
+    TORCH_CHECK(dmask.numel() == ((S + 15) / 16) * 2 * L * 64, "ina.lstm_bwd: dmask (from lstm_fwd) shape");
   }
   const int64_t NSLOT = U4 + NX;
   TORCH_CHECK(a2pack.numel() == 2 * ((NSLOT + 3) / 4) * ((4 * U4 + KPL - 1) / KPL) * 64 * KPL, "ina.lstm_bwd: a2pack");

@@ -314,9 +314,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
 
 // ------------------------------------------------------------------------------------------
 // bf16 forward fused with the LSTM output transpose (replaces h_natural_kernel + attn_fwd_kernel).
-// Input: lstm_fwd's step-pair records [tile][dir][P][2][U4][64][2] (16-bit; slot 0 = h of the 16
-// sequences of the tile in the lane layout: unit 4m + (li >> 4) of sequence li & 15 at [m][li]) and the
-// DropoutWrapper keep bits [tile][dir][P][64][2] (bit m of byte (li, step)).  One 512-thread workgroup per tile:
+// Input: lstm_fwd's step records [tile][dir][t][2][U4][64] (16-bit; slot 0 = h of the 16 sequences
+// of the tile in the lane layout: unit 4m + (li >> 4) of sequence li & 15 at [m][li]) and the
+// DropoutWrapper keep bits [tile][dir][t][64] (bit m of byte li).  One 512-thread workgroup per tile:
 //   1) every thread loads 4 16-B chunks (units 4m..4m+3) of the tile's h slots (+ their keep bytes)
 //      into registers, applies the dropout (model/graph.py:36-38: keep ? h / keep_prob : 0, bf16)
 //      and scatters them as 8-B pieces into the tile's natural rows [16][L][2U] in LDS
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NT <= 3 ? 6
                                                         float* __restrict__ e_out, float* __restrict__ alphas) {
   using Sh = AShape<U, NT, true>;
   constexpr int H2 = Sh::H2, NKS = Sh::NKS, MT = Sh::MT;
-  constexpr int U4 = U / 4;
+  constexpr int U4 = U / 4, CPP = U4 * 64 / 8;   // 16-B chunks per (dir, step) h slot
   extern __shared__ __attribute__((aligned(16))) unsigned short nat[];   // [16][L][2U] bf16
   const int tile = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -358,47 +358,39 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NT <= 3 ? 6
       mk[j][nt] = maskarr[row + (tok < L ? tok : L - 1)];
     }
   }
-  // 1) step-pair records -> registers -> dropout -> natural rows in LDS.  Records (lstm_fwd_kernel):
-  //    16-bit [tile][dir][P][2 slots][U4][64 lanes][2 steps], lane = 16 q + n holds unit 4m + q of
-  //    sequence n; keep bits 16-bit [tile][dir][P][64] (byte s = step 2p + s, bit m).
-  //    A work item = units 4m .. 4m + 3 (the 4 lane groups q) of sequences n0 .. n0 + 3 for both
-  //    steps of pair p: 4 16-B chunks (lanes 16q + n0 .. +3, 2 steps each) -> 8 8-B pieces of the
-  //    tile's natural rows (column d * U + 4m: 8-B aligned since U % 4 == 0)
-  const int P = (L + 1) >> 1;
-  const uint4* src = reinterpret_cast<const uint4*>(rec) + (size_t)tile * 2 * P * 2 * U4 * 16;
-  const int nit = 2 * P * U4 * 4;
+  // 1) records -> registers -> dropout -> natural rows in LDS
+  const uint4* src = reinterpret_cast<const uint4*>(rec + (size_t)tile * 2 * L * 2 * U4 * 64);
+  // a work item = the 4 chunks of units 4m .. 4m + 3 of 8 sequences n0..n0+7 (lanes 16r + n0, chunks
+  // 8m + 2r + n0 / 8 of the slot); each sequence's 4 values are one 8-B piece of its natural row
+  // (column d * U + 4m: 8-B aligned since U % 4 == 0)
+  const int nit = 2 * L * U4 * 2;
   uint2* nat64 = reinterpret_cast<uint2*>(nat);
   for (int c = threadIdx.x; c < ((INA_HA_PHASES & 1) ? nit : 0); c += 512) {
-    const int k = c / (U4 * 4), pc = c - k * (U4 * 4);   // k = dir * P + p
-    const int m = pc >> 2, n0 = (pc & 3) * 4;
-    const uint4* sk = src + (size_t)k * 2 * U4 * 16 + m * 16 + (n0 >> 2);   // h slot of pair k, unit group m
+    const int k = c / (U4 * 2), pc = c - k * (U4 * 2);   // k = dir * L + t
+    const int m = pc >> 1, n0 = (pc & 1) * 8;
+    const uint4* sk = src + (size_t)k * 2 * CPP + m * 8 + (n0 >> 3);   // h slot of record k
     uint4 v[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = sk[4 * r];
-    const int d = k >= P ? 1 : 0, p = k - d * P;
+    for (int r = 0; r < 4; ++r) v[r] = sk[2 * r];
+    const int d = k >= L ? 1 : 0, t = k - d * L;
     const int col4 = (d * U + 4 * m) >> 2;
     unsigned long long kb[4] = {~0ull, ~0ull, ~0ull, ~0ull};
     if (dmask) {
-      const unsigned char* kp = dmask + (((size_t)tile * 2 * P + k) * 64 + n0) * 2;
+      const unsigned char* kp = dmask + ((size_t)tile * 2 * L + k) * 64 + n0;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) kb[r] = *reinterpret_cast<const unsigned long long*>(kp + 32 * r);
+      for (int r = 0; r < 4; ++r) kb[r] = *reinterpret_cast<const unsigned long long*>(kp + 16 * r);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 8; ++i) {
+      uint32_t x[4];
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const int t = 2 * p + st;
-        if (t >= L) continue;
-        uint32_t x[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t w = i == 0 ? v[r].x : i == 1 ? v[r].y : i == 2 ? v[r].z : v[r].w;
-          unsigned short h = (unsigned short)(w >> (16 * st));
-          if (dmask) h = ((kb[r] >> (8 * (2 * i + st) + m)) & 1ull) ? f2bf(bf2f(h) * inv_kp) : (unsigned short)0;
-          x[r] = h;
-        }
-        nat64[((n0 + i) * L + t) * (H2 / 4) + col4] = make_uint2(x[0] | (x[1] << 16), x[2] | (x[3] << 16));
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t w = i < 2 ? v[r].x : i < 4 ? v[r].y : i < 6 ? v[r].z : v[r].w;
+        unsigned short h = (unsigned short)(w >> (16 * (i & 1)));
+        if (dmask) h = ((kb[r] >> (8 * i + m)) & 1ull) ? f2bf(bf2f(h) * inv_kp) : (unsigned short)0;
+        x[r] = h;
       }
+      nat64[((n0 + i) * L + t) * (H2 / 4) + col4] = make_uint2(x[0] | (x[1] << 16), x[2] | (x[3] << 16));
     }
   }
   // W1 fragments and b1 / w2 staged in LDS (read per sentence: registers stay free for occupancy)
@@ -687,9 +679,6 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
 // dW1 accumulated in 32-token K-steps through a small wave-private LDS transpose.
 // slab per block: [dW1 (H2*H2, row i, col j) | db1 (H2) | dw2 (H2)]
 constexpr int AB2_WAVES = 4;
-#ifndef INA_AB2_NODW
-#define INA_AB2_NODW 0   // timing experiment: skip the dW1 staging + MFMA flush (wrong dW1)
-#endif
 
 template <int U, int NT>
 __host__ __device__ constexpr int ab2_rows() { return ((2 * U + 15) / 16) * 16; }
@@ -863,7 +852,6 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(
       }
       // stage this tile's H (features) and dP columns for the dW1 K-step
       const int col = 16 * (tc & 1) + n;
-      if (INA_AB2_NODW) continue;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll

@@ -21,11 +21,8 @@
 
 using namespace ina;
 
-#ifndef INA_DROP_FAKE
-#define INA_DROP_FAKE 0   // timing experiment: forward keep bits without the hash (wrong values)
-#endif
-#ifndef INA_FWD_ALDS
-#define INA_FWD_ALDS 0   // bf16 forward: gate weight fragments read from LDS per step (frees ~40 VGPRs)
+#ifndef INA_FWD_PIPE
+#define INA_FWD_PIPE 1
 #endif
 namespace {
 
@@ -242,21 +239,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   using frag = typename FragT<BF16>::type;
   using celem = typename CT<BF16>::type;
   constexpr int U4 = Sh::U4, KPL = Sh::KPL, NKS = Sh::NKS, NMT = Sh::NMT;
-  extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
+  extern __shared__ __attribute__((aligned(16))) int2 ids_all[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = lane >> 4, n = lane & 15;
   const int dir = blockIdx.y;
   const int ntiles = (S + 15) / 16;
   const int tile = blockIdx.x * 4 + wave;
-  int2* ids = reinterpret_cast<int2*>(fsm) + wave * 16 * L;
+  int2* ids = ids_all + wave * 16 * L;
   constexpr bool FG = !BF16;   // fp32 mode gathers x per step
-  constexpr bool ALDS = BF16 && INA_FWD_ALDS;
-  frag* lA = reinterpret_cast<frag*>(fsm);   // ALDS: [NMT][NKS][64] pre-scaled gate fragments
-  if constexpr (ALDS) {
-    const frag* ap = apack + (size_t)dir * NMT * NKS * 64;
-    for (int i = threadIdx.x; i < NMT * NKS * 64; i += 256) lA[i] = fscale(ap[i], gate_scale(i & 3));
-    __syncthreads();
-  }
   if constexpr (FG) {
     // fp32 mode gathers x per step: stage (word, pos1 | pos2 << 16) of the wave's 16 sequences into LDS
     for (int i = lane; i < 16 * L; i += 64) {
@@ -276,14 +266,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   const int seq = tile * 16 + n;  // rows >= S are padding rows of hnat (allocated to 16 * ntiles)
   const uint32_t salt = dropout_salt(seed, (uint32_t)dir);
 
-  frag A[ALDS ? 1 : NMT][ALDS ? 1 : NKS];
-  if constexpr (!ALDS) {
-    const frag* ap = apack + (size_t)dir * NMT * NKS * 64;
+  frag A[NMT][NKS];
+  const frag* ap = apack + (size_t)dir * NMT * NKS * 64;
 #pragma unroll
-    for (int m = 0; m < NMT; ++m)
+  for (int m = 0; m < NMT; ++m)
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) A[m][ks] = fscale(ap[(m * NKS + ks) * 64 + lane], gate_scale(lane & 3));
-  }
+    for (int ks = 0; ks < NKS; ++ks) A[m][ks] = fscale(ap[(m * NKS + ks) * 64 + lane], gate_scale(lane & 3));
   float bm[NMT][4];   // pre-scaled gate biases (gate_bias)
 #pragma unroll
   for (int m = 0; m < NMT; ++m)
@@ -317,7 +305,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     }
   };
   // one recurrence step at processing index tau with input features xv
-  auto step = [&](const int tau, const float* xv) __attribute__((always_inline)) -> uint32_t {
+  auto step = [&](const int tau, const float* xv) __attribute__((always_inline)) {
     const int t = dir ? (L - 1 - tau) : tau;
     frag B[NKS];
 #pragma unroll
@@ -332,31 +320,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
           fset<BF16>(B[ks], j, xv[idx - U4]);
       }
     }
-    if constexpr (ALDS) asm volatile("" ::: "memory");   // re-read the LDS fragments every step
 #pragma unroll
     for (int m = 0; m < NMT; ++m) {
       f32x4_t acc = {bm[m][0], bm[m][1], bm[m][2], bm[m][3]};
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        if constexpr (ALDS)
-          acc = mma(lA[(m * NKS + ks) * 64 + lane], B[ks], acc);
-        else
-          acc = mma(A[ALDS ? 0 : m][ALDS ? 0 : ks], B[ks], acc);
-      }
+      for (int ks = 0; ks < NKS; ++ks) acc = mma(A[m][ks], B[ks], acc);
       const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
       c[m] = c[m] * fg + ig * jg;
       float hv = tanh_l2(c[m] * (2.f * LOG2E_F)) * og;
       if (BF16) hv = round_bf(hv);  // the stored / recurrent operand value
       h[m] = hv;
     }
-    uint32_t bits = 0;
     if constexpr (BF16) {
-      // bf16: the caller stores the step-pair records (store_pair / store_single)
+      // bf16 step record [tile][dir][t][2][U4][64] (16-bit): slot 0 = the raw recurrent h (bf16), slot 1
+      // = the cell state (fp16, training only); every store is a coalesced 128-B lane-layout run off
+      // ONE address.  The h slot is both the backward's stash and the attention input:
+      // h_natural_kernel transposes it to natural rows and applies the DropoutWrapper mask from the
+      // keep bits stored here.  (Natural [seq][t][2U] rows from here scatter each store over 16 rows,
+      // ~300 us of ~550; a separate dropped copy costs 303 MB more on a write-bandwidth-bound kernel.)
+      // 32-bit offsets (checked on the host); padding rows are stored too.
+      typename FragT<BF16>::elem* rec = hnat + ((uint32_t)((tile * 2 + dir) * L + t) * (2 * U4)) * 64 + lane;
+#pragma unroll
+      for (int m = 0; m < U4; ++m) rec[m * 64] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
+      if constexpr (STORE) {
+#pragma unroll
+        for (int m = 0; m < U4; ++m) rec[(U4 + m) * 64] = __builtin_bit_cast(unsigned short, (_Float16)c[m]);
+      }
       if constexpr (DROP) {
         const uint32_t base = ((uint32_t)seq * L + t) * U + q;
+        uint32_t bits = 0;
 #pragma unroll
-        for (int m = 0; m < U4; ++m)
-          bits |= (INA_DROP_FAKE ? ((base + 4 * m) & 7u) != 0u : dropout_keep_salted(salt, base + 4 * m, thr)) ? (1u << m) : 0u;
+        for (int m = 0; m < U4; ++m) bits |= dropout_keep_salted(salt, base + 4 * m, thr) ? (1u << m) : 0u;
+        dmask[(uint32_t)((tile * 2 + dir) * L + t) * 64 + lane] = (unsigned char)bits;
       }
     } else {
       // fp32: the attention input (dropout applied) in natural rows, h / c stash in the lane layout
@@ -386,8 +381,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
         for (int m = 0; m < U4; ++m) cp[m * 64] = (celem)c[m];
       }
     }
-    return bits;
   };
+  // two-step unrolled loop with ping-pong x buffers: the gather for step tau+1 is issued before
+  // step tau's math and consumed one step later (no register copies).  The loop body is ONE basic
+  // block (odd-L tail peeled, prefetch index clamped) so LLVM cannot sink the prefetch loads down
+  // to their uses.
   auto tof = [&](int tau) { return dir ? (L - 1 - tau) : tau; };
   // (Round 1 streamed the bf16 x rows through an inline-asm load ring retired by hand-counted
   // `s_waitcnt vmcnt(n)` waits.  It was removed: at u=8 it returned stale x values in 8 of 12
@@ -396,101 +394,75 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   // the register allocator (a spilled / copied in-flight destination corrupts state).  The loads
   // below are compiler-visible; the waitcnt pass inserts the waits.)
   float xa[NX], xb[NX];
-  if constexpr (FG) {
-    // fp32: one step at a time (step() stores), x_{tau+1} prefetched
-    load_x(tof(0), xa);
-    for (int tau = 0; tau < L; ++tau) {
-      load_x(tof(min(tau + 1, L - 1)), xb);
-      step(tau, xa);
-#pragma unroll
-      for (int xi = 0; xi < NX; ++xi) xa[xi] = xb[xi];
-    }
-    return;
-  }
-  // bf16 step-PAIR records, 16-bit elements [tile][dir][P = ceil(L/2)][2 slots][U4][64 lanes][2 steps]:
-  // slot 0 = the raw recurrent h (bf16), slot 1 = the cell state (fp16, training only); element
-  // [p][..][s] is time 2p + s.  Each store instruction writes one dword per lane (h or c of one unit
-  // for both steps of the pair): a 256-B run, half the store instructions of per-step 16-bit records
-  // (this kernel is bound by its store instructions: one per 5 cycles per CU).  Keep bits: one
-  // 16-bit word per lane and pair [tile][dir][P][64] (byte s = step 2p + s, bit m = unit 4m + q).
-  // The h slot is both the backward's stash and the attention input (hnat_attn_kernel transposes it
-  // to natural rows, applying the DropoutWrapper mask from the keep bits).  32-bit offsets (checked
-  // on the host); padding rows are stored too.
-  const int P = (L + 1) >> 1;
-  uint32_t* rec32 = reinterpret_cast<uint32_t*>(hnat) + (uint32_t)(tile * 2 + dir) * P * (2 * U4 * 64) + lane;
-  unsigned short* km16 = reinterpret_cast<unsigned short*>(dmask) + (uint32_t)(tile * 2 + dir) * P * 64 + lane;
-  float h1[U4], c1[U4];   // the pair's first processed step
-  auto pk_bf = [](float lo, float hi) { return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16); };
-  auto pk_h = [](float lo, float hi) {
-    return (uint32_t)__builtin_bit_cast(unsigned short, (_Float16)lo) |
-           ((uint32_t)__builtin_bit_cast(unsigned short, (_Float16)hi) << 16);
-  };
-  // store the pair p from (lo = time 2p, hi = time 2p + 1) values
-  auto store_pair = [&](int p, const float* hlo, const float* hhi, const float* clo, const float* chi, uint32_t blo,
-                        uint32_t bhi) __attribute__((always_inline)) {
-    uint32_t* r = rec32 + (uint32_t)p * (2 * U4 * 64);
-#pragma unroll
-    for (int m = 0; m < U4; ++m) r[m * 64] = pk_bf(hlo[m], hhi[m]);
-    if constexpr (STORE) {
-#pragma unroll
-      for (int m = 0; m < U4; ++m) r[(U4 + m) * 64] = pk_h(clo[m], chi[m]);
-    }
-    if constexpr (DROP) km16[(uint32_t)p * 64] = (unsigned short)(blo | (bhi << 8));
-  };
-  const float zero[U4] = {};
-  // dir 0 processes t = 0, 1, ... (pairs (2p, 2p+1) in order, a lone last step when L is odd);
-  // dir 1 processes t = L-1, L-2, ... (a lone FIRST step t = L-1 when L is odd, then (odd, even) pairs)
-  int tau = 0;
+#if INA_FWD_PIPE == 0
+  // simple loop: prefetch x_{tau+1}, copy at the end of the step
   load_x(tof(0), xa);
-  if (dir && (L & 1)) {   // lone step t = L - 1 (even): stored as the low half of its pair
-    load_x(tof(min(1, L - 1)), xb);
-    const uint32_t b0 = step(0, xa);
-    store_pair((L - 1) >> 1, h, zero, c, zero, b0, 0u);
+  for (int tau = 0; tau < L; ++tau) {
+    load_x(tof(min(tau + 1, L - 1)), xb);
+    step(tau, xa);
 #pragma unroll
     for (int xi = 0; xi < NX; ++xi) xa[xi] = xb[xi];
-    tau = 1;
   }
+#else
   // sched_barrier pins each prefetch ahead of the step it overlaps (the machine scheduler would
   // otherwise sink the loads next to their uses to save registers)
-  for (; tau + 1 < L; tau += 2) {
+  auto pair = [&](int tau) __attribute__((always_inline)) {
     load_x(tof(tau + 1), xb);
     __builtin_amdgcn_sched_barrier(0);
-    const uint32_t b1 = step(tau, xa);
-#pragma unroll
-    for (int m = 0; m < U4; ++m) {
-      h1[m] = h[m];
-      c1[m] = c[m];
-    }
+    step(tau, xa);
     __builtin_amdgcn_sched_barrier(0);
     load_x(tof(min(tau + 2, L - 1)), xa);
     __builtin_amdgcn_sched_barrier(0);
-    const uint32_t b2 = step(tau + 1, xb);
-    const int t2 = tof(tau + 1);
-    if (dir)   // second step is the even one (low half)
-      store_pair(t2 >> 1, h, h1, c, c1, b2, b1);
-    else
-      store_pair(t2 >> 1, h1, h, c1, c, b1, b2);
+    step(tau + 1, xb);
     __builtin_amdgcn_sched_barrier(0);
+  };
+  load_x(tof(0), xa);
+  int tau = 0;
+  // first pair peeled: the loop header is then entered with the same outstanding-VMEM state from
+  // the preheader and the latch, so the waitcnt pass can count precisely.
+  if (L >= 2) {
+    pair(0);
+    tau = 2;
   }
-  if (tau < L) {   // dir 0, L odd: lone last step t = L - 1 (even)
-    const uint32_t b0 = step(tau, xa);
-    store_pair(tof(tau) >> 1, h, zero, c, zero, b0, 0u);
-  }
+  for (; tau + 1 < L; tau += 2) pair(tau);
+  if (tau < L) step(tau, xa);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
-// bf16 forward output: step-pair records (lstm_fwd_kernel) -> natural rows [seq][t][2U] (the
-// attention input, model/graph.py:49 concat of the two directions) with the DropoutWrapper mask
-// applied from the stored keep bits.  Only the unfused path uses it (lstm_fwd op + attn_fwd; the
-// training / eval forward is hnat_attn_kernel): one workgroup per 16-sequence tile, thread (sequence
-// n = tid / 16, part) writes dwords part, part + 16, ... of n's contiguous [L][2U] run.
+// bf16 forward output, lane layout [tile][dir][t][U4][64] -> natural rows [seq][t][2U] (the
+// attention input, model/graph.py:49 concat of the two directions).  One workgroup per 16-sequence
+// tile: the tile's contiguous input block lands in LDS by LDS-DMA; each sequence's output rows are
+// one contiguous run written with coalesced dwords (16 threads per sequence).
 // ------------------------------------------------------------------------------------------
 template <int U>
 __global__ __launch_bounds__(256) void h_natural_kernel(const unsigned short* __restrict__ rec,
-                                                        const unsigned short* __restrict__ keep16, int L,
+                                                        const unsigned char* __restrict__ dmask, int L,
                                                         float inv_kp, unsigned short* __restrict__ hnat) {
-  constexpr int U4 = U / 4;
-  const int tile = blockIdx.x, P = (L + 1) >> 1;
+  constexpr int U4 = U / 4, PIECE = U4 * 64 * 2;   // bytes of one (dir, step) h slot
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds_h[];   // h [2][L][U4][64], keep bits
+  const int tile = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // 1) the h slots of the tile's step records ([2][L][2][U4][64]) and its keep bits [2][L][64] -> LDS
+  //    by LDS-DMA (16 B per lane, one piece per wave instruction), all in flight
+  const int hbytes = 2 * L * PIECE, hpad = (hbytes + 1023) & ~1023, mbytes = dmask ? 2 * L * 64 : 0;
+  const char* src = reinterpret_cast<const char*>(rec) + (size_t)tile * 2 * hbytes;
+  char* lds = reinterpret_cast<char*>(lds_h);
+  for (int k = wave; k < 2 * L; k += 4)
+    if (lane * 16 < PIECE)
+      __builtin_amdgcn_global_load_lds(src + (size_t)k * 2 * PIECE + lane * 16, lds + k * PIECE, 16, 0, 0);
+  if (dmask) {
+    const char* msrc = reinterpret_cast<const char*>(dmask) + (size_t)tile * mbytes;
+    for (int k = wave; k * 1024 < mbytes; k += 4) {
+      const int off = k * 1024 + lane * 16;
+      if (off < mbytes) __builtin_amdgcn_global_load_lds(msrc + off, lds + hpad + k * 1024, 16, 0, 0);
+    }
+  }
+  __syncthreads();
+  const unsigned char* keep = reinterpret_cast<const unsigned char*>(lds + hpad);
+  // 2) natural rows: thread (sequence n = tid / 16, part) writes dwords part, part + 16, ... of n's
+  //    contiguous run [L][2U] (dword = features (2p, 2p + 1) of one step); DropoutWrapper output
+  //    keep ? bf16(h / keep_prob) : 0 (model/graph.py:36-38)
   const int n = threadIdx.x >> 4, part = threadIdx.x & 15;
   uint32_t* dst = reinterpret_cast<uint32_t*>(hnat + ((size_t)tile * 16 + n) * L * 2 * U);
   for (int i = part; i < L * U; i += 16) {
@@ -500,9 +472,8 @@ __global__ __launch_bounds__(256) void h_natural_kernel(const unsigned short* __
     for (int e = 0; e < 2; ++e) {
       const int fe = f + e, d = fe >= U ? 1 : 0, u = fe - d * U;
       const int li = (u & 3) * 16 + n;
-      const size_t pr = ((size_t)tile * 2 + d) * P + (t >> 1);
-      unsigned short x = rec[((pr * 2 * U4 + (u >> 2)) * 64 + li) * 2 + (t & 1)];
-      if (keep16) x = ((keep16[pr * 64 + li] >> (8 * (t & 1) + (u >> 2))) & 1u) ? f2bf(bf2f(x) * inv_kp) : (unsigned short)0;
+      unsigned short x = lds_h[((d * L + t) * U4 + (u >> 2)) * 64 + li];
+      if (dmask) x = ((keep[(d * L + t) * 64 + li] >> (u >> 2)) & 1u) ? f2bf(bf2f(x) * inv_kp) : (unsigned short)0;
       v |= (uint32_t)x << (16 * e);
     }
     dst[i] = v;
@@ -611,14 +582,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     const typename CT<BF16>::type* cbase = cst + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
     const elem* hbase = hraw + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
     // bf16: the forward's step records [t][2][U4][64]: h slot, then c slot (fp16 bits)
-    // bf16: the forward's step-pair records [p][2 slots][U4][64][2 steps]: h slot, then c slot (fp16 bits)
-    const int P = (L + 1) >> 1;
-    const unsigned short* rbase =
-        reinterpret_cast<const unsigned short*>(hraw) + (((size_t)tile * 2 + dir) * P * 2 * U4 * 64 + lane) * 2;
+    const unsigned short* rbase = reinterpret_cast<const unsigned short*>(hraw) + ((size_t)tile * 2 + dir) * L * 2 * U4 * 64 + lane;
     auto ld_hc = [&](int tt, int m, float& hv, float& cv) {
       if constexpr (BF16) {
-        hv = bf2f(rbase[((size_t)(tt >> 1) * 2 * U4 + m) * 128 + (tt & 1)]);
-        cv = (float)__builtin_bit_cast(_Float16, rbase[((size_t)(tt >> 1) * 2 * U4 + U4 + m) * 128 + (tt & 1)]);
+        hv = bf2f(rbase[((size_t)tt * 2 * U4 + m) * 64]);
+        cv = (float)__builtin_bit_cast(_Float16, rbase[((size_t)tt * 2 * U4 + U4 + m) * 64]);
       } else {
         hv = from_elem(hbase[((size_t)tt * U4 + m) * 64]);
         cv = from_c(cbase[((size_t)tt * U4 + m) * 64]);
@@ -643,15 +611,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       wid_n = word[rowbase + t1]; p1_n = pos1[rowbase + t1]; p2_n = pos2[rowbase + t1];
     }
     float xv[NX], hp[U4], cprev[U4], ccur[U4], dhin[U4];
-    // fwd keep bits: bf16 [tile][dir][P][64] 16-bit (byte = step of the pair), fp32 [tile][dir][L][64]
-    const unsigned char* mbase = dmask + (size_t)(tile * 2 + dir) * (BF16 ? 2 * P : L) * 64 + (BF16 ? 2 : 1) * lane;
-    auto keep_bits = [&](int tt) -> uint32_t {
-      if constexpr (BF16) return mbase[(size_t)(tt >> 1) * 128 + (tt & 1)];
-      return mbase[(size_t)tt * 64];
-    };
+    const unsigned char* mbase = dmask + (size_t)(tile * 2 + dir) * L * 64 + lane;   // fwd keep bits
     {
       const int t = tof(L - 1), tp = tof(L >= 2 ? L - 2 : 0);
-      const uint32_t bits = drop ? keep_bits(t) : 0xFFu;
+      const uint32_t bits = drop ? (uint32_t)mbase[(size_t)t * 64] : 0xFFu;
       if constexpr (BF16) {
         load_xg(t, xv);
       } else {
@@ -699,7 +662,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         p2_nn = pos2[rowbase + tnn];
       }
       float xv_n[NX], hp_n[U4], cprev_n[U4], dhin_n[U4];
-      const uint32_t bits_n = drop ? keep_bits(tn) : 0xFFu;
+      const uint32_t bits_n = drop ? (uint32_t)mbase[(size_t)tn * 64] : 0xFFu;
       if constexpr (BF16) {
         load_xg(tn, xv_n);
       } else {
@@ -1119,10 +1082,7 @@ static int launch_fwd_t(const LstmArgs& a, hipStream_t st) {
   using elem = typename FragT<BF16>::elem;
   const int ntiles = (a.S + 15) / 16;
   dim3 grid((ntiles + 3) / 4, 2);
-  using Sh = Shape<U, NX, BF16>;
-  // fp32: token ids; bf16 (INA_FWD_ALDS): the gate weight fragments
-  size_t lds = BF16 ? (INA_FWD_ALDS ? (size_t)Sh::NMT * Sh::NKS * 64 * sizeof(frag) : 0)
-                    : (size_t)4 * 16 * a.L * sizeof(int2);
+  size_t lds = BF16 ? 0 : (size_t)4 * 16 * a.L * sizeof(int2);   // fp32: token ids
   const bool store = a.hraw != nullptr && a.cst != nullptr;
   auto kern = a.drop ? (store ? lstm_fwd_kernel<U, NX, BF16, true, true> : lstm_fwd_kernel<U, NX, BF16, true, false>)
                      : (store ? lstm_fwd_kernel<U, NX, BF16, false, true> : lstm_fwd_kernel<U, NX, BF16, false, false>);
@@ -1225,14 +1185,19 @@ int h_natural(const void* rec, const unsigned char* dmask, float inv_kp, int S, 
               hipStream_t st) {
   const int ntiles = (S + 15) / 16;
   if (ntiles <= 0) return 0;
-  const auto* in = (const unsigned short*)rec;
-  const auto* km = (const unsigned short*)dmask;
+  const size_t lds = (((size_t)2 * L * (U / 4) * 64 * sizeof(unsigned short) + 1023) & ~(size_t)1023) +
+                     (dmask ? (((size_t)2 * L * 64 + 1023) & ~(size_t)1023) : 0);
+  const auto* hl = rec;
+  if (lds > 160 * 1024) return -1;
+  const auto* in = (const unsigned short*)hl;
   auto* out = (unsigned short*)hnat;
-#define INA_HN(UV)                                                                                  \
-  if (U == UV) {                                                                                    \
-    hipLaunchKernelGGL(h_natural_kernel<UV>, dim3(ntiles), dim3(256), 0, st, in, km, L, inv_kp, out); \
-    INA_CHECK_LAUNCH();                                                                             \
-    return 0;                                                                                       \
+#define INA_HN(UV)                                                                                     \
+  if (U == UV) {                                                                                       \
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)h_natural_kernel<UV>,                        \
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+    hipLaunchKernelGGL(h_natural_kernel<UV>, dim3(ntiles), dim3(256), lds, st, in, dmask, L, inv_kp, out); \
+    INA_CHECK_LAUNCH();                                                                                \
+    return 0;                                                                                          \
   }
   INA_HN(20)
   INA_HN(32)

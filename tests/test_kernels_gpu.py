@@ -45,15 +45,12 @@ def _gathered(dd, inst):
     return [t[inst.long()] for t in dd.arrays()]
 
 
-def _split_stash(hlane, cst, L):
-    """lstm_fwd's backward stash as float lane-layout (h, c) [tiles][2][L][U4][64]: bf16 mode keeps both
-    in its step-pair records (h slot bf16, c slot fp16 bits; cst is empty); fp32 mode returns separate
-    arrays."""
-    if hlane.dim() == 7:   # bf16 [tiles][2][P][2 slots][U4][64][2 steps]
-        T, _, P, _, U4, _, _ = hlane.shape
-        r = hlane.permute(0, 1, 2, 6, 3, 4, 5).reshape(T, 2, 2 * P, 2, U4, 64)[:, :, :L]
-        h = r[:, :, :, 0].contiguous().float()
-        c = r[:, :, :, 1].contiguous().view(torch.float16).float()
+def _split_stash(hlane, cst):
+    """lstm_fwd's backward stash as float lane-layout (h, c): bf16 mode keeps both in its step records
+    (h slot bf16, c slot fp16 bits; cst is empty); fp32 mode returns separate arrays."""
+    if hlane.dim() == 6:   # bf16 step records [tiles][2][L][2 slots][U4][64]: h (bf16), c (fp16 bits)
+        h = hlane[:, :, :, 0].contiguous().float()
+        c = hlane[:, :, :, 1].contiguous().view(torch.float16).float()
         return h, c
     return hlane.float(), (cst.float() if cst is not None else None)
 
@@ -100,7 +97,7 @@ def test_lstm_forward(dtype, u, L):
     S, L = inst.shape[0], word.shape[1]
     ef = _relerr(hraw[..., :U].float(), hf)
     eb = _relerr(hraw[..., U:].float(), hb)
-    hs, cs = _split_stash(hlane, cst, word.shape[1])
+    hs, cs = _split_stash(hlane, cst)
     c = _unpack_cst(cs, S, L, U)
     ec = _relerr(c, torch.cat([cf, cb], -1))
     hl = _unpack_cst(hs, S, L, U)
@@ -126,7 +123,7 @@ def test_attention_forward(dtype, keep_prob):
     hlane, _, hdrop, _, _ = ops().lstm_fwd(inst, word, pos1, pos2, p["word_embedding"].detach(),
                                      p["pos1_embedding"].detach(), p["pos2_embedding"].detach(), apack, bias, U,
                                      lstm_shape(U, DIN, bf16)["NX"], bf16, True, seed, keep_prob, None, None)
-    hraw = _unpack_cst(_split_stash(hlane, None, word.shape[1])[0], inst.shape[0], word.shape[1], U)
+    hraw = _unpack_cst(_split_stash(hlane, None)[0], inst.shape[0], word.shape[1], U)
     w1p, _ = pack_attn(p["attn_kernel"], bf16)
     e, alphas = ops().attn_fwd(hdrop, inst, mask, w1p, p["attn_bias"].detach().contiguous(),
                                p["attn_w2"].detach().reshape(-1).contiguous(), U, bf16, 0)
@@ -219,7 +216,7 @@ def test_encoder_backward(dtype, keep_prob, u, L=37):
 
 @pytest.mark.parametrize("L", [24, 1, 2])
 def test_encoder_backward_short_and_even_L(L):
-    """step-pair records: even L, and the 1- and 2-step edge cases (a lone step in each direction)."""
+    """even L and the 1- and 2-step edge cases of the recurrences' peeled loops."""
     test_encoder_backward("bf16", 0.9, 20, L=L)
 
 
