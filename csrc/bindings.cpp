@@ -455,7 +455,7 @@ Tensor ntn_fwd(const Tensor& cls, const Tensor& e, const Tensor& mpack, const Te
   check_episode_rows(e, E, N, K, Q, "ina.ntn_fwd");
   const int64_t H = e.size(1), MTH = (H + 15) / 16, NKA = (MTH + 1) / 2;
   TORCH_CHECK(N <= 16 && N * Q <= 64, "ina.ntn_fwd: needs N <= 16 and N*Q <= 64");
-  TORCH_CHECK(MTH == 1 || MTH == 3 || MTH == 4, "ina.ntn_fwd: unsupported H ", H);
+  TORCH_CHECK((MTH == 1 || MTH == 3 || MTH == 4) && H % 8 == 0, "ina.ntn_fwd: unsupported H ", H);
   TORCH_CHECK(cls.numel() == E * N * H, "ina.ntn_fwd: cls shape");
   const int64_t hp = 2 * ((h + 1) / 2);  // packs are padded to an even number of slices
   TORCH_CHECK(mpack.numel() == hp * MTH * NKA * 64 * 8, "ina.ntn_fwd: mpack size");
@@ -505,7 +505,7 @@ std::tuple<Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tensor& e, c
   const int64_t H = e.size(1), MTH = (H + 15) / 16, NKB = (MTH + 1) / 2;
   TORCH_CHECK(N <= 16 && N * Q <= 64, "ina.ntn_bwd: needs N <= 16 and N*Q <= 64");
   TORCH_CHECK(MTH == 1 || MTH == 3 || MTH == 4, "ina.ntn_bwd: unsupported H");
-  TORCH_CHECK(H % 4 == 0, "ina.ntn_bwd: H must be a multiple of 4");
+  TORCH_CHECK(H % 8 == 0, "ina.ntn_bwd: H must be a multiple of 8 (float4 row loads)");
   TORCH_CHECK(dz.numel() == E * N * Q * N, "ina.ntn_bwd: dz shape");
   TORCH_CHECK(de.sizes() == e.sizes(), "ina.ntn_bwd: de shape");
   const int64_t hp = 2 * ((h + 1) / 2);

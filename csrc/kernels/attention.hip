@@ -679,6 +679,9 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
 // dW1 accumulated in 32-token K-steps through a small wave-private LDS transpose.
 // slab per block: [dW1 (H2*H2, row i, col j) | db1 (H2) | dw2 (H2)]
 constexpr int AB2_WAVES = 4;
+#ifndef INA_AB2_EXP
+#define INA_AB2_EXP 0   // timing experiments: 1 = loads from a few cached sentences, 2 = skip dW1 staging
+#endif
 
 template <int U, int NT>
 __host__ __device__ constexpr int ab2_rows() { return ((2 * U + 15) / 16) * 16; }
@@ -740,6 +743,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(
   };
 
   for (int s = gw; s < S; s += nw) {
+    const int sl_ = INA_AB2_EXP == 1 ? (gw & 255) : s;   // load source (experiment 1: L2-resident)
     // ---- every load of the sentence first: H tiles (bf16 MFMA operands), de, alphas
     u16x8_t hf[NT][NKS];
     float al[NT];
@@ -747,7 +751,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(
     for (int nt = 0; nt < NT; ++nt) {
       const int tok = 16 * nt + n;
       const bool tv = tok < L;
-      const size_t row = ((size_t)s * L + (tv ? tok : L - 1)) * H2;
+      const size_t row = ((size_t)sl_ * L + (tv ? tok : L - 1)) * H2;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
         const int k0 = 32 * ks + 8 * q;
@@ -755,7 +759,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(
         const u16x8_t v = *reinterpret_cast<const u16x8_t*>(hraw + row + (ok ? k0 : 0));
         hf[nt][ks] = ok ? v : u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
       }
-      const float a = alphas[(size_t)s * L + (tv ? tok : L - 1)];
+      const float a = alphas[(size_t)sl_ * L + (tv ? tok : L - 1)];
       al[nt] = tv ? a : 0.f;
     }
     float dev[NKS][8];
@@ -763,8 +767,8 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(
     for (int ks = 0; ks < NKS; ++ks) {
       const int k0 = 32 * ks + 8 * q;
       const bool ok = k0 < H2;
-      const float4 a = *reinterpret_cast<const float4*>(de + (size_t)s * H2 + (ok ? k0 : 0));
-      const float4 b = *reinterpret_cast<const float4*>(de + (size_t)s * H2 + (ok ? k0 : 0) + 4);
+      const float4 a = *reinterpret_cast<const float4*>(de + (size_t)sl_ * H2 + (ok ? k0 : 0));
+      const float4 b = *reinterpret_cast<const float4*>(de + (size_t)sl_ * H2 + (ok ? k0 : 0) + 4);
       const float z = ok ? 1.f : 0.f;
       dev[ks][0] = a.x * z; dev[ks][1] = a.y * z; dev[ks][2] = a.z * z; dev[ks][3] = a.w * z;
       dev[ks][4] = b.x * z; dev[ks][5] = b.y * z; dev[ks][6] = b.z * z; dev[ks][7] = b.w * z;
@@ -774,7 +778,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(
     for (int m = 0; m < MT; ++m) {
       const int i0 = 16 * m + 4 * q;
       const bool ok = i0 < H2;
-      const float4 a = *reinterpret_cast<const float4*>(de + (size_t)s * H2 + (ok ? i0 : 0));
+      const float4 a = *reinterpret_cast<const float4*>(de + (size_t)sl_ * H2 + (ok ? i0 : 0));
       dei[m][0] = ok ? a.x : 0.f; dei[m][1] = ok ? a.y : 0.f; dei[m][2] = ok ? a.z : 0.f; dei[m][3] = ok ? a.w : 0.f;
     }
     // ---- pass A (registers only): d(alpha)_t = de . H_t, sd = sum_t alpha_t d(alpha)_t
@@ -852,6 +856,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(
       }
       // stage this tile's H (features) and dP columns for the dW1 K-step
       const int col = 16 * (tc & 1) + n;
+      if (INA_AB2_EXP == 2) continue;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll

@@ -41,11 +41,29 @@ INA_DEVICE f32x4_t relu4(const f32x4_t& x) {
   return f32x4_t{fmaxf(x[0], 0.f), fmaxf(x[1], 0.f), fmaxf(x[2], 0.f), fmaxf(x[3], 0.f)};
 }
 INA_DEVICE int kmap32(int q, int j) { return 16 * (j >> 2) + 4 * q + (j & 3); }
+// Unconditional load from a clamped index, zero outside: a lane-dependent branch around each load
+// made hipcc wait vmcnt(0) per element (60-400 serialized L2 round trips in the prologues).
+// (multiply by 0/1 rather than select: a select lets LLVM sink the load back under a branch)
+INA_DEVICE float ldz(const float* __restrict__ p, bool ok, long idx) {
+  return p[ok ? idx : 0] * (ok ? 1.f : 0.f);
+}
+// 4 consecutive floats p[idx .. idx + 3] (idx % 4 == 0) -> bf16 elements j0 .. j0 + 3 of f (zeros if !ok)
+INA_DEVICE void ld4bf(const float* __restrict__ p, bool ok, long idx, u16x8_t& f, int j0) {
+  const float4 v = *reinterpret_cast<const float4*>(p + (ok ? idx : 0));
+  const float z = ok ? 1.f : 0.f;
+  f[j0] = f2bf(v.x * z);
+  f[j0 + 1] = f2bf(v.y * z);
+  f[j0 + 2] = f2bf(v.z * z);
+  f[j0 + 3] = f2bf(v.w * z);
+}
 constexpr f32x4_t Z4 = {0.f, 0.f, 0.f, 0.f};
 
 }  // namespace
 
 
+#ifndef INA_NTN_BWD_LD
+#define INA_NTN_BWD_LD 1   // branch-free vectorized prologue loads in ntn_bwd (153 vs 160 us despite 188 B of spills; 0 = the branchy per-element loads)
+#endif
 constexpr int NTN_WAVES = 8;
 constexpr int NTN_THREADS = NTN_WAVES * 64;
 
@@ -97,13 +115,14 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_fwd_kernel(const float* __res
     const bool act = ep < E;
     const int epc = act ? ep : E - 1;
     const long rq0 = (long)epc * (N * K + NQ) + N * K;
+    // H % 8 == 0 (host check): every 4-feature run is in or out of range as a whole -> float4 loads
     u16x8_t Cf[NKA];
 #pragma unroll
     for (int ka = 0; ka < NKA; ++ka)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int a = 32 * ka + 8 * q + j;
-        Cf[ka][j] = (n < N && a < H) ? f2bf(cls[((long)epc * N + n) * H + a]) : (unsigned short)0;
+      for (int h4 = 0; h4 < 2; ++h4) {
+        const int a = 32 * ka + 8 * q + 4 * h4;
+        ld4bf(cls, n < N && a < H, ((long)epc * N + n) * H + a, Cf[ka], 4 * h4);
       }
     u16x8_t Qf[QT][NKB];
 #pragma unroll
@@ -111,9 +130,9 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_fwd_kernel(const float* __res
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int qi = 16 * qt + n, b = 32 * kb + kmap32(q, j);
-          Qf[qt][kb][j] = (qi < NQ && b < H) ? f2bf(e[(rq0 + qi) * H + b]) : (unsigned short)0;
+        for (int h4 = 0; h4 < 2; ++h4) {   // kmap32: elements 4 h4 .. +3 = features 32 kb + 16 h4 + 4q .. +3
+          const int qi = 16 * qt + n, b = 32 * kb + 16 * h4 + 4 * q;
+          ld4bf(e, qi < NQ && b < H, (rq0 + qi) * H + b, Qf[qt][kb], 4 * h4);
         }
     f32x4_t Lg[QT];
 #pragma unroll
@@ -210,6 +229,72 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
     const int epc = act ? ep : E - 1;
     const long rq0 = (long)epc * (N * K + NQ) + N * K;
     const float* dze = dz + (long)epc * NQ * N;
+#if INA_NTN_BWD_LD
+    u16x8_t Cf[NKA];
+#pragma unroll
+    for (int ka = 0; ka < NKA; ++ka)
+#pragma unroll
+      for (int h4 = 0; h4 < 2; ++h4) {
+        const int a = 32 * ka + 8 * q + 4 * h4;
+        ld4bf(cls, n < N && a < H, ((long)epc * N + n) * H + a, Cf[ka], 4 * h4);
+      }
+    if (cls_bf && act && n < N) {
+#pragma unroll
+      for (int ka = 0; ka < NKA; ++ka) {
+        const int a = 32 * ka + 8 * q;
+        if (a < H) *reinterpret_cast<u16x8_t*>(cls_bf + ((long)ep * N + n) * H + a) = Cf[ka];
+      }
+    }
+    u16x8_t Qf[QT][NKB];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int h4 = 0; h4 < 2; ++h4) {
+          const int qi = 16 * qt + n, b = 32 * kb + 16 * h4 + 4 * q;
+          ld4bf(e, qi < NQ && b < H, (rq0 + qi) * H + b, Qf[qt][kb], 4 * h4);
+        }
+    // Q^T as the A operand over queries: A[i = b][k = query (kmap32)]
+    __builtin_amdgcn_sched_barrier(0);   // load groups in turn: bounded registers in flight
+    u16x8_t QTf[MTH][KQ];
+#pragma unroll
+    for (int mb = 0; mb < MTH; ++mb)
+#pragma unroll
+      for (int kq = 0; kq < KQ; ++kq)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int b = 16 * mb + n, qi = 32 * kq + kmap32(q, j);
+          QTf[mb][kq][j] = f2bf(ldz(e, qi < NQ && b < H, (rq0 + qi) * H + b));
+        }
+    __builtin_amdgcn_sched_barrier(0);
+    u16x8_t dzA[QT];           // A[i = query][k = c']
+    u16x8_t dzB[KQ];           // B[k = query (kmap32)][j = c']
+    f32x4_t dzC[QT], dzR[QT];  // accumulator layouts: dzC rows c / cols query, dzR rows query / cols c
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int qi = 16 * qt + n, cp = 8 * q + j;
+        dzA[qt][j] = f2bf(gs * ldz(dze, qi < NQ && cp < N, qi * N + cp));
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = 4 * q + r, qi = 16 * qt + n;
+        dzC[qt][r] = gs * ldz(dze, c < N && qi < NQ, qi * N + c);
+        const int qr = 16 * qt + 4 * q + r;
+        dzR[qt][r] = gs * ldz(dze, n < N && qr < NQ, qr * N + n);
+      }
+    }
+#pragma unroll
+    for (int kq = 0; kq < KQ; ++kq)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int qi = 32 * kq + kmap32(q, j);
+        dzB[kq][j] = f2bf(gs * ldz(dze, qi < NQ && n < N, qi * N + n));
+      }
+    __builtin_amdgcn_sched_barrier(0);
+#else
     u16x8_t Cf[NKA];
 #pragma unroll
     for (int ka = 0; ka < NKA; ++ka)
@@ -265,6 +350,7 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
         const int qi = 32 * kq + kmap32(q, j);
         dzB[kq][j] = (qi < NQ && n < N) ? f2bf(gs * dze[qi * N + n]) : (unsigned short)0;
       }
+#endif
     f32x4_t dCT[MTH], dQT[MTH][QT];
 #pragma unroll
     for (int m = 0; m < MTH; ++m) {
