@@ -674,47 +674,116 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
-// bf16 backward, v2: 8-wave workgroups, weight fragments shared in LDS, every load of a sentence
-// issued up front (H tiles kept in registers for both passes), d(alpha) from the same registers,
-// dW1 accumulated in 32-token K-steps through a small wave-private LDS transpose.
+// bf16 backward, v3 (4-wave workgroups, one sentence per wave at a time, persistent grid):
+//  * the NEXT sentence's H rows / alphas / de land in a wave-private LDS buffer by LDS-DMA
+//    (global_load_lds) while the current one is processed: the HBM latency of the per-sentence
+//    loads is off the critical path (v2 issued them at the top of each sentence: ~70 us of 317);
+//  * dW1 = sum_t H_t^T dP_t per 16-token tile with v_mfma_f32_16x16x16_bf16, both operands read by
+//    ds_read_b64_tr_b16 (hardware transpose): the A operand straight from the prefetched natural
+//    H image, the B operand from a [16 tokens][ROWS] dP image written with 8-B stores (v2 staged
+//    both through per-element 16-bit LDS stores: 84 ds_write_b16 per sentence);
+//  * weight fragments shared by the block in LDS, as before.
 // slab per block: [dW1 (H2*H2, row i, col j) | db1 (H2) | dw2 (H2)]
-constexpr int AB2_WAVES = 4;
-#ifndef INA_AB2_EXP
-#define INA_AB2_EXP 0   // timing experiments: 1 = loads from a few cached sentences, 2 = skip dW1 staging
-#endif
+// ------------------------------------------------------------------------------------------
+constexpr int AB3_WAVES = 4;
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
 
 template <int U, int NT>
-__host__ __device__ constexpr int ab2_rows() { return ((2 * U + 15) / 16) * 16; }
-constexpr int AB2_RS = 40;   // staging row stride (32 tokens + 8 pad), bf16 elements
+struct AB3 {
+  static constexpr int H2 = 2 * U, MT = (H2 + 15) / 16, ROWS = MT * 16;
+  static constexpr int NKS = (H2 + 31) / 32, NKS2 = (4 * MT + 7) / 8;
+  static constexpr int TOK = NT * 16;                                  // image rows (tokens, zero padded)
+  static constexpr int DEP = (32 * NKS > ROWS ? 32 * NKS : ROWS);      // de floats (zero padded)
+  static constexpr int HIMG = TOK * H2 * 2;                            // bytes, bf16 [TOK][H2]
+  static constexpr int BUF = HIMG + TOK * 4 + DEP * 4;                 // H image | alphas | de
+  static constexpr int DPI = 16 * ROWS * 2;                            // bf16 dP image [16][ROWS]
+  static constexpr int WAVE = 2 * BUF + DPI;
+  static constexpr int NA = MT * NKS * 64, NA2 = MT * NKS2 * 64;
+  static constexpr int HEAD = ((NA + NA2) * 16 + 2 * ROWS * 4 + 15) / 16 * 16;
+  static_assert(HIMG % 16 == 0 && BUF % 16 == 0 && WAVE % 16 == 0, "16-B LDS carve");
+};
+
+// LDS-DMA (global_load_lds: each active lane's 16 / 4 bytes land at M0 + lane * size) issued by
+// inline asm: through the builtin, LLVM's waitcnt pass assumes the in-flight DMA may alias every
+// later LDS access of the kernel and waits vmcnt(0) before them, serialising the prefetch.  The
+// kernel synchronises explicitly instead (s_waitcnt vmcnt(0) at the top of each sentence), and no
+// other code in it uses M0.  An asm VMEM op unknown to the compiler can only make the compiler's
+// own vmcnt waits longer, never shorter (in-order retirement), so its loads stay correct.
+INA_DEVICE uint32_t lds_off(const void* p) {   // generic pointer into LDS -> 32-bit LDS address (M0)
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+INA_DEVICE void lds_dma16(const void* g, const void* lds_wave_base) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds_wave_base));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory");
+}
+INA_DEVICE void lds_dma4(const void* g, const void* lds_wave_base) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds_wave_base));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(m0) : "memory");
+}
+// fp32 values of the prefetch buffer read through 16-bit vector types: with float-typed reads LLVM
+// treats them as possibly aliasing the in-flight LDS-DMA into the other buffer and inserts a full
+// vmcnt(0) wait before them (the prefetch latency back on the critical path)
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+INA_DEVICE float ldsf(const float* p) {
+  const u16x2_t v = *reinterpret_cast<const u16x2_t*>(p);
+  return __builtin_bit_cast(float, (uint32_t)v[0] | ((uint32_t)v[1] << 16));
+}
+INA_DEVICE void ldsf4(const float* p, float* o) {
+  const u16x8_t v = *reinterpret_cast<const u16x8_t*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = __builtin_bit_cast(float, (uint32_t)v[2 * i] | ((uint32_t)v[2 * i + 1] << 16));
+}
+// order this wave's LDS accesses without a memory fence: the wave's own LDS operations execute in
+// order in hardware, and a fence would also wait for the in-flight prefetch DMA (vmcnt(0))
+INA_DEVICE void lds_order() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+INA_DEVICE s16x4_t tr_read(const unsigned short* lds_addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)lds_addr);
+}
+INA_DEVICE f32x4_t mfma16_bf16(const s16x4_t& a, const s16x4_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
 
 template <int U, int NT>
-__global__ __launch_bounds__(256) void attn_bwd2_kernel(
+__global__ __launch_bounds__(256) void attn_bwd3_kernel(
     const unsigned short* __restrict__ hraw, int S, int L, const u16x8_t* __restrict__ w1pack,
     const u16x8_t* __restrict__ w1tpack, const float* __restrict__ b1, const float* __restrict__ w2,
     const float* __restrict__ de, const float* __restrict__ alphas, unsigned short* __restrict__ dHraw,
     float* __restrict__ slab) {
-  using Sh = AShape<U, NT, true>;
-  constexpr int H2 = Sh::H2, NKS = Sh::NKS, MT = Sh::MT, NKS2 = Sh::NKS2;
-  constexpr int ROWS = MT * 16;
-  constexpr int NA = MT * NKS * 64, NA2 = MT * NKS2 * 64;
+  using C = AB3<U, NT>;
+  constexpr int H2 = C::H2, NKS = C::NKS, MT = C::MT, NKS2 = C::NKS2, ROWS = C::ROWS, TOK = C::TOK;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = lane >> 4, n = lane & 15;
-  const int gw = blockIdx.x * AB2_WAVES + wave, nw = gridDim.x * AB2_WAVES;
+  const int gw = blockIdx.x * AB3_WAVES + wave, nw = gridDim.x * AB3_WAVES;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   u16x8_t* lA = reinterpret_cast<u16x8_t*>(smem);
-  u16x8_t* lAT = lA + NA;
-  float* lbw = reinterpret_cast<float*>(lAT + NA2);           // [b1 | w2] padded to ROWS each
-  unsigned short* stg = reinterpret_cast<unsigned short*>(lbw + 2 * ROWS) + (size_t)wave * 2 * ROWS * AB2_RS;
-  unsigned short* HT = stg;                                    // [feature i][token col]
-  unsigned short* DPT = stg + ROWS * AB2_RS;                   // [j][token col]
-  for (int i = threadIdx.x; i < NA; i += 256) lA[i] = w1pack[i];
-  for (int i = threadIdx.x; i < NA2; i += 256) lAT[i] = w1tpack[i];
+  u16x8_t* lAT = lA + C::NA;
+  float* lbw = reinterpret_cast<float*>(lAT + C::NA2);           // [b1 | w2] padded to ROWS each
+  unsigned char* wbase = smem + C::HEAD + (size_t)wave * C::WAVE;
+  unsigned short* dpi = reinterpret_cast<unsigned short*>(wbase + 2 * C::BUF);   // dP image [16][ROWS]
+  for (int i = threadIdx.x; i < C::NA; i += 256) lA[i] = w1pack[i];
+  for (int i = threadIdx.x; i < C::NA2; i += 256) lAT[i] = w1tpack[i];
   for (int i = threadIdx.x; i < ROWS; i += 256) {
     lbw[i] = i < H2 ? b1[i] : 0.f;
     lbw[ROWS + i] = i < H2 ? w2[i] : 0.f;
   }
-  for (int i = lane; i < 2 * ROWS * AB2_RS; i += 64) stg[i] = 0;
+  // zero the wave's buffers once: image rows >= L, alphas >= L and de >= H2 are never written by
+  // the DMA and must read as 0 (padding tokens / features)
+  for (int i = lane; i < C::WAVE / 16; i += 64) reinterpret_cast<uint4*>(wbase)[i] = make_uint4(0, 0, 0, 0);
   __syncthreads();
+
+  // one sentence's rows -> buffer bf (wave-uniform); lanes past the data stay inactive
+  const int hbytes = L * H2 * 2;
+  auto prefetch = [&](int s, int bf) {
+    unsigned char* bb = wbase + bf * C::BUF;
+    const unsigned char* hs = reinterpret_cast<const unsigned char*>(hraw) + (size_t)s * hbytes;
+    for (int k = 0; k * 1024 < hbytes; ++k)
+      if (k * 1024 + lane * 16 < hbytes) lds_dma16(hs + k * 1024 + lane * 16, bb + k * 1024);
+    if (lane < L) lds_dma4(alphas + (size_t)s * L + lane, bb + C::HIMG);
+    if (lane < H2) lds_dma4(de + (size_t)s * H2 + lane, bb + C::HIMG + TOK * 4);
+  };
 
   f32x4_t accW[MT][MT];
 #pragma unroll
@@ -726,62 +795,43 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int r = 0; r < 4; ++r) dw2a[m][r] = db1a[m][r] = 0.f;
-  int tc = 0;  // tiles staged by this wave (column half = tc & 1)
+  // transposed-read lane roles: lane 4 q' + p of its 16-lane group g reads row (token) 4 g + q',
+  // columns 4 p .. 4 p + 3 of a 4 x 16 block
+  const int trow = 4 * q + ((lane & 15) >> 2), tcol = 4 * (lane & 3);
 
-  auto flush = [&]() {
-    wave_lds_sync();
-    u16x8_t fb[MT];
-#pragma unroll
-    for (int b = 0; b < MT; ++b) fb[b] = *reinterpret_cast<const u16x8_t*>(&DPT[(16 * b + n) * AB2_RS + 8 * q]);
-#pragma unroll
-    for (int a = 0; a < MT; ++a) {
-      const u16x8_t fa = *reinterpret_cast<const u16x8_t*>(&HT[(16 * a + n) * AB2_RS + 8 * q]);
-#pragma unroll
-      for (int b = 0; b < MT; ++b) accW[a][b] = mfma_bf16(fa, fb[b], accW[a][b]);
-    }
-    wave_lds_sync();
-  };
-
-  for (int s = gw; s < S; s += nw) {
-    const int sl_ = INA_AB2_EXP == 1 ? (gw & 255) : s;   // load source (experiment 1: L2-resident)
-    // ---- every load of the sentence first: H tiles (bf16 MFMA operands), de, alphas
+  int bf = 0;
+  if (gw < S) prefetch(gw, 0);
+  for (int s = gw; s < S; s += nw, bf ^= 1) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // this buffer landed; old reads done
+    if (s + nw < S) prefetch(s + nw, bf ^ 1);
+    const unsigned char* bb = wbase + bf * C::BUF;
+    const unsigned short* img = reinterpret_cast<const unsigned short*>(bb);
+    const float* alv_l = reinterpret_cast<const float*>(bb + C::HIMG);
+    const float* de_l = reinterpret_cast<const float*>(bb + C::HIMG + TOK * 4);
+    // ---- the sentence's operands from LDS
     u16x8_t hf[NT][NKS];
     float al[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int tok = 16 * nt + n;
-      const bool tv = tok < L;
-      const size_t row = ((size_t)sl_ * L + (tv ? tok : L - 1)) * H2;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
         const int k0 = 32 * ks + 8 * q;
-        const bool ok = tv && (k0 < H2);
-        const u16x8_t v = *reinterpret_cast<const u16x8_t*>(hraw + row + (ok ? k0 : 0));
-        hf[nt][ks] = ok ? v : u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        const u16x8_t v = *reinterpret_cast<const u16x8_t*>(img + tok * H2 + (k0 < H2 ? k0 : 0));
+        hf[nt][ks] = k0 < H2 ? v : u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
       }
-      const float a = alphas[(size_t)sl_ * L + (tv ? tok : L - 1)];
-      al[nt] = tv ? a : 0.f;
+      al[nt] = ldsf(alv_l + tok);   // 0 for tok >= L
     }
     float dev[NKS][8];
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      const int k0 = 32 * ks + 8 * q;
-      const bool ok = k0 < H2;
-      const float4 a = *reinterpret_cast<const float4*>(de + (size_t)sl_ * H2 + (ok ? k0 : 0));
-      const float4 b = *reinterpret_cast<const float4*>(de + (size_t)sl_ * H2 + (ok ? k0 : 0) + 4);
-      const float z = ok ? 1.f : 0.f;
-      dev[ks][0] = a.x * z; dev[ks][1] = a.y * z; dev[ks][2] = a.z * z; dev[ks][3] = a.w * z;
-      dev[ks][4] = b.x * z; dev[ks][5] = b.y * z; dev[ks][6] = b.z * z; dev[ks][7] = b.w * z;
+      ldsf4(de_l + 32 * ks + 8 * q, &dev[ks][0]);
+      ldsf4(de_l + 32 * ks + 8 * q + 4, &dev[ks][4]);
     }
     float dei[MT][4];
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const int i0 = 16 * m + 4 * q;
-      const bool ok = i0 < H2;
-      const float4 a = *reinterpret_cast<const float4*>(de + (size_t)sl_ * H2 + (ok ? i0 : 0));
-      dei[m][0] = ok ? a.x : 0.f; dei[m][1] = ok ? a.y : 0.f; dei[m][2] = ok ? a.z : 0.f; dei[m][3] = ok ? a.w : 0.f;
-    }
-    // ---- pass A (registers only): d(alpha)_t = de . H_t, sd = sum_t alpha_t d(alpha)_t
+    for (int m = 0; m < MT; ++m) ldsf4(de_l + 16 * m + 4 * q, dei[m]);
+    // ---- pass A: d(alpha)_t = de . H_t, sd = sum_t alpha_t d(alpha)_t
     float da[NT];
     float sd = 0.f;
 #pragma unroll
@@ -795,8 +845,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(
       sd += al[nt] * da[nt];
     }
     sd = group16_sum(sd);
-    // ---- pass B per token tile (not unrolled: one tile's temporaries live at a time; the tile's
-    // registers are picked with compile-time selects, so no scratch indexing)
+    // ---- pass B per 16-token tile (not unrolled; the tile's registers picked with compile-time selects)
 #pragma unroll 1
     for (int nt = 0; nt < NT; ++nt) {
       asm volatile("" ::: "memory");   // re-read the LDS weight fragments per tile (no hoisting)
@@ -813,16 +862,16 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(
           for (int ks = 0; ks < NKS; ++ks) ht[ks] = hf[j][ks];
         }
       const int tok = 16 * nt + n;
-      const float ds = alv * (dav - sd);
+      const float ds = alv * (dav - sd);   // 0 for padding tokens (alpha 0)
       float dp[MT][4];
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        const float4 bj = *reinterpret_cast<const float4*>(&lbw[16 * m + 4 * q]);
-        const float4 wj = *reinterpret_cast<const float4*>(&lbw[ROWS + 16 * m + 4 * q]);
-        f32x4_t acc = {bj.x, bj.y, bj.z, bj.w};
+        float bj[4], wv[4];
+        ldsf4(&lbw[16 * m + 4 * q], bj);
+        ldsf4(&lbw[ROWS + 16 * m + 4 * q], wv);
+        f32x4_t acc = {bj[0], bj[1], bj[2], bj[3]};
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) acc = mfma_bf16(lA[(m * NKS + ks) * 64 + lane], ht[ks], acc);
-        const float wv[4] = {wj.x, wj.y, wj.z, wj.w};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float pr = tanhf_(acc[r]);
@@ -854,33 +903,28 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(
           *reinterpret_cast<uint2*>(dst + 16 * m + 4 * q) = pk;
         }
       }
-      // stage this tile's H (features) and dP columns for the dW1 K-step
-      const int col = 16 * (tc & 1) + n;
-      if (INA_AB2_EXP == 2) continue;
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = 32 * ks + 8 * q + j;
-          if (k < ROWS) HT[k * AB2_RS + col] = ht[ks][j];
-        }
+      // dP tile -> [token n][j] image (8-B stores), then dW1 += H_tile^T dP_tile, K = the 16 tokens
 #pragma unroll
       for (int m = 0; m < MT; ++m)
+        *reinterpret_cast<u16x4_t*>(dpi + n * ROWS + 16 * m + 4 * q) =
+            u16x4_t{f2bf(dp[m][0]), f2bf(dp[m][1]), f2bf(dp[m][2]), f2bf(dp[m][3])};
+      lds_order();
+      s16x4_t fb[MT];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) DPT[(16 * m + 4 * q + r) * AB2_RS + col] = f2bf(dp[m][r]);
-      if (tc & 1) flush();
-      ++tc;
+      for (int b = 0; b < MT; ++b) fb[b] = tr_read(dpi + trow * ROWS + 16 * b + tcol);
+#pragma unroll
+      for (int a = 0; a < MT; ++a) {
+        // features 16 a + tcol .. + 3 of token 16 nt + trow (columns >= H2 read the next row: they only
+        // feed dW1 rows >= H2, which are dropped)
+        const s16x4_t fa = tr_read(img + (16 * nt + trow) * H2 + 16 * a + tcol);
+#pragma unroll
+        for (int b = 0; b < MT; ++b) accW[a][b] = mfma16_bf16(fa, fb[b], accW[a][b]);
+      }
+      lds_order();
     }
   }
-  if (tc & 1) {   // half-filled last K-step: clear the other half, then flush
-#pragma unroll
-    for (int k = 0; k < ROWS; k += 4) {
-      HT[(k + q) * AB2_RS + 16 + n] = 0;
-      DPT[(k + q) * AB2_RS + 16 + n] = 0;
-    }
-    flush();
-  }
-  // ---- workgroup reduction into the slab (reuse the packs' LDS as fp32 after a barrier)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA in flight into the reused LDS
+  // ---- workgroup reduction into the slab (reuse the LDS as fp32 after a barrier)
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);
   const int NS = H2 * H2 + 2 * H2;
@@ -940,12 +984,11 @@ static int attn_fwd_t(const AttnArgs& a, hipStream_t st) {
   INA_CHECK_LAUNCH();
   return 0;
 }
-size_t attn_bwd2_lds_bytes(int U, int NT) {
-  const int H2 = 2 * U, MT = (H2 + 15) / 16, ROWS = MT * 16;
-  const int NKS = ((H2 + 31) / 32), NKS2 = (4 * MT + 7) / 8;
-  size_t b = (size_t)(MT * NKS * 64 + MT * NKS2 * 64) * 16 + (size_t)2 * ROWS * 4 +
-             (size_t)AB2_WAVES * 2 * ROWS * AB2_RS * 2;
-  const size_t r = (size_t)(H2 * H2 + 2 * H2) * 4;
+template <int U, int NT>
+static size_t attn_bwd3_lds_bytes() {
+  using C = AB3<U, NT>;
+  const size_t b = (size_t)C::HEAD + (size_t)AB3_WAVES * C::WAVE;
+  const size_t r = (size_t)(C::H2 * C::H2 + 2 * C::H2) * 4;
   return b > r ? b : r;
 }
 
@@ -953,11 +996,12 @@ template <int U, int NT, bool BF16>
 static int attn_bwd_t(const AttnArgs& a, hipStream_t st) {
   using F = FT<BF16>;
   if constexpr (BF16) {
-    const size_t lds2 = attn_bwd2_lds_bytes(U, NT);
-    if (lds2 > 64 * 1024)
-      (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<U, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    const size_t lds3 = attn_bwd3_lds_bytes<U, NT>();
+    if (lds3 > 160 * 1024) return -1;
+    if (lds3 > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<U, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
-    hipLaunchKernelGGL((attn_bwd2_kernel<U, NT>), dim3(a.blocks), dim3(256), lds2, st,
+    hipLaunchKernelGGL((attn_bwd3_kernel<U, NT>), dim3(a.blocks), dim3(256), lds3, st,
                        (const unsigned short*)a.hraw, a.S, a.L, (const u16x8_t*)a.w1pack,
                        (const u16x8_t*)a.w1tpack, a.b1, a.w2, a.de, a.alphas, (unsigned short*)a.dHraw, a.slab);
     INA_CHECK_LAUNCH();
