@@ -372,9 +372,12 @@ std::tuple<Tensor, Tensor> attn_bwd(const Tensor& hraw, const Tensor& inst, cons
   TORCH_CHECK(alphas.size(0) == S && alphas.size(1) == L, "ina.attn_bwd: alphas shape");
   const int64_t NT = (L + 15) / 16;
   TORCH_CHECK(NT >= 1 && NT <= 4, "ina.attn_bwd: L must be <= 64");
-  // 4-wave workgroups (bf16: attn_bwd2, LDS-shared weight fragments)
+  // 4-wave workgroups; bf16 (attn_bwd3, persistent): by default exactly the resident workgroups
   const int64_t wpb = 4;
-  if (blocks <= 0) blocks = 1024;
+  if (blocks <= 0) {
+    blocks = ina::attn_bwd_resident_blocks((int)U, (int)NT, bf16);
+    if (blocks <= 0) blocks = 1024;
+  }
   blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, (S + wpb - 1) / wpb));
   auto dH = at::empty({S, L, H2}, de.options().dtype(bf16 ? at::kBFloat16 : at::kFloat));
   auto slab = at::empty({blocks, H2 * H2 + 2 * H2}, de.options());

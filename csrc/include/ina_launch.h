@@ -75,6 +75,7 @@ struct AttnArgs {
 };
 int attn_fwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st);
 int attn_bwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st);
+int attn_bwd_resident_blocks(int U, int NT, bool bf16);
 // bf16: lstm_fwd step records (+ keep bits) -> natural rows hnat AND the attention forward (e, alphas)
 size_t hnat_attn_lds_bytes(int U, int L, bool drop);
 int hnat_attn(const void* rec, const unsigned char* dmask, float inv_kp, void* hnat, const AttnArgs& a, int U,

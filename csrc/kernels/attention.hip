@@ -808,58 +808,55 @@ __global__ __launch_bounds__(256) void attn_bwd3_kernel(
     const unsigned short* img = reinterpret_cast<const unsigned short*>(bb);
     const float* alv_l = reinterpret_cast<const float*>(bb + C::HIMG);
     const float* de_l = reinterpret_cast<const float*>(bb + C::HIMG + TOK * 4);
-    // ---- the sentence's operands from LDS
-    u16x8_t hf[NT][NKS];
-    float al[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
+    // ---- the sentence's operands from LDS (H tiles are re-read per pass: fewer live registers)
+    auto ld_h = [&](int nt, u16x8_t* ht) __attribute__((always_inline)) {
       const int tok = 16 * nt + n;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
         const int k0 = 32 * ks + 8 * q;
         const u16x8_t v = *reinterpret_cast<const u16x8_t*>(img + tok * H2 + (k0 < H2 ? k0 : 0));
-        hf[nt][ks] = k0 < H2 ? v : u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        ht[ks] = k0 < H2 ? v : u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
       }
-      al[nt] = ldsf(alv_l + tok);   // 0 for tok >= L
-    }
-    float dev[NKS][8];
+    };
+    float al[NT];
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      ldsf4(de_l + 32 * ks + 8 * q, &dev[ks][0]);
-      ldsf4(de_l + 32 * ks + 8 * q + 4, &dev[ks][4]);
-    }
-    float dei[MT][4];
-#pragma unroll
-    for (int m = 0; m < MT; ++m) ldsf4(de_l + 16 * m + 4 * q, dei[m]);
+    for (int nt = 0; nt < NT; ++nt) al[nt] = ldsf(alv_l + 16 * nt + n);   // 0 for tok >= L
     // ---- pass A: d(alpha)_t = de . H_t, sd = sum_t alpha_t d(alpha)_t
     float da[NT];
     float sd = 0.f;
+    {
+      float dev[NKS][8];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      float d = 0.f;
+      for (int ks = 0; ks < NKS; ++ks) {
+        ldsf4(de_l + 32 * ks + 8 * q, &dev[ks][0]);
+        ldsf4(de_l + 32 * ks + 8 * q + 4, &dev[ks][4]);
+      }
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
+      for (int nt = 0; nt < NT; ++nt) {
+        u16x8_t ht[NKS];
+        ld_h(nt, ht);
+        float d = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d += dev[ks][j] * bf2f(hf[nt][ks][j]);
-      da[nt] = cross_group_sum(d);
-      sd += al[nt] * da[nt];
+        for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d += dev[ks][j] * bf2f(ht[ks][j]);
+        da[nt] = cross_group_sum(d);
+        sd += al[nt] * da[nt];
+      }
     }
     sd = group16_sum(sd);
-    // ---- pass B per 16-token tile (not unrolled; the tile's registers picked with compile-time selects)
+    // ---- pass B per 16-token tile (not unrolled; the tile's scalars picked with compile-time selects)
 #pragma unroll 1
     for (int nt = 0; nt < NT; ++nt) {
-      asm volatile("" ::: "memory");   // re-read the LDS weight fragments per tile (no hoisting)
+      asm volatile("" ::: "memory");   // re-read the LDS operands per tile (no hoisting)
       u16x8_t ht[NKS];
+      ld_h(nt, ht);
       float alv = al[0], dav = da[0];
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) ht[ks] = hf[0][ks];
 #pragma unroll
       for (int j = 1; j < NT; ++j)
         if (j == nt) {
           alv = al[j];
           dav = da[j];
-#pragma unroll
-          for (int ks = 0; ks < NKS; ++ks) ht[ks] = hf[j][ks];
         }
       const int tok = 16 * nt + n;
       const float ds = alv * (dav - sd);   // 0 for padding tokens (alpha 0)
@@ -898,8 +895,10 @@ __global__ __launch_bounds__(256) void attn_bwd3_kernel(
         for (int ks = 0; ks < NKS2; ++ks) acc = mfma_bf16(lAT[(m * NKS2 + ks) * 64 + lane], B2[ks], acc);
         if (tok < L && 16 * m + 4 * q < H2) {
           uint2 pk;
-          pk.x = (uint32_t)f2bf(acc[0] + alv * dei[m][0]) | ((uint32_t)f2bf(acc[1] + alv * dei[m][1]) << 16);
-          pk.y = (uint32_t)f2bf(acc[2] + alv * dei[m][2]) | ((uint32_t)f2bf(acc[3] + alv * dei[m][3]) << 16);
+          float dei[4];
+          ldsf4(de_l + 16 * m + 4 * q, dei);
+          pk.x = (uint32_t)f2bf(acc[0] + alv * dei[0]) | ((uint32_t)f2bf(acc[1] + alv * dei[1]) << 16);
+          pk.y = (uint32_t)f2bf(acc[2] + alv * dei[2]) | ((uint32_t)f2bf(acc[3] + alv * dei[3]) << 16);
           *reinterpret_cast<uint2*>(dst + 16 * m + 4 * q) = pk;
         }
       }
@@ -1067,6 +1066,39 @@ int hnat_attn(const void* rec, const unsigned char* dmask, float inv_kp, void* h
   INA_HA(8) INA_HA(20) INA_HA(32)
 #undef INA_HA
   return -1;
+}
+
+// Workgroups of the persistent bf16 backward that are resident at once (occupancy x CUs): the grid
+// is sized to exactly that, so every wave runs the same number of sentences in one round (a grid of
+// 1024 at 3 workgroups per CU ran 1.33 rounds).  0 = unknown (fp32 kernel / query failed).
+template <int U, int NT>
+static int attn_bwd3_resident() {
+  static int cached = -1;
+  if (cached >= 0) return cached;
+  const size_t lds3 = attn_bwd3_lds_bytes<U, NT>();
+  if (lds3 > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<U, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, attn_bwd3_kernel<U, NT>, 256, lds3) != hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    per_cu = cus = 0;
+  cached = per_cu * cus;
+  return cached;
+}
+int attn_bwd_resident_blocks(int U, int NT, bool bf16) {
+  if (!bf16) return 0;
+#define INA_AB3R(UV)                                 \
+  if (U == UV) {                                     \
+    if (NT == 1) return attn_bwd3_resident<UV, 1>(); \
+    if (NT == 2) return attn_bwd3_resident<UV, 2>(); \
+    if (NT == 3) return attn_bwd3_resident<UV, 3>(); \
+    if (NT == 4) return attn_bwd3_resident<UV, 4>(); \
+  }
+  INA_AB3R(8) INA_AB3R(20) INA_AB3R(32)
+#undef INA_AB3R
+  return 0;
 }
 
 int attn_fwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st) { INA_ATTN_DISPATCH(attn_fwd_t) }
