@@ -47,6 +47,7 @@ int lstm_fwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
 // [16 * tiles][L][2U], with the dropout keep bits [tiles][2][L][64] applied when dmask is non-null
 int h_natural(const void* rec, const unsigned char* dmask, float inv_kp, int S, int L, int U, void* hnat,
               hipStream_t st);
+int lstm_bwd_resident_blocks(int U, int NX, bool bf16, int L, int PD);
 int lstm_bwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
 // bf16 mode: reduce a.dxp into slab [blocks][2 tables][2L][PD] (needs 2L <= 128, 2PD <= 16)
 int pos_grad(const LstmArgs& a, int blocks, float* slab, hipStream_t st);

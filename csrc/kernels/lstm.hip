@@ -1130,6 +1130,34 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   }                                                                                  \
   return -1;
 
+// Resident workgroups of the persistent backward PER DIRECTION (occupancy x CUs / 2): the default grid,
+// so all of the recurrence's waves run in one round (a 512-per-direction grid at 2 workgroups per CU
+// ran two rounds of 3-4 tile groups per workgroup: critical path 8 groups for 6.25 of work).
+template <int U, int NX, bool BF16>
+static int bwd_resident_t(int L, int PD) {
+  static int cached[2][129][9];
+  const int Lc = L < 128 ? L : 128, Pc = PD < 8 ? PD : 8;
+  int& c = cached[BF16][Lc][Pc];
+  if (c > 0) return c;
+  const size_t lds = lstm_bwd_lds_bytes(U, NX, BF16, L, PD);
+  (void)hipFuncSetAttribute((const void*)lstm_bwd_kernel<U, NX, BF16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_kernel<U, NX, BF16>, 256, lds) != hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  c = per_cu * cus / 2;
+  return c;
+}
+int lstm_bwd_resident_blocks(int U, int NX, bool bf16, int L, int PD) {
+#define INA_BR(UV, NV)                                                     \
+  if (U == UV && NX == NV) return bf16 ? bwd_resident_t<UV, NV, true>(L, PD) : bwd_resident_t<UV, NV, false>(L, PD);
+  INA_BR(20, 4) INA_BR(20, 16) INA_BR(32, 4) INA_BR(32, 16) INA_BR(8, 4)
+#undef INA_BR
+  return 0;
+}
+
 int lstm_fwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st) { INA_LSTM_DISPATCH(launch_fwd_t) }
 int lstm_bwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st) { INA_LSTM_DISPATCH(launch_bwd_t) }
 
