@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--encoder", default="bilstm", choices=["bilstm", "bert"])
-    ap.add_argument("--episodes-per-gpu", type=int, default=0, help="default 8192 (bilstm: measured best of 2048..16384, ~3%% over 4096 and 13%% over 2048; ~10 GB of activations of the 288 GB) / 8 (bert)")
+    ap.add_argument("--episodes-per-gpu", type=int, default=0, help="default 8192 (bilstm: measured best of 2048..16384, ~3%% over 4096 and 13%% over 2048; peak_mem_gb in the output) / 8 (bert)")
     ap.add_argument("--way", type=int, default=0, help="default 5 (bilstm) / 10 (bert)")
     ap.add_argument("--shot", type=int, default=5)
     ap.add_argument("--query", type=int, default=5)
@@ -140,6 +140,7 @@ def main():
             },
             ("eval_accuracy" if evalm else "final_loss"): round(loss, 6),
             "params_in_sync": bool(in_sync),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2),
         }
         print(json.dumps(out))
         if args.profile_json:
