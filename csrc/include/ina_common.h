@@ -15,6 +15,7 @@
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x8_t __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 namespace ina {
@@ -34,6 +35,24 @@ INA_DEVICE f32x4_t mfma_bf16(const u16x8_t& a, const u16x8_t& b, const f32x4_t& 
 }
 INA_DEVICE f32x4_t mfma_f32(float a, float b, const f32x4_t& c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// v_mfma_f32_16x16x16_bf16: lane l holds A[row l&15][k = 4(l>>4) + j], B[k = 4(l>>4) + j][col l&15], j < 4
+INA_DEVICE f32x4_t mfma16_bf16(const s16x4_t& a, const s16x4_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+// ds_read_b64_tr_b16 (gfx950 hardware transpose, EXEC must be all ones).  From a row-major LDS
+// image [k rows][cols] of 16-bit values, each lane passing the address of
+//   row 4 (l>>4) + ((l&15)>>2), column c0 + 4 (l&3)       (8-byte aligned)
+// returns the 16x16x16 operand fragment {image[4(l>>4) + j][c0 + (l&15)], j < 4}: a [k][col] block
+// read as a B operand, or as the A operand of the transposed block.
+INA_DEVICE s16x4_t tr_read(const unsigned short* lds_addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)lds_addr);
+}
+// order this wave's LDS accesses without a memory fence: a wave's own LDS operations execute in
+// order in hardware, and a fence would also wait for every in-flight global load (vmcnt(0))
+INA_DEVICE void lds_order() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
 }
 
 // ------------------------------------------------------------------ math

@@ -686,7 +686,6 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
 // slab per block: [dW1 (H2*H2, row i, col j) | db1 (H2) | dw2 (H2)]
 // ------------------------------------------------------------------------------------------
 constexpr int AB3_WAVES = 4;
-typedef short s16x4_t __attribute__((ext_vector_type(4)));
 
 template <int U, int NT>
 struct AB3 {
@@ -733,18 +732,7 @@ INA_DEVICE void ldsf4(const float* p, float* o) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) o[i] = __builtin_bit_cast(float, (uint32_t)v[2 * i] | ((uint32_t)v[2 * i + 1] << 16));
 }
-// order this wave's LDS accesses without a memory fence: the wave's own LDS operations execute in
-// order in hardware, and a fence would also wait for the in-flight prefetch DMA (vmcnt(0))
-INA_DEVICE void lds_order() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
-INA_DEVICE s16x4_t tr_read(const unsigned short* lds_addr) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)lds_addr);
-}
-INA_DEVICE f32x4_t mfma16_bf16(const s16x4_t& a, const s16x4_t& b, const f32x4_t& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
-}
+// (lds_order: also keeps the compiler from waiting on the in-flight prefetch DMA)
 
 template <int U, int NT>
 __global__ __launch_bounds__(256) void attn_bwd3_kernel(

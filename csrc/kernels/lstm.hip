@@ -533,6 +533,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   elem* xp_all = reinterpret_cast<elem*>(smem + off);
   elem* dgT = xp_all + (size_t)wave * XROWS * RS;
   elem* xhT = dgT + GT * 16 * RS;
+  // bf16 dW staging: a [32 samples][GCP] dG image and a [32 samples][FCP] [x;h;1] image (two steps
+  // x 16 sequences), lane-permuted columns so each lane writes its values with a few 8-/4-byte
+  // stores (lane (q, n): row 16 (tau & 1) + n, dG columns q*4U4 + 4m + g4, XH columns q*NSLP + slot;
+  // the old [gate row][sample] staging took 20 + 9 ds_write_b16 per step).  Both MFMA operands come
+  // back through ds_read_b64_tr_b16 (K = the pair's 32 samples, 16x16x32: the 16x16x16 form with
+  // K = one step measured 25% slower, half the MFMA rate).
+  constexpr int NSLP = (U4 + NX + 1) & ~1;               // XH slots per lane: U4 h, NX x (+1 pad)
+  constexpr int FTA = BF16 ? (4 * NSLP + 1 + 15) / 16 : FTMAX;
+  constexpr int GCP = GT * 16 + 4, FCP = FTA * 16 + 4;   // +4 elements: row stride != 0 mod 32 banks
+  static_assert(!BF16 || 32 * (GCP + FCP) <= XROWS * RS, "bf16 dW images exceed the staging region");
+  unsigned short* dgI = reinterpret_cast<unsigned short*>(dgT);
+  unsigned short* xhI = dgI + 32 * GCP;
+  const int tcol = 4 * (n & 3);
   {
     size_t xp = (size_t)4 * XROWS * RS * sizeof(elem);
     const size_t red = (size_t)G4 * (4 * NX + U + 1) * sizeof(float);
@@ -551,7 +564,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   // zero the wave's transpose buffers once (pad rows / columns stay zero; bias row = 1)
   for (int i = lane; i < XROWS * RS; i += 64) dgT[i] = to_elem(0.f, (elem*)nullptr);
   wave_lds_sync();
-  for (int i = lane; i < 32; i += 64) xhT[(DIN + U) * RS + i] = to_elem(1.f, (elem*)nullptr);
+  if constexpr (BF16) {
+    if (lane < 32) xhI[lane * FCP + 4 * NSLP] = f2bf(1.f);   // bias column
+  } else {
+    for (int i = lane; i < 32; i += 64) xhT[(DIN + U) * RS + i] = to_elem(1.f, (elem*)nullptr);
+  }
   __syncthreads();
 
   float bm[NMT][4];   // gate biases of the lane's units (registers, not per-step LDS reads)
@@ -559,11 +576,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   for (int m = 0; m < NMT; ++m)
 #pragma unroll
     for (int r = 0; r < 4; ++r) bm[m][r] = lbias[r * U + 4 * m + q];
-  f32x4_t accw[GT][FTMAX];
+  f32x4_t accw[GT][FTA];
 #pragma unroll
   for (int a = 0; a < GT; ++a)
 #pragma unroll
-    for (int b = 0; b < FTMAX; ++b) accw[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < FTA; ++b) accw[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   XSrc xs[NX];
 #pragma unroll
@@ -641,12 +658,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
 #pragma unroll
     for (int m = 0; m < U4; ++m) dh_rec[m] = dc_rec[m] = 0.f;
     if (L & 1) {
-      // odd L: the tile's first dW chunk {L, L-1} is half filled; clear the dG columns of the missing
+      // odd L: the tile's first dW chunk {L, L-1} is half filled; clear the dG samples of the missing
       // step (they still hold the previous tile's last chunk)
+      if constexpr (BF16) {
 #pragma unroll
-      for (int m = 0; m < U4; ++m)
+        for (int m = 0; m < U4; ++m)
+          *reinterpret_cast<u16x4_t*>(dgI + (16 + n) * GCP + q * (4 * U4) + 4 * m) = u16x4_t{0, 0, 0, 0};
+      } else {
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) dgT[(g4 * U + 4 * m + q) * RS + n + 16] = to_elem(0.f, (elem*)nullptr);
+        for (int m = 0; m < U4; ++m)
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) dgT[(g4 * U + 4 * m + q) * RS + n + 16] = to_elem(0.f, (elem*)nullptr);
+      }
     }
     for (int tau = L - 1; tau >= 0; --tau) {
       const int wid = wid_c, p1 = p1_c, p2 = p2_c;
@@ -762,6 +785,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
             if (xs[xi].sel == 0) atomicAdd(&dwemb[(long)wrow * E + xs[xi].col], dslot[U4 + xi]);
         }
       }
+      if constexpr (BF16) {
+        // ---- stage dG / [x;h] (image row 16 * (tau & 1) + n; 8-/4-byte stores), and every second
+        // step dW += dG^T [x;h;1] over the pair's 32 samples
+        const int rr = 16 * (tau & 1) + n;
+        unsigned short* gi = dgI + rr * GCP + q * (4 * U4);
+#pragma unroll
+        for (int m = 0; m < U4; ++m)
+          *reinterpret_cast<u16x4_t*>(gi + 4 * m) =
+              u16x4_t{f2bf(dg[m][0]), f2bf(dg[m][1]), f2bf(dg[m][2]), f2bf(dg[m][3])};
+        float sl[NSLP];
+#pragma unroll
+        for (int s = 0; s < NSLP; ++s) sl[s] = s < U4 ? hp[s] : (s < U4 + NX ? xv[s - U4] : 0.f);
+        uint32_t* xi32 = reinterpret_cast<uint32_t*>(xhI + rr * FCP + q * NSLP);
+#pragma unroll
+        for (int p = 0; p < NSLP / 2; ++p) xi32[p] = (uint32_t)f2bf(sl[2 * p]) | ((uint32_t)f2bf(sl[2 * p + 1]) << 16);
+        if ((tau & 1) == 0) {
+          lds_order();
+          // 16x16x32 operands: two transposed reads, samples 8q..8q+3 and 8q+4..8q+7
+          auto tr8 = [&](const unsigned short* img, int stride, int c0) {
+            const s16x4_t lo = tr_read(img + (8 * q + (n >> 2)) * stride + c0 + tcol);
+            const s16x4_t hi = tr_read(img + (8 * q + 4 + (n >> 2)) * stride + c0 + tcol);
+            return u16x8_t{(unsigned short)lo[0], (unsigned short)lo[1], (unsigned short)lo[2], (unsigned short)lo[3],
+                           (unsigned short)hi[0], (unsigned short)hi[1], (unsigned short)hi[2], (unsigned short)hi[3]};
+          };
+          u16x8_t fbx[FTA];
+#pragma unroll
+          for (int b = 0; b < FTA; ++b) fbx[b] = tr8(xhI, FCP, 16 * b);
+#pragma unroll
+          for (int a = 0; a < GT; ++a) {
+            const u16x8_t fa = tr8(dgI, GCP, 16 * a);
+#pragma unroll
+            for (int b = 0; b < FTA; ++b) accw[a][b] = mfma_bf16(fa, fbx[b], accw[a][b]);
+          }
+          lds_order();   // the next steps' stores come after these reads (in-order LDS)
+        }
+      } else {
       // ---- stage (dG, XH) for the dW MFMA: sample column = n + 16 * (tau & 1)
       const int scol = n + 16 * (tau & 1);
 #pragma unroll
@@ -781,31 +840,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         // the first chunk (tau = L-1) is half filled; the other half is zero because every
         // flush clears the lane's dG columns below.
         wave_lds_sync();
-        if constexpr (BF16) {
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
 #pragma unroll
           for (int a = 0; a < GT; ++a) {
-            const u16x8_t fa = *reinterpret_cast<const u16x8_t*>(&dgT[(a * 16 + n) * RS + 8 * q]);
+            const float fa = from_elem(dgT[(a * 16 + n) * RS + 4 * kk + q]);
 #pragma unroll
-            for (int b = 0; b < FTMAX; ++b) {   // rows >= NF of xhT are zero: no runtime bound needed
-              const u16x8_t fb = *reinterpret_cast<const u16x8_t*>(&xhT[(b * 16 + n) * RS + 8 * q]);
-              accw[a][b] = mfma_bf16(fa, fb, accw[a][b]);
-            }
-          }
-        } else {
-#pragma unroll
-          for (int kk = 0; kk < 8; ++kk) {
-#pragma unroll
-            for (int a = 0; a < GT; ++a) {
-              const float fa = dgT[(a * 16 + n) * RS + 4 * kk + q];
-#pragma unroll
-              for (int b = 0; b < FTMAX; ++b) {
-                const float fb = xhT[(b * 16 + n) * RS + 4 * kk + q];
-                accw[a][b] = mfma_f32(fa, fb, accw[a][b]);
-              }
+            for (int b = 0; b < FTMAX; ++b) {
+              const float fb = from_elem(xhT[(b * 16 + n) * RS + 4 * kk + q]);
+              accw[a][b] = mfma_f32(fa, fb, accw[a][b]);
             }
           }
         }
         wave_lds_sync();   // every later chunk rewrites both column halves: no clearing needed
+      }
       }
       // ---- rotate the pipeline
 #pragma unroll
@@ -827,16 +875,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   const int REDN = G4 * NF;
   for (int i = threadIdx.x; i < REDN; i += 256) red[i] = 0.f;
   __syncthreads();
+  // bf16: un-permute the image columns (dG column c -> gate row, XH column -> feature; -1 = pad)
+  int fmap[FTA];
+#pragma unroll
+  for (int b = 0; b < FTA; ++b) {
+    const int c = b * 16 + n;
+    if constexpr (BF16) {
+      const int qq = c / NSLP, s = c - qq * NSLP;
+      fmap[b] = c == 4 * NSLP ? DIN + U
+                : c > 4 * NSLP ? -1
+                : s < U4       ? DIN + 4 * s + qq
+                : (s < U4 + NX && 4 * (s - U4) + qq < DIN) ? 4 * (s - U4) + qq
+                               : -1;
+    } else {
+      fmap[b] = (b < FT && c < NF) ? c : -1;
+    }
+  }
   ordered_wave_accumulate(wave, 4, [&] {   // deterministic summation order
 #pragma unroll
     for (int a = 0; a < GT; ++a)
 #pragma unroll
-      for (int b = 0; b < FTMAX; ++b)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int gc = a * 16 + 4 * q + r, f = b * 16 + n;
-          if (b < FT && gc < G4 && f < NF) red[gc * NF + f] += accw[a][b][r];
+      for (int r = 0; r < 4; ++r) {
+        const int c = a * 16 + 4 * q + r;
+        int gc = c;
+        if constexpr (BF16) {
+          const int qq = c / (4 * U4), rem = c - qq * (4 * U4);
+          gc = (rem & 3) * U + 4 * (rem >> 2) + qq;
         }
+        if (c >= G4) continue;
+#pragma unroll
+        for (int b = 0; b < FTA; ++b)
+          if (fmap[b] >= 0) red[gc * NF + fmap[b]] += accw[a][b][r];
+      }
   });
   float* slab = dw_slab + ((size_t)blockIdx.x * 2 + dir) * REDN;
   for (int i = threadIdx.x; i < REDN; i += 256) slab[i] = red[i];
