@@ -95,8 +95,9 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd_impl(
                     : (store_c ? at::empty({ntiles, 2, L, U4, 64}, hopt) : at::empty({0}, hopt));
   // hnat is allocated with 16 * ntiles rows so the kernel stores padding rows unconditionally
   // (no lane-divergent store branch); callers see the first S rows.
-  auto hnat_full = at::empty({ntiles * 16, L, 2 * U}, hopt);
-  auto hnat = hnat_full.narrow(0, 0, S);
+  // (bf16 without natural: the attention reads the step records directly; no natural copy)
+  auto hnat_full = at::empty({(bf16 && !natural) ? 0 : ntiles * 16, L, 2 * U}, hopt);
+  auto hnat = hnat_full.narrow(0, 0, (bf16 && !natural) ? 0 : S);
   auto copt = wemb.options().dtype(bf16 ? at::kHalf : at::kFloat);   // fp16 cell states in bf16 mode
   Tensor cst = (store_c && !bf16) ? at::empty({ntiles, 2, L, U4, 64}, copt) : at::empty({0}, copt);
   TORCH_CHECK(ntiles * 16 * L * 2 * U < (1LL << 31) && ntiles * 2 * L * U4 * 64 < (1LL << 32),
@@ -164,34 +165,32 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd(const Tensor& inst, 
                        seed_dev, wrows, true);
 }
 
-// bf16 encoder forward in three launches: x_gather, lstm_fwd, hnat_attn (the LSTM output transpose +
-// dropout fused with the self-attention forward, attention.hip).  Returns lstm_fwd's outputs plus
-// attn_fwd's (e, alphas).  Callers check hnat_attn_ok first (else lstm_fwd + attn_fwd).  With
-// store_c false (no backward) hnat is left unwritten.
+// bf16 encoder forward in three launches: x_gather, lstm_fwd, rec_attn_fwd (the self-attention forward
+// straight from the step records, rec_attn.hip: no natural-layout copy of the LSTM output).  Returns
+// lstm_fwd's outputs (hnat empty) plus (e, alphas).  Callers check rec_attn_ok first (else lstm_fwd +
+// attn_fwd).  w1r = the record-order projection pack (ops/packing.py::pack_attn_rec).
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> lstm_attn_fwd(
     const Tensor& inst, const Tensor& word, const Tensor& pos1, const Tensor& pos2, const Tensor& wemb,
     const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U, int64_t NX,
     bool store_c, int64_t seed, double keep_prob, const std::optional<Tensor>& seed_dev,
-    const std::optional<Tensor>& wrows, const Tensor& mask, const Tensor& w1pack, const Tensor& b1, const Tensor& w2) {
+    const std::optional<Tensor>& wrows, const Tensor& mask, const Tensor& w1r, const Tensor& b1, const Tensor& w2) {
   check(mask, "mask", at::kInt);
-  check(w1pack, "w1pack", at::kBFloat16);
+  check(w1r, "w1r", at::kBFloat16);
   check(b1, "b1", at::kFloat);
   check(w2, "w2", at::kFloat);
-  const int64_t L = word.size(1), S = inst.size(0), NT = (L + 15) / 16;
+  const int64_t L = word.size(1), S = inst.size(0);
   TORCH_CHECK(mask.size(1) == L, "ina.lstm_attn_fwd: mask length");
   TORCH_CHECK(b1.numel() == 2 * U && w2.numel() == 2 * U, "ina.lstm_attn_fwd: b1/w2 size");
-  TORCH_CHECK(NT >= 1 && NT <= 4, "ina.lstm_attn_fwd: L must be <= 64");
-  const int64_t H2 = 2 * U, MT = (H2 + 15) / 16, NKS = (H2 + 31) / 32;
-  TORCH_CHECK(w1pack.numel() == MT * NKS * 64 * 8, "ina.lstm_attn_fwd: w1pack size");
+  TORCH_CHECK(L >= 1 && L <= 64, "ina.lstm_attn_fwd: L must be in [1, 64]");
+  const int64_t H2 = 2 * U, MT = (H2 + 15) / 16, NKR = (2 * (U / 4) + 7) / 8;
+  TORCH_CHECK(w1r.numel() == MT * NKR * 64 * 8, "ina.lstm_attn_fwd: w1r pack size");
   const bool drop = keep_prob < 1.0;
-  TORCH_CHECK(ina::hnat_attn_lds_bytes((int)U, (int)L, drop) <= 160 * 1024, "ina.lstm_attn_fwd: LDS budget");
   auto r = lstm_fwd_impl(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, bias, U, NX, true, store_c, seed, keep_prob,
                          seed_dev, wrows, false);
   auto e = at::empty({S, 2 * U}, b1.options());
   auto alphas = at::empty({S, L}, b1.options());
   if (S == 0) return {std::get<0>(r), std::get<1>(r), std::get<2>(r), std::get<3>(r), std::get<4>(r), e, alphas};
   const Tensor& hlane = std::get<0>(r);
-  const Tensor& hnat = std::get<2>(r);   // first S rows of the [16 * tiles] allocation
   const Tensor& dmask = std::get<3>(r);
   TORCH_CHECK(hlane.numel() == ((S + 15) / 16) * 2 * L * 2 * (U / 4) * 64, "ina.lstm_attn_fwd: step records");
   TORCH_CHECK(!drop || dmask.numel() == ((S + 15) / 16) * 2 * L * 64, "ina.lstm_attn_fwd: keep bits");
@@ -200,21 +199,71 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> lstm_attn_fwd
   a.mask = mask.data_ptr<int>();
   a.S = (int)S;
   a.L = (int)L;
-  a.w1pack = w1pack.data_ptr();
+  a.w1pack = w1r.data_ptr();
   a.b1 = b1.data_ptr<float>();
   a.w2 = w2.data_ptr<float>();
   a.e = e.data_ptr<float>();
   a.alphas = alphas.data_ptr<float>();
-  // without a backward (store_c false) the natural rows are not needed: hnat is returned unwritten
-  check_launch(ina::hnat_attn(hlane.data_ptr(), drop ? dmask.data_ptr<uint8_t>() : nullptr, (float)(1.0 / keep_prob),
-                              store_c ? hnat.data_ptr() : nullptr, a, (int)U, cur_stream()),
-               "hnat_attn");
-  return {std::get<0>(r), std::get<1>(r), hnat, std::get<3>(r), std::get<4>(r), e, alphas};
+  check_launch(ina::rec_attn_fwd(hlane.data_ptr(), drop ? dmask.data_ptr<uint8_t>() : nullptr, (float)(1.0 / keep_prob),
+                                 a, (int)U, cur_stream()),
+               "rec_attn_fwd");
+  return {std::get<0>(r), std::get<1>(r), std::get<2>(r), std::get<3>(r), std::get<4>(r), e, alphas};
 }
 
-bool hnat_attn_ok(int64_t U, int64_t L, double keep_prob) {
-  return (U == 8 || U == 20 || U == 32) && L >= 1 && L <= 64 &&
-         ina::hnat_attn_lds_bytes((int)U, (int)L, keep_prob < 1.0) <= 160 * 1024;
+bool rec_attn_ok(int64_t U, int64_t L) { return (U == 8 || U == 20 || U == 32) && L >= 1 && L <= 64; }
+
+// bf16 attention backward from the step records (rec_attn.hip; e = the forward's output) -> (dHl [tiles, 2, L, U/4, 64] bf16 in
+// lstm_bwd's lane layout, slab [blocks, H2*H2 + 2*H2] in attn_bwd's layout)
+std::tuple<Tensor, Tensor> rec_attn_bwd(const Tensor& hlane, const Tensor& dmask, const Tensor& w1r, const Tensor& w1rt,
+                                        const Tensor& b1, const Tensor& w2, const Tensor& de, const Tensor& e,
+                                        const Tensor& alphas, int64_t U, double keep_prob, int64_t blocks) {
+  check(hlane, "hlane", at::kBFloat16);
+  check(e, "e", at::kFloat);
+  check(w1r, "w1r", at::kBFloat16);
+  check(w1rt, "w1rt", at::kBFloat16);
+  check(b1, "b1", at::kFloat);
+  check(w2, "w2", at::kFloat);
+  check(de, "de", at::kFloat);
+  check(alphas, "alphas", at::kFloat);
+  TORCH_CHECK(rec_attn_ok(U, alphas.size(1)), "ina.rec_attn_bwd: unsupported (U, L)");
+  const int64_t S = de.size(0), L = alphas.size(1), H2 = 2 * U, U4 = U / 4, ntiles = (S + 15) / 16;
+  TORCH_CHECK(de.size(1) == H2 && alphas.size(0) == S && e.sizes() == de.sizes(), "ina.rec_attn_bwd: de / e / alphas shape");
+  TORCH_CHECK(hlane.numel() == ntiles * 2 * L * 2 * U4 * 64, "ina.rec_attn_bwd: step records shape");
+  const int64_t MT = (H2 + 15) / 16, NKR = (2 * U4 + 7) / 8, NRT = (2 * U4 + 3) / 4, NKS2 = (4 * MT + 7) / 8;
+  TORCH_CHECK(w1r.numel() == MT * NKR * 64 * 8 && w1rt.numel() == NRT * NKS2 * 64 * 8, "ina.rec_attn_bwd: pack sizes");
+  const bool drop = keep_prob < 1.0;
+  if (drop) {
+    check(dmask, "dmask", at::kByte);
+    TORCH_CHECK(dmask.numel() == ntiles * 2 * L * 64, "ina.rec_attn_bwd: keep bits shape");
+  }
+  if (blocks <= 0) {
+    blocks = ina::rec_attn_bwd_resident_blocks((int)U);
+    if (blocks <= 0) blocks = 1024;
+  }
+  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, (ntiles + 3) / 4));
+  auto dH = at::empty({ntiles, 2, L, U4, 64}, de.options().dtype(at::kBFloat16));
+  auto slab = at::empty({blocks, H2 * H2 + 2 * H2}, de.options());
+  if (S == 0) {
+    slab.zero_();
+    return {dH, slab};
+  }
+  ina::AttnArgs a{};
+  a.S = (int)S;
+  a.L = (int)L;
+  a.w1pack = w1r.data_ptr();
+  a.w1tpack = w1rt.data_ptr();
+  a.b1 = b1.data_ptr<float>();
+  a.w2 = w2.data_ptr<float>();
+  a.de = de.data_ptr<float>();
+  a.e = const_cast<float*>(e.data_ptr<float>());   // read-only here: the forward's pooled output (sd = de . e)
+  a.alphas = alphas.data_ptr<float>();
+  a.dHraw = dH.data_ptr();
+  a.slab = slab.data_ptr<float>();
+  a.blocks = (int)blocks;
+  check_launch(ina::rec_attn_bwd(hlane.data_ptr(), drop ? dmask.data_ptr<uint8_t>() : nullptr, (float)(1.0 / keep_prob),
+                                 a, (int)U, cur_stream()),
+               "rec_attn_bwd");
+  return {dH, slab};
 }
 
 std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
@@ -242,7 +291,12 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   const int64_t DIN = E + 2 * PD, NF = DIN + U + 1, U4 = U / 4, KPL = frag_elems(bf16);
   TORCH_CHECK(DIN <= 4 * NX, "ina.lstm_bwd: input dim too large");
   TORCH_CHECK(hraw.numel() == ((S + 15) / 16) * 2 * L * U4 * 64 * (bf16 ? 2 : 1), "ina.lstm_bwd: hlane shape");
-  TORCH_CHECK(dH.size(0) == S && dH.size(1) == L && dH.size(2) == 2 * U, "ina.lstm_bwd: dH shape");
+  // dH: natural [S, L, 2U] (attn_bwd) or, bf16, the step-record lane layout [tiles, 2, L, U/4, 64] (rec_attn_bwd)
+  const bool dh_lane = dH.dim() == 5;
+  TORCH_CHECK(dh_lane ? (bf16 && dH.size(0) == (S + 15) / 16 && dH.size(1) == 2 && dH.size(2) == L &&
+                         dH.size(3) == U / 4 && dH.size(4) == 64)
+                      : (dH.dim() == 3 && dH.size(0) == S && dH.size(1) == L && dH.size(2) == 2 * U),
+              "ina.lstm_bwd: dH shape");
   TORCH_CHECK(bf16 || cst.numel() == ((S + 15) / 16) * 2 * L * U4 * 64, "ina.lstm_bwd: cst shape");
   const bool drop_ = keep_prob < 1.0;
   if (drop_) {
@@ -309,6 +363,7 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   a.inv_kp = (float)(1.0 / keep_prob);
   a.drop = keep_prob < 1.0 ? 1 : 0;
   a.dxp = bf16 ? dxp.data_ptr() : nullptr;
+  a.dh_lane = dh_lane ? 1 : 0;
   a.xg = bf16 ? xg.data_ptr() : nullptr;
   a.posb = bf16 ? reinterpret_cast<const unsigned short*>(xg.data_ptr<at::BFloat16>() + ntiles * L * 64 * NX)
                 : nullptr;
@@ -661,7 +716,8 @@ TORCH_LIBRARY(ina, m) {
   m.def("lstm_fwd", &lstm_fwd);
   m.def("lstm_bwd", &lstm_bwd);
   m.def("lstm_attn_fwd", &lstm_attn_fwd);
-  m.def("hnat_attn_ok", &hnat_attn_ok);
+  m.def("rec_attn_ok", &rec_attn_ok);
+  m.def("rec_attn_bwd", &rec_attn_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("routing_fwd", &routing_fwd);

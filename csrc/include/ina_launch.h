@@ -39,6 +39,7 @@ struct LstmArgs {
   uint32_t seed, thr;
   float inv_kp;
   int drop;
+  int dh_lane;           // bwd: dH in the step-record lane layout [tiles][2][L][U/4][64] (else [S][L][2U])
 };
 // bf16 mode: gather every token's x features once into a.xg / a.posb (lstm.hip x_gather_kernel)
 int x_gather(const LstmArgs& a, int NX, hipStream_t st);
@@ -77,10 +78,13 @@ struct AttnArgs {
 int attn_fwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st);
 int attn_bwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st);
 int attn_bwd_resident_blocks(int U, int NT, bool bf16);
-// bf16: lstm_fwd step records (+ keep bits) -> natural rows hnat AND the attention forward (e, alphas)
-size_t hnat_attn_lds_bytes(int U, int L, bool drop);
-int hnat_attn(const void* rec, const unsigned char* dmask, float inv_kp, void* hnat, const AttnArgs& a, int U,
-              hipStream_t st);
+// bf16, attention straight from lstm_fwd's step records (+ keep bits), rec_attn.hip:
+//   fwd: a.w1pack = w1r pack -> a.e, a.alphas
+//   bwd: a.w1pack / a.w1tpack = w1r / w1rt packs, a.de, a.e (forward output), a.alphas -> a.dHraw (bf16 [tiles][2][L][U/4][64]),
+//        a.slab [a.blocks][H2*H2 + 2*H2]
+int rec_attn_fwd(const void* rec, const unsigned char* dmask, float inv_kp, const AttnArgs& a, int U, hipStream_t st);
+int rec_attn_bwd(const void* rec, const unsigned char* dmask, float inv_kp, const AttnArgs& a, int U, hipStream_t st);
+int rec_attn_bwd_resident_blocks(int U);
 
 int routing_fwd(const float* e, const float* Ws, int E, int N, int K, int Q, int R, int H, float* cls, int blocks,
                 hipStream_t st);

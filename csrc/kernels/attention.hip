@@ -103,10 +103,7 @@ INA_DEVICE void load_h(const typename FT<BF16>::elem* hraw, long seq, int tok, i
 
 // bf16 forward of one sentence from its H tiles (hf: token 16 * nt + n, features 32 * ks + 8 * q ..+7,
 // zero outside [L) x [2U)) and the mask ids of those tokens: projection (MFMA), tanh, w2 dot, masked
-// softmax over the tokens, pooling.  Shared by attn_fwd_kernel (H from global rows) and
-// hnat_attn_kernel (H from the LDS-transposed LSTM step records).
-// Weight operands: register arrays (attn_fwd_kernel) or LDS (hnat_attn_kernel: registers kept for
-// occupancy), read through wa / wb / ww.
+// softmax over the tokens, pooling.  Weight operands read through wa / wb / ww (register arrays).
 template <int MT, int NKS>
 struct RegW {
   const u16x8_t (&A)[MT][NKS];
@@ -115,15 +112,6 @@ struct RegW {
   INA_DEVICE u16x8_t wa(int m, int ks) const { return A[m][ks]; }
   INA_DEVICE float wb(int m, int r) const { return bj[m][r]; }
   INA_DEVICE float ww(int m, int r) const { return wj[m][r]; }
-};
-template <int MT, int NKS>
-struct LdsW {
-  const u16x8_t* lA;   // [MT * NKS][64]
-  const float* lbw;    // [b1 | w2], MT * 16 each
-  int lane, q;
-  INA_DEVICE u16x8_t wa(int m, int ks) const { return lA[(m * NKS + ks) * 64 + lane]; }
-  INA_DEVICE float wb(int m, int r) const { return lbw[16 * m + 4 * q + r]; }
-  INA_DEVICE float ww(int m, int r) const { return lbw[MT * 16 + 16 * m + 4 * q + r]; }
 };
 
 template <int U, int NT, typename W>
@@ -137,7 +125,6 @@ INA_DEVICE void attn_sentence_bf16(const u16x8_t (&hf)[NT][AShape<U, NT, true>::
   for (int nt = 0; nt < NT; ++nt) {
     const int tok = 16 * nt + n;
     float sp = 0.f;
-    asm volatile("" ::: "memory");   // LdsW: re-read the weight fragments per token tile (no hoisting)
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       f32x4_t acc = {w.wb(m, 0), w.wb(m, 1), w.wb(m, 2), w.wb(m, 3)};
@@ -309,131 +296,6 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
         if (k < H2) e_out[(long)s * H2 + k] = ev[v];
       }
     }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// bf16 forward fused with the LSTM output transpose (replaces h_natural_kernel + attn_fwd_kernel).
-// Input: lstm_fwd's step records [tile][dir][t][2][U4][64] (16-bit; slot 0 = h of the 16 sequences
-// of the tile in the lane layout: unit 4m + (li >> 4) of sequence li & 15 at [m][li]) and the
-// DropoutWrapper keep bits [tile][dir][t][64] (bit m of byte li).  One 512-thread workgroup per tile:
-//   1) every thread loads 4 16-B chunks (units 4m..4m+3) of the tile's h slots (+ their keep bytes)
-//      into registers, applies the dropout (model/graph.py:36-38: keep ? h / keep_prob : 0, bf16)
-//      and scatters them as 8-B pieces into the tile's natural rows [16][L][2U] in LDS
-//      (model/graph.py:49);
-//   2) the LDS rows -> HBM with 16-B stores (the tile's rows are one contiguous run of hnat, the
-//      backward's input);
-//   3) each wave pools 2 sentences from the LDS rows (attn_sentence_bf16: 16-B LDS reads); their
-//      instance ids and mask ids are loaded before the transpose.
-// LDS = the natural rows only (47 KB at L=37, u=20): 2 workgroups per CU.  Saves attn_fwd's 303 MB
-// re-read of the natural rows (default 5w5s, 2048 episodes) and a launch.
-// ------------------------------------------------------------------------------------------
-#ifndef INA_HA_PHASES
-#define INA_HA_PHASES 7   // timing experiments: bit 0 transpose, bit 1 natural-row write, bit 2 attention
-#endif
-template <int U, int NT>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NT <= 3 ? 6 : 4))) void hnat_attn_kernel(const unsigned short* __restrict__ rec,
-                                                        const unsigned char* __restrict__ dmask, int S, int L,
-                                                        float inv_kp, unsigned short* __restrict__ hnat,
-                                                        const int* __restrict__ inst, const int* __restrict__ maskarr,
-                                                        const u16x8_t* __restrict__ w1pack,
-                                                        const float* __restrict__ b1, const float* __restrict__ w2,
-                                                        float* __restrict__ e_out, float* __restrict__ alphas) {
-  using Sh = AShape<U, NT, true>;
-  constexpr int H2 = Sh::H2, NKS = Sh::NKS, MT = Sh::MT;
-  constexpr int U4 = U / 4, CPP = U4 * 64 / 8;   // 16-B chunks per (dir, step) h slot
-  extern __shared__ __attribute__((aligned(16))) unsigned short nat[];   // [16][L][2U] bf16
-  const int tile = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int q = lane >> 4, nl = lane & 15;
-  // sentence ids and mask ids first (their dependent loads overlap the transpose)
-  int mk[2][NT];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const long s = (long)tile * 16 + wave * 2 + j;
-    const long row = (long)inst[s < S ? s : S - 1] * L;
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int tok = 16 * nt + nl;
-      mk[j][nt] = maskarr[row + (tok < L ? tok : L - 1)];
-    }
-  }
-  // 1) records -> registers -> dropout -> natural rows in LDS
-  const uint4* src = reinterpret_cast<const uint4*>(rec + (size_t)tile * 2 * L * 2 * U4 * 64);
-  // a work item = the 4 chunks of units 4m .. 4m + 3 of 8 sequences n0..n0+7 (lanes 16r + n0, chunks
-  // 8m + 2r + n0 / 8 of the slot); each sequence's 4 values are one 8-B piece of its natural row
-  // (column d * U + 4m: 8-B aligned since U % 4 == 0)
-  const int nit = 2 * L * U4 * 2;
-  uint2* nat64 = reinterpret_cast<uint2*>(nat);
-  for (int c = threadIdx.x; c < ((INA_HA_PHASES & 1) ? nit : 0); c += 512) {
-    const int k = c / (U4 * 2), pc = c - k * (U4 * 2);   // k = dir * L + t
-    const int m = pc >> 1, n0 = (pc & 1) * 8;
-    const uint4* sk = src + (size_t)k * 2 * CPP + m * 8 + (n0 >> 3);   // h slot of record k
-    uint4 v[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = sk[2 * r];
-    const int d = k >= L ? 1 : 0, t = k - d * L;
-    const int col4 = (d * U + 4 * m) >> 2;
-    unsigned long long kb[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-    if (dmask) {
-      const unsigned char* kp = dmask + ((size_t)tile * 2 * L + k) * 64 + n0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) kb[r] = *reinterpret_cast<const unsigned long long*>(kp + 16 * r);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      uint32_t x[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const uint32_t w = i < 2 ? v[r].x : i < 4 ? v[r].y : i < 6 ? v[r].z : v[r].w;
-        unsigned short h = (unsigned short)(w >> (16 * (i & 1)));
-        if (dmask) h = ((kb[r] >> (8 * i + m)) & 1ull) ? f2bf(bf2f(h) * inv_kp) : (unsigned short)0;
-        x[r] = h;
-      }
-      nat64[((n0 + i) * L + t) * (H2 / 4) + col4] = make_uint2(x[0] | (x[1] << 16), x[2] | (x[3] << 16));
-    }
-  }
-  // W1 fragments and b1 / w2 staged in LDS (read per sentence: registers stay free for occupancy)
-  u16x8_t* lA = reinterpret_cast<u16x8_t*>(nat + 16 * L * H2);          // [MT * NKS][64]
-  float* lbw = reinterpret_cast<float*>(lA + MT * NKS * 64);             // [b1 | w2], MT * 16 each
-  for (int i = threadIdx.x; i < MT * NKS * 64; i += 512) lA[i] = w1pack[i];
-  for (int i = threadIdx.x; i < MT * 16; i += 512) {
-    lbw[i] = i < H2 ? b1[i] : 0.f;
-    lbw[MT * 16 + i] = i < H2 ? w2[i] : 0.f;
-  }
-  __syncthreads();
-  // 2) the tile's rows are one contiguous run of hnat (padding rows of the last tile included);
-  //    skipped without a backward (hnat == nullptr: eval / serving)
-  if ((INA_HA_PHASES & 2) && hnat) {
-    const uint4* ls = reinterpret_cast<const uint4*>(nat);
-    uint4* dst = reinterpret_cast<uint4*>(hnat + (size_t)tile * 16 * L * H2);
-    for (int i = threadIdx.x; i < 16 * L * H2 / 8; i += 512) dst[i] = ls[i];
-  }
-  // 3) attention forward, 2 sentences per wave (not unrolled; the sentence's mask ids are picked with
-  //    selects, so mk stays in registers)
-#pragma unroll 1
-  for (int j = 0; j < 2; ++j) {
-    const int n = wave * 2 + j;
-    const long s = (long)tile * 16 + n;
-    if (s >= S || !(INA_HA_PHASES & 4)) break;   // wave-uniform
-    u16x8_t hf[NT][NKS];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int tok = 16 * nt + nl;
-      const bool tv = tok < L;
-      const int hrow = (n * L + (tv ? tok : L - 1)) * H2;
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const int k0 = 32 * ks + 8 * q;
-        const bool ok = tv && (k0 < H2);
-        const u16x8_t v = *reinterpret_cast<const u16x8_t*>(nat + hrow + (ok ? k0 : 0));
-        hf[nt][ks] = ok ? v : u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-      }
-    }
-    int mkj[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) mkj[nt] = j == 0 ? mk[0][nt] : mk[1][nt];
-    attn_sentence_bf16<U, NT>(hf, mkj, LdsW<MT, NKS>{lA, lbw, lane, q}, s, L, q, nl, e_out, alphas);
   }
 }
 
@@ -1018,43 +880,6 @@ static int attn_bwd_t(const AttnArgs& a, hipStream_t st) {
     INA_ATTN_CASE(FN, 8) INA_ATTN_CASE(FN, 20) INA_ATTN_CASE(FN, 32) \
   }                                           \
   return -1;
-
-size_t hnat_attn_lds_bytes(int U, int L, bool) {
-  const int H2 = 2 * U, MT = (H2 + 15) / 16, NKS = (H2 + 31) / 32;
-  return (size_t)16 * L * H2 * 2 + (size_t)MT * NKS * 64 * 16 + (size_t)2 * MT * 16 * 4;
-}
-
-template <int U, int NT>
-static int hnat_attn_t(const void* rec, const unsigned char* dmask, float inv_kp, void* hnat, const AttnArgs& a,
-                       hipStream_t st) {
-  const size_t lds = hnat_attn_lds_bytes(U, a.L, dmask != nullptr);
-  if (lds > 160 * 1024) return -1;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)hnat_attn_kernel<U, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-  const int ntiles = (a.S + 15) / 16;
-  hipLaunchKernelGGL((hnat_attn_kernel<U, NT>), dim3(ntiles), dim3(512), lds, st, (const unsigned short*)rec, dmask,
-                     a.S, a.L, inv_kp, (unsigned short*)hnat, a.inst, a.mask, (const u16x8_t*)a.w1pack, a.b1, a.w2,
-                     a.e, a.alphas);
-  INA_CHECK_LAUNCH();
-  return 0;
-}
-
-int hnat_attn(const void* rec, const unsigned char* dmask, float inv_kp, void* hnat, const AttnArgs& a, int U,
-              hipStream_t st) {
-  if (a.S <= 0) return 0;
-  const int NT = (a.L + 15) / 16;
-#define INA_HA(UV)                                                         \
-  if (U == UV) {                                                           \
-    if (NT == 1) return hnat_attn_t<UV, 1>(rec, dmask, inv_kp, hnat, a, st); \
-    if (NT == 2) return hnat_attn_t<UV, 2>(rec, dmask, inv_kp, hnat, a, st); \
-    if (NT == 3) return hnat_attn_t<UV, 3>(rec, dmask, inv_kp, hnat, a, st); \
-    if (NT == 4) return hnat_attn_t<UV, 4>(rec, dmask, inv_kp, hnat, a, st); \
-  }
-  INA_HA(8) INA_HA(20) INA_HA(32)
-#undef INA_HA
-  return -1;
-}
 
 // Workgroups of the persistent bf16 backward that are resident at once (occupancy x CUs): the grid
 // is sized to exactly that, so every wave runs the same number of sentences in one round (a grid of

@@ -485,9 +485,8 @@ __global__ __launch_bounds__(256) void h_natural_kernel(const unsigned short* __
 // ------------------------------------------------------------------------------------------
 // dW slab layout per (block, dir): D[gc][f], gc in [0, 4U), f in [0, DIN + U + 1) where
 // f < DIN are x features, DIN..DIN+U-1 the h units and DIN+U the bias.
-#ifndef INA_DH_LANE
-#define INA_DH_LANE 0   // timing experiment: dH read in the lane layout (wrong values)
-#endif
+// dH layouts (dh_lane): 0 = natural [S][L][2U] (attn_bwd), 1 = the step-record lane layout
+// [tiles][2][L][U4][64] (rec_attn_bwd: coalesced 128-B rows per (step, m))
 // 2 waves/SIMD where the register set fits in 256 without spilling (the default u=20 / 5-d words
 // case); the wider instantiations keep 1 wave and no spills
 template <int U, int NX>
@@ -504,7 +503,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     const typename CT<BF16>::type* __restrict__ cst, const typename FragT<BF16>::elem* __restrict__ dH,
     float* __restrict__ dw_slab,
     float* __restrict__ dpos_slab, float* __restrict__ dwemb, const unsigned char* __restrict__ dmask, uint32_t seed,
-    uint32_t thr, float inv_kp, int drop, unsigned short* __restrict__ dxp, const unsigned short* __restrict__ xg) {
+    uint32_t thr, float inv_kp, int drop, unsigned short* __restrict__ dxp, const unsigned short* __restrict__ xg,
+    int dh_lane) {
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
   using elem = typename FragT<BF16>::elem;
@@ -596,6 +596,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     const bool valid = seq < S;
     const long seqc = valid ? seq : S - 1;  // clamped row for unconditional loads
     const long rowbase = (long)inst[seqc] * L;
+    // dH element (t, m) of the lane = dH[dh_base + t * dh_ts + m * dh_ms] (wave-uniform layout choice)
+    const size_t dh_base = dh_lane ? ((size_t)tile * 2 + dir) * L * U4 * 64 + lane
+                                   : (size_t)seqc * L * (2 * U) + dir * U + q;
+    const int dh_ts = dh_lane ? U4 * 64 : 2 * U, dh_ms = dh_lane ? 64 : 4;
     const typename CT<BF16>::type* cbase = cst + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
     const elem* hbase = hraw + ((size_t)tile * 2 + dir) * L * U4 * 64 + lane;
     // bf16: the forward's step records [t][2][U4][64]: h slot, then c slot (fp16 bits)
@@ -645,11 +649,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         ld_hc(tp, m, hv, cp);
         cprev[m] = L >= 2 ? cp : 0.f;
         hp[m] = (L >= 2 && valid) ? hv : 0.f;
-#if INA_DH_LANE
-        const float dv = from_elem(dH[(((size_t)tile * 2 + dir) * L + t) * U4 * 64 + m * 64 + lane]);
-#else
-        const float dv = from_elem(dH[(seqc * L + t) * (2 * U) + dir * U + 4 * m + q]);
-#endif
+        const float dv = from_elem(dH[dh_base + (size_t)t * dh_ts + m * dh_ms]);
         const bool keep = (bits >> m) & 1u;
         dhin[m] = (valid && keep) ? dv * inv_kp : 0.f;
       }
@@ -698,11 +698,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         ld_hc(tnp, m, hv, cp);
         cprev_n[m] = n_has_prev ? cp : 0.f;
         hp_n[m] = (n_has_prev && valid) ? hv : 0.f;
-#if INA_DH_LANE
-        const float dv = from_elem(dH[(((size_t)tile * 2 + dir) * L + tn) * U4 * 64 + m * 64 + lane]);
-#else
-        const float dv = from_elem(dH[(seqc * L + tn) * (2 * U) + dir * U + 4 * m + q]);
-#endif
+        const float dv = from_elem(dH[dh_base + (size_t)tn * dh_ts + m * dh_ms]);
         const bool keep = (bits_n >> m) & 1u;
         dhin_n[m] = (valid && keep) ? dv * inv_kp : 0.f;
       }
@@ -1179,7 +1175,7 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(kfn, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, (const frag*)a.a2pack, a.bias,
                      (const elem*)a.hraw, (const typename CT<BF16>::type*)a.cst, (const elem*)a.dH, a.dw_slab, a.dpos_slab, a.dwemb, a.dmask, a.seed, a.thr, a.inv_kp,
-                     a.drop, (unsigned short*)a.dxp, (const unsigned short*)a.xg);
+                     a.drop, (unsigned short*)a.dxp, (const unsigned short*)a.xg, a.dh_lane);
   INA_CHECK_LAUNCH();
   return 0;
 }

@@ -1,0 +1,507 @@
+// Word-level self-attention pooling straight from the BiLSTM step records, forward and backward
+// (K4 of SURVEY 2.3; the bf16 training / eval path).
+//
+// Reference (model/layer_module.py:49-98, model/graph.py:36-53):
+//   H      = DropoutWrapper output of the BiLSTM, [S, L, 2u]
+//   x_proj = tanh(H @ W1 + b1);  score = x_proj @ w2;  alphas = softmax_t(score + (1 - (mask>0)) * -2^31)
+//   e      = sum_t alphas_t H_t
+//
+// lstm_fwd leaves H in its step records [tile][dir][t][2 slots][U/4][64] (16-bit): h slot element
+// [m][l] = unit 4m + (l >> 4) of sequence 16 tile + (l & 15).  hnat_attn / attn_bwd3 first
+// transposed these into natural rows [S][L][2u] (a 300 MB round trip per 2048 episodes plus a
+// bank-conflicted LDS scatter).  These kernels never transpose H: one wave owns a 16-sequence tile
+// and walks its tokens, with the SEQUENCES on the MFMA columns:
+//   * lane (q, n) holds, per token, the features F_q = {d u + 4m + q : d < 2, m < u/4} of sequence
+//     n -- exactly its own record elements (one coalesced 128-B row per (dir, m) and step);
+//   * the projection P^T[j][seq] = W1^T[j][k] H^T[k][seq] contracts over k in that lane-permuted
+//     order (the A fragments, w1r, are packed to match: ops/packing.py::_attn_rec_idx), so the B
+//     operand is the lane's own values; the accumulator rows j = 16 mt + 4 q + r land per lane;
+//   * score / softmax / pooling are per column: a 4-group cross-lane sum gives every lane its
+//     sequence's score, and an online (running-max) softmax pools e in registers in one pass;
+//   * backward: dH^T = W1 dP^T feeds the dP accumulator straight back as the B operand (K = j in
+//     accumulator order; w1rt packed to match) and its rows come out as each lane's own features,
+//     i.e. dH leaves in the step-record lane layout that lstm_bwd reads with coalesced loads.
+//     dW1 = sum H^T dP contracts over the sequences: both operands are staged per step pair in
+//     lane-permuted [32 samples][columns] LDS images (4-/8-B stores) and read back transposed by
+//     ds_read_b64_tr_b16 for v_mfma_f32_16x16x32_bf16 (K = 32 samples).
+#include "ina_common.h"
+#include "ina_launch.h"
+
+using namespace ina;
+
+namespace {
+
+template <int U>
+struct RA {
+  static constexpr int U4 = U / 4, H2 = 2 * U;
+  static constexpr int NV = 2 * U4;                         // features per lane (both directions)
+  static constexpr int NKR = (NV + 7) / 8;                  // projection K-steps (8 slots per lane)
+  static constexpr int MT = (H2 + 15) / 16;                 // projection row tiles (j)
+  static constexpr int NJ = 4 * MT;                         // dP values per lane
+  static constexpr int NKS2 = (NJ + 7) / 8;                 // dH K-steps
+  static constexpr int NRT = (NV + 3) / 4;                  // dH row tiles
+  static constexpr int NVP = (NV + 1) & ~1;                 // H image columns per lane group (even)
+  static constexpr int HT = (4 * NVP + 15) / 16;            // dW1 row tiles (H image columns)
+  static constexpr int DEP = (NV + 3) & ~3;                 // de floats per lane in LDS (16-B reads)
+  static constexpr int HCP = HT * 16 + 4, JCP = MT * 16 + 4;   // image row strides (elements)
+  static constexpr int NA = MT * NKR * 64, NA2 = NRT * NKS2 * 64;
+  static constexpr int RSTEP = 2 * U4 * 64;                 // record elements per (dir, step)
+  static constexpr int WAVE_IMG = 32 * (HCP + JCP) * 2 + 64 * DEP * 4;   // bytes per wave (images | de)
+  static constexpr int NS = H2 * H2 + 2 * H2;               // slab floats
+  static_assert(U % 4 == 0 && NV <= 16, "rec_attn: u must be a multiple of 4, <= 32");
+};
+
+// feature index of slot idx (< NV) of lane group q
+template <int U>
+INA_DEVICE int rfeat(int idx, int q) {
+  constexpr int U4 = U / 4;
+  return (idx / U4) * U + 4 * (idx % U4) + q;
+}
+
+INA_DEVICE uint32_t cross_group_or(uint32_t v) {
+  float a, b;
+  dpp::swap16(__builtin_bit_cast(float, v), a, b);
+  v = __builtin_bit_cast(uint32_t, a) | __builtin_bit_cast(uint32_t, b);
+  dpp::swap32(__builtin_bit_cast(float, v), a, b);
+  return __builtin_bit_cast(uint32_t, a) | __builtin_bit_cast(uint32_t, b);
+}
+
+// one step of the tile's records: the lane's NV h values (16-bit) and its two keep bytes
+template <int U>
+struct RecStep {
+  unsigned short h[RA<U>::NV];
+  uint32_t kb;
+};
+template <int U>
+INA_DEVICE void rec_load(const unsigned short* r0, const unsigned short* r1, const unsigned char* k0,
+                         const unsigned char* k1, int t, RecStep<U>& o) {
+  constexpr int U4 = RA<U>::U4, RSTEP = RA<U>::RSTEP;
+#pragma unroll
+  for (int m = 0; m < U4; ++m) {
+    o.h[m] = r0[t * RSTEP + m * 64];
+    o.h[U4 + m] = r1[t * RSTEP + m * 64];
+  }
+  o.kb = k0 ? ((uint32_t)k0[t * 64] | ((uint32_t)k1[t * 64] << 8)) : 0xFFFFu;
+}
+// DropoutWrapper output (model/graph.py:36-38): keep ? bf16(h / keep_prob) : 0 -- the same rounding
+// as h_natural_kernel, so both attention paths see identical H
+template <int U>
+INA_DEVICE unsigned short rec_drop(const RecStep<U>& s, int idx, bool drop, float inv_kp) {
+  constexpr int U4 = RA<U>::U4;
+  const unsigned short h = s.h[idx];
+  if (!drop) return h;
+  const int bit = idx < U4 ? idx : 8 + idx - U4;
+  return ((s.kb >> bit) & 1u) ? f2bf(bf2f(h) * inv_kp) : (unsigned short)0;
+}
+
+INA_DEVICE u16x8_t tr8(const unsigned short* img, int stride, int c0, int q, int n) {
+  const s16x4_t lo = tr_read(img + (8 * q + (n >> 2)) * stride + c0 + 4 * (n & 3));
+  const s16x4_t hi = tr_read(img + (8 * q + 4 + (n >> 2)) * stride + c0 + 4 * (n & 3));
+  return u16x8_t{(unsigned short)lo[0], (unsigned short)lo[1], (unsigned short)lo[2], (unsigned short)lo[3],
+                 (unsigned short)hi[0], (unsigned short)hi[1], (unsigned short)hi[2], (unsigned short)hi[3]};
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// forward: one wave per tile, 4 tiles per workgroup.  Outputs e [S][2u] and alphas [S][L] (fp32).
+// The raw scores are parked in alphas (lane q stores the steps t = q mod 4 and re-reads only its
+// own stores) and normalised once the running max / sum are final.
+// ------------------------------------------------------------------------------------------
+template <int U>
+__global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
+    const unsigned short* __restrict__ rec, const unsigned char* __restrict__ dmask, int S, int L, float inv_kp,
+    const int* __restrict__ inst, const int* __restrict__ maskarr, const u16x8_t* __restrict__ w1r,
+    const float* __restrict__ b1, const float* __restrict__ w2, float* __restrict__ e_out,
+    float* __restrict__ alphas) {
+  using C = RA<U>;
+  constexpr int U4 = C::U4, H2 = C::H2, NV = C::NV, NKR = C::NKR, MT = C::MT;
+  const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15;
+  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // weights shared by the workgroup in LDS (registers kept for occupancy: the loop is latency-bound
+  // on the record loads, so resident waves are what hides them)
+  __shared__ u16x8_t lA[MT * NKR * 64];
+  __shared__ float lbw[2 * MT * 16];   // [b1 | w2]
+  for (int i = threadIdx.x; i < MT * NKR * 64; i += 256) lA[i] = w1r[i];
+  for (int i = threadIdx.x; i < MT * 16; i += 256) {
+    lbw[i] = i < H2 ? b1[i] : 0.f;
+    lbw[MT * 16 + i] = i < H2 ? w2[i] : 0.f;
+  }
+  __syncthreads();
+  if (tile * 16 >= S) return;   // wave-uniform; no workgroup barrier after this point
+  const int seq = tile * 16 + n;
+  const bool valid = seq < S;
+  const int seqc = valid ? seq : S - 1;
+  // token mask of the lane's sequence as a 64-bit set (L <= 64): 16 loads per lane, OR over the groups
+  uint32_t mlo = 0, mhi = 0;
+  {
+    const int* mrow = maskarr + (long)inst[seqc] * L;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int t = q + 4 * i;
+      const int v = mrow[t < L ? t : L - 1];
+      const uint32_t on = (t < L && v > 0) ? 1u : 0u;
+      if (i < 8) mlo |= on << t;
+      else mhi |= on << (t - 32);
+    }
+    mlo = cross_group_or(mlo);
+    mhi = cross_group_or(mhi);
+  }
+  const bool drop = dmask != nullptr;
+  const unsigned short* r0 = rec + (size_t)tile * 2 * L * C::RSTEP + lane;
+  const unsigned short* r1 = r0 + (size_t)L * C::RSTEP;
+  const unsigned char* k0 = drop ? dmask + (size_t)tile * 2 * L * 64 + lane : nullptr;
+  const unsigned char* k1 = drop ? k0 + (size_t)L * 64 : nullptr;
+  float* arow = alphas + (size_t)seqc * L;
+
+  RecStep<U> cur, nxt;
+  rec_load<U>(r0, r1, k0, k1, 0, cur);
+  float mx = -INFINITY, lsum = 0.f, ea[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) ea[i] = 0.f;
+  for (int t = 0; t < L; ++t) {
+    rec_load<U>(r0, r1, k0, k1, t + 1 < L ? t + 1 : t, nxt);   // one step of prefetch
+    float v[NV];
+    u16x8_t B[NKR];
+#pragma unroll
+    for (int ks = 0; ks < NKR; ++ks) B[ks] = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const unsigned short hb = rec_drop<U>(cur, i, drop, inv_kp);
+      v[i] = bf2f(hb);
+      B[i / 8][i % 8] = hb;
+    }
+    float sp = 0.f;
+    asm volatile("" ::: "memory");   // re-read the LDS weights per step (no hoisting into registers)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const float4 bv = *reinterpret_cast<const float4*>(&lbw[16 * m + 4 * q]);
+      const float4 wv = *reinterpret_cast<const float4*>(&lbw[MT * 16 + 16 * m + 4 * q]);
+      f32x4_t acc = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+      for (int ks = 0; ks < NKR; ++ks) acc = mfma_bf16(lA[(m * NKR + ks) * 64 + lane], B[ks], acc);
+      sp += wv.x * tanhf_(acc[0]) + wv.y * tanhf_(acc[1]) + wv.z * tanhf_(acc[2]) + wv.w * tanhf_(acc[3]);
+    }
+    sp = cross_group_sum(sp);
+    const uint32_t on = t < 32 ? (mlo >> t) & 1u : (mhi >> (t - 32)) & 1u;
+    const float sc = on ? sp : sp + -2147483648.f;
+    // online softmax: rescale the running sum and pooled vector when the max moves
+    const float mn = fmaxf(mx, sc);
+    const float c = __expf(mx - mn), p = __expf(sc - mn);
+    lsum = lsum * c + p;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) ea[i] = ea[i] * c + p * v[i];
+    mx = mn;
+    if ((t & 3) == q && valid) arow[t] = sc;
+    cur = nxt;
+  }
+  const float inv = 1.f / lsum;
+  if (valid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) e_out[(size_t)seq * H2 + rfeat<U>(i, q)] = ea[i] * inv;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int t = q + 4 * i;
+      if (t < L) arow[t] = __expf(arow[t] - mx) * inv;   // this lane's own stores
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward: persistent grid, one wave per tile at a time, 4 waves per workgroup.  One pass over the
+// tokens: sd = sum_t alpha_t d(alpha)_t = de . sum_t alpha_t H_t = de . e (the forward's output), so
+// no separate d(alpha) pass; per step
+//   recompute P, d(alpha)_t = de . H_t, ds_t = alpha_t (d(alpha)_t - sd), dP = ds w2 (1 - P^2),
+//   dH_t = W1 dP_t + alpha_t de -> dHl [tiles][2][L][u/4][64] bf16 (lstm_bwd's lane layout),
+//   dW1 += H^T dP (MFMAs per step pair), db1 += dP, dw2 += ds P (fp32: sum_t ds_t = 0 per sequence,
+//   so these sums cancel heavily -- bf16 dP through the MFMA measured 1e-2 relative error on db1)
+// slab per workgroup: [dW1 (H2*H2, row i, col j) | db1 (H2) | dw2 (H2)], the attn_bwd layout.
+// ------------------------------------------------------------------------------------------
+template <int U>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3 : 2))) void rec_attn_bwd_kernel(
+    const unsigned short* __restrict__ rec, const unsigned char* __restrict__ dmask, int S, int L, float inv_kp,
+    const u16x8_t* __restrict__ w1r, const u16x8_t* __restrict__ w1rt, const float* __restrict__ b1,
+    const float* __restrict__ w2, const float* __restrict__ de, const float* __restrict__ e_fwd,
+    const float* __restrict__ alphas, unsigned short* __restrict__ dHl, float* __restrict__ slab) {
+  using C = RA<U>;
+  constexpr int U4 = C::U4, H2 = C::H2, NV = C::NV, NKR = C::NKR, MT = C::MT, NJ = C::NJ, NKS2 = C::NKS2,
+                NRT = C::NRT, NVP = C::NVP, HT = C::HT, HCP = C::HCP, JCP = C::JCP, DEPC = C::DEP;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, n = lane & 15;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  u16x8_t* lA = reinterpret_cast<u16x8_t*>(smem);
+  u16x8_t* lAT = lA + C::NA;
+  float* lbw = reinterpret_cast<float*>(lAT + C::NA2);   // [b1 | w2], MT * 16 each
+  unsigned short* himg = reinterpret_cast<unsigned short*>(lbw + 2 * MT * 16) + (size_t)wave * (C::WAVE_IMG / 2);
+  unsigned short* pimg = himg + 32 * HCP;
+  for (int i = threadIdx.x; i < C::NA; i += 256) lA[i] = w1r[i];
+  for (int i = threadIdx.x; i < C::NA2; i += 256) lAT[i] = w1rt[i];
+  for (int i = threadIdx.x; i < MT * 16; i += 256) {
+    lbw[i] = i < H2 ? b1[i] : 0.f;
+    lbw[MT * 16 + i] = i < H2 ? w2[i] : 0.f;
+  }
+  float* lde = reinterpret_cast<float*>(pimg + 32 * JCP) + lane * C::DEP;   // the lane's de values
+  // images zeroed once: pad columns (>= 4 NVP resp. 4 NJ) are never written and must read as 0
+  for (int i = lane; i < C::WAVE_IMG / 4; i += 64) reinterpret_cast<uint32_t*>(himg)[i] = 0u;
+  __syncthreads();
+
+  f32x4_t accW[HT][MT];
+#pragma unroll
+  for (int a = 0; a < HT; ++a)
+#pragma unroll
+    for (int b = 0; b < MT; ++b) accW[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float dw2a[MT][4], db1a[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dw2a[m][r] = db1a[m][r] = 0.f;
+  const bool drop = dmask != nullptr;
+  const int ntiles = (S + 15) / 16;
+
+  for (int tile = blockIdx.x * 4 + wave; tile < ntiles; tile += gridDim.x * 4) {   // wave-uniform
+    const int seq = tile * 16 + n;
+    const bool valid = seq < S;
+    const int seqc = valid ? seq : S - 1;
+    // de of the lane's features -> LDS (re-read per step: registers kept for occupancy)
+    float sd = 0.f;
+    lds_order();   // the previous tile's reads of lde come first
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const size_t o = (size_t)seqc * H2 + rfeat<U>(i, q);
+      const float x = valid ? de[o] : 0.f;
+      lde[i] = x;
+      sd += x * e_fwd[o];
+    }
+    sd = cross_group_sum(sd);
+    const float* arow = alphas + (size_t)seqc * L;
+    const unsigned short* r0 = rec + (size_t)tile * 2 * L * C::RSTEP + lane;
+    const unsigned short* r1 = r0 + (size_t)L * C::RSTEP;
+    const unsigned char* k0 = drop ? dmask + (size_t)tile * 2 * L * 64 + lane : nullptr;
+    const unsigned char* k1 = drop ? k0 + (size_t)L * 64 : nullptr;
+    unsigned short* d0 = dHl + (size_t)tile * 2 * L * U4 * 64 + lane;   // dir 0; dir 1 at + L * U4 * 64
+    RecStep<U> cur, nxt;
+    rec_load<U>(r0, r1, k0, k1, 0, cur);
+    for (int t = 0; t < L; ++t) {
+      rec_load<U>(r0, r1, k0, k1, t + 1 < L ? t + 1 : t, nxt);
+      const float alv = valid ? arow[t] : 0.f;
+      float dev[DEPC];
+      asm volatile("" ::: "memory");   // re-read de from LDS per step (no hoisting)
+#pragma unroll
+      for (int i = 0; i < DEPC; i += 4) {
+        const float4 v4 = *reinterpret_cast<const float4*>(lde + i);
+        dev[i] = v4.x; dev[i + 1] = v4.y; dev[i + 2] = v4.z; dev[i + 3] = v4.w;
+      }
+      unsigned short hb[NVP];
+      u16x8_t B[NKR];
+#pragma unroll
+      for (int ks = 0; ks < NKR; ++ks) B[ks] = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      float d = 0.f;
+#pragma unroll
+      for (int i = 0; i < NVP; ++i) {
+        hb[i] = i < NV ? rec_drop<U>(cur, i, drop, inv_kp) : (unsigned short)0;
+        if (i < NV) {
+          B[i / 8][i % 8] = hb[i];
+          d += dev[i] * bf2f(hb[i]);
+        }
+      }
+      const float ds = alv * (cross_group_sum(d) - sd);   // 0 for padding sequences (alpha 0)
+      float dp[MT][4];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        f32x4_t acc;
+        float wv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          acc[r] = lbw[16 * m + 4 * q + r];
+          wv[r] = lbw[MT * 16 + 16 * m + 4 * q + r];
+        }
+#pragma unroll
+        for (int ks = 0; ks < NKR; ++ks) acc = mfma_bf16(lA[(m * NKR + ks) * 64 + lane], B[ks], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pr = tanhf_(acc[r]);
+          dp[m][r] = ds * wv[r] * (1.f - pr * pr);
+          dw2a[m][r] += ds * pr;
+          db1a[m][r] += dp[m][r];
+        }
+      }
+      // dH^T = W1 dP^T (+ alpha de): K = j in accumulator order, rows = the lane's own features
+      u16x8_t B2[NKS2];
+#pragma unroll
+      for (int ks = 0; ks < NKS2; ++ks) {
+        B2[ks] = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int idx = ks * 8 + j;
+          if (idx < NJ) B2[ks][j] = f2bf(dp[idx >> 2][idx & 3]);
+        }
+      }
+#pragma unroll
+      for (int T = 0; T < NRT; ++T) {
+        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NKS2; ++ks) acc = mfma_bf16(lAT[(T * NKS2 + ks) * 64 + lane], B2[ks], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int fi = 4 * T + r;
+          if (fi < NV) {
+            const int dd = fi / U4, m = fi % U4;
+            d0[((size_t)dd * L + t) * U4 * 64 + m * 64] = f2bf(acc[r] + alv * dev[fi]);
+          }
+        }
+      }
+      // ---- stage H / dP for dW1 (image row 16 (t & 1) + n), flush every step pair
+      const int rr = 16 * (t & 1) + n;
+      uint32_t* hw = reinterpret_cast<uint32_t*>(himg + rr * HCP + q * NVP);
+#pragma unroll
+      for (int p = 0; p < NVP / 2; ++p) hw[p] = (uint32_t)hb[2 * p] | ((uint32_t)hb[2 * p + 1] << 16);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        *reinterpret_cast<u16x4_t*>(pimg + rr * JCP + q * NJ + 4 * m) =
+            u16x4_t{f2bf(dp[m][0]), f2bf(dp[m][1]), f2bf(dp[m][2]), f2bf(dp[m][3])};
+      if ((t & 1) || t == L - 1) {
+        if (!(t & 1)) {
+          // lone last step (L odd): rows 16..31 still hold the previous (already flushed) pair
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+            *reinterpret_cast<u16x4_t*>(pimg + (16 + n) * JCP + q * NJ + 4 * m) = u16x4_t{0, 0, 0, 0};
+        }
+        lds_order();
+        u16x8_t fb[MT];
+#pragma unroll
+        for (int b = 0; b < MT; ++b) fb[b] = tr8(pimg, JCP, 16 * b, q, n);
+#pragma unroll
+        for (int a = 0; a < HT; ++a) {
+          const u16x8_t fa = tr8(himg, HCP, 16 * a, q, n);
+#pragma unroll
+          for (int b = 0; b < MT; ++b) accW[a][b] = mfma_bf16(fa, fb[b], accW[a][b]);
+        }
+        lds_order();   // the next pair's stores come after these reads (in-order LDS)
+      }
+      cur = nxt;
+    }
+  }
+  // ---- workgroup reduction into the slab (LDS reused as fp32 after a barrier)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  for (int i = threadIdx.x; i < C::NS; i += 256) red[i] = 0.f;
+  __syncthreads();
+  float d1s[MT][4], d2s[MT][4];   // cross-lane sums first (every lane takes part in the shuffles)
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      d1s[m][r] = group16_sum(db1a[m][r]);
+      d2s[m][r] = group16_sum(dw2a[m][r]);
+    }
+  // un-permute the image columns: H column c -> feature i, dP column c' -> projection row j
+  int jmap[MT];
+#pragma unroll
+  for (int b = 0; b < MT; ++b) {
+    const int c = 16 * b + n, qq = c / NJ, idx = c % NJ;
+    const int j = 16 * (idx >> 2) + 4 * qq + (idx & 3);
+    jmap[b] = (qq < 4 && j < H2) ? j : -1;
+  }
+  ordered_wave_accumulate(wave, 4, [&] {   // deterministic summation order
+#pragma unroll
+    for (int a = 0; a < HT; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = 16 * a + 4 * q + r, qq = c / NVP, idx = c % NVP;
+        if (qq >= 4 || idx >= NV) continue;
+        const int row = rfeat<U>(idx, qq) * H2;
+#pragma unroll
+        for (int b = 0; b < MT; ++b)
+          if (jmap[b] >= 0) red[row + jmap[b]] += accW[a][b][r];
+      }
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = 16 * m + 4 * q + r;
+        if (n == 0 && j < H2) {
+          red[H2 * H2 + j] += d1s[m][r];
+          red[H2 * H2 + H2 + j] += d2s[m][r];
+        }
+      }
+  });
+  for (int i = threadIdx.x; i < C::NS; i += 256) slab[(size_t)blockIdx.x * C::NS + i] = red[i];
+}
+
+// ------------------------------------------------------------------------------------------
+namespace ina {
+
+template <int U>
+static size_t rec_attn_bwd_lds() {
+  using C = RA<U>;
+  const size_t b = (size_t)(C::NA + C::NA2) * 16 + 2 * C::MT * 16 * 4 + 4 * (size_t)C::WAVE_IMG;
+  const size_t r = (size_t)C::NS * 4;
+  return b > r ? b : r;
+}
+
+template <int U>
+static int rec_attn_fwd_t(const void* rec, const unsigned char* dmask, float inv_kp, const AttnArgs& a,
+                          hipStream_t st) {
+  const int ntiles = (a.S + 15) / 16;
+  hipLaunchKernelGGL((rec_attn_fwd_kernel<U>), dim3((ntiles + 3) / 4), dim3(256), 0, st, (const unsigned short*)rec,
+                     dmask, a.S, a.L, inv_kp, a.inst, a.mask, (const u16x8_t*)a.w1pack, a.b1, a.w2, a.e, a.alphas);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int U>
+static int rec_attn_bwd_t(const void* rec, const unsigned char* dmask, float inv_kp, const AttnArgs& a,
+                          hipStream_t st) {
+  const size_t lds = rec_attn_bwd_lds<U>();
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)rec_attn_bwd_kernel<U>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+  hipLaunchKernelGGL((rec_attn_bwd_kernel<U>), dim3(a.blocks), dim3(256), lds, st, (const unsigned short*)rec, dmask,
+                     a.S, a.L, inv_kp, (const u16x8_t*)a.w1pack, (const u16x8_t*)a.w1tpack, a.b1, a.w2, a.de,
+                     a.e, a.alphas, (unsigned short*)a.dHraw, a.slab);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int U>
+static int rec_attn_bwd_resident_t() {
+  static int cached = -1;
+  if (cached >= 0) return cached;
+  const size_t lds = rec_attn_bwd_lds<U>();
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)rec_attn_bwd_kernel<U>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rec_attn_bwd_kernel<U>, 256, lds) != hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    per_cu = cus = 0;
+  cached = per_cu * cus;
+  return cached;
+}
+
+#define INA_RA_DISPATCH(EXPR_U) \
+  if (U == 8) return EXPR_U(8); \
+  if (U == 20) return EXPR_U(20); \
+  if (U == 32) return EXPR_U(32); \
+  return -1;
+
+int rec_attn_fwd(const void* rec, const unsigned char* dmask, float inv_kp, const AttnArgs& a, int U, hipStream_t st) {
+  if (a.S <= 0) return 0;
+#define INA_RA_F(UV) rec_attn_fwd_t<UV>(rec, dmask, inv_kp, a, st)
+  INA_RA_DISPATCH(INA_RA_F)
+#undef INA_RA_F
+}
+int rec_attn_bwd(const void* rec, const unsigned char* dmask, float inv_kp, const AttnArgs& a, int U, hipStream_t st) {
+  if (a.S <= 0) return 0;
+#define INA_RA_B(UV) rec_attn_bwd_t<UV>(rec, dmask, inv_kp, a, st)
+  INA_RA_DISPATCH(INA_RA_B)
+#undef INA_RA_B
+}
+int rec_attn_bwd_resident_blocks(int U) {
+#define INA_RA_R(UV) rec_attn_bwd_resident_t<UV>()
+  INA_RA_DISPATCH(INA_RA_R)
+#undef INA_RA_R
+}
+#undef INA_RA_DISPATCH
+
+}  // namespace ina

@@ -3,10 +3,12 @@
 One ``torch.autograd.Function`` spans the whole encoder so that the bf16 BiLSTM output never
 crosses an autograd boundary (its gradient stays fp32 inside ``backward``).
 
-forward:  lstm_fwd (gather + MFMA recurrence, both directions; applies the output dropout once and
-          stores the dropped copy)  ->  attn_fwd (MFMA projection, masked softmax, pooling)
-backward: attn_bwd (recompute projection, dH, dW1/db1/dw2 slabs)  ->  lstm_bwd (re-applies the dropout
-          mask from the counter hash, BPTT, dW/db/pos slabs)
+forward:  lstm_fwd (gather + MFMA recurrence, both directions; step records + dropout keep bits)
+          ->  attention (MFMA projection, masked softmax, pooling)
+backward: attention backward (recompute projection, dH, dW1/db1/dw2 slabs)  ->  lstm_bwd (re-applies
+          the dropout keep bits, BPTT, dW/db/pos slabs)
+bf16 (default): the attention kernels read the LSTM step records directly (rec_attn.hip; dH goes back
+in lstm_bwd's lane layout); fp32 or fuse_rec_attn=False: natural-layout H rows + attn_fwd / attn_bwd.
 
 Reference layers: model/base.py:76-86 (embedding), model/graph.py:30-53 (BiLSTM + attention),
 model/layer_module.py:49-98 (self_attention).
@@ -18,7 +20,7 @@ import weakref
 import torch
 
 from ._ext import ops
-from .packing import lstm_shape, pack_attn, pack_lstm
+from .packing import lstm_shape, pack_attn, pack_attn_rec, pack_lstm
 
 
 def _route_grad(meta, name, g):
@@ -78,23 +80,26 @@ class EncoderFn(torch.autograd.Function):
             bias = torch.stack([bf.detach(), bb.detach()]).float().contiguous()
         need_grad = ctx.needs_input_grad[5:15].count(True) > 0 if hasattr(ctx, "needs_input_grad") else True
         kp = float(meta["keep_prob"])
-        w1pack, w1tpack = (pk["w1pack"], pk["w1tpack"]) if pk is not None else pack_attn(W1, bf16)
         lstm_args = (inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
                      p2emb.detach().contiguous(), apack, bias, U, sh["NX"])
         tail = (int(meta["seed"]), kp, meta.get("seed_dev"),
                 word_rows(word, wemb, bool(meta.get("word_grad", False))) if bf16 else None)
         b1c, w2c = b1.detach().contiguous(), w2.detach().reshape(-1).contiguous()
-        if bf16 and meta.get("fuse_hnat_attn", True) and o.hnat_attn_ok(U, word.shape[1], kp):
-            # LSTM output transpose + dropout fused with the attention forward (hnat_attn_kernel)
+        rec = bf16 and meta.get("fuse_rec_attn", True) and o.rec_attn_ok(U, word.shape[1])
+        if rec:
+            # attention straight from the step records (no natural-layout copy of H)
+            w1pack, w1tpack = ((pk["w1rpack"], pk["w1rtpack"]) if pk is not None and "w1rpack" in pk
+                               else pack_attn_rec(W1))
             hlane, cst, hnat, dmask, xg, e, alphas = o.lstm_attn_fwd(*lstm_args, bool(need_grad), *tail,
                                                                      mask, w1pack, b1c, w2c)
         else:
+            w1pack, w1tpack = (pk["w1pack"], pk["w1tpack"]) if pk is not None else pack_attn(W1, bf16)
             hlane, cst, hnat, dmask, xg = o.lstm_fwd(*lstm_args, bf16, bool(need_grad), *tail)
             e, alphas = o.attn_fwd(hnat, inst, mask, w1pack, b1c, w2c, U, bf16, int(meta.get("attn_blocks", 0)))
         if need_grad:
             ctx.save_for_backward(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst,
-                                  w1pack, w1tpack, b1, w2, alphas, hnat, dmask, xg)
-            ctx.meta = dict(meta, NX=sh["NX"], DIN=DIN)
+                                  w1pack, w1tpack, b1, w2, alphas, hnat, dmask, xg, e)
+            ctx.meta = dict(meta, NX=sh["NX"], DIN=DIN, rec=rec)
         ctx.mark_non_differentiable(alphas)
         ctx.set_materialize_grads(False)   # no zero-fill launch for the alphas gradient
         return e, alphas
@@ -103,13 +108,17 @@ class EncoderFn(torch.autograd.Function):
     def backward(ctx, de, _dalpha):
         o = ops()
         (inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst, w1pack, w1tpack, b1, w2,
-         alphas, hnat, dmask, xg) = ctx.saved_tensors
+         alphas, hnat, dmask, xg, e) = ctx.saved_tensors
         m = ctx.meta
         U, bf16, DIN = m["U"], m["bf16"], m["DIN"]
         H2 = 2 * U
-        dH, aslab = o.attn_bwd(hnat, inst, w1pack, w1tpack, b1.detach().contiguous(),
-                               w2.detach().reshape(-1).contiguous(), de.contiguous().float(), alphas, U, bf16,
-                               int(m.get("attn_blocks", 0)))
+        b1c, w2c = b1.detach().contiguous(), w2.detach().reshape(-1).contiguous()
+        if m["rec"]:   # dH in lstm_bwd's lane layout [tiles, 2, L, U/4, 64]
+            dH, aslab = o.rec_attn_bwd(hlane, dmask, w1pack, w1tpack, b1c, w2c, de.contiguous().float(), e, alphas,
+                                       U, float(m["keep_prob"]), int(m.get("attn_blocks", 0)))
+        else:
+            dH, aslab = o.attn_bwd(hnat, inst, w1pack, w1tpack, b1c, w2c, de.contiguous().float(), alphas, U, bf16,
+                                   int(m.get("attn_blocks", 0)))
         word_grad = bool(m.get("word_grad", False))
         dw_slab, dpos_slab, dwemb = o.lstm_bwd(inst, word, pos1, pos2, wemb.detach().contiguous(),
                                                p1emb.detach().contiguous(), p2emb.detach().contiguous(), apack, a2pack,

@@ -26,7 +26,7 @@ import numpy as np
 import torch
 
 from ._ext import ops
-from .packing import _attn_idx, _lstm_idx, _ntn_m_idx, _ntn_w_idx, lstm_shape
+from .packing import _attn_idx, _attn_rec_idx, _lstm_idx, _ntn_m_idx, _ntn_w_idx, lstm_shape
 
 
 class StepGlue:
@@ -110,6 +110,10 @@ class StepGlue:
         Z = H2 * H2
         put("w1pack", np.where(pi < Z, off["attn_kernel"] + pi, -1), bf16)
         put("w1tpack", np.where(ti < Z, off["attn_kernel"] + ti, -1), bf16)
+        if bf16 and U in (8, 20, 32):   # record-layout attention kernels (ops/packing.py::_attn_rec_idx)
+            ri, rti = (t.numpy() for t in _attn_rec_idx(U))
+            put("w1rpack", np.where(ri < Z, off["attn_kernel"] + ri, -1), True)
+            put("w1rtpack", np.where(rti < Z, off["attn_kernel"] + rti, -1), True)
         if head is not None:
             H, h, N, paper = head
             mi, m2i = (t.numpy() for t in _ntn_m_idx(H, h))

@@ -142,6 +142,57 @@ def pack_attn(W1: torch.Tensor, bf16: bool):
     return We[_on(pi, dev)].to(dt).contiguous(), We[_on(ti, dev)].to(dt).contiguous()
 
 
+@lru_cache(maxsize=None)
+def _attn_rec_idx(U: int):
+    """Flat indices into [W1 [2U, 2U] | 0] for the record-layout attention kernels (rec_attn.hip).
+    Lane group q owns the features rfeat(idx, q) = (idx // U4) * U + 4 * (idx % U4) + q, idx < 2 * U4.
+      w1r  [MT][NKR][64][8]:  A[row j = 16 m + (l & 15)][k slot (l >> 4, jj)] = W1[rfeat(8 ks + jj, l >> 4)][j]
+      w1rt [NRT][NKS2][64][8]: A[row (qr, rr) = l & 15][k slot (l >> 4, jj)] = W1[rfeat(4 T + rr, qr)][j] with
+                              j = 16 (idx >> 2) + 4 (l >> 4) + (idx & 3), idx = 8 ks + jj (dP accumulator order)."""
+    U4, H2 = U // 4, 2 * U
+    NV, MT = 2 * U4, (H2 + 15) // 16
+    NKR, NJ = (NV + 7) // 8, 4 * MT
+    NKS2, NRT = (NJ + 7) // 8, (NV + 3) // 4
+    Z = H2 * H2
+
+    def rfeat(idx, q):
+        return (idx // U4) * U + 4 * (idx % U4) + q
+
+    p = np.full((MT, NKR, 64, 8), Z, dtype=np.int64)
+    for m in range(MT):
+        for ks in range(NKR):
+            for l in range(64):
+                j = 16 * m + (l & 15)
+                for jj in range(8):
+                    idx = 8 * ks + jj
+                    if idx < NV and j < H2:
+                        p[m, ks, l, jj] = rfeat(idx, l >> 4) * H2 + j
+    t = np.full((NRT, NKS2, 64, 8), Z, dtype=np.int64)
+    for T in range(NRT):
+        for ks in range(NKS2):
+            for l in range(64):
+                r16 = l & 15
+                fi = 4 * T + (r16 & 3)
+                if fi >= NV:
+                    continue
+                i = rfeat(fi, r16 >> 2)
+                for jj in range(8):
+                    idx = 8 * ks + jj
+                    j = 16 * (idx >> 2) + 4 * (l >> 4) + (idx & 3)
+                    if idx < NJ and j < H2:
+                        t[T, ks, l, jj] = i * H2 + j
+    return torch.from_numpy(p), torch.from_numpy(t)
+
+
+def pack_attn_rec(W1: torch.Tensor):
+    """-> (w1r, w1rt) bf16 packs of the record-layout attention kernels (see _attn_rec_idx)."""
+    U = W1.shape[0] // 2
+    pi, ti = _attn_rec_idx(U)
+    dev = W1.device
+    We = torch.cat([W1.detach().float().reshape(-1), W1.new_zeros(1, dtype=torch.float32)])
+    return We[_on(pi, dev)].to(torch.bfloat16).contiguous(), We[_on(ti, dev)].to(torch.bfloat16).contiguous()
+
+
 # ------------------------------------------------------------------ NTN (bf16 only)
 def _kmap32(q: int, j: int) -> int:
     return 16 * (j >> 2) + 4 * q + (j & 3)

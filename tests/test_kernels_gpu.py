@@ -144,13 +144,17 @@ def test_attention_forward(dtype, keep_prob):
     assert ee < tol and ea < tol
 
 
-@pytest.mark.parametrize("keep_prob,store", [(1.0, True), (0.9, True), (1.0, False)])
-@pytest.mark.parametrize("tail", [0, 5])
-def test_fused_hnat_attention_matches_unfused(keep_prob, store, tail):
-    """lstm_attn_fwd (transpose + dropout + attention in one kernel) == lstm_fwd + attn_fwd, bitwise."""
+def _lane_to_natural(x, S):
+    """[tiles, 2, L, U/4, 64] (step-record lane layout) -> [S, L, 2U]."""
+    T, _, L, U4, _ = x.shape
+    y = x.view(T, 2, L, U4, 4, 16).permute(0, 5, 2, 1, 3, 4)   # tile, n, t, dir, m, q
+    return y.reshape(T * 16, L, 8 * U4)[:S]
+
+
+def _rec_problem(keep_prob, tail, u=20):
     from induction_network_on_fewrel_amd.ops import ops
-    from induction_network_on_fewrel_amd.ops.packing import lstm_shape, pack_attn, pack_lstm
-    cfg, data, model, dd, inst, _ = _problem(dtype="bf16")
+    from induction_network_on_fewrel_amd.ops.packing import lstm_shape, pack_attn, pack_attn_rec, pack_lstm
+    cfg, data, model, dd, inst, _ = _problem(dtype="bf16", u=u)
     if tail:
         inst = inst[: inst.shape[0] - tail].contiguous()   # a partial last 16-sequence tile
     p = model.pdict()
@@ -159,22 +163,66 @@ def test_fused_hnat_attention_matches_unfused(keep_prob, store, tail):
     apack, _ = pack_lstm(p["lstm_fw_kernel"], p["lstm_bw_kernel"], U, DIN, True)
     bias = torch.stack([p["lstm_fw_bias"], p["lstm_bw_bias"]]).detach().float().contiguous()
     word, pos1, pos2, mask = dd.arrays()
-    assert ops().hnat_attn_ok(U, word.shape[1], keep_prob)
+    assert ops().rec_attn_ok(U, word.shape[1])
     args = (inst, word, pos1, pos2, p["word_embedding"].detach(), p["pos1_embedding"].detach(),
             p["pos2_embedding"].detach(), apack, bias, U, lstm_shape(U, DIN, True)["NX"])
-    w1p, _ = pack_attn(p["attn_kernel"], True)
-    b1 = p["attn_bias"].detach().contiguous()
-    w2 = p["attn_w2"].detach().reshape(-1).contiguous()
+    return dict(U=U, inst=inst, mask=mask, args=args, packs=pack_attn(p["attn_kernel"], True),
+                rpacks=pack_attn_rec(p["attn_kernel"]), b1=p["attn_bias"].detach().contiguous(),
+                w2=p["attn_w2"].detach().reshape(-1).contiguous())
+
+
+@pytest.mark.parametrize("keep_prob,store", [(1.0, True), (0.9, True), (1.0, False)])
+@pytest.mark.parametrize("tail", [0, 5])
+@pytest.mark.parametrize("u", [8, 20, 32])
+def test_rec_attention_forward_matches_natural(keep_prob, store, tail, u):
+    """lstm_attn_fwd (attention straight from the step records, rec_attn_fwd_kernel) == lstm_fwd +
+    attn_fwd on the natural rows: same records / keep bits bitwise, (e, alphas) to fp32 rounding (the
+    record kernel pools with an online softmax)."""
+    from induction_network_on_fewrel_amd.ops import ops
+    P = _rec_problem(keep_prob, tail, u)
+    U, inst, mask, args = P["U"], P["inst"], P["mask"], P["args"]
     hl0, _, hn0, dm0, _ = ops().lstm_fwd(*args, True, True, 77, keep_prob, None, None)
-    e0, a0 = ops().attn_fwd(hn0, inst, mask, w1p, b1, w2, U, True, 0)
-    hl1, _, hn1, dm1, _, e1, a1 = ops().lstm_attn_fwd(*args, store, 77, keep_prob, None, None, mask, w1p, b1, w2)
+    e0, a0 = ops().attn_fwd(hn0, inst, mask, P["packs"][0], P["b1"], P["w2"], U, True, 0)
+    hl1, _, hn1, dm1, _, e1, a1 = ops().lstm_attn_fwd(*args, store, 77, keep_prob, None, None, mask, P["rpacks"][0],
+                                                      P["b1"], P["w2"])
     torch.cuda.synchronize()
-    assert hn1.shape == hn0.shape and e1.shape == e0.shape and a1.shape == a0.shape
-    if store:   # eval mode (no backward) leaves the natural rows unwritten
-        assert torch.equal(hl1, hl0) and torch.equal(dm1, dm0)
-        assert torch.equal(hn1, hn0), "natural rows differ"
-    assert torch.equal(e1, e0), (e1 - e0).abs().max()
-    assert torch.equal(a1, a0), (a1 - a0).abs().max()
+    assert hn1.numel() == 0 and e1.shape == e0.shape and a1.shape == a0.shape
+    # h slots always; the c slots only when stored (the no-backward kernel leaves them unwritten)
+    assert torch.equal(hl1[:, :, :, 0], hl0[:, :, :, 0]) and torch.equal(dm1, dm0)
+    if store:
+        assert torch.equal(hl1, hl0)
+    torch.testing.assert_close(e1, e0, rtol=2e-5, atol=2e-6)
+    torch.testing.assert_close(a1, a0, rtol=2e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("keep_prob", [1.0, 0.9])
+@pytest.mark.parametrize("tail", [0, 5])
+@pytest.mark.parametrize("u", [8, 20, 32])
+def test_rec_attention_backward_matches_natural(keep_prob, tail, u):
+    """rec_attn_bwd (records in, dH out in lstm_bwd's lane layout) against attn_bwd on the natural rows:
+    dH (bf16) and the dW1 / db1 / dw2 slab sums."""
+    from induction_network_on_fewrel_amd.ops import ops
+    P = _rec_problem(keep_prob, tail, u)
+    U, inst, mask, args = P["U"], P["inst"], P["mask"], P["args"]
+    hl, _, hn, dm, _ = ops().lstm_fwd(*args, True, True, 77, keep_prob, None, None)
+    e, a = ops().attn_fwd(hn, inst, mask, P["packs"][0], P["b1"], P["w2"], U, True, 0)
+    de = torch.randn_like(e)
+    dH0, s0 = ops().attn_bwd(hn, inst, P["packs"][0], P["packs"][1], P["b1"], P["w2"], de, a, U, True, 0)
+    dHl, s1 = ops().rec_attn_bwd(hl, dm, P["rpacks"][0], P["rpacks"][1], P["b1"], P["w2"], de, e, a, U, keep_prob, 0)
+    torch.cuda.synchronize()
+    dH1 = _lane_to_natural(dHl, inst.shape[0])
+    err = _relerr(dH1.float(), dH0.float())
+    g0, g1 = s0.sum(0), s1.sum(0)
+    H2 = 2 * U
+    parts = {k: _relerr(g1[a:b], g0[a:b]) for k, (a, b) in
+             dict(dW1=(0, H2 * H2), db1=(H2 * H2, H2 * H2 + H2), dw2=(H2 * H2 + H2, H2 * H2 + 2 * H2)).items()}
+    print(f"rec attn bwd u={u} kp={keep_prob}: dH {err:.2e} " + " ".join(f"{k} {v:.2e}" for k, v in parts.items()))
+    assert err < 1e-2 and max(parts.values()) < 2e-3
+    # padding sequences of the last tile get exactly zero dH
+    v = inst.shape[0] - 16 * (dHl.shape[0] - 1)
+    if v < 16:
+        pad = dHl[-1].reshape(2, -1, 4, 16)[..., v:]
+        assert pad.float().abs().max().item() == 0
 
 
 def _encoder_grads_ref(model, dd, inst, de, keep_prob, seed, bf16):
