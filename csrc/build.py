@@ -27,6 +27,10 @@ OUT_DIR = os.path.join(ROOT, "build", "obj" + (f"_{_TAG}" if _TAG else ""))
 LIB = (os.path.join(ROOT, "variants", f"_ina_kernels_{_TAG}.so") if _TAG
        else os.path.join(ROOT, "induction_network_on_fewrel_amd", "_ina_kernels.so"))
 ARCH = os.environ.get("INA_OFFLOAD_ARCH", "gfx950")
+# Per-file code generation flags.  rec_attn.hip: MFMA results in VGPRs (gfx950's unified register
+# file allows it); the default AGPR form cost 12 v_accvgpr_read per token step of the attention
+# forward, whose tanh / softmax epilogue reads every accumulator back on the VALU.
+FILE_FLAGS = {"rec_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 
 
 def _torch_paths():
@@ -66,7 +70,8 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
         objs.append(obj)
         if _newer(obj, [src, *headers, __file__]):
             tasks.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", *_VFLAGS,
-                          "-I" + os.path.join(CSRC, "include"), "-c", src, "-o", obj])
+                          *FILE_FLAGS.get(os.path.basename(src), []), "-I" + os.path.join(CSRC, "include"), "-c", src,
+                          "-o", obj])
     for bsrc in sorted(glob.glob(os.path.join(CSRC, "*.cpp"))):   # host-only torch bindings (g++)
         bobj = os.path.join(OUT_DIR, os.path.basename(bsrc) + ".o")
         objs.append(bobj)

@@ -72,6 +72,16 @@ INA_DEVICE float tanhf_(float x) {
 constexpr float LOG2E_F = 1.44269504088896341f;
 INA_DEVICE float sigmoid_l2(float z) { return fast_rcp(1.0f + __builtin_amdgcn_exp2f(-z)); }
 INA_DEVICE float tanh_l2(float z) { return 1.0f - 2.0f * fast_rcp(__builtin_amdgcn_exp2f(z) + 1.0f); }
+// r = 1 / (e^{2x} + 1): tanh(x) = 1 - 2 r and 1 - tanh(x)^2 = 4 r (1 - r) (same rounding as tanhf_)
+INA_DEVICE float tanh_r(float x) { return fast_rcp(__builtin_amdgcn_exp2f(x * (2.0f * LOG2E_F)) + 1.0f); }
+// the same for a 4-vector (the range multiply as two packed v_pk_mul_f32)
+INA_DEVICE f32x4_t tanh_r4(f32x4_t x) {
+  x *= 2.0f * LOG2E_F;
+  f32x4_t r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = fast_rcp(__builtin_amdgcn_exp2f(x[i]) + 1.0f);
+  return r;
+}
 
 // ------------------------------------------------------------------ RNG
 // Counter-based hash; bit-identical to models/reference.py::hash_u32.

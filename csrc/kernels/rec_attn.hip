@@ -71,28 +71,76 @@ template <int U>
 struct RecStep {
   unsigned short h[RA<U>::NV];
   uint32_t kb;
+  float al;   // backward: alpha of the step (prefetched with the records)
 };
+// k0 / k1 always point at readable memory (the records themselves without dropout) and kor = 0xFFFF
+// then sets every keep bit: no branch around the loads (an exec-masked load block here made the
+// compiler wait vmcnt(0) right after issuing the prefetch)
 template <int U>
 INA_DEVICE void rec_load(const unsigned short* r0, const unsigned short* r1, const unsigned char* k0,
-                         const unsigned char* k1, int t, RecStep<U>& o) {
+                         const unsigned char* k1, uint32_t kor, int t, RecStep<U>& o) {
   constexpr int U4 = RA<U>::U4, RSTEP = RA<U>::RSTEP;
 #pragma unroll
   for (int m = 0; m < U4; ++m) {
     o.h[m] = r0[t * RSTEP + m * 64];
     o.h[U4 + m] = r1[t * RSTEP + m * 64];
   }
-  o.kb = k0 ? ((uint32_t)k0[t * 64] | ((uint32_t)k1[t * 64] << 8)) : 0xFFFFu;
+  o.kb = ((uint32_t)k0[t * 64] | ((uint32_t)k1[t * 64] << 8)) | kor;
+}
+// token loop over ping-pong step buffers (2x unrolled): the prefetch of step t+1 goes into the other
+// buffer, so no register copy of in-flight load results (a cur = nxt rotation forces vmcnt(0) at
+// the loop latch, i.e. no overlap at all)
+#ifndef INA_RA_PF_FWD
+#define INA_RA_PF_FWD 1   // forward prefetch distance in token steps (1: two buffers, 2: three)
+#endif
+template <int U, int PF, class LD, class F>
+INA_DEVICE void rec_steps(int L, LD&& load, F&& step) {
+  if constexpr (PF == 1) {
+  RecStep<U> a, b;
+  load(0, a);
+  int t = 0;
+  for (; t + 1 < L; t += 2) {
+    load(t + 1, b);
+    step(t, a);
+    load(t + 2 < L ? t + 2 : t + 1, a);
+    step(t + 1, b);
+  }
+  if (t < L) step(t, a);
+  } else {
+  RecStep<U> a, b, c;
+  auto cl = [&](int x) { return x < L ? x : L - 1; };
+  load(0, a);
+  load(cl(1), b);
+  int t = 0;
+  for (; t + 2 < L; t += 3) {
+    load(t + 2, c);
+    step(t, a);
+    load(cl(t + 3), a);
+    step(t + 1, b);
+    load(cl(t + 4), b);
+    step(t + 2, c);
+  }
+  if (t < L) step(t, a);
+  if (t + 1 < L) step(t + 1, b);
+  }
 }
 // DropoutWrapper output (model/graph.py:36-38): keep ? bf16(h / keep_prob) : 0 -- the same rounding
-// as h_natural_kernel, so both attention paths see identical H
+// as h_natural_kernel, so both attention paths see identical H.  Branch-free (a select here compiled
+// to one branch per element): scale = keep bit * inv_kp (inv_kp = 1 and all bits set without
+// dropout, which reproduces h exactly).  Two values per call: packed bf16 pair (B operand word) and
+// the rounded fp32 values.
 template <int U>
-INA_DEVICE unsigned short rec_drop(const RecStep<U>& s, int idx, bool drop, float inv_kp) {
+INA_DEVICE uint32_t rec_drop2(const RecStep<U>& s, int i, float inv_kp, float& v0, float& v1) {
   constexpr int U4 = RA<U>::U4;
-  const unsigned short h = s.h[idx];
-  if (!drop) return h;
-  const int bit = idx < U4 ? idx : 8 + idx - U4;
-  return ((s.kb >> bit) & 1u) ? f2bf(bf2f(h) * inv_kp) : (unsigned short)0;
+  const int b0 = i < U4 ? i : 8 + i - U4, b1 = i + 1 < U4 ? i + 1 : 8 + i + 1 - U4;
+  const float x0 = bf2f(s.h[i]) * ((float)((s.kb >> b0) & 1u) * inv_kp);
+  const float x1 = bf2f(s.h[i + 1]) * ((float)((s.kb >> b1) & 1u) * inv_kp);
+  const uint32_t w = (uint32_t)f2bf(x0) | ((uint32_t)f2bf(x1) << 16);
+  v0 = __builtin_bit_cast(float, w << 16);
+  v1 = __builtin_bit_cast(float, w & 0xFFFF0000u);
+  return w;
 }
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
 INA_DEVICE u16x8_t tr8(const unsigned short* img, int stride, int c0, int q, int n) {
   const s16x4_t lo = tr_read(img + (8 * q + (n >> 2)) * stride + c0 + 4 * (n & 3));
@@ -150,28 +198,31 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
   const bool drop = dmask != nullptr;
   const unsigned short* r0 = rec + (size_t)tile * 2 * L * C::RSTEP + lane;
   const unsigned short* r1 = r0 + (size_t)L * C::RSTEP;
-  const unsigned char* k0 = drop ? dmask + (size_t)tile * 2 * L * 64 + lane : nullptr;
-  const unsigned char* k1 = drop ? k0 + (size_t)L * 64 : nullptr;
+  const unsigned char* k0 = drop ? dmask + (size_t)tile * 2 * L * 64 + lane : reinterpret_cast<const unsigned char*>(r0);
+  const unsigned char* k1 = drop ? k0 + (size_t)L * 64 : k0;
+  const uint32_t kor = drop ? 0u : 0xFFFFu;
   float* arow = alphas + (size_t)seqc * L;
-
-  RecStep<U> cur, nxt;
-  rec_load<U>(r0, r1, k0, k1, 0, cur);
+  // sum_j w_j tanh(x_j) = sum_j w_j - 2 sum_j w_j r_j (tanh_r): the lane's share of sum_j w_j
+  float wl = 0.f;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) wl += lbw[MT * 16 + 16 * m + 4 * q + r];
   float mx = -INFINITY, lsum = 0.f, ea[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) ea[i] = 0.f;
-  for (int t = 0; t < L; ++t) {
-    rec_load<U>(r0, r1, k0, k1, t + 1 < L ? t + 1 : t, nxt);   // one step of prefetch
+  auto load = [&](int t, RecStep<U>& o) { rec_load<U>(r0, r1, k0, k1, kor, t, o); };
+  rec_steps<U, INA_RA_PF_FWD>(L, load, [&](int t, const RecStep<U>& cur) {
     float v[NV];
+    u32x4_t Bw[NKR];
+#pragma unroll
+    for (int ks = 0; ks < NKR; ++ks) Bw[ks] = u32x4_t{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < NV; i += 2) Bw[i / 8][(i % 8) / 2] = rec_drop2<U>(cur, i, inv_kp, v[i], v[i + 1]);
     u16x8_t B[NKR];
 #pragma unroll
-    for (int ks = 0; ks < NKR; ++ks) B[ks] = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const unsigned short hb = rec_drop<U>(cur, i, drop, inv_kp);
-      v[i] = bf2f(hb);
-      B[i / 8][i % 8] = hb;
-    }
-    float sp = 0.f;
+    for (int ks = 0; ks < NKR; ++ks) B[ks] = __builtin_bit_cast(u16x8_t, Bw[ks]);
+    float sr = 0.f;
     asm volatile("" ::: "memory");   // re-read the LDS weights per step (no hoisting into registers)
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
@@ -180,9 +231,10 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
       f32x4_t acc = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
       for (int ks = 0; ks < NKR; ++ks) acc = mfma_bf16(lA[(m * NKR + ks) * 64 + lane], B[ks], acc);
-      sp += wv.x * tanhf_(acc[0]) + wv.y * tanhf_(acc[1]) + wv.z * tanhf_(acc[2]) + wv.w * tanhf_(acc[3]);
+      const f32x4_t rr = tanh_r4(acc);
+      sr += wv.x * rr[0] + wv.y * rr[1] + wv.z * rr[2] + wv.w * rr[3];
     }
-    sp = cross_group_sum(sp);
+    const float sp = cross_group_sum(wl - 2.f * sr);
     const uint32_t on = t < 32 ? (mlo >> t) & 1u : (mhi >> (t - 32)) & 1u;
     const float sc = on ? sp : sp + -2147483648.f;
     // online softmax: rescale the running sum and pooled vector when the max moves
@@ -193,8 +245,7 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
     for (int i = 0; i < NV; ++i) ea[i] = ea[i] * c + p * v[i];
     mx = mn;
     if ((t & 3) == q && valid) arow[t] = sc;
-    cur = nxt;
-  }
+  });
   const float inv = 1.f / lsum;
   if (valid) {
 #pragma unroll
@@ -249,7 +300,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3
   for (int a = 0; a < HT; ++a)
 #pragma unroll
     for (int b = 0; b < MT; ++b) accW[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float dw2a[MT][4], db1a[MT][4];
+  float dw2a[MT][4], db1a[MT][4], sds = 0.f;   // dw2a: sum ds rr; sds: sum ds
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -269,20 +320,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3
       const size_t o = (size_t)seqc * H2 + rfeat<U>(i, q);
       const float x = valid ? de[o] : 0.f;
       lde[i] = x;
-      sd += x * e_fwd[o];
+      sd = fmaf(x, e_fwd[o], sd);   // same sequential fma order as d(alpha) below: exact 0 for L = 1
     }
     sd = cross_group_sum(sd);
     const float* arow = alphas + (size_t)seqc * L;
     const unsigned short* r0 = rec + (size_t)tile * 2 * L * C::RSTEP + lane;
     const unsigned short* r1 = r0 + (size_t)L * C::RSTEP;
-    const unsigned char* k0 = drop ? dmask + (size_t)tile * 2 * L * 64 + lane : nullptr;
-    const unsigned char* k1 = drop ? k0 + (size_t)L * 64 : nullptr;
+    const unsigned char* k0 = drop ? dmask + (size_t)tile * 2 * L * 64 + lane : reinterpret_cast<const unsigned char*>(r0);
+    const unsigned char* k1 = drop ? k0 + (size_t)L * 64 : k0;
+    const uint32_t kor = drop ? 0u : 0xFFFFu;
     unsigned short* d0 = dHl + (size_t)tile * 2 * L * U4 * 64 + lane;   // dir 0; dir 1 at + L * U4 * 64
-    RecStep<U> cur, nxt;
-    rec_load<U>(r0, r1, k0, k1, 0, cur);
-    for (int t = 0; t < L; ++t) {
-      rec_load<U>(r0, r1, k0, k1, t + 1 < L ? t + 1 : t, nxt);
-      const float alv = valid ? arow[t] : 0.f;
+    auto load = [&](int t, RecStep<U>& o) {
+      rec_load<U>(r0, r1, k0, k1, kor, t, o);
+      o.al = arow[t];
+    };
+    rec_steps<U, 1>(L, load, [&](int t, const RecStep<U>& cur) {
+      const float alv = valid ? cur.al : 0.f;
       float dev[DEPC];
       asm volatile("" ::: "memory");   // re-read de from LDS per step (no hoisting)
 #pragma unroll
@@ -290,20 +343,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3
         const float4 v4 = *reinterpret_cast<const float4*>(lde + i);
         dev[i] = v4.x; dev[i + 1] = v4.y; dev[i + 2] = v4.z; dev[i + 3] = v4.w;
       }
-      unsigned short hb[NVP];
-      u16x8_t B[NKR];
+      // H (dropped, bf16 pairs) -> B operand and straight into the dW1 image (row 16 (t & 1) + n)
+      const int rr = 16 * (t & 1) + n;
+      uint32_t* hw = reinterpret_cast<uint32_t*>(himg + rr * HCP + q * NVP);
+      u32x4_t Bw[NKR];
 #pragma unroll
-      for (int ks = 0; ks < NKR; ++ks) B[ks] = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      for (int ks = 0; ks < NKR; ++ks) Bw[ks] = u32x4_t{0u, 0u, 0u, 0u};
       float d = 0.f;
 #pragma unroll
-      for (int i = 0; i < NVP; ++i) {
-        hb[i] = i < NV ? rec_drop<U>(cur, i, drop, inv_kp) : (unsigned short)0;
-        if (i < NV) {
-          B[i / 8][i % 8] = hb[i];
-          d += dev[i] * bf2f(hb[i]);
-        }
+      for (int i = 0; i < NV; i += 2) {
+        float v0, v1;
+        const uint32_t w = rec_drop2<U>(cur, i, inv_kp, v0, v1);
+        Bw[i / 8][(i % 8) / 2] = w;
+        hw[i / 2] = w;
+        d = fmaf(dev[i], v0, d);
+        d = fmaf(dev[i + 1], v1, d);
       }
+      u16x8_t B[NKR];
+#pragma unroll
+      for (int ks = 0; ks < NKR; ++ks) B[ks] = __builtin_bit_cast(u16x8_t, Bw[ks]);
       const float ds = alv * (cross_group_sum(d) - sd);   // 0 for padding sequences (alpha 0)
+      const float ds4 = 4.f * ds;
+      sds += ds;
       float dp[MT][4];
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
@@ -316,11 +377,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3
         }
 #pragma unroll
         for (int ks = 0; ks < NKR; ++ks) acc = mfma_bf16(lA[(m * NKR + ks) * 64 + lane], B[ks], acc);
+        const f32x4_t r4 = tanh_r4(acc);                    // P = 1 - 2 rr, 1 - P^2 = 4 rr (1 - rr)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float pr = tanhf_(acc[r]);
-          dp[m][r] = ds * wv[r] * (1.f - pr * pr);
-          dw2a[m][r] += ds * pr;
+          const float rr = r4[r];
+          dp[m][r] = ds4 * (wv[r] * (rr - rr * rr));
+          dw2a[m][r] += ds * rr;                             // dw2 = sum ds P = sum ds - 2 sum ds rr
           db1a[m][r] += dp[m][r];
         }
       }
@@ -349,11 +411,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3
           }
         }
       }
-      // ---- stage H / dP for dW1 (image row 16 (t & 1) + n), flush every step pair
-      const int rr = 16 * (t & 1) + n;
-      uint32_t* hw = reinterpret_cast<uint32_t*>(himg + rr * HCP + q * NVP);
-#pragma unroll
-      for (int p = 0; p < NVP / 2; ++p) hw[p] = (uint32_t)hb[2 * p] | ((uint32_t)hb[2 * p + 1] << 16);
+      // ---- stage dP for dW1 (image row rr), flush every step pair
 #pragma unroll
       for (int m = 0; m < MT; ++m)
         *reinterpret_cast<u16x4_t*>(pimg + rr * JCP + q * NJ + 4 * m) =
@@ -377,8 +435,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3
         }
         lds_order();   // the next pair's stores come after these reads (in-order LDS)
       }
-      cur = nxt;
-    }
+    });
   }
   // ---- workgroup reduction into the slab (LDS reused as fp32 after a barrier)
   __syncthreads();
@@ -386,12 +443,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3
   for (int i = threadIdx.x; i < C::NS; i += 256) red[i] = 0.f;
   __syncthreads();
   float d1s[MT][4], d2s[MT][4];   // cross-lane sums first (every lane takes part in the shuffles)
+  const float sdsum = group16_sum(sds);
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       d1s[m][r] = group16_sum(db1a[m][r]);
-      d2s[m][r] = group16_sum(dw2a[m][r]);
+      d2s[m][r] = sdsum - 2.f * group16_sum(dw2a[m][r]);
     }
   // un-permute the image columns: H column c -> feature i, dP column c' -> projection row j
   int jmap[MT];
