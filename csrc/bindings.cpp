@@ -145,7 +145,7 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd_impl(
   if (bf16) {
     a.xg = xg.data_ptr();
     a.posb = reinterpret_cast<const unsigned short*>(xg.data_ptr<at::BFloat16>() + ntiles * L * 64 * NX);
-    check_launch(ina::x_gather(a, (int)NX, cur_stream()), "x_gather");
+    check_launch(ina::x_gather(a, (int)U, (int)NX, cur_stream()), "x_gather");
   }
   check_launch(ina::lstm_fwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_fwd");
   if (bf16 && natural)

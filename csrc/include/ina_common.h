@@ -108,6 +108,20 @@ INA_DEVICE bool dropout_keep_salted(uint32_t salt, uint32_t idx, uint32_t thr) {
 INA_DEVICE bool dropout_keep(uint32_t seed, uint32_t dir, uint32_t idx, uint32_t thr) {
   return dropout_keep_salted(dropout_salt(seed, dir), idx, thr);
 }
+// LSTM output dropout (DropoutWrapper): ONE hash per pair of adjacent units.  Element e (flat
+// (seq*L + t)*U + unit, U even) keeps iff 16-bit half (e & 1) of mix(e >> 1) is < thr >> 16
+// (keep rate floor(kp * 65536) / 65536).  Bit-identical to models/reference.py::dropout_keep_mask.
+INA_DEVICE uint32_t dropout_mix(uint32_t salt, uint32_t pidx) {
+  uint32_t x = pidx * 0x6C8E9CF5u + salt;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  return x;
+}
+INA_DEVICE bool lstm_keep(uint32_t salt, uint32_t e, uint32_t thr) {
+  const uint32_t x = dropout_mix(salt, e >> 1);
+  return ((e & 1u) ? (x >> 16) : (x & 0xFFFFu)) < (thr >> 16);
+}
 
 // ------------------------------------------------------------------ reductions
 // Cross-lane data movement without the LDS pipe: __shfl_xor lowers to ds_bpermute_b32 (an LDS

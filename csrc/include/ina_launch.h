@@ -41,8 +41,9 @@ struct LstmArgs {
   int drop;
   int dh_lane;           // bwd: dH in the step-record lane layout [tiles][2][L][U/4][64] (else [S][L][2U])
 };
-// bf16 mode: gather every token's x features once into a.xg / a.posb (lstm.hip x_gather_kernel)
-int x_gather(const LstmArgs& a, int NX, hipStream_t st);
+// bf16 mode: gather every token's x features once into a.xg / a.posb, and (a.drop) the dropout keep
+// bits into a.dmask (lstm.hip x_gather_kernel); must run before lstm_fwd in bf16 mode
+int x_gather(const LstmArgs& a, int U, int NX, hipStream_t st);
 int lstm_fwd(const LstmArgs& a, int U, int NX, bool bf16, hipStream_t st);
 // bf16: the h slots of lstm_fwd's step records [tiles][2][L][2][U/4][64] -> natural rows
 // [16 * tiles][L][2U], with the dropout keep bits [tiles][2][L][64] applied when dmask is non-null

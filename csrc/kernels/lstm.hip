@@ -162,6 +162,9 @@ INA_DEVICE void wave_lds_sync() {
 //   xg[tile][t][lane = 16 q + n][xi] = bf16 x feature 4 xi + q of sequence 16 tile + n at step t
 //                                      (0 past DIN and for padding sequences >= S)
 //   posb[tile][t][n] = pos1 | pos2 << 8 (position ids of the pos-table gradient kernels)
+//   dmask[tile][dir][t][lane] = DropoutWrapper keep bits (bit m: unit 4m + q), when dropout is on --
+//                                the counter hash of lstm_fwd's fp32 path, off the recurrence's
+//                                critical path (it was ~1/3 of the bf16 forward's VALU per step)
 // x enters the gate MFMAs as bf16 in this mode, so the values are exactly the ones the per-step
 // gather produced.
 // ------------------------------------------------------------------------------------------
@@ -175,7 +178,9 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
                                                       const float* __restrict__ p1emb,
                                                       const float* __restrict__ p2emb, int PD,
                                                       unsigned short* __restrict__ xg,
-                                                      unsigned short* __restrict__ posb) {
+                                                      unsigned short* __restrict__ posb,
+                                                      unsigned char* __restrict__ dmask, int U, uint32_t seed,
+                                                      const int* __restrict__ seed_dev, uint32_t thr) {
   // the two position tables ([2L, PD] each, tiny) in LDS: per-feature loads from them were most of
   // this kernel's vector-memory instructions
   __shared__ float ptab[2 * 128 * 8];
@@ -218,6 +223,27 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
           u16x4_t{v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
   }
   posb[(size_t)(tile * L + t) * 16 + n] = (unsigned short)(p1 | (p2 << 8));
+  if (dmask) {   // uniform
+    const uint32_t sd = seed_dev ? (uint32_t)seed_dev[0] : seed;
+    const uint32_t thr16 = thr >> 16;
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const uint32_t salt = dropout_salt(sd, (uint32_t)d);
+      const uint32_t pbase = (((uint32_t)seq * L + t) * U) >> 1;   // U even: the row's first unit pair
+      uint32_t by[4] = {0u, 0u, 0u, 0u};                            // keep byte of lane group q
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {                                // units 2k, 2k + 1 (lstm_keep)
+        if (2 * k >= U) break;
+        const uint32_t x = dropout_mix(salt, pbase + k);
+        const int u0 = 2 * k, u1 = 2 * k + 1;
+        by[u0 & 3] |= ((x & 0xFFFFu) < thr16 ? 1u : 0u) << (u0 >> 2);
+        by[u1 & 3] |= ((x >> 16) < thr16 ? 1u : 0u) << (u1 >> 2);
+      }
+      unsigned char* mrow = dmask + (size_t)((tile * 2 + d) * L + t) * 64 + n;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) mrow[16 * q] = (unsigned char)by[q];
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -350,7 +376,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
         const uint32_t base = ((uint32_t)seq * L + t) * U + q;
         uint32_t bits = 0;
 #pragma unroll
-        for (int m = 0; m < U4; ++m) bits |= dropout_keep_salted(salt, base + 4 * m, thr) ? (1u << m) : 0u;
+        for (int m = 0; m < U4; ++m) bits |= lstm_keep(salt, base + 4 * m, thr) ? (1u << m) : 0u;
         dmask[(uint32_t)((tile * 2 + dir) * L + t) * 64 + lane] = (unsigned char)bits;
       }
     } else {
@@ -361,7 +387,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
         uint32_t bits = 0;
 #pragma unroll
         for (int m = 0; m < U4; ++m) {
-          const bool keep = dropout_keep_salted(salt, base + 4 * m, thr);
+          const bool keep = lstm_keep(salt, base + 4 * m, thr);
           bits |= keep ? (1u << m) : 0u;
           hn[4 * m] = to_elem(keep ? h[m] * inv_kp : 0.f, (typename FragT<BF16>::elem*)nullptr);
         }
@@ -1150,8 +1176,10 @@ static int launch_fwd_t(const LstmArgs& a, hipStream_t st) {
   dim3 grid((ntiles + 3) / 4, 2);
   size_t lds = BF16 ? 0 : (size_t)4 * 16 * a.L * sizeof(int2);   // fp32: token ids
   const bool store = a.hraw != nullptr && a.cst != nullptr;
-  auto kern = a.drop ? (store ? lstm_fwd_kernel<U, NX, BF16, true, true> : lstm_fwd_kernel<U, NX, BF16, true, false>)
-                     : (store ? lstm_fwd_kernel<U, NX, BF16, false, true> : lstm_fwd_kernel<U, NX, BF16, false, false>);
+  // bf16: the keep bits come from x_gather_kernel (x_gather must run first); fp32 hashes them here
+  const bool drop = a.drop && !BF16;
+  auto kern = drop ? (store ? lstm_fwd_kernel<U, NX, BF16, !BF16, true> : lstm_fwd_kernel<U, NX, BF16, !BF16, false>)
+                   : (store ? lstm_fwd_kernel<U, NX, BF16, false, true> : lstm_fwd_kernel<U, NX, BF16, false, false>);
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, a.bias, (elem*)a.hraw,
                      (typename CT<BF16>::type*)a.cst, (elem*)a.hdrop, a.dmask, a.seed, a.thr, a.inv_kp, a.drop, a.seed_dev,
@@ -1300,7 +1328,7 @@ int h_natural(const void* rec, const unsigned char* dmask, float inv_kp, int S, 
   return -1;
 }
 
-int x_gather(const LstmArgs& a, int NX, hipStream_t st) {
+int x_gather(const LstmArgs& a, int U, int NX, hipStream_t st) {
   const int ntiles = (a.S + 15) / 16;
   if (ntiles <= 0) return 0;
   auto* xg = (unsigned short*)a.xg;
@@ -1310,7 +1338,8 @@ int x_gather(const LstmArgs& a, int NX, hipStream_t st) {
   const auto* wr16 = (const unsigned short*)a.wrows;
 #define INA_XG_LAUNCH(NXV, DIR)                                                                          \
   hipLaunchKernelGGL((x_gather_kernel<NXV, DIR>), grid, dim3(256), 0, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, \
-                     a.wemb, wr16, a.E, a.p1emb, a.p2emb, a.PD, xg, posb)
+                     a.wemb, wr16, a.E, a.p1emb, a.p2emb, a.PD, xg, posb, a.drop ? a.dmask : nullptr, U, a.seed, \
+                     a.seed_dev, a.thr)
   if (NX == 4 && a.wrows)
     INA_XG_LAUNCH(4, true);
   else if (NX == 4)

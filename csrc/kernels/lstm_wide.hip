@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void lstm_wide_fwd_step_kernel(
     float ho = hv;
     if (drop) {
       const uint32_t idx = ((uint32_t)s * L + t) * U + u;   // same index as the fused kernel / oracle
-      ho = dropout_keep_salted(dir ? salt1 : salt0, idx, thr) ? hv * inv_kp : 0.f;
+      ho = lstm_keep(dir ? salt1 : salt0, idx, thr) ? hv * inv_kp : 0.f;
     }
     hout[((size_t)s * L + t) * 2 * U + dir * U + u] = f2bf(ho);
   }
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void lstm_wide_bwd_step_kernel(
     float dout = bf2f(dH[((size_t)s * L + t) * 2 * U + dir * U + u]);
     if (drop) {
       const uint32_t idx = ((uint32_t)s * L + t) * U + u;
-      dout = dropout_keep_salted(dir ? salt1 : salt0, idx, thr) ? dout * inv_kp : 0.f;
+      dout = lstm_keep(dir ? salt1 : salt0, idx, thr) ? dout * inv_kp : 0.f;
     }
     const size_t so = (((size_t)dir * S + s) * L + t) * U + u;
     const size_t go = (((size_t)dir * S + s) * L + t) * 4 * U;

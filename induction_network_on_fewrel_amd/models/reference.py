@@ -51,16 +51,18 @@ def hash_u32(x: torch.Tensor) -> torch.Tensor:
 def dropout_keep_mask(seed: int, direction: int, S: int, L: int, u: int, keep_prob: float,
                       device=None) -> torch.Tensor:
     """Bernoulli(keep_prob) mask [S, L, u] for one LSTM direction's outputs (float 0/1).
-    Same integer recipe as ``dropout_keep_salted`` in csrc/include/ina_common.h (products are
-    reduced mod 2^32 after every multiply; all factors < 2^32 so int64 never overflows)."""
-    idx = torch.arange(S * L * u, dtype=torch.int64, device=device)
+    Same integer recipe as ``lstm_keep`` in csrc/include/ina_common.h: one 32-bit hash per pair of
+    adjacent units (element e uses 16-bit half e & 1 of mix(e >> 1)), kept iff the half is below
+    thr >> 16 (products are reduced mod 2^32 after every multiply; int64 never overflows)."""
+    e = torch.arange(S * L * u, dtype=torch.int64, device=device)
     salt = ((seed & 0x7FFFFFFF) * 0x2545F491 + direction * 0x3C6EF372 + 0x1234567) & _M32
-    x = (idx * 0x6C8E9CF5 + salt) & _M32
+    x = ((e >> 1) * 0x6C8E9CF5 + salt) & _M32
     x = x ^ (x >> 16)
     x = (x * 0x7FEB352D) & _M32
     x = x ^ (x >> 15)
-    thr = min(int(keep_prob * 4294967296.0), 0xFFFFFFFF)
-    return (x < thr).to(torch.float32).view(S, L, u)
+    thr16 = min(int(keep_prob * 4294967296.0), 0xFFFFFFFF) >> 16
+    half = torch.where((e & 1) == 1, x >> 16, x & 0xFFFF)
+    return (half < thr16).to(torch.float32).view(S, L, u)
 
 
 # ------------------------------------------------------------------ encoder

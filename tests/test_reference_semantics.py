@@ -147,6 +147,9 @@ def test_dropout_mask_rate_and_determinism():
     m3 = ref.dropout_keep_mask(7, 1, 64, 37, 20, 0.9)
     assert torch.equal(m1, m2) and not torch.equal(m1, m3)
     assert abs(float(m1.mean()) - 0.9) < 0.01
+    # the two units of a hash pair (16-bit halves of one mix) are independent draws
+    both = float((m1[..., 0::2] * m1[..., 1::2]).mean())
+    assert abs(both - 0.81) < 0.01
 
 
 def test_full_forward_runtime_nkq():
