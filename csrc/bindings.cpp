@@ -323,8 +323,8 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   const bool shift = bf16 && pos_shift && (L + 1 + 15) / 16 <= 5;
   auto dpos_slab = shift ? at::empty({1, 1, 2, 2 * L, PD}, opt)
                          : (bf16 ? at::empty({pblocks, 1, 2, 2 * L, PD}, opt) : at::empty({blocks, 2, 2, 2 * L, PD}, opt));
-  // [2 dir][tiles][L][2PD][16] bf16 dx of the pos features
-  Tensor dxp = bf16 ? at::empty({2 * 2 * PD * ntiles * L * 16}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
+  // [2 dir][tiles][L][2PD + 1][16] bf16 dx of the pos features (+ a trash row for the other lanes)
+  Tensor dxp = bf16 ? at::empty({2 * (2 * PD + 1) * ntiles * L * 16}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
   if (bf16) {
     check(xg, "xg", at::kBFloat16);
     TORCH_CHECK(xg.numel() == ntiles * L * (64 * NX + 16), "ina.lstm_bwd: xg (from lstm_fwd) shape");

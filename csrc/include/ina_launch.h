@@ -32,7 +32,7 @@ struct LstmArgs {
   void* hdrop;
   unsigned char* dmask;  // [tiles][2][L][64] dropout keep bits (bit m = unit 4m+q), written by fwd, read by bwd
   const int* seed_dev;   // optional device-resident dropout seed (overrides seed; HIP-graph replay)
-  void* dxp;             // bf16 bwd: pos-feature gradients [2 dir][tiles][L][2PD][16] (reduced by pos_grad)
+  void* dxp;             // bf16 bwd: pos-feature gradients [2 dir][tiles][L][2PD + 1 (trash row)][16] (reduced by pos_grad)
   void* xg;              // bf16: x_gather output [tiles][L][64 lanes][NX] (input of lstm_fwd / lstm_bwd)
   const unsigned short* posb;   // bf16: x_gather position ids [tiles][L][16] = pos1 | pos2 << 8
   const void* wrows;     // optional bf16 [NI * L][8]: word rows per token, zero padded (x_gather DIRECT)

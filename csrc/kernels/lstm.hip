@@ -611,9 +611,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   XSrc xs[NX];
 #pragma unroll
   for (int xi = 0; xi < NX; ++xi) xs[xi] = make_xsrc(4 * xi + q, wemb, E, p1emb, p2emb, PD);
-  int pofs[NX];   // lane's element offset inside a dxp [NPF][16] step block (pos features only)
+  // lane's element offset inside a dxp [NPF + 1][16] step block: its pos feature's row, or the
+  // trash row NPF (word / padding features) -- the per-step stores then need no lane-dependent branch
+  int pofs[NX];
 #pragma unroll
-  for (int xi = 0; xi < NX; ++xi) pofs[xi] = (4 * xi + q - E) * 16 + n;
+  for (int xi = 0; xi < NX; ++xi)
+    pofs[xi] = ((uint32_t)(xs[xi].sel - 1) < 2u ? 4 * xi + q - E : NPF) * 16 + n;
 
   for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const int tile = g * 4 + wave;
@@ -786,10 +789,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       // float atomics here sat on the recurrence's critical path (~20% of this kernel).  fp32: LDS
       // atomics into the block's pos tables.
       if constexpr (BF16) {
-        unsigned short* drow = dxp + (((size_t)dir * ntiles + tile) * L + tof(tau)) * NPF * 16;
+        unsigned short* drow = dxp + (((size_t)dir * ntiles + tile) * L + tof(tau)) * (NPF + 1) * 16;
 #pragma unroll
-        for (int xi = 0; xi < NX; ++xi)
-          if ((uint32_t)(xs[xi].sel - 1) < 2u) drow[pofs[xi]] = f2bf(valid ? dslot[U4 + xi] : 0.f);
+        for (int xi = 0; xi < NX; ++xi) drow[pofs[xi]] = f2bf(valid ? dslot[U4 + xi] : 0.f);
         // (the reduction's position ids come from x_gather_kernel's posb)
       } else {
 #pragma unroll
@@ -955,7 +957,7 @@ __global__ __launch_bounds__(256) void pos_grad_kernel(const unsigned short* __r
   const int i16 = lane & 15, kg = lane >> 4;
   const int ntiles = (S + 15) / 16, npairs = (L + 1) / 2, NPF = 2 * PD, P2 = 2 * L;
   const long items = (long)ntiles * npairs;
-  const size_t dstride = (size_t)ntiles * L * NPF * 16;   // one direction of dxp
+  const size_t dstride = (size_t)ntiles * L * (NPF + 1) * 16;   // one direction of dxp (+ trash row)
   const int half = (kg & 1) * 8, sstep = kg >> 1;         // fragment k = 8 kg + e <-> (step, seq)
   const int col = i16 < NPF ? i16 : NPF - 1;
   f32x4_t acc[2][NPT];
@@ -972,7 +974,7 @@ __global__ __launch_bounds__(256) void pos_grad_kernel(const unsigned short* __r
     const int tile = (int)(itc / npairs), pr = (int)(itc - (long)tile * npairs);
     const int t = 2 * pr + sstep;
     const int tc = t < L ? t : L - 1;
-    const size_t o = (((size_t)tile * L + tc) * NPF + col) * 16 + half;
+    const size_t o = (((size_t)tile * L + tc) * (NPF + 1) + col) * 16 + half;
     b0 = *reinterpret_cast<const u16x8_t*>(dxp + o);
     b1 = *reinterpret_cast<const u16x8_t*>(dxp + dstride + o);
     pp = *reinterpret_cast<const u16x8_t*>(posb + ((size_t)tile * L + tc) * 16 + half);
@@ -1066,7 +1068,7 @@ __global__ __launch_bounds__(256) void pos_shift_gemm_kernel(const unsigned shor
   const bool cval = ci < ncol;
   const int t = cval ? ci / PD : 0;
   const int f = tb * PD + (cval ? ci - t * PD : 0);
-  const size_t dstride = (size_t)ntiles * L * NPF * 16;
+  const size_t dstride = (size_t)ntiles * L * (NPF + 1) * 16;   // dxp rows: NPF features + trash row
   const int half = (q & 1) * 8, sh = tb * 8;
   const int ksteps = (ntiles + 1) / 2;   // 32 sequences (2 tiles) per K-step
   const int k0 = blockIdx.y * kps, k1 = min(ksteps, k0 + kps);
@@ -1079,7 +1081,7 @@ __global__ __launch_bounds__(256) void pos_shift_gemm_kernel(const unsigned shor
     const int tile = 2 * ks + (q >> 1);
     ok = cval && tile < ntiles && ks < k1;
     const int tl = tile < ntiles ? tile : ntiles - 1;
-    const size_t o = (((size_t)tl * L + t) * NPF + f) * 16 + half;
+    const size_t o = (((size_t)tl * L + t) * (NPF + 1) + f) * 16 + half;
     b0 = *reinterpret_cast<const u16x8_t*>(dxp + o);
     b1 = *reinterpret_cast<const u16x8_t*>(dxp + dstride + o);
     pp = *reinterpret_cast<const u16x8_t*>(posb + (size_t)tl * L * 16 + half);   // ids at t = 0
