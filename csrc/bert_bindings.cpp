@@ -156,7 +156,8 @@ std::tuple<Tensor, Tensor, Tensor> bert_ln_res_bwd(const Tensor& dy, const Tenso
   blocks = std::max<int64_t>(1, std::min<int64_t>(blocks > 0 ? blocks : 1024, (T + 3) / 4));
   auto dres = at::empty_like(a_);
   auto da = at::empty_like(a_);
-  auto slab = at::zeros({blocks, 2, HD}, gamma.options());
+  // [blocks][d gamma | d beta | column sums of da]; every block writes its whole row
+  auto slab = T == 0 ? at::zeros({blocks, 3, HD}, gamma.options()) : at::empty({blocks, 3, HD}, gamma.options());
   if (T == 0) return {dres, da, slab};
   ina::BertLnArgs a{};
   a.a = a_.data_ptr();

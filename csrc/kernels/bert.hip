@@ -106,13 +106,15 @@ __global__ __launch_bounds__(256) void ln_res_bwd_kernel(
     unsigned short* __restrict__ da, float* __restrict__ slab, int T, uint32_t salt, uint32_t thr, float inv_kp,
     int drop) {
   constexpr int HD = 256 * NCH;
-  __shared__ float red[4][2][HD];
+  __shared__ float red[4][3][HD];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float dg[NCH][4], db[NCH][4];
+  // slab rows: d gamma, d beta, and the column sums of da (the bias gradient of the projection that
+  // produced a: one pass instead of a separate reduction over the [T, HD] activation gradient)
+  float dg[NCH][4], db[NCH][4], dd[NCH][4];
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) dg[c][r] = db[c][r] = 0.f;
+    for (int r = 0; r < 4; ++r) dg[c][r] = db[c][r] = dd[c][r] = 0.f;
   for (int row = blockIdx.x * 4 + wave; row < T; row += gridDim.x * 4) {
     const size_t base = (size_t)row * HD;
     const float mean = stats[2 * row], rstd = stats[2 * row + 1];
@@ -149,6 +151,7 @@ __global__ __launch_bounds__(256) void ln_res_bwd_kernel(
       for (int r = 0; r < 4; ++r) {
         dx[r] = rstd * (dyg[c][r] - m1 - xh[c][r] * m2);
         dav[r] = drop ? (keep[c][r] ? dx[r] * inv_kp : 0.f) : dx[r];
+        dd[c][r] += round_bf(dav[r]);   // the stored bf16 values
       }
       st4(dres + base + col, dx);
       st4(da + base + col, dav);
@@ -160,10 +163,11 @@ __global__ __launch_bounds__(256) void ln_res_bwd_kernel(
     for (int r = 0; r < 4; ++r) {
       red[wave][0][256 * c + 4 * lane + r] = dg[c][r];
       red[wave][1][256 * c + 4 * lane + r] = db[c][r];
+      red[wave][2][256 * c + 4 * lane + r] = dd[c][r];
     }
   __syncthreads();
-  float* out = slab + (size_t)blockIdx.x * 2 * HD;
-  for (int i = threadIdx.x; i < 2 * HD; i += 256) {
+  float* out = slab + (size_t)blockIdx.x * 3 * HD;
+  for (int i = threadIdx.x; i < 3 * HD; i += 256) {
     const int k = i / HD, col = i - k * HD;
     out[i] = red[0][k][col] + red[1][k][col] + red[2][k][col] + red[3][k][col];
   }

@@ -59,10 +59,12 @@ class _Linear(torch.autograd.Function):
     gradient buffer spans (trainer path) or returns them per parameter (plain autograd)."""
 
     @staticmethod
-    def forward(ctx, x, Wb, bb, gW, gb, nw, on_done, *params):
+    def forward(ctx, x, Wb, bb, gW, gb, nw, on_done, db_ext, *params):
+        """db_ext: the bias gradient is produced by the consumer's backward (_LnRes: column sums of
+        the same dy, fused into its kernel), so this backward skips the dy.sum(0) pass."""
         y = torch.addmm(bb, x, Wb.t()) if bb is not None else torch.mm(x, Wb.t())
         ctx.save_for_backward(x, Wb)
-        ctx.cfg = (gW, gb, nw, [tuple(p.shape) for p in params], bb is not None, on_done)
+        ctx.cfg = (gW, gb, nw, [tuple(p.shape) for p in params], bb is not None and not db_ext, on_done)
         return y
 
     @staticmethod
@@ -91,7 +93,7 @@ class _Linear(torch.autograd.Function):
                     o += shapes[i][0]
         if on_done is not None:   # last backward op of a layer: its gradient bucket is final
             on_done()
-        return (dx, None, None, None, None, None, None) + tuple(outs)
+        return (dx, None, None, None, None, None, None, None) + tuple(outs)
 
 
 class _Embed(torch.autograd.Function):
@@ -130,25 +132,26 @@ class _Embed(torch.autograd.Function):
 
 
 class _LnRes(torch.autograd.Function):
-    """y = LN(res + dropout(a))."""
+    """y = LN(res + dropout(a)); a = x W^T + ab (a _Linear with db_ext): ab's gradient is the column
+    sum of da, which the backward kernel accumulates in the same pass (slab row 2)."""
 
     @staticmethod
-    def forward(ctx, a, res, gamma, beta, seed, stream, p, meta, gname, bname):
+    def forward(ctx, a, res, gamma, beta, seed, stream, p, meta, gname, bname, ab, abname):
         y, stats = ops().bert_ln_res_fwd(a.contiguous(), res.contiguous(), gamma.detach(), beta.detach(), seed,
                                          stream, p)
         ctx.save_for_backward(a, res, gamma, stats)
-        ctx.cfg = (seed, stream, p, meta, gname, bname)
+        ctx.cfg = (seed, stream, p, meta, gname, bname, abname)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         a, res, gamma, stats = ctx.saved_tensors
-        seed, stream, p, meta, gname, bname = ctx.cfg
+        seed, stream, p, meta, gname, bname, abname = ctx.cfg
         dres, da, slab = ops().bert_ln_res_bwd(dy.contiguous(), a.contiguous(), res.contiguous(), gamma.detach(),
                                                stats, seed, stream, p, 0)
         sl = slab.sum(0)
         return (da, dres, _route_grad(meta, gname, sl[0]), _route_grad(meta, bname, sl[1]), None, None, None, None,
-                None, None)
+                None, None, _route_grad(meta, abname, sl[2]), None)
 
 
 class _BiasGelu(torch.autograd.Function):
@@ -236,10 +239,10 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
         cnt = sum(offs[m][1] for m in ns)
         return torch.as_strided(g0, (cnt,), (1,), g0.storage_offset())
 
-    def linear(x, wn, bn, out_dim, in_dim, on_done=None):
+    def linear(x, wn, bn, out_dim, in_dim, on_done=None, db_ext=False):
         Wb = wspan(wn, (out_dim, in_dim))
         bb = wspan(bn, (out_dim,)) if bn else None
-        return _Linear.apply(x, Wb, bb, gspan(wn), gspan(bn) if bn else None, len(wn), on_done,
+        return _Linear.apply(x, Wb, bb, gspan(wn), gspan(bn) if bn else None, len(wn), on_done, db_ext,
                              *[P(n) for n in wn], *[P(n) for n in (bn or [])])
 
     # DP overlap: the QKV projection's backward is the last backward op of layer i -> bucket i is final
@@ -261,15 +264,17 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
         bn = [a + f"self.{k}.bias" for k in ("query", "key", "value")]
         qkv = linear(x, qn, bn, 3 * Hd, Hd, layer_ready(i))
         ctx = _Mha.apply(qkv, inst, mask, L, nh, seed, 17 + 3 * i, pa)
-        o = linear(ctx, [a + "output.dense.weight"], [a + "output.dense.bias"], Hd, Hd)
+        o = linear(ctx, [a + "output.dense.weight"], [a + "output.dense.bias"], Hd, Hd, db_ext=True)
         x = _LnRes.apply(o, x, P(a + "output.LayerNorm.weight"), P(a + "output.LayerNorm.bias"), seed, 18 + 3 * i, pd,
-                         meta, by_name[a + "output.LayerNorm.weight"], by_name[a + "output.LayerNorm.bias"])
+                         meta, by_name[a + "output.LayerNorm.weight"], by_name[a + "output.LayerNorm.bias"],
+                         P(a + "output.dense.bias"), by_name[a + "output.dense.bias"])
         I = cfg.bert_intermediate
         hpre = linear(x, [pre + "intermediate.dense.weight"], None, I, Hd)
         h = _BiasGelu.apply(hpre, P(pre + "intermediate.dense.bias"), meta, by_name[pre + "intermediate.dense.bias"])
-        o = linear(h, [pre + "output.dense.weight"], [pre + "output.dense.bias"], Hd, I)
+        o = linear(h, [pre + "output.dense.weight"], [pre + "output.dense.bias"], Hd, I, db_ext=True)
         x = _LnRes.apply(o, x, P(pre + "output.LayerNorm.weight"), P(pre + "output.LayerNorm.bias"), seed, 19 + 3 * i,
-                         pd, meta, by_name[pre + "output.LayerNorm.weight"], by_name[pre + "output.LayerNorm.bias"])
+                         pd, meta, by_name[pre + "output.LayerNorm.weight"], by_name[pre + "output.LayerNorm.bias"],
+                         P(pre + "output.dense.bias"), by_name[pre + "output.dense.bias"])
     # ---- pooling + projection (fp32)
     xs = x.view(S, L, Hd)
     ar = torch.arange(S, device=x.device)

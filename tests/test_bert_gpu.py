@@ -46,6 +46,8 @@ def test_ln_res(HD, p):
     sl = slab.sum(0)
     _close(sl[0], gf.grad, rtol=1e-2)
     _close(sl[1], bf.grad, rtol=1e-2)
+    # row 2: column sums of the stored da (the producing projection's bias gradient)
+    torch.testing.assert_close(sl[2], da.float().sum(0), rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.parametrize("p", [0.0, 0.1])
