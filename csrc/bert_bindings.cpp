@@ -244,8 +244,11 @@ std::tuple<Tensor, Tensor> bert_mha_fwd(const Tensor& qkv, const Tensor& inst, c
   return {ctx, lse};
 }
 
-Tensor bert_mha_bwd(const Tensor& qkv, const Tensor& ctx, const Tensor& dctx, const Tensor& lse, const Tensor& inst,
-                    const Tensor& mask, int64_t L, int64_t nh, int64_t seed, int64_t stream_id, double p) {
+// -> (dqkv [S*L, 3*nh*64] bf16, bsum [S*nh, 3, 64] fp32 per-(sequence, head) column sums of dQ | dK | dV:
+//     the QKV bias gradient is bsum.view(S, nh, 3, 64).sum(0).transpose(0, 1))
+std::tuple<Tensor, Tensor> bert_mha_bwd(const Tensor& qkv, const Tensor& ctx, const Tensor& dctx, const Tensor& lse,
+                                        const Tensor& inst, const Tensor& mask, int64_t L, int64_t nh, int64_t seed,
+                                        int64_t stream_id, double p) {
   mha_checks(qkv, inst, mask, L, nh);
   chk(ctx, "ctx", at::kBFloat16);
   chk(dctx, "dctx", at::kBFloat16);
@@ -254,7 +257,8 @@ Tensor bert_mha_bwd(const Tensor& qkv, const Tensor& ctx, const Tensor& dctx, co
   TORCH_CHECK(ctx.size(0) == S * L && ctx.size(1) == 64 * nh && dctx.sizes() == ctx.sizes(), "ina.bert_mha_bwd: ctx");
   TORCH_CHECK(lse.numel() == S * nh * ina::mha_lp((int)L), "ina.bert_mha_bwd: lse");
   auto dqkv = at::empty_like(qkv);
-  if (S == 0) return dqkv;
+  auto bsum = (S == 0 ? at::zeros({S * nh, 3, 64}, lse.options()) : at::empty({S * nh, 3, 64}, lse.options()));
+  if (S == 0) return {dqkv, bsum};
   ina::BertMhaArgs a{};
   a.qkv = qkv.data_ptr();
   a.inst = inst.data_ptr<int>();
@@ -266,12 +270,13 @@ Tensor bert_mha_bwd(const Tensor& qkv, const Tensor& ctx, const Tensor& dctx, co
   a.lse = lse.data_ptr<float>();
   a.dctx = dctx.data_ptr();
   a.dqkv = dqkv.data_ptr();
+  a.bsum = bsum.data_ptr<float>();
   a.salt = salt_of(seed, stream_id);
   a.thr = thr_of(1.0 - p);
   a.inv_kp = (float)(1.0 / (1.0 - p));
   a.drop = p > 0.0 ? 1 : 0;
   launched(ina::mha_bwd(a, stream()), "mha_bwd");
-  return dqkv;
+  return {dqkv, bsum};
 }
 
 }  // namespace

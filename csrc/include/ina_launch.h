@@ -227,6 +227,7 @@ struct BertMhaArgs {         // fused attention, head dim 64, L <= 128
   float* lse;                // [S, nh, LP]
   const void* dctx;
   void* dqkv;
+  float* bsum;               // bwd, optional: [S*nh][3][64] per-block column sums of dQ | dK | dV
   uint32_t salt, thr;
   float inv_kp;
   int drop;

@@ -505,6 +505,8 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const unsigned short* __re
 }
 
 // dqkv: [T, 3*HDm] bf16 (dQ | dK | dV), fully written (rows of tokens < L).
+// bsum (optional): [S * nh][3][64] column sums of this block's stored dQ / dK / dV (the QKV bias
+// gradient before the sum over sequences; one small slab instead of a [T, 3*HDm] reduction).
 template <int LP>
 __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __restrict__ qkv,
                                                       const unsigned short* __restrict__ ctx,
@@ -512,7 +514,7 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
                                                       const float* __restrict__ lse, const int* __restrict__ inst,
                                                       const int* __restrict__ mask_all, int S, int L, int nh,
                                                       unsigned short* __restrict__ dqkv, uint32_t salt, uint32_t thr,
-                                                      float inv_kp, int drop) {
+                                                      float inv_kp, int drop, float* __restrict__ bsum) {
   constexpr int NT = LP / 16;
   constexpr int TSTR = LP + 8;       // row stride of the [d][q] / [d][key] transposed images
   constexpr int SSTR = LP + 8;       // row stride of dS [q][key]
@@ -522,6 +524,7 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
   __shared__ float delta[LP];
   __shared__ float madd[LP];
   __shared__ float lsel[LP];
+  __shared__ float wsum[4][3][HDIM];   // per-wave column sums (dQ | dK | dV), summed in fixed order
   unsigned short* Qt = TA;
   unsigned short* dOt = TA + HDIM * TSTR;
   unsigned short* Kt = TA;
@@ -575,7 +578,17 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
     madd[k] = (k < L && mrow[k < L ? k : 0] > 0) ? 0.f : -INFINITY;
     lsel[k] = lrow[k];
   }
+  for (int i = threadIdx.x; i < 4 * 3 * HDIM; i += 256) (&wsum[0][0][0])[i] = 0.f;
   __syncthreads();
+  // add the column sums (over the 16 lanes n) of one 16-row output tile into this wave's partials
+  // (the rounded bf16 values that are stored; lanes of rows >= L pass zeros)
+  auto colsum = [&](int part, int dt, const float (&v)[4], bool ok) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float t = group16_sum(ok ? round_bf(v[r]) : 0.f);
+      if (n == 0) wsum[wave][part][16 * dt + 4 * g + r] += t;
+    }
+  };
   const float c2 = 0.125f * LOG2E;
   const float scale = 0.125f;
   // phase 1: each wave owns key tiles kt = wave, wave + 4
@@ -667,15 +680,19 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
         }
     }
     // outputs: dK^T / dV^T tiles -> rows of dqkv (lane: key = 16kt + n, d = 16dt + 4g + r)
-    if (kok) {
-      unsigned short* dk = dqkv + (tok0 + key) * ROW + HDm + hh * HDIM;
-      unsigned short* dv = dk + HDm;
+    unsigned short* dk = dqkv + (tok0 + key) * ROW + HDm + hh * HDIM;
+    unsigned short* dv = dk + HDm;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        float a[4] = {dK[dt][0] * scale, dK[dt][1] * scale, dK[dt][2] * scale, dK[dt][3] * scale};
-        float b[4] = {dV[dt][0], dV[dt][1], dV[dt][2], dV[dt][3]};
+    for (int dt = 0; dt < 4; ++dt) {
+      float a[4] = {dK[dt][0] * scale, dK[dt][1] * scale, dK[dt][2] * scale, dK[dt][3] * scale};
+      float b[4] = {dV[dt][0], dV[dt][1], dV[dt][2], dV[dt][3]};
+      if (kok) {
         st4(dk + 16 * dt + 4 * g, a);
         st4(dv + 16 * dt + 4 * g, b);
+      }
+      if (bsum) {   // uniform
+        colsum(1, dt, a, kok);
+        colsum(2, dt, b, kok);
       }
     }
   }
@@ -711,13 +728,19 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma_bf16(ld8(&Kt[(16 * dt + n) * TSTR + 32 * k2 + 8 * g]), bs, acc[dt]);
     }
-    if (q < L) {
-      unsigned short* dq = dqkv + (tok0 + q) * ROW + hh * HDIM;
+    unsigned short* dq = dqkv + (tok0 + q) * ROW + hh * HDIM;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        float a[4] = {acc[dt][0] * scale, acc[dt][1] * scale, acc[dt][2] * scale, acc[dt][3] * scale};
-        st4(dq + 16 * dt + 4 * g, a);
-      }
+    for (int dt = 0; dt < 4; ++dt) {
+      float a[4] = {acc[dt][0] * scale, acc[dt][1] * scale, acc[dt][2] * scale, acc[dt][3] * scale};
+      if (q < L) st4(dq + 16 * dt + 4 * g, a);
+      if (bsum) colsum(0, dt, a, q < L);
+    }
+  }
+  if (bsum) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * HDIM; i += 256) {
+      const float* w = &wsum[0][0][0] + i;
+      bsum[(size_t)blockIdx.x * 3 * HDIM + i] = ((w[0] + w[3 * HDIM]) + w[6 * HDIM]) + w[9 * HDIM];
     }
   }
 }
@@ -837,7 +860,7 @@ int mha_bwd(const BertMhaArgs& a, hipStream_t st) {
 #define CALL(LP)                                                                                              \
   hipLaunchKernelGGL(mha_bwd_kernel<LP>, grid, dim3(256), 0, st, (const unsigned short*)a.qkv,               \
                      (const unsigned short*)a.ctx, (const unsigned short*)a.dctx, a.lse, a.inst, a.mask, a.S, \
-                     a.L, a.nh, (unsigned short*)a.dqkv, a.salt, a.thr, a.inv_kp, a.drop)
+                     a.L, a.nh, (unsigned short*)a.dqkv, a.salt, a.thr, a.inv_kp, a.drop, a.bsum)
   switch (mha_lp(a.L)) {
     case 32: CALL(32); break;
     case 64: CALL(64); break;

@@ -171,20 +171,25 @@ class _BiasGelu(torch.autograd.Function):
 
 
 class _Mha(torch.autograd.Function):
+    """ctx = MHA(qkv), qkv = x Wqkv^T + [bq | bk | bv] (a _Linear with db_ext): the QKV bias gradient is
+    the column sum of dqkv, accumulated by the backward kernel per (sequence, head) block."""
+
     @staticmethod
-    def forward(ctx, qkv, inst, mask, L, nh, seed, stream, p):
+    def forward(ctx, qkv, inst, mask, L, nh, seed, stream, p, meta, bnames, bq, bk, bv):
         qkv = qkv.contiguous()
         out, lse = ops().bert_mha_fwd(qkv, inst, mask, L, nh, seed, stream, p)
         ctx.save_for_backward(qkv, out, lse, inst, mask)
-        ctx.cfg = (L, nh, seed, stream, p)
+        ctx.cfg = (L, nh, seed, stream, p, meta, bnames)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         qkv, out, lse, inst, mask = ctx.saved_tensors
-        L, nh, seed, stream, p = ctx.cfg
-        dqkv = ops().bert_mha_bwd(qkv, out, dout.contiguous(), lse, inst, mask, L, nh, seed, stream, p)
-        return dqkv, None, None, None, None, None, None, None
+        L, nh, seed, stream, p, meta, bnames = ctx.cfg
+        dqkv, bsum = ops().bert_mha_bwd(qkv, out, dout.contiguous(), lse, inst, mask, L, nh, seed, stream, p)
+        db = bsum.view(inst.shape[0], nh, 3, 64).sum(0).transpose(0, 1).reshape(3, nh * 64)
+        return (dqkv, None, None, None, None, None, None, None, None, None) + tuple(
+            _route_grad(meta, bnames[i], db[i]) for i in range(3))
 
 
 def layer_spans(model, flat_names, offsets, numels):
@@ -262,8 +267,9 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
         a = pre + "attention."
         qn = [a + f"self.{k}.weight" for k in ("query", "key", "value")]
         bn = [a + f"self.{k}.bias" for k in ("query", "key", "value")]
-        qkv = linear(x, qn, bn, 3 * Hd, Hd, layer_ready(i))
-        ctx = _Mha.apply(qkv, inst, mask, L, nh, seed, 17 + 3 * i, pa)
+        qkv = linear(x, qn, bn, 3 * Hd, Hd, layer_ready(i), db_ext=True)
+        ctx = _Mha.apply(qkv, inst, mask, L, nh, seed, 17 + 3 * i, pa, meta, [by_name[n] for n in bn],
+                         *[P(n) for n in bn])
         o = linear(ctx, [a + "output.dense.weight"], [a + "output.dense.bias"], Hd, Hd, db_ext=True)
         x = _LnRes.apply(o, x, P(a + "output.LayerNorm.weight"), P(a + "output.LayerNorm.bias"), seed, 18 + 3 * i, pd,
                          meta, by_name[a + "output.LayerNorm.weight"], by_name[a + "output.LayerNorm.bias"],

@@ -112,9 +112,12 @@ def test_mha(L, p):
     _close(ctx, ref)
     dctx = torch.randn(S * L, Hd, device=dev).bfloat16()
     ref.backward(dctx.float())
-    dqkv = _ops().bert_mha_bwd(qkv, ctx, dctx, lse, inst, mask_all, L, nh, seed, stream, p)
+    dqkv, bsum = _ops().bert_mha_bwd(qkv, ctx, dctx, lse, inst, mask_all, L, nh, seed, stream, p)
     for part in range(3):
         _close(dqkv.view(S * L, 3, Hd)[:, part], qf.grad.view(S * L, 3, Hd)[:, part])
+    # fused QKV bias gradient: column sums of the stored dqkv
+    db = bsum.view(S, nh, 3, 64).sum(0).transpose(0, 1).reshape(-1)
+    torch.testing.assert_close(db, dqkv.float().sum(0), rtol=1e-4, atol=1e-3)
 
 
 def test_bert_encoder_end_to_end():
