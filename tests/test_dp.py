@@ -1,4 +1,4 @@
-"""Episode data parallelism, multi-process on CPU with the gloo backend (world_size 2).
+"""Episode data parallelism, multi-process on CPU with the gloo backend (world_size 2 and 4).
 
 Checks: the all-reduced gradient equals the average of the per-rank gradients,
 parameters stay bitwise identical across ranks after optimizer steps, and rank samplers differ.
@@ -97,12 +97,13 @@ def test_dp_resume_keeps_per_rank_samplers(tmp_path):
 
 
 @pytest.mark.slow
-def test_dp_gloo_world2(tmp_path):
-    world = 2
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_gloo_world(tmp_path, world):
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     r = [torch.load(tmp_path / f"r{i}.pt", weights_only=True) for i in range(world)]
     assert all(x["ok_sum"] for x in r)
     assert all(x["in_sync"] for x in r)
     assert all(x["ok_overlap"] for x in r)
-    assert not torch.equal(r[0]["idx"], r[1]["idx"])   # rank-folded sampling
+    for i in range(1, world):
+        assert not torch.equal(r[0]["idx"], r[i]["idx"])   # rank-folded sampling
