@@ -59,20 +59,24 @@ class _Linear(torch.autograd.Function):
     gradient buffer spans (trainer path) or returns them per parameter (plain autograd)."""
 
     @staticmethod
-    def forward(ctx, x, Wb, bb, gW, gb, nw, on_done, db_ext, *params):
-        """db_ext: the bias gradient is produced by the consumer's backward (_LnRes: column sums of
-        the same dy, fused into its kernel), so this backward skips the dy.sum(0) pass."""
+    def forward(ctx, x, Wb, bb, gW, gb, nw, on_done, db_ext, dx_acc, *params):
+        """db_ext: the bias gradient is produced by the consumer's backward (_LnRes / _Mha: column sums
+        of the same dy, fused into their kernels), so this backward skips the dy.sum(0) pass.
+        dx_acc: a _ResGrad holder; x's other gradient (the residual branch of the LayerNorm that also
+        reads x) is added by the dgrad GEMM itself (addmm, beta = 1) instead of autograd's bf16 add."""
         y = torch.addmm(bb, x, Wb.t()) if bb is not None else torch.mm(x, Wb.t())
         ctx.save_for_backward(x, Wb)
-        ctx.cfg = (gW, gb, nw, [tuple(p.shape) for p in params], bb is not None and not db_ext, on_done)
+        ctx.cfg = (gW, gb, nw, [tuple(p.shape) for p in params], bb is not None and not db_ext, on_done, dx_acc)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, Wb = ctx.saved_tensors
-        gW, gb, nw, shapes, has_b, on_done = ctx.cfg
+        gW, gb, nw, shapes, has_b, on_done, dx_acc = ctx.cfg
         dy = dy.contiguous()
-        dx = torch.mm(dy, Wb)
+        res = dx_acc.take() if dx_acc is not None else None
+        # in place into the LayerNorm's fresh residual gradient (out-of-place addmm copies C first)
+        dx = res.addmm_(dy, Wb) if res is not None else torch.mm(dy, Wb)
         dW = _wgrad(dy, x)
         db = dy.sum(0, dtype=torch.float32) if has_b else None
         outs = [None] * len(shapes)
@@ -93,7 +97,22 @@ class _Linear(torch.autograd.Function):
                     o += shapes[i][0]
         if on_done is not None:   # last backward op of a layer: its gradient bucket is final
             on_done()
-        return (dx, None, None, None, None, None, None, None) + tuple(outs)
+        return (dx, None, None, None, None, None, None, None, None) + tuple(outs)
+
+
+class _ResGrad:
+    """Hands a LayerNorm's residual-input gradient to the dgrad GEMM of the _Linear that reads the same
+    x (both consumers of x; the LayerNorm's backward always runs first)."""
+
+    def __init__(self):
+        self.g = None
+
+    def put(self, g):
+        self.g = g
+
+    def take(self):
+        g, self.g = self.g, None
+        return g
 
 
 class _Embed(torch.autograd.Function):
@@ -136,22 +155,27 @@ class _LnRes(torch.autograd.Function):
     sum of da, which the backward kernel accumulates in the same pass (slab row 2)."""
 
     @staticmethod
-    def forward(ctx, a, res, gamma, beta, seed, stream, p, meta, gname, bname, ab, abname):
+    def forward(ctx, a, res, gamma, beta, seed, stream, p, meta, gname, bname, ab, abname, res_sink):
+        """res_sink: a _ResGrad: the residual gradient goes to the dgrad GEMM of res's other consumer
+        (returned as None here) instead of being summed by autograd."""
         y, stats = ops().bert_ln_res_fwd(a.contiguous(), res.contiguous(), gamma.detach(), beta.detach(), seed,
                                          stream, p)
         ctx.save_for_backward(a, res, gamma, stats)
-        ctx.cfg = (seed, stream, p, meta, gname, bname, abname)
+        ctx.cfg = (seed, stream, p, meta, gname, bname, abname, res_sink)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         a, res, gamma, stats = ctx.saved_tensors
-        seed, stream, p, meta, gname, bname, abname = ctx.cfg
+        seed, stream, p, meta, gname, bname, abname, res_sink = ctx.cfg
         dres, da, slab = ops().bert_ln_res_bwd(dy.contiguous(), a.contiguous(), res.contiguous(), gamma.detach(),
                                                stats, seed, stream, p, 0)
         sl = slab.sum(0)
+        if res_sink is not None:
+            res_sink.put(dres)
+            dres = None
         return (da, dres, _route_grad(meta, gname, sl[0]), _route_grad(meta, bname, sl[1]), None, None, None, None,
-                None, None, _route_grad(meta, abname, sl[2]), None)
+                None, None, _route_grad(meta, abname, sl[2]), None, None)
 
 
 class _BiasGelu(torch.autograd.Function):
@@ -244,10 +268,10 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
         cnt = sum(offs[m][1] for m in ns)
         return torch.as_strided(g0, (cnt,), (1,), g0.storage_offset())
 
-    def linear(x, wn, bn, out_dim, in_dim, on_done=None, db_ext=False):
+    def linear(x, wn, bn, out_dim, in_dim, on_done=None, db_ext=False, dx_acc=None):
         Wb = wspan(wn, (out_dim, in_dim))
         bb = wspan(bn, (out_dim,)) if bn else None
-        return _Linear.apply(x, Wb, bb, gspan(wn), gspan(bn) if bn else None, len(wn), on_done, db_ext,
+        return _Linear.apply(x, Wb, bb, gspan(wn), gspan(bn) if bn else None, len(wn), on_done, db_ext, dx_acc,
                              *[P(n) for n in wn], *[P(n) for n in (bn or [])])
 
     # DP overlap: the QKV projection's backward is the last backward op of layer i -> bucket i is final
@@ -267,20 +291,21 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
         a = pre + "attention."
         qn = [a + f"self.{k}.weight" for k in ("query", "key", "value")]
         bn = [a + f"self.{k}.bias" for k in ("query", "key", "value")]
-        qkv = linear(x, qn, bn, 3 * Hd, Hd, layer_ready(i), db_ext=True)
+        r1, r2 = _ResGrad(), _ResGrad()   # x feeds qkv + LN1's residual; x1 feeds FFN1 + LN2's residual
+        qkv = linear(x, qn, bn, 3 * Hd, Hd, layer_ready(i), db_ext=True, dx_acc=r1)
         ctx = _Mha.apply(qkv, inst, mask, L, nh, seed, 17 + 3 * i, pa, meta, [by_name[n] for n in bn],
                          *[P(n) for n in bn])
         o = linear(ctx, [a + "output.dense.weight"], [a + "output.dense.bias"], Hd, Hd, db_ext=True)
         x = _LnRes.apply(o, x, P(a + "output.LayerNorm.weight"), P(a + "output.LayerNorm.bias"), seed, 18 + 3 * i, pd,
                          meta, by_name[a + "output.LayerNorm.weight"], by_name[a + "output.LayerNorm.bias"],
-                         P(a + "output.dense.bias"), by_name[a + "output.dense.bias"])
+                         P(a + "output.dense.bias"), by_name[a + "output.dense.bias"], r1)
         I = cfg.bert_intermediate
-        hpre = linear(x, [pre + "intermediate.dense.weight"], None, I, Hd)
+        hpre = linear(x, [pre + "intermediate.dense.weight"], None, I, Hd, dx_acc=r2)
         h = _BiasGelu.apply(hpre, P(pre + "intermediate.dense.bias"), meta, by_name[pre + "intermediate.dense.bias"])
         o = linear(h, [pre + "output.dense.weight"], [pre + "output.dense.bias"], Hd, I, db_ext=True)
         x = _LnRes.apply(o, x, P(pre + "output.LayerNorm.weight"), P(pre + "output.LayerNorm.bias"), seed, 19 + 3 * i,
                          pd, meta, by_name[pre + "output.LayerNorm.weight"], by_name[pre + "output.LayerNorm.bias"],
-                         P(pre + "output.dense.bias"), by_name[pre + "output.dense.bias"])
+                         P(pre + "output.dense.bias"), by_name[pre + "output.dense.bias"], r2)
     # ---- pooling + projection (fp32)
     xs = x.view(S, L, Hd)
     ar = torch.arange(S, device=x.device)
