@@ -78,7 +78,11 @@ class EncoderFn(torch.autograd.Function):
         else:
             apack, a2pack = pack_lstm(Kf, Kb, U, DIN, bf16)
             bias = torch.stack([bf.detach(), bb.detach()]).float().contiguous()
-        need_grad = ctx.needs_input_grad[5:15].count(True) > 0 if hasattr(ctx, "needs_input_grad") else True
+        # (ctx.needs_input_grad is True for trainable parameters even under torch.no_grad(): the caller
+        # passes the grad mode, so eval / serving runs the forward without the backward's stash)
+        need_grad = meta.get("need_grad")
+        if need_grad is None:
+            need_grad = ctx.needs_input_grad[5:15].count(True) > 0 if hasattr(ctx, "needs_input_grad") else True
         kp = float(meta["keep_prob"])
         lstm_args = (inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
                      p2emb.detach().contiguous(), apack, bias, U, sh["NX"])
@@ -160,7 +164,9 @@ def encode(inst, data, params, meta):
     """data = (word, pos1, pos2, mask) device int32 arrays [NI, L]; returns (e [S, 2u], alphas [S, L])."""
     word, pos1, pos2, mask = data
     # position ids known to be shifted aranges (ops/sampler.py::DeviceArrays): cheaper pos-table gradient
-    meta = dict(meta, pos_shift=bool(getattr(data, "pos_shift", False)))
+    meta = dict(meta, pos_shift=bool(getattr(data, "pos_shift", False)),
+                need_grad=torch.is_grad_enabled() and any(
+                    isinstance(t, torch.Tensor) and t.requires_grad for t in params.values()))
     return EncoderFn.apply(inst, word, pos1, pos2, mask, params["word_embedding"], params["pos1_embedding"],
                            params["pos2_embedding"], params["lstm_fw_kernel"], params["lstm_fw_bias"],
                            params["lstm_bw_kernel"], params["lstm_bw_bias"], params["attn_kernel"],
