@@ -419,6 +419,55 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   // after a load is not a safe completion bound, and an inline-asm load destination is invisible to
   // the register allocator (a spilled / copied in-flight destination corrupts state).  The loads
   // below are compiler-visible; the waitcnt pass inserts the waits.)
+  // bf16: the ping-pong buffers hold the RAW x_gather rows, converted inside the step: converting at
+  // the load made the compiler wait for it right there (s_waitcnt vmcnt(0), which also drained the
+  // previous step's record stores), i.e. no prefetch at all
+  if constexpr (!FG) {
+    u16x4_t ra[NX / 4], rb[NX / 4];
+    auto load_raw = [&](int t, u16x4_t* r) {
+      const unsigned short* xp = xg + ((uint32_t)(tile * L + t) * 64 + lane) * NX;
+#pragma unroll
+      for (int c = 0; c < NX / 4; ++c) r[c] = *reinterpret_cast<const u16x4_t*>(xp + 4 * c);
+    };
+    auto step_raw = [&](const int tau, const u16x4_t* r) __attribute__((always_inline)) {
+      // the empty asm pins the conversion here: pure shifts / ands were otherwise hoisted above the
+      // sched_barrier into the previous step, with a vmcnt(0) wait for this prefetch in front of them
+      u16x4_t rr[NX / 4];
+#pragma unroll
+      for (int c = 0; c < NX / 4; ++c) {
+        rr[c] = r[c];
+        asm volatile("" : "+v"(rr[c]));
+      }
+      float xv[NX];
+#pragma unroll
+      for (int c = 0; c < NX / 4; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[4 * c + e] = bf2f(rr[c][e]);
+      step(tau, xv);
+    };
+    // pair structure as below: sched_barrier pins each prefetch ahead of the step it overlaps, and the
+    // first pair is peeled so the loop header is entered with the same outstanding-VMEM state from
+    // the preheader and the latch (the waitcnt pass can then count precisely)
+    auto rpair = [&](int tau) __attribute__((always_inline)) {
+      load_raw(tof(tau + 1), rb);
+      __builtin_amdgcn_sched_barrier(0);
+      step_raw(tau, ra);
+      __builtin_amdgcn_sched_barrier(0);
+      load_raw(tof(min(tau + 2, L - 1)), ra);
+      __builtin_amdgcn_sched_barrier(0);
+      step_raw(tau + 1, rb);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    load_raw(tof(0), ra);
+    int tau = 0;
+    if (L >= 2) {
+      rpair(0);
+      tau = 2;
+    }
+    for (; tau + 1 < L; tau += 2) rpair(tau);
+    if (tau < L) step_raw(tau, ra);
+    return;
+  }
   float xa[NX], xb[NX];
 #if INA_FWD_PIPE == 0
   // simple loop: prefetch x_{tau+1}, copy at the end of the step
