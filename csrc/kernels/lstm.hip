@@ -568,7 +568,10 @@ template <int U, int NX>
 struct BwdWaves {
   static constexpr int value = (U <= 20 && NX == 4) ? 2 : 1;
 };
-template <int U, int NX, bool BF16>
+// WG: trained word table (word-row gradients by global atomics).  A template flag rather than a
+// runtime branch: the join after a skipped atomic block made LLVM drain every outstanding load
+// (s_waitcnt vmcnt(0), a register of that block is reused) on every step, prefetch included.
+template <int U, int NX, bool BF16, bool WG = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U, NX>::value))) void lstm_bwd_kernel(
     const int* __restrict__ inst, int S, const int* __restrict__ word, const int* __restrict__ pos1,
     const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
@@ -709,29 +712,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       wid_c = word[rowbase + t0]; p1_c = pos1[rowbase + t0]; p2_c = pos2[rowbase + t0];
       wid_n = word[rowbase + t1]; p1_n = pos1[rowbase + t1]; p2_n = pos2[rowbase + t1];
     }
-    float xv[NX], hp[U4], cprev[U4], ccur[U4], dhin[U4];
     const unsigned char* mbase = dmask + (size_t)(tile * 2 + dir) * L * 64 + lane;   // fwd keep bits
-    {
-      const int t = tof(L - 1), tp = tof(L >= 2 ? L - 2 : 0);
-      const uint32_t bits = drop ? (uint32_t)mbase[(size_t)t * 64] : 0xFFu;
-      if constexpr (BF16) {
-        load_xg(t, xv);
-      } else {
-#pragma unroll
-        for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(xs[xi], xrow(wid_c, p1_c, p2_c, E, PD));
-      }
-#pragma unroll
-      for (int m = 0; m < U4; ++m) {
-        float hdummy, cp, hv;
-        ld_hc(t, m, hdummy, ccur[m]);
-        ld_hc(tp, m, hv, cp);
-        cprev[m] = L >= 2 ? cp : 0.f;
-        hp[m] = (L >= 2 && valid) ? hv : 0.f;
-        const float dv = from_elem(dH[dh_base + (size_t)t * dh_ts + m * dh_ms]);
-        const bool keep = (bits >> m) & 1u;
-        dhin[m] = (valid && keep) ? dv * inv_kp : 0.f;
-      }
-    }
+    float ccur[U4];
     float dh_rec[U4], dc_rec[U4];
 #pragma unroll
     for (int m = 0; m < U4; ++m) dh_rec[m] = dc_rec[m] = 0.f;
@@ -749,37 +731,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
           for (int g4 = 0; g4 < 4; ++g4) dgT[(g4 * U + 4 * m + q) * RS + n + 16] = to_elem(0.f, (elem*)nullptr);
       }
     }
-    for (int tau = L - 1; tau >= 0; --tau) {
-      const int wid = wid_c, p1 = p1_c, p2 = p2_c;
-      // ---- prefetch step tau-1 (x, h_{tau-2}, c_{tau-2}, dH_{tau-1}) and ids of tau-2
-      const int taun = tau >= 1 ? tau - 1 : 0;
-      const int taunn = tau >= 2 ? tau - 2 : 0;
-      const bool n_has_prev = tau >= 2;
-      const int tn = tof(taun), tnp = tof(taunn), tnn = tof(taunn);
-      int wid_nn = 0, p1_nn = 0, p2_nn = 0;
-      if constexpr (!BF16) {
-        wid_nn = word[rowbase + tnn];
-        p1_nn = pos1[rowbase + tnn];
-        p2_nn = pos2[rowbase + tnn];
-      }
-      float xv_n[NX], hp_n[U4], cprev_n[U4], dhin_n[U4];
-      const uint32_t bits_n = drop ? (uint32_t)mbase[(size_t)tn * 64] : 0xFFu;
-      if constexpr (BF16) {
-        load_xg(tn, xv_n);
-      } else {
-#pragma unroll
-        for (int xi = 0; xi < NX; ++xi) xv_n[xi] = gather_x(xs[xi], xrow(wid_n, p1_n, p2_n, E, PD));
-      }
-#pragma unroll
-      for (int m = 0; m < U4; ++m) {
-        float hv, cp;
-        ld_hc(tnp, m, hv, cp);
-        cprev_n[m] = n_has_prev ? cp : 0.f;
-        hp_n[m] = (n_has_prev && valid) ? hv : 0.f;
-        const float dv = from_elem(dH[dh_base + (size_t)tn * dh_ts + m * dh_ms]);
-        const bool keep = (bits_n >> m) & 1u;
-        dhin_n[m] = (valid && keep) ? dv * inv_kp : 0.f;
-      }
+    // one BPTT step at processing index tau from its converted inputs (ccur, dh_rec, dc_rec, accw
+    // carried by reference); wid / p1 / p2: fp32 mode's token ids (unused in bf16 mode)
+    auto compute = [&](const int tau, const int wid, const int p1, const int p2, const float* xv, const float* hp,
+                       const float* cprev, const float* dhin) __attribute__((always_inline)) {
       // ---- recompute gates
       frag B[NKS];
 #pragma unroll
@@ -850,7 +805,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         }
       }
       // word table (global atomics, only when trained)
-      if (dwemb) {
+      if constexpr (WG) {
         if (valid) {
           const int wrow = BF16 ? word[rowbase + tof(tau)] : wid;   // bf16: not pipelined (trained words only)
 #pragma unroll
@@ -928,6 +883,61 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         wave_lds_sync();   // every later chunk rewrites both column halves: no clearing needed
       }
       }
+    };
+    if constexpr (!BF16) {
+    float xv[NX], hp[U4], cprev[U4], dhin[U4];
+    {
+      const int t = tof(L - 1), tp = tof(L >= 2 ? L - 2 : 0);
+      const uint32_t bits = drop ? (uint32_t)mbase[(size_t)t * 64] : 0xFFu;
+      if constexpr (BF16) {
+        load_xg(t, xv);
+      } else {
+#pragma unroll
+        for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(xs[xi], xrow(wid_c, p1_c, p2_c, E, PD));
+      }
+#pragma unroll
+      for (int m = 0; m < U4; ++m) {
+        float hdummy, cp, hv;
+        ld_hc(t, m, hdummy, ccur[m]);
+        ld_hc(tp, m, hv, cp);
+        cprev[m] = L >= 2 ? cp : 0.f;
+        hp[m] = (L >= 2 && valid) ? hv : 0.f;
+        const float dv = from_elem(dH[dh_base + (size_t)t * dh_ts + m * dh_ms]);
+        const bool keep = (bits >> m) & 1u;
+        dhin[m] = (valid && keep) ? dv * inv_kp : 0.f;
+      }
+    }
+    for (int tau = L - 1; tau >= 0; --tau) {
+      // ---- prefetch step tau-1 (x, h_{tau-2}, c_{tau-2}, dH_{tau-1}) and ids of tau-2
+      const int taun = tau >= 1 ? tau - 1 : 0;
+      const int taunn = tau >= 2 ? tau - 2 : 0;
+      const bool n_has_prev = tau >= 2;
+      const int tn = tof(taun), tnp = tof(taunn), tnn = tof(taunn);
+      int wid_nn = 0, p1_nn = 0, p2_nn = 0;
+      if constexpr (!BF16) {
+        wid_nn = word[rowbase + tnn];
+        p1_nn = pos1[rowbase + tnn];
+        p2_nn = pos2[rowbase + tnn];
+      }
+      float xv_n[NX], hp_n[U4], cprev_n[U4], dhin_n[U4];
+      const uint32_t bits_n = drop ? (uint32_t)mbase[(size_t)tn * 64] : 0xFFu;
+      if constexpr (BF16) {
+        load_xg(tn, xv_n);
+      } else {
+#pragma unroll
+        for (int xi = 0; xi < NX; ++xi) xv_n[xi] = gather_x(xs[xi], xrow(wid_n, p1_n, p2_n, E, PD));
+      }
+#pragma unroll
+      for (int m = 0; m < U4; ++m) {
+        float hv, cp;
+        ld_hc(tnp, m, hv, cp);
+        cprev_n[m] = n_has_prev ? cp : 0.f;
+        hp_n[m] = (n_has_prev && valid) ? hv : 0.f;
+        const float dv = from_elem(dH[dh_base + (size_t)tn * dh_ts + m * dh_ms]);
+        const bool keep = (bits_n >> m) & 1u;
+        dhin_n[m] = (valid && keep) ? dv * inv_kp : 0.f;
+      }
+      compute(tau, wid_c, p1_c, p2_c, xv, hp, cprev, dhin);
       // ---- rotate the pipeline
 #pragma unroll
       for (int m = 0; m < U4; ++m) {
@@ -940,6 +950,72 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       for (int xi = 0; xi < NX; ++xi) xv[xi] = xv_n[xi];
       wid_c = wid_n; p1_c = p1_n; p2_c = p2_n;
       wid_n = wid_nn; p1_n = p1_nn; p2_n = p2_nn;
+    }
+    } else {
+      // bf16: ping-pong RAW step buffers (2x unrolled).  The prefetch of step tau-1 lands in the other
+      // buffer and is converted only when that step runs; the empty asm on the raw registers pins the
+      // conversion there (pure conversions were otherwise hoisted into the previous step together
+      // with a wait for the prefetch, i.e. no overlap).
+      struct RawB {
+        unsigned short h[U4], c[U4], d[U4];   // h / c of processing step tau-1, dH of step tau
+        unsigned short kb;                     // keep bits of step tau (| kor in bstep, after the pin)
+        u16x4_t x[NX / 4];                     // x_gather row of step tau
+      };
+      const unsigned char* kbase = drop ? mbase : reinterpret_cast<const unsigned char*>(rbase);
+      const uint32_t kor = drop ? 0u : 0xFFu;
+      auto rload = [&](int tau, RawB& o) __attribute__((always_inline)) {
+        const int tn = tof(tau), tp = tof(tau >= 1 ? tau - 1 : 0);
+#pragma unroll
+        for (int m = 0; m < U4; ++m) {
+          o.h[m] = rbase[((size_t)tp * 2 * U4 + m) * 64];
+          o.c[m] = rbase[((size_t)tp * 2 * U4 + U4 + m) * 64];
+          o.d[m] = reinterpret_cast<const unsigned short*>(dH)[dh_base + (size_t)tn * dh_ts + m * dh_ms];
+        }
+        o.kb = kbase[(size_t)tn * 64];
+        const unsigned short* xp = xg + ((uint32_t)(tile * L + tn) * 64 + lane) * NX;
+#pragma unroll
+        for (int c = 0; c < NX / 4; ++c) o.x[c] = *reinterpret_cast<const u16x4_t*>(xp + 4 * c);
+      };
+      auto bstep = [&](int tau, const RawB& X0) __attribute__((always_inline)) {
+        RawB X = X0;
+#pragma unroll
+        for (int m = 0; m < U4; ++m) asm volatile("" : "+v"(X.h[m]), "+v"(X.c[m]), "+v"(X.d[m]));
+        asm volatile("" : "+v"(X.kb));
+#pragma unroll
+        for (int c = 0; c < NX / 4; ++c) asm volatile("" : "+v"(X.x[c]));
+        const bool hasp = tau >= 1;
+        float xv[NX], hp[U4], cprev[U4], dhin[U4];
+#pragma unroll
+        for (int c = 0; c < NX / 4; ++c)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) xv[4 * c + e] = bf2f(X.x[c][e]);
+#pragma unroll
+        for (int m = 0; m < U4; ++m) {
+          hp[m] = (hasp && valid) ? bf2f(X.h[m]) : 0.f;
+          cprev[m] = hasp ? (float)__builtin_bit_cast(_Float16, X.c[m]) : 0.f;
+          dhin[m] = (valid && ((((uint32_t)X.kb | kor) >> m) & 1u)) ? bf2f(X.d[m]) * inv_kp : 0.f;
+        }
+        compute(tau, 0, 0, 0, xv, hp, cprev, dhin);
+#pragma unroll
+        for (int m = 0; m < U4; ++m) ccur[m] = cprev[m];
+      };
+#pragma unroll
+      for (int m = 0; m < U4; ++m)   // c of the first processed step
+        ccur[m] = (float)__builtin_bit_cast(_Float16, rbase[((size_t)tof(L - 1) * 2 * U4 + U4 + m) * 64]);
+      RawB A, B;
+      rload(L - 1, A);
+      int tau = L - 1;
+      for (; tau >= 1; tau -= 2) {
+        rload(tau - 1, B);
+        __builtin_amdgcn_sched_barrier(0);
+        bstep(tau, A);
+        __builtin_amdgcn_sched_barrier(0);
+        rload(tau >= 2 ? tau - 2 : 0, A);
+        __builtin_amdgcn_sched_barrier(0);
+        bstep(tau - 1, B);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (tau == 0) bstep(0, A);
     }
   }
   // ---- reduce dW across the 4 waves through LDS (reuse the transpose region as f32)
@@ -1245,10 +1321,13 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   using elem = typename FragT<BF16>::elem;
   dim3 grid(a.bwd_blocks, 2);
   size_t lds = lstm_bwd_lds_bytes(U, NX, BF16, a.L, a.PD);
-  auto kfn = lstm_bwd_kernel<U, NX, BF16>;
+  auto kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true> : lstm_bwd_kernel<U, NX, BF16, false>;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)lstm_bwd_kernel<U, NX, BF16, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    hipFuncSetAttribute((const void*)lstm_bwd_kernel<U, NX, BF16, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
     attr_set = true;
   }
   hipLaunchKernelGGL(kfn, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
@@ -1285,10 +1364,10 @@ static int bwd_resident_t(int L, int PD) {
   int& c = cached[BF16][Lc][Pc];
   if (c > 0) return c;
   const size_t lds = lstm_bwd_lds_bytes(U, NX, BF16, L, PD);
-  (void)hipFuncSetAttribute((const void*)lstm_bwd_kernel<U, NX, BF16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)lstm_bwd_kernel<U, NX, BF16, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
   int per_cu = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_kernel<U, NX, BF16>, 256, lds) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lstm_bwd_kernel<U, NX, BF16, false>, 256, lds) != hipSuccess ||
       hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
