@@ -23,14 +23,20 @@ CSRC = os.path.join(ROOT, "csrc")
 # (load it with INA_KERNEL_LIB=<path>); the default build is the in-tree package library.
 _TAG = os.environ.get("INA_BUILD_TAG", "")
 _VFLAGS = os.environ.get("INA_VARIANT_FLAGS", "").split()
+# per-file variant flags: INA_VARIANT_FILE_FLAGS="rec_attn.hip:-fno-slp-vectorize;lstm.hip:-DX=1"
+_VFILE = {f: fl.split(",") for f, fl in (e.split(":", 1) for e in os.environ.get("INA_VARIANT_FILE_FLAGS", "").split(";")
+                                          if ":" in e)}
 OUT_DIR = os.path.join(ROOT, "build", "obj" + (f"_{_TAG}" if _TAG else ""))
 LIB = (os.path.join(ROOT, "variants", f"_ina_kernels_{_TAG}.so") if _TAG
        else os.path.join(ROOT, "induction_network_on_fewrel_amd", "_ina_kernels.so"))
 ARCH = os.environ.get("INA_OFFLOAD_ARCH", "gfx950")
 # Per-file code generation flags.  rec_attn.hip: MFMA results in VGPRs (gfx950's unified register
 # file allows it); the default AGPR form cost 12 v_accvgpr_read per token step of the attention
-# forward, whose tanh / softmax epilogue reads every accumulator back on the VALU.
-FILE_FLAGS = {"rec_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+# forward, whose tanh / softmax epilogue reads every accumulator back on the VALU.  No SLP
+# vectoriser there: its v_pk_fma_f32 broadcasts pair a scalar with whatever register sits next to it,
+# and the wait-count pass then treats a prefetch landing in that neighbour as a dependency (a
+# vmcnt(0) in the middle of the backward's step); 444 vs 464 us forward, 746 vs 756 us backward.
+FILE_FLAGS = {"rec_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"]}
 
 
 def _torch_paths():
@@ -70,7 +76,8 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
         objs.append(obj)
         if _newer(obj, [src, *headers, __file__]):
             tasks.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", *_VFLAGS,
-                          *FILE_FLAGS.get(os.path.basename(src), []), "-I" + os.path.join(CSRC, "include"), "-c", src,
+                          *FILE_FLAGS.get(os.path.basename(src), []),
+                          *_VFILE.get(os.path.basename(src), []), "-I" + os.path.join(CSRC, "include"), "-c", src,
                           "-o", obj])
     for bsrc in sorted(glob.glob(os.path.join(CSRC, "*.cpp"))):   # host-only torch bindings (g++)
         bobj = os.path.join(OUT_DIR, os.path.basename(bsrc) + ".o")

@@ -70,8 +70,9 @@ INA_DEVICE uint32_t cross_group_or(uint32_t v) {
 template <int U>
 struct RecStep {
   unsigned short h[RA<U>::NV];
-  uint32_t kb;
-  float al;   // backward: alpha of the step (prefetched with the records)
+  uint32_t k0, k1;   // raw keep bytes of the two directions
+  uint32_t kb;             // combined keep bits (set by rec_pin in the consuming step)
+  float al;                // backward: alpha of the step (prefetched with the records)
 };
 // k0 / k1 always point at readable memory (the records themselves without dropout) and kor = 0xFFFF
 // then sets every keep bit: no branch around the loads (an exec-masked load block here made the
@@ -85,7 +86,20 @@ INA_DEVICE void rec_load(const unsigned short* r0, const unsigned short* r1, con
     o.h[m] = r0[t * RSTEP + m * 64];
     o.h[U4 + m] = r1[t * RSTEP + m * 64];
   }
-  o.kb = ((uint32_t)k0[t * 64] | ((uint32_t)k1[t * 64] << 8)) | kor;
+  o.k0 = k0[t * 64];
+  o.k1 = k1[t * 64];
+}
+// first thing in the consuming step: pins the raw load results there and only then combines the keep
+// bytes.  Any arithmetic on a prefetched value (the keep-byte combine at the load, or a pure op the
+// scheduler hoists) forces vmcnt(0) right after the prefetch is issued, i.e. no overlap at all.
+template <int U, bool AL>
+INA_DEVICE void rec_pin(RecStep<U>& s, uint32_t kor) {
+#pragma unroll
+  for (int i = 0; i < RA<U>::NV; ++i) asm volatile("" : "+v"(s.h[i]));
+  asm volatile("" : "+v"(s.k0));
+  asm volatile("" : "+v"(s.k1));
+  if constexpr (AL) asm volatile("" : "+v"(s.al));
+  s.kb = ((uint32_t)s.k0 | ((uint32_t)s.k1 << 8)) | kor;
 }
 // token loop over ping-pong step buffers (2x unrolled): the prefetch of step t+1 goes into the other
 // buffer, so no register copy of in-flight load results (a cur = nxt rotation forces vmcnt(0) at
@@ -153,8 +167,8 @@ INA_DEVICE u16x8_t tr8(const unsigned short* img, int stride, int c0, int q, int
 
 // ------------------------------------------------------------------------------------------
 // forward: one wave per tile, 4 tiles per workgroup.  Outputs e [S][2u] and alphas [S][L] (fp32).
-// The raw scores are parked in alphas (lane q stores the steps t = q mod 4 and re-reads only its
-// own stores) and normalised once the running max / sum are final.
+// The raw scores are parked in LDS (lane q stores the steps t = q mod 4 and re-reads only its own
+// stores) and normalised into alphas once the running max / sum are final.
 // ------------------------------------------------------------------------------------------
 template <int U>
 __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
@@ -170,6 +184,10 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
   // on the record loads, so resident waves are what hides them)
   __shared__ u16x8_t lA[MT * NKR * 64];
   __shared__ float lbw[2 * MT * 16];   // [b1 | w2]
+  // raw scores [t][sequence] per wave (L <= 64): LDS, not alphas -- an exec-masked global store in
+  // the step loop made the compiler drain vmcnt (the prefetch) at the join after it
+  __shared__ float lsc[4][64 * 16];
+  float* sl = lsc[threadIdx.x >> 6];
   for (int i = threadIdx.x; i < MT * NKR * 64; i += 256) lA[i] = w1r[i];
   for (int i = threadIdx.x; i < MT * 16; i += 256) {
     lbw[i] = i < H2 ? b1[i] : 0.f;
@@ -212,7 +230,8 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
 #pragma unroll
   for (int i = 0; i < NV; ++i) ea[i] = 0.f;
   auto load = [&](int t, RecStep<U>& o) { rec_load<U>(r0, r1, k0, k1, kor, t, o); };
-  rec_steps<U, INA_RA_PF_FWD>(L, load, [&](int t, const RecStep<U>& cur) {
+  rec_steps<U, INA_RA_PF_FWD>(L, load, [&](int t, RecStep<U>& cur) {
+    rec_pin<U, false>(cur, kor);
     float v[NV];
     u32x4_t Bw[NKR];
 #pragma unroll
@@ -244,7 +263,7 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
 #pragma unroll
     for (int i = 0; i < NV; ++i) ea[i] = ea[i] * c + p * v[i];
     mx = mn;
-    if ((t & 3) == q && valid) arow[t] = sc;
+    if ((t & 3) == q) sl[t * 16 + n] = sc;
   });
   const float inv = 1.f / lsum;
   if (valid) {
@@ -253,7 +272,7 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int t = q + 4 * i;
-      if (t < L) arow[t] = __expf(arow[t] - mx) * inv;   // this lane's own stores
+      if (t < L) arow[t] = __expf(sl[t * 16 + n] - mx) * inv;   // this lane's own LDS stores
     }
   }
 }
@@ -334,7 +353,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3
       rec_load<U>(r0, r1, k0, k1, kor, t, o);
       o.al = arow[t];
     };
-    rec_steps<U, 1>(L, load, [&](int t, const RecStep<U>& cur) {
+    rec_steps<U, 1>(L, load, [&](int t, RecStep<U>& cur) {
+      rec_pin<U, true>(cur, kor);
       const float alv = valid ? cur.al : 0.f;
       float dev[DEPC];
       asm volatile("" ::: "memory");   // re-read de from LDS per step (no hoisting)
