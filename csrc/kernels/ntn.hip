@@ -358,6 +358,23 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt) dQT[m][qt] = Z4;
     }
+    // Per-lane store bases of the per-slice dP / dw outputs, chosen once per group: lanes outside
+    // the N x N / H ranges point into the trash tail the host allocates past each buffer, so the
+    // slice loop's stores are unconditional.  (Guarded stores split the loop into ~15 basic
+    // blocks -- exec-mask branches the scheduler cannot move MFMAs across -- and re-derived the
+    // 64-bit row offsets with v_mul_lo_u32 per slice.)
+    unsigned short* dpb[MTH];
+#pragma unroll
+    for (int mb = 0; mb < MTH; ++mb) {
+      const int b0 = 16 * mb + 4 * q;
+      dpb[mb] = dp_out + ((n < N && b0 < H) ? ((long)epc * N + n) * hH + b0 : (long)E * N * hH);
+    }
+    float* dwb[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 4 * q + r;
+      dwb[r] = dw_slab + ((!PAPER && c < N && n < N) ? ((long)epc * h * N + c) * N + n : (long)E * h * N * N);
+    }
     __syncthreads();
     ntn_stage<MTH, NSW, true>(ntn_lds, 0, mpack, m2pack, wtpack, 2);
     stage_wait();
@@ -439,10 +456,7 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
 #pragma unroll
             for (int kq = 0; kq < KQ; ++kq) dw = mfma_bf16(pack2(VT[2 * kq], VT[2 * kq + 1]), dzB[kq], dw);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int c = 4 * q + r;
-              if (c < N && n < N) dw_slab[(((long)ep * h + s) * N + c) * N + n] = dw[r];
-            }
+            for (int r = 0; r < 4; ++r) dwb[r][s * N * N] = dw[r];
           }
           // dP^T[b, c] = sum_q Q[q, b] dT[c, q]
           f32x4_t dPT[2 * NKB];
@@ -464,16 +478,10 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
               dCT[ma] = mfma_bf16(buf[(F1 + (sl * MTH + ma) * NKB + kb) * 64 + lane], dPf, dCT[ma]);
           }
           // dP -> bf16 [E*N][h*H] for the dM reduction GEMM
-          if (n < N) {
 #pragma unroll
-            for (int mb = 0; mb < MTH; ++mb) {
-              const int b0 = 16 * mb + 4 * q;
-              if (b0 < H) {
-                u16x4_t v = {f2bf(dPT[mb][0]), f2bf(dPT[mb][1]), f2bf(dPT[mb][2]), f2bf(dPT[mb][3])};
-                *reinterpret_cast<u16x4_t*>(dp_out + ((long)ep * N + n) * hH + (long)s * H + b0) = v;
-              }
-            }
-          }
+          for (int mb = 0; mb < MTH; ++mb)
+            *reinterpret_cast<u16x4_t*>(dpb[mb] + s * H) =
+                u16x4_t{f2bf(dPT[mb][0]), f2bf(dPT[mb][1]), f2bf(dPT[mb][2]), f2bf(dPT[mb][3])};
         }
         // dQ^T[b, q] += sum_{s in pair, c} P_s[c, b] dT_s[c, q]
 #pragma unroll
