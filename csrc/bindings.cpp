@@ -495,7 +495,7 @@ Tensor routing_bwd(const Tensor& e, const Tensor& Ws, const Tensor& dcls, Tensor
   TORCH_CHECK(de.sizes() == e.sizes(), "ina.routing_bwd: de shape");
   TORCH_CHECK(dcls.numel() == E * N * H, "ina.routing_bwd: dcls shape");
   TORCH_CHECK(ina::routing_lds_bytes((int)N, (int)K, (int)H, (int)R, true) <= 160 * 1024, "ina.routing_bwd: N*K too large");
-  if (blocks <= 0) blocks = 4096;   // work items = (episode, class) pairs; slab per block
+  if (blocks <= 0) blocks = ina::routing_bwd_default_blocks((int)N, (int)K, (int)H, (int)R);   // slab per block
   blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, std::max<int64_t>(E * N, 1)));
   auto slab = at::empty({blocks, H, H}, e.options());   // every block writes its whole slab
   if (E == 0) return slab.zero_();

@@ -92,6 +92,7 @@ int routing_fwd(const float* e, const float* Ws, int E, int N, int K, int Q, int
 int routing_bwd(const float* e, const float* Ws, int E, int N, int K, int Q, int R, int H, const float* dcls, float* de,
                 float* slab, int blocks, hipStream_t st);
 size_t routing_lds_bytes(int N, int K, int H, int R, bool bwd);
+int routing_bwd_default_blocks(int N, int K, int H, int R);
 
 struct NtnArgs {
   const float* cls;

@@ -358,6 +358,14 @@ def test_head_forward_backward(head, shape):
     er = e.detach().clone().requires_grad_(True)
     ev = er.view(B, N * K + N * Q, H)
     cls = ref.dynamic_routing(ev[:, : N * K].reshape(B, N, K, H), pr["W_s"], 3)
+    # the oracle's NTN takes the routing KERNEL's class vectors as values (gradient still through the
+    # oracle routing): fp32 routing differs in the last bits, and where a class-vector element sits on a
+    # bf16 rounding boundary the two roundings differ by one ulp -- through the NTN's ReLU edges that
+    # can move single gradient entries by more than the tolerance (routing is checked tightly on its own
+    # in test_routing_only_fp32)
+    from induction_network_on_fewrel_amd.ops import ops
+    cls_k = ops().routing_fwd(e.detach().contiguous(), p["W_s"].detach().contiguous(), B, N, K, Q, 3, 0)
+    cls = cls + (cls_k.view_as(cls) - cls).detach()
     probs_r = ref.relation_probs(cls, ev[:, N * K:], pr["M"], pr["ntn_w"], pr["ntn_b"], head, bf16=True)
     (probs_r * dp).sum().backward()
     ep = _relerr(probs.detach(), probs_r.detach())
@@ -370,27 +378,29 @@ def test_head_forward_backward(head, shape):
         assert err < 6e-2, k
 
 
-@pytest.mark.parametrize("N,K,H", [(5, 3, 40), (10, 5, 64)])
-def test_routing_only_fp32(N, K, H):
-    """routing is fp32 VALU end to end: must match the oracle tightly (10-way 5-shot at H=64 needs the
-    >64 KB LDS opt-in)."""
+@pytest.mark.parametrize("N,K,H,R", [(5, 3, 40, 3), (10, 5, 64, 3), (5, 1, 40, 3), (5, 10, 40, 3), (3, 2, 16, 2),
+                                     (5, 5, 40, 1), (5, 5, 40, 4), (4, 4, 40, 3)])
+def test_routing_only_fp32(N, K, H, R):
+    """routing is fp32 end to end: must match the oracle tightly.  Grouped kernels (4 items per wave)
+    for K in {1, 2, 3, 5, 10}, R <= 3; R = 4 and K = 4 take the per-item kernels (10-way 5-shot at
+    H=64 on those needs the >64 KB LDS opt-in)."""
     from induction_network_on_fewrel_amd.ops import ops
     Q, B = 2, 6
     torch.manual_seed(1)
     S = B * (N * K + N * Q)
     e = torch.randn(S, H, device=DEV)
     Ws = torch.randn(H, H, device=DEV) * 0.2
-    cls = ops().routing_fwd(e, Ws, B, N, K, Q, 3, 0)
+    cls = ops().routing_fwd(e, Ws, B, N, K, Q, R, 0)
     ev = e.view(B, N * K + N * Q, H)
-    cls_r = ref.dynamic_routing(ev[:, : N * K].reshape(B, N, K, H), Ws, 3)
+    cls_r = ref.dynamic_routing(ev[:, : N * K].reshape(B, N, K, H), Ws, R)
     assert _relerr(cls, cls_r) < 1e-5
     er = e.clone().requires_grad_(True)
     Wr = Ws.clone().requires_grad_(True)
-    cr = ref.dynamic_routing(er.view(B, N * K + N * Q, H)[:, : N * K].reshape(B, N, K, H), Wr, 3)
+    cr = ref.dynamic_routing(er.view(B, N * K + N * Q, H)[:, : N * K].reshape(B, N, K, H), Wr, R)
     dc = torch.randn_like(cr)
     (cr * dc).sum().backward()
     de = torch.zeros_like(e)
-    slab = ops().routing_bwd(e, Ws, dc.contiguous(), de, B, N, K, Q, 3, 0)
+    slab = ops().routing_bwd(e, Ws, dc.contiguous(), de, B, N, K, Q, R, 0)
     dWs = slab.sum(0)
     sup_rows = torch.cat([torch.arange(b * (N * K + N * Q), b * (N * K + N * Q) + N * K) for b in range(B)]).to(DEV)
     assert _relerr(de[sup_rows], er.grad[sup_rows]) < 1e-4
