@@ -42,7 +42,9 @@ class DistContext:
         else:
             dev = torch.device("cpu")
         ctx = cls(rank, world, local_rank, dev, None)
-        if world > 1:
+        # INA_FORCE_DIST=1: initialise the process group even at world size 1, so the collective path
+        # (RCCL all-reduce / broadcast / barrier) runs on a one-GPU box (tests/test_dp_gpu.py)
+        if world > 1 or os.environ.get("INA_FORCE_DIST") == "1":
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29500")
             os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
@@ -66,7 +68,8 @@ class DistContext:
     def barrier(self) -> None:
         if self.initialized:
             if self.backend == "nccl":
-                dist.barrier(device_ids=[self.device.index])
+                idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+                dist.barrier(device_ids=[idx])
             else:
                 dist.barrier()
 

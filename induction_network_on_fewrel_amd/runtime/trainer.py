@@ -64,8 +64,8 @@ class Trainer:
         cfg.validate()
         self.cfg = cfg
         self.dist = dist_ctx or DistContext.from_env(device if device != "auto" else cfg.device)
-        if device not in ("auto", None) and self.dist.world == 1:
-            self.dist.device = torch.device(device)
+        if device not in ("auto", None) and self.dist.world == 1 and torch.device(device).type != self.dist.device.type:
+            self.dist.device = torch.device(device)   # (keeps from_env's device index for a matching type)
         self.device = self.dist.device
         self.train_data = train_data
         self.val_data = val_data if val_data is not None else train_data
@@ -85,7 +85,7 @@ class Trainer:
         if self.device.type == "cuda" and cfg.encoder == "bilstm" and cfg.step_glue:
             from ..ops.glue import StepGlue
             self.glue = StepGlue(self.flat)
-        if self.dist.world > 1:
+        if self.dist.initialized:
             self.dist.broadcast_(self.flat.flat, 0)
         l2_names = [n for n, p in self.model.params.trainable().items()
                     if any(p is q for q in self.model.params.l2_vars())]
@@ -187,12 +187,12 @@ class Trainer:
         self.flat.zero_grad()
         gv = self.grad_views if self.device.type == "cuda" else None
         ov = None
-        if self.dist.world > 1 and cfg.encoder == "bert" and self.device.type == "cuda":
+        if self.dist.initialized and cfg.encoder == "bert" and self.device.type == "cuda":
             # per-layer buckets all-reduced under the rest of backward (~28 MB fp32 each at BERT-base)
             from ..ops.bert import layer_spans
             ov = self.dist.overlap(self.flat.grad, layer_spans(self.model, self.flat.names, self.flat.offsets,
                                                                self.flat.numels))
-        elif self.dist.world > 1 and self.glue is not None and self._head_span is not None:
+        elif self.dist.initialized and self.glue is not None and self._head_span is not None:
             # BiLSTM step: the relation head's gradients (W_s, M, w, b: ~94% of the parameters) are final
             # after the head backward -> their all-reduce runs under the attention + BiLSTM backward
             ov = self.dist.overlap(self.flat.grad, [self._head_span])
@@ -207,7 +207,7 @@ class Trainer:
         t2 = time.perf_counter()
         if ov is not None:
             ov.finish()
-        elif self.dist.world > 1:
+        elif self.dist.initialized:
             self.dist.allreduce_buckets_(self.flat.grad)
         e3 = self._sync()
         t3 = time.perf_counter()
@@ -393,7 +393,7 @@ class Trainer:
         self.best_acc = float(meta.get("best_acc", 0.0))
         self.opt.set_skipped(int(meta.get("skipped_steps", 0)))
         self._restore_sampler(meta)
-        if self.dist.world > 1:
+        if self.dist.initialized:
             self.dist.broadcast_(self.flat.flat, 0)
 
     def _restore_sampler(self, meta: dict) -> None:

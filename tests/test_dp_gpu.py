@@ -42,3 +42,21 @@ def test_bench_world2_one_gpu(graph):
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 128
     assert out["params_in_sync"] is True
     assert out["final_loss"] == out["final_loss"] and out["value"] > 0
+
+
+def test_bench_rccl_world1():
+    """The RCCL (backend "nccl") collective path itself on one card: world size 1 with the process
+    group forced on, so the timed step's bucketed all-reduce, the barriers with device ids, the MAX
+    timing reduction and the params_in_sync broadcast all go through RCCL."""
+    env = dict(os.environ, INA_FORCE_DIST="1", OMP_NUM_THREADS="2")
+    env.pop("INA_DIST_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--steps", "3", "--warmup", "2", "--episodes-per-gpu", "64"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 1 and out["params_in_sync"] is True
+    assert out["final_loss"] == out["final_loss"] and out["value"] > 0
