@@ -58,6 +58,9 @@ class InductionNetwork(nn.Module):
             from ..ops.head import head
             return head(e, p, dict(E=B, N=N, K=K, Q=Q, iters=cfg.routing_iters,
                                    paper=(cfg.relation_head == "paper"), grad_views=grad_views))
+        if e.is_cuda and cfg.dtype == "bf16":
+            from ..ops.wide import head_wide
+            return head_wide(e, p, B, N, K, Q, cfg.routing_iters, cfg.relation_head)
         return ref.head_forward(p, e.float(), B, N, K, Q, cfg.routing_iters, cfg.relation_head)
 
     def check_gpu_config(self, N: int, Q: int, L: int) -> None:

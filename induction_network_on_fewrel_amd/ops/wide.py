@@ -89,13 +89,123 @@ class WideBiLSTM(torch.autograd.Function):
         return dX.view(S, L, D), dKs[0], dbs[0], dKs[1], dbs[1], None, None, None
 
 
+class SmallTableGather(torch.autograd.Function):
+    """rows = table[idx] for a SMALL table (the [2L, 5] position tables).  Autograd's index backward
+    scatters 1.2 M token gradients into ~74 rows with a sort + segmented accumulate that measured
+    14.4 ms per table per step at the paper configuration (41% of the step, profiles/r2_paper1);
+    here the table gradient is the GEMM OneHot(idx)^T dRows in fp32, in token chunks (deterministic,
+    a few hundred microseconds)."""
+
+    SPLIT = 256   # split-K batches: a [P, T] x [T, 5] GEMM has ~5 output tiles (measured 0.5 ms per
+                  # 2^18-token chunk as one GEMM); as 256 independent K-slices + an ordered sum it fills the chip
+
+    @staticmethod
+    def forward(ctx, table, idx):
+        ctx.save_for_backward(idx)
+        ctx.rows = table.shape[0]
+        return table[idx]
+
+    @staticmethod
+    def backward(ctx, d):
+        (idx,) = ctx.saved_tensors
+        P = ctx.rows
+        fi = idx.reshape(-1)
+        fd = d.reshape(fi.shape[0], -1).float()
+        T, C = fd.shape
+        nb = SmallTableGather.SPLIT
+        Tp = (T + nb - 1) // nb * nb
+        if Tp != T:   # pad with tokens of zero gradient
+            fi = torch.cat([fi, fi.new_zeros(Tp - T)])
+            fd = torch.cat([fd, fd.new_zeros(Tp - T, C)])
+        oh = torch.nn.functional.one_hot(fi, P).to(torch.float32).view(nb, Tp // nb, P)
+        g = torch.bmm(oh.transpose(1, 2), fd.view(nb, Tp // nb, C)).sum(0)
+        return g.to(d.dtype), None
+
+
+class ProjBF16(torch.autograd.Function):
+    """Z = X W in fp32 from bf16 operands (X [T, n] bf16, W [n, m] fp32 master): the attention
+    projection of the wide path as a bf16 MFMA GEMM (the fp32 formulation of models/reference.py ran
+    it as an fp32 GEMM over all S*L tokens).  Backward: dX = dZ W^T (bf16), dW = X^T dZ (fp32)."""
+
+    @staticmethod
+    def forward(ctx, X, W):
+        Wb = W.detach().to(torch.bfloat16)
+        ctx.save_for_backward(X, Wb)
+        return torch.mm(X, Wb, out_dtype=torch.float32)
+
+    @staticmethod
+    def backward(ctx, dZ):
+        X, Wb = ctx.saved_tensors
+        dZb = dZ.contiguous().to(torch.bfloat16)
+        dX = torch.mm(dZb, Wb.t()) if ctx.needs_input_grad[0] else None
+        dW = _wgrad(X, dZb) if ctx.needs_input_grad[1] else None
+        return dX, dW
+
+
+def attention_wide(H, mask, W1, b1, w2):
+    """Self-attention pooling (reference model/layer_module.py:49-98) over bf16 BiLSTM outputs
+    H [S, L, 2u]: bf16 projection GEMM, tanh / score / masked softmax / pooling in fp32."""
+    from ..models import reference as ref
+    S, L, D = H.shape
+    proj = torch.tanh(ProjBF16.apply(H.reshape(S * L, D), W1).view(S, L, -1) + b1)
+    # the score as a broadcast product + row sum, not a [S*L, D] x [D, 1] GEMM: that GEMM's weight
+    # gradient (K = S*L = 1.2 M, one output column) ran on ~16 workgroups for 3.6 ms per step
+    score = (proj * w2[:, 0]).sum(-1, keepdim=True)                     # [S, L, 1]
+    adder = (1.0 - mask.to(score.dtype)).unsqueeze(-1) * ref.MASK_ADDER
+    alphas = torch.softmax(score + adder, dim=1)
+    e = torch.bmm(H.transpose(1, 2).float(), alphas).squeeze(-1)
+    return e, alphas
+
+
 def encode_wide(inst, data, p, U: int, keep_prob: float, seed: int):
     """Wide GPU encoder: embedding gather + WideBiLSTM + self-attention (GEMM formulation)."""
     from ..models import reference as ref
     word, pos1, pos2, mask = (t[inst.long()] for t in data)
-    X = torch.cat([p["word_embedding"][word.long()], p["pos1_embedding"][pos1.long()],
-                   p["pos2_embedding"][pos2.long()]], -1).float()
+    X = torch.cat([p["word_embedding"][word.long()], SmallTableGather.apply(p["pos1_embedding"], pos1.long()),
+                   SmallTableGather.apply(p["pos2_embedding"], pos2.long())], -1).float()
     H = WideBiLSTM.apply(X, p["lstm_fw_kernel"], p["lstm_fw_bias"], p["lstm_bw_kernel"], p["lstm_bw_bias"], U,
                          int(seed), float(keep_prob))
-    e, alphas = ref.self_attention(H.float(), mask > 0, p["attn_kernel"], p["attn_bias"], p["attn_w2"])
+    e, alphas = attention_wide(H, mask > 0, p["attn_kernel"], p["attn_bias"], p["attn_w2"])
     return e, alphas.squeeze(-1)
+
+
+class TallSkinnyMM(torch.autograd.Function):
+    """y = x w for tall x [T, n] and a skinny weight w [n, m] (m = N classes): the weight gradient
+    x^T dy has an [n, m] output that a single GEMM covers with a handful of workgroups over K = T;
+    it is computed as 64 K-slices (bmm) and an ordered sum instead (fp32)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = dy @ w.t() if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            T = x.shape[0]
+            nb = 64 if T % 64 == 0 and T >= 4096 else 1
+            dw = torch.bmm(x.view(nb, T // nb, -1).transpose(1, 2), dy.contiguous().view(nb, T // nb, -1)).sum(0)
+        return dx, dw
+
+
+def head_wide(e, p, B: int, N: int, K: int, Q: int, iters: int, head: str):
+    """Routing + relation head at widths outside the fused kernels (the paper's H = 2u = 256):
+    dynamic routing in fp32 (models/reference.py), the neural tensor layer's two contractions
+    (P = C M over all classes at once, then T = Q P per episode) as bf16 MFMA GEMMs with
+    fp32 accumulation -- the precision of the fused bf16 NTN kernel -- and ReLU / FC / sigmoid in fp32."""
+    from ..models import reference as ref
+    H = e.shape[-1]
+    ev = e.float().view(B, N * K + N * Q, H)
+    cls = ref.dynamic_routing(ev[:, : N * K].reshape(B, N, K, H), p["W_s"], iters)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        T = ref.ntn_features(cls, ev[:, N * K:], p["M"])              # [B, NQ, h, N]
+    V = torch.relu(T.float())
+    h = V.shape[2]
+    if head == "reference":
+        logits = TallSkinnyMM.apply(V.reshape(B * N * Q, h * N), p["ntn_w"]).view(B, N * Q, N) + p["ntn_b"]
+    else:
+        logits = torch.einsum("bqsn,s->bqn", V, p["ntn_w"][:, 0]) + p["ntn_b"]
+    return torch.sigmoid(logits)
