@@ -110,6 +110,32 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
     out[i] = accumulate ? out[i] + s : s;
   }
 }
+// float4 form (len % 4 == 0, 16-byte aligned): four slabs' loads in flight per step, same summation
+// order as the scalar kernel (slab 0 first) -- the split-K weight-gradient partials of the BERT GEMMs
+// (16 x [o*i]) summed straight into the flat gradient span
+__global__ __launch_bounds__(256) void slab_reduce4_kernel(const float4* __restrict__ slabs, long nslab, long len4,
+                                                           float4* __restrict__ out, int accumulate) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < len4; i += stride) {
+    float4 s = accumulate ? out[i] : float4{0.f, 0.f, 0.f, 0.f};
+    float4 t = {0.f, 0.f, 0.f, 0.f};
+    long k = 0;
+    for (; k + 4 <= nslab; k += 4) {
+      const float4 a = slabs[k * len4 + i], b = slabs[(k + 1) * len4 + i], c = slabs[(k + 2) * len4 + i],
+                   d = slabs[(k + 3) * len4 + i];
+      t.x += a.x; t.y += a.y; t.z += a.z; t.w += a.w;
+      t.x += b.x; t.y += b.y; t.z += b.z; t.w += b.w;
+      t.x += c.x; t.y += c.y; t.z += c.z; t.w += c.w;
+      t.x += d.x; t.y += d.y; t.z += d.z; t.w += d.w;
+    }
+    for (; k < nslab; ++k) {
+      const float4 a = slabs[k * len4 + i];
+      t.x += a.x; t.y += a.y; t.z += a.z; t.w += a.w;
+    }
+    s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    out[i] = s;
+  }
+}
 
 namespace ina {
 
@@ -154,6 +180,12 @@ int step_control(int* ctl, float* lrt, long long seedA, long long seedB, double 
 }
 
 int slab_reduce(const float* slabs, long nslab, long len, float* out, int accumulate, hipStream_t st) {
+  if (len % 4 == 0 && ((uintptr_t)slabs & 15) == 0 && ((uintptr_t)out & 15) == 0) {
+    hipLaunchKernelGGL(slab_reduce4_kernel, dim3(grid_for(len / 4)), dim3(256), 0, st, (const float4*)slabs, nslab,
+                       len / 4, (float4*)out, accumulate);
+    INA_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for(len)), dim3(256), 0, st, slabs, nslab, len, out, accumulate);
   INA_CHECK_LAUNCH();
   return 0;

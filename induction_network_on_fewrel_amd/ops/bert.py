@@ -38,6 +38,16 @@ def _contiguous_region(ts: List[torch.Tensor]) -> Optional[torch.Tensor]:
     return torch.as_strided(base.detach(), (total,), (1,), off)
 
 
+def _wgrad_parts(dy: torch.Tensor, x: torch.Tensor):
+    """The 16 fp32 K-chunk partials of dy^T x ([16, o, i]), or None where _wgrad uses one GEMM."""
+    T, o = dy.shape
+    i = x.shape[1]
+    nc = 16
+    if T % nc != 0 or T < 4096:
+        return None
+    return torch.bmm(dy.view(nc, T // nc, o).transpose(1, 2), x.view(nc, T // nc, i), out_dtype=torch.float32)
+
+
 def _wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     """dW = dy^T x in fp32.  K = tokens is the long dimension and the output has few 256x256 tiles, so
     the reduction is split by hand into 16 K-chunks (one batched GEMM, fp32 out) + a sum: 1.4-3x the
@@ -77,12 +87,17 @@ class _Linear(torch.autograd.Function):
         res = dx_acc.take() if dx_acc is not None else None
         # in place into the LayerNorm's fresh residual gradient (out-of-place addmm copies C first)
         dx = res.addmm_(dy, Wb) if res is not None else torch.mm(dy, Wb)
-        dW = _wgrad(dy, x)
         db = dy.sum(0, dtype=torch.float32) if has_b else None
         outs = [None] * len(shapes)
-        if gW is not None:
-            gW.add_(dW.view(gW.shape))
+        part = _wgrad_parts(dy, x) if gW is not None and gW.is_contiguous() else None
+        if part is not None:
+            # the split-K partials summed straight into the flat gradient span (one pass instead of
+            # a reduction to a temporary plus an add)
+            ops().slab_reduce(part, gW, True)
+        elif gW is not None:
+            gW.add_(_wgrad(dy, x).view(gW.shape))
         else:
+            dW = _wgrad(dy, x)
             o = 0
             for i in range(nw):
                 outs[i] = dW[o:o + shapes[i][0]]

@@ -153,3 +153,24 @@ def test_bert_encoder_end_to_end():
               "bert.embeddings.word_embeddings.weight", "bert.encoder.layer.0.intermediate.dense.bias"):
         assert n in got, n
         _close(got[n], p[n].grad, rtol=8e-2)
+
+
+def test_split_k_weight_grad_accumulated_into_flat_span():
+    """_Linear's trainer path: the 16 split-K partials of dW = dy^T x are summed by ina.slab_reduce
+    straight into the (pre-filled) flat-gradient span, float4 path and scalar tail path."""
+    from induction_network_on_fewrel_amd.ops import ops
+    from induction_network_on_fewrel_amd.ops.bert import _wgrad_parts
+    torch.manual_seed(3)
+    for (o, i) in ((96, 64), (30, 7)):
+        T = 4096
+        dy = torch.randn(T, o, device=dev).to(torch.bfloat16)
+        x = torch.randn(T, i, device=dev).to(torch.bfloat16)
+        g = torch.randn(o, i, device=dev)
+        want = g + dy.float().t() @ x.float()
+        part = _wgrad_parts(dy, x)
+        assert part is not None and part.shape == (16, o, i)
+        ops().slab_reduce(part, g, True)
+        torch.testing.assert_close(g, want, rtol=1e-4, atol=1e-3)
+        out = torch.empty(o, i, device=dev)
+        ops().slab_reduce(part, out, False)
+        torch.testing.assert_close(out, part.sum(0), rtol=1e-5, atol=1e-4)
