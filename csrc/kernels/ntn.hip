@@ -96,7 +96,7 @@ INA_DEVICE void stage_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); 
 
 // ------------------------------------------------------------------------------------------
 template <int MTH, int QT, bool PAPER>
-__global__ __launch_bounds__(NTN_THREADS) void ntn_fwd_kernel(const float* __restrict__ cls, const float* __restrict__ e,
+__global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void ntn_fwd_kernel(const float* __restrict__ cls, const float* __restrict__ e,
                                                               int E, int N, int K, int Q, int H, int h,
                                                               const u16x8_t* __restrict__ mpack,
                                                               const u16x8_t* __restrict__ wpack,
