@@ -169,7 +169,10 @@ INA_DEVICE void wave_lds_sync() {
 // gather produced.
 // ------------------------------------------------------------------------------------------
 constexpr int XG_T = 16;   // steps per workgroup (16 sequences x 16 steps = 256 threads)
-template <int NX, bool DIRECT>
+// UT / ET / PT: compile-time U, word dim and position dim (0 = the runtime arguments): the reference
+// default (U 20, 5-d words, 5-d positions) gets a fully unrolled, branch-free feature select and keep-bit
+// hash loop
+template <int NX, bool DIRECT, int UT = 0, int ET = 0, int PT = 0>
 __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ inst, int S,
                                                       const int* __restrict__ word, const int* __restrict__ pos1,
                                                       const int* __restrict__ pos2, int L,
@@ -184,8 +187,11 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
   // the two position tables ([2L, PD] each, tiny) in LDS: per-feature loads from them were most of
   // this kernel's vector-memory instructions
   __shared__ float ptab[2 * 128 * 8];
-  const int PT = 2 * L * PD;
-  for (int i = threadIdx.x; i < 2 * PT; i += 256) ptab[i] = i < PT ? p1emb[i] : p2emb[i - PT];
+  if constexpr (UT > 0) U = UT;
+  if constexpr (ET > 0) E = ET;
+  if constexpr (PT > 0) PD = PT;
+  const int PTN = 2 * L * PD;
+  for (int i = threadIdx.x; i < 2 * PTN; i += 256) ptab[i] = i < PTN ? p1emb[i] : p2emb[i - PTN];
   __syncthreads();
   // thread = one token (sequence n = tid & 15, step t0 + tid / 16): its id / row loads are runs along
   // t (coalesced), and it writes its NX x 4 features as 4 lane-group chunks; for a fixed step the
@@ -197,7 +203,7 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
   const long r = (long)inst[valid ? seq : S - 1] * L + min(t, L - 1);   // clamped: unconditional loads
   const int p1 = pos1[r], p2 = pos2[r];
   const float* p1row = ptab + p1 * PD;
-  const float* p2row = ptab + PT + p2 * PD;
+  const float* p2row = ptab + PTN + p2 * PD;
   const int DIN = E + 2 * PD;
   // DIRECT: the token's word row as one 16-byte load of 8 bf16 (E <= 8, zero padded)
   u16x8_t wr = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
@@ -1466,11 +1472,13 @@ int x_gather(const LstmArgs& a, int U, int NX, hipStream_t st) {
   const dim3 grid(ntiles, (a.L + XG_T - 1) / XG_T);
   if (2 * a.L * a.PD > 128 * 8) return -1;   // pos tables staged in LDS
   const auto* wr16 = (const unsigned short*)a.wrows;
-#define INA_XG_LAUNCH(NXV, DIR)                                                                          \
-  hipLaunchKernelGGL((x_gather_kernel<NXV, DIR>), grid, dim3(256), 0, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, \
+#define INA_XG_LAUNCH(NXV, DIR, ...)                                                                     \
+  hipLaunchKernelGGL((x_gather_kernel<NXV, DIR, ##__VA_ARGS__>), grid, dim3(256), 0, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, \
                      a.wemb, wr16, a.E, a.p1emb, a.p2emb, a.PD, xg, posb, a.drop ? a.dmask : nullptr, U, a.seed, \
                      a.seed_dev, a.thr)
-  if (NX == 4 && a.wrows)
+  if (NX == 4 && a.wrows && U == 20 && a.E == 5 && a.PD == 5)
+    INA_XG_LAUNCH(4, true, 20, 5, 5);
+  else if (NX == 4 && a.wrows)
     INA_XG_LAUNCH(4, true);
   else if (NX == 4)
     INA_XG_LAUNCH(4, false);

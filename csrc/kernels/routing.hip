@@ -369,7 +369,7 @@ __global__ __launch_bounds__(256) void routing_g_fwd_kernel(const float* __restr
 
 // dws_slab: [gridDim.x][H][H] (row a, col h)
 template <int H, int K>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void routing_g_bwd_kernel(const float* __restrict__ e, const float* __restrict__ Ws,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void routing_g_bwd_kernel(const float* __restrict__ e, const float* __restrict__ Ws,
                                                             int E, int N, int Q, int R,
                                                             const float* __restrict__ dcls, float* __restrict__ de,
                                                             float* __restrict__ dws_slab) {
