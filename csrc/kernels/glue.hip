@@ -45,10 +45,15 @@ constexpr float CE_P_MIN = 1e-30f;     // models/reference.py::CE_P_MIN (z >= -6
 // rows = E * NQ; probs/dz [rows][N]; labels int32 [rows] (N = NOTA).
 // ce = 0: MSE on the sigmoid scores vs one-hot (reference).  ce = 1: softmax cross-entropy over the
 // pre-sigmoid scores z = log p - log(1 - p) (models/reference.py::ce_loss); NOTA rows contribute 0.
+// NT: compile-time class count (0 = runtime N <= HL_NMAX): the 5-way instantiation loads each row's
+// scores unconditionally and reduces 5 bias-gradient columns instead of 16
+template <int NT>
 __global__ __launch_bounds__(256) void head_loss_kernel(const float* __restrict__ probs,
                                                         const int* __restrict__ labels, long rows, int N,
                                                         float scale, int ce, float* __restrict__ dz,
                                                         float* __restrict__ part) {
+  constexpr int HL_NMAX = NT > 0 ? NT : ::HL_NMAX;
+  if constexpr (NT > 0) N = NT;
   __shared__ float red[4][HL_PART];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float ls = 0.f, cor = 0.f, db[HL_NMAX];
@@ -116,7 +121,7 @@ __global__ __launch_bounds__(256) void head_loss_kernel(const float* __restrict_
     red[wave][0] = ls;
     red[wave][1] = cor;
 #pragma unroll
-    for (int c = 0; c < HL_NMAX; ++c) red[wave][2 + c] = db[c];
+    for (int c = 0; c < ::HL_NMAX; ++c) red[wave][2 + c] = c < HL_NMAX ? db[c < HL_NMAX ? c : 0] : 0.f;
   }
   __syncthreads();
   if (threadIdx.x < HL_PART)
@@ -236,7 +241,10 @@ int gather_pack(const float* src, const int* idx, long nb, long ntot, void* outb
 int head_loss(const float* probs, const int* labels, long rows, int N, float scale, int ce, float* dz, float* out,
               float* part, int blocks, hipStream_t st) {
   if (N > HL_NMAX || rows <= 0) return -1;
-  hipLaunchKernelGGL(head_loss_kernel, dim3(blocks), dim3(256), 0, st, probs, labels, rows, N, scale, ce, dz, part);
+  if (N == 5)
+    hipLaunchKernelGGL(head_loss_kernel<5>, dim3(blocks), dim3(256), 0, st, probs, labels, rows, N, scale, ce, dz, part);
+  else
+    hipLaunchKernelGGL(head_loss_kernel<0>, dim3(blocks), dim3(256), 0, st, probs, labels, rows, N, scale, ce, dz, part);
   INA_CHECK_LAUNCH();
   hipLaunchKernelGGL(head_loss_finish_kernel, dim3(1), dim3(256), 0, st, part, blocks, rows, N, scale, out);
   INA_CHECK_LAUNCH();
