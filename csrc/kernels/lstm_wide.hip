@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void lstm_wide_bwd_step_kernel(
     const float* __restrict__ call,          // [2][S][L][U] fp32 cell states
     const unsigned short* __restrict__ acts, // [2][S][L][4U] bf16
     unsigned short* __restrict__ dG,         // [2][S][L][4U] bf16 out (pre-activation gate grads)
-    unsigned short* __restrict__ dGcur,      // [2][S][4U] bf16 out (this step, operand of dG W_h^T)
+    unsigned short* __restrict__ dGcur,      // [2][S][4U] bf16 out (this step, operand of dG W_h^T) or null
     int S, int L, int U, int tau, uint32_t salt0, uint32_t salt1, uint32_t thr, float inv_kp, int drop) {
   const long total = 2L * S * U;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -105,11 +105,13 @@ __global__ __launch_bounds__(256) void lstm_wide_bwd_step_kernel(
     dG[go + U + u] = bj;
     dG[go + 2 * U + u] = bff;
     dG[go + 3 * U + u] = bo;
-    const size_t gc = ((size_t)dir * S + s) * 4 * U;
-    dGcur[gc + u] = bi;
-    dGcur[gc + U + u] = bj;
-    dGcur[gc + 2 * U + u] = bff;
-    dGcur[gc + 3 * U + u] = bo;
+    if (dGcur) {   // (the caller may read this step's rows of dG through a strided view instead)
+      const size_t gc = ((size_t)dir * S + s) * 4 * U;
+      dGcur[gc + u] = bi;
+      dGcur[gc + U + u] = bj;
+      dGcur[gc + 2 * U + u] = bff;
+      dGcur[gc + 3 * U + u] = bo;
+    }
   }
 }
 

@@ -74,7 +74,7 @@ void lstm_wide_bwd_step(const Tensor& dH, const Tensor& dhrec, const Tensor& dcr
   chk(call, "call", at::kFloat, 2 * S * L * U);
   chk(acts, "acts", at::kBFloat16, 2 * S * L * 4 * U);
   chk(dG, "dG", at::kBFloat16, 2 * S * L * 4 * U);
-  chk(dGcur, "dGcur", at::kBFloat16, 2 * S * 4 * U);
+  if (dGcur.numel() > 0) chk(dGcur, "dGcur", at::kBFloat16, 2 * S * 4 * U);   // empty: not written
   ina::LstmWideArgs a{};
   a.S = (int)S;
   a.L = (int)L;
@@ -85,7 +85,7 @@ void lstm_wide_bwd_step(const Tensor& dH, const Tensor& dhrec, const Tensor& dcr
   a.call = call.data_ptr<float>();
   a.acts = acts.data_ptr();
   a.dG = dG.data_ptr();
-  a.dGcur = dGcur.data_ptr();
+  a.dGcur = dGcur.numel() > 0 ? dGcur.data_ptr() : nullptr;
   fill_drop(a, seed, keep_prob);
   TORCH_CHECK(ina::lstm_wide_bwd_step(a, (int)tau, c10::hip::getCurrentHIPStream().stream()) == 0,
               "ina.lstm_wide_bwd_step: launch failed");

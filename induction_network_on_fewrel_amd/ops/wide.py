@@ -70,12 +70,17 @@ class WideBiLSTM(torch.autograd.Function):
         dhrec = torch.zeros(2, S, U, device=dev)
         dcrec = torch.zeros(2, S, U, device=dev)
         dG = torch.empty(2, S, L, 4 * U, device=dev, dtype=torch.bfloat16)
-        dGcur = torch.empty(2, S, 4 * U, device=dev, dtype=torch.bfloat16)
+        nodg = torch.empty(0, device=dev, dtype=torch.bfloat16)
         WhT = Wh.transpose(1, 2).contiguous()                                    # [2, 4U, U]
+        G4 = 4 * U
         for tau in reversed(range(L)):
-            o.lstm_wide_bwd_step(dH, dhrec, dcrec, call, acts, dG, dGcur, tau, seed, kp)
+            o.lstm_wide_bwd_step(dH, dhrec, dcrec, call, acts, dG, nodg, tau, seed, kp)
             if tau > 0:
-                dhrec = torch.bmm(dGcur, WhT, out_dtype=torch.float32)
+                # this step's dG rows of both directions (times tau and L-1-tau) read in place: one
+                # strided view (batch stride S*L*4U + (t1 - t0)*4U, row stride L*4U), no per-step copy
+                t0, t1 = tau, L - 1 - tau
+                cur = dG.as_strided((2, S, G4), (S * L * G4 + (t1 - t0) * G4, L * G4, 1), t0 * G4)
+                dhrec = torch.bmm(cur, WhT, out_dtype=torch.float32)
         # h_{t-1} in each direction's processing order (zeros at its first step)
         hprev = torch.zeros_like(hall)
         hprev[0, :, 1:] = hall[0, :, :-1]
