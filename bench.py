@@ -15,7 +15,11 @@ BERT configuration (BASELINE.json "FewRel 10-way 5-shot with BERT-base encoder")
   python bench.py --encoder bert   (10-way 5-shot Q=5, BERT-base 12x768, L=128, 8 episodes/GPU)
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--episodes-per-gpu B] [--shot K]
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+Multi-GPU, either form:
+  python bench.py --gpus N       (no launcher: this process starts N rank processes itself -- before it
+                                  touches the GPU -- and exits non-zero if any rank fails or times out)
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+One process per GPU (LOCAL_RANK -> device), RCCL all-reduce ("nccl" backend) of the flat gradient.
 """
 import argparse
 import json
@@ -25,6 +29,63 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int, argv, timeout_s: float) -> int:
+    """Start ``n`` rank processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set),
+    forward rank 0's stdout, return non-zero if any rank fails or exceeds ``timeout_s``.
+
+    Called before anything imports torch's GPU runtime: the parent never initialises HIP, so it
+    is safe to fork/spawn the ranks (each rank then owns its device)."""
+    import signal
+    import subprocess
+    import tempfile
+    port = _free_port()
+    out_file = tempfile.TemporaryFile(mode="w+")   # rank 0's stdout (a file: no pipe to fill up)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), INA_BENCH_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=out_file if r == 0 else subprocess.DEVNULL,
+                                      start_new_session=True, text=True))
+    t_end = time.time() + timeout_s
+    rc = 0
+    try:   # poll every rank: the first failure (or the deadline) ends the whole job
+        while any(p.poll() is None for p in procs):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if time.time() > t_end:
+                print(f"bench: ranks still running after {timeout_s:.0f}s, killing all", file=sys.stderr)
+                rc = 124
+                break
+            time.sleep(0.2)
+        rc = rc or next((p.returncode for p in procs if p.returncode), 0)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+    out_file.seek(0)
+    sys.stdout.write(out_file.read())
+    sys.stdout.flush()
+    if rc != 0:
+        print(f"bench: rank failure (exit codes {[p.returncode for p in procs]})", file=sys.stderr)
+    return rc
 
 
 def main():
@@ -48,7 +109,13 @@ def main():
                     help="eval: forward-only episodic evaluation (FewRel 2.0 style, dropout off, accuracy "
                          "computed); a step = one batch of --episodes-per-gpu episodes (default 16384)")
     ap.add_argument("--nota", type=float, default=0.0, help="eval: none-of-the-above query rate (FewRel 2.0)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: the oracle path (launcher / plumbing tests only; not a benchmark)")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="self-launched multi-rank run: kill every rank after this many seconds")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))
 
     import torch
     from induction_network_on_fewrel_amd.config import Config
@@ -56,10 +123,12 @@ def main():
     from induction_network_on_fewrel_amd.parallel.dp import DistContext
     from induction_network_on_fewrel_amd.runtime.trainer import Trainer
 
-    dist = DistContext.from_env("cuda")
+    dist = DistContext.from_env(args.device)
     world = dist.world
-    if world != args.gpus and dist.is_main:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
+    cuda = args.device == "cuda"
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
     bert = args.encoder == "bert"
     evalm = args.mode == "eval"
     B = args.episodes_per_gpu or (8 if bert else (16384 if evalm else 8192))
@@ -84,7 +153,7 @@ def main():
         f["ids"][:, -1] = 3
         f["length"][:] = cfg.bert_max_length
         data.bert = f
-    tr = Trainer(cfg, data, None, device="cuda", dist_ctx=dist, log=False)
+    tr = Trainer(cfg, data, None, device=args.device, dist_ctx=dist, log=False)
     if evalm:
         tr.nota_threshold = 0.5 if args.nota > 0 else None
 
@@ -94,18 +163,19 @@ def main():
         step = tr.train_step_async
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     loss_t = None
     for _ in range(args.steps):
         loss_t, _ = step()
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    dt = dist.max_scalar(dt)
+    sync()
+    dt_rank = time.perf_counter() - t0
+    rank_ms = [round(1000 * float(x) / args.steps, 3) for x in dist.all_gather_objects(dt_rank)]
+    dt = dist.max_scalar(dt_rank)
     loss = float(loss_t) if loss_t is not None else float("nan")
     in_sync = dist.params_in_sync(tr.flat.flat)
     episodes = args.steps * B * world
@@ -122,7 +192,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": args.dtype,
+            "dtype": args.dtype if cuda else "fp32",
             "data": ("synthetic (64 relations x 700 instances, " +
                      (f"L={cfg.bert_max_length} full-length token ids over a {cfg.bert_vocab} vocab"
                       if bert else f"L=37, 400k vocab, {args.word_dim}-d word table") + "); random-init weights"),
@@ -140,7 +210,10 @@ def main():
             },
             ("eval_accuracy" if evalm else "final_loss"): round(loss, 6),
             "params_in_sync": bool(in_sync),
-            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2),
+            "rccl_world": (torch.distributed.get_world_size() if dist.initialized else 1),
+            "backend": dist.backend or "none",
+            "rank_ms_per_step": rank_ms,
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if cuda else 0.0,
         }
         print(json.dumps(out))
         if args.profile_json:

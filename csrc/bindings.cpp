@@ -617,8 +617,11 @@ std::tuple<Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tensor& e, c
 }
 
 // ------------------------------------------------------------------ optim / misc
-void adam_step(Tensor p, Tensor m, Tensor v, const Tensor& g, const std::optional<Tensor>& l2mask, double lr_t,
-               double b1, double b2, double eps, double gscale, double l2, const std::optional<Tensor>& lr_dev,
+// lr: the scheduled rate (or lr_dev[0]); the kernel applies TF1's bias correction for the applied-step
+// count t = (t_dev[0] if given else t_host) - skips[0] (skips: steps the guard skipped)
+void adam_step(Tensor p, Tensor m, Tensor v, const Tensor& g, const std::optional<Tensor>& l2mask, double lr,
+               int64_t t_host, double b1, double b2, double eps, double gscale, double l2,
+               const std::optional<Tensor>& lr_dev, const std::optional<Tensor>& t_dev,
                const std::optional<Tensor>& guard, const std::optional<Tensor>& skips) {
   check(p, "p", at::kFloat);
   check(m, "m", at::kFloat);
@@ -634,8 +637,9 @@ void adam_step(Tensor p, Tensor m, Tensor v, const Tensor& g, const std::optiona
   }
   if (n == 0) return;
   check_launch(ina::adam_step(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), g.data_ptr<float>(), mk, n,
-                              (float)lr_t, (float)b1, (float)b2, (float)eps, (float)gscale, (float)l2,
-                              dev_float(lr_dev, "lr_dev"), dev_float(guard, "guard"), guard_skips(guard, skips),
+                              (float)lr, (int)t_host, (float)b1, (float)b2, (float)eps, (float)gscale, (float)l2,
+                              dev_float(lr_dev, "lr_dev"), dev_int(t_dev, "t_dev"), dev_float(guard, "guard"),
+                              guard_skips(guard, skips),
                               cur_stream()),
                "adam_step");
 }
@@ -711,7 +715,7 @@ void step_control(Tensor ctl, Tensor lrt, int64_t seedA, int64_t seedB, double l
                "step_control");
 }
 
-int64_t abi_version() { return 4; }
+int64_t abi_version() { return 5; }
 
 }  // namespace
 

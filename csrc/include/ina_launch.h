@@ -138,9 +138,9 @@ int head_loss_part_floats();
 int slab_scatter(const SlabJobs& jobs, float* dst, float* ws, hipStream_t st);
 int ntn_bwd(const NtnArgs& a, hipStream_t st);
 
-int adam_step(float* p, float* m, float* v, const float* g, const unsigned char* l2mask, long n, float lr_t, float b1,
-              float b2, float eps, float gscale, float l2, const float* lr_dev, const float* guard, int* skips,
-              hipStream_t st);
+int adam_step(float* p, float* m, float* v, const float* g, const unsigned char* l2mask, long n, float lr, int t_host,
+              float b1, float b2, float eps, float gscale, float l2, const float* lr_dev, const int* t_dev,
+              const float* guard, int* skips, hipStream_t st);
 int adagrad_step(float* p, float* acc, const float* g, const unsigned char* l2mask, long n, float lr, float gscale,
                  float l2, const float* lr_dev, const float* guard, int* skips, hipStream_t st);
 int nonfinite_flag(const float* g, long n, const float* loss, float* flag, hipStream_t st);

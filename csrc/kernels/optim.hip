@@ -3,6 +3,10 @@
 // single streaming kernel.  Reference: tf.contrib.layers.optimize_loss(optimizer="Adam") with
 // staircase exponential decay (model/base.py:94-99); TF1 Adam update form:
 //   lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t)
+// t is the number of APPLIED updates: t = (host step count | device step counter) - skips, where
+// skips counts the steps the NaN/Inf guard skipped.  The bias correction is computed in the kernel
+// from that device count, so a skipped step does not advance Adam's t (skips only changes in
+// skipped launches, which never read t: no read/write race between workgroups).
 //   m = b1 m + (1 - b1) g ;  v = b2 v + (1 - b2) g^2 ;  p -= lr_t * m / (sqrt(v) + eps)
 // Optional L2 (the reference's dead L2 term, opt-in): g += l2 * p where l2mask[i] != 0.
 // Adagrad (the paper's optimizer, TF1 form): acc += g^2 ; p -= lr * g / sqrt(acc).
@@ -32,14 +36,17 @@ __global__ __launch_bounds__(256) void nonfinite_flag_kernel(const float* __rest
 
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                                                    const float* __restrict__ g, const unsigned char* __restrict__ l2mask,
-                                                   long n, float lr_t, float b1, float b2, float eps, float gscale,
-                                                   float l2, const float* __restrict__ lr_dev,
-                                                   const float* __restrict__ guard, int* __restrict__ skips) {
+                                                   long n, float lr, int t_host, float b1, float b2, float eps,
+                                                   float gscale, float l2, const float* __restrict__ lr_dev,
+                                                   const int* __restrict__ t_dev, const float* __restrict__ guard,
+                                                   int* __restrict__ skips) {
   if (guard && guard[0] != 0.f) {   // non-finite step: no update; block 0 counts it
     if (blockIdx.x == 0 && threadIdx.x == 0) skips[0] = skips[0] + 1;
     return;
   }
-  if (lr_dev) lr_t = lr_dev[0];   // device-resident schedule (HIP-graph replay)
+  if (lr_dev) lr = lr_dev[0];   // device-resident schedule (HIP-graph replay)
+  const int t = (t_dev ? t_dev[0] : t_host) - (skips ? skips[0] : 0);
+  const float lr_t = (float)((double)lr * sqrt(1.0 - pow((double)b2, (double)t)) / (1.0 - pow((double)b1, (double)t)));
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float gi = g[i] * gscale;
@@ -78,8 +85,8 @@ __global__ __launch_bounds__(256) void adagrad_kernel(float* __restrict__ p, flo
 // arguments, so the per-step values are computed on the device by the graph's first kernel from
 // counters that live in device memory (the same formulas as the host: runtime/trainer.py
 // dropout_seed, ops/sampler.py seeds, ops/optim.py lr_at + TF1 Adam bias correction).
-// ctl: [0] dropout seed, [1] sampler seed, [2] global step, [3] sampler calls, [4] optimizer t
-// lrt: [0] learning rate for the optimizer kernel (Adam: bias-corrected lr_t)
+// ctl: [0] dropout seed, [1] sampler seed, [2] global step, [3] sampler calls, [4] optimizer step calls
+// lrt: [0] scheduled learning rate for the optimizer kernel (Adam corrects it from ctl[4] - skips)
 __global__ void step_control_kernel(int* __restrict__ ctl, float* __restrict__ lrt, long long seedA, long long seedB,
                                     double lr0, double decay_steps, double decay_rate, int staircase, int constant,
                                     int adam, double b1, double b2) {
@@ -93,7 +100,7 @@ __global__ void step_control_kernel(int* __restrict__ ctl, float* __restrict__ l
     const double e = staircase ? floor((double)step / decay_steps) : (double)step / decay_steps;
     lr = lr0 * pow(decay_rate, e);
   }
-  if (adam) lr = lr * sqrt(1.0 - pow(b2, (double)t)) / (1.0 - pow(b1, (double)t));
+  (void)adam; (void)b1; (void)b2;   // bias correction: adam_kernel, from the applied-step count
   lrt[0] = (float)lr;
   ctl[2] = (int)(step + 1);
   ctl[3] = (int)(calls + 1);
@@ -146,11 +153,11 @@ static int grid_for(long n) {
   return (int)b;
 }
 
-int adam_step(float* p, float* m, float* v, const float* g, const unsigned char* l2mask, long n, float lr_t, float b1,
-              float b2, float eps, float gscale, float l2, const float* lr_dev, const float* guard, int* skips,
-              hipStream_t st) {
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, m, v, g, l2mask, n, lr_t, b1, b2, eps, gscale,
-                     l2, lr_dev, guard, skips);
+int adam_step(float* p, float* m, float* v, const float* g, const unsigned char* l2mask, long n, float lr, int t_host,
+              float b1, float b2, float eps, float gscale, float l2, const float* lr_dev, const int* t_dev,
+              const float* guard, int* skips, hipStream_t st) {
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, m, v, g, l2mask, n, lr, t_host, b1, b2, eps,
+                     gscale, l2, lr_dev, t_dev, guard, skips);
   INA_CHECK_LAUNCH();
   return 0;
 }

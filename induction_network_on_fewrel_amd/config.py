@@ -104,7 +104,8 @@ class Config:
     dtype: str = "bf16"                # MFMA operand dtype on GPU: "bf16" | "fp32"
     device: str = "auto"               # "auto" | "cuda" | "cpu"
     seed: int = 12345
-    deterministic: bool = False
+    deterministic: bool = False        # seeds + torch deterministic algorithms (utils/seeding.py); the fused
+                                       # GPU path is deterministic regardless (ordered reductions)
     use_hip_graph: bool = False        # replay the BiLSTM train step as one captured hipGraph (runtime/graph.py)
     step_glue: bool = True             # GPU BiLSTM: one-launch packs / loss / gradient scatter (ops/glue.py)
     nota_rate: float = 0.0             # FewRel 2.0 none-of-the-above probability per query

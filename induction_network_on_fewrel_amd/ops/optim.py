@@ -97,9 +97,15 @@ class FusedOptimizer:
         self.b1, self.b2, self.eps = beta1, beta2, eps
         self.l2 = float(l2)
         self.l2_mask = l2_mask if (l2_mask is not None and self.l2 > 0) else None
-        self.t = 0  # number of optimizer steps (TF's beta powers = beta^t)
+        # Adam's t counts APPLIED updates only (a step the NaN/Inf guard skips must not advance the bias
+        # correction): t = t_base + calls - skips since the base, where the base is set at construction /
+        # checkpoint load.  On the GPU the kernel derives t from the host call count (or the graph's
+        # device counter) minus the device skip counter, so no host synchronisation is needed.
+        self.t_base = 0       # applied updates at the base
+        self.calls = 0        # step() calls since the base (applied + skipped)
         dev = flat.flat.device
-        self.skips_host = 0   # steps skipped by the NaN/Inf guard (CPU path + restored from a checkpoint)
+        self.skips_base = 0   # skipped steps before the base (restored from a checkpoint)
+        self.skips_cpu = 0    # CPU path: skipped steps since the base
         self.skips_dev = torch.zeros(1, dtype=torch.int32, device=dev) if dev.type == "cuda" else None
         if kind == "adam":
             self.m = torch.zeros(flat.numel, dtype=torch.float32, device=dev)
@@ -114,26 +120,43 @@ class FusedOptimizer:
             return {"m": self.m, "v": self.v}
         return {"acc": self.acc}
 
+    def _skips_since_base(self) -> int:
+        return self.skips_cpu + (int(self.skips_dev.item()) if self.skips_dev is not None else 0)
+
     def skipped(self) -> int:
         """Steps the NaN/Inf guard skipped so far (reads the device counter: synchronises)."""
-        return self.skips_host + (int(self.skips_dev.item()) if self.skips_dev is not None else 0)
+        return self.skips_base + self._skips_since_base()
 
-    def set_skipped(self, n: int) -> None:
-        self.skips_host = int(n)
+    @property
+    def t(self) -> int:
+        """Applied Adam updates (TF's beta powers are beta^(t+1) after them); synchronises on the GPU."""
+        return self.t_base + self.calls - self._skips_since_base()
+
+    @property
+    def t_host(self) -> int:
+        """What the kernel subtracts the device skip count from: t_base + calls (no synchronisation)."""
+        return self.t_base + self.calls
+
+    def load_counters(self, t_applied: int, skipped_total: int) -> None:
+        """Re-base the step accounting (checkpoint restore)."""
+        self.t_base, self.calls = int(t_applied), 0
+        self.skips_base, self.skips_cpu = int(skipped_total), 0
         if self.skips_dev is not None:
             self.skips_dev.zero_()
 
     def step(self, lr: float, grad_scale: float = 1.0, lr_dev: Optional[torch.Tensor] = None,
-             check_finite: bool = False, loss: Optional[torch.Tensor] = None) -> None:
-        """``lr_dev``: device scalar holding the (bias-corrected for Adam) rate, overriding ``lr``
-        (HIP-graph replay: written by ina.step_control inside the captured step).
+             check_finite: bool = False, loss: Optional[torch.Tensor] = None,
+             t_dev: Optional[torch.Tensor] = None) -> None:
+        """``lr``: the scheduled rate; Adam's bias correction is applied for the applied-step count.
+        ``lr_dev`` / ``t_dev``: device scalars overriding ``lr`` and the host step count (HIP-graph
+        replay: written by ina.step_control inside the captured step).
 
         ``check_finite``: skip the whole update (parameters and moments untouched) when any gradient
         -- or ``loss``, a scalar -- is NaN/Inf.  On the GPU the decision is made on the device
         (``ina.nonfinite_flag`` -> guard word in the gradient buffer tail -> the optimizer kernel), so
         the step stays asynchronous / graph-capturable; skips are counted in ``skips_dev``.  Under DP
         pass the all-reduced gradients and no loss, so every rank takes the same decision."""
-        self.t += 1
+        self.calls += 1
         p, g = self.flat.flat, self.flat.grad
         if p.is_cuda:
             o = ops()
@@ -142,22 +165,22 @@ class FusedOptimizer:
                 guard = self.flat.guard
                 o.nonfinite_flag(g, loss.detach().reshape(1).float() if loss is not None else None, guard)
             if self.kind == "adam":
-                lr_t = lr * math.sqrt(1 - self.b2 ** self.t) / (1 - self.b1 ** self.t)
-                o.adam_step(p, self.m, self.v, g, self.l2_mask, lr_t, self.b1, self.b2, self.eps, grad_scale, self.l2,
-                            lr_dev, guard, self.skips_dev)
+                o.adam_step(p, self.m, self.v, g, self.l2_mask, lr, self.t_host, self.b1, self.b2, self.eps, grad_scale,
+                            self.l2, lr_dev, t_dev, guard, self.skips_dev)
             else:
                 o.adagrad_step(p, self.acc, g, self.l2_mask, lr, grad_scale, self.l2, lr_dev, guard, self.skips_dev)
             return
         if check_finite and (not bool(torch.isfinite(g).all())
                              or (loss is not None and not bool(torch.isfinite(loss.detach()).all()))):
-            self.skips_host += 1
+            self.skips_cpu += 1
             return
         with torch.no_grad():
             gg = g * grad_scale
             if self.l2_mask is not None:
                 gg = gg + self.l2 * p * self.l2_mask.float()
             if self.kind == "adam":
-                lr_t = lr * math.sqrt(1 - self.b2 ** self.t) / (1 - self.b1 ** self.t)
+                t = self.t   # applied updates including this one (CPU: no device counter)
+                lr_t = lr * math.sqrt(1 - self.b2 ** t) / (1 - self.b1 ** t)
                 self.m.mul_(self.b1).add_(gg, alpha=1 - self.b1)
                 self.v.mul_(self.b2).addcmul_(gg, gg, value=1 - self.b2)
                 p.sub_(lr_t * self.m / (self.v.sqrt() + self.eps))

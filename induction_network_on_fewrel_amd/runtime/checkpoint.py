@@ -86,6 +86,7 @@ def save(model_dir: str, name: str, step: int, tensors: "OrderedDict[str, torch.
                             for k, v in cpu.items()})
     with open(os.path.join(d, stem + ".index.json"), "w") as fh:
         json.dump(index, fh, indent=1, sort_keys=True)
+    prev_best = best_stem(model_dir)
     if best:
         with open(_best_file(model_dir) + ".tmp", "w") as fh:
             fh.write(f'model_checkpoint_path: "{stem}"\n')
@@ -95,15 +96,22 @@ def save(model_dir: str, name: str, step: int, tensors: "OrderedDict[str, torch.
     allp = [p for p in allp if p != stem] + [stem]
     while len(allp) > max_to_keep:
         old = allp.pop(0)
-        if old == keep:
-            continue   # dropped from the rotation list, file kept
-        for ext in (".safetensors", ".index.json"):
-            try:
-                os.remove(os.path.join(d, old + ext))
-            except FileNotFoundError:
-                pass
+        if old != keep:   # the best checkpoint leaves the rotation list but its files stay
+            _remove(d, old)
+    # a superseded best that already left the rotation is referenced by nothing any more: delete it
+    # (otherwise every best that outlives max_to_keep periodic saves and is then beaten leaks a file)
+    if best and prev_best is not None and prev_best != stem and prev_best not in allp:
+        _remove(d, prev_best)
     _write_state(model_dir, stem, allp)
     return os.path.join(d, stem)
+
+
+def _remove(d: str, stem: str) -> None:
+    for ext in (".safetensors", ".index.json"):
+        try:
+            os.remove(os.path.join(d, stem + ext))
+        except FileNotFoundError:
+            pass
 
 
 def latest(model_dir: str) -> Optional[str]:

@@ -28,9 +28,10 @@ class GraphedTrainStep:
         dev = trainer.device
         self.dist = trainer.dist
         self.with_opt = trainer.dist.world == 1
-        # ctl: [dropout seed, sampler seed, global step, sampler calls, optimizer t]
+        # ctl: [dropout seed, sampler seed, global step, sampler calls, optimizer step calls (t_base + calls;
+        # the Adam kernel subtracts the device skip count)]
         s = trainer.train_eps
-        self.ctl = torch.tensor([0, 0, trainer.global_step, s.calls, trainer.opt.t, 0, 0, 0], dtype=torch.int32,
+        self.ctl = torch.tensor([0, 0, trainer.global_step, s.calls, trainer.opt.t_host, 0, 0, 0], dtype=torch.int32,
                                 device=dev)
         self.lrt = torch.zeros(2, dtype=torch.float32, device=dev)
         self.seedA = (cfg.seed * 2654435761 + trainer.dist.rank * 7919) & 0x7FFFFFFF
@@ -50,11 +51,11 @@ class GraphedTrainStep:
             self._after_eager_or_replay()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
-        saved = (s.calls, tr.opt.t)
+        saved = (s.calls, tr.opt.calls)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.loss, self.acc = self._body()
-        s.calls, tr.opt.t = saved           # capture does not execute: undo the host bookkeeping
+        s.calls, tr.opt.calls = saved           # capture does not execute: undo the host bookkeeping
         return loss, acc
 
     def _body(self):
@@ -73,14 +74,16 @@ class GraphedTrainStep:
             tr.glue.flush()
         tr.flat.sync_grads_into_flat()
         if self.with_opt:
-            tr.opt.step(0.0, grad_scale=1.0, lr_dev=self.lrt[0:1], check_finite=cfg.grad_check_finite, loss=loss)
+            tr.opt.step(0.0, grad_scale=1.0, lr_dev=self.lrt[0:1], check_finite=cfg.grad_check_finite, loss=loss,
+                        t_dev=self.ctl[4:5])
         return loss.detach(), acc
 
     def _after_eager_or_replay(self):
         tr = self.tr
         if not self.with_opt:
             tr.dist.allreduce_buckets_(tr.flat.grad)
-            tr.opt.step(0.0, grad_scale=1.0 / tr.dist.world, lr_dev=self.lrt[0:1], check_finite=tr.cfg.grad_check_finite)
+            tr.opt.step(0.0, grad_scale=1.0 / tr.dist.world, lr_dev=self.lrt[0:1], check_finite=tr.cfg.grad_check_finite,
+                        t_dev=self.ctl[4:5])
         tr.global_step += 1
 
     def step(self):
@@ -92,6 +95,6 @@ class GraphedTrainStep:
         self.graph.replay()
         tr.train_eps.calls += 1
         if self.with_opt:
-            tr.opt.t += 1
+            tr.opt.calls += 1
         self._after_eager_or_replay()
         return self.loss, self.acc

@@ -63,6 +63,9 @@ class Trainer:
                  test_data: Optional[FewRelDataset] = None):
         cfg.validate()
         self.cfg = cfg
+        if cfg.deterministic:
+            from ..utils import make_deterministic
+            make_deterministic(cfg.seed)
         self.dist = dist_ctx or DistContext.from_env(device if device != "auto" else cfg.device)
         if device not in ("auto", None) and self.dist.world == 1 and torch.device(device).type != self.dist.device.type:
             self.dist.device = torch.device(device)   # (keeps from_env's device index for a matching type)
@@ -370,7 +373,8 @@ class Trainer:
         skipped = self.skipped_steps
         if not self.dist.is_main:
             return None
-        meta = {"best_acc": self.best_acc, "optimizer_t": self.opt.t, "config": self.cfg.to_dict(),
+        meta = {"best_acc": self.best_acc, "optimizer_t": self.opt.t, "optimizer_t_counts": "applied",
+                "config": self.cfg.to_dict(),
                 "train_samplers": samplers, "skipped_steps": skipped, "world_size": self.dist.world}
         return ckpt.save(self.cfg.model_dir, self.cfg.ckpt_name, self.global_step, self.state_tensors(), meta,
                          self.cfg.max_to_keep, best=best)
@@ -389,9 +393,13 @@ class Trainer:
                 elif self.opt.kind == "adagrad" and tf + "/Adagrad" in tensors:
                     self.flat.view(st["acc"], attr).copy_(tensors[tf + "/Adagrad"])
         self.global_step = int(tensors["global_step"].item()) if "global_step" in tensors else int(meta["global_step"])
-        self.opt.t = int(meta.get("optimizer_t", self.global_step))
         self.best_acc = float(meta.get("best_acc", 0.0))
-        self.opt.set_skipped(int(meta.get("skipped_steps", 0)))
+        skipped = int(meta.get("skipped_steps", 0))
+        # optimizer_t: applied Adam updates (older checkpoints stored the step count, skips included)
+        t = int(meta["optimizer_t"]) if "optimizer_t" in meta else self.global_step - skipped
+        if meta.get("optimizer_t_counts") != "applied":
+            t -= skipped
+        self.opt.load_counters(max(0, t), skipped)
         self._restore_sampler(meta)
         if self.dist.initialized:
             self.dist.broadcast_(self.flat.flat, 0)

@@ -1,4 +1,3 @@
-from .timing import GpuTimer, PhaseTimer
-from .seeding import seed_everything
+from .seeding import make_deterministic, seed_everything
 
-__all__ = ["GpuTimer", "PhaseTimer", "seed_everything"]
+__all__ = ["make_deterministic", "seed_everything"]

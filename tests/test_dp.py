@@ -1,10 +1,17 @@
 """Episode data parallelism, multi-process on CPU with the gloo backend (world_size 2 and 4).
 
-Checks: the all-reduced gradient equals the average of the per-rank gradients,
-parameters stay bitwise identical across ranks after optimizer steps, and rank samplers differ.
+Checks:
+* the DP step's gradient (all-reduce of the per-rank gradients, then the optimizer's 1/world scale)
+  equals the gradient of ONE single-rank step over the union of every rank's episodes;
+* parameters stay bitwise identical across ranks after optimizer steps, and rank samplers differ;
+* ``python bench.py --gpus 2`` without a launcher starts the ranks itself (gloo on CPU here; the
+  one-card GPU form is tests/test_dp_gpu.py).
 """
+import json
 import os
 import socket
+import subprocess
+import sys
 
 import pytest
 import torch
@@ -31,17 +38,29 @@ def _worker(rank, world, port, out_dir):
     data = make_synthetic(num_relations=10, instances_per_relation=30, vocab=300, seed=0)
     cfg = Config(N=5, K=2, Q=2, episodes_per_step=2, model_dir=os.path.join(out_dir, "m"), resume=False, seed=5)
     tr = Trainer(cfg, data, None, device="cpu", dist_ctx=dist, log=False)
-    # 1) gradient all-reduce == mean of local gradients
-    idx, lab = tr.train_eps.sample(2, 5, 2, 2)
-    tr.flat.zero_grad()
-    probs, _ = tr.model(idx.view(-1), tr.train_eps.arrays, 2, 5, 2, 2, training=False)
-    tr.model.loss(probs, lab).backward()
-    tr.flat.sync_grads_into_flat()
-    local = tr.flat.grad.clone()
-    gathered = [torch.zeros_like(local) for _ in range(world)]
-    torch.distributed.all_gather(gathered, local)
+    # 1) DP gradient == single-rank gradient over the union of the ranks' episodes.  Dropout off
+    #    (training=False) so the union forward sees exactly the rows each rank saw.
+    B = 2
+    idx, lab = tr.train_eps.sample(B, 5, 2, 2)
+
+    def grad_of(i, l, b):
+        tr.flat.zero_grad()
+        probs, _ = tr.model(i.reshape(-1), tr.train_eps.arrays, b, 5, 2, 2, training=False)
+        tr.model.loss(probs, l).backward()
+        tr.flat.sync_grads_into_flat()
+        return tr.flat.grad.clone()
+
+    local = grad_of(idx, lab, B)
+    tr.flat.grad.copy_(local)
     tr.dist.allreduce_buckets_(tr.flat.grad, bucket_mb=0.05)   # several buckets
-    ok_sum = torch.allclose(tr.flat.grad, sum(gathered), atol=1e-6)
+    dp_grad = tr.flat.grad.clone() * (1.0 / world)               # the optimizer's grad_scale
+    all_idx = [torch.zeros_like(idx) for _ in range(world)]
+    all_lab = [torch.zeros_like(lab) for _ in range(world)]
+    torch.distributed.all_gather(all_idx, idx)
+    torch.distributed.all_gather(all_lab, lab)
+    union = grad_of(torch.cat(all_idx), torch.cat(all_lab), B * world)
+    ok_sum = bool(torch.allclose(dp_grad, union, rtol=1e-5, atol=1e-8)) and bool(local.abs().sum() > 0) \
+        and not torch.equal(local * world, union)   # the ranks' gradients really differ
     # 2) params identical after optimizer steps
     for _ in range(3):
         tr.train_step()
@@ -107,3 +126,25 @@ def test_dp_gloo_world(tmp_path, world):
     assert all(x["ok_overlap"] for x in r)
     for i in range(1, world):
         assert not torch.equal(r[0]["idx"], r[i]["idx"])   # rank-folded sampling
+
+
+def test_bench_self_launch_world2_cpu():
+    """``bench.py --gpus 2`` with no torch.distributed.run: the parent starts both ranks, rank 0 prints
+    one JSON line with the real collective world size; a failing rank fails the whole job."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "INA_FAULT_STEP"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--device", "cpu", "--steps", "2",
+           "--warmup", "1", "--episodes-per-gpu", "2", "--launch-timeout", "240"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["rccl_world"] == 2 and out["backend"] == "gloo"
+    assert out["params_in_sync"] is True and len(out["rank_ms_per_step"]) == 2
+    assert out["config"]["global_batch"] == 4 and out["config"]["parallelism"] == "dp2"
+    bad = subprocess.run(cmd, cwd=root, env=dict(env, INA_FAULT_STEP="1", INA_FAULT_RANK="1"), capture_output=True,
+                         text=True, timeout=300)
+    assert bad.returncode != 0

@@ -59,4 +59,23 @@ def test_bench_rccl_world1():
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 1 and out["params_in_sync"] is True
+    assert out["rccl_world"] == 1 and out["backend"] == "nccl"
     assert out["final_loss"] == out["final_loss"] and out["value"] > 0
+
+
+def test_bench_self_launch_world2_one_gpu():
+    """The driver's form, ``python bench.py --gpus 2`` with NO launcher: bench.py starts both ranks
+    itself (before touching the GPU), both ranks share the one card (gloo collectives on CUDA
+    tensors), and rank 0 reports the real collective world size."""
+    env = dict(os.environ, INA_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
+           "--episodes-per-gpu", "64", "--launch-timeout", "100"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=115)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["rccl_world"] == 2 and out["backend"] == "gloo"
+    assert out["params_in_sync"] is True and len(out["rank_ms_per_step"]) == 2

@@ -417,8 +417,8 @@ def test_adam_matches_tf_formula():
     v = torch.zeros(n, device=DEV)
     p0 = p.clone()
     b1, b2, eps, lr = 0.9, 0.999, 1e-8, 1e-3
-    lr_t = lr * (1 - b2) ** 0.5 / (1 - b1)
-    ops().adam_step(p, m, v, g, None, lr_t, b1, b2, eps, 1.0, 0.0, None, None, None)
+    lr_t = lr * (1 - b2) ** 0.5 / (1 - b1)   # TF1 bias correction at t = 1, applied inside the kernel
+    ops().adam_step(p, m, v, g, None, lr, 1, b1, b2, eps, 1.0, 0.0, None, None, None, None)
     m_r = (1 - b1) * g
     v_r = (1 - b2) * g * g
     p_r = p0 - lr_t * m_r / (v_r.sqrt() + eps)

@@ -79,6 +79,27 @@ def test_best_checkpoint_survives_rotation_and_newer_saves(tmp_path):
     assert "inductionNetwork-4.safetensors" not in files and "inductionNetwork-2.safetensors" in files
 
 
+def test_superseded_best_is_deleted(tmp_path):
+    """Advisor finding: a best that left the rotation and is then beaten must not stay on disk."""
+    md = str(tmp_path / "m")
+    t = lambda step: {"W_s": torch.ones(2, 2) * step, "global_step": torch.tensor(step)}
+    ckpt.save(md, "inductionNetwork", 2, t(2), {}, max_to_keep=2, best=True)
+    for step in (4, 6, 8):
+        ckpt.save(md, "inductionNetwork", step, t(step), {}, max_to_keep=2)
+    ckpt.save(md, "inductionNetwork", 10, t(10), {}, max_to_keep=2, best=True)   # beats best-2
+    files = sorted(os.listdir(os.path.join(md, "checkpoint")))
+    assert "inductionNetwork-2.safetensors" not in files and "inductionNetwork-2.index.json" not in files
+    assert ckpt.best(md).endswith("inductionNetwork-10")
+    # a best still inside the rotation is left to the rotation (it is a regular checkpoint too)
+    ckpt.save(md, "inductionNetwork", 12, t(12), {}, max_to_keep=2, best=True)
+    files = sorted(os.listdir(os.path.join(md, "checkpoint")))
+    assert "inductionNetwork-10.safetensors" in files and ckpt.best(md).endswith("inductionNetwork-12")
+    ckpt.save(md, "inductionNetwork", 14, t(14), {}, max_to_keep=2)
+    files = sorted(os.listdir(os.path.join(md, "checkpoint")))
+    assert [f for f in files if f.endswith(".safetensors")] == ["inductionNetwork-12.safetensors",
+                                                                "inductionNetwork-14.safetensors"]
+
+
 def test_test_best_loads_best_not_latest(tmp_path):
     """test_best with periodic saves: the final test must run on the best-val weights."""
     tr = _trainer(tmp_path, resume=False, save_every=1, train_iter=4, val_step=2, val_iter=2, test_iter=2,
