@@ -17,6 +17,7 @@ typedef unsigned short u16x8_t __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x4_t __attribute__((ext_vector_type(4)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
 namespace ina {
 

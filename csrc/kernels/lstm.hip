@@ -577,7 +577,10 @@ struct BwdWaves {
 // WG: trained word table (word-row gradients by global atomics).  A template flag rather than a
 // runtime branch: the join after a skipped atomic block made LLVM drain every outstanding load
 // (s_waitcnt vmcnt(0), a register of that block is reused) on every step, prefetch included.
-template <int U, int NX, bool BF16, bool WG = false>
+// PM (bf16 only): dH arrives in the step-record lane layout ALREADY multiplied by the DropoutWrapper
+// scale (rec_attn_bwd), and the BPTT runs the lean step below (raw bf16 operands, no keep bits, no
+// per-lane validity selects, uniform per-step addresses).
+template <int U, int NX, bool BF16, bool WG = false, bool PM = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U, NX>::value))) void lstm_bwd_kernel(
     const int* __restrict__ inst, int S, const int* __restrict__ word, const int* __restrict__ pos1,
     const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
@@ -890,7 +893,221 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       }
       }
     };
-    if constexpr (!BF16) {
+    if constexpr (BF16 && PM) {
+      // ---------------- lean bf16 BPTT (premasked lane-layout dH) ----------------
+      // Every per-step address is wave-uniform base + a per-lane constant (saddr loads / stores, no
+      // 64-bit VALU address math); h / x stay raw bf16 bits from the load to the B operand and the dW
+      // image (v_perm pairs, no f32 round trip); dH needs one shift (it carries the dropout scale).
+      const int tu = __builtin_amdgcn_readfirstlane(tile);
+      // buffer descriptors over this (tile, dir)'s regions: per-step offsets go in SGPR soffset, the lane's
+      // part in a loop-invariant voffset (no per-step VALU address math)
+      auto rsrc = [](const void* base, uint32_t bytes) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+      };
+      const uint32_t RSTEPB = 2 * U4 * 64 * 2, DSTEPB = U4 * 64 * 2, XSTEPB = 64 * NX * 2, PSTEPB = (NPF + 1) * 16 * 2;
+      const auto rrec = rsrc(reinterpret_cast<const unsigned short*>(hraw) + ((size_t)tu * 2 + dir) * L * 2 * U4 * 64,
+                             (uint32_t)L * RSTEPB);
+      const auto rdh = rsrc(reinterpret_cast<const unsigned short*>(dH) + ((size_t)tu * 2 + dir) * L * U4 * 64,
+                            (uint32_t)L * DSTEPB);
+      const auto rx = rsrc(xg + (size_t)tu * L * 64 * NX, (uint32_t)L * XSTEPB);
+      const auto rdx = rsrc(dxp + ((size_t)dir * ntiles + tu) * L * (NPF + 1) * 16, (uint32_t)L * PSTEPB);
+      const int vl2 = lane * 2, vx = lane * NX * 2;
+      constexpr int NXW = NX / 2;   // x words (2 features each) per lane and step
+      struct Raw {
+        uint32_t h[U4], c[U4], d[U4];   // 16-bit loads (upper halves never read)
+        uint32_t x[NXW];
+      };
+      auto rload = [&](int tau, Raw& o) __attribute__((always_inline)) {
+        const int tn = tof(tau), tp = tof(tau >= 1 ? tau - 1 : 0);
+        const int sr = tp * RSTEPB, sd = tn * DSTEPB, sx = tn * XSTEPB;
+#pragma unroll
+        for (int m = 0; m < U4; ++m) {
+          o.h[m] = __builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + m * 128, sr, 0);
+          o.c[m] = __builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + (U4 + m) * 128, sr, 0);
+          o.d[m] = __builtin_amdgcn_raw_buffer_load_b16(rdh, vl2 + m * 128, sd, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < NXW / 2; ++k) {
+          const auto v = __builtin_amdgcn_raw_buffer_load_b64(rx, vx + 8 * k, sx, 0);
+          o.x[2 * k] = (uint32_t)v[0];
+          o.x[2 * k + 1] = (uint32_t)v[1];
+        }
+      };
+      auto pkf = [](float a, float b) {   // two floats -> packed bf16 pair (one v_cvt_pk_bf16_f32)
+        typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+        const bf2_t v = {(__bf16)a, (__bf16)b};
+        return __builtin_bit_cast(uint32_t, v);
+      };
+      // HASP: the step has a predecessor (tau >= 1; else h_{-1} = c_{-1} = 0).  ODD: tau is odd (image
+      // rows 16..31); an even step completes the pair {tau + 1, tau} and flushes it into dW.
+      auto bstep = [&](auto hasp_c, auto odd_c, const int tau, const Raw& X0) __attribute__((always_inline)) {
+        constexpr bool HASP = decltype(hasp_c)::value, ODD = decltype(odd_c)::value;
+        Raw X = X0;
+#pragma unroll
+        for (int m = 0; m < U4; ++m) asm volatile("" : "+v"(X.h[m]), "+v"(X.c[m]), "+v"(X.d[m]));
+#pragma unroll
+        for (int k = 0; k < NXW; ++k) asm volatile("" : "+v"(X.x[k]));
+        const int t = tof(tau);
+        // slot words [h (U4) ; x (NX slots) ; 0]: the gate B operand and the dW image row.  Slot s is the
+        // 16-bit half `off` (byte 0 or 2, -1 = zero) of register word `wd`; a pair word is ONE v_perm.
+        struct Half {
+          uint32_t wd;
+          int off;
+        };
+        auto slot = [&](int sidx) -> Half {
+          if (sidx < U4) return HASP ? Half{X.h[sidx], 0} : Half{0u, -1};
+          const int xi = sidx - U4;
+          if (xi < NX) return Half{X.x[xi >> 1], 2 * (xi & 1)};
+          return Half{0u, -1};
+        };
+        constexpr int NW = NKS * 4;   // B operand words (8 slots per K-step)
+        uint32_t bw[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          const int s0 = 2 * w, s1 = 2 * w + 1;
+          const Half lo = slot(s0), hi = slot(s1);
+          if (lo.off < 0 && hi.off < 0) {
+            bw[w] = 0u;
+          } else if (s0 >= U4 && ((s0 - U4) & 1) == 0 && s1 < U4 + NX) {
+            bw[w] = lo.wd;   // an aligned x pair is one loaded word
+          } else {           // v_perm: bytes 0-3 of src1 (lo word), 4-7 of src0 (hi word), 0x0C = zero byte
+            const uint32_t sl = lo.off < 0 ? 0x0C0Cu : (uint32_t)(lo.off | ((lo.off + 1) << 8));
+            const uint32_t sh = hi.off < 0 ? 0x0C0Cu : (uint32_t)((4 + hi.off) | ((5 + hi.off) << 8));
+            bw[w] = __builtin_amdgcn_perm(hi.off < 0 ? 0u : hi.wd, lo.off < 0 ? 0u : lo.wd, sl | (sh << 16));
+          }
+        }
+        float cprev[U4], dhin[U4];
+#pragma unroll
+        for (int m = 0; m < U4; ++m) {
+          cprev[m] = HASP ? (float)__builtin_bit_cast(_Float16, (unsigned short)X.c[m]) : 0.f;
+          dhin[m] = __builtin_bit_cast(float, X.d[m] << 16);
+        }
+        // ---- recompute gates
+        float dg[U4][4];
+#pragma unroll
+        for (int m = 0; m < NMT; ++m) {
+          f32x4_t acc = {bm[m][0], bm[m][1], bm[m][2], bm[m][3]};
+#pragma unroll
+          for (int ks = 0; ks < NKS; ++ks)
+            acc = mma(lA[(m * NKS + ks) * 64 + lane],
+                      __builtin_bit_cast(u16x8_t, u32x4_t{bw[4 * ks], bw[4 * ks + 1], bw[4 * ks + 2], bw[4 * ks + 3]}), acc);
+          const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
+          const float tc = tanh_l2(ccur[m] * (2.f * LOG2E_F));
+          const float dh = dh_rec[m] + dhin[m];
+          const float dc = dc_rec[m] + dh * og * (1.f - tc * tc);
+          dc_rec[m] = dc * fg;
+          dg[m][0] = dc * jg * (ig - ig * ig);
+          dg[m][1] = dc * ig * (1.f - jg * jg);
+          dg[m][2] = dc * cprev[m] * (fg - fg * fg);
+          dg[m][3] = dh * tc * (og - og * og);
+          ccur[m] = cprev[m];
+        }
+        uint32_t dgw[2 * U4];   // packed bf16 dG pairs: the W dG operand and the dW image row
+#pragma unroll
+        for (int m = 0; m < U4; ++m) {
+          dgw[2 * m] = pkf(dg[m][0], dg[m][1]);
+          dgw[2 * m + 1] = pkf(dg[m][2], dg[m][3]);
+        }
+        // ---- d[x;h] = W dG
+        float dslot[NMT2 * 4];
+#pragma unroll
+        for (int mt = 0; mt < NMT2; ++mt) {
+          f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < NKS2; ++ks) {
+            uint32_t w4[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w4[j] = 4 * ks + j < 2 * U4 ? dgw[4 * ks + j] : 0u;
+            acc = mma(lA2[(mt * NKS2 + ks) * 64 + lane], __builtin_bit_cast(u16x8_t, u32x4_t{w4[0], w4[1], w4[2], w4[3]}),
+                      acc);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dslot[mt * 4 + r] = acc[r];
+        }
+#pragma unroll
+        for (int m = 0; m < U4; ++m) dh_rec[m] = dslot[m];
+        // pos-feature gradients -> dxp rows (word / padding features: the trash row)
+        const int sp = t * PSTEPB;
+#pragma unroll
+        for (int xi = 0; xi < NX; xi += 2) {
+          const uint32_t w = pkf(dslot[U4 + xi], xi + 1 < NX ? dslot[U4 + xi + 1] : 0.f);
+          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)w, rdx, 2 * pofs[xi], sp, 0);
+          if (xi + 1 < NX) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(w >> 16), rdx, 2 * pofs[xi + 1], sp, 0);
+        }
+        if constexpr (WG) {   // trained word table: global atomics
+          if (valid) {
+            const int wrow = word[rowbase + t];
+#pragma unroll
+            for (int xi = 0; xi < NX; ++xi)
+              if (xs[xi].sel == 0) atomicAdd(&dwemb[(long)wrow * E + xs[xi].col], dslot[U4 + xi]);
+          }
+        }
+        // ---- stage dG / [h;x] into the pair's image rows, flush on the even step
+        constexpr int RR = ODD ? 16 : 0;
+        uint32_t* gi = reinterpret_cast<uint32_t*>(dgI + (RR + n) * GCP + q * (4 * U4));
+#pragma unroll
+        for (int w = 0; w < 2 * U4; ++w) gi[w] = dgw[w];
+        uint32_t* xi32 = reinterpret_cast<uint32_t*>(xhI + (RR + n) * FCP + q * NSLP);
+#pragma unroll
+        for (int w = 0; w < NSLP / 2; ++w) xi32[w] = w < NW ? bw[w] : 0u;
+        if constexpr (!ODD) {
+          lds_order();
+          auto tr8 = [&](const unsigned short* img, int stride, int c0) {
+            const s16x4_t lo = tr_read(img + (8 * q + (n >> 2)) * stride + c0 + tcol);
+            const s16x4_t hi = tr_read(img + (8 * q + 4 + (n >> 2)) * stride + c0 + tcol);
+            return u16x8_t{(unsigned short)lo[0], (unsigned short)lo[1], (unsigned short)lo[2], (unsigned short)lo[3],
+                           (unsigned short)hi[0], (unsigned short)hi[1], (unsigned short)hi[2], (unsigned short)hi[3]};
+          };
+          u16x8_t fbx[FTA];
+#pragma unroll
+          for (int b = 0; b < FTA; ++b) fbx[b] = tr8(xhI, FCP, 16 * b);
+#pragma unroll
+          for (int a = 0; a < GT; ++a) {
+            const u16x8_t fa = tr8(dgI, GCP, 16 * a);
+#pragma unroll
+            for (int b = 0; b < FTA; ++b) accw[a][b] = mfma_bf16(fa, fbx[b], accw[a][b]);
+          }
+          lds_order();
+        }
+      };
+      using T_ = std::true_type;
+      using F_ = std::false_type;
+#pragma unroll
+      for (int m = 0; m < U4; ++m)   // c of the first processed step
+        ccur[m] = (float)__builtin_bit_cast(
+            _Float16, (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + (U4 + m) * 128, tof(L - 1) * RSTEPB, 0));
+      int tau = L - 1;
+      if (tau % 2 == 0) {   // odd L: the first step (even tau) alone, completing the half-filled pair
+        Raw S0;
+        rload(tau, S0);
+        if (tau == 0) {
+          bstep(F_{}, F_{}, 0, S0);
+          tau = -1;
+        } else {
+          bstep(T_{}, F_{}, tau, S0);
+          tau -= 1;
+        }
+      }
+      if (tau >= 1) {   // tau odd: pairs (tau, tau - 1), ping-pong prefetch
+        Raw A, B;
+        rload(tau, A);
+        for (; tau >= 3; tau -= 2) {
+          rload(tau - 1, B);
+          __builtin_amdgcn_sched_barrier(0);
+          bstep(T_{}, T_{}, tau, A);
+          __builtin_amdgcn_sched_barrier(0);
+          rload(tau - 2, A);
+          __builtin_amdgcn_sched_barrier(0);
+          bstep(T_{}, F_{}, tau - 1, B);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        rload(0, B);
+        __builtin_amdgcn_sched_barrier(0);
+        bstep(T_{}, T_{}, 1, A);
+        __builtin_amdgcn_sched_barrier(0);
+        bstep(F_{}, F_{}, 0, B);
+      }
+    } else if constexpr (!BF16) {
     float xv[NX], hp[U4], cprev[U4], dhin[U4];
     {
       const int t = tof(L - 1), tp = tof(L >= 2 ? L - 2 : 0);
@@ -1327,13 +1544,15 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   using elem = typename FragT<BF16>::elem;
   dim3 grid(a.bwd_blocks, 2);
   size_t lds = lstm_bwd_lds_bytes(U, NX, BF16, a.L, a.PD);
-  auto kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true> : lstm_bwd_kernel<U, NX, BF16, false>;
+  // bf16 + lane-layout dH (rec_attn_bwd, premasked): the lean PM step
+  const bool pm = BF16 && a.dh_lane;
+  auto kfn = pm ? (a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, BF16> : lstm_bwd_kernel<U, NX, BF16, false, BF16>)
+                : (a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, false> : lstm_bwd_kernel<U, NX, BF16, false, false>);
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)lstm_bwd_kernel<U, NX, BF16, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
-    hipFuncSetAttribute((const void*)lstm_bwd_kernel<U, NX, BF16, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
+    for (auto f : {lstm_bwd_kernel<U, NX, BF16, true, false>, lstm_bwd_kernel<U, NX, BF16, false, false>,
+                   lstm_bwd_kernel<U, NX, BF16, true, BF16>, lstm_bwd_kernel<U, NX, BF16, false, BF16>})
+      hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   hipLaunchKernelGGL(kfn, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,

@@ -143,18 +143,22 @@ INA_DEVICE void rec_steps(int L, LD&& load, F&& step) {
 // to one branch per element): scale = keep bit * inv_kp (inv_kp = 1 and all bits set without
 // dropout, which reproduces h exactly).  Two values per call: packed bf16 pair (B operand word) and
 // the rounded fp32 values.
+// the DropoutWrapper scale of the lane's slot i: keep bit * inv_kp
+template <int U>
+INA_DEVICE float rec_scale(const RecStep<U>& s, int i, float inv_kp) {
+  constexpr int U4 = RA<U>::U4;
+  const int b = i < U4 ? i : 8 + i - U4;
+  return (float)((s.kb >> b) & 1u) * inv_kp;
+}
 template <int U>
 INA_DEVICE uint32_t rec_drop2(const RecStep<U>& s, int i, float inv_kp, float& v0, float& v1) {
-  constexpr int U4 = RA<U>::U4;
-  const int b0 = i < U4 ? i : 8 + i - U4, b1 = i + 1 < U4 ? i + 1 : 8 + i + 1 - U4;
-  const float x0 = bf2f(s.h[i]) * ((float)((s.kb >> b0) & 1u) * inv_kp);
-  const float x1 = bf2f(s.h[i + 1]) * ((float)((s.kb >> b1) & 1u) * inv_kp);
+  const float x0 = bf2f(s.h[i]) * rec_scale<U>(s, i, inv_kp);
+  const float x1 = bf2f(s.h[i + 1]) * rec_scale<U>(s, i + 1, inv_kp);
   const uint32_t w = (uint32_t)f2bf(x0) | ((uint32_t)f2bf(x1) << 16);
   v0 = __builtin_bit_cast(float, w << 16);
   v1 = __builtin_bit_cast(float, w & 0xFFFF0000u);
   return w;
 }
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
 INA_DEVICE u16x8_t tr8(const unsigned short* img, int stride, int c0, int q, int n) {
   const s16x4_t lo = tr_read(img + (8 * q + (n >> 2)) * stride + c0 + 4 * (n & 3));
@@ -282,7 +286,9 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
 // tokens: sd = sum_t alpha_t d(alpha)_t = de . sum_t alpha_t H_t = de . e (the forward's output), so
 // no separate d(alpha) pass; per step
 //   recompute P, d(alpha)_t = de . H_t, ds_t = alpha_t (d(alpha)_t - sd), dP = ds w2 (1 - P^2),
-//   dH_t = W1 dP_t + alpha_t de -> dHl [tiles][2][L][u/4][64] bf16 (lstm_bwd's lane layout),
+//   dH_t = W1 dP_t + alpha_t de -> dHl [tiles][2][L][u/4][64] bf16 (lstm_bwd's lane layout), already
+//   multiplied by the DropoutWrapper scale (keep bit * 1/keep_prob): the gradient w.r.t. the LSTM's
+//   own output h, so lstm_bwd needs neither the keep bits nor a per-step mask,
 //   dW1 += H^T dP (MFMAs per step pair), db1 += dP, dw2 += ds P (fp32: sum_t ds_t = 0 per sequence,
 //   so these sums cancel heavily -- bf16 dP through the MFMA measured 1e-2 relative error on db1)
 // slab per workgroup: [dW1 (H2*H2, row i, col j) | db1 (H2) | dw2 (H2)], the attn_bwd layout.
@@ -427,7 +433,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3
           const int fi = 4 * T + r;
           if (fi < NV) {
             const int dd = fi / U4, m = fi % U4;
-            d0[((size_t)dd * L + t) * U4 * 64 + m * 64] = f2bf(acc[r] + alv * dev[fi]);
+            d0[((size_t)dd * L + t) * U4 * 64 + m * 64] = f2bf((acc[r] + alv * dev[fi]) * rec_scale<U>(cur, fi, inv_kp));
           }
         }
       }

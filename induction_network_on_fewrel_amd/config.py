@@ -116,6 +116,9 @@ class Config:
     test_best: bool = False            # final test from the best-val checkpoint (reference: the last weights)
     grad_check_finite: bool = True     # NaN/Inf guard on the loss
     profile: bool = False              # per-phase GPU time (HIP events) into metrics.jsonl at log points
+    # optimize_loss summaries (model/base.py:98,113; tf.contrib.layers.optimize_loss's default list is
+    # loss, learning_rate, global_gradient_norm); add "gradient_norm" for one norm per variable
+    summaries: str = "loss,learning_rate,global_gradient_norm"
     watchdog_s: float = 0.0            # abort (traceback + exit) if one train step takes longer (0 = off)
     save_every: int = 0                # periodic checkpoints for restart-resume (reference: best-val only)
 

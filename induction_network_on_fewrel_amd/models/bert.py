@@ -3,7 +3,8 @@
 The reference has no BERT (its encoder is the BiLSTM of model/graph.py:30-53); this module adds the
 "FewRel 10-way 5-shot with BERT-base encoder" configuration of BASELINE.json.  Architecture =
 BERT (post-LN transformer, GELU FFN) with HuggingFace parameter names and layouts (Linear weights
-``[out, in]``), so a local HF checkpoint directory can be loaded by name (``load_hf_state``).
+``[out, in]``), so a local HF checkpoint directory (``Config.bert_checkpoint``) is loaded by name
+(``load_hf_state``; pinned to ``transformers.BertModel`` by tests/test_bert.py).
 The sentence vector is pooled at the entity-start markers (concat of the [E1] and [E2] states) or
 at [CLS], then projected to ``bert_out_dim`` -- the width the induction (routing) and relation
 (NTN) heads run at (their fused kernels are instantiated for H in {16, 40, 64}).
@@ -130,6 +131,13 @@ def attention(q, k, v, mask, nh: int, seed: int, stream: int, p: float, training
 def encode_ref(p: Dict[str, torch.Tensor], ids, mask, e1, e2, cfg, training: bool = False,
                seed: int = 0) -> torch.Tensor:
     """Pure-PyTorch BERT encoder + pooling + projection -> [S, bert_out_dim] (fp32)."""
+    x = hidden_states_ref(p, ids, mask, cfg, training, seed)
+    return pool_project(p, x, e1, e2, cfg.bert_pool)
+
+
+def hidden_states_ref(p: Dict[str, torch.Tensor], ids, mask, cfg, training: bool = False,
+                      seed: int = 0) -> torch.Tensor:
+    """The encoder's last hidden states [S, L, Hd] (HF ``BertModel(...).last_hidden_state``)."""
     S, L = ids.shape
     pd, ad = cfg.bert_dropout, cfg.bert_attn_dropout
     e = "bert.embeddings."
@@ -151,7 +159,7 @@ def encode_ref(p: Dict[str, torch.Tensor], ids, mask, e1, e2, cfg, training: boo
         o = h @ p[pre + "output.dense.weight"].t() + p[pre + "output.dense.bias"]
         o = _dropout(o, seed, 19 + 3 * i, pd, training)
         x = layer_norm(x + o, p[pre + "output.LayerNorm.weight"], p[pre + "output.LayerNorm.bias"])
-    return pool_project(p, x, e1, e2, cfg.bert_pool)
+    return x
 
 
 def pool_project(p, x, e1, e2, pool: str) -> torch.Tensor:
@@ -166,3 +174,69 @@ def pool_project(p, x, e1, e2, pool: str) -> torch.Tensor:
 
 def hf_names(cfg) -> List[str]:
     return [n for n in param_specs(cfg) if n.startswith("bert.")]
+
+
+# ------------------------------------------------------------------ HF checkpoint import
+def read_hf_checkpoint(path: str) -> Dict[str, torch.Tensor]:
+    """Tensors of a LOCAL HuggingFace checkpoint: a directory holding ``model.safetensors`` (or sharded
+    ``model-*.safetensors``) or ``pytorch_model.bin``, or one such file.  Nothing that executes code
+    is used: safetensors, or ``torch.load(weights_only=True)``."""
+    import glob
+    import os
+    from safetensors.torch import load_file
+    if os.path.isdir(path):
+        st = sorted(glob.glob(os.path.join(path, "model*.safetensors")))
+        if st:
+            out: Dict[str, torch.Tensor] = {}
+            for f in st:
+                out.update(load_file(f))
+            return out
+        binf = os.path.join(path, "pytorch_model.bin")
+        if not os.path.exists(binf):
+            raise FileNotFoundError(f"no model*.safetensors or pytorch_model.bin in {path}")
+        path = binf
+    if path.endswith(".safetensors"):
+        return load_file(path)
+    return torch.load(path, map_location="cpu", weights_only=True)
+
+
+def hf_key_map(keys) -> Dict[str, str]:
+    """checkpoint key -> our parameter name (``bert.`` prefixed HF names).  Accepts BertModel keys
+    (``embeddings.*``, ``encoder.*``), task-model keys (``bert.*``) and the TF-converted LayerNorm
+    names (``gamma`` / ``beta``); pooler / task-head keys are ignored."""
+    out = {}
+    for k in keys:
+        n = k if k.startswith("bert.") else "bert." + k
+        n = n.replace("LayerNorm.gamma", "LayerNorm.weight").replace("LayerNorm.beta", "LayerNorm.bias")
+        if n.startswith(("bert.embeddings.", "bert.encoder.")):
+            out[k] = n
+    return out
+
+
+def load_hf_state(params, path: str, cfg, strict: bool = True) -> List[str]:
+    """Copy a local HF BERT checkpoint into ``params`` (models/params.py InductionParams, BERT mode).
+    Every encoder tensor of our parameter table must be present with the same shape (``strict``), except
+    that a checkpoint with more position embeddings than ``bert_max_position`` is cut to that length.
+    The projection to ``bert_out_dim`` (``bert_proj/*``) is not part of BERT and keeps its init.
+    Returns the loaded parameter names."""
+    src = read_hf_checkpoint(path)
+    km = hf_key_map(src.keys())
+    by_name = {v: k for k, v in km.items()}
+    loaded = []
+    with torch.no_grad():
+        for name in hf_names(cfg):
+            dst = getattr(params, attr_of(name))
+            if name not in by_name:
+                if strict:
+                    raise KeyError(f"BERT checkpoint {path} has no tensor for {name}")
+                continue
+            t = src[by_name[name]]
+            if name.endswith("position_embeddings.weight") and t.shape[0] > dst.shape[0]:
+                t = t[: dst.shape[0]]
+            if tuple(t.shape) != tuple(dst.shape):
+                raise ValueError(f"BERT checkpoint {name}: shape {tuple(t.shape)} vs model {tuple(dst.shape)} "
+                                 "(set bert_hidden / bert_layers / bert_heads / bert_intermediate / bert_vocab "
+                                 "to the checkpoint's config)")
+            dst.copy_(t.to(dst.device, dst.dtype))
+            loaded.append(name)
+    return loaded

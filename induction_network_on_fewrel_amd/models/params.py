@@ -113,6 +113,8 @@ class InductionParams(nn.Module):
                 a = B.attr_of(name)
                 setattr(self, a, nn.Parameter(B.init_tensor(shape, kind, gen)))
                 self._names[a] = name
+            if cfg.bert_checkpoint:   # a local HF checkpoint (safetensors / weights-only torch file)
+                B.load_hf_state(self, cfg.bert_checkpoint, cfg)
             H = cfg.bert_out_dim
             self.word_dim = cfg.bert_hidden
             self.input_dim = cfg.bert_hidden

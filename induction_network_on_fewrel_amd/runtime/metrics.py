@@ -1,7 +1,9 @@
 """Structured metrics: JSONL + a dependency-free TensorBoard event-file writer.
 
 Reference (model/base.py:109-113,125,155): scalar summaries ``loss``, ``accuracy``, ``learning_rate``
-written every train step to ``<model_dir>/train`` via ``tf.summary.FileWriter``. TensorBoard is not
+written every train step to ``<model_dir>/train`` via ``tf.summary.FileWriter``, merged with the
+summaries ``optimize_loss`` registers (model/base.py:98,113: ``global_norm/gradient_norm``, and per
+variable ``gradient_norm/<var>`` when asked for; Config.summaries). TensorBoard is not
 installed here, so the event file is produced directly: TFRecord framing (length, masked CRC32C of
 the length, payload, masked CRC32C of the payload) around hand-encoded ``Event`` protos
 (wall_time=1:double, step=2:int64, file_version=3:string, summary=5:{value=1:{tag=1, simple_value=2}}).
@@ -164,6 +166,9 @@ def _parse_event(b: bytes):
     return step, vals
 
 
+TB_PREFIXES = ("global_norm/", "gradient_norm/")   # optimize_loss's gradient summaries
+
+
 class MetricsLogger:
     """Rank-0 JSONL (``<model_dir>/train/metrics.jsonl``) + TensorBoard events + stdout."""
 
@@ -186,7 +191,8 @@ class MetricsLogger:
         rec.update({k: (float(v) if isinstance(v, (int, float)) else v) for k, v in values.items()})
         self.jsonl.write(json.dumps(rec) + "\n")
         if self.tb is not None and kind == "train":
-            self.tb.scalars(step, {k: v for k, v in values.items() if k in ("loss", "accuracy", "learning_rate")})
+            self.tb.scalars(step, {k: v for k, v in values.items()
+                                   if k in ("loss", "accuracy", "learning_rate") or k.startswith(TB_PREFIXES)})
 
     def print(self, msg: str) -> None:
         if self.enabled and self.stdout:

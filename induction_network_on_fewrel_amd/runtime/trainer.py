@@ -151,6 +151,26 @@ class Trainer:
         self._pending_events = []
         return dict(self.gpu_phase_ms)
 
+    def gradient_norms(self, per_variable: bool = False) -> "OrderedDict[str, float]":
+        """optimize_loss's gradient summaries from the flat gradient of the last step (read at log points
+        only): ``global_norm/gradient_norm`` (one device reduction) and, with ``per_variable``,
+        ``gradient_norm/<TF variable name>`` (one segmented reduction).  Under DP the buffer holds the
+        all-reduced SUM; the norms are of the applied (1/world-scaled) gradient."""
+        g = self.flat.grad.detach().float()
+        scale = 1.0 / self.dist.world
+        out = OrderedDict()
+        sq = g * g
+        if per_variable:
+            lens = torch.tensor(self.flat.numels, device=g.device)
+            seg = torch.segment_reduce(sq, "sum", lengths=lens)
+            vals = (seg.sqrt() * scale).tolist()
+            out["global_norm/gradient_norm"] = float(sum(v * v for v in vals)) ** 0.5
+            for n, v in zip(self.flat.names, vals):
+                out["gradient_norm/" + self.model.params.tf_name(n)] = v
+        else:
+            out["global_norm/gradient_norm"] = float(sq.sum().sqrt()) * scale
+        return out
+
     @property
     def skipped_steps(self) -> int:
         """Optimizer steps skipped by the NaN/Inf guard (synchronises on the GPU)."""
@@ -293,8 +313,13 @@ class Trainer:
                 it_n += pend_n
                 pend_loss = pend_acc = None
                 pend_n = 0
+                summ = set(x.strip() for x in cfg.summaries.split(",") if x.strip())
+                norms = (self.gradient_norms("gradient_norm" in summ)
+                         if summ & {"global_gradient_norm", "gradient_norm"} else {})
+                if "global_gradient_norm" not in summ:
+                    norms.pop("global_norm/gradient_norm", None)
                 self.log.log(self.global_step, "train", loss=it_loss / it_n, accuracy=it_acc / it_n,
-                             learning_rate=self._last_lr)
+                             learning_rate=self._last_lr, **norms)
                 if cfg.profile and self.device.type == "cuda":
                     self.log.log(self.global_step, "profile", **{f"gpu_{k}_ms": v for k, v in
                                                                  self.drain_phase_events().items()},
@@ -410,9 +435,9 @@ class Trainer:
         map onto the new ranks: keep the fresh rank-folded seeds and only carry the call counter of the
         device sampler forward (new episodes, no replay of the pre-restart ones)."""
         states = meta.get("train_samplers")
-        if states is None:   # older single-state checkpoints: rank 0's state -> counter only
+        if states is None:   # older single-state checkpoints: rank 0's state; exact only at world size 1
             states = [meta["train_sampler"]] if "train_sampler" in meta else []
-            same_world = False
+            same_world = bool(states) and int(meta.get("world_size", 1)) == 1 and self.dist.world == 1
         else:
             same_world = len(states) == self.dist.world
         if same_world:

@@ -108,3 +108,63 @@ def test_synthetic_features_markers():
         assert f["ids"][i, 0] == 2 and f["ids"][i, f["length"][i] - 1] == 3
         assert f["ids"][i, f["e1"][i]] == 5 and f["ids"][i, f["e2"][i]] == 7
         assert f["ids"][i].max() < 100
+
+
+def _tiny_hf(tmp_path, fmt="safetensors", prefix=False):
+    """A random transformers.BertModel built offline from a tiny BertConfig, saved to a local dir."""
+    import os
+    import transformers
+    hc = transformers.BertConfig(vocab_size=600, hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
+                                 intermediate_size=512, max_position_embeddings=64, hidden_dropout_prob=0.0,
+                                 attention_probs_dropout_prob=0.0, hidden_act="gelu", layer_norm_eps=1e-12)
+    torch.manual_seed(11)
+    hf = transformers.BertModel(hc, add_pooling_layer=True).eval()
+    with torch.no_grad():   # non-trivial LayerNorm affine / biases
+        for n, t in hf.named_parameters():
+            if "LayerNorm" in n or n.endswith("bias"):
+                t.add_(torch.randn_like(t) * 0.1)
+    d = str(tmp_path / f"hf_{fmt}_{int(prefix)}")
+    if fmt == "safetensors":
+        hf.save_pretrained(d, safe_serialization=True)
+    else:
+        os.makedirs(d, exist_ok=True)
+        sd = {("bert." + k if prefix else k): v.clone() for k, v in hf.state_dict().items()}
+        torch.save(sd, os.path.join(d, "pytorch_model.bin"))
+    return hf, d
+
+
+def _hidden_vs_hf(hf, d):
+    cfg = Config(**dict(TINY, bert_checkpoint=d, bert_dropout=0.0, bert_attn_dropout=0.0))
+    m = InductionNetwork(cfg, None, vocab_size=10, seed=0)
+    g = torch.Generator().manual_seed(5)
+    ids = torch.randint(0, 600, (3, 32), generator=g)
+    mask = torch.ones(3, 32, dtype=torch.int64)
+    mask[1, 20:] = 0
+    mask[2, 7:] = 0
+    with torch.no_grad():
+        ours = B.hidden_states_ref(m.bert_pdict(), ids, mask, cfg)
+        ref_h = hf(input_ids=ids, attention_mask=mask).last_hidden_state
+    valid = mask.bool()
+    return float((ours - ref_h)[valid].abs().max()), float(ref_h[valid].abs().max())
+
+
+def test_bert_checkpoint_matches_hf_bertmodel(tmp_path):
+    """bert_checkpoint: a saved transformers.BertModel (model.safetensors) loads by name, and our
+    oracle encoder reproduces its last_hidden_state (dropout 0) -- the HF-layout claim, pinned."""
+    hf, d = _tiny_hf(tmp_path, "safetensors")
+    err, mx = _hidden_vs_hf(hf, d)
+    assert err < 2e-5 * max(1.0, mx), err
+
+
+def test_bert_checkpoint_torch_bin_with_prefix(tmp_path):
+    """pytorch_model.bin (weights_only load) with task-model ``bert.`` keys and a pooler to ignore."""
+    hf, d = _tiny_hf(tmp_path, "bin", prefix=True)
+    err, mx = _hidden_vs_hf(hf, d)
+    assert err < 2e-5 * max(1.0, mx), err
+
+
+def test_bert_checkpoint_shape_mismatch_is_loud(tmp_path):
+    import pytest
+    hf, d = _tiny_hf(tmp_path, "safetensors")
+    with pytest.raises(ValueError, match="shape"):
+        InductionNetwork(Config(**dict(TINY, bert_checkpoint=d, bert_intermediate=1024)), None, vocab_size=10)

@@ -133,3 +133,18 @@ def test_sampler_nota():
     s = EpisodeSampler(ds, seed=0, nota_rate=0.5)
     idx, lab = s.next_batch_indices(50, 5, 1, 5)
     assert 0.3 < (lab == 5).mean() < 0.7
+
+
+def test_convert_glove_cli(tmp_path):
+    """util/convert_glove_vec.py equivalent: first K dims, lower-cased words, glove.6B.<K>d.json name."""
+    import json
+    import subprocess
+    import sys
+    src = tmp_path / "glove.6B.50d.json"
+    json.dump([{"word": "The", "vec": [float(i) for i in range(50)]}, {"word": "cat", "vec": [1.0] * 50}],
+              open(src, "w"))
+    r = subprocess.run([sys.executable, "-m", "induction_network_on_fewrel_amd.data.convert_glove", "--input",
+                        str(src), "--dim", "5"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.load(open(tmp_path / "glove.6B.5d.json"))
+    assert out == [{"word": "the", "vec": [0.0, 1.0, 2.0, 3.0, 4.0]}, {"word": "cat", "vec": [1.0] * 5}]

@@ -151,6 +151,15 @@ def _lane_to_natural(x, S):
     return y.reshape(T * 16, L, 8 * U4)[:S]
 
 
+def _keep_natural(dm, S, L, U):
+    """dropout keep bytes [tiles, 2, L, 64] (bit m of lane (q, n) = unit 4m + q) -> [S, L, 2U] 0/1."""
+    U4 = U // 4
+    d = dm.reshape(-1, 2, L, 4, 16).long()
+    bits = torch.stack([(d >> m) & 1 for m in range(U4)], -1)       # tile, dir, t, q, n, m
+    y = bits.permute(0, 4, 2, 1, 5, 3)                               # tile, n, t, dir, m, q
+    return y.reshape(-1, L, 2 * U)[:S].float()
+
+
 def _rec_problem(keep_prob, tail, u=20):
     from induction_network_on_fewrel_amd.ops import ops
     from induction_network_on_fewrel_amd.ops.packing import lstm_shape, pack_attn, pack_attn_rec, pack_lstm
@@ -211,6 +220,9 @@ def test_rec_attention_backward_matches_natural(keep_prob, tail, u):
     dHl, s1 = ops().rec_attn_bwd(hl, dm, P["rpacks"][0], P["rpacks"][1], P["b1"], P["w2"], de, e, a, U, keep_prob, 0)
     torch.cuda.synchronize()
     dH1 = _lane_to_natural(dHl, inst.shape[0])
+    # rec_attn_bwd returns the gradient w.r.t. the LSTM output h (DropoutWrapper keep / keep_prob applied)
+    L = dHl.shape[2]
+    dH0 = dH0.float() * (_keep_natural(dm, inst.shape[0], L, U) / keep_prob if keep_prob < 1.0 else 1.0)
     err = _relerr(dH1.float(), dH0.float())
     g0, g1 = s0.sum(0), s1.sum(0)
     H2 = 2 * U

@@ -195,3 +195,46 @@ def test_fault_injection_then_resume(tmp_path):
     assert r.returncode == 0, r.stderr
     assert "resumed from" in r.stdout and "inductionNetwork-4" in r.stdout
     assert "Test accuracy" in r.stdout
+
+
+def test_gradient_norm_summaries(tmp_path):
+    """optimize_loss's gradient summaries (model/base.py:98,113): the global norm of the last step's
+    gradient and, on request, one norm per TF variable -- in metrics.jsonl and the TensorBoard file."""
+    import glob
+    import json
+    from induction_network_on_fewrel_amd.runtime.trainer import Trainer
+    data = make_synthetic(num_relations=10, instances_per_relation=40, vocab=500, seed=0)
+    cfg = Config(N=5, K=2, Q=3, episodes_per_step=2, model_dir=str(tmp_path / "run"), seed=3, resume=False,
+                 train_iter=3, val_step=1000, test_iter=2, log_every=1,
+                 summaries="loss,learning_rate,global_gradient_norm,gradient_norm")
+    tr = Trainer(cfg, data, None, device="cpu", log=True)
+    tr.train_step()
+    norms = tr.gradient_norms(per_variable=True)
+    g = tr.flat.grad
+    assert abs(norms["global_norm/gradient_norm"] - float(g.norm())) < 1e-4 * float(g.norm())
+    ms = tr.flat.view(g, "M")
+    assert abs(norms["gradient_norm/M"] - float(ms.norm())) < 1e-3 * float(ms.norm())
+    assert "gradient_norm/bidirectional_rnn/fw/basic_lstm_cell/kernel" in norms
+    tr.train()
+    recs = [json.loads(x) for x in open(tmp_path / "run" / "train" / "metrics.jsonl")]
+    tr_recs = [r for r in recs if r["kind"] == "train"]
+    assert tr_recs and all("global_norm/gradient_norm" in r and "gradient_norm/M" in r for r in tr_recs)
+    ev = read_events(glob.glob(str(tmp_path / "run" / "train" / "events.out.tfevents.*"))[0])
+    tags = set().union(*(v.keys() for _, v in ev))
+    assert {"loss", "learning_rate", "global_norm/gradient_norm", "gradient_norm/M"} <= tags
+
+
+def test_legacy_single_sampler_checkpoint_resumes_exactly(tmp_path):
+    """Advisor finding: an older checkpoint with one 'train_sampler' entry must restore the CPU
+    sampler's RNG in full at world size 1 (not restart it and replay episodes)."""
+    import json
+    tr = _trainer(tmp_path, resume=False)
+    tr.train_step()
+    stem = tr.save()
+    cont = tr.train_eps.sample(4, 5, 2, 3)[0]
+    idx = stem + ".index.json"
+    meta = json.load(open(idx))
+    meta["train_sampler"] = meta.pop("train_samplers")[0]   # the pre-DP checkpoint format
+    json.dump(meta, open(idx, "w"))
+    tr2 = _trainer(tmp_path, resume=True)
+    assert torch.equal(tr2.train_eps.sample(4, 5, 2, 3)[0], cont)
