@@ -109,6 +109,11 @@ def main():
                     help="eval: forward-only episodic evaluation (FewRel 2.0 style, dropout off, accuracy "
                          "computed); a step = one batch of --episodes-per-gpu episodes (default 16384)")
     ap.add_argument("--nota", type=float, default=0.0, help="eval: none-of-the-above query rate (FewRel 2.0)")
+    ap.add_argument("--ragged", type=int, default=1,
+                    help="length-sorted ragged tiles (forward direction + attention stop at each tile's longest "
+                         "length; exact)")
+    ap.add_argument("--skip-padding", type=int, default=0,
+                    help="lstm_skip_padding: TF sequence_length semantics (NOT the reference's full-L BiLSTM)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: the oracle path (launcher / plumbing tests only; not a benchmark)")
     ap.add_argument("--launch-timeout", type=float, default=1500.0,
@@ -136,7 +141,8 @@ def main():
     cfg = Config(N=args.way, K=args.shot, Q=args.query, max_length=37, hidden_size=args.hidden, dtype=args.dtype,
                  episodes_per_step=B, seed=1234, resume=False, model_dir="/tmp/ina_bench",
                  train_iter=args.steps + args.warmup, use_hip_graph=bool(args.graph) and not bert and not evalm,
-                 nota_rate=args.nota, eval_batch=B)
+                 nota_rate=args.nota, eval_batch=B, ragged_tiles=bool(args.ragged),
+                 lstm_skip_padding=bool(args.skip_padding))
     if bert:
         cfg = cfg.replace(encoder="bert", bert_layers=args.bert_layers, bert_max_length=args.bert_len,
                           relation_head="reference")
@@ -207,6 +213,8 @@ def main():
                 "sentences_per_step_per_gpu": B * args.way * (args.shot + args.query),
                 "parallelism": f"dp{world}",
                 "mode": args.mode + (f", nota_rate={args.nota}" if evalm else ""),
+                "lstm": ("sequence_length (lstm_skip_padding)" if args.skip_padding else
+                         "full-L parity" + (", ragged tiles" if args.ragged else "")),
             },
             ("eval_accuracy" if evalm else "final_loss"): round(loss, 6),
             "params_in_sync": bool(in_sync),

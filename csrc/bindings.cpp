@@ -49,6 +49,14 @@ int* guard_skips(const std::optional<Tensor>& guard, const std::optional<Tensor>
   return skips->data_ptr<int>();
 }
 
+// ragged-tile arrays (ops/encoder.py): int32 device vectors of an exact length, or absent
+const int* ragged_arg(const std::optional<Tensor>& t, int64_t n, const char* name) {
+  if (!t.has_value() || !t->defined() || t->numel() == 0) return nullptr;
+  check(*t, name, at::kInt);
+  TORCH_CHECK(t->numel() == n, "ina: ", name, " must have ", n, " elements, got ", t->numel());
+  return t->data_ptr<int>();
+}
+
 int64_t frag_elems(bool bf16) { return bf16 ? 8 : 1; }
 uint32_t keep_threshold(double kp) {
   const double t = kp * 4294967296.0;
@@ -66,7 +74,8 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd_impl(
     const Tensor& inst, const Tensor& word, const Tensor& pos1, const Tensor& pos2, const Tensor& wemb,
     const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U, int64_t NX, bool bf16,
     bool store_c, int64_t seed, double keep_prob, const std::optional<Tensor>& seed_dev,
-    const std::optional<Tensor>& wrows, bool natural) {
+    const std::optional<Tensor>& wrows, bool natural, const std::optional<Tensor>& tlen = std::nullopt,
+    const std::optional<Tensor>& slen = std::nullopt) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -142,6 +151,10 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd_impl(
     TORCH_CHECK(wrows->numel() == word.numel() * 8 && E <= 8, "ina.lstm_fwd: wrows must be bf16 [NI * L, 8] (E <= 8)");
     a.wrows = wrows->data_ptr();
   }
+  a.tlen = ragged_arg(tlen, ntiles, "tlen");
+  a.slen = ragged_arg(slen, S, "slen");
+  TORCH_CHECK(!a.tlen || (bf16 && !natural), "ina.lstm_fwd: ragged tiles need the bf16 record path");
+  TORCH_CHECK(!a.slen || a.tlen, "ina.lstm_fwd: slen needs tlen");
   if (bf16) {
     a.xg = xg.data_ptr();
     a.posb = reinterpret_cast<const unsigned short*>(xg.data_ptr<at::BFloat16>() + ntiles * L * 64 * NX);
@@ -173,7 +186,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> lstm_attn_fwd
     const Tensor& inst, const Tensor& word, const Tensor& pos1, const Tensor& pos2, const Tensor& wemb,
     const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U, int64_t NX,
     bool store_c, int64_t seed, double keep_prob, const std::optional<Tensor>& seed_dev,
-    const std::optional<Tensor>& wrows, const Tensor& mask, const Tensor& w1r, const Tensor& b1, const Tensor& w2) {
+    const std::optional<Tensor>& wrows, const Tensor& mask, const Tensor& w1r, const Tensor& b1, const Tensor& w2,
+    const std::optional<Tensor>& tlen, const std::optional<Tensor>& perm, const std::optional<Tensor>& slen) {
   check(mask, "mask", at::kInt);
   check(w1r, "w1r", at::kBFloat16);
   check(b1, "b1", at::kFloat);
@@ -186,7 +200,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> lstm_attn_fwd
   TORCH_CHECK(w1r.numel() == MT * NKR * 64 * 8, "ina.lstm_attn_fwd: w1r pack size");
   const bool drop = keep_prob < 1.0;
   auto r = lstm_fwd_impl(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, bias, U, NX, true, store_c, seed, keep_prob,
-                         seed_dev, wrows, false);
+                         seed_dev, wrows, false, tlen, slen);
   auto e = at::empty({S, 2 * U}, b1.options());
   auto alphas = at::empty({S, L}, b1.options());
   if (S == 0) return {std::get<0>(r), std::get<1>(r), std::get<2>(r), std::get<3>(r), std::get<4>(r), e, alphas};
@@ -204,6 +218,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> lstm_attn_fwd
   a.w2 = w2.data_ptr<float>();
   a.e = e.data_ptr<float>();
   a.alphas = alphas.data_ptr<float>();
+  a.tlen = ragged_arg(tlen, (S + 15) / 16, "tlen");
+  a.perm = ragged_arg(perm, S, "perm");
   check_launch(ina::rec_attn_fwd(hlane.data_ptr(), drop ? dmask.data_ptr<uint8_t>() : nullptr, (float)(1.0 / keep_prob),
                                  a, (int)U, cur_stream()),
                "rec_attn_fwd");
@@ -216,7 +232,8 @@ bool rec_attn_ok(int64_t U, int64_t L) { return (U == 8 || U == 20 || U == 32) &
 // lstm_bwd's lane layout, slab [blocks, H2*H2 + 2*H2] in attn_bwd's layout)
 std::tuple<Tensor, Tensor> rec_attn_bwd(const Tensor& hlane, const Tensor& dmask, const Tensor& w1r, const Tensor& w1rt,
                                         const Tensor& b1, const Tensor& w2, const Tensor& de, const Tensor& e,
-                                        const Tensor& alphas, int64_t U, double keep_prob, int64_t blocks) {
+                                        const Tensor& alphas, int64_t U, double keep_prob, int64_t blocks,
+                                        const std::optional<Tensor>& tlen, const std::optional<Tensor>& perm) {
   check(hlane, "hlane", at::kBFloat16);
   check(e, "e", at::kFloat);
   check(w1r, "w1r", at::kBFloat16);
@@ -260,6 +277,8 @@ std::tuple<Tensor, Tensor> rec_attn_bwd(const Tensor& hlane, const Tensor& dmask
   a.dHraw = dH.data_ptr();
   a.slab = slab.data_ptr<float>();
   a.blocks = (int)blocks;
+  a.tlen = ragged_arg(tlen, ntiles, "tlen");
+  a.perm = ragged_arg(perm, S, "perm");
   check_launch(ina::rec_attn_bwd(hlane.data_ptr(), drop ? dmask.data_ptr<uint8_t>() : nullptr, (float)(1.0 / keep_prob),
                                  a, (int)U, cur_stream()),
                "rec_attn_bwd");
@@ -272,7 +291,8 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
                                             const Tensor& bias, const Tensor& hraw, const Tensor& cst, const Tensor& dH,
                                             const Tensor& dmask, const Tensor& xg, int64_t U, int64_t NX, bool bf16,
                                             bool word_grad, int64_t blocks, int64_t seed, double keep_prob,
-                                            bool pos_shift) {
+                                            bool pos_shift, const std::optional<Tensor>& tlen,
+                                            const std::optional<Tensor>& slen) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -364,6 +384,10 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   a.drop = keep_prob < 1.0 ? 1 : 0;
   a.dxp = bf16 ? dxp.data_ptr() : nullptr;
   a.dh_lane = dh_lane ? 1 : 0;
+  a.tlen = ragged_arg(tlen, ntiles, "tlen");
+  a.slen = ragged_arg(slen, S, "slen");
+  TORCH_CHECK(!a.tlen || (bf16 && dh_lane), "ina.lstm_bwd: ragged tiles need the bf16 lane-layout dH path");
+  TORCH_CHECK(!a.slen || a.tlen, "ina.lstm_bwd: slen needs tlen");
   a.xg = bf16 ? xg.data_ptr() : nullptr;
   a.posb = bf16 ? reinterpret_cast<const unsigned short*>(xg.data_ptr<at::BFloat16>() + ntiles * L * 64 * NX)
                 : nullptr;
@@ -715,7 +739,7 @@ void step_control(Tensor ctl, Tensor lrt, int64_t seedA, int64_t seedB, double l
                "step_control");
 }
 
-int64_t abi_version() { return 5; }
+int64_t abi_version() { return 6; }
 
 }  // namespace
 

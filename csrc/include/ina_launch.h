@@ -40,6 +40,12 @@ struct LstmArgs {
   float inv_kp;
   int drop;
   int dh_lane;           // bwd: dH in the step-record lane layout [tiles][2][L][U/4][64] (else [S][L][2U])
+  // ragged tiles (bf16 record path; rows sorted by length on the host, ops/encoder.py): tlen[tile] = the
+  // tile's longest valid length.  The forward direction and the attention stop there (padding outputs are
+  // masked: exact); the backward direction runs all L steps (parity) or, with slen (the sorted rows'
+  // lengths; lstm_skip_padding), starts at tlen - 1 and resets each row's state past its own length
+  const int* tlen;
+  const int* slen;
 };
 // bf16 mode: gather every token's x features once into a.xg / a.posb, and (a.drop) the dropout keep
 // bits into a.dmask (lstm.hip x_gather_kernel); must run before lstm_fwd in bf16 mode
@@ -75,6 +81,8 @@ struct AttnArgs {
   void* dHraw;      // bf16 mode: bf16; fp32 mode: fp32
   float* slab;
   int blocks;
+  const int* tlen;  // rec_attn: per-tile step count (ragged tiles; nullptr = L)
+  const int* perm;  // rec_attn: row s of the (length-sorted) records is row perm[s] of e / alphas / de
 };
 int attn_fwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st);
 int attn_bwd(const AttnArgs& a, int U, int NT, bool bf16, hipStream_t st);

@@ -24,6 +24,9 @@ using namespace ina;
 #ifndef INA_FWD_PIPE
 #define INA_FWD_PIPE 1
 #endif
+#ifndef INA_LSTM_PM
+#define INA_LSTM_PM 1   // 0: timing-only A/B build -- lane-layout dH through the generic step (double-masked)
+#endif
 namespace {
 
 template <int U, int NX, bool BF16>
@@ -257,7 +260,9 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
 // ------------------------------------------------------------------------------------------
 // DROP / STORE are compile-time so the step loop has no branches: the waitcnt pass can then count
 // the stores issued after each prefetch and wait only for the prefetched loads.
-template <int U, int NX, bool BF16, bool DROP, bool STORE>
+// SKIP (bf16): sequence_length semantics for the backward direction (lstm_skip_padding): it starts at the
+// tile's longest length and each row's state is reset to zero past its own length (TF dynamic_rnn)
+template <int U, int NX, bool BF16, bool DROP, bool STORE, bool SKIP = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void lstm_fwd_kernel(
     const int* __restrict__ inst, int S, const int* __restrict__ word, const int* __restrict__ pos1,
     const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
@@ -265,7 +270,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     const typename FragT<BF16>::type* __restrict__ apack, const float* __restrict__ bias,
     typename FragT<BF16>::elem* __restrict__ hlane, typename CT<BF16>::type* __restrict__ cst,
     typename FragT<BF16>::elem* __restrict__ hnat, unsigned char* __restrict__ dmask, uint32_t seed, uint32_t thr,
-    float inv_kp, int drop, const int* __restrict__ seed_dev, const unsigned short* __restrict__ xg) {
+    float inv_kp, int drop, const int* __restrict__ seed_dev, const unsigned short* __restrict__ xg,
+    const int* __restrict__ tlen, const int* __restrict__ slen) {
   if (seed_dev) seed = (uint32_t)seed_dev[0];   // device-resident dropout seed (HIP-graph replay)
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
@@ -297,6 +303,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   if (tile >= ntiles) return;
   const int seq = tile * 16 + n;  // rows >= S are padding rows of hnat (allocated to 16 * ntiles)
   const uint32_t salt = dropout_salt(seed, (uint32_t)dir);
+  // ragged tiles: processing steps [tb, te).  Forward direction: t < Lt (the tile's longest length; later
+  // outputs are masked out of the attention and its final state is unused).  Backward direction: all L
+  // (parity: it runs through the padding first), or t < Lt with per-row resets (SKIP).
+  const int Lt = tlen ? tlen[tile] : L;
+  const int tb = (SKIP && dir == 1) ? L - Lt : 0, te = dir == 0 ? Lt : L;
+  const int mylen = SKIP ? (seq < S ? slen[seq] : 0) : L;
 
   frag A[NMT][NKS];
   const frag* ap = apack + (size_t)dir * NMT * NKS * 64;
@@ -362,6 +374,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
       float hv = tanh_l2(c[m] * (2.f * LOG2E_F)) * og;
       if (BF16) hv = round_bf(hv);  // the stored / recurrent operand value
       h[m] = hv;
+    }
+    if constexpr (SKIP) {   // backward direction past the row's length: state (and output) reset to zero
+      if (dir == 1 && t >= mylen) {
+#pragma unroll
+        for (int m = 0; m < U4; ++m) h[m] = c[m] = 0.f;
+      }
     }
     if constexpr (BF16) {
       // bf16 step record [tile][dir][t][2][U4][64] (16-bit): slot 0 = the raw recurrent h (bf16), slot 1
@@ -459,19 +477,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
       __builtin_amdgcn_sched_barrier(0);
       step_raw(tau, ra);
       __builtin_amdgcn_sched_barrier(0);
-      load_raw(tof(min(tau + 2, L - 1)), ra);
+      load_raw(tof(min(tau + 2, te - 1)), ra);
       __builtin_amdgcn_sched_barrier(0);
       step_raw(tau + 1, rb);
       __builtin_amdgcn_sched_barrier(0);
     };
-    load_raw(tof(0), ra);
-    int tau = 0;
-    if (L >= 2) {
-      rpair(0);
-      tau = 2;
+    load_raw(tof(tb), ra);
+    int tau = tb;
+    if (te - tb >= 2) {
+      rpair(tb);
+      tau = tb + 2;
     }
-    for (; tau + 1 < L; tau += 2) rpair(tau);
-    if (tau < L) step_raw(tau, ra);
+    for (; tau + 1 < te; tau += 2) rpair(tau);
+    if (tau < te) step_raw(tau, ra);
     return;
   }
   float xa[NX], xb[NX];
@@ -591,7 +609,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     float* __restrict__ dw_slab,
     float* __restrict__ dpos_slab, float* __restrict__ dwemb, const unsigned char* __restrict__ dmask, uint32_t seed,
     uint32_t thr, float inv_kp, int drop, unsigned short* __restrict__ dxp, const unsigned short* __restrict__ xg,
-    int dh_lane) {
+    int dh_lane, const int* __restrict__ tlen, const int* __restrict__ slen) {
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
   using elem = typename FragT<BF16>::elem;
@@ -726,7 +744,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     float dh_rec[U4], dc_rec[U4];
 #pragma unroll
     for (int m = 0; m < U4; ++m) dh_rec[m] = dc_rec[m] = 0.f;
-    if (L & 1) {
+    if (!(BF16 && PM) && (L & 1)) {
       // odd L: the tile's first dW chunk {L, L-1} is half filled; clear the dG samples of the missing
       // step (they still hold the previous tile's last chunk)
       if constexpr (BF16) {
@@ -907,8 +925,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       const uint32_t RSTEPB = 2 * U4 * 64 * 2, DSTEPB = U4 * 64 * 2, XSTEPB = 64 * NX * 2, PSTEPB = (NPF + 1) * 16 * 2;
       const auto rrec = rsrc(reinterpret_cast<const unsigned short*>(hraw) + ((size_t)tu * 2 + dir) * L * 2 * U4 * 64,
                              (uint32_t)L * RSTEPB);
+      // ragged tiles: the tile's steps [0, Lt) carry attention gradient; the descriptor's range ends there,
+      // so dH loads past it return 0 (the backward direction's padding steps in parity mode)
+      const int Lt = tlen ? tlen[tu] : L;
       const auto rdh = rsrc(reinterpret_cast<const unsigned short*>(dH) + ((size_t)tu * 2 + dir) * L * U4 * 64,
-                            (uint32_t)L * DSTEPB);
+                            (uint32_t)Lt * DSTEPB);
+      const bool lane_reset = slen != nullptr && dir == 1;   // sequence_length semantics (backward direction)
+      const int mylen = slen != nullptr ? (valid ? slen[seq] : 0) : L;
       const auto rx = rsrc(xg + (size_t)tu * L * 64 * NX, (uint32_t)L * XSTEPB);
       const auto rdx = rsrc(dxp + ((size_t)dir * ntiles + tu) * L * (NPF + 1) * 16, (uint32_t)L * PSTEPB);
       const int vl2 = lane * 2, vx = lane * NX * 2;
@@ -938,10 +961,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         const bf2_t v = {(__bf16)a, (__bf16)b};
         return __builtin_bit_cast(uint32_t, v);
       };
-      // HASP: the step has a predecessor (tau >= 1; else h_{-1} = c_{-1} = 0).  ODD: tau is odd (image
-      // rows 16..31); an even step completes the pair {tau + 1, tau} and flushes it into dW.
-      auto bstep = [&](auto hasp_c, auto odd_c, const int tau, const Raw& X0) __attribute__((always_inline)) {
-        constexpr bool HASP = decltype(hasp_c)::value, ODD = decltype(odd_c)::value;
+      // HASP: the step has a predecessor state (else it is zero: the direction's first step in time, or the
+      // SKIP backward direction's tile start).  HI: the step stages into image rows 16..31 and completes
+      // the pair (rows 0..15 = the previous step), FLUSH: the pair goes into dW after staging.
+      auto bstep = [&](auto hasp_c, auto hi_c, auto flush_c, const int tau, const Raw& X0) __attribute__((always_inline)) {
+        constexpr bool HASP = decltype(hasp_c)::value, ODD = decltype(hi_c)::value, FLUSH = decltype(flush_c)::value;
         Raw X = X0;
 #pragma unroll
         for (int m = 0; m < U4; ++m) asm volatile("" : "+v"(X.h[m]), "+v"(X.c[m]), "+v"(X.d[m]));
@@ -1026,6 +1050,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         }
 #pragma unroll
         for (int m = 0; m < U4; ++m) dh_rec[m] = dslot[m];
+        if (lane_reset) {   // the row's state before this step (in time order: t + 1) was reset to zero
+          const float k = t + 1 < mylen ? 1.f : 0.f;
+#pragma unroll
+          for (int m = 0; m < U4; ++m) {
+            dh_rec[m] *= k;
+            dc_rec[m] *= k;
+          }
+        }
         // pos-feature gradients -> dxp rows (word / padding features: the trash row)
         const int sp = t * PSTEPB;
 #pragma unroll
@@ -1050,7 +1082,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         uint32_t* xi32 = reinterpret_cast<uint32_t*>(xhI + (RR + n) * FCP + q * NSLP);
 #pragma unroll
         for (int w = 0; w < NSLP / 2; ++w) xi32[w] = w < NW ? bw[w] : 0u;
-        if constexpr (!ODD) {
+        if constexpr (FLUSH) {
           lds_order();
           auto tr8 = [&](const unsigned short* img, int stride, int c0) {
             const s16x4_t lo = tr_read(img + (8 * q + (n >> 2)) * stride + c0 + tcol);
@@ -1072,40 +1104,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       };
       using T_ = std::true_type;
       using F_ = std::false_type;
+      // processing steps tau_start .. tau_end (descending; tof maps to time).  Forward direction: from the
+      // tile's last valid step (its later steps have zero gradient).  Backward direction: all L (parity) or
+      // time [0, Lt) (SKIP).  The last processed step never has a predecessor state.
+      const int tau_start = dir == 0 ? Lt - 1 : L - 1;
+      const int tau_end = (dir == 1 && slen != nullptr) ? L - Lt : 0;
+      const int nst = tau_start - tau_end + 1;
+      // dxp rows of the steps not processed: zero (the pos-gradient reduction reads every step)
+      for (int t = Lt; t < L; ++t) {
+        if (dir == 1 && slen == nullptr) break;
+#pragma unroll
+        for (int xi = 0; xi < NX; ++xi)
+          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)0, rdx, 2 * pofs[xi], t * PSTEPB, 0);
+      }
 #pragma unroll
       for (int m = 0; m < U4; ++m)   // c of the first processed step
         ccur[m] = (float)__builtin_bit_cast(
-            _Float16, (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + (U4 + m) * 128, tof(L - 1) * RSTEPB, 0));
-      int tau = L - 1;
-      if (tau % 2 == 0) {   // odd L: the first step (even tau) alone, completing the half-filled pair
-        Raw S0;
-        rload(tau, S0);
-        if (tau == 0) {
-          bstep(F_{}, F_{}, 0, S0);
-          tau = -1;
-        } else {
-          bstep(T_{}, F_{}, tau, S0);
-          tau -= 1;
-        }
+            _Float16, (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + (U4 + m) * 128, tof(tau_start) * RSTEPB, 0));
+      Raw A, B;
+      rload(tau_start, A);
+      int k = 0;   // processed steps so far: pairs (k, k + 1) -> image rows 0..15 / 16..31
+      for (; k + 2 < nst; k += 2) {
+        rload(tau_start - k - 1, B);
+        __builtin_amdgcn_sched_barrier(0);
+        bstep(T_{}, F_{}, F_{}, tau_start - k, A);
+        __builtin_amdgcn_sched_barrier(0);
+        rload(tau_start - k - 2, A);
+        __builtin_amdgcn_sched_barrier(0);
+        bstep(T_{}, T_{}, T_{}, tau_start - k - 1, B);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      if (tau >= 1) {   // tau odd: pairs (tau, tau - 1), ping-pong prefetch
-        Raw A, B;
-        rload(tau, A);
-        for (; tau >= 3; tau -= 2) {
-          rload(tau - 1, B);
-          __builtin_amdgcn_sched_barrier(0);
-          bstep(T_{}, T_{}, tau, A);
-          __builtin_amdgcn_sched_barrier(0);
-          rload(tau - 2, A);
-          __builtin_amdgcn_sched_barrier(0);
-          bstep(T_{}, F_{}, tau - 1, B);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        rload(0, B);
+      if (nst - k == 2) {
+        rload(tau_end, B);
         __builtin_amdgcn_sched_barrier(0);
-        bstep(T_{}, T_{}, 1, A);
+        bstep(T_{}, F_{}, F_{}, tau_start - k, A);
         __builtin_amdgcn_sched_barrier(0);
-        bstep(F_{}, F_{}, 0, B);
+        bstep(F_{}, T_{}, T_{}, tau_end, B);
+      } else {   // a lone last step: its pair's other half (rows 16..31) holds flushed data -> zero dG
+#pragma unroll
+        for (int m = 0; m < U4; ++m)
+          *reinterpret_cast<u16x4_t*>(dgI + (16 + n) * GCP + q * (4 * U4) + 4 * m) = u16x4_t{0, 0, 0, 0};
+        bstep(F_{}, F_{}, T_{}, tau_end, A);
       }
     } else if constexpr (!BF16) {
     float xv[NX], hp[U4], cprev[U4], dhin[U4];
@@ -1530,10 +1569,12 @@ static int launch_fwd_t(const LstmArgs& a, hipStream_t st) {
   const bool drop = a.drop && !BF16;
   auto kern = drop ? (store ? lstm_fwd_kernel<U, NX, BF16, !BF16, true> : lstm_fwd_kernel<U, NX, BF16, !BF16, false>)
                    : (store ? lstm_fwd_kernel<U, NX, BF16, false, true> : lstm_fwd_kernel<U, NX, BF16, false, false>);
+  if (BF16 && a.slen)   // sequence_length semantics (lstm_skip_padding)
+    kern = store ? lstm_fwd_kernel<U, NX, BF16, false, true, BF16> : lstm_fwd_kernel<U, NX, BF16, false, false, BF16>;
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, a.bias, (elem*)a.hraw,
                      (typename CT<BF16>::type*)a.cst, (elem*)a.hdrop, a.dmask, a.seed, a.thr, a.inv_kp, a.drop, a.seed_dev,
-                     (const unsigned short*)a.xg);
+                     (const unsigned short*)a.xg, BF16 ? a.tlen : nullptr, BF16 ? a.slen : nullptr);
   INA_CHECK_LAUNCH();
   return 0;
 }
@@ -1545,7 +1586,7 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   dim3 grid(a.bwd_blocks, 2);
   size_t lds = lstm_bwd_lds_bytes(U, NX, BF16, a.L, a.PD);
   // bf16 + lane-layout dH (rec_attn_bwd, premasked): the lean PM step
-  const bool pm = BF16 && a.dh_lane;
+  const bool pm = INA_LSTM_PM && BF16 && a.dh_lane;
   auto kfn = pm ? (a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, BF16> : lstm_bwd_kernel<U, NX, BF16, false, BF16>)
                 : (a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, false> : lstm_bwd_kernel<U, NX, BF16, false, false>);
   static bool attr_set = false;
@@ -1558,7 +1599,8 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(kfn, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, (const frag*)a.a2pack, a.bias,
                      (const elem*)a.hraw, (const typename CT<BF16>::type*)a.cst, (const elem*)a.dH, a.dw_slab, a.dpos_slab, a.dwemb, a.dmask, a.seed, a.thr, a.inv_kp,
-                     a.drop, (unsigned short*)a.dxp, (const unsigned short*)a.xg, a.dh_lane);
+                     a.drop, (unsigned short*)a.dxp, (const unsigned short*)a.xg, a.dh_lane, pm ? a.tlen : nullptr,
+                     pm ? a.slen : nullptr);
   INA_CHECK_LAUNCH();
   return 0;
 }

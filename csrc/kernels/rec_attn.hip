@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
     const unsigned short* __restrict__ rec, const unsigned char* __restrict__ dmask, int S, int L, float inv_kp,
     const int* __restrict__ inst, const int* __restrict__ maskarr, const u16x8_t* __restrict__ w1r,
     const float* __restrict__ b1, const float* __restrict__ w2, float* __restrict__ e_out,
-    float* __restrict__ alphas) {
+    float* __restrict__ alphas, const int* __restrict__ tlen, const int* __restrict__ perm) {
   using C = RA<U>;
   constexpr int U4 = C::U4, H2 = C::H2, NV = C::NV, NKR = C::NKR, MT = C::MT;
   const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15;
@@ -202,6 +202,10 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
   const int seq = tile * 16 + n;
   const bool valid = seq < S;
   const int seqc = valid ? seq : S - 1;
+  // ragged tiles: the tile's steps t >= Lt are padding of every row (alpha exactly 0): not visited;
+  // output rows go to perm[seq] (the records are in length-sorted row order)
+  const int Lt = tlen ? tlen[tile] : L;
+  const int orow = perm ? perm[seqc] : seqc;
   // token mask of the lane's sequence as a 64-bit set (L <= 64): 16 loads per lane, OR over the groups
   uint32_t mlo = 0, mhi = 0;
   {
@@ -223,7 +227,7 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
   const unsigned char* k0 = drop ? dmask + (size_t)tile * 2 * L * 64 + lane : reinterpret_cast<const unsigned char*>(r0);
   const unsigned char* k1 = drop ? k0 + (size_t)L * 64 : k0;
   const uint32_t kor = drop ? 0u : 0xFFFFu;
-  float* arow = alphas + (size_t)seqc * L;
+  float* arow = alphas + (size_t)orow * L;
   // sum_j w_j tanh(x_j) = sum_j w_j - 2 sum_j w_j r_j (tanh_r): the lane's share of sum_j w_j
   float wl = 0.f;
 #pragma unroll
@@ -234,7 +238,7 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
 #pragma unroll
   for (int i = 0; i < NV; ++i) ea[i] = 0.f;
   auto load = [&](int t, RecStep<U>& o) { rec_load<U>(r0, r1, k0, k1, kor, t, o); };
-  rec_steps<U, INA_RA_PF_FWD>(L, load, [&](int t, RecStep<U>& cur) {
+  rec_steps<U, INA_RA_PF_FWD>(Lt, load, [&](int t, RecStep<U>& cur) {
     rec_pin<U, false>(cur, kor);
     float v[NV];
     u32x4_t Bw[NKR];
@@ -272,11 +276,11 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
   const float inv = 1.f / lsum;
   if (valid) {
 #pragma unroll
-    for (int i = 0; i < NV; ++i) e_out[(size_t)seq * H2 + rfeat<U>(i, q)] = ea[i] * inv;
+    for (int i = 0; i < NV; ++i) e_out[(size_t)orow * H2 + rfeat<U>(i, q)] = ea[i] * inv;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int t = q + 4 * i;
-      if (t < L) arow[t] = __expf(sl[t * 16 + n] - mx) * inv;   // this lane's own LDS stores
+      if (t < L) arow[t] = t < Lt ? __expf(sl[t * 16 + n] - mx) * inv : 0.f;   // this lane's own LDS stores
     }
   }
 }
@@ -298,7 +302,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3
     const unsigned short* __restrict__ rec, const unsigned char* __restrict__ dmask, int S, int L, float inv_kp,
     const u16x8_t* __restrict__ w1r, const u16x8_t* __restrict__ w1rt, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ de, const float* __restrict__ e_fwd,
-    const float* __restrict__ alphas, unsigned short* __restrict__ dHl, float* __restrict__ slab) {
+    const float* __restrict__ alphas, unsigned short* __restrict__ dHl, float* __restrict__ slab,
+    const int* __restrict__ tlen, const int* __restrict__ perm) {
   using C = RA<U>;
   constexpr int U4 = C::U4, H2 = C::H2, NV = C::NV, NKR = C::NKR, MT = C::MT, NJ = C::NJ, NKS2 = C::NKS2,
                 NRT = C::NRT, NVP = C::NVP, HT = C::HT, HCP = C::HCP, JCP = C::JCP, DEPC = C::DEP;
@@ -337,18 +342,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3
     const int seq = tile * 16 + n;
     const bool valid = seq < S;
     const int seqc = valid ? seq : S - 1;
+    const int Lt = tlen ? tlen[tile] : L;          // ragged tiles: dH rows t >= Lt are never read
+    const int orow = perm ? perm[seqc] : seqc;     // de / e / alphas row of record row seq
     // de of the lane's features -> LDS (re-read per step: registers kept for occupancy)
     float sd = 0.f;
     lds_order();   // the previous tile's reads of lde come first
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      const size_t o = (size_t)seqc * H2 + rfeat<U>(i, q);
+      const size_t o = (size_t)orow * H2 + rfeat<U>(i, q);
       const float x = valid ? de[o] : 0.f;
       lde[i] = x;
       sd = fmaf(x, e_fwd[o], sd);   // same sequential fma order as d(alpha) below: exact 0 for L = 1
     }
     sd = cross_group_sum(sd);
-    const float* arow = alphas + (size_t)seqc * L;
+    const float* arow = alphas + (size_t)orow * L;
     const unsigned short* r0 = rec + (size_t)tile * 2 * L * C::RSTEP + lane;
     const unsigned short* r1 = r0 + (size_t)L * C::RSTEP;
     const unsigned char* k0 = drop ? dmask + (size_t)tile * 2 * L * 64 + lane : reinterpret_cast<const unsigned char*>(r0);
@@ -359,7 +366,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3
       rec_load<U>(r0, r1, k0, k1, kor, t, o);
       o.al = arow[t];
     };
-    rec_steps<U, 1>(L, load, [&](int t, RecStep<U>& cur) {
+    rec_steps<U, 1>(Lt, load, [&](int t, RecStep<U>& cur) {
       rec_pin<U, true>(cur, kor);
       const float alv = valid ? cur.al : 0.f;
       float dev[DEPC];
@@ -442,7 +449,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3
       for (int m = 0; m < MT; ++m)
         *reinterpret_cast<u16x4_t*>(pimg + rr * JCP + q * NJ + 4 * m) =
             u16x4_t{f2bf(dp[m][0]), f2bf(dp[m][1]), f2bf(dp[m][2]), f2bf(dp[m][3])};
-      if ((t & 1) || t == L - 1) {
+      if ((t & 1) || t == Lt - 1) {
         if (!(t & 1)) {
           // lone last step (L odd): rows 16..31 still hold the previous (already flushed) pair
 #pragma unroll
@@ -527,7 +534,8 @@ static int rec_attn_fwd_t(const void* rec, const unsigned char* dmask, float inv
                           hipStream_t st) {
   const int ntiles = (a.S + 15) / 16;
   hipLaunchKernelGGL((rec_attn_fwd_kernel<U>), dim3((ntiles + 3) / 4), dim3(256), 0, st, (const unsigned short*)rec,
-                     dmask, a.S, a.L, inv_kp, a.inst, a.mask, (const u16x8_t*)a.w1pack, a.b1, a.w2, a.e, a.alphas);
+                     dmask, a.S, a.L, inv_kp, a.inst, a.mask, (const u16x8_t*)a.w1pack, a.b1, a.w2, a.e, a.alphas,
+                     a.tlen, a.perm);
   INA_CHECK_LAUNCH();
   return 0;
 }
@@ -541,7 +549,7 @@ static int rec_attn_bwd_t(const void* rec, const unsigned char* dmask, float inv
                               160 * 1024);
   hipLaunchKernelGGL((rec_attn_bwd_kernel<U>), dim3(a.blocks), dim3(256), lds, st, (const unsigned short*)rec, dmask,
                      a.S, a.L, inv_kp, (const u16x8_t*)a.w1pack, (const u16x8_t*)a.w1tpack, a.b1, a.w2, a.de,
-                     a.e, a.alphas, (unsigned short*)a.dHraw, a.slab);
+                     a.e, a.alphas, (unsigned short*)a.dHraw, a.slab, a.tlen, a.perm);
   INA_CHECK_LAUNCH();
   return 0;
 }

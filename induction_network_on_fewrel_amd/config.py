@@ -53,7 +53,10 @@ class Config:
     ntn_slices: int = 100              # neural_tensor_layer(out_size=100)
     relation_head: str = "reference"   # "reference": W[h*N, N] mixes classes; "paper": per-pair W_r in R^h
     encoder: str = "bilstm"            # "bilstm" | "bert"
-    lstm_skip_padding: bool = False    # parity: process all L steps
+    lstm_skip_padding: bool = False    # parity: process all L steps; True: TF sequence_length
+                                       # semantics (fw stops at length, bw starts at length - 1)
+    ragged_tiles: bool = True          # GPU bf16: length-sorted 16-row tiles; the fw direction and the attention
+                                       # stop at each tile's longest length (exact: padding is masked)
     lstm_impl: str = "auto"            # GPU BiLSTM: "fused" (lane-ownership kernel, u<=32) | "wide" (GEMM + cell kernels) | "auto"
     train_word_embedding: bool = False # only used when no pretrained table is given
 

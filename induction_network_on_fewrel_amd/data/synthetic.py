@@ -1,8 +1,9 @@
 """Synthetic FewRel-shaped data (benchmarks and tests run on synthetic tokens).
 
-Shapes follow the measured val.json statistics (length 6..36, L=37, ~33%
-padding). Each relation owns a few "trigger" tokens placed between the two entities so
-that the task is learnable (integration tests check that accuracy rises above chance).
+Shapes follow the measured val.json statistics (L=37, ~33% padding): sentence lengths are
+drawn from val.json's length histogram (6..36 tokens, mean 24.8; ``length_dist="uniform"`` gives the
+round-1/2 uniform 6..36 draw, mean 21). Each relation owns a few "trigger" tokens placed between the
+two entities so that the task is learnable (integration tests check that accuracy rises above chance).
 """
 from __future__ import annotations
 
@@ -11,6 +12,12 @@ from collections import OrderedDict
 import numpy as np
 
 from .fewrel import FewRelDataset
+
+
+# instances per token length in the reference's data/val.json (lengths 6..36; 11,200 instances)
+FEWREL_VAL_LENGTH_HIST = {6: 2, 7: 7, 8: 18, 9: 22, 10: 52, 11: 156, 12: 216, 13: 158, 14: 226, 15: 260, 16: 275,
+                          17: 343, 18: 355, 19: 424, 20: 429, 21: 485, 22: 567, 23: 566, 24: 574, 25: 578, 26: 596,
+                          27: 602, 28: 618, 29: 586, 30: 550, 31: 537, 32: 507, 33: 447, 34: 360, 35: 343, 36: 341}
 
 
 def random_word_vectors(vocab: int, dim: int, seed: int = 0) -> np.ndarray:
@@ -26,7 +33,7 @@ def random_word_vectors(vocab: int, dim: int, seed: int = 0) -> np.ndarray:
 def make_synthetic(num_relations: int = 64, instances_per_relation: int = 700, max_length: int = 37,
                    vocab: int = 400000, word_dim: int = 5, min_len: int = 6, max_len: int = 36,
                    triggers_per_relation: int = 8, triggers_per_sentence: int = 3, seed: int = 0,
-                   with_word_vectors: bool = True) -> FewRelDataset:
+                   with_word_vectors: bool = True, length_dist: str = "fewrel") -> FewRelDataset:
     rng = np.random.default_rng(seed)
     L = max_length
     R, I = num_relations, instances_per_relation
@@ -34,7 +41,17 @@ def make_synthetic(num_relations: int = 64, instances_per_relation: int = 700, m
     unk, blank = vocab, vocab + 1
     max_len = min(max_len, L)
     min_len = max(1, min(min_len, max_len))
-    lengths = rng.integers(min_len, max_len + 1, size=tot).astype(np.int32)
+    if length_dist == "fewrel":
+        ls = np.array([k for k in FEWREL_VAL_LENGTH_HIST if min_len <= k <= max_len], dtype=np.int32)
+        if len(ls) == 0:   # a max_length below FewRel's shortest sentence: every row full length
+            lengths = np.full(tot, max_len, dtype=np.int32)
+        else:
+            w = np.array([FEWREL_VAL_LENGTH_HIST[k] for k in ls], dtype=np.float64)
+            lengths = rng.choice(ls, size=tot, p=w / w.sum()).astype(np.int32)
+    elif length_dist == "uniform":
+        lengths = rng.integers(min_len, max_len + 1, size=tot).astype(np.int32)
+    else:
+        raise ValueError(f"unknown length_dist {length_dist}")
     word = rng.integers(0, vocab, size=(tot, L)).astype(np.int32)
     # a sprinkle of OOV tokens, like real text
     oov = rng.random((tot, L)) < 0.02

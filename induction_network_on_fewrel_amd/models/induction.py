@@ -95,17 +95,20 @@ class InductionNetwork(nn.Module):
             if self.use_fused_lstm(word.shape[1]):
                 from ..ops.encoder import encode
                 meta = dict(U=cfg.hidden_size, bf16=(cfg.dtype == "bf16"), keep_prob=kp, seed=int(dropout_seed),
+                            ragged=cfg.ragged_tiles, skip_padding=cfg.lstm_skip_padding,
                             word_grad=bool(isinstance(p["word_embedding"], nn.Parameter)
                                            and p["word_embedding"].requires_grad), grad_views=grad_views,
                             seed_dev=seed_dev)
                 e, alphas = encode(inst, data, p, meta)
             else:   # wide layers (e.g. the paper's u=128, E=300): GEMM + fused-cell path
                 from ..ops.wide import encode_wide
+                if cfg.lstm_skip_padding:
+                    raise NotImplementedError("lstm_skip_padding: the wide GPU path runs the reference's full L")
                 e, alphas = encode_wide(inst, data, p, cfg.hidden_size, kp, int(dropout_seed))
             return self._head(e, p, B, N, K, Q, grad_views), alphas
         word, pos1, pos2, mask = (t[inst.long()] for t in data)
         probs, alphas = ref.forward(p, word, pos1, pos2, mask, B, N, K, Q, cfg.routing_iters, cfg.relation_head,
-                                    kp, int(dropout_seed), bf16=False)
+                                    kp, int(dropout_seed), bf16=False, skip_padding=cfg.lstm_skip_padding)
         return probs, alphas.squeeze(-1)
 
     def _forward_bert(self, inst, data, B, N, K, Q, training, dropout_seed, grad_views, p, overlap=None):
@@ -151,8 +154,8 @@ class InductionNetwork(nn.Module):
         U, bf16 = cfg.hidden_size, cfg.dtype == "bf16"
         paper = cfg.relation_head == "paper"
         packs = glue.packs(p, U, lstm_din(p), bf16, (H, p["M"].shape[2], N, paper))
-        meta = dict(U=U, bf16=bf16, keep_prob=cfg.keep_prob, seed=int(dropout_seed),
-                    word_grad=bool(isinstance(p["word_embedding"], nn.Parameter) and p["word_embedding"].requires_grad),
+        meta = dict(U=U, bf16=bf16, keep_prob=cfg.keep_prob, seed=int(dropout_seed), ragged=cfg.ragged_tiles,
+                    skip_padding=cfg.lstm_skip_padding, word_grad=bool(isinstance(p["word_embedding"], nn.Parameter) and p["word_embedding"].requires_grad),
                     grad_views=grad_views, seed_dev=seed_dev, packs=packs, glue=glue, pdict=p)
         e, _ = encode(inst, data, p, meta)
         return head_loss(e, p, labels, dict(E=B, N=N, K=K, Q=Q, iters=cfg.routing_iters, paper=paper, glue=glue,

@@ -71,8 +71,13 @@ def embed(word_emb, pos1_emb, pos2_emb, word, pos1, pos2) -> torch.Tensor:
 
 
 def lstm_direction(x: torch.Tensor, kernel: torch.Tensor, bias: torch.Tensor, reverse: bool,
-                   bf16: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Returns (h_all, c_all) [S, L, u] in *time* order (bw outputs re-reversed)."""
+                   bf16: bool = False, lengths: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Returns (h_all, c_all) [S, L, u] in *time* order (bw outputs re-reversed).
+
+    ``lengths`` (opt-in ``lstm_skip_padding``): TF ``dynamic_rnn(sequence_length=...)`` semantics -- at
+    t >= length the output is zero and the state is carried unchanged, so the backward direction starts
+    at length - 1 from the zero state.  None = the reference: every L step, padding included
+    (model/graph.py:44-47)."""
     S, L, _ = x.shape
     u = kernel.shape[1] // 4
     h = x.new_zeros(S, u)
@@ -84,10 +89,24 @@ def lstm_direction(x: torch.Tensor, kernel: torch.Tensor, bias: torch.Tensor, re
         xh = torch.cat([_r(x[:, t], bf16), _r(h, bf16)], dim=-1)
         g = xh @ W + bias
         i, j, f, o = g.split(u, dim=-1)
-        c = c * torch.sigmoid(f + 1.0) + torch.sigmoid(i) * torch.tanh(j)
-        h = torch.tanh(c) * torch.sigmoid(o)
-        hs[t], cs[t] = h, c
+        c_new = c * torch.sigmoid(f + 1.0) + torch.sigmoid(i) * torch.tanh(j)
+        h_new = torch.tanh(c_new) * torch.sigmoid(o)
+        if lengths is None:
+            h, c = h_new, c_new
+            hs[t], cs[t] = h, c
+        else:
+            m = (t < lengths).to(x.dtype).unsqueeze(-1)
+            h = m * h_new + (1 - m) * h
+            c = m * c_new + (1 - m) * c
+            hs[t], cs[t] = m * h, m * c
     return torch.stack(hs, 1), torch.stack(cs, 1)
+
+
+def valid_lengths(mask: torch.Tensor) -> torch.Tensor:
+    """Per row: 1 + the last position with mask > 0 (0 for an all-padding row)."""
+    L = mask.shape[-1]
+    pos = torch.arange(1, L + 1, device=mask.device).expand_as(mask)
+    return torch.where(mask > 0, pos, torch.zeros_like(pos)).amax(-1)
 
 
 def self_attention(Hin: torch.Tensor, mask01: torch.Tensor, kernel, bias, w2, bf16: bool = False):
@@ -101,11 +120,13 @@ def self_attention(Hin: torch.Tensor, mask01: torch.Tensor, kernel, bias, w2, bf
 
 
 def encode(p: Dict[str, torch.Tensor], word, pos1, pos2, mask, keep_prob: float = 1.0,
-           dropout_seed: int = 0, bf16: bool = False, return_all: bool = False):
-    """Sentence encoder: [S, L] id arrays -> e [S, 2u] (+ alphas)."""
+           dropout_seed: int = 0, bf16: bool = False, return_all: bool = False, skip_padding: bool = False):
+    """Sentence encoder: [S, L] id arrays -> e [S, 2u] (+ alphas).  ``skip_padding``: the BiLSTM gets
+    sequence lengths (``lstm_skip_padding``; the reference runs through the padding)."""
     x = embed(p["word_embedding"], p["pos1_embedding"], p["pos2_embedding"], word, pos1, pos2)
-    hf, cf = lstm_direction(x, p["lstm_fw_kernel"], p["lstm_fw_bias"], False, bf16)
-    hb, cb = lstm_direction(x, p["lstm_bw_kernel"], p["lstm_bw_bias"], True, bf16)
+    lens = valid_lengths(mask) if skip_padding else None
+    hf, cf = lstm_direction(x, p["lstm_fw_kernel"], p["lstm_fw_bias"], False, bf16, lens)
+    hb, cb = lstm_direction(x, p["lstm_bw_kernel"], p["lstm_bw_bias"], True, bf16, lens)
     if bf16:   # kernels store the LSTM outputs as bf16
         hf, hb = _r(hf, True), _r(hb, True)
     if keep_prob < 1.0:
@@ -212,9 +233,9 @@ def accuracy(probs: torch.Tensor, labels: torch.Tensor, nota_threshold: Optional
 # ------------------------------------------------------------------ full model
 def forward(p: Dict[str, torch.Tensor], word, pos1, pos2, mask, B: int, N: int, K: int, Q: int,
             routing_iters: int = 3, head: str = "reference", keep_prob: float = 1.0, dropout_seed: int = 0,
-            bf16: bool = False):
+            bf16: bool = False, skip_padding: bool = False):
     """Episode batch forward. Row layout per episode: [support N*K ; query N*Q]."""
-    e, alphas = encode(p, word, pos1, pos2, mask, keep_prob, dropout_seed, bf16)
+    e, alphas = encode(p, word, pos1, pos2, mask, keep_prob, dropout_seed, bf16, skip_padding=skip_padding)
     return head_forward(p, e, B, N, K, Q, routing_iters, head, bf16), alphas
 
 

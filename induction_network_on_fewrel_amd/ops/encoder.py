@@ -5,8 +5,11 @@ crosses an autograd boundary (its gradient stays fp32 inside ``backward``).
 
 forward:  lstm_fwd (gather + MFMA recurrence, both directions; step records + dropout keep bits)
           ->  attention (MFMA projection, masked softmax, pooling)
-backward: attention backward (recompute projection, dH, dW1/db1/dw2 slabs)  ->  lstm_bwd (re-applies
-          the dropout keep bits, BPTT, dW/db/pos slabs)
+backward: attention backward (recompute projection, dH premasked by the dropout keep bits, dW1/db1/dw2
+          slabs)  ->  lstm_bwd (BPTT, dW/db/pos slabs)
+ragged tiles (bf16 record path, default): rows are sorted by valid length (``ragged_plan``) and each
+16-row tile's forward direction / attention stops at its longest length -- exact in parity mode;
+``lstm_skip_padding`` adds TF sequence_length semantics for the backward direction.
 bf16 (default): the attention kernels read the LSTM step records directly (rec_attn.hip; dH goes back
 in lstm_bwd's lane layout); fp32 or fuse_rec_attn=False: natural-layout H rows + attn_fwd / attn_bwd.
 
@@ -64,6 +67,25 @@ def word_rows(word: torch.Tensor, wemb: torch.Tensor, fresh: bool):
     return rows
 
 
+def ragged_plan(inst: torch.Tensor, lengths: torch.Tensor, skip: bool):
+    """Length-sorted rows for the record kernels: (inst_sorted, perm, tlen, slen).
+
+    perm = the stable argsort of the rows' valid lengths (row s of every record array is row perm[s] of
+    e / alphas / de); tlen [tiles] = each 16-row tile's longest length (>= 1): the forward direction and
+    the attention stop there -- padding outputs are masked out of the attention (alpha exactly 0), so
+    this is exact -- and sorted tiles make it ~the rows' own lengths.  slen (lstm_skip_padding only) =
+    the sorted lengths, for the backward direction's per-row sequence_length resets."""
+    S = inst.shape[0]
+    lens = lengths.index_select(0, inst.long())
+    perm = torch.argsort(lens, stable=True)
+    slen = lens.index_select(0, perm)
+    ntiles = (S + 15) // 16
+    last = torch.clamp(torch.arange(ntiles, device=inst.device) * 16 + 15, max=max(S - 1, 0))
+    tlen = torch.clamp(slen.index_select(0, last), min=1).to(torch.int32).contiguous()
+    return (inst.index_select(0, perm).contiguous(), perm.to(torch.int32).contiguous(), tlen,
+            slen.to(torch.int32).contiguous() if skip else None)
+
+
 class EncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, inst, word, pos1, pos2, mask, wemb, p1emb, p2emb, Kf, bf, Kb, bb, W1, b1, w2, meta):
@@ -90,19 +112,28 @@ class EncoderFn(torch.autograd.Function):
                 word_rows(word, wemb, bool(meta.get("word_grad", False))) if bf16 else None)
         b1c, w2c = b1.detach().contiguous(), w2.detach().reshape(-1).contiguous()
         rec = bf16 and meta.get("fuse_rec_attn", True) and o.rec_attn_ok(U, word.shape[1])
+        skip = bool(meta.get("skip_padding", False))
+        lengths = meta.get("lengths")
+        if skip and not (rec and lengths is not None):
+            raise NotImplementedError("lstm_skip_padding on the GPU needs the bf16 record path (u in {8, 20, 32}, "
+                                      "L <= 64) and device lengths")
+        perm = tlen = slen = None
         if rec:
             # attention straight from the step records (no natural-layout copy of H)
             w1pack, w1tpack = ((pk["w1rpack"], pk["w1rtpack"]) if pk is not None and "w1rpack" in pk
                                else pack_attn_rec(W1))
+            if lengths is not None and (meta.get("ragged", True) or skip):
+                inst, perm, tlen, slen = ragged_plan(inst, lengths, skip)
+                lstm_args = (inst,) + lstm_args[1:]
             hlane, cst, hnat, dmask, xg, e, alphas = o.lstm_attn_fwd(*lstm_args, bool(need_grad), *tail,
-                                                                     mask, w1pack, b1c, w2c)
+                                                                     mask, w1pack, b1c, w2c, tlen, perm, slen)
         else:
             w1pack, w1tpack = (pk["w1pack"], pk["w1tpack"]) if pk is not None else pack_attn(W1, bf16)
             hlane, cst, hnat, dmask, xg = o.lstm_fwd(*lstm_args, bf16, bool(need_grad), *tail)
             e, alphas = o.attn_fwd(hnat, inst, mask, w1pack, b1c, w2c, U, bf16, int(meta.get("attn_blocks", 0)))
         if need_grad:
             ctx.save_for_backward(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst,
-                                  w1pack, w1tpack, b1, w2, alphas, hnat, dmask, xg, e)
+                                  w1pack, w1tpack, b1, w2, alphas, hnat, dmask, xg, e, perm, tlen, slen)
             ctx.meta = dict(meta, NX=sh["NX"], DIN=DIN, rec=rec)
         ctx.mark_non_differentiable(alphas)
         ctx.set_materialize_grads(False)   # no zero-fill launch for the alphas gradient
@@ -112,14 +143,14 @@ class EncoderFn(torch.autograd.Function):
     def backward(ctx, de, _dalpha):
         o = ops()
         (inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst, w1pack, w1tpack, b1, w2,
-         alphas, hnat, dmask, xg, e) = ctx.saved_tensors
+         alphas, hnat, dmask, xg, e, perm, tlen, slen) = ctx.saved_tensors
         m = ctx.meta
         U, bf16, DIN = m["U"], m["bf16"], m["DIN"]
         H2 = 2 * U
         b1c, w2c = b1.detach().contiguous(), w2.detach().reshape(-1).contiguous()
         if m["rec"]:   # dH in lstm_bwd's lane layout [tiles, 2, L, U/4, 64]
             dH, aslab = o.rec_attn_bwd(hlane, dmask, w1pack, w1tpack, b1c, w2c, de.contiguous().float(), e, alphas,
-                                       U, float(m["keep_prob"]), int(m.get("attn_blocks", 0)))
+                                       U, float(m["keep_prob"]), int(m.get("attn_blocks", 0)), tlen, perm)
         else:
             dH, aslab = o.attn_bwd(hnat, inst, w1pack, w1tpack, b1c, w2c, de.contiguous().float(), alphas, U, bf16,
                                    int(m.get("attn_blocks", 0)))
@@ -128,7 +159,7 @@ class EncoderFn(torch.autograd.Function):
                                                p1emb.detach().contiguous(), p2emb.detach().contiguous(), apack, a2pack,
                                                bias, hlane, cst, dH, dmask, xg, U, m["NX"], bf16, word_grad,
                                                int(m.get("lstm_blocks", 0)), int(m["seed"]), float(m["keep_prob"]),
-                                               bool(m.get("pos_shift", False)))
+                                               bool(m.get("pos_shift", False)), tlen, slen)
         glue = m.get("glue")
         if glue is not None:
             # slabs -> flat gradient in the step's single slab_scatter_add launch (StepGlue.flush)
@@ -164,7 +195,7 @@ def encode(inst, data, params, meta):
     """data = (word, pos1, pos2, mask) device int32 arrays [NI, L]; returns (e [S, 2u], alphas [S, L])."""
     word, pos1, pos2, mask = data
     # position ids known to be shifted aranges (ops/sampler.py::DeviceArrays): cheaper pos-table gradient
-    meta = dict(meta, pos_shift=bool(getattr(data, "pos_shift", False)),
+    meta = dict(meta, pos_shift=bool(getattr(data, "pos_shift", False)), lengths=getattr(data, "lengths", None),
                 need_grad=torch.is_grad_enabled() and any(
                     isinstance(t, torch.Tensor) and t.requires_grad for t in params.values()))
     return EncoderFn.apply(inst, word, pos1, pos2, mask, params["word_embedding"], params["pos1_embedding"],

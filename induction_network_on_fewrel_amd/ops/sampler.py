@@ -17,8 +17,16 @@ from ._ext import ops
 class DeviceArrays(tuple):
     """(word, pos1, pos2, mask) device arrays; ``pos_shift`` = every sequence's position ids are a
     shifted arange (pos[s][t] = pos[s][0] + t, 0 <= pos[s][0] <= L: FewRel's ``j - p + L``), which
-    lets the backward reduce the position-table gradients as a per-sequence one-hot GEMM."""
+    lets the backward reduce the position-table gradients as a per-sequence one-hot GEMM.
+    ``lengths`` = int32 [NI]: 1 + each instance's last position with mask > 0 (ragged tiles)."""
     pos_shift = False
+    lengths = None
+
+
+def valid_lengths_np(mask: np.ndarray) -> np.ndarray:
+    L = mask.shape[1]
+    pos = np.where(mask > 0, np.arange(1, L + 1, dtype=np.int32)[None], 0)
+    return pos.max(1).astype(np.int32) if mask.size else np.zeros(mask.shape[0], np.int32)
 
 
 def positions_are_shifted(pos: np.ndarray) -> bool:
@@ -38,6 +46,7 @@ class DeviceDataset:
         self.pos1 = t(data.data_pos1)
         self.pos2 = t(data.data_pos2)
         self.mask = t(data.data_mask)
+        self.lengths = t(valid_lengths_np(np.asarray(data.data_mask)))
         sc = data.scope_array()
         self.scopes = t(sc)
         self.min_span = int((sc[:, 1] - sc[:, 0]).min()) if len(sc) else 0
@@ -53,6 +62,7 @@ class DeviceDataset:
             return self.bert["ids"], self.bert["mask"], self.bert["e1"], self.bert["e2"]
         out = DeviceArrays((self.word, self.pos1, self.pos2, self.mask))
         out.pos_shift = self.pos_shift
+        out.lengths = self.lengths
         return out
 
 

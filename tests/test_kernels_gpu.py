@@ -193,7 +193,7 @@ def test_rec_attention_forward_matches_natural(keep_prob, store, tail, u):
     hl0, _, hn0, dm0, _ = ops().lstm_fwd(*args, True, True, 77, keep_prob, None, None)
     e0, a0 = ops().attn_fwd(hn0, inst, mask, P["packs"][0], P["b1"], P["w2"], U, True, 0)
     hl1, _, hn1, dm1, _, e1, a1 = ops().lstm_attn_fwd(*args, store, 77, keep_prob, None, None, mask, P["rpacks"][0],
-                                                      P["b1"], P["w2"])
+                                                      P["b1"], P["w2"], None, None, None)
     torch.cuda.synchronize()
     assert hn1.numel() == 0 and e1.shape == e0.shape and a1.shape == a0.shape
     # h slots always; the c slots only when stored (the no-backward kernel leaves them unwritten)
@@ -217,7 +217,8 @@ def test_rec_attention_backward_matches_natural(keep_prob, tail, u):
     e, a = ops().attn_fwd(hn, inst, mask, P["packs"][0], P["b1"], P["w2"], U, True, 0)
     de = torch.randn_like(e)
     dH0, s0 = ops().attn_bwd(hn, inst, P["packs"][0], P["packs"][1], P["b1"], P["w2"], de, a, U, True, 0)
-    dHl, s1 = ops().rec_attn_bwd(hl, dm, P["rpacks"][0], P["rpacks"][1], P["b1"], P["w2"], de, e, a, U, keep_prob, 0)
+    dHl, s1 = ops().rec_attn_bwd(hl, dm, P["rpacks"][0], P["rpacks"][1], P["b1"], P["w2"], de, e, a, U, keep_prob, 0,
+                                 None, None)
     torch.cuda.synchronize()
     dH1 = _lane_to_natural(dHl, inst.shape[0])
     # rec_attn_bwd returns the gradient w.r.t. the LSTM output h (DropoutWrapper keep / keep_prob applied)
@@ -237,11 +238,11 @@ def test_rec_attention_backward_matches_natural(keep_prob, tail, u):
         assert pad.float().abs().max().item() == 0
 
 
-def _encoder_grads_ref(model, dd, inst, de, keep_prob, seed, bf16):
+def _encoder_grads_ref(model, dd, inst, de, keep_prob, seed, bf16, skip_padding=False):
     p = {k: v.detach().clone().requires_grad_(True) for k, v in model.pdict().items()}
     p["word_embedding"].requires_grad_(False)
     w, a1, a2, m = _gathered(dd, inst)
-    e, _ = ref.encode(p, w.long(), a1.long(), a2.long(), m, keep_prob, seed, bf16)
+    e, _ = ref.encode(p, w.long(), a1.long(), a2.long(), m, keep_prob, seed, bf16, skip_padding=skip_padding)
     (e * de).sum().backward()
     return e.detach(), {k: v.grad for k, v in p.items() if v.grad is not None}
 
@@ -272,6 +273,57 @@ def test_encoder_backward(dtype, keep_prob, u, L=37):
         err = _relerr(g, g_ref[k])
         print(f"  grad {k}: {err:.2e}")
         assert err < tol_g, k
+
+
+@pytest.mark.parametrize("u", [8, 20, 32])
+@pytest.mark.parametrize("keep_prob", [1.0, 0.9])
+def test_encoder_skip_padding(keep_prob, u):
+    """lstm_skip_padding: TF sequence_length semantics (fw stops at the length, bw starts at length - 1
+    from the zero state, per-row resets inside length-sorted ragged tiles) vs the fp32 oracle with the
+    same semantics; and it must differ from the reference's full-L parity output."""
+    from induction_network_on_fewrel_amd.ops.encoder import encode
+    cfg, data, model, dd, inst, _ = _problem(dtype="bf16", u=u)
+    seed = 99
+    meta = dict(U=cfg.hidden_size, bf16=True, keep_prob=keep_prob, seed=seed, word_grad=False, skip_padding=True)
+    p = model.pdict()
+    e, _ = encode(inst, dd.arrays(), p, meta)
+    de = torch.randn_like(e)
+    (e * de).sum().backward()
+    torch.cuda.synchronize()
+    e_ref, g_ref = _encoder_grads_ref(model, dd, inst, de, keep_prob, seed, bf16=False, skip_padding=True)
+    e_par, _ = _encoder_grads_ref(model, dd, inst, de, keep_prob, seed, bf16=False, skip_padding=False)
+    ee = _relerr(e.detach(), e_ref)
+    print(f"encoder skip u={u} kp={keep_prob}: e {ee:.2e} (vs parity oracle {_relerr(e.detach(), e_par):.2e})")
+    assert ee < 3e-2 and _relerr(e_par, e_ref) > 1e-2
+    for k in ("pos1_embedding", "pos2_embedding", "lstm_fw_kernel", "lstm_fw_bias", "lstm_bw_kernel", "lstm_bw_bias",
+              "attn_kernel", "attn_bias", "attn_w2"):
+        err = _relerr(getattr(model.params, k).grad, g_ref[k])
+        print(f"  grad {k}: {err:.2e}")
+        assert err < 6e-2, k
+
+
+@pytest.mark.parametrize("keep_prob", [1.0, 0.9])
+def test_ragged_tiles_match_full_length(keep_prob):
+    """Ragged tiles (rows sorted by length, forward direction + attention stop at each tile's longest
+    length) are exact: e and alphas bitwise equal to the full-L unsorted run, gradients equal up to the
+    fp32 summation order of the dW reductions."""
+    from induction_network_on_fewrel_amd.ops.encoder import encode
+    cfg, data, model, dd, inst, _ = _problem(dtype="bf16", B=7)
+    out = []
+    for ragged in (False, True):
+        p = {k: v.detach().clone().requires_grad_(v.requires_grad) for k, v in model.pdict().items()}
+        meta = dict(U=cfg.hidden_size, bf16=True, keep_prob=keep_prob, seed=5, word_grad=False, ragged=ragged)
+        e, a = encode(inst, dd.arrays(), p, meta)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        de = torch.randn(e.shape, generator=g, device="cuda")
+        (e * de).sum().backward()
+        out.append((e.detach(), a, {k: v.grad for k, v in p.items() if v.grad is not None}))
+    (e0, a0, g0), (e1, a1, g1) = out
+    assert torch.equal(e0, e1) and torch.equal(a0, a1)
+    for k in g0:
+        err = _relerr(g1[k], g0[k])
+        print(f"  ragged grad {k}: {err:.2e}")
+        assert err < 1e-4, k
 
 
 @pytest.mark.parametrize("L", [24, 1, 2])
@@ -341,7 +393,7 @@ def test_pos_grad_shift_matches_general(B):
     outs = []
     for shift in (False, True):
         _, dpos, _ = ops().lstm_bwd(inst, word, pos1, pos2, *tabs, apack, a2pack, bias, hlane, cst, dH, dmask, xg, U, NX,
-                                    True, False, 0, 5, 0.9, shift)
+                                    True, False, 0, 5, 0.9, shift, None, None)
         outs.append(dpos.sum((0, 1)))
     torch.cuda.synchronize()
     err = _relerr(outs[1], outs[0])
