@@ -104,7 +104,9 @@ def main():
     ap.add_argument("--hidden", type=int, default=20)
     ap.add_argument("--word-dim", type=int, default=5, help="5 = reference train.py; paper config: --hidden 128 --word-dim 300")
     ap.add_argument("--profile-json", default="")
-    ap.add_argument("--graph", type=int, default=0, help="capture the BiLSTM train step as a hipGraph (1/0)")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="capture the BiLSTM train step as a hipGraph: 1 always, 0 never, -1 auto (steps of <= 64 "
+                         "episodes, Config.hip_graph_max_episodes)")
     ap.add_argument("--mode", default="train", choices=["train", "eval"],
                     help="eval: forward-only episodic evaluation (FewRel 2.0 style, dropout off, accuracy "
                          "computed); a step = one batch of --episodes-per-gpu episodes (default 16384)")
@@ -140,7 +142,8 @@ def main():
     args.way = args.way or (10 if bert else 5)
     cfg = Config(N=args.way, K=args.shot, Q=args.query, max_length=37, hidden_size=args.hidden, dtype=args.dtype,
                  episodes_per_step=B, seed=1234, resume=False, model_dir="/tmp/ina_bench",
-                 train_iter=args.steps + args.warmup, use_hip_graph=bool(args.graph) and not bert and not evalm,
+                 train_iter=args.steps + args.warmup, use_hip_graph=args.graph == 1 and not bert and not evalm,
+                 hip_graph_max_episodes=64 if args.graph == -1 else 0,
                  nota_rate=args.nota, eval_batch=B, ragged_tiles=bool(args.ragged),
                  lstm_skip_padding=bool(args.skip_padding))
     if bert:

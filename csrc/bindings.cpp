@@ -75,7 +75,7 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd_impl(
     const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U, int64_t NX, bool bf16,
     bool store_c, int64_t seed, double keep_prob, const std::optional<Tensor>& seed_dev,
     const std::optional<Tensor>& wrows, bool natural, const std::optional<Tensor>& tlen = std::nullopt,
-    const std::optional<Tensor>& slen = std::nullopt) {
+    const std::optional<Tensor>& slen = std::nullopt, const std::optional<Tensor>& perm = std::nullopt) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -153,6 +153,7 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd_impl(
   }
   a.tlen = ragged_arg(tlen, ntiles, "tlen");
   a.slen = ragged_arg(slen, S, "slen");
+  a.perm = ragged_arg(perm, S, "perm");
   TORCH_CHECK(!a.tlen || (bf16 && !natural), "ina.lstm_fwd: ragged tiles need the bf16 record path");
   TORCH_CHECK(!a.slen || a.tlen, "ina.lstm_fwd: slen needs tlen");
   if (bf16) {
@@ -200,7 +201,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> lstm_attn_fwd
   TORCH_CHECK(w1r.numel() == MT * NKR * 64 * 8, "ina.lstm_attn_fwd: w1r pack size");
   const bool drop = keep_prob < 1.0;
   auto r = lstm_fwd_impl(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, bias, U, NX, true, store_c, seed, keep_prob,
-                         seed_dev, wrows, false, tlen, slen);
+                         seed_dev, wrows, false, tlen, slen, perm);
   auto e = at::empty({S, 2 * U}, b1.options());
   auto alphas = at::empty({S, L}, b1.options());
   if (S == 0) return {std::get<0>(r), std::get<1>(r), std::get<2>(r), std::get<3>(r), std::get<4>(r), e, alphas};
@@ -711,7 +712,8 @@ void slab_reduce(const Tensor& slabs, Tensor out, bool accumulate) {
 }
 
 std::tuple<Tensor, Tensor> sample_episodes(const Tensor& scopes, int64_t E, int64_t N, int64_t K, int64_t Q, int64_t seed,
-                                           double nota_rate, const std::optional<Tensor>& seed_dev) {
+                                           double nota_rate, const std::optional<Tensor>& seed_dev,
+                                           const std::optional<Tensor>& fail) {
   check(scopes, "scopes", at::kInt);
   TORCH_CHECK(scopes.dim() == 2 && scopes.size(1) == 2, "ina.sample_episodes: scopes must be [R, 2]");
   const int64_t R = scopes.size(0);
@@ -722,7 +724,8 @@ std::tuple<Tensor, Tensor> sample_episodes(const Tensor& scopes, int64_t E, int6
   if (E == 0) return {idx, lab};
   check_launch(ina::sample_episodes(scopes.data_ptr<int>(), (int)R, (int)E, (int)N, (int)K, (int)Q, (uint32_t)seed,
                                     (float)nota_rate, idx.data_ptr<int>(), lab.data_ptr<int>(),
-                                    dev_int(seed_dev, "seed_dev"), cur_stream()),
+                                    dev_int(seed_dev, "seed_dev"), const_cast<int*>(dev_int(fail, "fail")),
+                                    cur_stream()),
                "sample_episodes");
   return {idx, lab};
 }

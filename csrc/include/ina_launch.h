@@ -46,6 +46,7 @@ struct LstmArgs {
   // lengths; lstm_skip_padding), starts at tlen - 1 and resets each row's state past its own length
   const int* tlen;
   const int* slen;
+  const int* perm;   // x_gather: record row s is original row perm[s] (dropout hash counter)
 };
 // bf16 mode: gather every token's x features once into a.xg / a.posb, and (a.drop) the dropout keep
 // bits into a.dmask (lstm.hip x_gather_kernel); must run before lstm_fwd in bf16 mode
@@ -157,7 +158,7 @@ int step_control(int* ctl, float* lrt, long long seedA, long long seedB, double 
 int slab_reduce(const float* slabs, long nslab, long len, float* out, int accumulate, hipStream_t st);
 bool sampler_supported(int N, int K, int Q);
 int sample_episodes(const int* scopes, int R, int E, int N, int K, int Q, uint32_t seed, float nota_rate, int* idx,
-                    int* lab, const int* seed_dev, hipStream_t st);
+                    int* lab, const int* seed_dev, int* fail, hipStream_t st);
 
 // ---------------------------------------------------------------- wide BiLSTM cell (lstm_wide.hip)
 struct LstmWideArgs {

@@ -186,7 +186,8 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
                                                       unsigned short* __restrict__ xg,
                                                       unsigned short* __restrict__ posb,
                                                       unsigned char* __restrict__ dmask, int U, uint32_t seed,
-                                                      const int* __restrict__ seed_dev, uint32_t thr) {
+                                                      const int* __restrict__ seed_dev, uint32_t thr,
+                                                      const int* __restrict__ perm) {
   // the two position tables ([2L, PD] each, tiny) in LDS: per-feature loads from them were most of
   // this kernel's vector-memory instructions
   __shared__ float ptab[2 * 128 * 8];
@@ -238,7 +239,10 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
 #pragma unroll
     for (int d = 0; d < 2; ++d) {
       const uint32_t salt = dropout_salt(sd, (uint32_t)d);
-      const uint32_t pbase = (((uint32_t)seq * L + t) * U) >> 1;   // U even: the row's first unit pair
+      // the hash counter uses the row's ORIGINAL index (ragged tiles sort the rows): the same mask as
+      // the unsorted run and the oracle
+      const uint32_t oseq = (perm && valid) ? (uint32_t)perm[seq] : (uint32_t)seq;
+      const uint32_t pbase = ((oseq * L + t) * U) >> 1;   // U even: the row's first unit pair
       uint32_t by[4] = {0u, 0u, 0u, 0u};                            // keep byte of lane group q
 #pragma unroll
       for (int k = 0; k < 16; ++k) {                                // units 2k, 2k + 1 (lstm_keep)
@@ -1736,7 +1740,7 @@ int x_gather(const LstmArgs& a, int U, int NX, hipStream_t st) {
 #define INA_XG_LAUNCH(NXV, DIR, ...)                                                                     \
   hipLaunchKernelGGL((x_gather_kernel<NXV, DIR, ##__VA_ARGS__>), grid, dim3(256), 0, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, \
                      a.wemb, wr16, a.E, a.p1emb, a.p2emb, a.PD, xg, posb, a.drop ? a.dmask : nullptr, U, a.seed, \
-                     a.seed_dev, a.thr)
+                     a.seed_dev, a.thr, a.perm)
   if (NX == 4 && a.wrows && U == 20 && a.E == 5 && a.PD == 5)
     INA_XG_LAUNCH(4, true, 20, 5, 5);
   else if (NX == 4 && a.wrows)

@@ -8,6 +8,8 @@
 //     replaced by an instance of a relation outside the episode and labelled N (FewRel 2.0).
 // Randomness: counter-based hash of (seed, episode, draw) -> independent of launch geometry,
 // reproducible, and rank-disjoint when the caller folds the DP rank into the seed.
+// Every rejection loop ends after MAX_ROUNDS (an exit each wave reaches); one that runs out sets the
+// caller's device flag `fail` (the host checks it at log points, ops/sampler.py).
 #include "ina_common.h"
 
 using namespace ina;
@@ -49,7 +51,7 @@ INA_DEVICE void wave_lds_sync() {
 __global__ __launch_bounds__(256) void sample_episodes_kernel(const int* __restrict__ scopes, int R, int E, int N, int K,
                                                               int Q, uint32_t seed, float nota_rate,
                                                               int* __restrict__ idx_out, int* __restrict__ lab_out,
-                                                              const int* __restrict__ seed_dev) {
+                                                              const int* __restrict__ seed_dev, int* __restrict__ fail) {
   __shared__ int s_q[SW][MAXNQ];
   __shared__ int s_l[SW][MAXNQ];
   __shared__ uint32_t s_key[SW][MAXNQ];
@@ -66,12 +68,15 @@ __global__ __launch_bounds__(256) void sample_episodes_kernel(const int* __restr
   // ---- N distinct classes (every lane runs the same stream: wave-uniform control flow)
   Rng rc{ekey, 0u};
   int my_cls = -1;
+  bool exhausted = false;   // a rejection loop ran out of rounds: the episode may hold duplicates
   for (int i = 0; i < N; ++i) {
     int c = 0;
-    for (int round = 0; round < MAX_ROUNDS; ++round) {
+    int round = 0;
+    for (; round < MAX_ROUNDS; ++round) {
       c = (int)rc.below((uint32_t)R);
       if (__ballot(lane < i && my_cls == c) == 0) break;
     }
+    exhausted |= round == MAX_ROUNDS;
     if (lane == i) my_cls = c;
   }
   // ---- K + Q distinct instances of each class
@@ -81,7 +86,8 @@ __global__ __launch_bounds__(256) void sample_episodes_kernel(const int* __restr
     Rng ri{stream_key(ekey, (uint32_t)(i * 64 + lane)), 0u};
     int x = 0;
     bool need = lane < KQ;
-    for (int round = 0; round < MAX_ROUNDS; ++round) {
+    int round = 0;
+    for (; round < MAX_ROUNDS; ++round) {
       if (need) x = (int)ri.below((uint32_t)span);
       s_x[w][lane] = x;
       wave_lds_sync();
@@ -92,6 +98,7 @@ __global__ __launch_bounds__(256) void sample_episodes_kernel(const int* __restr
       need = dup;
       if (__ballot(need) == 0) break;
     }
+    exhausted |= round == MAX_ROUNDS;
     if (lane < K) row[i * K + lane] = b + x;
     else if (lane < KQ) {
       s_q[w][i * Q + lane - K] = b + x;
@@ -105,18 +112,21 @@ __global__ __launch_bounds__(256) void sample_episodes_kernel(const int* __restr
       Rng rn{stream_key(ekey, (uint32_t)(MAXN * 64 + qq)), 0u};
       if (rn.uniform() < nota_rate) {
         int c = 0;
-        for (int round = 0; round < MAX_ROUNDS; ++round) {
+        int round = 0;
+        for (; round < MAX_ROUNDS; ++round) {
           c = (int)rn.below((uint32_t)R);
           bool in = false;
           for (int j = 0; j < N; ++j) in |= (__shfl(my_cls, j, 64) == c);
           if (!in) break;
         }
+        if (round == MAX_ROUNDS && fail) fail[0] = 1;   // (lane-divergent: a vector store)
         const int b = scopes[2 * c], e = scopes[2 * c + 1];
         s_q[w][qq] = b + (int)rn.below((uint32_t)(e - b));
         s_l[w][qq] = N;
       }
     }
   }
+  if (exhausted && fail && lane == 0) fail[0] = 1;   // every writer stores the same value
   // ---- uniform random permutation of the queries: rank by random keys (ties broken by index)
   for (int qq = lane; qq < NQ; qq += 64) {
     Rng rk{stream_key(ekey, (uint32_t)(2 * MAXN * 64 + qq)), 0u};
@@ -140,9 +150,9 @@ namespace ina {
 bool sampler_supported(int N, int K, int Q) { return N <= MAXN && N <= 64 && K + Q <= MAXKQ && N * Q <= MAXNQ; }
 
 int sample_episodes(const int* scopes, int R, int E, int N, int K, int Q, uint32_t seed, float nota_rate, int* idx,
-                    int* lab, const int* seed_dev, hipStream_t st) {
+                    int* lab, const int* seed_dev, int* fail, hipStream_t st) {
   hipLaunchKernelGGL(sample_episodes_kernel, dim3((E + SW - 1) / SW), dim3(256), 0, st, scopes, R, E, N, K, Q, seed,
-                     nota_rate, idx, lab, seed_dev);
+                     nota_rate, idx, lab, seed_dev, fail);
   INA_CHECK_LAUNCH();
   return 0;
 }

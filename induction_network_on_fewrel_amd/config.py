@@ -110,6 +110,8 @@ class Config:
     deterministic: bool = False        # seeds + torch deterministic algorithms (utils/seeding.py); the fused
                                        # GPU path is deterministic regardless (ordered reductions)
     use_hip_graph: bool = False        # replay the BiLSTM train step as one captured hipGraph (runtime/graph.py)
+    hip_graph_max_episodes: int = 64   # ... and by default whenever episodes_per_step <= this (launch-bound small
+                                       # steps, e.g. the reference's 1 episode per step); 0 = only use_hip_graph
     step_glue: bool = True             # GPU BiLSTM: one-launch packs / loss / gradient scatter (ops/glue.py)
     nota_rate: float = 0.0             # FewRel 2.0 none-of-the-above probability per query
     eval_nota_rate: float = -1.0       # NOTA rate of val/test episodes (-1: same as nota_rate)

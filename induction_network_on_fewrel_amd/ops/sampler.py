@@ -72,6 +72,8 @@ class DeviceEpisodeSampler:
         self.seed = int(seed) & 0x7FFFFFFF
         self.nota_rate = float(nota_rate)
         self.calls = 0
+        # set by the kernel when a rejection loop runs out of rounds (possible duplicate classes / instances)
+        self.fail = torch.zeros(1, dtype=torch.int32, device=dd.device)
 
     def sample(self, B: int, N: int, K: int, Q: int, seed_dev=None):
         """-> (idx int32 [B, N*K+N*Q], labels int32 [B, N*Q]) on the device.  ``seed_dev`` (int32
@@ -82,7 +84,13 @@ class DeviceEpisodeSampler:
                              f"each (have {self.dd.num_relations}, smallest {self.dd.min_span})")
         s = (self.seed * 1000003 + self.calls * 7919) & 0x7FFFFFFF
         self.calls += 1
-        return ops().sample_episodes(self.dd.scopes, B, N, K, Q, s, self.nota_rate, seed_dev)
+        return ops().sample_episodes(self.dd.scopes, B, N, K, Q, s, self.nota_rate, seed_dev, self.fail)
+
+    def check(self) -> None:
+        """Raise if any sampled episode hit the rejection-round limit (reads the flag: synchronises)."""
+        if int(self.fail.item()) != 0:
+            raise RuntimeError("device episode sampler: a rejection loop ran out of rounds (duplicate classes or "
+                               "instances possible); the relations' instance spans are too small for N / K + Q")
 
     def seed_base(self) -> int:
         """seed(calls) = (seed_base + calls * 7919) mod 2^31 (the device step-control formula)."""

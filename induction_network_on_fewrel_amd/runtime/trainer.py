@@ -172,6 +172,15 @@ class Trainer:
         return out
 
     @property
+    def graph_step_enabled(self) -> bool:
+        """The train step runs as a captured hipGraph: ``use_hip_graph``, or automatically for small
+        (launch-bound) steps of the fused BiLSTM path."""
+        cfg = self.cfg
+        if self.device.type != "cuda" or cfg.encoder != "bilstm" or self.glue is None:
+            return False
+        return cfg.use_hip_graph or 0 < cfg.episodes_per_step <= cfg.hip_graph_max_episodes
+
+    @property
     def skipped_steps(self) -> int:
         """Optimizer steps skipped by the NaN/Inf guard (synchronises on the GPU)."""
         return self.opt.skipped()
@@ -192,8 +201,7 @@ class Trainer:
         buffer (grad_views), which is also the DP all-reduce bucket and the fused optimizer input."""
         cfg = self.cfg
         B, N, K, Q = cfg.episodes_per_step, cfg.N, cfg.K, cfg.Q
-        if (cfg.use_hip_graph and self.device.type == "cuda" and cfg.encoder == "bilstm"
-                and self.global_step != self._fault_step):
+        if self.graph_step_enabled and self.global_step != self._fault_step:
             if self._graph is None:
                 from .graph import GraphedTrainStep
                 self._graph = GraphedTrainStep(self)   # first step eager (warm-up) + capture, then replays
@@ -302,6 +310,8 @@ class Trainer:
             if (it % cfg.log_every == 0 or it % cfg.val_step == 0 or (it + 1) % cfg.val_step == 0
                     or it + 1 == cfg.train_iter):
                 pl, pa = float(pend_loss), float(pend_acc)
+                if hasattr(self.train_eps, "check"):
+                    self.train_eps.check()   # device sampler's rejection-limit flag
                 if cfg.grad_check_finite:
                     sk = self.skipped_steps
                     if sk > seen_skips:

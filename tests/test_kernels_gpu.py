@@ -579,7 +579,7 @@ def test_hip_graph_step_matches_eager(tmp_path):
     runs = []
     for graph in (False, True):
         cfg = Config(N=5, K=2, Q=3, episodes_per_step=16, model_dir=str(tmp_path / f"g{int(graph)}"), seed=4,
-                     resume=False, use_hip_graph=graph, learning_rate=1e-2)
+                     resume=False, use_hip_graph=graph, hip_graph_max_episodes=0, learning_rate=1e-2)
         tr = Trainer(cfg, data, None, device="cuda", log=False)
         losses = [float(tr.train_step()[0]) for _ in range(6)]
         runs.append((losses, tr.flat.flat.detach().clone(), tr.global_step, tr.opt.t, tr.train_eps.calls))
@@ -654,3 +654,32 @@ def test_step_glue_gradients_match_autograd():
     for n in f0.names:
         x, y = f0.view(g1, n), f0.view(g0, n)
         assert _relerr(x, y) < 1e-2, (n, _relerr(x, y))
+
+
+def test_sampler_rejection_limit_sets_flag():
+    """The device sampler's rejection loops end after a bounded number of rounds; a run that exhausts
+    them (relation spans smaller than K + Q, refused by the host wrapper, forced here) sets the device
+    flag instead of silently returning duplicates; a normal batch leaves it clear."""
+    from induction_network_on_fewrel_amd.ops import ops
+    ok = torch.tensor([[0, 40], [40, 80], [80, 120], [120, 160], [160, 200], [200, 240]], dtype=torch.int32,
+                      device=DEV)
+    flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ops().sample_episodes(ok, 64, 5, 5, 5, 3, 0.0, None, flag)
+    assert int(flag.item()) == 0
+    small = torch.tensor([[0, 3], [3, 6], [6, 9], [9, 12], [12, 15], [15, 18]], dtype=torch.int32, device=DEV)
+    ops().sample_episodes(small, 4, 5, 5, 5, 3, 0.0, None, flag)
+    assert int(flag.item()) == 1
+
+
+def test_small_steps_run_as_hip_graph(tmp_path):
+    """episodes_per_step <= hip_graph_max_episodes: the fused step is captured and replayed by default
+    (the reference's 1-episode steps are launch-bound)."""
+    from induction_network_on_fewrel_amd.runtime.trainer import Trainer
+    data = make_synthetic(num_relations=8, instances_per_relation=30, vocab=300, seed=0)
+    cfg = Config(N=5, K=5, Q=5, episodes_per_step=1, model_dir=str(tmp_path / "g"), seed=1, resume=False)
+    tr = Trainer(cfg, data, None, device="cuda", log=False)
+    assert tr.graph_step_enabled
+    for _ in range(3):
+        loss, _ = tr.train_step()
+        assert loss == loss
+    assert tr._graph is not None and tr._graph.graph is not None and tr.global_step == 3
