@@ -21,6 +21,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "csrc")
 # Experiment variants: INA_BUILD_TAG=<tag> INA_VARIANT_FLAGS="-DX=1" builds variants/_ina_kernels_<tag>.so
 # (load it with INA_KERNEL_LIB=<path>); the default build is the in-tree package library.
+# Host AddressSanitizer build: `python csrc/build.py --asan` (or INA_ASAN=1) ->
+# variants/_ina_kernels_asan.so, host code only (bindings + the kernels' host launch stubs;
+# `-fsanitize=address` goes after -Xarch_host on the hipcc lines, GPU code is never instrumented).  Load it
+# in a CPU process with LD_PRELOAD=$(gcc -print-file-name=libasan.so) (tests/test_native_build.py).
+_ASAN = os.environ.get("INA_ASAN") == "1" or "--asan" in sys.argv
+if _ASAN:
+    os.environ.setdefault("INA_BUILD_TAG", "asan")
 _TAG = os.environ.get("INA_BUILD_TAG", "")
 _VFLAGS = os.environ.get("INA_VARIANT_FLAGS", "").split()
 # per-file variant flags: INA_VARIANT_FILE_FLAGS="rec_attn.hip:-fno-slp-vectorize;lstm.hip:-DX=1"
@@ -76,6 +83,8 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
         objs.append(obj)
         if _newer(obj, [src, *headers, __file__]):
             tasks.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", *_VFLAGS,
+                          *(["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
+                            if _ASAN else []),
                           *FILE_FLAGS.get(os.path.basename(src), []),
                           *_VFILE.get(os.path.basename(src), []), "-I" + os.path.join(CSRC, "include"), "-c", src,
                           "-o", obj])
@@ -86,6 +95,8 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
             cxx = shutil.which("g++") or "c++"
             cmd = [cxx, "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
                    "-D_GLIBCXX_USE_CXX11_ABI=1", "-I/opt/rocm/include"]
+            if _ASAN:
+                cmd += ["-fsanitize=address", "-fno-omit-frame-pointer", "-g"]
             cmd += ["-I" + p for p in inc]
             cmd += ["-I" + sysconfig.get_paths()["include"], "-I" + os.path.join(CSRC, "include"), "-c", bsrc, "-o",
                     bobj]
@@ -97,6 +108,9 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
     if tasks or not os.path.exists(LIB) or _newer(LIB, objs):
         cmd = [hipcc, "-shared", "-fPIC", "-o", LIB, *objs, f"-L{tlib}", "-ltorch", "-ltorch_cpu", "-lc10",
                "-lc10_hip", "-ltorch_hip", f"-Wl,-rpath,{tlib}"]
+        if _ASAN:   # the host ASan runtime (gcc's; the process preloads it)
+            cmd += [subprocess.run(["gcc", "-print-file-name=libasan.so"], capture_output=True,
+                                   text=True).stdout.strip()]
         _run(cmd)
     return LIB
 

@@ -67,6 +67,9 @@ def word_rows(word: torch.Tensor, wemb: torch.Tensor, fresh: bool):
     return rows
 
 
+RAGGED_MIN_ROWS = 16384   # 1024 tiles: ~4 per CU
+
+
 def ragged_plan(inst: torch.Tensor, lengths: torch.Tensor, skip: bool):
     """Length-sorted rows for the record kernels: (inst_sorted, perm, tlen, slen).
 
@@ -122,7 +125,10 @@ class EncoderFn(torch.autograd.Function):
             # attention straight from the step records (no natural-layout copy of H)
             w1pack, w1tpack = ((pk["w1rpack"], pk["w1rtpack"]) if pk is not None and "w1rpack" in pk
                                else pack_attn_rec(W1))
-            if lengths is not None and (meta.get("ragged", True) or skip):
+            # ragged tiles pay off once the kernels are throughput-bound (many tiles per CU); small steps are
+            # latency-bound on the backward direction's full-length chain and would only add the sort
+            if lengths is not None and (skip or (meta.get("ragged", True)
+                                                 and inst.shape[0] >= meta.get("ragged_min_rows", RAGGED_MIN_ROWS))):
                 inst, perm, tlen, slen = ragged_plan(inst, lengths, skip)
                 lstm_args = (inst,) + lstm_args[1:]
             hlane, cst, hnat, dmask, xg, e, alphas = o.lstm_attn_fwd(*lstm_args, bool(need_grad), *tail,

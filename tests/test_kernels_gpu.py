@@ -255,7 +255,7 @@ def test_encoder_backward(dtype, keep_prob, u, L=37):
     cfg, data, model, dd, inst, _ = _problem(dtype=dtype, u=u, L=L)
     bf16 = dtype == "bf16"
     seed = 99
-    meta = dict(U=cfg.hidden_size, bf16=bf16, keep_prob=keep_prob, seed=seed, word_grad=False)
+    meta = dict(U=cfg.hidden_size, bf16=bf16, keep_prob=keep_prob, seed=seed, word_grad=False, ragged_min_rows=0)
     p = model.pdict()
     e, alphas = encode(inst, dd.arrays(), p, meta)
     de = torch.randn_like(e)
@@ -312,7 +312,8 @@ def test_ragged_tiles_match_full_length(keep_prob):
     out = []
     for ragged in (False, True):
         p = {k: v.detach().clone().requires_grad_(v.requires_grad) for k, v in model.pdict().items()}
-        meta = dict(U=cfg.hidden_size, bf16=True, keep_prob=keep_prob, seed=5, word_grad=False, ragged=ragged)
+        meta = dict(U=cfg.hidden_size, bf16=True, keep_prob=keep_prob, seed=5, word_grad=False, ragged=ragged,
+                    ragged_min_rows=0)
         e, a = encode(inst, dd.arrays(), p, meta)
         g = torch.Generator(device="cuda").manual_seed(1)
         de = torch.randn(e.shape, generator=g, device="cuda")
