@@ -182,6 +182,32 @@ struct LstmWideArgs {
 };
 int lstm_wide_fwd_step(const LstmWideArgs& a, int tau, hipStream_t st);
 int lstm_wide_bwd_step(const LstmWideArgs& a, int tau, hipStream_t st);
+// persistent wide BiLSTM (whole recurrence in one launch per pass; U in {64, 100, 128}, lstm_wide.hip):
+// gate columns permuted to c = 4u + g (u < UP = U padded to 32), ops/packing.py::pack_lstm_wide
+struct WideSeqArgs {
+  int S, L, U;
+  const void* gx;         // [2][S*L][G4] bf16: x W_x (pre-scaled, row s*L + t)
+  const float* bx;        // [2][G4] fp32: pre-scaled biases (forget gate +1)
+  const void* apk;        // [2][NW][4][KS][64] x 8 bf16 forward W_h fragments (pre-scaled)
+  const void* a2pk;       // [2][NW][KS2][64] x 8 bf16 backward W_h fragments
+  void* hprev;            // [2][S][L][UP] bf16: each step's recurrent input h_{t-1} (dW_h GEMM operand)
+  void* acts;             // [2][S][L][G4] bf16: i, j, f, o activations
+  void* cst;              // [2][S][L][UP] fp16: cell states
+  void* hout;             // [S][L][2U] bf16: DropoutWrapper output (attention input)
+  const void* dH;         // [S][L][2U] bf16: gradient w.r.t. hout
+  void* dG;               // [2][S][L][G4] bf16: pre-activation gate gradients
+  uint32_t salt0, salt1, thr;
+  float inv_kp;
+  int drop;
+  int stash;              // forward: write hprev / acts / cst (training)
+};
+bool lstm_wide_seq_supported(int U);
+int wide_x_gather(const int* inst, int S, int L, const int* word, const int* pos1, const int* pos2, const float* wemb,
+                  int E, const float* p1emb, const float* p2emb, int PD, void* xb, hipStream_t st);
+int wide_pos_grad(const float* dxp, const int* inst, const int* pos1, const int* pos2, int S, int L, int PD, int P2,
+                  int chunks, float* part, hipStream_t st);
+int lstm_wide_seq_fwd(const WideSeqArgs& a, hipStream_t st);
+int lstm_wide_seq_bwd(const WideSeqArgs& a, hipStream_t st);
 
 // ---------------------------------------------------------------- BERT (csrc/kernels/bert.hip)
 struct BertLnArgs {          // y = LN(res + dropout(a)); HD = 256 * {1..4}

@@ -143,3 +143,348 @@ int lstm_wide_bwd_step(const LstmWideArgs& a, int tau, hipStream_t st) {
 }
 
 }  // namespace ina
+
+// ==========================================================================================
+// Persistent wide BiLSTM: the whole recurrence of a 32-sequence tile and one direction in ONE
+// workgroup (NW = UP / 16 waves, 16 units per wave), U in {64, 100, 128} (the reference Base default
+// u=100, the paper's u=128).  The per-step kernels above round-trip the recurrent GEMM's fp32 output
+// (131 MB per step at the paper configuration) and relaunch 2 x L times; here
+//   * each wave keeps ITS slice of W_h as MFMA A fragments in VGPRs for the whole sequence
+//     (forward: 4 M-tiles x UP/32 K-steps; backward: UP*4/32 K-steps over the permuted gate columns);
+//   * gates are computed transposed, G^T[gate rows, seqs] = W_h^T h^T (+ the precomputed x W_x + b),
+//     with the row order chosen so lane group q holds the 4 gates of unit 16w + 4m + q in its 4
+//     accumulator registers (the lane-ownership layout of lstm.hip): c and h never leave the lane;
+//   * h_t is exchanged through a double-buffered LDS image [32 seqs][UP] bf16 (the next step's B
+//     operand), ONE workgroup barrier per step; the same image feeds coalesced row copies of the
+//     attention input (DropoutWrapper applied) and the backward's h_{t-1} stash;
+//   * backward: dG (bf16) goes to an LDS image [32][4 UP] and is contracted with the backward W_h
+//     fragments, whose row permutation lands dh of unit 16w + 4r + q in accumulator register r of
+//     lane group q -- the lane that owns that unit's gates.
+// Gate columns are permuted to c = 4u + g (unit-major, the 4 gates of a unit adjacent: one 16-byte
+// gx load, one 8-byte acts / dG store per lane and unit).  ops/packing.py::pack_lstm_wide builds the
+// fragments and is checked by tests/test_packing.py's MFMA-layout emulation.
+// ==========================================================================================
+namespace {
+
+template <int U>
+struct WideCfg {
+  static constexpr int UP = (U + 31) / 32 * 32;
+  static constexpr int NW = UP / 16;     // waves per workgroup
+  static constexpr int M = 4;            // forward M-tiles per wave (16 gate rows = 4 units)
+  static constexpr int KS = UP / 32;     // forward K-steps (input units)
+  static constexpr int G4 = 4 * UP;      // permuted gate columns
+  static constexpr int KS2 = G4 / 32;    // backward K-steps (gate columns)
+  static constexpr int NT = 2;           // 16-sequence tiles per workgroup
+  static constexpr int HS = UP + 8;      // h image row stride (elements; +16 B against bank aliasing)
+  static constexpr int GS = G4 + 8;      // dG image row stride
+  static constexpr int SEQ = NT * 16;
+};
+
+INA_DEVICE uint32_t pack_bf2(float a, float b) {
+  typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+  const bf2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+}  // namespace
+
+template <int U>
+__global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_fwd_kernel(
+    const unsigned short* __restrict__ gx, const float* __restrict__ bx, const u16x8_t* __restrict__ apk, int S, int L,
+    unsigned short* __restrict__ hprev, unsigned short* __restrict__ acts, _Float16* __restrict__ cst,
+    unsigned short* __restrict__ hout, uint32_t salt0, uint32_t salt1, uint32_t thr, float inv_kp, int drop,
+    int stash) {
+  using C = WideCfg<U>;
+  constexpr int UP = C::UP, NW = C::NW, M = C::M, KS = C::KS, G4 = C::G4, NT = C::NT, HS = C::HS, SEQ = C::SEQ;
+  constexpr int NTH = NW * 64;
+  __shared__ __attribute__((aligned(16))) unsigned short himg[2][SEQ * HS];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4, n = lane & 15;
+  const int dir = blockIdx.y, s0 = blockIdx.x * SEQ;
+  const uint32_t salt = dir ? salt1 : salt0, thr16 = thr >> 16;
+  u16x8_t A[M][KS];
+  {
+    const u16x8_t* ap = apk + (size_t)(dir * NW + w) * M * KS * 64 + lane;
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) A[m][ks] = ap[(m * KS + ks) * 64];
+  }
+  for (int i = threadIdx.x; i < SEQ * HS; i += NTH) reinterpret_cast<uint32_t*>(himg)[i] = 0u;   // both images
+  __syncthreads();
+  float c[M][NT];
+  int srow[NT];
+  bool sval[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int s = s0 + nt * 16 + n;
+    sval[nt] = s < S;
+    srow[nt] = sval[nt] ? s : S - 1;
+#pragma unroll
+    for (int m = 0; m < M; ++m) c[m][nt] = 0.f;
+  }
+  const int ub = 16 * w;   // the wave's units: ub + 4m + q
+  float4 bias[M];          // pre-scaled gate biases of the lane's units (forget gate +1)
+#pragma unroll
+  for (int m = 0; m < M; ++m) bias[m] = *reinterpret_cast<const float4*>(bx + dir * G4 + 4 * (ub + 4 * m + q));
+  // row-copy geometry: one 16-byte chunk (8 units) of one sequence row per thread and pass
+  constexpr int CH = UP / 8, NCH = SEQ * CH;
+  for (int tau = 0; tau < L; ++tau) {
+    const int t = dir ? L - 1 - tau : tau;
+    const unsigned short* hin = himg[tau & 1];
+    unsigned short* hnx = himg[(tau + 1) & 1];
+    if (stash) {   // this step's recurrent input h_{t-1} -> hprev[dir][s][t] (the dW_h GEMM's rows)
+      for (int i = threadIdx.x; i < NCH; i += NTH) {
+        const int r = i / CH, ch = i - r * CH, s = s0 + r;
+        if (s < S)
+          *reinterpret_cast<u16x8_t*>(hprev + (((size_t)dir * S + s) * L + t) * UP + 8 * ch) =
+              *reinterpret_cast<const u16x8_t*>(hin + r * HS + 8 * ch);
+      }
+    }
+    u16x8_t B[NT][KS];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) B[nt][ks] = *reinterpret_cast<const u16x8_t*>(hin + (nt * 16 + n) * HS + 32 * ks + 8 * q);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int u = ub + 4 * m + q;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const size_t row = ((size_t)dir * S + srow[nt]) * L + t;
+        const uint2 g4 = *reinterpret_cast<const uint2*>(gx + row * G4 + 4 * u);   // bf16 x W_x (4 gates)
+        f32x4_t acc = {bias[m].x + bf2f((unsigned short)g4.x), bias[m].y + bf2f((unsigned short)(g4.x >> 16)),
+                       bias[m].z + bf2f((unsigned short)g4.y), bias[m].w + bf2f((unsigned short)(g4.y >> 16))};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) acc = mfma_bf16(A[m][ks], B[nt][ks], acc);
+        const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
+        const float cn = c[m][nt] * fg + ig * jg;
+        c[m][nt] = cn;
+        const float hv = tanh_l2(cn * (2.f * LOG2E_F)) * og;
+        hnx[(nt * 16 + n) * HS + u] = f2bf(hv);
+        if (stash && sval[nt]) {
+          *reinterpret_cast<uint2*>(acts + row * G4 + 4 * u) = uint2{pack_bf2(ig, jg), pack_bf2(fg, og)};
+          cst[row * UP + u] = (_Float16)cn;   // fp16 cell state (|c| <= L: far inside range, 11-bit mantissa)
+        }
+      }
+    }
+    __syncthreads();   // hnx complete; every wave is past its reads of hin
+    // attention input h_t (DropoutWrapper: keep ? h / keep_prob : 0, one hash per unit pair as the
+    // fused kernels / oracle) -> hout[s][t][dir U + u], two units per 4-byte store
+    for (int i = threadIdx.x; i < SEQ * (UP / 2); i += NTH) {
+      const int r = i / (UP / 2), u = 2 * (i - r * (UP / 2)), s = s0 + r;
+      if (s >= S || u >= U) continue;
+      const uint32_t hv = *reinterpret_cast<const uint32_t*>(hnx + r * HS + u);
+      uint32_t o = hv;
+      if (drop) {
+        const uint32_t x = dropout_mix(salt, (((uint32_t)s * L + t) * U + u) >> 1);
+        const float a = bf2f((unsigned short)hv), b = bf2f((unsigned short)(hv >> 16));
+        o = pack_bf2((x & 0xFFFFu) < thr16 ? a * inv_kp : 0.f, (x >> 16) < thr16 ? b * inv_kp : 0.f);
+      }
+      *reinterpret_cast<uint32_t*>(hout + ((size_t)s * L + t) * 2 * U + dir * U + u) = o;
+    }
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_bwd_kernel(
+    const unsigned short* __restrict__ dH, const unsigned short* __restrict__ acts, const _Float16* __restrict__ cst,
+    const u16x8_t* __restrict__ a2pk, unsigned short* __restrict__ dG, int S, int L, uint32_t salt0, uint32_t salt1,
+    uint32_t thr, float inv_kp, int drop) {
+  using C = WideCfg<U>;
+  constexpr int UP = C::UP, NW = C::NW, M = C::M, G4 = C::G4, KS2 = C::KS2, NT = C::NT, GS = C::GS, SEQ = C::SEQ;
+  __shared__ __attribute__((aligned(16))) unsigned short gimg[2][SEQ * GS];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4, n = lane & 15;
+  const int dir = blockIdx.y, s0 = blockIdx.x * SEQ;
+  const uint32_t salt = dir ? salt1 : salt0;
+  u16x8_t A2[KS2];
+  {
+    const u16x8_t* ap = a2pk + (size_t)(dir * NW + w) * KS2 * 64 + lane;
+#pragma unroll
+    for (int ks = 0; ks < KS2; ++ks) A2[ks] = ap[ks * 64];
+  }
+  int srow[NT];
+  bool sval[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int s = s0 + nt * 16 + n;
+    sval[nt] = s < S;
+    srow[nt] = sval[nt] ? s : S - 1;
+  }
+  f32x4_t dhr[NT];     // dh of units ub + 4r + q (register r), from the previous processed step
+  float dcr[M][NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    dhr[nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < M; ++m) dcr[m][nt] = 0.f;
+  }
+  const int ub = 16 * w;
+  for (int tau = L - 1; tau >= 0; --tau) {
+    const int t = dir ? L - 1 - tau : tau;
+    const int tp = dir ? t + 1 : t - 1;   // the step before in processing order (its c is c_{t-1})
+    unsigned short* gcur = gimg[tau & 1];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int u = ub + 4 * m + q;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const size_t row = ((size_t)dir * S + srow[nt]) * L + t;
+        const uint2 av = *reinterpret_cast<const uint2*>(acts + row * G4 + 4 * u);
+        const float ig = bf2f((unsigned short)av.x), jg = bf2f((unsigned short)(av.x >> 16));
+        const float fg = bf2f((unsigned short)av.y), og = bf2f((unsigned short)(av.y >> 16));
+        const float cn = (float)cst[row * UP + u];
+        const float cp = tau > 0 ? (float)cst[(((size_t)dir * S + srow[nt]) * L + tp) * UP + u] : 0.f;
+        float dout = 0.f;
+        if (u < U && sval[nt]) {
+          const int s = srow[nt];
+          dout = bf2f(dH[((size_t)s * L + t) * 2 * U + dir * U + u]);
+          if (drop) dout = lstm_keep(salt, ((uint32_t)s * L + t) * U + u, thr) ? dout * inv_kp : 0.f;
+        }
+        const float tc = tanh_l2(cn * (2.f * LOG2E_F));
+        const float dh = dout + dhr[nt][m];
+        const float dc = dcr[m][nt] + dh * og * (1.f - tc * tc);
+        dcr[m][nt] = dc * fg;
+        const uint2 gw = uint2{pack_bf2(dc * jg * (ig - ig * ig), dc * ig * (1.f - jg * jg)),
+                               pack_bf2(dc * cp * (fg - fg * fg), dh * tc * (og - og * og))};
+        if (sval[nt]) *reinterpret_cast<uint2*>(dG + row * G4 + 4 * u) = gw;
+        *reinterpret_cast<uint2*>(gcur + (nt * 16 + n) * GS + 4 * u) = gw;
+      }
+    }
+    __syncthreads();   // the dG image of this step is complete
+    if (tau > 0) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS2; ++ks)
+          acc = mfma_bf16(A2[ks], *reinterpret_cast<const u16x8_t*>(gcur + (nt * 16 + n) * GS + 32 * ks + 8 * q), acc);
+        dhr[nt] = acc;
+      }
+    }
+  }
+}
+
+namespace ina {
+
+bool lstm_wide_seq_supported(int U) { return U == 64 || U == 100 || U == 128; }
+
+template <int U>
+static int wide_seq_fwd_t(const WideSeqArgs& a, hipStream_t st) {
+  using C = WideCfg<U>;
+  const dim3 grid((a.S + C::SEQ - 1) / C::SEQ, 2);
+  hipLaunchKernelGGL(lstm_wide_seq_fwd_kernel<U>, grid, dim3(C::NW * 64), 0, st, (const unsigned short*)a.gx, a.bx,
+                     (const u16x8_t*)a.apk, a.S, a.L, (unsigned short*)a.hprev, (unsigned short*)a.acts,
+                     (_Float16*)a.cst, (unsigned short*)a.hout, a.salt0,
+                     a.salt1, a.thr, a.inv_kp, a.drop, a.stash);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+template <int U>
+static int wide_seq_bwd_t(const WideSeqArgs& a, hipStream_t st) {
+  using C = WideCfg<U>;
+  const dim3 grid((a.S + C::SEQ - 1) / C::SEQ, 2);
+  hipLaunchKernelGGL(lstm_wide_seq_bwd_kernel<U>, grid, dim3(C::NW * 64), 0, st, (const unsigned short*)a.dH,
+                     (const unsigned short*)a.acts, (const _Float16*)a.cst, (const u16x8_t*)a.a2pk, (unsigned short*)a.dG, a.S, a.L,
+                     a.salt0, a.salt1, a.thr, a.inv_kp, a.drop);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int lstm_wide_seq_fwd(const WideSeqArgs& a, hipStream_t st) {
+  if (a.U == 64) return wide_seq_fwd_t<64>(a, st);
+  if (a.U == 100) return wide_seq_fwd_t<100>(a, st);
+  if (a.U == 128) return wide_seq_fwd_t<128>(a, st);
+  return -1;
+}
+int lstm_wide_seq_bwd(const WideSeqArgs& a, hipStream_t st) {
+  if (a.U == 64) return wide_seq_bwd_t<64>(a, st);
+  if (a.U == 100) return wide_seq_bwd_t<100>(a, st);
+  if (a.U == 128) return wide_seq_bwd_t<128>(a, st);
+  return -1;
+}
+
+}  // namespace ina
+
+// ------------------------------------------------------------------------------------------
+// Wide encoder input (K1 at wide shapes): Xb[s*L + t] = bf16 [word row ; pos1 row ; pos2 row] of token
+// (inst[s], t) -- one pass instead of a word gather (fp32), a cast, two position gathers and a concat.
+// One wave per token row (grid-stride), two columns (one 4-byte store) per lane and pass.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void wide_x_gather_kernel(const int* __restrict__ inst, int S, int L,
+                                                            const int* __restrict__ word, const int* __restrict__ pos1,
+                                                            const int* __restrict__ pos2, const float* __restrict__ wemb,
+                                                            int E, const float* __restrict__ p1emb,
+                                                            const float* __restrict__ p2emb, int PD,
+                                                            unsigned short* __restrict__ xb) {
+  const int lane = threadIdx.x & 63;
+  const int D = E + 2 * PD;
+  const long rows = (long)S * L;
+  for (long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (long)gridDim.x * 4) {
+    const int s = (int)(r / L), t = (int)(r - (long)s * L);
+    const long tok = (long)inst[s] * L + t;
+    const float* wr = wemb + (long)word[tok] * E;
+    const float* q1 = p1emb + (long)pos1[tok] * PD;
+    const float* q2 = p2emb + (long)pos2[tok] * PD;
+    auto col = [&](int c) { return c < E ? wr[c] : (c < E + PD ? q1[c - E] : q2[c - E - PD]); };
+    unsigned short* dst = xb + r * D;
+    for (int c = 2 * lane; c < D; c += 128) {
+      if (c + 1 < D && (D & 1) == 0) {
+        typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+        const bf2_t v = {(__bf16)col(c), (__bf16)col(c + 1)};
+        *reinterpret_cast<uint32_t*>(dst + c) = __builtin_bit_cast(uint32_t, v);
+      } else {
+        dst[c] = f2bf(col(c));
+        if (c + 1 < D) dst[c + 1] = f2bf(col(c + 1));
+      }
+    }
+  }
+}
+
+// Position-table gradients from the input gradient's position columns, for FewRel's shifted-arange
+// ids (pos[i][t] = pos[i][0] + t, ops/sampler.py::positions_are_shifted): table tb row p collects
+// dX[s][p - p0(s)][E + tb PD + c] over the sequences s with 0 <= p - p0(s) < L.  Thread = one output
+// (tb, p, c), grid.y = sequence chunks -> partials [chunks][2][P2][PD] (summed in order by the caller:
+// deterministic, no atomics).  dxp = dX's position columns, [S*L][2PD] fp32.
+__global__ __launch_bounds__(256) void wide_pos_grad_kernel(const float* __restrict__ dxp, const int* __restrict__ inst,
+                                                            const int* __restrict__ pos1, const int* __restrict__ pos2,
+                                                            int S, int L, int PD, int P2, int chunk,
+                                                            float* __restrict__ part) {
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  const int nout = 2 * P2 * PD;
+  if (o >= nout) return;
+  const int c = o % PD, p = (o / PD) % P2, tb = o / (PD * P2);
+  const int* pos = tb ? pos2 : pos1;
+  const int s0 = blockIdx.y * chunk, s1 = min(S, s0 + chunk);
+  float acc = 0.f;
+  for (int s = s0; s < s1; ++s) {
+    const int t = p - pos[(long)inst[s] * L];
+    if (t >= 0 && t < L) acc += dxp[((long)s * L + t) * 2 * PD + tb * PD + c];
+  }
+  part[(long)blockIdx.y * nout + o] = acc;
+}
+
+namespace ina {
+
+int wide_x_gather(const int* inst, int S, int L, const int* word, const int* pos1, const int* pos2, const float* wemb,
+                  int E, const float* p1emb, const float* p2emb, int PD, void* xb, hipStream_t st) {
+  const long rows = (long)S * L;
+  long blocks = (rows + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) return 0;
+  hipLaunchKernelGGL(wide_x_gather_kernel, dim3((int)blocks), dim3(256), 0, st, inst, S, L, word, pos1, pos2, wemb, E,
+                     p1emb, p2emb, PD, (unsigned short*)xb);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+int wide_pos_grad(const float* dxp, const int* inst, const int* pos1, const int* pos2, int S, int L, int PD, int P2,
+                  int chunks, float* part, hipStream_t st) {
+  const int nout = 2 * P2 * PD;
+  const int chunk = (S + chunks - 1) / chunks;
+  hipLaunchKernelGGL(wide_pos_grad_kernel, dim3((nout + 255) / 256, chunks), dim3(256), 0, st, dxp, inst, pos1, pos2, S,
+                     L, PD, P2, chunk, part);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace ina

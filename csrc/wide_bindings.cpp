@@ -91,9 +91,138 @@ void lstm_wide_bwd_step(const Tensor& dH, const Tensor& dhrec, const Tensor& dcr
               "ina.lstm_wide_bwd_step: launch failed");
 }
 
+// ---- persistent wide BiLSTM (one launch per pass; lstm_wide.hip lstm_wide_seq_*)
+int64_t wide_up(int64_t U) { return (U + 31) / 32 * 32; }
+
+// gx [2, S*L, 4UP] bf16 (x W_x, permuted + pre-scaled gate columns), bx [2, 4UP] fp32 biases, apk =
+// pack_lstm_wide's forward fragments -> (hout [S, L, 2U] bf16, hprev [2, S, L, UP] bf16,
+// acts [2, S*L, 4UP] bf16, cst [2, S*L, UP] fp16);
+// the last three only when stash (training), else empty
+std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_wide_seq_fwd(const Tensor& gx, const Tensor& bx, const Tensor& apk,
+                                                             int64_t S, int64_t L, int64_t U, bool stash, int64_t seed,
+                                                             double keep_prob) {
+  TORCH_CHECK(ina::lstm_wide_seq_supported((int)U), "ina.lstm_wide_seq_fwd: U must be 64, 100 or 128");
+  const int64_t UP = wide_up(U), G4 = 4 * UP, NW = UP / 16;
+  chk(gx, "gx", at::kBFloat16, 2 * S * L * G4);
+  chk(bx, "bx", at::kFloat, 2 * G4);
+  chk(apk, "apk", at::kBFloat16, 2 * NW * 4 * (UP / 32) * 64 * 8);
+  TORCH_CHECK(S * L * G4 < (1LL << 31) * 2, "ina.lstm_wide_seq_fwd: batch too large");
+  auto bopt = gx.options().dtype(at::kBFloat16), hopt = gx.options().dtype(at::kHalf);
+  auto hout = at::empty({S, L, 2 * U}, bopt);
+  auto hprev = stash ? at::empty({2, S, L, UP}, bopt) : at::empty({0}, bopt);
+  auto acts = stash ? at::empty({2, S * L, G4}, bopt) : at::empty({0}, bopt);
+  auto cst = stash ? at::empty({2, S * L, UP}, hopt) : at::empty({0}, hopt);
+  if (S == 0) return {hout, hprev, acts, cst};
+  ina::WideSeqArgs a{};
+  a.S = (int)S;
+  a.L = (int)L;
+  a.U = (int)U;
+  a.gx = gx.data_ptr();
+  a.bx = bx.data_ptr<float>();
+  a.apk = apk.data_ptr();
+  a.hprev = stash ? hprev.data_ptr() : nullptr;
+  a.acts = stash ? acts.data_ptr() : nullptr;
+  a.cst = stash ? cst.data_ptr() : nullptr;
+  a.hout = hout.data_ptr();
+  a.stash = stash ? 1 : 0;
+  ina::LstmWideArgs d{};
+  fill_drop(d, seed, keep_prob);
+  a.salt0 = d.salt0;
+  a.salt1 = d.salt1;
+  a.thr = d.thr;
+  a.inv_kp = d.inv_kp;
+  a.drop = d.drop;
+  TORCH_CHECK(ina::lstm_wide_seq_fwd(a, c10::hip::getCurrentHIPStream().stream()) == 0,
+              "ina.lstm_wide_seq_fwd: launch failed");
+  return {hout, hprev, acts, cst};
+}
+
+// dH [S, L, 2U] bf16 (gradient w.r.t. hout) + the forward's stash -> dG [2, S*L, 4UP] bf16 (permuted columns)
+Tensor lstm_wide_seq_bwd(const Tensor& dH, const Tensor& acts, const Tensor& cst, const Tensor& a2pk, int64_t S,
+                         int64_t L, int64_t U, int64_t seed, double keep_prob) {
+  TORCH_CHECK(ina::lstm_wide_seq_supported((int)U), "ina.lstm_wide_seq_bwd: U must be 64, 100 or 128");
+  const int64_t UP = wide_up(U), G4 = 4 * UP, NW = UP / 16;
+  chk(dH, "dH", at::kBFloat16, S * L * 2 * U);
+  chk(acts, "acts", at::kBFloat16, 2 * S * L * G4);
+  chk(cst, "cst", at::kHalf, 2 * S * L * UP);
+  chk(a2pk, "a2pk", at::kBFloat16, 2 * NW * (G4 / 32) * 64 * 8);
+  auto dG = at::empty({2, S * L, G4}, dH.options());
+  if (S == 0) return dG;
+  ina::WideSeqArgs a{};
+  a.S = (int)S;
+  a.L = (int)L;
+  a.U = (int)U;
+  a.dH = dH.data_ptr();
+  a.acts = acts.data_ptr();
+  a.cst = cst.data_ptr();
+  a.a2pk = a2pk.data_ptr();
+  a.dG = dG.data_ptr();
+  ina::LstmWideArgs d{};
+  fill_drop(d, seed, keep_prob);
+  a.salt0 = d.salt0;
+  a.salt1 = d.salt1;
+  a.thr = d.thr;
+  a.inv_kp = d.inv_kp;
+  a.drop = d.drop;
+  TORCH_CHECK(ina::lstm_wide_seq_bwd(a, c10::hip::getCurrentHIPStream().stream()) == 0,
+              "ina.lstm_wide_seq_bwd: launch failed");
+  return dG;
+}
+
+bool lstm_wide_seq_ok(int64_t U) { return ina::lstm_wide_seq_supported((int)U); }
+
+void chk_ids(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kInt, "ina.wide: ", name,
+              " must be a contiguous int32 GPU tensor");
+}
+
+// Xb [S*L, E + 2PD] bf16 = [word row ; pos1 row ; pos2 row] of every token of the rows inst
+Tensor wide_x_gather(const Tensor& inst, const Tensor& word, const Tensor& pos1, const Tensor& pos2,
+                     const Tensor& wemb, const Tensor& p1emb, const Tensor& p2emb) {
+  chk_ids(inst, "inst");
+  chk_ids(word, "word");
+  chk_ids(pos1, "pos1");
+  chk_ids(pos2, "pos2");
+  chk(wemb, "wemb", at::kFloat, wemb.numel());
+  chk(p1emb, "p1emb", at::kFloat, p1emb.numel());
+  chk(p2emb, "p2emb", at::kFloat, p2emb.numel());
+  const int64_t S = inst.size(0), L = word.size(1), E = wemb.size(1), PD = p1emb.size(1);
+  TORCH_CHECK(pos1.sizes() == word.sizes() && pos2.sizes() == word.sizes() && p2emb.size(1) == PD,
+              "ina.wide_x_gather: shapes");
+  auto xb = at::empty({S * L, E + 2 * PD}, wemb.options().dtype(at::kBFloat16));
+  TORCH_CHECK(ina::wide_x_gather(inst.data_ptr<int>(), (int)S, (int)L, word.data_ptr<int>(), pos1.data_ptr<int>(),
+                                 pos2.data_ptr<int>(), wemb.data_ptr<float>(), (int)E, p1emb.data_ptr<float>(),
+                                 p2emb.data_ptr<float>(), (int)PD, xb.data_ptr(),
+                                 c10::hip::getCurrentHIPStream().stream()) == 0,
+              "ina.wide_x_gather: launch failed");
+  return xb;
+}
+
+// position-table gradients [2, P2, PD] from dX's position columns dxp [S*L, 2PD] fp32 (shifted-arange ids)
+Tensor wide_pos_grad(const Tensor& dxp, const Tensor& inst, const Tensor& pos1, const Tensor& pos2, int64_t P2) {
+  chk_ids(inst, "inst");
+  chk_ids(pos1, "pos1");
+  chk_ids(pos2, "pos2");
+  const int64_t S = inst.size(0), L = pos1.size(1), PD = dxp.size(1) / 2;
+  chk(dxp, "dxp", at::kFloat, S * L * 2 * PD);
+  const int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(256, S / 64));
+  auto part = at::empty({chunks, 2, P2, PD}, dxp.options());
+  if (S == 0) return part.sum(0);
+  TORCH_CHECK(ina::wide_pos_grad(dxp.data_ptr<float>(), inst.data_ptr<int>(), pos1.data_ptr<int>(), pos2.data_ptr<int>(),
+                                 (int)S, (int)L, (int)PD, (int)P2, (int)chunks, part.data_ptr<float>(),
+                                 c10::hip::getCurrentHIPStream().stream()) == 0,
+              "ina.wide_pos_grad: launch failed");
+  return part.sum(0);
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(ina, m) {
   m.def("lstm_wide_fwd_step", &lstm_wide_fwd_step);
   m.def("lstm_wide_bwd_step", &lstm_wide_bwd_step);
+  m.def("lstm_wide_seq_fwd", &lstm_wide_seq_fwd);
+  m.def("lstm_wide_seq_bwd", &lstm_wide_seq_bwd);
+  m.def("lstm_wide_seq_ok", &lstm_wide_seq_ok);
+  m.def("wide_x_gather", &wide_x_gather);
+  m.def("wide_pos_grad", &wide_pos_grad);
 }

@@ -14,7 +14,8 @@ _DEV_CACHE = {}
 
 def _on(t: torch.Tensor, dev) -> torch.Tensor:
     """Device copy of a cached (lru_cache'd, hence immortal) host index tensor, made once: no per-step
-    host-to-device copies (and HIP-graph capturable)."""
+    host-to-device copies (and HIP-graph capturable).  The key is id(t): never pass a temporary (a
+    freed tensor's id is reused, and the cache would return another index table)."""
     key = (id(t), str(dev))
     v = _DEV_CACHE.get(key)
     if v is None:
@@ -259,3 +260,109 @@ def pack_ntn_w(w: torch.Tensor, h: int, N: int):
     dev = w.device
     we = torch.cat([w.detach().float().reshape(-1), w.new_zeros(1, dtype=torch.float32)])
     return we[_on(wi, dev)].to(torch.bfloat16).contiguous(), we[_on(wti, dev)].to(torch.bfloat16).contiguous()
+
+
+# ------------------------------------------------------------------ wide BiLSTM (lstm_wide.hip persistent kernels)
+LOG2E = 1.4426950408889634
+
+
+def wide_shape(U: int):
+    """Persistent wide-BiLSTM geometry (csrc/kernels/lstm_wide.hip WideCfg): UP = units padded to 32,
+    NW = UP / 16 waves per workgroup (16 units each), 4 forward M-tiles (16 gate rows = 4 units) and UP / 32
+    K-steps per wave, G4 = 4 UP permuted gate columns (column 4u + g), G4 / 32 backward K-steps."""
+    UP = (U + 31) // 32 * 32
+    return dict(UP=UP, NW=UP // 16, M=4, KS=UP // 32, G4=4 * UP, KS2=4 * UP // 32)
+
+
+def gate_scales(device=None) -> torch.Tensor:
+    """exp2 range factor per gate (i, j, f, o): the kernels evaluate sigmoid / tanh as exp2-based forms
+    of pre-scaled arguments (ina_common.h sigmoid_l2 / tanh_l2)."""
+    return torch.tensor([LOG2E, 2 * LOG2E, LOG2E, LOG2E], dtype=torch.float32, device=device)
+
+
+@lru_cache(maxsize=None)
+def _wide_idx(U: int):
+    """Index tables (into a padded [U+1, 4U+1] matrix whose last row / column are zero) for
+    * fwd A fragments [NW][M][KS][64][8]: row R = 4q' + g of M-tile m of wave w = gate g of unit
+      u = 16w + 4m + q'; k = 32 ks + 8 (l >> 4) + j = input unit; value W_h[k][g U + u]
+    * bwd A fragments [NW][KS2][64][8]: row R -> u_in = 16w + 4 (R & 3) + (R >> 2) (so the dh
+      accumulator register r of lane group q is unit 16w + 4r + q: the forward's lane ownership);
+      k = permuted gate column 4 u_out + g; value W_h[u_in][g U + u_out]
+    * permuted gate column c = 4u + g -> TF column g U + u (or the zero column)."""
+    s = wide_shape(U)
+    UP, NW, M, KS, G4, KS2 = s["UP"], s["NW"], s["M"], s["KS"], s["G4"], s["KS2"]
+    ZR, ZC = U, 4 * U
+    W = 4 * U + 1
+    l = np.arange(64)
+    R, kg = l & 15, l >> 4
+    j = np.arange(8)
+    fwd = np.empty((NW, M, KS, 64, 8), dtype=np.int64)
+    for w in range(NW):
+        for m in range(M):
+            u = 16 * w + 4 * m + (R >> 2)
+            g = R & 3
+            for ks in range(KS):
+                k = 32 * ks + 8 * kg[:, None] + j[None, :]
+                row = np.where(k < U, k, ZR)
+                col = np.where(u < U, g * U + u, ZC)[:, None]
+                fwd[w, m, ks] = row * W + np.where(k < U, col, ZC)
+    bwd = np.empty((NW, KS2, 64, 8), dtype=np.int64)
+    for w in range(NW):
+        u_in = 16 * w + 4 * (R & 3) + (R >> 2)
+        for ks in range(KS2):
+            k = 32 * ks + 8 * kg[:, None] + j[None, :]
+            u_out, g = k >> 2, k & 3
+            row = np.where(u_in < U, u_in, ZR)[:, None]
+            col = np.where(u_out < U, g * U + u_out, ZC)
+            bwd[w, ks] = row * W + col
+    c = np.arange(G4)
+    u, g = c >> 2, c & 3
+    perm = np.where(u < U, g * U + u, ZC)
+    gscale = np.array([LOG2E, 2 * LOG2E, LOG2E, LOG2E], dtype=np.float32)[g]
+    keep = u < U   # real (unpadded) permuted columns and their TF columns, for unpack_wide_grads
+    return (torch.from_numpy(fwd.reshape(-1)), torch.from_numpy(bwd.reshape(-1)), torch.from_numpy(perm),
+            torch.from_numpy(gscale), torch.from_numpy(c[keep]), torch.from_numpy(perm[keep]))
+
+
+def pack_lstm_wide(Kf: torch.Tensor, bf: torch.Tensor, Kb: torch.Tensor, bb: torch.Tensor, U: int, D: int):
+    """TF BasicLSTMCell kernels [D + U, 4U] + biases of both directions -> the persistent kernels'
+    operands:
+      wx   [2, D, G4] bf16   x-projection, permuted gate columns (4u + g), exp2-pre-scaled (gx GEMM)
+      bx   [2, G4]    fp32   bias (+1 on the forget gate), pre-scaled
+      wxt  [2, D, G4] bf16   the same columns UNscaled (dX = dG wxt^T)
+      apk  [2, NW, M, KS, 64, 8] bf16   forward W_h fragments, pre-scaled
+      a2pk [2, NW, KS2, 64, 8]   bf16   backward W_h fragments (true weights)"""
+    fwd_i, bwd_i, perm, gsc, _, _ = _wide_idx(U)
+    dev = Kf.device
+    fwd_i, bwd_i, perm, gsc = (_on(t, dev) for t in (fwd_i, bwd_i, perm, gsc))
+    outs = {k: [] for k in ("wx", "bx", "wxt", "apk", "a2pk")}
+    for K, b in ((Kf, bf), (Kb, bb)):
+        K = K.detach().float()
+        b = b.detach().float()
+        Wx = torch.nn.functional.pad(K[:D], (0, 1))                       # [D, 4U+1]
+        wxt = Wx[:, perm]                                                 # [D, G4]
+        outs["wxt"].append(wxt.to(torch.bfloat16))
+        outs["wx"].append((wxt * gsc).to(torch.bfloat16))
+        bfull = torch.nn.functional.pad(b, (0, 1))
+        fb = torch.zeros_like(bfull)
+        fb[2 * U:3 * U] = 1.0                                             # TF forget_bias
+        outs["bx"].append(((bfull + fb)[perm] * gsc).contiguous())
+        Wh = torch.nn.functional.pad(K[D:D + U], (0, 1, 0, 1)).reshape(-1)  # [U+1, 4U+1] flat
+        a = Wh[fwd_i].view(-1, 8)
+        # fwd fragment scale: the gate of row R = 4q' + g is g = (l & 15) & 3
+        gl = (torch.arange(a.shape[0], device=dev) // 1) % 64 % 16 % 4
+        outs["apk"].append((a * gate_scales(dev)[gl][:, None]).to(torch.bfloat16))
+        outs["a2pk"].append(Wh[bwd_i].to(torch.bfloat16))
+    return {k: torch.stack(v).contiguous() for k, v in outs.items()}
+
+
+def unpack_wide_grads(dwx: torch.Tensor, dwh: torch.Tensor, db: torch.Tensor, U: int):
+    """Permuted-gate-column gradients of one direction ([D, G4], [UP, G4], [G4]) -> TF layout
+    kernel [D + U, 4U] and bias [4U]."""
+    _, _, _, _, src, dst = _wide_idx(U)   # (lru-cached, immortal: safe keys for the device cache)
+    src, dst = _on(src, dwx.device), _on(dst, dwx.device)
+    K = torch.zeros(dwx.shape[0] + U, 4 * U, device=dwx.device, dtype=torch.float32)
+    K[:dwx.shape[0]].index_copy_(1, dst, dwx.float().index_select(1, src))
+    K[dwx.shape[0]:].index_copy_(1, dst, dwh[:U].float().index_select(1, src))
+    bias = torch.zeros(4 * U, device=db.device, dtype=torch.float32).index_copy_(0, dst, db.float().index_select(0, src))
+    return K, bias

@@ -98,6 +98,89 @@ class WideBiLSTM(torch.autograd.Function):
         return dX.view(S, L, D).to(ctx.xdtype), dKs[0], dbs[0], dKs[1], dbs[1], None, None, None
 
 
+class WideSeqBiLSTM(torch.autograd.Function):
+    """Embedding + BiLSTM of the wide path on hand-written kernels (lstm_wide.hip, U in {64, 100, 128}):
+      wide_x_gather     the encoder input rows Xb [S*L, E + 2PD] bf16 in one pass;
+      one GEMM          x W_x for both directions (permuted, pre-scaled gate columns, bf16 out);
+      lstm_wide_seq_fwd the whole forward recurrence in ONE launch (W_h in registers, h through LDS,
+                        fused bias / activations / DropoutWrapper output);
+      lstm_wide_seq_bwd the whole BPTT in one launch (dG stash); weight gradients as whole-sequence
+                        GEMMs; the input gradient only for the trainable columns (the reference's word table
+                        is frozen, model/base.py:55-59) and the position tables' gradient by
+                        wide_pos_grad (FewRel's shifted-arange position ids) or a one-hot GEMM."""
+
+    @staticmethod
+    def forward(ctx, inst, word, pos1, pos2, wemb, p1emb, p2emb, Kf, bf, Kb, bb, U, seed, keep_prob, pos_shift):
+        from .packing import pack_lstm_wide
+        o = ops()
+        S, L = inst.shape[0], word.shape[1]
+        E, P = wemb.shape[1], p1emb.shape[1]
+        D = E + 2 * P
+        pk = pack_lstm_wide(Kf, bf, Kb, bb, U, D)
+        Xb = o.wide_x_gather(inst, word, pos1, pos2, wemb.detach().float().contiguous(),
+                             p1emb.detach().float().contiguous(), p2emb.detach().float().contiguous())
+        # x W_x for both directions as ONE bf16-output GEMM (the kernel adds the fp32 biases): an fp32 output
+        # plus a separate bias pass moved ~15 GB per step at the paper configuration
+        gx = torch.bmm(Xb.unsqueeze(0).expand(2, -1, -1), pk["wx"])
+        need = any(ctx.needs_input_grad[4:11])
+        hout, hprev, acts, cst = o.lstm_wide_seq_fwd(gx, pk["bx"], pk["apk"], S, L, U, bool(need), int(seed),
+                                                     float(keep_prob))
+        if need:
+            ctx.save_for_backward(inst, word, pos1, pos2, Xb, pk["wxt"], pk["a2pk"], hprev, acts, cst)
+            ctx.cfg = (S, L, E, P, U, int(seed), float(keep_prob), bool(pos_shift), p1emb.shape[0], wemb.shape[0])
+        return hout
+
+    @staticmethod
+    def backward(ctx, dout):
+        from .packing import unpack_wide_grads
+        o = ops()
+        inst, word, pos1, pos2, Xb, wxt, a2pk, hprev, acts, cst = ctx.saved_tensors
+        S, L, E, P, U, seed, kp, shift, P2, V = ctx.cfg
+        dG = o.lstm_wide_seq_bwd(dout.contiguous().to(torch.bfloat16), acts, cst, a2pk, S, L, U, seed, kp)
+        UP = hprev.shape[-1]
+        dKs, dbs = [], []
+        for d in range(2):
+            g = dG[d]
+            dK, db = unpack_wide_grads(_wgrad(Xb, g), _wgrad(hprev[d].reshape(S * L, UP), g),
+                                       g.sum(0, dtype=torch.float32), U)
+            dKs.append(dK)
+            dbs.append(db)
+        need_w = ctx.needs_input_grad[4]
+        cols = slice(0, E + 2 * P) if need_w else slice(E, E + 2 * P)
+        dX = torch.mm(dG[0], wxt[0][cols].t(), out_dtype=torch.float32)
+        dX += torch.mm(dG[1], wxt[1][cols].t(), out_dtype=torch.float32)
+        dxp = dX[:, -2 * P:].contiguous()
+        if shift:
+            tp = o.wide_pos_grad(dxp, inst, pos1, pos2, P2)
+            dp1, dp2 = tp[0], tp[1]
+        else:
+            il = inst.long()
+            dp1 = table_grad(pos1[il].reshape(-1).long(), dxp[:, :P], P2)
+            dp2 = table_grad(pos2[il].reshape(-1).long(), dxp[:, P:], P2)
+        dw = None
+        if need_w:
+            dw = table_grad(word[inst.long()].reshape(-1).long(), dX[:, :E], V)
+        return (None, None, None, None, dw, dp1, dp2, dKs[0], dbs[0], dKs[1], dbs[1], None, None, None, None)
+
+
+def table_grad(idx: torch.Tensor, d: torch.Tensor, rows: int) -> torch.Tensor:
+    """sum of the rows d[i] into table row idx[i] -- deterministic: a one-hot GEMM, split-K for small tables
+    (autograd's index backward is a sort + segmented accumulate, 14 ms per [74, 5] table per step at the
+    paper configuration); index_add_ for large tables (trained word embeddings)."""
+    if rows > 4096:
+        return torch.zeros(rows, d.shape[1], device=d.device, dtype=torch.float32).index_add_(0, idx, d.float())
+    fd = d.float()
+    T, C = fd.shape
+    nb = SmallTableGather.SPLIT
+    Tp = (T + nb - 1) // nb * nb
+    fi = idx
+    if Tp != T:   # pad with tokens of zero gradient
+        fi = torch.cat([fi, fi.new_zeros(Tp - T)])
+        fd = torch.cat([fd, fd.new_zeros(Tp - T, C)])
+    oh = torch.nn.functional.one_hot(fi, rows).to(torch.float32).view(nb, Tp // nb, rows)
+    return torch.bmm(oh.transpose(1, 2), fd.view(nb, Tp // nb, C)).sum(0)
+
+
 class SmallTableGather(torch.autograd.Function):
     """rows = table[idx] for a SMALL table (the [2L, 5] position tables).  Autograd's index backward
     scatters 1.2 M token gradients into ~74 rows with a sort + segmented accumulate that measured
@@ -117,18 +200,8 @@ class SmallTableGather(torch.autograd.Function):
     @staticmethod
     def backward(ctx, d):
         (idx,) = ctx.saved_tensors
-        P = ctx.rows
         fi = idx.reshape(-1)
-        fd = d.reshape(fi.shape[0], -1).float()
-        T, C = fd.shape
-        nb = SmallTableGather.SPLIT
-        Tp = (T + nb - 1) // nb * nb
-        if Tp != T:   # pad with tokens of zero gradient
-            fi = torch.cat([fi, fi.new_zeros(Tp - T)])
-            fd = torch.cat([fd, fd.new_zeros(Tp - T, C)])
-        oh = torch.nn.functional.one_hot(fi, P).to(torch.float32).view(nb, Tp // nb, P)
-        g = torch.bmm(oh.transpose(1, 2), fd.view(nb, Tp // nb, C)).sum(0)
-        return g.to(d.dtype), None
+        return table_grad(fi, d.reshape(fi.shape[0], -1), ctx.rows).to(d.dtype), None
 
 
 class ProjBF16(torch.autograd.Function):
@@ -171,12 +244,20 @@ def attention_wide(H, mask, W1, b1, w2):
 def encode_wide(inst, data, p, U: int, keep_prob: float, seed: int):
     """Wide GPU encoder: embedding gather + WideBiLSTM + self-attention (GEMM formulation)."""
     from ..models import reference as ref
+    if ops().lstm_wide_seq_ok(U):   # hand-written kernels end to end (u in {64, 100, 128})
+        wa, p1a, p2a, ma = data
+        H = WideSeqBiLSTM.apply(inst, wa, p1a, p2a, p["word_embedding"], p["pos1_embedding"], p["pos2_embedding"],
+                                p["lstm_fw_kernel"], p["lstm_fw_bias"], p["lstm_bw_kernel"], p["lstm_bw_bias"], U,
+                                int(seed), float(keep_prob), bool(getattr(data, "pos_shift", False)))
+        e, alphas = attention_wide(H, ma[inst.long()] > 0, p["attn_kernel"], p["attn_bias"], p["attn_w2"])
+        return e, alphas.squeeze(-1)
     word, pos1, pos2, mask = (t[inst.long()] for t in data)
     # the encoder input is built in bf16 (the GEMM operand dtype): half the concat traffic and no
     # separate fp32 -> bf16 pass; autograd casts the fp32 input gradient back for the position tables
     bf = torch.bfloat16
-    X = torch.cat([p["word_embedding"][word.long()].to(bf), SmallTableGather.apply(p["pos1_embedding"], pos1.long()).to(bf),
-                   SmallTableGather.apply(p["pos2_embedding"], pos2.long()).to(bf)], -1)
+    Xp = torch.cat([SmallTableGather.apply(p["pos1_embedding"], pos1.long()),
+                    SmallTableGather.apply(p["pos2_embedding"], pos2.long())], -1)
+    X = torch.cat([p["word_embedding"][word.long()].to(bf), Xp.to(bf)], -1)
     H = WideBiLSTM.apply(X, p["lstm_fw_kernel"], p["lstm_fw_bias"], p["lstm_bw_kernel"], p["lstm_bw_bias"], U,
                          int(seed), float(keep_prob))
     e, alphas = attention_wide(H, mask > 0, p["attn_kernel"], p["attn_bias"], p["attn_w2"])

@@ -99,3 +99,63 @@ def test_rec_attn_pack_zero_padding():
         Z = (2 * U) ** 2
         assert int(pi.max()) <= Z and int(ti.max()) <= Z
         assert torch.all((pi >= 0) & (ti >= 0))
+
+
+def test_wide_lstm_packs_emulated_mfma():
+    """ops/packing.py::pack_lstm_wide against a numpy emulation of v_mfma_f32_16x16x32_bf16's lane
+    layout (lane l: A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15]): the forward fragments give each
+    lane group q the 4 (pre-scaled) gates of unit 16w + 4m + q, the backward fragments give dh of unit
+    16w + 4r + q in accumulator register r (the forward's ownership), and the permuted x-projection /
+    bias columns c = 4u + g round-trip through unpack_wide_grads."""
+    import torch
+    from induction_network_on_fewrel_amd.ops.packing import (LOG2E, pack_lstm_wide, unpack_wide_grads,
+                                                              wide_shape)
+    for U, D in ((100, 310), (128, 60), (64, 15)):
+        g = torch.Generator().manual_seed(U)
+        Kf, Kb = torch.randn(D + U, 4 * U, generator=g), torch.randn(D + U, 4 * U, generator=g)
+        bf_, bb_ = torch.randn(4 * U, generator=g), torch.randn(4 * U, generator=g)
+        s = wide_shape(U)
+        NW, M, KS, G4, KS2, UP = s["NW"], s["M"], s["KS"], s["G4"], s["KS2"], s["UP"]
+        p = pack_lstm_wide(Kf, bf_, Kb, bb_, U, D)
+        sc = np.array([LOG2E, 2 * LOG2E, LOG2E, LOG2E])
+        for d, (K, b) in enumerate(((Kf, bf_), (Kb, bb_))):
+            Wh = K[D:].double().numpy()
+            rb = lambda x: torch.tensor(x).float().bfloat16().double().numpy()   # the packs' bf16 rounding
+            h = np.zeros(UP)
+            h[:U] = np.random.default_rng(1).standard_normal(U)
+            A = p["apk"][d].float().double().numpy().reshape(NW, M, KS, 64, 8)
+            for w in range(NW):
+                for m in range(M):
+                    acc = np.zeros(16)
+                    for ks in range(KS):
+                        for lane in range(64):
+                            R, kg = lane & 15, lane >> 4
+                            acc[R] += sum(A[w, m, ks, lane, j] * h[32 * ks + 8 * kg + j] for j in range(8))
+                    for R in range(16):
+                        u, gg = 16 * w + 4 * m + (R >> 2), R & 3
+                        wcol = (K[D:, gg * U + u].float() * torch.tensor(sc[gg], dtype=torch.float32)) if u < U else None
+                        want = wcol.bfloat16().double().numpy() @ h[:U] if u < U else 0.0
+                        assert abs(acc[R] - want) <= 1e-9 * (1 + abs(want)), (U, d, w, m, R)
+            dGn = np.random.default_rng(2).standard_normal((4, U))
+            dGp = np.zeros(G4)
+            for u in range(U):
+                dGp[4 * u:4 * u + 4] = dGn[:, u]
+            A2 = p["a2pk"][d].float().double().numpy().reshape(NW, KS2, 64, 8)
+            for w in range(NW):
+                acc = np.zeros(16)
+                for ks in range(KS2):
+                    for lane in range(64):
+                        R, kg = lane & 15, lane >> 4
+                        acc[R] += sum(A2[w, ks, lane, j] * dGp[32 * ks + 8 * kg + j] for j in range(8))
+                for q in range(4):
+                    for r in range(4):
+                        u_in = 16 * w + 4 * r + q
+                        want = sum(rb(Wh[u_in, gg * U: gg * U + U]) @ dGn[gg] for gg in range(4)) if u_in < U else 0.0
+                        assert abs(acc[4 * q + r] - want) <= 1e-9 * (1 + abs(want)), (U, d, w, q, r)
+            # x-projection columns / bias, and the gradient un-permutation
+            wxt = p["wxt"][d].float()
+            assert torch.allclose(wxt[:, 4 * 3 + 2], K[:D, 2 * U + 3].bfloat16().float())
+            assert abs(float(p["bx"][d][4 * 5 + 2]) - (float(b[2 * U + 5]) + 1.0) * LOG2E) < 1e-5
+            dK, db = unpack_wide_grads(wxt, torch.nn.functional.pad(K[D:].bfloat16().float()[:, :0], (0, G4)),
+                                       torch.zeros(G4), U)
+            assert torch.allclose(dK[:D], K[:D].bfloat16().float())

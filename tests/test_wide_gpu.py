@@ -17,7 +17,7 @@ def _relerr(a, b):
     return float((a - b).abs().max() / (b.abs().max() + 1e-12))
 
 
-def _setup(u, E, impl, kp_train=True, N=5, K=2, Q=3, B=3, L=37):
+def _setup(u, E, impl, kp_train=True, N=5, K=2, Q=3, B=3, L=37, shifted=True):
     cfg = Config(N=N, K=K, Q=Q, max_length=L, hidden_size=u, lstm_impl=impl, relation_head="reference")
     data = make_synthetic(num_relations=10, instances_per_relation=30, max_length=L, vocab=800, word_dim=E, seed=1)
     torch.manual_seed(0)
@@ -27,14 +27,20 @@ def _setup(u, E, impl, kp_train=True, N=5, K=2, Q=3, B=3, L=37):
             getattr(model.params, n).copy_(torch.randn_like(getattr(model.params, n)) * 0.3)
     idx, lab = EpisodeSampler(data, seed=2).next_batch_indices(B, N, K, Q)
     inst = torch.tensor(idx.reshape(-1), dtype=torch.int32, device=DEV)
-    arrays = tuple(torch.as_tensor(a).to(DEV) for a in (data.data_word, data.data_pos1, data.data_pos2,
-                                                        data.data_mask))
+    from induction_network_on_fewrel_amd.ops.sampler import DeviceDataset
+    arrays = DeviceDataset(data, DEV).arrays()   # pos_shift: the wide_pos_grad kernel path
+    if not shifted:
+        arrays = tuple(arrays)                   # plain tuple: the one-hot GEMM path
     return cfg, model, inst, arrays, torch.tensor(lab, device=DEV), (B, N, K, Q)
 
 
+@pytest.mark.parametrize("u", [100, 128, 64])
 @pytest.mark.parametrize("keep_prob", [1.0, 0.9])
-def test_paper_config_forward_backward_vs_oracle(keep_prob):
-    cfg, model, inst, arrays, lab, (B, N, K, Q) = _setup(128, 50, "auto")
+def test_paper_config_forward_backward_vs_oracle(keep_prob, u):
+    """u=128 (the paper), u=100 (the reference Base default, model/base.py:16) and u=64 on the persistent
+    wide BiLSTM kernels (lstm_wide.hip lstm_wide_seq_*) + the wide head, against the fp32 oracle; the
+    position-table gradient by wide_pos_grad (shifted ids) for keep_prob 1, by the one-hot GEMM for 0.9."""
+    cfg, model, inst, arrays, lab, (B, N, K, Q) = _setup(u, 50, "auto", shifted=keep_prob == 1.0)
     cfg.keep_prob = keep_prob
     assert not model.use_fused_lstm(37)
     probs, _ = model(inst, arrays, B, N, K, Q, training=True, dropout_seed=5)
