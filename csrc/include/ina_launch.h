@@ -191,8 +191,8 @@ struct WideSeqArgs {
   const void* apk;        // [2][NW][4][KS][64] x 8 bf16 forward W_h fragments (pre-scaled)
   const void* a2pk;       // [2][NW][KS2][64] x 8 bf16 backward W_h fragments
   void* hprev;            // [2][S][L][UP] bf16: each step's recurrent input h_{t-1} (dW_h GEMM operand)
-  void* acts;             // [2][S][L][G4] bf16: i, j, f, o activations
-  void* cst;              // [2][S][L][UP] fp16: cell states
+  void* acts;             // i, j, f, o activations, bf16, tile-major (lstm_wide.hip WideStash)
+  void* cst;              // cell states, fp16, tile-major (lstm_wide.hip WideStash)
   void* hout;             // [S][L][2U] bf16: DropoutWrapper output (attention input)
   const void* dH;         // [S][L][2U] bf16: gradient w.r.t. hout
   void* dG;               // [2][S][L][G4] bf16: pre-activation gate gradients
@@ -208,6 +208,28 @@ int wide_pos_grad(const float* dxp, const int* inst, const int* pos1, const int*
                   int chunks, float* part, hipStream_t st);
 int lstm_wide_seq_fwd(const WideSeqArgs& a, hipStream_t st);
 int lstm_wide_seq_bwd(const WideSeqArgs& a, hipStream_t st);
+
+// self-attention pooling over the wide BiLSTM outputs, H = 2u in {128, 200, 256} (attn_wide.hip)
+struct WideAttnArgs {
+  int S, L, H, SB;        // SB sequences per workgroup
+  const void* hin;        // [S][L][H] bf16 (the BiLSTM output)
+  const int* inst;        // [S] dataset rows of the sequences
+  const int* mask;        // [rows][L] int32, > 0 = real token
+  const void* w1t;        // [HP/16][HP/32][64] x 8 bf16: A fragments of W1^T (row j, k = input feature)
+  const void* w1;         // [HP/16][HP/32][64] x 8 bf16: A fragments of W1 (row k, k-dim j)
+  const float* b1;        // [HP]
+  const float* w2;        // [HP]
+  float* e;               // forward: [S][H] pooled output
+  float* alpha;           // forward out / backward in: [S][L]
+  const float* de;        // backward: [S][H]
+  void* dH;               // backward: [S][L][H] bf16
+  void* dZ;               // backward: [S*L][H] bf16 (pre-activation gradient, the dW1 GEMM operand)
+  float* part;            // backward: [grid][2][HP] (dw2, db1) partial sums
+};
+int wide_attn_hp(int H);
+size_t wide_attn_smem(int H, int L, int SB, bool bwd);
+int wide_attn_fwd(const WideAttnArgs& a, hipStream_t st);
+int wide_attn_bwd(const WideAttnArgs& a, hipStream_t st);
 
 // ---------------------------------------------------------------- BERT (csrc/kernels/bert.hip)
 struct BertLnArgs {          // y = LN(res + dropout(a)); HD = 256 * {1..4}

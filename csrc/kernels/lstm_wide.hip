@@ -152,22 +152,28 @@ int lstm_wide_bwd_step(const LstmWideArgs& a, int tau, hipStream_t st) {
 //   * each wave keeps ITS slice of W_h as MFMA A fragments in VGPRs for the whole sequence
 //     (forward: 4 M-tiles x UP/32 K-steps; backward: UP*4/32 K-steps over the permuted gate columns);
 //   * gates are computed transposed, G^T[gate rows, seqs] = W_h^T h^T (+ the precomputed x W_x + b),
-//     with the row order chosen so lane group q holds the 4 gates of unit 16w + 4m + q in its 4
-//     accumulator registers (the lane-ownership layout of lstm.hip): c and h never leave the lane;
+//     with the row order chosen so lane group q holds, in M-tile m, the 4 gates of unit 16w + 4q + m:
+//     a lane owns 4 CONTIGUOUS units (one 32-byte gate load / dG store, one 8-byte h write per tile);
+//     c and h never leave the lane (the lane-ownership layout of lstm.hip);
 //   * h_t is exchanged through a double-buffered LDS image [32 seqs][UP] bf16 (the next step's B
 //     operand), ONE workgroup barrier per step; the same image feeds coalesced row copies of the
 //     attention input (DropoutWrapper applied) and the backward's h_{t-1} stash;
+//   * every global input of a step (forward: x W_x; backward: activations, cells, attention gradient)
+//     is loaded one step ahead into ping-pong registers (loops unrolled by two), so HBM latency hides
+//     behind the previous step's recurrence instead of sitting on the serial chain;
+//   * the activation / cell stash is tile-major (WideStash): 512 contiguous bytes per wave access;
 //   * backward: dG (bf16) goes to an LDS image [32][4 UP] and is contracted with the backward W_h
-//     fragments, whose row permutation lands dh of unit 16w + 4r + q in accumulator register r of
-//     lane group q -- the lane that owns that unit's gates.
-// Gate columns are permuted to c = 4u + g (unit-major, the 4 gates of a unit adjacent: one 16-byte
-// gx load, one 8-byte acts / dG store per lane and unit).  ops/packing.py::pack_lstm_wide builds the
-// fragments and is checked by tests/test_packing.py's MFMA-layout emulation.
+//     fragments, whose rows land dh of unit 16w + 4q + r in accumulator register r of lane group q --
+//     the lane that owns that unit's gates.
+// Gate columns are permuted to c = 4u + g (unit-major, the 4 gates of a unit adjacent).
+// ops/packing.py::pack_lstm_wide builds the fragments and is checked by tests/test_packing.py's
+// MFMA-layout emulation.
 // ==========================================================================================
 namespace {
 
 template <int U>
 struct WideCfg {
+  static_assert(U % 4 == 0, "a lane owns 4 contiguous units: U must be a multiple of 4");
   static constexpr int UP = (U + 31) / 32 * 32;
   static constexpr int NW = UP / 16;     // waves per workgroup
   static constexpr int M = 4;            // forward M-tiles per wave (16 gate rows = 4 units)
@@ -188,13 +194,35 @@ INA_DEVICE uint32_t pack_bf2(float a, float b) {
 
 }  // namespace
 
+INA_DEVICE uint32_t pack_h2(float a, float b) {
+  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+  const h2_t v = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+INA_DEVICE float2 unpack_h2(uint32_t v) {
+  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+  const h2_t h = __builtin_bit_cast(h2_t, v);
+  return float2{(float)h.x, (float)h.y};
+}
+
+// Tile-major stash (internal to the forward/backward pair, any layout works): per (dir, tile, t) one
+// contiguous block, [NW][M][NT][64 lanes] x uint2 (4 bf16 activations) and [NW][NT][64] x uint2
+// (the 4 fp16 cells of a lane's 4 units), so every stash load/store of a wave is 512 contiguous bytes.
+template <int U>
+struct WideStash {
+  using C = WideCfg<U>;
+  static constexpr int ASTEP = C::NW * C::M * C::NT * 64;   // uint2 per (dir, tile, t)
+  static constexpr int CSTEP = C::NW * C::NT * 64;
+};
+
 template <int U>
 __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_fwd_kernel(
     const unsigned short* __restrict__ gx, const float* __restrict__ bx, const u16x8_t* __restrict__ apk, int S, int L,
-    unsigned short* __restrict__ hprev, unsigned short* __restrict__ acts, _Float16* __restrict__ cst,
+    unsigned short* __restrict__ hprev, uint2* __restrict__ acts, uint2* __restrict__ cst,
     unsigned short* __restrict__ hout, uint32_t salt0, uint32_t salt1, uint32_t thr, float inv_kp, int drop,
     int stash) {
   using C = WideCfg<U>;
+  using Z = WideStash<U>;
   constexpr int UP = C::UP, NW = C::NW, M = C::M, KS = C::KS, G4 = C::G4, NT = C::NT, HS = C::HS, SEQ = C::SEQ;
   constexpr int NTH = NW * 64;
   __shared__ __attribute__((aligned(16))) unsigned short himg[2][SEQ * HS];
@@ -213,23 +241,36 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_fwd_kernel(
   __syncthreads();
   float c[M][NT];
   int srow[NT];
-  bool sval[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int s = s0 + nt * 16 + n;
-    sval[nt] = s < S;
-    srow[nt] = sval[nt] ? s : S - 1;
+    srow[nt] = s < S ? s : S - 1;   // tail rows recompute the last sequence (their stash rows are padding)
 #pragma unroll
     for (int m = 0; m < M; ++m) c[m][nt] = 0.f;
   }
-  const int ub = 16 * w;   // the wave's units: ub + 4m + q
-  float4 bias[M];          // pre-scaled gate biases of the lane's units (forget gate +1)
+  const int u0 = 16 * w + 4 * q;   // the lane's 4 contiguous units u0 + m (packing.py _wide_idx)
+  float4 bias[M];                  // pre-scaled gate biases of the lane's units (forget gate +1)
 #pragma unroll
-  for (int m = 0; m < M; ++m) bias[m] = *reinterpret_cast<const float4*>(bx + dir * G4 + 4 * (ub + 4 * m + q));
-  // row-copy geometry: one 16-byte chunk (8 units) of one sequence row per thread and pass
-  constexpr int CH = UP / 8, NCH = SEQ * CH;
-  for (int tau = 0; tau < L; ++tau) {
+  for (int m = 0; m < M; ++m) bias[m] = *reinterpret_cast<const float4*>(bx + dir * G4 + 4 * (u0 + m));
+  uint2* const actp = acts + (size_t)(dir * gridDim.x + blockIdx.x) * L * Z::ASTEP + w * (M * NT * 64) + lane;
+  uint2* const cstp = cst + (size_t)(dir * gridDim.x + blockIdx.x) * L * Z::CSTEP + w * (NT * 64) + lane;
+  // x W_x of one step (bf16, 4 gates x 4 units = 32 contiguous bytes per lane and tile): software-
+  // pipelined one step ahead so the HBM latency hides behind the previous step's recurrence
+  auto load_gx = [&](int t, uint4 (&g)[NT][2]) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const uint4* src = reinterpret_cast<const uint4*>(gx + (((size_t)dir * S + srow[nt]) * L + t) * G4 + 4 * u0);
+      g[nt][0] = src[0];
+      g[nt][1] = src[1];
+    }
+  };
+  constexpr int CH = UP / 8, NCH = SEQ * CH;   // row copies: one 16-byte chunk (8 units) per thread and pass
+  // one step; gcur holds its x W_x, gnx receives the next step's (ping-pong buffers: the loop below is
+  // unrolled by two so no register copy forces an early wait on the prefetch)
+  auto step = [&](int tau, const uint4 (&gcur)[NT][2], uint4 (&gnx)[NT][2]) __attribute__((always_inline)) {
     const int t = dir ? L - 1 - tau : tau;
+    const int tn = tau + 1 < L ? (dir ? t - 1 : t + 1) : t;
+    load_gx(tn, gnx);
     const unsigned short* hin = himg[tau & 1];
     unsigned short* hnx = himg[(tau + 1) & 1];
     if (stash) {   // this step's recurrent input h_{t-1} -> hprev[dir][s][t] (the dW_h GEMM's rows)
@@ -246,26 +287,29 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_fwd_kernel(
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) B[nt][ks] = *reinterpret_cast<const u16x8_t*>(hin + (nt * 16 + n) * HS + 32 * ks + 8 * q);
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const int u = ub + 4 * m + q;
+    for (int nt = 0; nt < NT; ++nt) {
+      const uint32_t gw[8] = {gcur[nt][0].x, gcur[nt][0].y, gcur[nt][0].z, gcur[nt][0].w,
+                              gcur[nt][1].x, gcur[nt][1].y, gcur[nt][1].z, gcur[nt][1].w};
+      float hv[M];
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const size_t row = ((size_t)dir * S + srow[nt]) * L + t;
-        const uint2 g4 = *reinterpret_cast<const uint2*>(gx + row * G4 + 4 * u);   // bf16 x W_x (4 gates)
-        f32x4_t acc = {bias[m].x + bf2f((unsigned short)g4.x), bias[m].y + bf2f((unsigned short)(g4.x >> 16)),
-                       bias[m].z + bf2f((unsigned short)g4.y), bias[m].w + bf2f((unsigned short)(g4.y >> 16))};
+      for (int m = 0; m < M; ++m) {
+        f32x4_t acc = {bias[m].x + bf2f((unsigned short)gw[2 * m]), bias[m].y + bf2f((unsigned short)(gw[2 * m] >> 16)),
+                       bias[m].z + bf2f((unsigned short)gw[2 * m + 1]),
+                       bias[m].w + bf2f((unsigned short)(gw[2 * m + 1] >> 16))};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) acc = mfma_bf16(A[m][ks], B[nt][ks], acc);
         const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
         const float cn = c[m][nt] * fg + ig * jg;
         c[m][nt] = cn;
-        const float hv = tanh_l2(cn * (2.f * LOG2E_F)) * og;
-        hnx[(nt * 16 + n) * HS + u] = f2bf(hv);
-        if (stash && sval[nt]) {
-          *reinterpret_cast<uint2*>(acts + row * G4 + 4 * u) = uint2{pack_bf2(ig, jg), pack_bf2(fg, og)};
-          cst[row * UP + u] = (_Float16)cn;   // fp16 cell state (|c| <= L: far inside range, 11-bit mantissa)
-        }
+        hv[m] = tanh_l2(cn * (2.f * LOG2E_F)) * og;
+        if (stash) actp[(size_t)t * Z::ASTEP + (m * NT + nt) * 64] = uint2{pack_bf2(ig, jg), pack_bf2(fg, og)};
       }
+      *reinterpret_cast<uint2*>(hnx + (nt * 16 + n) * HS + u0) = uint2{pack_bf2(hv[0], hv[1]), pack_bf2(hv[2], hv[3])};
+    }
+    if (stash) {   // fp16 cells (|c| <= L: far inside range, 11-bit mantissa), the lane's 4 units per store
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        cstp[(size_t)t * Z::CSTEP + nt * 64] = uint2{pack_h2(c[0][nt], c[1][nt]), pack_h2(c[2][nt], c[3][nt])};
     }
     __syncthreads();   // hnx complete; every wave is past its reads of hin
     // attention input h_t (DropoutWrapper: keep ? h / keep_prob : 0, one hash per unit pair as the
@@ -282,15 +326,24 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_fwd_kernel(
       }
       *reinterpret_cast<uint32_t*>(hout + ((size_t)s * L + t) * 2 * U + dir * U + u) = o;
     }
+  };
+  uint4 g0[NT][2], g1[NT][2];
+  load_gx(dir ? L - 1 : 0, g0);
+  int tau = 0;
+  for (; tau + 1 < L; tau += 2) {
+    step(tau, g0, g1);
+    step(tau + 1, g1, g0);
   }
+  if (tau < L) step(tau, g0, g1);
 }
 
 template <int U>
 __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_bwd_kernel(
-    const unsigned short* __restrict__ dH, const unsigned short* __restrict__ acts, const _Float16* __restrict__ cst,
+    const unsigned short* __restrict__ dH, const uint2* __restrict__ acts, const uint2* __restrict__ cst,
     const u16x8_t* __restrict__ a2pk, unsigned short* __restrict__ dG, int S, int L, uint32_t salt0, uint32_t salt1,
     uint32_t thr, float inv_kp, int drop) {
   using C = WideCfg<U>;
+  using Z = WideStash<U>;
   constexpr int UP = C::UP, NW = C::NW, M = C::M, G4 = C::G4, KS2 = C::KS2, NT = C::NT, GS = C::GS, SEQ = C::SEQ;
   __shared__ __attribute__((aligned(16))) unsigned short gimg[2][SEQ * GS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4, n = lane & 15;
@@ -310,58 +363,106 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_bwd_kernel(
     sval[nt] = s < S;
     srow[nt] = sval[nt] ? s : S - 1;
   }
-  f32x4_t dhr[NT];     // dh of units ub + 4r + q (register r), from the previous processed step
+  const int u0 = 16 * w + 4 * q;   // the lane's 4 contiguous units (the forward's ownership)
+  const bool uval = u0 < U;        // U % 4 == 0: a lane's units are all real or all padding
+  const uint2* const actp = acts + (size_t)(dir * gridDim.x + blockIdx.x) * L * Z::ASTEP + w * (M * NT * 64) + lane;
+  const uint2* const cstp = cst + (size_t)(dir * gridDim.x + blockIdx.x) * L * Z::CSTEP + w * (NT * 64) + lane;
+  // one step's inputs, loaded a step ahead: activations, the previous step's cells, attention gradient
+  struct In {
+    uint2 a[M][NT];
+    uint2 cp[NT];
+    uint2 dout[NT];   // raw attention gradient of the 4 units (bf16): no use of the loaded values here
+  };
+  auto load_in = [&](int tau, In& v) {
+    const int t = dir ? L - 1 - tau : tau;
+    const int tp = tau > 0 ? (dir ? t + 1 : t - 1) : t;   // the step before in processing order
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) v.a[m][nt] = actp[(size_t)t * Z::ASTEP + (m * NT + nt) * 64];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      v.cp[nt] = cstp[(size_t)tp * Z::CSTEP + nt * 64];
+      if (tau == 0) v.cp[nt] = uint2{0u, 0u};
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)   // padding units: any valid address, masked at use
+      v.dout[nt] = *reinterpret_cast<const uint2*>(dH + ((size_t)srow[nt] * L + t) * 2 * U + dir * U + min(u0, U - 4));
+  };
+  f32x4_t dhr[NT];     // dh of units u0 + r (register r), from the previous processed step
   float dcr[M][NT];
+  uint2 cn2[NT];       // this step's cells (the previous iteration's c_{t-1})
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     dhr[nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    cn2[nt] = cstp[(size_t)(dir ? 0 : L - 1) * Z::CSTEP + nt * 64];
 #pragma unroll
     for (int m = 0; m < M; ++m) dcr[m][nt] = 0.f;
   }
-  const int ub = 16 * w;
-  for (int tau = L - 1; tau >= 0; --tau) {
+  auto step = [&](int tau, const In& cur, In& nx) __attribute__((always_inline)) {
     const int t = dir ? L - 1 - tau : tau;
-    const int tp = dir ? t + 1 : t - 1;   // the step before in processing order (its c is c_{t-1})
+    load_in(tau > 0 ? tau - 1 : 0, nx);
     unsigned short* gcur = gimg[tau & 1];
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const int u = ub + 4 * m + q;
+    for (int nt = 0; nt < NT; ++nt) {
+      const float2 c01 = unpack_h2(cn2[nt].x), c23 = unpack_h2(cn2[nt].y);
+      const float2 p01 = unpack_h2(cur.cp[nt].x), p23 = unpack_h2(cur.cp[nt].y);
+      const float cnv[M] = {c01.x, c01.y, c23.x, c23.y}, cpv[M] = {p01.x, p01.y, p23.x, p23.y};
+      const size_t row = ((size_t)dir * S + srow[nt]) * L + t;
+      const float dov[M] = {bf2f((unsigned short)cur.dout[nt].x), bf2f((unsigned short)(cur.dout[nt].x >> 16)),
+                            bf2f((unsigned short)cur.dout[nt].y), bf2f((unsigned short)(cur.dout[nt].y >> 16))};
+      uint32_t gw[2 * M];
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const size_t row = ((size_t)dir * S + srow[nt]) * L + t;
-        const uint2 av = *reinterpret_cast<const uint2*>(acts + row * G4 + 4 * u);
+      for (int m = 0; m < M; ++m) {
+        const int u = u0 + m;
+        const uint2 av = cur.a[m][nt];
         const float ig = bf2f((unsigned short)av.x), jg = bf2f((unsigned short)(av.x >> 16));
         const float fg = bf2f((unsigned short)av.y), og = bf2f((unsigned short)(av.y >> 16));
-        const float cn = (float)cst[row * UP + u];
-        const float cp = tau > 0 ? (float)cst[(((size_t)dir * S + srow[nt]) * L + tp) * UP + u] : 0.f;
+        const float tc = tanh_l2(cnv[m] * (2.f * LOG2E_F));
         float dout = 0.f;
-        if (u < U && sval[nt]) {
-          const int s = srow[nt];
-          dout = bf2f(dH[((size_t)s * L + t) * 2 * U + dir * U + u]);
-          if (drop) dout = lstm_keep(salt, ((uint32_t)s * L + t) * U + u, thr) ? dout * inv_kp : 0.f;
+        if (uval && sval[nt]) {   // DropoutWrapper on the attention gradient (same hash as the forward)
+          dout = dov[m];
+          if (drop) dout = lstm_keep(salt, ((uint32_t)srow[nt] * L + t) * U + u, thr) ? dout * inv_kp : 0.f;
         }
-        const float tc = tanh_l2(cn * (2.f * LOG2E_F));
         const float dh = dout + dhr[nt][m];
         const float dc = dcr[m][nt] + dh * og * (1.f - tc * tc);
         dcr[m][nt] = dc * fg;
-        const uint2 gw = uint2{pack_bf2(dc * jg * (ig - ig * ig), dc * ig * (1.f - jg * jg)),
-                               pack_bf2(dc * cp * (fg - fg * fg), dh * tc * (og - og * og))};
-        if (sval[nt]) *reinterpret_cast<uint2*>(dG + row * G4 + 4 * u) = gw;
-        *reinterpret_cast<uint2*>(gcur + (nt * 16 + n) * GS + 4 * u) = gw;
+        gw[2 * m] = pack_bf2(dc * jg * (ig - ig * ig), dc * ig * (1.f - jg * jg));
+        gw[2 * m + 1] = pack_bf2(dc * cpv[m] * (fg - fg * fg), dh * tc * (og - og * og));
       }
+      const uint4 g_lo = {gw[0], gw[1], gw[2], gw[3]}, g_hi = {gw[4], gw[5], gw[6], gw[7]};
+      if (sval[nt]) {
+        uint4* dst = reinterpret_cast<uint4*>(dG + row * G4 + 4 * u0);
+        dst[0] = g_lo;
+        dst[1] = g_hi;
+      }
+      uint4* li = reinterpret_cast<uint4*>(gcur + (nt * 16 + n) * GS + 4 * u0);
+      li[0] = g_lo;
+      li[1] = g_hi;
+      cn2[nt] = cur.cp[nt];
     }
     __syncthreads();   // the dG image of this step is complete
-    if (tau > 0) {
+    if (tau > 0) {     // dh_{t-1} = dG W_h^T: two accumulators per tile (shorter dependent MFMA chains)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+        f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < KS2; ++ks)
-          acc = mfma_bf16(A2[ks], *reinterpret_cast<const u16x8_t*>(gcur + (nt * 16 + n) * GS + 32 * ks + 8 * q), acc);
-        dhr[nt] = acc;
+        for (int ks = 0; ks < KS2; ks += 2) {
+          a0 = mfma_bf16(A2[ks], *reinterpret_cast<const u16x8_t*>(gcur + (nt * 16 + n) * GS + 32 * ks + 8 * q), a0);
+          a1 = mfma_bf16(A2[ks + 1], *reinterpret_cast<const u16x8_t*>(gcur + (nt * 16 + n) * GS + 32 * ks + 32 + 8 * q), a1);
+        }
+        dhr[nt] = a0 + a1;
       }
     }
+  };
+  In b0, b1;   // ping-pong prefetch buffers (loop unrolled by two)
+  load_in(L - 1, b0);
+  int tau = L - 1;
+  for (; tau >= 1; tau -= 2) {
+    step(tau, b0, b1);
+    step(tau - 1, b1, b0);
   }
+  if (tau == 0) step(0, b0, b1);
 }
 
 namespace ina {
@@ -373,8 +474,8 @@ static int wide_seq_fwd_t(const WideSeqArgs& a, hipStream_t st) {
   using C = WideCfg<U>;
   const dim3 grid((a.S + C::SEQ - 1) / C::SEQ, 2);
   hipLaunchKernelGGL(lstm_wide_seq_fwd_kernel<U>, grid, dim3(C::NW * 64), 0, st, (const unsigned short*)a.gx, a.bx,
-                     (const u16x8_t*)a.apk, a.S, a.L, (unsigned short*)a.hprev, (unsigned short*)a.acts,
-                     (_Float16*)a.cst, (unsigned short*)a.hout, a.salt0,
+                     (const u16x8_t*)a.apk, a.S, a.L, (unsigned short*)a.hprev, (uint2*)a.acts,
+                     (uint2*)a.cst, (unsigned short*)a.hout, a.salt0,
                      a.salt1, a.thr, a.inv_kp, a.drop, a.stash);
   INA_CHECK_LAUNCH();
   return 0;
@@ -384,7 +485,7 @@ static int wide_seq_bwd_t(const WideSeqArgs& a, hipStream_t st) {
   using C = WideCfg<U>;
   const dim3 grid((a.S + C::SEQ - 1) / C::SEQ, 2);
   hipLaunchKernelGGL(lstm_wide_seq_bwd_kernel<U>, grid, dim3(C::NW * 64), 0, st, (const unsigned short*)a.dH,
-                     (const unsigned short*)a.acts, (const _Float16*)a.cst, (const u16x8_t*)a.a2pk, (unsigned short*)a.dG, a.S, a.L,
+                     (const uint2*)a.acts, (const uint2*)a.cst, (const u16x8_t*)a.a2pk, (unsigned short*)a.dG, a.S, a.L,
                      a.salt0, a.salt1, a.thr, a.inv_kp, a.drop);
   INA_CHECK_LAUNCH();
   return 0;

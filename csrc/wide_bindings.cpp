@@ -1,5 +1,7 @@
 // Torch op registrations of the wide BiLSTM cell kernels (csrc/kernels/lstm_wide.hip).
 // Both ops update their output tensors in place (the per-step driver loop lives in ops/wide.py).
+#include <algorithm>
+
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
@@ -92,11 +94,12 @@ void lstm_wide_bwd_step(const Tensor& dH, const Tensor& dhrec, const Tensor& dcr
 }
 
 // ---- persistent wide BiLSTM (one launch per pass; lstm_wide.hip lstm_wide_seq_*)
+static int64_t wide_seq_pad(int64_t S) { return (S + 31) / 32 * 32; }
 int64_t wide_up(int64_t U) { return (U + 31) / 32 * 32; }
 
 // gx [2, S*L, 4UP] bf16 (x W_x, permuted + pre-scaled gate columns), bx [2, 4UP] fp32 biases, apk =
 // pack_lstm_wide's forward fragments -> (hout [S, L, 2U] bf16, hprev [2, S, L, UP] bf16,
-// acts [2, S*L, 4UP] bf16, cst [2, S*L, UP] fp16);
+// acts [2, Sp*L, 4UP] bf16, cst [2, Sp*L, UP] fp16: tile-major, Sp = S rounded up to 32);
 // the last three only when stash (training), else empty
 std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_wide_seq_fwd(const Tensor& gx, const Tensor& bx, const Tensor& apk,
                                                              int64_t S, int64_t L, int64_t U, bool stash, int64_t seed,
@@ -110,8 +113,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_wide_seq_fwd(const Tensor& gx, c
   auto bopt = gx.options().dtype(at::kBFloat16), hopt = gx.options().dtype(at::kHalf);
   auto hout = at::empty({S, L, 2 * U}, bopt);
   auto hprev = stash ? at::empty({2, S, L, UP}, bopt) : at::empty({0}, bopt);
-  auto acts = stash ? at::empty({2, S * L, G4}, bopt) : at::empty({0}, bopt);
-  auto cst = stash ? at::empty({2, S * L, UP}, hopt) : at::empty({0}, hopt);
+  const int64_t Sp = wide_seq_pad(S);   // tile-major stash: whole 32-sequence tiles
+  auto acts = stash ? at::empty({2, Sp * L, G4}, bopt) : at::empty({0}, bopt);
+  auto cst = stash ? at::empty({2, Sp * L, UP}, hopt) : at::empty({0}, hopt);
   if (S == 0) return {hout, hprev, acts, cst};
   ina::WideSeqArgs a{};
   a.S = (int)S;
@@ -143,8 +147,8 @@ Tensor lstm_wide_seq_bwd(const Tensor& dH, const Tensor& acts, const Tensor& cst
   TORCH_CHECK(ina::lstm_wide_seq_supported((int)U), "ina.lstm_wide_seq_bwd: U must be 64, 100 or 128");
   const int64_t UP = wide_up(U), G4 = 4 * UP, NW = UP / 16;
   chk(dH, "dH", at::kBFloat16, S * L * 2 * U);
-  chk(acts, "acts", at::kBFloat16, 2 * S * L * G4);
-  chk(cst, "cst", at::kHalf, 2 * S * L * UP);
+  chk(acts, "acts", at::kBFloat16, 2 * wide_seq_pad(S) * L * G4);
+  chk(cst, "cst", at::kHalf, 2 * wide_seq_pad(S) * L * UP);
   chk(a2pk, "a2pk", at::kBFloat16, 2 * NW * (G4 / 32) * 64 * 8);
   auto dG = at::empty({2, S * L, G4}, dH.options());
   if (S == 0) return dG;
@@ -217,6 +221,82 @@ Tensor wide_pos_grad(const Tensor& dxp, const Tensor& inst, const Tensor& pos1, 
 
 }  // namespace
 
+// ---- fused self-attention pooling over the wide BiLSTM output (attn_wide.hip)
+static int64_t attn_sb(int64_t L) { return std::max<int64_t>(1, 80 / L); }   // ~80 tokens per workgroup
+
+static ina::WideAttnArgs attn_args(const Tensor& hin, const Tensor& inst, const Tensor& mask, const Tensor& w1t,
+                                   const Tensor& b1, const Tensor& w2) {
+  TORCH_CHECK(hin.dim() == 3, "ina.wide_attn: hin must be [S, L, H]");
+  const int64_t S = hin.size(0), L = hin.size(1), H = hin.size(2), HP = ina::wide_attn_hp((int)H);
+  TORCH_CHECK(HP > 0, "ina.wide_attn: H must be 128, 200 or 256");
+  TORCH_CHECK(L >= 1 && L <= 256, "ina.wide_attn: L must be in [1, 256]");
+  chk(hin, "hin", at::kBFloat16, S * L * H);
+  chk(inst, "inst", at::kInt, S);
+  TORCH_CHECK(mask.dim() == 2 && mask.size(1) == L, "ina.wide_attn: mask must be [rows, L]");
+  chk(mask, "mask", at::kInt, mask.numel());
+  chk(w1t, "w1t", at::kBFloat16, HP * HP);
+  chk(b1, "b1", at::kFloat, HP);
+  chk(w2, "w2", at::kFloat, HP);
+  TORCH_CHECK(S * L * H < (1LL << 31), "ina.wide_attn: batch too large");
+  ina::WideAttnArgs a{};
+  a.S = (int)S;
+  a.L = (int)L;
+  a.H = (int)H;
+  a.SB = (int)attn_sb(L);
+  a.hin = hin.data_ptr();
+  a.inst = inst.data_ptr<int>();
+  a.mask = mask.data_ptr<int>();
+  a.w1t = w1t.data_ptr();
+  a.b1 = b1.data_ptr<float>();
+  a.w2 = w2.data_ptr<float>();
+  return a;
+}
+
+static void attn_smem_attr(const ina::WideAttnArgs& a, bool bwd) {
+  TORCH_CHECK(ina::wide_attn_smem(a.H, a.L, a.SB, bwd) <= 160 * 1024, "ina.wide_attn: L too long for LDS");
+}
+
+// hin [S, L, H] bf16 -> (e [S, H] fp32, alpha [S, L] fp32)
+std::tuple<Tensor, Tensor> wide_attn_fwd(const Tensor& hin, const Tensor& inst, const Tensor& mask, const Tensor& w1t,
+                                         const Tensor& b1, const Tensor& w2) {
+  auto a = attn_args(hin, inst, mask, w1t, b1, w2);
+  attn_smem_attr(a, false);
+  auto fopt = hin.options().dtype(at::kFloat);
+  auto e = at::empty({a.S, a.H}, fopt), alpha = at::empty({a.S, a.L}, fopt);
+  a.e = e.data_ptr<float>();
+  a.alpha = alpha.data_ptr<float>();
+  TORCH_CHECK(ina::wide_attn_fwd(a, c10::hip::getCurrentHIPStream().stream()) == 0, "ina.wide_attn_fwd: launch failed");
+  return {e, alpha};
+}
+
+// + alpha [S, L], de [S, H] fp32 -> (dH [S, L, H] bf16, dZ [S*L, H] bf16, part [blocks, 2, HP] fp32: dw2, db1)
+std::tuple<Tensor, Tensor, Tensor> wide_attn_bwd(const Tensor& hin, const Tensor& inst, const Tensor& mask,
+                                                 const Tensor& w1t, const Tensor& w1, const Tensor& b1,
+                                                 const Tensor& w2, const Tensor& alpha, const Tensor& de) {
+  auto a = attn_args(hin, inst, mask, w1t, b1, w2);
+  attn_smem_attr(a, true);
+  const int64_t HP = ina::wide_attn_hp(a.H), blocks = (a.S + a.SB - 1) / a.SB;
+  chk(w1, "w1", at::kBFloat16, HP * HP);
+  chk(alpha, "alpha", at::kFloat, (int64_t)a.S * a.L);
+  chk(de, "de", at::kFloat, (int64_t)a.S * a.H);
+  auto dH = at::empty({a.S, a.L, a.H}, hin.options());
+  auto dZ = at::empty({(int64_t)a.S * a.L, a.H}, hin.options());
+  auto part = at::empty({blocks, 2, HP}, hin.options().dtype(at::kFloat));
+  a.w1 = w1.data_ptr();
+  a.alpha = alpha.data_ptr<float>();
+  a.de = de.data_ptr<float>();
+  a.dH = dH.data_ptr();
+  a.dZ = dZ.data_ptr();
+  a.part = part.data_ptr<float>();
+  TORCH_CHECK(ina::wide_attn_bwd(a, c10::hip::getCurrentHIPStream().stream()) == 0, "ina.wide_attn_bwd: launch failed");
+  return {dH, dZ, part};
+}
+
+bool wide_attn_ok(int64_t H, int64_t L) {
+  return ina::wide_attn_hp((int)H) > 0 && L >= 1 && L <= 256 &&
+         ina::wide_attn_smem((int)H, (int)L, (int)attn_sb(L), true) <= 160 * 1024;
+}
+
 TORCH_LIBRARY_FRAGMENT(ina, m) {
   m.def("lstm_wide_fwd_step", &lstm_wide_fwd_step);
   m.def("lstm_wide_bwd_step", &lstm_wide_bwd_step);
@@ -225,4 +305,7 @@ TORCH_LIBRARY_FRAGMENT(ina, m) {
   m.def("lstm_wide_seq_ok", &lstm_wide_seq_ok);
   m.def("wide_x_gather", &wide_x_gather);
   m.def("wide_pos_grad", &wide_pos_grad);
+  m.def("wide_attn_fwd", &wide_attn_fwd);
+  m.def("wide_attn_bwd", &wide_attn_bwd);
+  m.def("wide_attn_ok", &wide_attn_ok);
 }

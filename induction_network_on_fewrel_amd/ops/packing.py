@@ -284,9 +284,11 @@ def gate_scales(device=None) -> torch.Tensor:
 def _wide_idx(U: int):
     """Index tables (into a padded [U+1, 4U+1] matrix whose last row / column are zero) for
     * fwd A fragments [NW][M][KS][64][8]: row R = 4q' + g of M-tile m of wave w = gate g of unit
-      u = 16w + 4m + q'; k = 32 ks + 8 (l >> 4) + j = input unit; value W_h[k][g U + u]
-    * bwd A fragments [NW][KS2][64][8]: row R -> u_in = 16w + 4 (R & 3) + (R >> 2) (so the dh
-      accumulator register r of lane group q is unit 16w + 4r + q: the forward's lane ownership);
+      u = 16w + 4q' + m (lane group q' owns the 4 CONTIGUOUS units 16w + 4q' .. + 3: one 32-byte gate
+      load / store and one 8-byte h write per lane and tile); k = 32 ks + 8 (l >> 4) + j = input unit;
+      value W_h[k][g U + u]
+    * bwd A fragments [NW][KS2][64][8]: row R -> u_in = 16w + R (so the dh accumulator register r of
+      lane group q is unit 16w + 4q + r: the forward's lane ownership);
       k = permuted gate column 4 u_out + g; value W_h[u_in][g U + u_out]
     * permuted gate column c = 4u + g -> TF column g U + u (or the zero column)."""
     s = wide_shape(U)
@@ -299,7 +301,7 @@ def _wide_idx(U: int):
     fwd = np.empty((NW, M, KS, 64, 8), dtype=np.int64)
     for w in range(NW):
         for m in range(M):
-            u = 16 * w + 4 * m + (R >> 2)
+            u = 16 * w + 4 * (R >> 2) + m
             g = R & 3
             for ks in range(KS):
                 k = 32 * ks + 8 * kg[:, None] + j[None, :]
@@ -308,7 +310,7 @@ def _wide_idx(U: int):
                 fwd[w, m, ks] = row * W + np.where(k < U, col, ZC)
     bwd = np.empty((NW, KS2, 64, 8), dtype=np.int64)
     for w in range(NW):
-        u_in = 16 * w + 4 * (R & 3) + (R >> 2)
+        u_in = 16 * w + R
         for ks in range(KS2):
             k = 32 * ks + 8 * kg[:, None] + j[None, :]
             u_out, g = k >> 2, k & 3
@@ -366,3 +368,37 @@ def unpack_wide_grads(dwx: torch.Tensor, dwh: torch.Tensor, db: torch.Tensor, U:
     K[dwx.shape[0]:].index_copy_(1, dst, dwh[:U].float().index_select(1, src))
     bias = torch.zeros(4 * U, device=db.device, dtype=torch.float32).index_copy_(0, dst, db.float().index_select(0, src))
     return K, bias
+
+
+@lru_cache(maxsize=None)
+def _attn_idx(H: int):
+    """Flat indices into a zero-padded [HP, HP] W1 (HP = H rounded up to 32) for the fused attention
+    kernels' MFMA A fragments [HP/16 tiles][HP/32 K-steps][64 lanes][8] (csrc/kernels/attn_wide.hip):
+    lane l of tile t, K-step ks, element i covers row 16t + (l & 15) and k = 32ks + 8(l >> 4) + i;
+    * w1t: A = W1^T (row = output feature j, k = input feature): W1[k][row]   (Z^T = W1^T H^T)
+    * w1:  A = W1   (row = input feature k, k = output feature j): W1[row][k]  (dH^T = W1 dZ^T)"""
+    HP = (H + 31) // 32 * 32
+    t = np.arange(HP // 16)[:, None, None, None]
+    ks = np.arange(HP // 32)[None, :, None, None]
+    l = np.arange(64)[None, None, :, None]
+    i = np.arange(8)[None, None, None, :]
+    row = 16 * t + (l & 15)
+    kk = 32 * ks + 8 * (l >> 4) + i
+    return HP, torch.from_numpy((kk * HP + row).reshape(-1)), torch.from_numpy((row * HP + kk).reshape(-1))
+
+
+def pack_attn_wide(W1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor):
+    """Self-attention weights (W1 [H, H], b1 [H], w2 [H, 1]) -> the fused attention kernels' operands:
+    w1t / w1 bf16 A fragments (see _attn_idx), b1 / w2 fp32 zero-padded to HP."""
+    H = W1.shape[0]
+    HP, it, iw = _attn_idx(H)
+    dev = W1.device
+    Wp = torch.zeros(HP, HP, device=dev, dtype=torch.float32)
+    Wp[:H, :H] = W1.detach().float()
+    flat = Wp.reshape(-1)
+    b1p = torch.zeros(HP, device=dev, dtype=torch.float32)
+    b1p[:H] = b1.detach().float().reshape(-1)
+    w2p = torch.zeros(HP, device=dev, dtype=torch.float32)
+    w2p[:H] = w2.detach().float().reshape(-1)
+    return {"w1t": flat[_on(it, dev)].to(torch.bfloat16), "w1": flat[_on(iw, dev)].to(torch.bfloat16),
+            "b1": b1p, "w2": w2p}

@@ -224,6 +224,35 @@ class ProjBF16(torch.autograd.Function):
         return dX, dW
 
 
+class WideAttn(torch.autograd.Function):
+    """Fused self-attention pooling (csrc/kernels/attn_wide.hip; reference model/layer_module.py:49-98)
+    over the bf16 BiLSTM output Hb [S, L, H], H = 2u in {128, 200, 256}: one forward kernel (projection
+    on MFMA, tanh / score / masked softmax / pooling on the staged block), one backward kernel (dH,
+    the dZ operand and dw2 / db1 partials) + the dW1 = H^T dZ split-K GEMM.  alphas carry no
+    gradient (the reference fetches them for inspection only, model/base.py:144)."""
+
+    @staticmethod
+    def forward(ctx, Hb, inst, mask, W1, b1, w2):
+        from .packing import pack_attn_wide
+        pk = pack_attn_wide(W1, b1, w2)
+        e, alpha = ops().wide_attn_fwd(Hb, inst, mask, pk["w1t"], pk["b1"], pk["w2"])
+        ctx.save_for_backward(Hb, inst, mask, alpha)
+        ctx.pk = pk
+        ctx.mark_non_differentiable(alpha)
+        return e, alpha
+
+    @staticmethod
+    def backward(ctx, de, _dalpha):
+        Hb, inst, mask, alpha = ctx.saved_tensors
+        pk = ctx.pk
+        H = Hb.shape[-1]
+        dH, dZ, part = ops().wide_attn_bwd(Hb, inst, mask, pk["w1t"], pk["w1"], pk["b1"], pk["w2"], alpha,
+                                           de.contiguous().float())
+        dW1 = _wgrad(Hb.reshape(-1, H), dZ) if ctx.needs_input_grad[3] else None
+        ps = part.sum(0)
+        return dH, None, None, dW1, ps[1, :H], ps[0, :H].unsqueeze(1)
+
+
 def attention_wide(H, mask, W1, b1, w2):
     """Self-attention pooling (reference model/layer_module.py:49-98) over bf16 BiLSTM outputs
     H [S, L, 2u]: bf16 projection GEMM, tanh / score / masked softmax / pooling in fp32."""
@@ -249,6 +278,9 @@ def encode_wide(inst, data, p, U: int, keep_prob: float, seed: int):
         H = WideSeqBiLSTM.apply(inst, wa, p1a, p2a, p["word_embedding"], p["pos1_embedding"], p["pos2_embedding"],
                                 p["lstm_fw_kernel"], p["lstm_fw_bias"], p["lstm_bw_kernel"], p["lstm_bw_bias"], U,
                                 int(seed), float(keep_prob), bool(getattr(data, "pos_shift", False)))
+        if ops().wide_attn_ok(H.shape[-1], H.shape[1]):
+            mi = ma if ma.dtype == torch.int32 else ma.int()
+            return WideAttn.apply(H, inst.int(), mi.contiguous(), p["attn_kernel"], p["attn_bias"], p["attn_w2"])
         e, alphas = attention_wide(H, ma[inst.long()] > 0, p["attn_kernel"], p["attn_bias"], p["attn_w2"])
         return e, alphas.squeeze(-1)
     word, pos1, pos2, mask = (t[inst.long()] for t in data)

@@ -104,8 +104,8 @@ def test_rec_attn_pack_zero_padding():
 def test_wide_lstm_packs_emulated_mfma():
     """ops/packing.py::pack_lstm_wide against a numpy emulation of v_mfma_f32_16x16x32_bf16's lane
     layout (lane l: A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15]): the forward fragments give each
-    lane group q the 4 (pre-scaled) gates of unit 16w + 4m + q, the backward fragments give dh of unit
-    16w + 4r + q in accumulator register r (the forward's ownership), and the permuted x-projection /
+    lane group q the 4 (pre-scaled) gates of unit 16w + 4q + m in M-tile m, the backward fragments give
+    dh of unit 16w + 4q + r in accumulator register r (the forward's ownership), and the permuted x-projection /
     bias columns c = 4u + g round-trip through unpack_wide_grads."""
     import torch
     from induction_network_on_fewrel_amd.ops.packing import (LOG2E, pack_lstm_wide, unpack_wide_grads,
@@ -132,7 +132,7 @@ def test_wide_lstm_packs_emulated_mfma():
                             R, kg = lane & 15, lane >> 4
                             acc[R] += sum(A[w, m, ks, lane, j] * h[32 * ks + 8 * kg + j] for j in range(8))
                     for R in range(16):
-                        u, gg = 16 * w + 4 * m + (R >> 2), R & 3
+                        u, gg = 16 * w + 4 * (R >> 2) + m, R & 3
                         wcol = (K[D:, gg * U + u].float() * torch.tensor(sc[gg], dtype=torch.float32)) if u < U else None
                         want = wcol.bfloat16().double().numpy() @ h[:U] if u < U else 0.0
                         assert abs(acc[R] - want) <= 1e-9 * (1 + abs(want)), (U, d, w, m, R)
@@ -149,7 +149,7 @@ def test_wide_lstm_packs_emulated_mfma():
                         acc[R] += sum(A2[w, ks, lane, j] * dGp[32 * ks + 8 * kg + j] for j in range(8))
                 for q in range(4):
                     for r in range(4):
-                        u_in = 16 * w + 4 * r + q
+                        u_in = 16 * w + 4 * q + r
                         want = sum(rb(Wh[u_in, gg * U: gg * U + U]) @ dGn[gg] for gg in range(4)) if u_in < U else 0.0
                         assert abs(acc[4 * q + r] - want) <= 1e-9 * (1 + abs(want)), (U, d, w, q, r)
             # x-projection columns / bias, and the gradient un-permutation
@@ -159,3 +159,24 @@ def test_wide_lstm_packs_emulated_mfma():
             dK, db = unpack_wide_grads(wxt, torch.nn.functional.pad(K[D:].bfloat16().float()[:, :0], (0, G4)),
                                        torch.zeros(G4), U)
             assert torch.allclose(dK[:D], K[:D].bfloat16().float())
+
+
+def test_attn_wide_fragments():
+    """ops/packing.py::pack_attn_wide: fragment element (tile t, K-step ks, lane l, i) of w1t is
+    W1[32ks + 8(l>>4) + i][16t + (l&15)] (A = W1^T), of w1 W1[16t + (l&15)][32ks + 8(l>>4) + i] (A = W1);
+    zero outside H (H = 200 pads to 224)."""
+    import torch
+    from induction_network_on_fewrel_amd.ops.packing import pack_attn_wide
+    for H in (128, 200, 256):
+        HP = (H + 31) // 32 * 32
+        W1 = torch.randn(H, H)
+        pk = pack_attn_wide(W1, torch.randn(H), torch.randn(H, 1))
+        Wp = torch.zeros(HP, HP)
+        Wp[:H, :H] = W1.bfloat16().float()
+        a = pk["w1t"].float().reshape(HP // 16, HP // 32, 64, 8)
+        b = pk["w1"].float().reshape(HP // 16, HP // 32, 64, 8)
+        for t, ks, l, i in ((0, 0, 0, 0), (HP // 16 - 1, HP // 32 - 1, 63, 7), (3, 1, 37, 5), (HP // 16 - 2, 2, 22, 3)):
+            k, r = 32 * ks + 8 * (l >> 4) + i, 16 * t + (l & 15)
+            assert float(a[t, ks, l, i]) == float(Wp[k, r])
+            assert float(b[t, ks, l, i]) == float(Wp[r, k])
+        assert pk["b1"].shape == (HP,) and float(pk["w2"][H:].abs().sum()) == 0.0

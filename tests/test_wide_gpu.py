@@ -68,3 +68,46 @@ def test_wide_matches_fused_at_u20():
     assert _relerr(p1, p0) < 2e-2
     assert _relerr(g1, g0) < 6e-2
     assert _relerr(a1, a0) < 6e-2
+
+
+@pytest.mark.parametrize("H,L,S", [(256, 37, 101), (200, 37, 64), (128, 37, 33), (256, 90, 5)])
+def test_fused_attention_vs_fp32(H, L, S):
+    """csrc/kernels/attn_wide.hip (ops/wide.py WideAttn) against the fp32 autograd of the reference
+    self-attention (model/layer_module.py:49-98) on the same bf16 BiLSTM output: e, alphas and the
+    gradients of H, W1, b1, w2.  Odd S covers a partial last block; L=90 the one-sequence-per-block
+    geometry; rows with short masks and one fully-padded-but-one sequence check the masking."""
+    from induction_network_on_fewrel_amd.ops.wide import WideAttn
+    g = torch.Generator(device="cpu").manual_seed(H + L)
+    Hb = (torch.randn(S, L, H, generator=g) * 0.7).to(torch.bfloat16).to(DEV)
+    lens = torch.randint(1, L + 1, (S,), generator=g)
+    lens[0] = 1
+    rows = 2 * S + 3
+    mask = torch.zeros(rows, L, dtype=torch.int32)
+    inst = torch.randperm(rows, generator=g)[:S].to(torch.int32)
+    for i in range(S):
+        mask[inst[i], :lens[i]] = torch.randint(1, 4, (int(lens[i]),), generator=g).to(torch.int32)
+    mask, inst = mask.to(DEV), inst.to(DEV)
+    W1 = (torch.randn(H, H, generator=g) / H ** 0.5).to(DEV).requires_grad_()
+    b1 = (torch.randn(H, generator=g) * 0.3).to(DEV).requires_grad_()
+    w2 = (torch.randn(H, 1, generator=g) * 0.5).to(DEV).requires_grad_()
+    Hk = Hb.clone().requires_grad_()
+    e, alpha = WideAttn.apply(Hk, inst, mask, W1, b1, w2)
+    de = torch.randn(S, H, generator=g).to(DEV)
+    (e * de).sum().backward()
+    # fp32 oracle on the bf16-rounded weights the kernels use (bf16 MFMA operands, fp32 accumulation)
+    Hr = Hb.float().requires_grad_()
+    W1r = W1.detach().clone().requires_grad_()
+    b1r, w2r = b1.detach().clone().requires_grad_(), w2.detach().clone().requires_grad_()
+    proj = torch.tanh(Hr @ W1r.to(torch.bfloat16).float() + b1r)
+    score = (proj @ w2r).squeeze(-1)
+    valid = mask[inst.long()] > 0
+    al = torch.softmax(score.masked_fill(~valid, float("-inf")), dim=1)
+    er = (Hr * al.unsqueeze(-1)).sum(1)
+    (er * de).sum().backward()
+    assert _relerr(e.detach(), er.detach()) < 1e-2
+    assert _relerr(alpha, al.detach()) < 1e-2
+    assert float(alpha[~valid].abs().max()) == 0.0
+    assert _relerr(Hk.grad.float(), Hr.grad) < 2e-2
+    assert _relerr(W1.grad, W1r.grad) < 3e-2
+    assert _relerr(b1.grad, b1r.grad) < 2e-2
+    assert _relerr(w2.grad, w2r.grad) < 2e-2

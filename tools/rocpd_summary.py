@@ -36,7 +36,10 @@ def main():
     a = ap.parse_args()
     if a.sequence:
         c = sqlite3.connect(a.db)
-        ks = c.execute("select name, start, end from kernels order by start").fetchall()
+        cols = [r[1] for r in c.execute("pragma table_info(kernels)").fetchall()]
+        grid = [g for g in ("grid_size_x", "grid_size_y", "grid_size_z", "grid_x", "grid_y", "grid_z") if g in cols]
+        sel = ", ".join(["name", "start", "end"] + grid)
+        ks = c.execute(f"select {sel} from kernels order by start").fetchall()
         marks = [i for i, k in enumerate(ks) if a.sequence in k[0]]
         if len(marks) >= 2:
             lo, hi = marks[-2] + 1, marks[-1] + 1
@@ -45,7 +48,8 @@ def main():
             print(f"step: {hi - lo} kernels, span {span:.1f} us, kernel-busy {busy:.1f} us")
             prev_end = ks[lo - 1][2]
             for k in ks[lo:hi]:
-                print(f"{(k[2] - k[1]) / 1e3:9.2f} us  gap {(k[1] - prev_end) / 1e3:7.2f}  {short(k[0], 110)}")
+                g = ("grid " + "x".join(str(v) for v in k[3:]) + "  ") if grid else ""
+                print(f"{(k[2] - k[1]) / 1e3:9.2f} us  gap {(k[1] - prev_end) / 1e3:7.2f}  {g}{short(k[0], 110)}")
                 prev_end = k[2]
         return
     rows, tot = summary(a.db)
