@@ -186,7 +186,7 @@ int lstm_wide_bwd_step(const LstmWideArgs& a, int tau, hipStream_t st);
 // gate columns permuted to c = 4u + g (u < UP = U padded to 32), ops/packing.py::pack_lstm_wide
 struct WideSeqArgs {
   int S, L, U;
-  const void* gx;         // [2][S*L][G4] bf16: x W_x (pre-scaled, row s*L + t)
+  const void* gx;         // [S*L][2][G4] bf16: x W_x (pre-scaled, row s*L + t, both directions)
   const float* bx;        // [2][G4] fp32: pre-scaled biases (forget gate +1)
   const void* apk;        // [2][NW][4][KS][64] x 8 bf16 forward W_h fragments (pre-scaled)
   const void* a2pk;       // [2][NW][KS2][64] x 8 bf16 backward W_h fragments
@@ -195,7 +195,7 @@ struct WideSeqArgs {
   void* cst;              // cell states, fp16, tile-major (lstm_wide.hip WideStash)
   void* hout;             // [S][L][2U] bf16: DropoutWrapper output (attention input)
   const void* dH;         // [S][L][2U] bf16: gradient w.r.t. hout
-  void* dG;               // [2][S][L][G4] bf16: pre-activation gate gradients
+  void* dG;               // [S*L][2][G4] bf16: pre-activation gate gradients (both directions)
   uint32_t salt0, salt1, thr;
   float inv_kp;
   int drop;
@@ -203,7 +203,7 @@ struct WideSeqArgs {
 };
 bool lstm_wide_seq_supported(int U);
 int wide_x_gather(const int* inst, int S, int L, const int* word, const int* pos1, const int* pos2, const float* wemb,
-                  int E, const float* p1emb, const float* p2emb, int PD, void* xb, hipStream_t st);
+                  int E, const float* p1emb, const float* p2emb, int PD, int DP, void* xb, hipStream_t st);
 int wide_pos_grad(const float* dxp, const int* inst, const int* pos1, const int* pos2, int S, int L, int PD, int P2,
                   int chunks, float* part, hipStream_t st);
 int lstm_wide_seq_fwd(const WideSeqArgs& a, hipStream_t st);
@@ -224,12 +224,14 @@ struct WideAttnArgs {
   const float* de;        // backward: [S][H]
   void* dH;               // backward: [S][L][H] bf16
   void* dZ;               // backward: [S*L][H] bf16 (pre-activation gradient, the dW1 GEMM operand)
-  float* part;            // backward: [grid][2][HP] (dw2, db1) partial sums
+  float* part;            // backward: [grid][2][HP] (dw2, db1) partial sums, one row per workgroup
 };
-int wide_attn_hp(int H);
-size_t wide_attn_smem(int H, int L, int SB, bool bwd);
-int wide_attn_fwd(const WideAttnArgs& a, hipStream_t st);
-int wide_attn_bwd(const WideAttnArgs& a, hipStream_t st);
+int wide_attn_hp(int H);                        // padded H (0: unsupported)
+int wide_attn_sb(int L);                        // sequences per block
+size_t wide_attn_smem(int H, int L, bool bwd);  // dynamic LDS bytes
+int wide_attn_grid(int H, int L, int S, bool bwd);   // persistent grid (resident workgroups); < 0 on error
+int wide_attn_fwd(const WideAttnArgs& a, int grid, hipStream_t st);
+int wide_attn_bwd(const WideAttnArgs& a, int grid, hipStream_t st);   // part: [grid][2][HP]
 
 // ---------------------------------------------------------------- BERT (csrc/kernels/bert.hip)
 struct BertLnArgs {          // y = LN(res + dropout(a)); HD = 256 * {1..4}

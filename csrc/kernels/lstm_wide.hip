@@ -259,7 +259,7 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_fwd_kernel(
   auto load_gx = [&](int t, uint4 (&g)[NT][2]) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      const uint4* src = reinterpret_cast<const uint4*>(gx + (((size_t)dir * S + srow[nt]) * L + t) * G4 + 4 * u0);
+      const uint4* src = reinterpret_cast<const uint4*>(gx + ((size_t)srow[nt] * L + t) * (2 * G4) + dir * G4 + 4 * u0);
       g[nt][0] = src[0];
       g[nt][1] = src[1];
     }
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_bwd_kernel(
       const float2 c01 = unpack_h2(cn2[nt].x), c23 = unpack_h2(cn2[nt].y);
       const float2 p01 = unpack_h2(cur.cp[nt].x), p23 = unpack_h2(cur.cp[nt].y);
       const float cnv[M] = {c01.x, c01.y, c23.x, c23.y}, cpv[M] = {p01.x, p01.y, p23.x, p23.y};
-      const size_t row = ((size_t)dir * S + srow[nt]) * L + t;
+      const size_t row = (size_t)srow[nt] * L + t;   // dG [S*L][2][G4]: both directions on one row
       const float dov[M] = {bf2f((unsigned short)cur.dout[nt].x), bf2f((unsigned short)(cur.dout[nt].x >> 16)),
                             bf2f((unsigned short)cur.dout[nt].y), bf2f((unsigned short)(cur.dout[nt].y >> 16))};
       uint32_t gw[2 * M];
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_bwd_kernel(
       }
       const uint4 g_lo = {gw[0], gw[1], gw[2], gw[3]}, g_hi = {gw[4], gw[5], gw[6], gw[7]};
       if (sval[nt]) {
-        uint4* dst = reinterpret_cast<uint4*>(dG + row * G4 + 4 * u0);
+        uint4* dst = reinterpret_cast<uint4*>(dG + row * (2 * G4) + dir * G4 + 4 * u0);
         dst[0] = g_lo;
         dst[1] = g_hi;
       }
@@ -515,28 +515,33 @@ __global__ __launch_bounds__(256) void wide_x_gather_kernel(const int* __restric
                                                             const int* __restrict__ word, const int* __restrict__ pos1,
                                                             const int* __restrict__ pos2, const float* __restrict__ wemb,
                                                             int E, const float* __restrict__ p1emb,
-                                                            const float* __restrict__ p2emb, int PD,
+                                                            const float* __restrict__ p2emb, int PD, int DP,
                                                             unsigned short* __restrict__ xb) {
+  // one wave per row: the word vector as float4 loads -> 4 bf16 (8-byte stores) when E % 4 == 0,
+  // then the 2 PD position columns, the ones column (index D) and zero padding up to DP
   const int lane = threadIdx.x & 63;
   const int D = E + 2 * PD;
   const long rows = (long)S * L;
+  typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
   for (long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (long)gridDim.x * 4) {
     const int s = (int)(r / L), t = (int)(r - (long)s * L);
     const long tok = (long)inst[s] * L + t;
     const float* wr = wemb + (long)word[tok] * E;
+    unsigned short* dst = xb + r * DP;
+    int c0 = 0;
+    if ((E & 3) == 0) {
+      for (int c = 4 * lane; c < E; c += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(wr + c);
+        const bf2_t lo = {(__bf16)v.x, (__bf16)v.y}, hi = {(__bf16)v.z, (__bf16)v.w};
+        *reinterpret_cast<uint2*>(dst + c) = uint2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
+      }
+      c0 = E;
+    }
     const float* q1 = p1emb + (long)pos1[tok] * PD;
     const float* q2 = p2emb + (long)pos2[tok] * PD;
-    auto col = [&](int c) { return c < E ? wr[c] : (c < E + PD ? q1[c - E] : q2[c - E - PD]); };
-    unsigned short* dst = xb + r * D;
-    for (int c = 2 * lane; c < D; c += 128) {
-      if (c + 1 < D && (D & 1) == 0) {
-        typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
-        const bf2_t v = {(__bf16)col(c), (__bf16)col(c + 1)};
-        *reinterpret_cast<uint32_t*>(dst + c) = __builtin_bit_cast(uint32_t, v);
-      } else {
-        dst[c] = f2bf(col(c));
-        if (c + 1 < D) dst[c + 1] = f2bf(col(c + 1));
-      }
+    for (int c = c0 + lane; c < DP; c += 64) {
+      const float v = c < E ? wr[c] : c < E + PD ? q1[c - E] : c < D ? q2[c - E - PD] : c == D ? 1.f : 0.f;
+      dst[c] = f2bf(v);
     }
   }
 }
@@ -567,13 +572,13 @@ __global__ __launch_bounds__(256) void wide_pos_grad_kernel(const float* __restr
 namespace ina {
 
 int wide_x_gather(const int* inst, int S, int L, const int* word, const int* pos1, const int* pos2, const float* wemb,
-                  int E, const float* p1emb, const float* p2emb, int PD, void* xb, hipStream_t st) {
+                  int E, const float* p1emb, const float* p2emb, int PD, int DP, void* xb, hipStream_t st) {
   const long rows = (long)S * L;
-  long blocks = (rows + 3) / 4;
-  if (blocks > 8192) blocks = 8192;
+  long blocks = (rows + 3) / 4;   // one row per wave: the inst -> word id -> vector chain is latency-bound
+  if (blocks > (1L << 30)) blocks = 1L << 30;
   if (blocks < 1) return 0;
   hipLaunchKernelGGL(wide_x_gather_kernel, dim3((int)blocks), dim3(256), 0, st, inst, S, L, word, pos1, pos2, wemb, E,
-                     p1emb, p2emb, PD, (unsigned short*)xb);
+                     p1emb, p2emb, PD, DP, (unsigned short*)xb);
   INA_CHECK_LAUNCH();
   return 0;
 }

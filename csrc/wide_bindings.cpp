@@ -97,7 +97,7 @@ void lstm_wide_bwd_step(const Tensor& dH, const Tensor& dhrec, const Tensor& dcr
 static int64_t wide_seq_pad(int64_t S) { return (S + 31) / 32 * 32; }
 int64_t wide_up(int64_t U) { return (U + 31) / 32 * 32; }
 
-// gx [2, S*L, 4UP] bf16 (x W_x, permuted + pre-scaled gate columns), bx [2, 4UP] fp32 biases, apk =
+// gx [S*L, 2 * 4UP] bf16 (x W_x of both directions, permuted + pre-scaled gate columns), bx [2, 4UP] fp32 biases, apk =
 // pack_lstm_wide's forward fragments -> (hout [S, L, 2U] bf16, hprev [2, S, L, UP] bf16,
 // acts [2, Sp*L, 4UP] bf16, cst [2, Sp*L, UP] fp16: tile-major, Sp = S rounded up to 32);
 // the last three only when stash (training), else empty
@@ -141,7 +141,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_wide_seq_fwd(const Tensor& gx, c
   return {hout, hprev, acts, cst};
 }
 
-// dH [S, L, 2U] bf16 (gradient w.r.t. hout) + the forward's stash -> dG [2, S*L, 4UP] bf16 (permuted columns)
+// dH [S, L, 2U] bf16 (gradient w.r.t. hout) + the forward's stash -> dG [S*L, 2 * 4UP] bf16 (both directions, permuted columns)
 Tensor lstm_wide_seq_bwd(const Tensor& dH, const Tensor& acts, const Tensor& cst, const Tensor& a2pk, int64_t S,
                          int64_t L, int64_t U, int64_t seed, double keep_prob) {
   TORCH_CHECK(ina::lstm_wide_seq_supported((int)U), "ina.lstm_wide_seq_bwd: U must be 64, 100 or 128");
@@ -150,7 +150,7 @@ Tensor lstm_wide_seq_bwd(const Tensor& dH, const Tensor& acts, const Tensor& cst
   chk(acts, "acts", at::kBFloat16, 2 * wide_seq_pad(S) * L * G4);
   chk(cst, "cst", at::kHalf, 2 * wide_seq_pad(S) * L * UP);
   chk(a2pk, "a2pk", at::kBFloat16, 2 * NW * (G4 / 32) * 64 * 8);
-  auto dG = at::empty({2, S * L, G4}, dH.options());
+  auto dG = at::empty({S * L, 2 * G4}, dH.options());
   if (S == 0) return dG;
   ina::WideSeqArgs a{};
   a.S = (int)S;
@@ -193,10 +193,11 @@ Tensor wide_x_gather(const Tensor& inst, const Tensor& word, const Tensor& pos1,
   const int64_t S = inst.size(0), L = word.size(1), E = wemb.size(1), PD = p1emb.size(1);
   TORCH_CHECK(pos1.sizes() == word.sizes() && pos2.sizes() == word.sizes() && p2emb.size(1) == PD,
               "ina.wide_x_gather: shapes");
-  auto xb = at::empty({S * L, E + 2 * PD}, wemb.options().dtype(at::kBFloat16));
+  const int64_t DP = (E + 2 * PD + 1 + 31) / 32 * 32;   // + the ones column, K padded to 32 (packing.wide_x_cols)
+  auto xb = at::empty({S * L, DP}, wemb.options().dtype(at::kBFloat16));
   TORCH_CHECK(ina::wide_x_gather(inst.data_ptr<int>(), (int)S, (int)L, word.data_ptr<int>(), pos1.data_ptr<int>(),
                                  pos2.data_ptr<int>(), wemb.data_ptr<float>(), (int)E, p1emb.data_ptr<float>(),
-                                 p2emb.data_ptr<float>(), (int)PD, xb.data_ptr(),
+                                 p2emb.data_ptr<float>(), (int)PD, (int)DP, xb.data_ptr(),
                                  c10::hip::getCurrentHIPStream().stream()) == 0,
               "ina.wide_x_gather: launch failed");
   return xb;
@@ -222,8 +223,6 @@ Tensor wide_pos_grad(const Tensor& dxp, const Tensor& inst, const Tensor& pos1, 
 }  // namespace
 
 // ---- fused self-attention pooling over the wide BiLSTM output (attn_wide.hip)
-static int64_t attn_sb(int64_t L) { return std::max<int64_t>(1, 80 / L); }   // ~80 tokens per workgroup
-
 static ina::WideAttnArgs attn_args(const Tensor& hin, const Tensor& inst, const Tensor& mask, const Tensor& w1t,
                                    const Tensor& b1, const Tensor& w2) {
   TORCH_CHECK(hin.dim() == 3, "ina.wide_attn: hin must be [S, L, H]");
@@ -242,7 +241,7 @@ static ina::WideAttnArgs attn_args(const Tensor& hin, const Tensor& inst, const 
   a.S = (int)S;
   a.L = (int)L;
   a.H = (int)H;
-  a.SB = (int)attn_sb(L);
+  a.SB = ina::wide_attn_sb((int)L);
   a.hin = hin.data_ptr();
   a.inst = inst.data_ptr<int>();
   a.mask = mask.data_ptr<int>();
@@ -252,20 +251,25 @@ static ina::WideAttnArgs attn_args(const Tensor& hin, const Tensor& inst, const 
   return a;
 }
 
-static void attn_smem_attr(const ina::WideAttnArgs& a, bool bwd) {
-  TORCH_CHECK(ina::wide_attn_smem(a.H, a.L, a.SB, bwd) <= 160 * 1024, "ina.wide_attn: L too long for LDS");
+static int attn_grid(const ina::WideAttnArgs& a, bool bwd) {
+  TORCH_CHECK(ina::wide_attn_smem(a.H, a.L, bwd) <= 160 * 1024, "ina.wide_attn: L too long for LDS");
+  const int g = ina::wide_attn_grid(a.H, a.L, a.S, bwd);
+  TORCH_CHECK(g >= 0, "ina.wide_attn: occupancy query failed");
+  return g;
 }
 
 // hin [S, L, H] bf16 -> (e [S, H] fp32, alpha [S, L] fp32)
 std::tuple<Tensor, Tensor> wide_attn_fwd(const Tensor& hin, const Tensor& inst, const Tensor& mask, const Tensor& w1t,
                                          const Tensor& b1, const Tensor& w2) {
   auto a = attn_args(hin, inst, mask, w1t, b1, w2);
-  attn_smem_attr(a, false);
+  const int grid = attn_grid(a, false);
   auto fopt = hin.options().dtype(at::kFloat);
   auto e = at::empty({a.S, a.H}, fopt), alpha = at::empty({a.S, a.L}, fopt);
   a.e = e.data_ptr<float>();
   a.alpha = alpha.data_ptr<float>();
-  TORCH_CHECK(ina::wide_attn_fwd(a, c10::hip::getCurrentHIPStream().stream()) == 0, "ina.wide_attn_fwd: launch failed");
+  if (a.S > 0)
+    TORCH_CHECK(ina::wide_attn_fwd(a, grid, c10::hip::getCurrentHIPStream().stream()) == 0,
+                "ina.wide_attn_fwd: launch failed");
   return {e, alpha};
 }
 
@@ -274,27 +278,29 @@ std::tuple<Tensor, Tensor, Tensor> wide_attn_bwd(const Tensor& hin, const Tensor
                                                  const Tensor& w1t, const Tensor& w1, const Tensor& b1,
                                                  const Tensor& w2, const Tensor& alpha, const Tensor& de) {
   auto a = attn_args(hin, inst, mask, w1t, b1, w2);
-  attn_smem_attr(a, true);
-  const int64_t HP = ina::wide_attn_hp(a.H), blocks = (a.S + a.SB - 1) / a.SB;
+  const int grid = attn_grid(a, true);
+  const int64_t HP = ina::wide_attn_hp(a.H);
   chk(w1, "w1", at::kBFloat16, HP * HP);
   chk(alpha, "alpha", at::kFloat, (int64_t)a.S * a.L);
   chk(de, "de", at::kFloat, (int64_t)a.S * a.H);
   auto dH = at::empty({a.S, a.L, a.H}, hin.options());
   auto dZ = at::empty({(int64_t)a.S * a.L, a.H}, hin.options());
-  auto part = at::empty({blocks, 2, HP}, hin.options().dtype(at::kFloat));
+  auto part = at::zeros({std::max(grid, 1), 2, HP}, hin.options().dtype(at::kFloat));
   a.w1 = w1.data_ptr();
   a.alpha = alpha.data_ptr<float>();
   a.de = de.data_ptr<float>();
   a.dH = dH.data_ptr();
   a.dZ = dZ.data_ptr();
   a.part = part.data_ptr<float>();
-  TORCH_CHECK(ina::wide_attn_bwd(a, c10::hip::getCurrentHIPStream().stream()) == 0, "ina.wide_attn_bwd: launch failed");
+  if (a.S > 0)
+    TORCH_CHECK(ina::wide_attn_bwd(a, grid, c10::hip::getCurrentHIPStream().stream()) == 0,
+                "ina.wide_attn_bwd: launch failed");
   return {dH, dZ, part};
 }
 
 bool wide_attn_ok(int64_t H, int64_t L) {
   return ina::wide_attn_hp((int)H) > 0 && L >= 1 && L <= 256 &&
-         ina::wide_attn_smem((int)H, (int)L, (int)attn_sb(L), true) <= 160 * 1024;
+         ina::wide_attn_smem((int)H, (int)L, true) <= 160 * 1024;
 }
 
 TORCH_LIBRARY_FRAGMENT(ina, m) {

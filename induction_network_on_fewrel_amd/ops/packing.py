@@ -326,25 +326,37 @@ def _wide_idx(U: int):
             torch.from_numpy(gscale), torch.from_numpy(c[keep]), torch.from_numpy(perm[keep]))
 
 
+def wide_x_cols(D: int) -> int:
+    """Row width of the wide path's encoder input Xb: the D = E + 2PD embedding columns, a ones column
+    (index D: the x-projection GEMM's bias row, so dW_x's GEMM yields the bias gradient as row D) and
+    zero padding to a multiple of 32 (64-byte rows; a K multiple of 32 moves hipBLASLt's x-projection
+    GEMM off its edge-tile kernels: 1.60 -> 1.16 ms at the paper configuration, tools/gemm_probe.py)."""
+    return (D + 1 + 31) // 32 * 32
+
+
 def pack_lstm_wide(Kf: torch.Tensor, bf: torch.Tensor, Kb: torch.Tensor, bb: torch.Tensor, U: int, D: int):
     """TF BasicLSTMCell kernels [D + U, 4U] + biases of both directions -> the persistent kernels'
-    operands:
-      wx   [2, D, G4] bf16   x-projection, permuted gate columns (4u + g), exp2-pre-scaled (gx GEMM)
-      bx   [2, G4]    fp32   bias (+1 on the forget gate), pre-scaled
-      wxt  [2, D, G4] bf16   the same columns UNscaled (dX = dG wxt^T)
+    operands (G4 = 4 UP permuted gate columns 4u + g per direction; both directions side by side,
+    column dir * G4 + c, so ONE GEMM covers them):
+      wxc  [DP, 2 G4] bf16  x-projection, exp2-pre-scaled, zero rows D .. DP (the ones / pad columns
+                            of Xb: the fp32 bias is added in-kernel)
+      wxtc [D, 2 G4]  bf16  the same columns UNscaled (dX = dG wxtc^T)
+      wxt  [2, D, G4] bf16  per-direction view of wxtc
+      bx   [2, G4]    fp32  bias (+1 on the forget gate), pre-scaled
       apk  [2, NW, M, KS, 64, 8] bf16   forward W_h fragments, pre-scaled
       a2pk [2, NW, KS2, 64, 8]   bf16   backward W_h fragments (true weights)"""
     fwd_i, bwd_i, perm, gsc, _, _ = _wide_idx(U)
     dev = Kf.device
     fwd_i, bwd_i, perm, gsc = (_on(t, dev) for t in (fwd_i, bwd_i, perm, gsc))
+    DP = wide_x_cols(D)
     outs = {k: [] for k in ("wx", "bx", "wxt", "apk", "a2pk")}
     for K, b in ((Kf, bf), (Kb, bb)):
         K = K.detach().float()
         b = b.detach().float()
         Wx = torch.nn.functional.pad(K[:D], (0, 1))                       # [D, 4U+1]
         wxt = Wx[:, perm]                                                 # [D, G4]
-        outs["wxt"].append(wxt.to(torch.bfloat16))
-        outs["wx"].append((wxt * gsc).to(torch.bfloat16))
+        outs["wxt"].append(wxt)
+        outs["wx"].append(torch.nn.functional.pad(wxt * gsc, (0, 0, 0, DP - D)))
         bfull = torch.nn.functional.pad(b, (0, 1))
         fb = torch.zeros_like(bfull)
         fb[2 * U:3 * U] = 1.0                                             # TF forget_bias
@@ -355,7 +367,12 @@ def pack_lstm_wide(Kf: torch.Tensor, bf: torch.Tensor, Kb: torch.Tensor, bb: tor
         gl = (torch.arange(a.shape[0], device=dev) // 1) % 64 % 16 % 4
         outs["apk"].append((a * gate_scales(dev)[gl][:, None]).to(torch.bfloat16))
         outs["a2pk"].append(Wh[bwd_i].to(torch.bfloat16))
-    return {k: torch.stack(v).contiguous() for k, v in outs.items()}
+    wxtc = torch.cat(outs["wxt"], 1).to(torch.bfloat16)
+    G4 = wxtc.shape[1] // 2
+    return {"wxc": torch.cat(outs["wx"], 1).to(torch.bfloat16), "wxtc": wxtc,
+            "wxt": wxtc.view(D, 2, G4).transpose(0, 1),
+            "bx": torch.stack(outs["bx"]).contiguous(), "apk": torch.stack(outs["apk"]).contiguous(),
+            "a2pk": torch.stack(outs["a2pk"]).contiguous()}
 
 
 def unpack_wide_grads(dwx: torch.Tensor, dwh: torch.Tensor, db: torch.Tensor, U: int):

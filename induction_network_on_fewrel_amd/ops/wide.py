@@ -18,11 +18,13 @@ import torch
 from ._ext import ops
 
 
-def _wgrad(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """a^T b in fp32 for tall bf16 a [T, m], b [T, n] (K = T split into 16 chunks)."""
+def _wgrad(a: torch.Tensor, b: torch.Tensor, split: int = 16) -> torch.Tensor:
+    """a^T b in fp32 for tall bf16 a [T, m], b [T, n] (K = T split into `split` chunks: hipBLASLt runs a
+    single K = 1.2 M GEMM on a handful of output tiles; tools/gemm_probe.py measured 16-64 best)."""
     T = a.shape[0]
-    if T % 16 == 0 and T >= 4096:
-        part = torch.bmm(a.view(16, T // 16, -1).transpose(1, 2), b.view(16, T // 16, -1), out_dtype=torch.float32)
+    if T % split == 0 and T >= 256 * split:
+        part = torch.bmm(a.view(split, T // split, -1).transpose(1, 2), b.view(split, T // split, -1),
+                         out_dtype=torch.float32)
         return part.sum(0)
     return torch.mm(a.t(), b, out_dtype=torch.float32)
 
@@ -100,8 +102,10 @@ class WideBiLSTM(torch.autograd.Function):
 
 class WideSeqBiLSTM(torch.autograd.Function):
     """Embedding + BiLSTM of the wide path on hand-written kernels (lstm_wide.hip, U in {64, 100, 128}):
-      wide_x_gather     the encoder input rows Xb [S*L, E + 2PD] bf16 in one pass;
-      one GEMM          x W_x for both directions (permuted, pre-scaled gate columns, bf16 out);
+      wide_x_gather     the encoder input rows Xb [S*L, DP] bf16 in one pass (E + 2PD embedding columns,
+                        a ones column, zero padding: packing.wide_x_cols);
+      one GEMM          x W_x for both directions side by side (permuted, pre-scaled gate columns, bf16
+                        out, [S*L, 2 G4]);
       lstm_wide_seq_fwd the whole forward recurrence in ONE launch (W_h in registers, h through LDS,
                         fused bias / activations / DropoutWrapper output);
       lstm_wide_seq_bwd the whole BPTT in one launch (dG stash); weight gradients as whole-sequence
@@ -121,12 +125,12 @@ class WideSeqBiLSTM(torch.autograd.Function):
                              p1emb.detach().float().contiguous(), p2emb.detach().float().contiguous())
         # x W_x for both directions as ONE bf16-output GEMM (the kernel adds the fp32 biases): an fp32 output
         # plus a separate bias pass moved ~15 GB per step at the paper configuration
-        gx = torch.bmm(Xb.unsqueeze(0).expand(2, -1, -1), pk["wx"])
+        gx = torch.mm(Xb, pk["wxc"])
         need = any(ctx.needs_input_grad[4:11])
         hout, hprev, acts, cst = o.lstm_wide_seq_fwd(gx, pk["bx"], pk["apk"], S, L, U, bool(need), int(seed),
                                                      float(keep_prob))
         if need:
-            ctx.save_for_backward(inst, word, pos1, pos2, Xb, pk["wxt"], pk["a2pk"], hprev, acts, cst)
+            ctx.save_for_backward(inst, word, pos1, pos2, Xb, pk["wxtc"], pk["a2pk"], hprev, acts, cst)
             ctx.cfg = (S, L, E, P, U, int(seed), float(keep_prob), bool(pos_shift), p1emb.shape[0], wemb.shape[0])
         return hout
 
@@ -134,21 +138,23 @@ class WideSeqBiLSTM(torch.autograd.Function):
     def backward(ctx, dout):
         from .packing import unpack_wide_grads
         o = ops()
-        inst, word, pos1, pos2, Xb, wxt, a2pk, hprev, acts, cst = ctx.saved_tensors
+        inst, word, pos1, pos2, Xb, wxtc, a2pk, hprev, acts, cst = ctx.saved_tensors
         S, L, E, P, U, seed, kp, shift, P2, V = ctx.cfg
+        D = E + 2 * P
         dG = o.lstm_wide_seq_bwd(dout.contiguous().to(torch.bfloat16), acts, cst, a2pk, S, L, U, seed, kp)
-        UP = hprev.shape[-1]
+        UP, G4 = hprev.shape[-1], dG.shape[1] // 2
+        # ONE GEMM for both directions' x-kernel gradients; Xb's ones column (row D) makes it the bias
+        # gradient as well (no separate column-sum pass over dG)
+        dwx = _wgrad(Xb, dG)                                              # [DP, 2 G4]
         dKs, dbs = [], []
         for d in range(2):
-            g = dG[d]
-            dK, db = unpack_wide_grads(_wgrad(Xb, g), _wgrad(hprev[d].reshape(S * L, UP), g),
-                                       g.sum(0, dtype=torch.float32), U)
+            c = slice(d * G4, (d + 1) * G4)
+            dK, db = unpack_wide_grads(dwx[:D, c], _wgrad(hprev[d].reshape(S * L, UP), dG[:, c], 64), dwx[D, c], U)
             dKs.append(dK)
             dbs.append(db)
         need_w = ctx.needs_input_grad[4]
-        cols = slice(0, E + 2 * P) if need_w else slice(E, E + 2 * P)
-        dX = torch.mm(dG[0], wxt[0][cols].t(), out_dtype=torch.float32)
-        dX += torch.mm(dG[1], wxt[1][cols].t(), out_dtype=torch.float32)
+        cols = slice(0, D) if need_w else slice(E, D)
+        dX = torch.mm(dG, wxtc[cols].t(), out_dtype=torch.float32)      # both directions: K = 2 G4
         dxp = dX[:, -2 * P:].contiguous()
         if shift:
             tp = o.wide_pos_grad(dxp, inst, pos1, pos2, P2)

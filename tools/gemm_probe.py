@@ -1,0 +1,46 @@
+"""Time the wide path's big GEMM shapes under layout variants (hipBLASLt picks differ by shape/stride).
+usage (GPU box): python tools/gemm_probe.py"""
+import torch
+
+T = 32000 * 37
+dev = "cuda"
+
+
+def bench(name, fn, it=10):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    print(f"{s.elapsed_time(e) / it * 1000:9.1f} us  {name}", flush=True)
+
+
+bf = torch.bfloat16
+for K in (310, 312, 320):
+    X = torch.randn(T, K, device=dev, dtype=bf)
+    W = torch.randn(K, 1024, device=dev, dtype=bf)
+    Wt = W.t().contiguous()
+    bench(f"gx mm X[T,{K}] W[{K},1024]", lambda: torch.mm(X, W))
+    bench(f"gx mm X[T,{K}] Wt.t()", lambda: torch.mm(X, Wt.t()))
+    bench(f"gx (W^T X^T)^T: mm(Wt, X.t())", lambda: torch.mm(Wt, X.t()))
+    G = torch.randn(T, 1024, device=dev, dtype=bf)
+    bench(f"dwx mm(X.t(), G) fp32 K={K}", lambda: torch.mm(X.t(), G, out_dtype=torch.float32))
+    for sp in (8, 16, 32, 64):
+        bench(f"dwx split{sp} bmm K={K}", lambda: torch.bmm(X.view(sp, T // sp, K).transpose(1, 2), G.view(sp, T // sp, 1024),
+                                                            out_dtype=torch.float32).sum(0))
+    del X, W, Wt, G
+Hp = torch.randn(2, T, 128, device=dev, dtype=bf)
+G = torch.randn(T, 1024, device=dev, dtype=bf)
+for sp in (16, 64):
+    bench(f"dwh strided split{sp}", lambda: torch.bmm(Hp[0].view(sp, T // sp, 128).transpose(1, 2),
+                                                      G[:, :512].view(sp, T // sp, 512), out_dtype=torch.float32).sum(0))
+bench("dwh both dirs as one [T, 256]^T [T, 1024] (wasteful 2x)", lambda: torch.mm(Hp.permute(1, 0, 2).reshape(T, 256).t(), G, out_dtype=torch.float32))
+Wp = torch.randn(1024, 10, device=dev, dtype=bf)
+bench("dX pos mm(G, W[1024,10])", lambda: torch.mm(G, Wp, out_dtype=torch.float32))
+Wp16 = torch.randn(1024, 16, device=dev, dtype=bf)
+bench("dX pos mm(G, W[1024,16])", lambda: torch.mm(G, Wp16, out_dtype=torch.float32))
+bench("dX pos mm(G, W16) bf16 out", lambda: torch.mm(G, Wp16))
