@@ -388,7 +388,7 @@ def unpack_wide_grads(dwx: torch.Tensor, dwh: torch.Tensor, db: torch.Tensor, U:
 
 
 @lru_cache(maxsize=None)
-def _attn_idx(H: int):
+def _attn_wide_idx(H: int):
     """Flat indices into a zero-padded [HP, HP] W1 (HP = H rounded up to 32) for the fused attention
     kernels' MFMA A fragments [HP/16 tiles][HP/32 K-steps][64 lanes][8] (csrc/kernels/attn_wide.hip):
     lane l of tile t, K-step ks, element i covers row 16t + (l & 15) and k = 32ks + 8(l >> 4) + i;
@@ -406,9 +406,9 @@ def _attn_idx(H: int):
 
 def pack_attn_wide(W1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor):
     """Self-attention weights (W1 [H, H], b1 [H], w2 [H, 1]) -> the fused attention kernels' operands:
-    w1t / w1 bf16 A fragments (see _attn_idx), b1 / w2 fp32 zero-padded to HP."""
+    w1t / w1 bf16 A fragments (see _attn_wide_idx), b1 / w2 fp32 zero-padded to HP."""
     H = W1.shape[0]
-    HP, it, iw = _attn_idx(H)
+    HP, it, iw = _attn_wide_idx(H)
     dev = W1.device
     Wp = torch.zeros(HP, HP, device=dev, dtype=torch.float32)
     Wp[:H, :H] = W1.detach().float()

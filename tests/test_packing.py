@@ -182,3 +182,14 @@ def test_attn_wide_fragments():
             assert float(a[t, ks, l, i]) == float(Wp[k, r])
             assert float(b[t, ks, l, i]) == float(Wp[r, k])
         assert pk["b1"].shape == (HP,) and float(pk["w2"][H:].abs().sum()) == 0.0
+
+
+def test_narrow_and_wide_attention_index_helpers_coexist():
+    """The fused narrow path's pack index (ops/glue.py -> packing._attn_idx(H2, bf16)) and the wide
+    attention's fragments (packing._attn_wide_idx(H)) are separate helpers: a name clash once broke
+    every narrow-path step."""
+    from induction_network_on_fewrel_amd.ops import packing
+    pi, ti = packing._attn_idx(40, True)
+    assert pi.numel() > 0 and ti.numel() > 0
+    HP, it, iw = packing._attn_wide_idx(256)
+    assert HP == 256 and it.numel() == iw.numel() == 256 * 256

@@ -6,7 +6,8 @@ uses the same held-out relations as ``train.py --split_val true --train_relation
 ``--instance`` mirrors ``--split_mode instance`` (prototypes and queries from the last 30% of each
 relation).  Episodes: N-way K-shot, 5 queries per class, 2000 episodes.
 
-usage: python tools/tfidf_baseline.py [--val gpudata/val.json] [--train_relations 11] [--instance]
+usage: python tools/tfidf_baseline.py [--val gpudata/val.json] [--train_relations 11] [--instance] [--fold k]
+(--fold k: the held-out relations of ``train.py --fold k``, relations 5k .. 5k+4 in JSON order, wrapping)
 """
 import argparse
 import collections
@@ -22,6 +23,7 @@ def main():
     ap.add_argument("--train_relations", type=int, default=11)
     ap.add_argument("--instance", action="store_true")
     ap.add_argument("--episodes", type=int, default=2000)
+    ap.add_argument("--fold", type=int, default=-1)
     args = ap.parse_args()
     d = json.load(open(args.val))
     rels = list(d.keys())
@@ -29,7 +31,8 @@ def main():
         test = rels
         pools = {r: d[r][int(round(0.7 * len(d[r]))):] for r in rels}
     else:
-        test = rels[args.train_relations:]
+        test = ([rels[(5 * args.fold + i) % len(rels)] for i in range(5)] if args.fold >= 0
+                else rels[args.train_relations:])
         pools = {r: d[r] for r in test}
     docs = {r: [[t.lower() for t in x["tokens"]] for x in d[r]] for r in rels}
     df = collections.Counter()
@@ -62,7 +65,7 @@ def main():
                 ql += [i] * 5
             P, Qm = np.stack(protos), np.concatenate(qs)
             acc.append(((Qm @ P.T).argmax(1) == np.array(ql)).mean())
-        print(json.dumps({"split": "instance" if args.instance else "relation", "way": 5, "shot": K,
+        print(json.dumps({"split": "instance" if args.instance else "relation", "fold": args.fold, "way": 5, "shot": K,
                           "accuracy": round(float(np.mean(acc)), 4)}))
 
 

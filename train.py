@@ -33,6 +33,9 @@ def build_parser():
     p.add_argument("--eval_only", type=lambda s: s.lower() in ("1", "true", "yes"), default=False)
     p.add_argument("--train_relations", type=int, default=0,
                    help="with --split_val: how many of val.json's relations train (default: half)")
+    p.add_argument("--fold", type=int, default=-1,
+                   help="with --split_val (relation mode): hold out relations 5*fold .. 5*fold+4 (JSON order, "
+                        "wrapping) and train on the rest -- rotating folds for mean +- std accuracy")
     p.add_argument("--split_mode", default="relation", choices=["relation", "instance"],
                    help="with --split_val: 'relation' = disjoint relations (few-shot transfer); 'instance' = "
                         "every relation in both halves, disjoint sentences (train_fraction of each relation)")
@@ -70,7 +73,13 @@ def load_data(cfg: Config, args):
                 raise SystemExit("--split_mode instance is implemented for the BiLSTM encoder")
             return (full.subset_relations(rels, "train_split", part=(0.0, f)),
                     full.subset_relations(rels, "val_split", part=(f, 1.0)))
-        half = args.train_relations or len(rels) // 2
+        if getattr(args, "fold", -1) >= 0:   # rotate: the held-out block of 5 relations goes last
+            test = [rels[(5 * args.fold + i) % len(rels)] for i in range(5)]
+            rels = [r for r in rels if r not in test] + test
+            half = len(rels) - 5
+            print(f"fold {args.fold}: held-out relations {test}", flush=True)
+        else:
+            half = args.train_relations or len(rels) // 2
         tr, va = full.subset_relations(rels[:half], "train_split"), full.subset_relations(rels[half:], "val_split")
         return _with_bert(cfg, tr, va, cfg.val_file, full, rels, half)
     tr = FewRelDataset.from_json(cfg.train_file, wv, cfg.max_length, cfg.case_sensitive, processed_dir=cfg.processed_dir)
