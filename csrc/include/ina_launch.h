@@ -233,6 +233,17 @@ int wide_attn_grid(int H, int L, int S, bool bwd);   // persistent grid (residen
 int wide_attn_fwd(const WideAttnArgs& a, int grid, hipStream_t st);
 int wide_attn_bwd(const WideAttnArgs& a, int grid, hipStream_t st);   // part: [grid][2][HP]
 
+// wide induction / relation head (head_wide.hip): routing iterations over e_hat [items][K][H] fp32
+// (items = episodes * N), NTN ReLU / FC / sigmoid epilogue over T [rows][N*h] (column c*h + s)
+bool routing_wide_supported(int K, int H, int R);
+int routing_wide_fwd(const float* eh, int items, int K, int H, int R, float* cls, void* cls_bf, hipStream_t st);
+int routing_wide_bwd(const float* eh, const float* dcls, int items, int K, int H, int R, float* deh, hipStream_t st);
+bool ntn_wide_epi_supported(int N, bool paper);
+int ntn_wide_epi_fwd(const float* T, long rows, int N, int h, const float* w, const float* b, bool paper, float* probs,
+                     hipStream_t st);
+int ntn_wide_epi_bwd(float* T, long rows, int N, int h, const float* w, const float* dz, const float* g, bool paper,
+                     void* dT, float* dzs, hipStream_t st);
+
 // ---------------------------------------------------------------- BERT (csrc/kernels/bert.hip)
 struct BertLnArgs {          // y = LN(res + dropout(a)); HD = 256 * {1..4}
   const void* a;

@@ -303,7 +303,84 @@ bool wide_attn_ok(int64_t H, int64_t L) {
          ina::wide_attn_smem((int)H, (int)L, true) <= 160 * 1024;
 }
 
+// ---------------------------------------------------------------- wide head (head_wide.hip)
+bool routing_wide_ok(int64_t K, int64_t H, int64_t R) { return ina::routing_wide_supported((int)K, (int)H, (int)R); }
+
+// eh [items * K, H] fp32 -> (cls [items, H] fp32, cls_bf [items, H] bf16)
+std::tuple<Tensor, Tensor> routing_wide_fwd(const Tensor& eh, int64_t items, int64_t K, int64_t R) {
+  TORCH_CHECK(eh.dim() == 2, "ina.routing_wide_fwd: eh must be [items * K, H]");
+  const int64_t H = eh.size(1);
+  TORCH_CHECK(ina::routing_wide_supported((int)K, (int)H, (int)R), "ina.routing_wide_fwd: unsupported K/H/R");
+  chk(eh, "eh", at::kFloat, items * K * H);
+  auto cls = at::empty({items, H}, eh.options());
+  auto cls_bf = at::empty({items, H}, eh.options().dtype(at::kBFloat16));
+  TORCH_CHECK(ina::routing_wide_fwd(eh.data_ptr<float>(), (int)items, (int)K, (int)H, (int)R, cls.data_ptr<float>(),
+                                    cls_bf.data_ptr(), c10::hip::getCurrentHIPStream().stream()) == 0,
+              "ina.routing_wide_fwd: launch failed");
+  return {cls, cls_bf};
+}
+
+// eh [items * K, H], dcls [items, H] fp32 -> deh [items * K, H] fp32
+Tensor routing_wide_bwd(const Tensor& eh, const Tensor& dcls, int64_t items, int64_t K, int64_t R) {
+  TORCH_CHECK(eh.dim() == 2, "ina.routing_wide_bwd: eh must be [items * K, H]");
+  const int64_t H = eh.size(1);
+  TORCH_CHECK(ina::routing_wide_supported((int)K, (int)H, (int)R), "ina.routing_wide_bwd: unsupported K/H/R");
+  chk(eh, "eh", at::kFloat, items * K * H);
+  chk(dcls, "dcls", at::kFloat, items * H);
+  auto deh = at::empty_like(eh);
+  TORCH_CHECK(ina::routing_wide_bwd(eh.data_ptr<float>(), dcls.data_ptr<float>(), (int)items, (int)K, (int)H, (int)R,
+                                    deh.data_ptr<float>(), c10::hip::getCurrentHIPStream().stream()) == 0,
+              "ina.routing_wide_bwd: launch failed");
+  return deh;
+}
+
+bool ntn_wide_epi_ok(int64_t N, bool paper) { return ina::ntn_wide_epi_supported((int)N, paper); }
+
+static void epi_check(const Tensor& T, int64_t N, int64_t h, const Tensor& w, bool paper, const char* op) {
+  TORCH_CHECK(T.is_cuda() && T.is_contiguous() && T.scalar_type() == at::kFloat, op, ": T must be contiguous fp32");
+  TORCH_CHECK(N >= 1 && h >= 1 && T.numel() % (N * h) == 0, op, ": T is not [rows, N*h]");
+  TORCH_CHECK(ina::ntn_wide_epi_supported((int)N, paper), op, ": unsupported N for this head");
+  chk(w, "w", at::kFloat, paper ? h : h * N * N);
+}
+
+// T [rows, N*h] fp32 (column c*h + s) -> probs [rows, N]
+Tensor ntn_wide_epi_fwd(const Tensor& T, int64_t N, int64_t h, const Tensor& w, const Tensor& b, bool paper) {
+  epi_check(T, N, h, w, paper, "ina.ntn_wide_epi_fwd");
+  chk(b, "b", at::kFloat, paper ? 1 : N);
+  const int64_t rows = T.numel() / (N * h);
+  auto probs = at::empty({rows, N}, T.options());
+  TORCH_CHECK(ina::ntn_wide_epi_fwd(T.data_ptr<float>(), (long)rows, (int)N, (int)h, w.data_ptr<float>(),
+                                    b.data_ptr<float>(), paper, probs.data_ptr<float>(),
+                                    c10::hip::getCurrentHIPStream().stream()) == 0,
+              "ina.ntn_wide_epi_fwd: launch failed");
+  return probs;
+}
+
+// T (in: pre-ReLU, out: ReLU(T)), dz [rows, N] fp32, g: [] or [1] upstream scale -> (dT [rows, N*h] bf16, dzs)
+std::tuple<Tensor, Tensor> ntn_wide_epi_bwd(Tensor T, int64_t N, int64_t h, const Tensor& w, const Tensor& dz,
+                                            const Tensor& g, bool paper) {
+  epi_check(T, N, h, w, paper, "ina.ntn_wide_epi_bwd");
+  const int64_t rows = T.numel() / (N * h);
+  chk(dz, "dz", at::kFloat, rows * N);
+  TORCH_CHECK(g.numel() == 0 || (g.numel() == 1 && g.is_cuda() && g.scalar_type() == at::kFloat),
+              "ina.ntn_wide_epi_bwd: g must be empty or one fp32 GPU scalar");
+  auto dT = at::empty({rows, N * h}, T.options().dtype(at::kBFloat16));
+  auto dzs = at::empty({rows, N}, T.options());
+  TORCH_CHECK(ina::ntn_wide_epi_bwd(T.data_ptr<float>(), (long)rows, (int)N, (int)h, w.data_ptr<float>(),
+                                    dz.data_ptr<float>(), g.numel() ? g.data_ptr<float>() : nullptr, paper,
+                                    dT.data_ptr(), dzs.data_ptr<float>(),
+                                    c10::hip::getCurrentHIPStream().stream()) == 0,
+              "ina.ntn_wide_epi_bwd: launch failed");
+  return {dT, dzs};
+}
+
 TORCH_LIBRARY_FRAGMENT(ina, m) {
+  m.def("routing_wide_ok", &routing_wide_ok);
+  m.def("routing_wide_fwd", &routing_wide_fwd);
+  m.def("routing_wide_bwd", &routing_wide_bwd);
+  m.def("ntn_wide_epi_ok", &ntn_wide_epi_ok);
+  m.def("ntn_wide_epi_fwd", &ntn_wide_epi_fwd);
+  m.def("ntn_wide_epi_bwd", &ntn_wide_epi_bwd);
   m.def("lstm_wide_fwd_step", &lstm_wide_fwd_step);
   m.def("lstm_wide_bwd_step", &lstm_wide_bwd_step);
   m.def("lstm_wide_seq_fwd", &lstm_wide_seq_fwd);

@@ -63,6 +63,18 @@ class InductionNetwork(nn.Module):
             return head_wide(e, p, B, N, K, Q, cfg.routing_iters, cfg.relation_head)
         return ref.head_forward(p, e.float(), B, N, K, Q, cfg.routing_iters, cfg.relation_head)
 
+    def use_wide_head_loss(self, inst, data, N: int, K: int, Q: int) -> bool:
+        """Training step through the wide head's fused loss node (head_wide.hip + ina.head_loss): GPU, bf16,
+        a head shape outside the fused head kernels, and one the wide head kernels cover."""
+        cfg = self.cfg
+        if not (inst.is_cuda and cfg.dtype == "bf16"):
+            return False
+        H = int(self.params.head_dim)
+        if H in (16, 40, 64) and N <= 16 and N * Q <= 64:
+            return False
+        from ..ops.wide import head_wide_ok
+        return head_wide_ok(H, N, K, cfg.routing_iters, cfg.relation_head)
+
     def check_gpu_config(self, N: int, Q: int, L: int) -> None:
         u = self.cfg.hidden_size
         din = self.params.input_dim
@@ -78,10 +90,12 @@ class InductionNetwork(nn.Module):
     def forward(self, inst: torch.Tensor, data: Tuple[torch.Tensor, ...], B: int, N: int, K: int, Q: int,
                 training: bool = True, dropout_seed: int = 0,
                 grad_views: Optional[Dict[str, torch.Tensor]] = None, overlap=None,
-                seed_dev: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                seed_dev: Optional[torch.Tensor] = None, embeddings_only: bool = False
+                ) -> Tuple[torch.Tensor, torch.Tensor]:
         """inst: int32 [B*(N*K+N*Q)] instance rows (episode layout, support first).
         data: (word, pos1, pos2, mask) [NI, L] int32 on the same device.
-        Returns probs [B, N*Q, N] and alphas [B*(N*K+N*Q), L]."""
+        Returns probs [B, N*Q, N] and alphas [B*(N*K+N*Q), L] (``embeddings_only``: the sentence
+        vectors e [B*(N*K+N*Q), H] instead of probs; GPU path only)."""
         cfg = self.cfg
         kp = cfg.keep_prob if training else 1.0
         p = self.pdict()
@@ -89,7 +103,8 @@ class InductionNetwork(nn.Module):
             raise ValueError(f"reference relation head was built for N={p['ntn_w'].shape[1]}, got N={N} "
                              "(use relation_head='paper' for N-independent scoring)")
         if cfg.encoder == "bert":
-            return self._forward_bert(inst, data, B, N, K, Q, training, dropout_seed, grad_views, p, overlap)
+            return self._forward_bert(inst, data, B, N, K, Q, training, dropout_seed, grad_views, p, overlap,
+                                      embeddings_only)
         if inst.is_cuda:
             word, pos1, pos2, mask = data
             if self.use_fused_lstm(word.shape[1]):
@@ -105,19 +120,24 @@ class InductionNetwork(nn.Module):
                 if cfg.lstm_skip_padding:
                     raise NotImplementedError("lstm_skip_padding: the wide GPU path runs the reference's full L")
                 e, alphas = encode_wide(inst, data, p, cfg.hidden_size, kp, int(dropout_seed))
+            if embeddings_only:
+                return e, alphas
             return self._head(e, p, B, N, K, Q, grad_views), alphas
         word, pos1, pos2, mask = (t[inst.long()] for t in data)
         probs, alphas = ref.forward(p, word, pos1, pos2, mask, B, N, K, Q, cfg.routing_iters, cfg.relation_head,
                                     kp, int(dropout_seed), bf16=False, skip_padding=cfg.lstm_skip_padding)
         return probs, alphas.squeeze(-1)
 
-    def _forward_bert(self, inst, data, B, N, K, Q, training, dropout_seed, grad_views, p, overlap=None):
+    def _forward_bert(self, inst, data, B, N, K, Q, training, dropout_seed, grad_views, p, overlap=None,
+                      embeddings_only=False):
         """BERT encoder (data = (ids, mask, e1, e2) [NI, Lb] int32) + the same induction/relation head.
         Returns probs and the [CLS]-row attention-free placeholder alphas (None)."""
         cfg = self.cfg
         if inst.is_cuda:
             from ..ops.bert import bert_encode
             e = bert_encode(self, inst, data, training, int(dropout_seed), grad_views, overlap)
+            if embeddings_only:
+                return e, None
             return self._head(e, p, B, N, K, Q, grad_views), None
         from . import bert as Bm
         ids, mask, e1, e2 = (t[inst.long()] for t in data)
@@ -141,6 +161,12 @@ class InductionNetwork(nn.Module):
         fused = (glue is not None and inst.is_cuda and cfg.encoder == "bilstm" and grad_views is not None
                  and self.use_fused_lstm(data[0].shape[1]) and H in (16, 40, 64) and N <= 16 and N * Q <= 64
                  and not (cfg.relation_head == "reference" and p["ntn_w"].shape[1] != N))
+        if not fused and self.use_wide_head_loss(inst, data, N, K, Q):
+            from ..ops.wide import head_wide_loss
+            e, _ = self.forward(inst, data, B, N, K, Q, training=True, dropout_seed=dropout_seed,
+                                grad_views=grad_views, overlap=overlap, seed_dev=seed_dev, embeddings_only=True)
+            return head_wide_loss(e, p, labels, B, N, K, Q, cfg.routing_iters, cfg.relation_head, cfg.loss_type,
+                                  cfg.loss_reduction)
         if not fused:
             probs, _ = self.forward(inst, data, B, N, K, Q, training=True, dropout_seed=dropout_seed,
                                     grad_views=grad_views, overlap=overlap, seed_dev=seed_dev)

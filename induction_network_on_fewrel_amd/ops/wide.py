@@ -324,7 +324,151 @@ class TallSkinnyMM(torch.autograd.Function):
         return dx, dw
 
 
+def head_wide_ok(H: int, N: int, K: int, R: int, head: str) -> bool:
+    """Shapes the hand-written wide head (csrc/kernels/head_wide.hip) covers."""
+    o = ops()
+    return bool(o.routing_wide_ok(K, H, R)) and bool(o.ntn_wide_epi_ok(N, head == "paper"))
+
+
+def _split_sum_mm(a: torch.Tensor, b: torch.Tensor, nb: int = 64) -> torch.Tensor:
+    """a^T b (fp32) for tall a [T, m], b [T, n]: K = T split into nb batched slices + an ordered sum."""
+    T = a.shape[0]
+    if T % nb or T < 64 * nb:
+        nb = 1
+    return torch.bmm(a.view(nb, T // nb, -1).transpose(1, 2), b.view(nb, T // nb, -1)).sum(0)
+
+
+def _wide_head_forward(e, Ws, M, w, b, E, N, K, Q, R, paper):
+    """Routing (e_hat GEMM + routing_wide_fwd) -> NTN (P = C M', T = Q P^T as bf16 GEMMs) -> epilogue.
+    M' = M permuted to [a, (s, b')] so that P [E*N, h*H] viewed [E, N*h, H] is each episode's
+    [(class, slice), feature] operand: T[e] = Q[e] P[e]^T is ONE batched GEMM with columns c*h + s."""
+    o = ops()
+    H, h = e.shape[1], M.shape[2]
+    NK, NQ = N * K, N * Q
+    ev = e.view(E, NK + NQ, H)
+    sup = ev[:, :NK].reshape(E * NK, H).float()
+    eh = torch.mm(sup, Ws.detach().float())                                     # [E*NK, H] fp32
+    cls, cls_bf = o.routing_wide_fwd(eh, E * N, K, R)
+    Mt = M.detach().permute(0, 2, 1).reshape(H, h * H).to(torch.bfloat16)      # [a, s*H + b']
+    P = torch.mm(cls_bf, Mt)                                                    # [E*N, h*H] bf16
+    qb = ev[:, NK:].to(torch.bfloat16).contiguous()                             # [E, NQ, H]
+    T = torch.bmm(qb, P.view(E, N * h, H).transpose(1, 2), out_dtype=torch.float32)   # [E, NQ, N*h]
+    wf = w.detach().float().contiguous().view(-1)
+    probs = o.ntn_wide_epi_fwd(T, N, h, wf, b.detach().float().contiguous().view(-1), paper)
+    return probs.view(E, NQ, N), (sup, eh, cls_bf, Mt, P, qb, T, wf)
+
+
+def _wide_head_backward(ctx, dz, g):
+    """Shared backward of HeadWideFn / HeadWideLossFn: dz = dL/dlogit [E*NQ, N] (g: upstream scale)."""
+    o = ops()
+    sup, eh, cls_bf, Mt, P, qb, T, wf, Ws = ctx.saved_tensors
+    E, N, K, Q, R, paper = ctx.cfg
+    H, h = sup.shape[1], T.shape[2] // N
+    NK, NQ = N * K, N * Q
+    dT, dzs = o.ntn_wide_epi_bwd(T, N, h, wf, dz, g, paper)                     # T <- ReLU(T)
+    dT = dT.view(E, NQ, N * h)
+    dQ = torch.bmm(dT, P.view(E, N * h, H), out_dtype=torch.float32)           # [E, NQ, H]
+    dP = torch.bmm(dT.transpose(1, 2), qb)                                      # [E, N*h, H] bf16
+    dPf = dP.view(E * N, h * H)
+    dcls = torch.mm(dPf, Mt.t(), out_dtype=torch.float32)                       # [E*N, H]
+    dMt = _wgrad(cls_bf, dPf, _dm_split(E * N))                                 # [H, h*H] fp32
+    dM = dMt.view(H, h, H).permute(0, 2, 1)
+    deh = o.routing_wide_bwd(eh, dcls, E * N, K, R)                            # [E*NK, H]
+    dWs = torch.mm(sup.t(), deh)
+    dsup = torch.mm(deh, Ws.t())
+    de = torch.cat([dsup.view(E, NK, H), dQ], 1).view(E * (NK + NQ), H)
+    V = T.view(E * NQ, N * h)
+    if paper:
+        dw = _split_sum_mm(V.view(-1, h), dzs.view(-1, 1))                     # [h, 1]
+        db = dzs.sum().view(1)
+    else:
+        dw = _split_sum_mm(V, dzs).view(N, h, N).permute(1, 0, 2).reshape(h * N, N)   # row s*N + c
+        db = dzs.sum(0)
+    return de, dWs, dM, dw, db
+
+
+def _dm_split(rows: int) -> int:
+    for ns in (8, 4, 2):
+        if rows % ns == 0 and rows // ns >= 256:
+            return ns
+    return 1
+
+
+class HeadWideProbsFn(torch.autograd.Function):
+    """Wide routing + NTN head -> probs, differentiable w.r.t. e and the head parameters."""
+
+    @staticmethod
+    def forward(ctx, e, Ws, M, w, b, cfg):
+        E, N, K, Q, R, paper = cfg
+        probs, saved = _wide_head_forward(e, Ws, M, w, b, E, N, K, Q, R, paper)
+        ctx.save_for_backward(*saved, Ws.detach().float())
+        ctx.cfg = cfg
+        ctx.edtype = e.dtype
+        ctx.probs = probs
+        return probs
+
+    @staticmethod
+    def backward(ctx, dprobs):
+        p = ctx.probs
+        dz = (dprobs * p * (1.0 - p)).float().contiguous().view(-1, ctx.cfg[1])
+        g = torch.empty(0, device=dz.device)
+        de, dWs, dM, dw, db = _wide_head_backward(ctx, dz, g)
+        return de.to(ctx.edtype), dWs, dM, dw, db, None
+
+
+class HeadWideLossFn(torch.autograd.Function):
+    """Wide routing + NTN + sigmoid + loss (MSE / CE) + accuracy in one autograd node: the loss,
+    accuracy and dL/dlogit come from ina.head_loss (glue.hip) in one launch; the backward scales dz by
+    the upstream loss gradient on the device.  Returns (loss, accuracy, probs)."""
+
+    LOSS_BLOCKS = 64
+
+    @staticmethod
+    def forward(ctx, e, Ws, M, w, b, labels, cfg, loss_type, reduction):
+        o = ops()
+        E, N, K, Q, R, paper = cfg
+        probs, saved = _wide_head_forward(e, Ws, M, w, b, E, N, K, Q, R, paper)
+        rows = E * N * Q
+        ce = loss_type == "ce"
+        scale = (1.0 / rows if ce else 1.0 / (rows * N)) if reduction == "mean" else 1.0 / max(1, E)
+        dz = torch.empty(rows, N, dtype=torch.float32, device=e.device)
+        out = torch.empty(N + 3, dtype=torch.float32, device=e.device)
+        blocks = max(1, min(HeadWideLossFn.LOSS_BLOCKS, (rows + 255) // 256))
+        part = torch.empty(blocks * 18, dtype=torch.float32, device=e.device)
+        o.head_loss(probs.view(rows, N), labels.reshape(-1).int().contiguous(), scale, dz, out, part, blocks, ce)
+        ctx.save_for_backward(*saved, Ws.detach().float())
+        ctx.dz = dz
+        ctx.cfg = cfg
+        ctx.edtype = e.dtype
+        ctx.set_materialize_grads(False)
+        loss, acc = out[0], out[1]
+        ctx.mark_non_differentiable(acc, probs)
+        return loss, acc, probs
+
+    @staticmethod
+    def backward(ctx, gloss, _gacc, _gprobs):
+        g = (gloss.reshape(1).float().contiguous() if gloss is not None
+             else torch.zeros(1, device=ctx.dz.device))
+        de, dWs, dM, dw, db = _wide_head_backward(ctx, ctx.dz, g)
+        return de.to(ctx.edtype), dWs, dM, dw, db, None, None, None, None
+
+
 def head_wide(e, p, B: int, N: int, K: int, Q: int, iters: int, head: str):
+    """Routing + relation head at widths outside the fused kernels (the paper's H = 2u = 256): the
+    hand-written wide head (head_wide.hip + GEMMs) when it covers the shape, else the GEMM formulation."""
+    if head_wide_ok(e.shape[-1], N, K, iters, head):
+        return HeadWideProbsFn.apply(e, p["W_s"], p["M"], p["ntn_w"], p["ntn_b"], (B, N, K, Q, iters, head == "paper"))
+    return head_wide_torch(e, p, B, N, K, Q, iters, head)
+
+
+def head_wide_loss(e, p, labels, B: int, N: int, K: int, Q: int, iters: int, head: str, loss_type: str,
+                   reduction: str):
+    """(loss, accuracy, probs) of the wide head with the fused loss kernel."""
+    return HeadWideLossFn.apply(e, p["W_s"], p["M"], p["ntn_w"], p["ntn_b"], labels,
+                                (B, N, K, Q, iters, head == "paper"), loss_type, reduction)
+
+
+def head_wide_torch(e, p, B: int, N: int, K: int, Q: int, iters: int, head: str):
     """Routing + relation head at widths outside the fused kernels (the paper's H = 2u = 256):
     dynamic routing in fp32 (models/reference.py), the neural tensor layer's two contractions
     (P = C M over all classes at once, then T = Q P per episode) as bf16 MFMA GEMMs with
