@@ -223,6 +223,7 @@ def main():
             "params_in_sync": bool(in_sync),
             "rccl_world": (torch.distributed.get_world_size() if dist.initialized else 1),
             "backend": dist.backend or "none",
+            "comm": dist.comm_name,
             "rank_ms_per_step": rank_ms,
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if cuda else 0.0,
         }

@@ -107,7 +107,7 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
                 print(out)
     if tasks or not os.path.exists(LIB) or _newer(LIB, objs):
         cmd = [hipcc, "-shared", "-fPIC", "-o", LIB, *objs, f"-L{tlib}", "-ltorch", "-ltorch_cpu", "-lc10",
-               "-lc10_hip", "-ltorch_hip", f"-Wl,-rpath,{tlib}"]
+               "-lc10_hip", "-ltorch_hip", "-lrccl", f"-Wl,-rpath,{tlib}"]
         if _ASAN:   # the host ASan runtime (gcc's; the process preloads it)
             cmd += [subprocess.run(["gcc", "-print-file-name=libasan.so"], capture_output=True,
                                    text=True).stdout.strip()]

@@ -35,6 +35,25 @@ void gather_pack(const Tensor& src, const Tensor& idx, int64_t nb, Tensor out_bf
                                out_f32.data_ptr<float>(), stream()) == 0, op, ": launch failed");
 }
 
+// ragged record plan: inst int32 [S] (dataset rows), lengths int32 [NI] (valid lengths, <= L) ->
+// (inst_sorted, perm, tlen [ceil(S/16)], slen) = the stable argsort of lengths[inst] and its derivatives
+std::tuple<Tensor, Tensor, Tensor, Tensor> ragged_sort(const Tensor& inst, const Tensor& lengths, int64_t L) {
+  const char* op = "ina.ragged_sort";
+  need(inst, op, "inst", at::kInt);
+  need(lengths, op, "lengths", at::kInt);
+  TORCH_CHECK(L >= 0 && L <= ina::ragged_max_len(), op, ": L must be in [0, ", ina::ragged_max_len(), "]");
+  const int64_t S = inst.numel();
+  auto io = inst.options();
+  auto perm = at::empty({S}, io), inst_s = at::empty({S}, io), slen = at::empty({S}, io);
+  auto tlen = at::empty({(S + 15) / 16}, io);
+  auto ws = at::empty({std::max<int64_t>(1, 2 * (L + 1) * (int64_t)ina::ragged_blocks(S))}, io);
+  TORCH_CHECK(ina::ragged_sort(inst.data_ptr<int>(), lengths.data_ptr<int>(), (long)S, (int)L, ws.data_ptr<int>(),
+                               perm.data_ptr<int>(), inst_s.data_ptr<int>(), slen.data_ptr<int>(),
+                               tlen.data_ptr<int>(), stream()) == 0,
+              op, ": launch failed");
+  return {inst_s, perm, tlen, slen};
+}
+
 // probs [rows, N] fp32, labels int32 [rows]; writes dz [rows, N] and out [N + 3] =
 // (loss, accuracy, db[0..N), db_total); part: workspace [blocks * 18].  ce: softmax cross-entropy
 // over the pre-sigmoid scores instead of the reference MSE
@@ -109,5 +128,6 @@ int64_t slab_scatter_add(Tensor dst, const std::vector<Tensor>& srcs, const std:
 TORCH_LIBRARY_FRAGMENT(ina, m) {
   m.def("gather_pack", &gather_pack);
   m.def("head_loss", &head_loss);
+  m.def("ragged_sort", &ragged_sort);
   m.def("slab_scatter_add", &slab_scatter_add);
 }

@@ -233,6 +233,12 @@ int wide_attn_grid(int H, int L, int S, bool bwd);   // persistent grid (residen
 int wide_attn_fwd(const WideAttnArgs& a, int grid, hipStream_t st);
 int wide_attn_bwd(const WideAttnArgs& a, int grid, hipStream_t st);   // part: [grid][2][HP]
 
+// stable counting sort of rows by valid length (ragged.hip); ws >= 2 * (L + 1) * ragged_blocks(S) ints
+int ragged_blocks(long S);
+int ragged_max_len();
+int ragged_sort(const int* inst, const int* lengths, long S, int L, int* ws, int* perm, int* inst_s, int* slen,
+                int* tlen, hipStream_t st);
+
 // wide induction / relation head (head_wide.hip): routing iterations over e_hat [items][K][H] fp32
 // (items = episodes * N), NTN ReLU / FC / sigmoid epilogue over T [rows][N*h] (column c*h + s)
 bool routing_wide_supported(int K, int H, int R);

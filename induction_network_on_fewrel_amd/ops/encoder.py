@@ -70,7 +70,7 @@ def word_rows(word: torch.Tensor, wemb: torch.Tensor, fresh: bool):
 RAGGED_MIN_ROWS = 16384   # 1024 tiles: ~4 per CU
 
 
-def ragged_plan(inst: torch.Tensor, lengths: torch.Tensor, skip: bool):
+def ragged_plan(inst: torch.Tensor, lengths: torch.Tensor, skip: bool, L: int = 64):
     """Length-sorted rows for the record kernels: (inst_sorted, perm, tlen, slen).
 
     perm = the stable argsort of the rows' valid lengths (row s of every record array is row perm[s] of
@@ -79,6 +79,10 @@ def ragged_plan(inst: torch.Tensor, lengths: torch.Tensor, skip: bool):
     this is exact -- and sorted tiles make it ~the rows' own lengths.  slen (lstm_skip_padding only) =
     the sorted lengths, for the backward direction's per-row sequence_length resets."""
     S = inst.shape[0]
+    if inst.is_cuda and inst.dtype == torch.int32 and lengths.dtype == torch.int32:
+        # one counting-sort pass on the device (csrc/kernels/ragged.hip): lengths are 0..L
+        inst_s, perm, tlen, slen = ops().ragged_sort(inst.contiguous(), lengths.contiguous(), L)
+        return inst_s, perm, tlen, (slen if skip else None)
     lens = lengths.index_select(0, inst.long())
     perm = torch.argsort(lens, stable=True)
     slen = lens.index_select(0, perm)
@@ -129,7 +133,7 @@ class EncoderFn(torch.autograd.Function):
             # latency-bound on the backward direction's full-length chain and would only add the sort
             if lengths is not None and (skip or (meta.get("ragged", True)
                                                  and inst.shape[0] >= meta.get("ragged_min_rows", RAGGED_MIN_ROWS))):
-                inst, perm, tlen, slen = ragged_plan(inst, lengths, skip)
+                inst, perm, tlen, slen = ragged_plan(inst, lengths, skip, int(word.shape[1]))
                 lstm_args = (inst,) + lstm_args[1:]
             hlane, cst, hnat, dmask, xg, e, alphas = o.lstm_attn_fwd(*lstm_args, bool(need_grad), *tail,
                                                                      mask, w1pack, b1c, w2c, tlen, perm, slen)

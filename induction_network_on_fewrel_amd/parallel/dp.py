@@ -10,7 +10,8 @@ collective is pure latency, so fewer/larger steps = more episodes per GPU is wha
 Large models (BERT encoder) are bucketed at ``bucket_mb`` (default 64 MB: 7 xGMI links x ~153 GB/s
 per GPU make a ring all-reduce of 64 MB ~0.5 ms, large enough to run at link rate, small enough to
 overlap with the rest of backward). ``torch.distributed`` backend "nccl" is RCCL on ROCm; "gloo" is
-used on CPU (tests).
+used on CPU (tests).  ``INA_COMM=native`` keeps gloo for the control plane and moves every GPU tensor
+collective onto the C++ RCCL communicator of csrc/comm_bindings.cpp (parallel/native_comm.py).
 """
 from __future__ import annotations
 
@@ -29,6 +30,7 @@ class DistContext:
         self.device = device or torch.device("cpu")
         self.backend = backend
         self.initialized = False
+        self.native = None   # NativeComm when INA_COMM=native (GPU tensors), gloo for the rest
 
     @classmethod
     def from_env(cls, device: str = "auto", timeout_s: int = 1800) -> "DistContext":
@@ -50,7 +52,8 @@ class DistContext:
             os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
             # INA_DIST_BACKEND=gloo: several ranks sharing ONE GPU (RCCL refuses duplicate devices) --
             # the one-card rehearsal of the multi-rank GPU step (tests/test_dp_gpu.py)
-            backend = os.environ.get("INA_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
+            native = use_cuda and os.environ.get("INA_COMM") == "native"
+            backend = os.environ.get("INA_DIST_BACKEND") or ("nccl" if use_cuda and not native else "gloo")
             kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
             if use_cuda and backend == "nccl":
                 kw["device_id"] = dev
@@ -58,7 +61,17 @@ class DistContext:
                 dist.init_process_group(**kw)
             ctx.backend = backend
             ctx.initialized = True
+            if native:
+                from .native_comm import NativeComm
+                ctx.native = NativeComm(rank, world, dev, dist.distributed_c10d._get_default_store())
         return ctx
+
+    @property
+    def comm_name(self) -> str:
+        """Data-plane backend of the GPU collectives ("rccl-native", "nccl" = torch RCCL, "gloo", "none")."""
+        if not self.initialized:
+            return "none"
+        return "rccl-native" if self.native is not None else str(self.backend)
 
     # ------------------------------------------------------------------
     @property
@@ -73,24 +86,46 @@ class DistContext:
             else:
                 dist.barrier()
 
+    def _native_ok(self, t: torch.Tensor) -> bool:
+        return self.native is not None and t.is_cuda
+
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.initialized:
-            dist.broadcast(t, src)
+            if self._native_ok(t):
+                self.native.broadcast_(t, src)
+                self.native.wait()
+            else:
+                dist.broadcast(t, src)
         return t
 
     def allreduce_(self, t: torch.Tensor, op=None) -> torch.Tensor:
         if self.initialized:
-            dist.all_reduce(t, op=op or dist.ReduceOp.SUM)
+            if self._native_ok(t):
+                self.native.allreduce_(t, "max" if op == dist.ReduceOp.MAX else "sum")
+                self.native.wait()
+            else:
+                dist.all_reduce(t, op=op or dist.ReduceOp.SUM)
         return t
+
+    def allreduce_async_(self, t: torch.Tensor):
+        """Sum-all-reduce started now; returns a handle whose ``wait()`` orders the caller's stream."""
+        if self._native_ok(t):
+            from .native_comm import _NativeWork
+            self.native.allreduce_(t, "sum")
+            return _NativeWork(self.native)
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
 
     def allreduce_buckets_(self, flat: torch.Tensor, bucket_mb: float = 64.0) -> None:
         """Sum-all-reduce a flat buffer in ``bucket_mb`` chunks, all issued async then waited."""
         if not self.initialized or flat.numel() == 0:
             return
         n = max(1, int(bucket_mb * 1024 * 1024 // flat.element_size()))
-        works: List = []
-        for off in range(0, flat.numel(), n):
-            works.append(dist.all_reduce(flat[off:off + n], op=dist.ReduceOp.SUM, async_op=True))
+        chunks = [flat[off:off + n] for off in range(0, flat.numel(), n)]
+        if self._native_ok(flat):   # one grouped RCCL launch for all buckets
+            self.native.allreduce_many_(chunks, "sum")
+            self.native.wait()
+            return
+        works: List = [dist.all_reduce(c, op=dist.ReduceOp.SUM, async_op=True) for c in chunks]
         for w in works:
             w.wait()
 
@@ -130,6 +165,10 @@ class DistContext:
         return self.max_scalar(diff) == 0.0
 
     def destroy(self) -> None:
+        if self.native is not None:
+            self.native.sync()
+            self.native.destroy()
+            self.native = None
         if self.initialized and dist.is_initialized():
             dist.destroy_process_group()
             self.initialized = False
@@ -157,7 +196,7 @@ class OverlapAllReduce:
             return
         off, n = self.spans[i]
         self.launched[i] = True
-        self.works.append(dist.all_reduce(self.flat[off:off + n], op=dist.ReduceOp.SUM, async_op=True))
+        self.works.append(self.ctx.allreduce_async_(self.flat[off:off + n]))
 
     def finish(self) -> None:
         if not self.ctx.initialized:
@@ -172,7 +211,7 @@ class OverlapAllReduce:
         if pos < self.flat.numel():
             rest.append((pos, self.flat.numel() - pos))
         for off, n in rest:
-            self.works.append(dist.all_reduce(self.flat[off:off + n], op=dist.ReduceOp.SUM, async_op=True))
+            self.works.append(self.ctx.allreduce_async_(self.flat[off:off + n]))
         for w in self.works:
             w.wait()
         self.works = []

@@ -79,3 +79,47 @@ def test_bench_self_launch_world2_one_gpu():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["rccl_world"] == 2 and out["backend"] == "gloo"
     assert out["params_in_sync"] is True and len(out["rank_ms_per_step"]) == 2
+
+
+def test_bench_native_rccl_world1():
+    """INA_COMM=native: the gradient all-reduce, params_in_sync broadcast and bucket paths on the C++ RCCL
+    communicator (csrc/comm_bindings.cpp, its own HIP stream + events), gloo for the control plane."""
+    env = dict(os.environ, INA_FORCE_DIST="1", INA_COMM="native", OMP_NUM_THREADS="2")
+    env.pop("INA_DIST_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--steps", "3", "--warmup", "2", "--episodes-per-gpu", "64"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["comm"] == "rccl-native" and out["backend"] == "gloo" and out["rccl_world"] == 1
+    assert out["params_in_sync"] is True and out["final_loss"] == out["final_loss"]
+
+
+def test_native_comm_collectives_world1():
+    """The communicator's ops in-process: all-reduce (sum / max), grouped buckets, broadcast, the
+    stream ordering against the compute stream, async-error check."""
+    import torch
+    import torch.distributed as dist
+    from induction_network_on_fewrel_amd.parallel.native_comm import NativeComm
+    store = dist.TCPStore("127.0.0.1", _free_port(), 1, True)
+    c = NativeComm(0, 1, torch.device("cuda", 0), store, tag="t")
+    try:
+        assert c.info()["world"] == 1
+        x = torch.arange(1000, device="cuda", dtype=torch.float32)
+        y = x * 2                       # produced on the compute stream right before the enqueue
+        c.allreduce_(y)
+        c.wait()
+        z = y + 1                       # consumed after wait() on the compute stream
+        assert torch.equal(z, x * 2 + 1)
+        parts = [torch.full((n,), float(n), device="cuda") for n in (3, 7, 1 << 20)]
+        c.allreduce_many_(parts)
+        c.broadcast_(parts[0], 0)
+        c.wait()
+        assert all(bool((p == p.numel()).all()) for p in parts)
+        c.allreduce_(y, "max")
+        c.sync()
+    finally:
+        c.destroy()
