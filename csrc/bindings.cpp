@@ -377,6 +377,8 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   a.dw_slab = dw_slab.data_ptr<float>();
   a.dpos_slab = dpos_slab.data_ptr<float>();
   a.dwemb = word_grad ? dwemb.data_ptr<float>() : nullptr;
+  // the FewRel / synthetic word tables end with the padding row BLANK = V + 1 (data/fewrel.py)
+  a.wblank = word_grad ? (int)wemb.size(0) - 1 : -1;
   a.dmask = drop_ ? dmask.data_ptr<uint8_t>() : nullptr;
   a.bwd_blocks = (int)blocks;
   a.seed = (uint32_t)seed;
@@ -572,6 +574,12 @@ Tensor ntn_fwd(const Tensor& cls, const Tensor& e, const Tensor& mpack, const Te
   a.paper = paper ? 1 : 0;
   if (blocks <= 0) blocks = 1024;  // workgroups of 8 episodes (grid-stride beyond)
   a.blocks = (int)std::max<int64_t>(1, blocks);
+  a.split = ina::ntn_split((int)E, (int)h);
+  Tensor part;
+  if (a.split > 1) {
+    part = at::empty({a.split * E * N * Q * N}, e.options());
+    a.part = part.data_ptr<float>();
+  }
   check_launch(ina::ntn_fwd(a, cur_stream()), "ntn_fwd");
   return probs;
 }
@@ -637,6 +645,14 @@ std::tuple<Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tensor& e, c
   }
   if (blocks <= 0) blocks = 1024;
   a.blocks = (int)std::max<int64_t>(1, blocks);
+  a.split = ina::ntn_split((int)E, (int)h);
+  Tensor pc, pq;
+  if (a.split > 1) {
+    pc = at::empty({a.split * E * N * H}, e.options());
+    pq = at::empty({a.split * E * N * Q * H}, e.options());
+    a.part = pc.data_ptr<float>();
+    a.part2 = pq.data_ptr<float>();
+  }
   check_launch(ina::ntn_bwd(a, cur_stream()), "ntn_bwd");
   return {dcls, dp, dw};
 }

@@ -47,6 +47,7 @@ struct LstmArgs {
   const int* tlen;
   const int* slen;
   const int* perm;   // x_gather: record row s is original row perm[s] (dropout hash counter)
+  int wblank;        // bwd with a trained word table: the padding (BLANK) row id, summed in registers (-1: none)
 };
 // bf16 mode: gather every token's x features once into a.xg / a.posb, and (a.drop) the dropout keep
 // bits into a.dmask (lstm.hip x_gather_kernel); must run before lstm_fwd in bf16 mode
@@ -123,7 +124,13 @@ struct NtnArgs {
   int paper;
   const float* gscale;   // bwd: optional device scalar multiplying dz (upstream loss gradient)
   void* cls_bf;          // bwd: optional bf16 copy of cls [E*N][H] (operand of the dM GEMM)
+  // slice split (small E, ntn_split): grid.y = split workgroup rows over the slice pairs; partials in
+  // part (fwd: [split][E][NQ][N] logits; bwd: dC [split][E][N][H]) and part2 (bwd: dQ [split][E][NQ][H])
+  int split;
+  float* part;
+  float* part2;
 };
+int ntn_split(int E, int h);
 int ntn_fwd(const NtnArgs& a, hipStream_t st);
 
 // step glue (glue.hip)

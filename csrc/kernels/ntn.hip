@@ -101,7 +101,8 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(4))
                                                               const u16x8_t* __restrict__ mpack,
                                                               const u16x8_t* __restrict__ wpack,
                                                               const float* __restrict__ wvec,
-                                                              const float* __restrict__ bias, float* __restrict__ probs) {
+                                                              const float* __restrict__ bias, float* __restrict__ probs,
+                                                              float* __restrict__ part) {
   constexpr int NKA = (MTH + 1) / 2;  // K steps over a (32 each)
   constexpr int NKB = (MTH + 1) / 2;  // K steps over b (pairs of accumulator tiles)
   constexpr int NSW = PAPER ? 0 : 1;
@@ -110,6 +111,9 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(4))
   const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15, wave = threadIdx.x >> 6;
   const int NQ = N * Q;
   const int npair = (h + 1) / 2;
+  // slice split (small episode batches): workgroup row blockIdx.y takes slice pairs [p0, p1) and writes
+  // raw logit partials; ntn_fwd_finish sums them in split order (deterministic)
+  const int p0 = (int)((long)npair * blockIdx.y / gridDim.y), p1 = (int)((long)npair * (blockIdx.y + 1) / gridDim.y);
   for (int g = blockIdx.x; g * NTN_WAVES < E; g += gridDim.x) {
     const int ep = g * NTN_WAVES + wave;
     const bool act = ep < E;
@@ -138,12 +142,12 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) Lg[qt] = Z4;
     __syncthreads();  // previous group's readers are done with buffer 0
-    ntn_stage<MTH, NSW, false>(ntn_lds, 0, mpack, nullptr, wpack, 1);
+    ntn_stage<MTH, NSW, false>(ntn_lds, p0, mpack, nullptr, wpack, 1);
     stage_wait();
     __syncthreads();
-    for (int p = 0; p < npair; ++p) {
-      const u16x8_t* buf = ntn_lds + (p & 1) * FR * 64;
-      if (p + 1 < npair) ntn_stage<MTH, NSW, false>(ntn_lds + ((p + 1) & 1) * FR * 64, p + 1, mpack, nullptr, wpack, 1);
+    for (int p = p0; p < p1; ++p) {
+      const u16x8_t* buf = ntn_lds + ((p - p0) & 1) * FR * 64;
+      if (p + 1 < p1) ntn_stage<MTH, NSW, false>(ntn_lds + ((p + 1 - p0) & 1) * FR * 64, p + 1, mpack, nullptr, wpack, 1);
       if (act) {
         f32x4_t V[2][QT];
 #pragma unroll
@@ -191,12 +195,14 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(4))
       for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          if (PAPER) {  // rows c, cols query
-            const int c = 4 * q + r, qi = 16 * qt + n;
-            if (c < N && qi < NQ) probs[((long)ep * NQ + qi) * N + c] = sigmoidf_(Lg[qt][r] + bias[0]);
-          } else {      // rows query, cols c'
-            const int qi = 16 * qt + 4 * q + r, c = n;
-            if (c < N && qi < NQ) probs[((long)ep * NQ + qi) * N + c] = sigmoidf_(Lg[qt][r] + bias[c]);
+          // PAPER: rows c, cols query; reference head: rows query, cols c'
+          const int c = PAPER ? 4 * q + r : n, qi = PAPER ? 16 * qt + n : 16 * qt + 4 * q + r;
+          if (c < N && qi < NQ) {
+            const long o = ((long)ep * NQ + qi) * N + c;
+            if (gridDim.y == 1)
+              probs[o] = sigmoidf_(Lg[qt][r] + bias[PAPER ? 0 : c]);
+            else
+              part[(long)blockIdx.y * E * NQ * N + o] = Lg[qt][r];
           }
         }
     }
@@ -212,7 +218,7 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
     const u16x8_t* __restrict__ mpack, const u16x8_t* __restrict__ m2pack, const u16x8_t* __restrict__ wtpack,
     const float* __restrict__ wvec, const float* __restrict__ dz, float* __restrict__ dcls, float* __restrict__ de,
     unsigned short* __restrict__ dp_out, float* __restrict__ dw_slab, const float* __restrict__ gscale,
-    unsigned short* __restrict__ cls_bf) {
+    unsigned short* __restrict__ cls_bf, float* __restrict__ pc, float* __restrict__ pq) {
   constexpr int NKA = (MTH + 1) / 2, NKB = (MTH + 1) / 2, KQ = (QT + 1) / 2;
   const float gs = gscale ? gscale[0] : 1.f;   // upstream scale of dz (loss.backward(g))
   constexpr int NSW = PAPER ? 0 : 2;
@@ -223,6 +229,9 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
   const int NQ = N * Q;
   const long hH = (long)h * H;
   const int npair = (h + 1) / 2;
+  // slice split: pairs [p0, p1) of workgroup row blockIdx.y; dC / dQ partials -> pc / pq (ntn_bwd_finish)
+  const int p0 = (int)((long)npair * blockIdx.y / gridDim.y), p1 = (int)((long)npair * (blockIdx.y + 1) / gridDim.y);
+  if (gridDim.y > 1 && blockIdx.y > 0) cls_bf = nullptr;   // one writer of the bf16 class vectors
   for (int g = blockIdx.x; g * NTN_WAVES < E; g += gridDim.x) {
     const int ep = g * NTN_WAVES + wave;
     const bool act = ep < E;
@@ -376,12 +385,12 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
       dwb[r] = dw_slab + ((!PAPER && c < N && n < N) ? ((long)epc * h * N + c) * N + n : (long)E * h * N * N);
     }
     __syncthreads();
-    ntn_stage<MTH, NSW, true>(ntn_lds, 0, mpack, m2pack, wtpack, 2);
+    ntn_stage<MTH, NSW, true>(ntn_lds, p0, mpack, m2pack, wtpack, 2);
     stage_wait();
     __syncthreads();
-    for (int p = 0; p < npair; ++p) {
-      const u16x8_t* buf = ntn_lds + (p & 1) * FR * 64;
-      if (p + 1 < npair) ntn_stage<MTH, NSW, true>(ntn_lds + ((p + 1) & 1) * FR * 64, p + 1, mpack, m2pack, wtpack, 2);
+    for (int p = p0; p < p1; ++p) {
+      const u16x8_t* buf = ntn_lds + ((p - p0) & 1) * FR * 64;
+      if (p + 1 < p1) ntn_stage<MTH, NSW, true>(ntn_lds + ((p + 1 - p0) & 1) * FR * 64, p + 1, mpack, m2pack, wtpack, 2);
       if (act) {
         f32x4_t Ps[2][MTH], dTs[2][QT];
 #pragma unroll
@@ -495,24 +504,60 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
       __syncthreads();
     }
     if (act) {
+      const bool split = gridDim.y > 1;
+      float* dc_out = split ? pc + (long)blockIdx.y * E * N * H : dcls;
 #pragma unroll
       for (int ma = 0; ma < MTH; ++ma) {
         const int a0 = 16 * ma + 4 * q;
-        if (n < N && a0 < H) *reinterpret_cast<f32x4_t*>(dcls + ((long)ep * N + n) * H + a0) = dCT[ma];
+        if (n < N && a0 < H) *reinterpret_cast<f32x4_t*>(dc_out + ((long)ep * N + n) * H + a0) = dCT[ma];
       }
+      // query-row gradients: straight into de, or this split's compact [E][NQ][H] partial
+      float* dq_base = split ? pq + ((long)blockIdx.y * E + ep) * NQ * H : de + rq0 * H;
 #pragma unroll
       for (int nb = 0; nb < MTH; ++nb)
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
           const int b0 = 16 * nb + 4 * q, qi = 16 * qt + n;
-          if (qi < NQ && b0 < H) *reinterpret_cast<f32x4_t*>(de + (rq0 + qi) * H + b0) = dQT[nb][qt];
+          if (qi < NQ && b0 < H) *reinterpret_cast<f32x4_t*>(dq_base + (long)qi * H + b0) = dQT[nb][qt];
         }
+    }
+  }
+}
+
+// sums of the slice-split partials, in split order (deterministic)
+__global__ __launch_bounds__(256) void ntn_fwd_finish_kernel(const float* __restrict__ part, int ny, long n, int N,
+                                                             int paper, const float* __restrict__ bias,
+                                                             float* __restrict__ probs) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int y = 0; y < ny; ++y) s += part[(long)y * n + i];
+    probs[i] = sigmoidf_(s + bias[paper ? 0 : (int)(i % N)]);
+  }
+}
+__global__ __launch_bounds__(256) void ntn_bwd_finish_kernel(const float* __restrict__ pc, const float* __restrict__ pq,
+                                                             int ny, int E, int N, int K, int Q, int H,
+                                                             float* __restrict__ dcls, float* __restrict__ de) {
+  const long n1 = (long)E * N * H, nqh = (long)N * Q * H, n2 = (long)E * nqh;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n1 + n2; i += (long)gridDim.x * 256) {
+    float s = 0.f;
+    if (i < n1) {
+      for (int y = 0; y < ny; ++y) s += pc[(long)y * n1 + i];
+      dcls[i] = s;
+    } else {
+      const long j = i - n1, ep = j / nqh, r = j - ep * nqh;
+      for (int y = 0; y < ny; ++y) s += pq[(long)y * n2 + j];
+      de[(ep * (long)(N * K + N * Q) + N * K) * H + r] = s;
     }
   }
 }
 
 // ------------------------------------------------------------------------------------------
 namespace ina {
+
+static int finish_grid(long n) {
+  const long g = (n + 255) / 256;
+  return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
+}
 
 static size_t ntn_lds_bytes(int MTH, bool paper, bool bwd) {
   const int NKA = (MTH + 1) / 2;
@@ -524,9 +569,15 @@ template <int MTH, int QT, bool P>
 static int ntn_fwd_t(const NtnArgs& a, hipStream_t st) {
   const int groups = (a.E + NTN_WAVES - 1) / NTN_WAVES;
   const int blocks = groups < a.blocks ? groups : a.blocks;
-  hipLaunchKernelGGL((ntn_fwd_kernel<MTH, QT, P>), dim3(blocks), dim3(NTN_THREADS), ntn_lds_bytes(MTH, P, false), st,
-                     a.cls, a.e, a.E, a.N, a.K, a.Q, a.H, a.h, (const u16x8_t*)a.mpack, (const u16x8_t*)a.wpack,
-                     a.wvec, a.bias, a.probs);
+  const int ny = a.split > 1 ? a.split : 1;
+  hipLaunchKernelGGL((ntn_fwd_kernel<MTH, QT, P>), dim3(blocks, ny), dim3(NTN_THREADS), ntn_lds_bytes(MTH, P, false),
+                     st, a.cls, a.e, a.E, a.N, a.K, a.Q, a.H, a.h, (const u16x8_t*)a.mpack, (const u16x8_t*)a.wpack,
+                     a.wvec, a.bias, a.probs, a.part);
+  if (ny > 1) {
+    const long n = (long)a.E * a.N * a.Q * a.N;
+    hipLaunchKernelGGL(ntn_fwd_finish_kernel, dim3(finish_grid(n)), dim3(256), 0, st, a.part, ny, n, a.N, a.paper,
+                       a.bias, a.probs);
+  }
   INA_CHECK_LAUNCH();
   return 0;
 }
@@ -534,10 +585,16 @@ template <int MTH, int QT, bool P>
 static int ntn_bwd_t(const NtnArgs& a, hipStream_t st) {
   const int groups = (a.E + NTN_WAVES - 1) / NTN_WAVES;
   const int blocks = groups < a.blocks ? groups : a.blocks;
-  hipLaunchKernelGGL((ntn_bwd_kernel<MTH, QT, P>), dim3(blocks), dim3(NTN_THREADS), ntn_lds_bytes(MTH, P, true), st,
-                     a.cls, a.e, a.E, a.N, a.K, a.Q, a.H, a.h, (const u16x8_t*)a.mpack, (const u16x8_t*)a.m2pack,
+  const int ny = a.split > 1 ? a.split : 1;
+  hipLaunchKernelGGL((ntn_bwd_kernel<MTH, QT, P>), dim3(blocks, ny), dim3(NTN_THREADS), ntn_lds_bytes(MTH, P, true),
+                     st, a.cls, a.e, a.E, a.N, a.K, a.Q, a.H, a.h, (const u16x8_t*)a.mpack, (const u16x8_t*)a.m2pack,
                      (const u16x8_t*)a.wtpack, a.wvec, a.dz, a.dcls, a.de, (unsigned short*)a.dp_out, a.dw_slab,
-                     a.gscale, (unsigned short*)a.cls_bf);
+                     a.gscale, (unsigned short*)a.cls_bf, a.part, a.part2);
+  if (ny > 1) {
+    const long n = (long)a.E * a.N * a.H * (1 + a.Q);
+    hipLaunchKernelGGL(ntn_bwd_finish_kernel, dim3(finish_grid(n)), dim3(256), 0, st, a.part, a.part2, ny, a.E, a.N,
+                       a.K, a.Q, a.H, a.dcls, a.de);
+  }
   INA_CHECK_LAUNCH();
   return 0;
 }
@@ -559,6 +616,15 @@ static int ntn_bwd_t(const NtnArgs& a, hipStream_t st) {
     if (MTH == 4) { INA_NTN_QT(FN, 4, false) }                            \
   }                                                                       \
   return -1;
+
+// slice-split factor for small episode batches: fill ~256 workgroups, >= 2 slice pairs per split
+int ntn_split(int E, int h) {
+  const int groups = (E + NTN_WAVES - 1) / NTN_WAVES, npair = (h + 1) / 2;
+  if (groups >= 64) return 1;
+  int ny = 256 / groups;
+  if (ny > npair / 2) ny = npair / 2;
+  return ny > 1 ? ny : 1;
+}
 
 int ntn_fwd(const NtnArgs& a, hipStream_t st) {
   const int MTH = (a.H + 15) / 16, qt_needed = (a.N * a.Q + 15) / 16;
