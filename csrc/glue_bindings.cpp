@@ -35,6 +35,25 @@ void gather_pack(const Tensor& src, const Tensor& idx, int64_t nb, Tensor out_bf
                                out_f32.data_ptr<float>(), stream()) == 0, op, ": launch failed");
 }
 
+// the same gather with a per-element affine map ma [2][ntot] (out = v * ma[0][i] + ma[1][i]); the
+// indices must lie inside src (checked here once per call against the plan's maximum)
+void gather_pack_affine(const Tensor& src, const Tensor& idx, int64_t nb, Tensor out_bf16, Tensor out_f32,
+                        const Tensor& ma, int64_t idx_max) {
+  const char* op = "ina.gather_pack_affine";
+  need(src, op, "src", at::kFloat);
+  need(idx, op, "idx", at::kInt);
+  need(out_bf16, op, "out_bf16", at::kBFloat16);
+  need(out_f32, op, "out_f32", at::kFloat);
+  need(ma, op, "ma", at::kFloat);
+  const int64_t ntot = idx.numel();
+  TORCH_CHECK(nb >= 0 && nb <= ntot && out_bf16.numel() == nb && out_f32.numel() == ntot - nb,
+              op, ": output sizes must split idx into [nb | rest]");
+  TORCH_CHECK(ma.numel() == 2 * ntot, op, ": ma must be [2, ntot]");
+  TORCH_CHECK(idx_max < src.numel() && src.numel() < (int64_t)1 << 31, op, ": index plan exceeds src");
+  TORCH_CHECK(ina::gather_pack(src.data_ptr<float>(), idx.data_ptr<int>(), (long)nb, (long)ntot, out_bf16.data_ptr(),
+                               out_f32.data_ptr<float>(), stream(), ma.data_ptr<float>()) == 0, op, ": launch failed");
+}
+
 // ragged record plan: inst int32 [S] (dataset rows), lengths int32 [NI] (valid lengths, <= L) ->
 // (inst_sorted, perm, tlen [ceil(S/16)], slen) = the stable argsort of lengths[inst] and its derivatives
 std::tuple<Tensor, Tensor, Tensor, Tensor> ragged_sort(const Tensor& inst, const Tensor& lengths, int64_t L) {
@@ -129,5 +148,6 @@ TORCH_LIBRARY_FRAGMENT(ina, m) {
   m.def("gather_pack", &gather_pack);
   m.def("head_loss", &head_loss);
   m.def("ragged_sort", &ragged_sort);
+  m.def("gather_pack_affine", &gather_pack_affine);
   m.def("slab_scatter_add", &slab_scatter_add);
 }

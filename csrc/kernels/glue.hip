@@ -23,12 +23,15 @@ using namespace ina;
 
 namespace {
 
+// ma (optional): [2][ntot] per-element affine map out = v * ma[i] + ma[ntot + i] (the wide path's
+// exp2 gate pre-scales and the TF forget bias, ops/wide_packs.py)
 __global__ __launch_bounds__(256) void gather_pack_kernel(const float* __restrict__ src, const int* __restrict__ idx,
                                                           long nb, long ntot, unsigned short* __restrict__ outb,
-                                                          float* __restrict__ outf) {
+                                                          float* __restrict__ outf, const float* __restrict__ ma) {
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < ntot; i += (long)gridDim.x * 256) {
     const int k = idx[i];
-    const float v = k >= 0 ? src[k] : 0.f;
+    float v = k >= 0 ? src[k] : 0.f;
+    if (ma != nullptr) v = v * ma[i] + ma[ntot + i];
     if (i < nb)
       outb[i] = f2bf(v);
     else
@@ -228,12 +231,13 @@ __global__ __launch_bounds__(256) void slab_finish_kernel(SlabJobs jobs, const f
 
 namespace ina {
 
-int gather_pack(const float* src, const int* idx, long nb, long ntot, void* outb, float* outf, hipStream_t st) {
+int gather_pack(const float* src, const int* idx, long nb, long ntot, void* outb, float* outf, hipStream_t st,
+                const float* ma) {
   if (ntot <= 0) return 0;
   long g = (ntot + 255) / 256;
   if (g > 2048) g = 2048;
   hipLaunchKernelGGL(gather_pack_kernel, dim3((unsigned)g), dim3(256), 0, st, src, idx, nb, ntot,
-                     (unsigned short*)outb, outf);
+                     (unsigned short*)outb, outf, ma);
   INA_CHECK_LAUNCH();
   return 0;
 }

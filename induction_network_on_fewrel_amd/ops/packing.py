@@ -334,7 +334,8 @@ def wide_x_cols(D: int) -> int:
     return (D + 1 + 31) // 32 * 32
 
 
-def pack_lstm_wide(Kf: torch.Tensor, bf: torch.Tensor, Kb: torch.Tensor, bb: torch.Tensor, U: int, D: int):
+def pack_lstm_wide(Kf: torch.Tensor, bf: torch.Tensor, Kb: torch.Tensor, bb: torch.Tensor, U: int, D: int,
+                   scaled: bool = True, cast: bool = True):
     """TF BasicLSTMCell kernels [D + U, 4U] + biases of both directions -> the persistent kernels'
     operands (G4 = 4 UP permuted gate columns 4u + g per direction; both directions side by side,
     column dir * G4 + c, so ONE GEMM covers them):
@@ -344,32 +345,38 @@ def pack_lstm_wide(Kf: torch.Tensor, bf: torch.Tensor, Kb: torch.Tensor, bb: tor
       wxt  [2, D, G4] bf16  per-direction view of wxtc
       bx   [2, G4]    fp32  bias (+1 on the forget gate), pre-scaled
       apk  [2, NW, M, KS, 64, 8] bf16   forward W_h fragments, pre-scaled
-      a2pk [2, NW, KS2, 64, 8]   bf16   backward W_h fragments (true weights)"""
+      a2pk [2, NW, KS2, 64, 8]   bf16   backward W_h fragments (true weights)
+    scaled=False skips the exp2 pre-scales and the forget bias, cast=False keeps fp32: the pure element
+    permutation that ops/wide_packs.py turns into one gather index (+ a per-element affine map)."""
     fwd_i, bwd_i, perm, gsc, _, _ = _wide_idx(U)
     dev = Kf.device
     fwd_i, bwd_i, perm, gsc = (_on(t, dev) for t in (fwd_i, bwd_i, perm, gsc))
     DP = wide_x_cols(D)
     outs = {k: [] for k in ("wx", "bx", "wxt", "apk", "a2pk")}
+    bfl = (lambda t: t.to(torch.bfloat16)) if cast else (lambda t: t)
     for K, b in ((Kf, bf), (Kb, bb)):
         K = K.detach().float()
         b = b.detach().float()
         Wx = torch.nn.functional.pad(K[:D], (0, 1))                       # [D, 4U+1]
         wxt = Wx[:, perm]                                                 # [D, G4]
         outs["wxt"].append(wxt)
-        outs["wx"].append(torch.nn.functional.pad(wxt * gsc, (0, 0, 0, DP - D)))
+        outs["wx"].append(torch.nn.functional.pad(wxt * gsc if scaled else wxt, (0, 0, 0, DP - D)))
         bfull = torch.nn.functional.pad(b, (0, 1))
-        fb = torch.zeros_like(bfull)
-        fb[2 * U:3 * U] = 1.0                                             # TF forget_bias
-        outs["bx"].append(((bfull + fb)[perm] * gsc).contiguous())
+        if scaled:
+            fb = torch.zeros_like(bfull)
+            fb[2 * U:3 * U] = 1.0                                         # TF forget_bias
+            outs["bx"].append(((bfull + fb)[perm] * gsc).contiguous())
+        else:
+            outs["bx"].append(bfull[perm].contiguous())
         Wh = torch.nn.functional.pad(K[D:D + U], (0, 1, 0, 1)).reshape(-1)  # [U+1, 4U+1] flat
         a = Wh[fwd_i].view(-1, 8)
         # fwd fragment scale: the gate of row R = 4q' + g is g = (l & 15) & 3
         gl = (torch.arange(a.shape[0], device=dev) // 1) % 64 % 16 % 4
-        outs["apk"].append((a * gate_scales(dev)[gl][:, None]).to(torch.bfloat16))
-        outs["a2pk"].append(Wh[bwd_i].to(torch.bfloat16))
-    wxtc = torch.cat(outs["wxt"], 1).to(torch.bfloat16)
+        outs["apk"].append(bfl(a * gate_scales(dev)[gl][:, None] if scaled else a))
+        outs["a2pk"].append(bfl(Wh[bwd_i]))
+    wxtc = bfl(torch.cat(outs["wxt"], 1))
     G4 = wxtc.shape[1] // 2
-    return {"wxc": torch.cat(outs["wx"], 1).to(torch.bfloat16), "wxtc": wxtc,
+    return {"wxc": bfl(torch.cat(outs["wx"], 1)), "wxtc": wxtc,
             "wxt": wxtc.view(D, 2, G4).transpose(0, 1),
             "bx": torch.stack(outs["bx"]).contiguous(), "apk": torch.stack(outs["apk"]).contiguous(),
             "a2pk": torch.stack(outs["a2pk"]).contiguous()}
@@ -404,7 +411,7 @@ def _attn_wide_idx(H: int):
     return HP, torch.from_numpy((kk * HP + row).reshape(-1)), torch.from_numpy((row * HP + kk).reshape(-1))
 
 
-def pack_attn_wide(W1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor):
+def pack_attn_wide(W1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, cast: bool = True):
     """Self-attention weights (W1 [H, H], b1 [H], w2 [H, 1]) -> the fused attention kernels' operands:
     w1t / w1 bf16 A fragments (see _attn_wide_idx), b1 / w2 fp32 zero-padded to HP."""
     H = W1.shape[0]
@@ -417,5 +424,5 @@ def pack_attn_wide(W1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor):
     b1p[:H] = b1.detach().float().reshape(-1)
     w2p = torch.zeros(HP, device=dev, dtype=torch.float32)
     w2p[:H] = w2.detach().float().reshape(-1)
-    return {"w1t": flat[_on(it, dev)].to(torch.bfloat16), "w1": flat[_on(iw, dev)].to(torch.bfloat16),
-            "b1": b1p, "w2": w2p}
+    bfl = (lambda t: t.to(torch.bfloat16)) if cast else (lambda t: t)
+    return {"w1t": bfl(flat[_on(it, dev)]), "w1": bfl(flat[_on(iw, dev)]), "b1": b1p, "w2": w2p}

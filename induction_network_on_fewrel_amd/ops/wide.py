@@ -114,13 +114,14 @@ class WideSeqBiLSTM(torch.autograd.Function):
                         wide_pos_grad (FewRel's shifted-arange position ids) or a one-hot GEMM."""
 
     @staticmethod
-    def forward(ctx, inst, word, pos1, pos2, wemb, p1emb, p2emb, Kf, bf, Kb, bb, U, seed, keep_prob, pos_shift):
+    def forward(ctx, inst, word, pos1, pos2, wemb, p1emb, p2emb, Kf, bf, Kb, bb, U, seed, keep_prob, pos_shift,
+                packs=None):
         from .packing import pack_lstm_wide
         o = ops()
         S, L = inst.shape[0], word.shape[1]
         E, P = wemb.shape[1], p1emb.shape[1]
         D = E + 2 * P
-        pk = pack_lstm_wide(Kf, bf, Kb, bb, U, D)
+        pk = packs if packs is not None else pack_lstm_wide(Kf, bf, Kb, bb, U, D)
         Xb = o.wide_x_gather(inst, word, pos1, pos2, wemb.detach().float().contiguous(),
                              p1emb.detach().float().contiguous(), p2emb.detach().float().contiguous())
         # x W_x for both directions as ONE bf16-output GEMM (the kernel adds the fp32 biases): an fp32 output
@@ -166,7 +167,7 @@ class WideSeqBiLSTM(torch.autograd.Function):
         dw = None
         if need_w:
             dw = table_grad(word[inst.long()].reshape(-1).long(), dX[:, :E], V)
-        return (None, None, None, None, dw, dp1, dp2, dKs[0], dbs[0], dKs[1], dbs[1], None, None, None, None)
+        return (None, None, None, None, dw, dp1, dp2, dKs[0], dbs[0], dKs[1], dbs[1], None, None, None, None, None)
 
 
 def table_grad(idx: torch.Tensor, d: torch.Tensor, rows: int) -> torch.Tensor:
@@ -238,9 +239,9 @@ class WideAttn(torch.autograd.Function):
     gradient (the reference fetches them for inspection only, model/base.py:144)."""
 
     @staticmethod
-    def forward(ctx, Hb, inst, mask, W1, b1, w2):
+    def forward(ctx, Hb, inst, mask, W1, b1, w2, packs=None):
         from .packing import pack_attn_wide
-        pk = pack_attn_wide(W1, b1, w2)
+        pk = packs if packs is not None else pack_attn_wide(W1, b1, w2)
         e, alpha = ops().wide_attn_fwd(Hb, inst, mask, pk["w1t"], pk["b1"], pk["w2"])
         ctx.save_for_backward(Hb, inst, mask, alpha)
         ctx.pk = pk
@@ -256,7 +257,7 @@ class WideAttn(torch.autograd.Function):
                                            de.contiguous().float())
         dW1 = _wgrad(Hb.reshape(-1, H), dZ) if ctx.needs_input_grad[3] else None
         ps = part.sum(0)
-        return dH, None, None, dW1, ps[1, :H], ps[0, :H].unsqueeze(1)
+        return dH, None, None, dW1, ps[1, :H], ps[0, :H].unsqueeze(1), None
 
 
 def attention_wide(H, mask, W1, b1, w2):
@@ -281,12 +282,20 @@ def encode_wide(inst, data, p, U: int, keep_prob: float, seed: int):
     from ..models import reference as ref
     if ops().lstm_wide_seq_ok(U):   # hand-written kernels end to end (u in {64, 100, 128})
         wa, p1a, p2a, ma = data
+        attn_fused = bool(ops().wide_attn_ok(2 * U, wa.shape[1]))
+        packs = None
+        if attn_fused:   # every weight pack of the step from ONE gather launch (ops/wide_packs.py)
+            from .wide_packs import wide_packs
+            D = p["word_embedding"].shape[1] + 2 * p["pos1_embedding"].shape[1]
+            packs = wide_packs(p["lstm_fw_kernel"], p["lstm_fw_bias"], p["lstm_bw_kernel"], p["lstm_bw_bias"],
+                               p["attn_kernel"], p["attn_bias"], p["attn_w2"], U, D)
         H = WideSeqBiLSTM.apply(inst, wa, p1a, p2a, p["word_embedding"], p["pos1_embedding"], p["pos2_embedding"],
                                 p["lstm_fw_kernel"], p["lstm_fw_bias"], p["lstm_bw_kernel"], p["lstm_bw_bias"], U,
-                                int(seed), float(keep_prob), bool(getattr(data, "pos_shift", False)))
-        if ops().wide_attn_ok(H.shape[-1], H.shape[1]):
+                                int(seed), float(keep_prob), bool(getattr(data, "pos_shift", False)), packs)
+        if attn_fused:
             mi = ma if ma.dtype == torch.int32 else ma.int()
-            return WideAttn.apply(H, inst.int(), mi.contiguous(), p["attn_kernel"], p["attn_bias"], p["attn_w2"])
+            return WideAttn.apply(H, inst.int(), mi.contiguous(), p["attn_kernel"], p["attn_bias"], p["attn_w2"],
+                                  packs)
         e, alphas = attention_wide(H, ma[inst.long()] > 0, p["attn_kernel"], p["attn_bias"], p["attn_w2"])
         return e, alphas.squeeze(-1)
     word, pos1, pos2, mask = (t[inst.long()] for t in data)

@@ -111,3 +111,19 @@ def test_fused_attention_vs_fp32(H, L, S):
     assert _relerr(W1.grad, W1r.grad) < 3e-2
     assert _relerr(b1.grad, b1r.grad) < 2e-2
     assert _relerr(w2.grad, w2r.grad) < 2e-2
+
+
+@pytest.mark.parametrize("U,D", [(128, 310), (100, 60), (64, 30)])
+def test_wide_packs_single_gather_matches_pack_functions(U, D):
+    """ops/wide_packs.py: every wide-path weight pack from ONE ina.gather_pack_affine launch over the flat
+    parameter buffer == the pack functions (gate pre-scales and forget bias via the affine map)."""
+    from induction_network_on_fewrel_amd.ops.optim import FlatParams
+    from induction_network_on_fewrel_amd.ops.wide_packs import plan_check
+    g = torch.Generator().manual_seed(U)
+    H = 2 * U
+    shapes = dict(Kf=(D + U, 4 * U), bf=(4 * U,), Kb=(D + U, 4 * U), bb=(4 * U,), W1=(H, H), b1=(H,), w2=(H, 1))
+    params = {k: torch.nn.Parameter(torch.randn(s, generator=g).to(DEV)) for k, s in shapes.items()}
+    FlatParams(params)   # re-homes the parameters into one flat buffer (the trainer's layout)
+    ts = tuple(params[k] for k in shapes)
+    err = plan_check(ts, U, D)
+    assert err <= 1e-2 * max(float(t.abs().max()) for t in ts) * 2.0, err
