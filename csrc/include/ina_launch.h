@@ -210,8 +210,9 @@ struct WideSeqArgs {
   int stash;              // forward: write hprev / acts / cst (training)
 };
 bool lstm_wide_seq_supported(int U);
-int wide_x_gather(const int* inst, int S, int L, const int* word, const int* pos1, const int* pos2, const float* wemb,
-                  int E, const float* p1emb, const float* p2emb, int PD, int DP, void* xb, hipStream_t st);
+int wide_x_gather(const int* inst, int S, int L, const int* word, const int* pos1, const int* pos2, const void* wemb,
+                  bool wemb_bf16, int E, const float* p1emb, const float* p2emb, int PD, int DP, void* xb,
+                  hipStream_t st);
 int wide_pos_grad(const float* dxp, const int* inst, const int* pos1, const int* pos2, int S, int L, int PD, int P2,
                   int chunks, float* part, hipStream_t st);
 int lstm_wide_seq_fwd(const WideSeqArgs& a, hipStream_t st);

@@ -511,36 +511,68 @@ int lstm_wide_seq_bwd(const WideSeqArgs& a, hipStream_t st) {
 // (inst[s], t) -- one pass instead of a word gather (fp32), a cast, two position gathers and a concat.
 // One wave per token row (grid-stride), two columns (one 4-byte store) per lane and pass.
 // ------------------------------------------------------------------------------------------
+// WB: the word table is a cached bf16 copy (frozen tables, ops/wide.py::word_table_bf16): half the
+// bytes of the random row reads.  RW rows per wave, every row's index chain (inst -> word id) and word
+// vector loads issued before the first store: one row per wave left the kernel latency-bound on that
+// dependent chain (646 us at the paper configuration, ~2.5 TB/s).
+template <bool WB, int RW>
 __global__ __launch_bounds__(256) void wide_x_gather_kernel(const int* __restrict__ inst, int S, int L,
                                                             const int* __restrict__ word, const int* __restrict__ pos1,
-                                                            const int* __restrict__ pos2, const float* __restrict__ wemb,
+                                                            const int* __restrict__ pos2, const void* __restrict__ wemb_v,
                                                             int E, const float* __restrict__ p1emb,
                                                             const float* __restrict__ p2emb, int PD, int DP,
                                                             unsigned short* __restrict__ xb) {
-  // one wave per row: the word vector as float4 loads -> 4 bf16 (8-byte stores) when E % 4 == 0,
-  // then the 2 PD position columns, the ones column (index D) and zero padding up to DP
   const int lane = threadIdx.x & 63;
   const int D = E + 2 * PD;
   const long rows = (long)S * L;
+  const long r0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RW;
+  if (r0 >= rows) return;
   typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
-  for (long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (long)gridDim.x * 4) {
+  long tok[RW], wbase[RW];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    const long r = r0 + i < rows ? r0 + i : rows - 1;
     const int s = (int)(r / L), t = (int)(r - (long)s * L);
-    const long tok = (long)inst[s] * L + t;
-    const float* wr = wemb + (long)word[tok] * E;
-    unsigned short* dst = xb + r * DP;
-    int c0 = 0;
-    if ((E & 3) == 0) {
-      for (int c = 4 * lane; c < E; c += 256) {
-        const float4 v = *reinterpret_cast<const float4*>(wr + c);
-        const bf2_t lo = {(__bf16)v.x, (__bf16)v.y}, hi = {(__bf16)v.z, (__bf16)v.w};
-        *reinterpret_cast<uint2*>(dst + c) = uint2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
+    tok[i] = (long)inst[s] * L + t;
+  }
+#pragma unroll
+  for (int i = 0; i < RW; ++i) wbase[i] = (long)word[tok[i]] * E;
+  int c0 = 0;
+  if ((E & 3) == 0) {   // word columns, 4 per lane and pass: all RW rows' loads in flight together
+    for (int c = 4 * lane; c < E; c += 256) {
+      uint2 v[RW];
+#pragma unroll
+      for (int i = 0; i < RW; ++i) {
+        if constexpr (WB) {
+          v[i] = *reinterpret_cast<const uint2*>(static_cast<const unsigned short*>(wemb_v) + wbase[i] + c);
+        } else {
+          const float4 f = *reinterpret_cast<const float4*>(static_cast<const float*>(wemb_v) + wbase[i] + c);
+          const bf2_t lo = {(__bf16)f.x, (__bf16)f.y}, hi = {(__bf16)f.z, (__bf16)f.w};
+          v[i] = uint2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
+        }
       }
-      c0 = E;
+#pragma unroll
+      for (int i = 0; i < RW; ++i)
+        if (r0 + i < rows) *reinterpret_cast<uint2*>(xb + (r0 + i) * DP + c) = v[i];
     }
-    const float* q1 = p1emb + (long)pos1[tok] * PD;
-    const float* q2 = p2emb + (long)pos2[tok] * PD;
+    c0 = E;
+  }
+  // position columns, the ones column (index D) and zero padding up to DP (and the word columns when E % 4)
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    if (r0 + i >= rows) break;
+    const float* q1 = p1emb + (long)pos1[tok[i]] * PD;
+    const float* q2 = p2emb + (long)pos2[tok[i]] * PD;
+    unsigned short* dst = xb + (r0 + i) * DP;
     for (int c = c0 + lane; c < DP; c += 64) {
-      const float v = c < E ? wr[c] : c < E + PD ? q1[c - E] : c < D ? q2[c - E - PD] : c == D ? 1.f : 0.f;
+      float wv = 0.f;
+      if (c < E) {
+        if constexpr (WB)
+          wv = bf2f(static_cast<const unsigned short*>(wemb_v)[wbase[i] + c]);
+        else
+          wv = static_cast<const float*>(wemb_v)[wbase[i] + c];
+      }
+      const float v = c < E ? wv : c < E + PD ? q1[c - E] : c < D ? q2[c - E - PD] : c == D ? 1.f : 0.f;
       dst[c] = f2bf(v);
     }
   }
@@ -571,14 +603,20 @@ __global__ __launch_bounds__(256) void wide_pos_grad_kernel(const float* __restr
 
 namespace ina {
 
-int wide_x_gather(const int* inst, int S, int L, const int* word, const int* pos1, const int* pos2, const float* wemb,
-                  int E, const float* p1emb, const float* p2emb, int PD, int DP, void* xb, hipStream_t st) {
+int wide_x_gather(const int* inst, int S, int L, const int* word, const int* pos1, const int* pos2, const void* wemb,
+                  bool wemb_bf16, int E, const float* p1emb, const float* p2emb, int PD, int DP, void* xb,
+                  hipStream_t st) {
+  constexpr int RW = 8;   // rows per wave
   const long rows = (long)S * L;
-  long blocks = (rows + 3) / 4;   // one row per wave: the inst -> word id -> vector chain is latency-bound
-  if (blocks > (1L << 30)) blocks = 1L << 30;
+  const long blocks = (rows + 4 * RW - 1) / (4 * RW);
   if (blocks < 1) return 0;
-  hipLaunchKernelGGL(wide_x_gather_kernel, dim3((int)blocks), dim3(256), 0, st, inst, S, L, word, pos1, pos2, wemb, E,
-                     p1emb, p2emb, PD, DP, (unsigned short*)xb);
+  if (blocks >= (1L << 31)) return -1;
+  if (wemb_bf16)
+    hipLaunchKernelGGL((wide_x_gather_kernel<true, RW>), dim3((int)blocks), dim3(256), 0, st, inst, S, L, word, pos1,
+                       pos2, wemb, E, p1emb, p2emb, PD, DP, (unsigned short*)xb);
+  else
+    hipLaunchKernelGGL((wide_x_gather_kernel<false, RW>), dim3((int)blocks), dim3(256), 0, st, inst, S, L, word, pos1,
+                       pos2, wemb, E, p1emb, p2emb, PD, DP, (unsigned short*)xb);
   INA_CHECK_LAUNCH();
   return 0;
 }

@@ -187,16 +187,17 @@ Tensor wide_x_gather(const Tensor& inst, const Tensor& word, const Tensor& pos1,
   chk_ids(word, "word");
   chk_ids(pos1, "pos1");
   chk_ids(pos2, "pos2");
-  chk(wemb, "wemb", at::kFloat, wemb.numel());
+  const bool wb = wemb.scalar_type() == at::kBFloat16;   // cached bf16 copy of a frozen word table
+  chk(wemb, "wemb", wb ? at::kBFloat16 : at::kFloat, wemb.numel());
   chk(p1emb, "p1emb", at::kFloat, p1emb.numel());
   chk(p2emb, "p2emb", at::kFloat, p2emb.numel());
   const int64_t S = inst.size(0), L = word.size(1), E = wemb.size(1), PD = p1emb.size(1);
   TORCH_CHECK(pos1.sizes() == word.sizes() && pos2.sizes() == word.sizes() && p2emb.size(1) == PD,
               "ina.wide_x_gather: shapes");
   const int64_t DP = (E + 2 * PD + 1 + 31) / 32 * 32;   // + the ones column, K padded to 32 (packing.wide_x_cols)
-  auto xb = at::empty({S * L, DP}, wemb.options().dtype(at::kBFloat16));
+  auto xb = at::empty({S * L, DP}, p1emb.options().dtype(at::kBFloat16));
   TORCH_CHECK(ina::wide_x_gather(inst.data_ptr<int>(), (int)S, (int)L, word.data_ptr<int>(), pos1.data_ptr<int>(),
-                                 pos2.data_ptr<int>(), wemb.data_ptr<float>(), (int)E, p1emb.data_ptr<float>(),
+                                 pos2.data_ptr<int>(), wemb.data_ptr(), wb, (int)E, p1emb.data_ptr<float>(),
                                  p2emb.data_ptr<float>(), (int)PD, (int)DP, xb.data_ptr(),
                                  c10::hip::getCurrentHIPStream().stream()) == 0,
               "ina.wide_x_gather: launch failed");

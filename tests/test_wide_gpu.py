@@ -127,3 +127,26 @@ def test_wide_packs_single_gather_matches_pack_functions(U, D):
     ts = tuple(params[k] for k in shapes)
     err = plan_check(ts, U, D)
     assert err <= 1e-2 * max(float(t.abs().max()) for t in ts) * 2.0, err
+
+
+@pytest.mark.parametrize("E", [300, 50])
+@pytest.mark.parametrize("table_bf16", [False, True])
+def test_wide_x_gather_rows(E, table_bf16):
+    """ina.wide_x_gather (8 rows in flight per wave; fp32 or cached-bf16 word table) == the torch gather
+    of [word row ; pos1 row ; pos2 row ; 1 ; 0 pad] in bf16, incl. a partial last wave."""
+    from induction_network_on_fewrel_amd.ops import ops
+    g = torch.Generator().manual_seed(E)
+    NI, L, V, PD, S = 40, 37, 500, 5, 13
+    word = torch.randint(0, V, (NI, L), generator=g, dtype=torch.int32).to(DEV)
+    pos1 = torch.randint(0, 2 * L, (NI, L), generator=g, dtype=torch.int32).to(DEV)
+    pos2 = torch.randint(0, 2 * L, (NI, L), generator=g, dtype=torch.int32).to(DEV)
+    inst = torch.randint(0, NI, (S,), generator=g, dtype=torch.int32).to(DEV)
+    wemb = torch.randn(V, E, generator=g).to(DEV)
+    p1, p2 = torch.randn(2 * L, PD, generator=g).to(DEV), torch.randn(2 * L, PD, generator=g).to(DEV)
+    tab = wemb.to(torch.bfloat16) if table_bf16 else wemb
+    xb = ops().wide_x_gather(inst, word, pos1, pos2, tab, p1, p2)
+    il = inst.long()
+    ref = torch.cat([wemb[word[il].long()], p1[pos1[il].long()], p2[pos2[il].long()],
+                     torch.ones(S, L, 1, device=DEV)], -1).reshape(S * L, -1)
+    ref = torch.nn.functional.pad(ref, (0, xb.shape[1] - ref.shape[1])).to(torch.bfloat16)
+    assert torch.equal(xb, ref)
