@@ -386,10 +386,12 @@ def _wide_head_forward(e, Ws, M, w, b, E, N, K, Q, R, paper):
     return probs.view(E, NQ, N), (sup, eh, cls_bf, Mt, P, qb, T, wf)
 
 
-def _wide_head_backward(ctx, dz, g):
-    """Shared backward of HeadWideFn / HeadWideLossFn: dz = dL/dlogit [E*NQ, N] (g: upstream scale)."""
+def _wide_head_backward(ctx, saved, dz, g):
+    """Shared backward of HeadWideProbsFn / HeadWideLossFn: dz = dL/dlogit [E*NQ, N] (g: upstream scale);
+    saved = the forward's (sup, eh, cls_bf, Mt, P, qb, T, wf, Ws).  T is overwritten with ReLU(T) (the FC
+    weight-gradient operand): the backward runs once (no retain_graph double backward)."""
     o = ops()
-    sup, eh, cls_bf, Mt, P, qb, T, wf, Ws = ctx.saved_tensors
+    sup, eh, cls_bf, Mt, P, qb, T, wf, Ws = saved
     E, N, K, Q, R, paper = ctx.cfg
     H, h = sup.shape[1], T.shape[2] // N
     NK, NQ = N * K, N * Q
@@ -429,18 +431,19 @@ class HeadWideProbsFn(torch.autograd.Function):
     def forward(ctx, e, Ws, M, w, b, cfg):
         E, N, K, Q, R, paper = cfg
         probs, saved = _wide_head_forward(e, Ws, M, w, b, E, N, K, Q, R, paper)
-        ctx.save_for_backward(*saved, Ws.detach().float())
+        # the output is saved through save_for_backward (an attribute would form a ctx <-> output cycle)
+        ctx.save_for_backward(*saved, Ws.detach().float(), probs)
         ctx.cfg = cfg
         ctx.edtype = e.dtype
-        ctx.probs = probs
         return probs
 
     @staticmethod
     def backward(ctx, dprobs):
-        p = ctx.probs
+        saved = ctx.saved_tensors
+        p = saved[-1]
         dz = (dprobs * p * (1.0 - p)).float().contiguous().view(-1, ctx.cfg[1])
         g = torch.empty(0, device=dz.device)
-        de, dWs, dM, dw, db = _wide_head_backward(ctx, dz, g)
+        de, dWs, dM, dw, db = _wide_head_backward(ctx, saved[:-1], dz, g)
         return de.to(ctx.edtype), dWs, dM, dw, db, None
 
 
@@ -477,7 +480,7 @@ class HeadWideLossFn(torch.autograd.Function):
     def backward(ctx, gloss, _gacc, _gprobs):
         g = (gloss.reshape(1).float().contiguous() if gloss is not None
              else torch.zeros(1, device=ctx.dz.device))
-        de, dWs, dM, dw, db = _wide_head_backward(ctx, ctx.dz, g)
+        de, dWs, dM, dw, db = _wide_head_backward(ctx, ctx.saved_tensors, ctx.dz, g)
         return de.to(ctx.edtype), dWs, dM, dw, db, None, None, None, None
 
 
