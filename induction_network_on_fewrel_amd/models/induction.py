@@ -90,7 +90,7 @@ class InductionNetwork(nn.Module):
     def forward(self, inst: torch.Tensor, data: Tuple[torch.Tensor, ...], B: int, N: int, K: int, Q: int,
                 training: bool = True, dropout_seed: int = 0,
                 grad_views: Optional[Dict[str, torch.Tensor]] = None, overlap=None,
-                seed_dev: Optional[torch.Tensor] = None, embeddings_only: bool = False
+                seed_dev: Optional[torch.Tensor] = None, embeddings_only: bool = False, glue=None
                 ) -> Tuple[torch.Tensor, torch.Tensor]:
         """inst: int32 [B*(N*K+N*Q)] instance rows (episode layout, support first).
         data: (word, pos1, pos2, mask) [NI, L] int32 on the same device.
@@ -104,7 +104,7 @@ class InductionNetwork(nn.Module):
                              "(use relation_head='paper' for N-independent scoring)")
         if cfg.encoder == "bert":
             return self._forward_bert(inst, data, B, N, K, Q, training, dropout_seed, grad_views, p, overlap,
-                                      embeddings_only)
+                                      embeddings_only, glue)
         if inst.is_cuda:
             word, pos1, pos2, mask = data
             if self.use_fused_lstm(word.shape[1]):
@@ -129,13 +129,14 @@ class InductionNetwork(nn.Module):
         return probs, alphas.squeeze(-1)
 
     def _forward_bert(self, inst, data, B, N, K, Q, training, dropout_seed, grad_views, p, overlap=None,
-                      embeddings_only=False):
+                      embeddings_only=False, glue=None):
         """BERT encoder (data = (ids, mask, e1, e2) [NI, Lb] int32) + the same induction/relation head.
         Returns probs and the [CLS]-row attention-free placeholder alphas (None)."""
         cfg = self.cfg
         if inst.is_cuda:
             from ..ops.bert import bert_encode
-            e = bert_encode(self, inst, data, training, int(dropout_seed), grad_views, overlap)
+            e = bert_encode(self, inst, data, training, int(dropout_seed), grad_views, overlap,
+                            glue if training else None)
             if embeddings_only:
                 return e, None
             return self._head(e, p, B, N, K, Q, grad_views), None
@@ -164,12 +165,13 @@ class InductionNetwork(nn.Module):
         if not fused and self.use_wide_head_loss(inst, data, N, K, Q):
             from ..ops.wide import head_wide_loss
             e, _ = self.forward(inst, data, B, N, K, Q, training=True, dropout_seed=dropout_seed,
-                                grad_views=grad_views, overlap=overlap, seed_dev=seed_dev, embeddings_only=True)
+                                grad_views=grad_views, overlap=overlap, seed_dev=seed_dev, embeddings_only=True,
+                                glue=glue)
             return head_wide_loss(e, p, labels, B, N, K, Q, cfg.routing_iters, cfg.relation_head, cfg.loss_type,
                                   cfg.loss_reduction)
         if not fused:
             probs, _ = self.forward(inst, data, B, N, K, Q, training=True, dropout_seed=dropout_seed,
-                                    grad_views=grad_views, overlap=overlap, seed_dev=seed_dev)
+                                    grad_views=grad_views, overlap=overlap, seed_dev=seed_dev, glue=glue)
             loss = self.loss(probs, labels)
             with torch.no_grad():
                 acc = ref.accuracy(probs.detach(), labels.long())

@@ -25,6 +25,15 @@ from ._ext import ops
 from .encoder import _route_grad
 
 
+def _glue_maps(meta, names):
+    """The StepGlue and the flat-gradient maps of ``names`` when every one of them is routed to the flat
+    gradient buffer (trainer path), else (None, None): the caller reduces with torch and routes."""
+    glue, views = meta.get("glue"), meta.get("grad_views")
+    if glue is None or views is None or any(n is None or n not in views for n in names):
+        return None, None
+    return glue, [glue.map_grad(views[n]) for n in names]
+
+
 def _contiguous_region(ts: List[torch.Tensor]) -> Optional[torch.Tensor]:
     """A 1-D view spanning ts if they are back-to-back in one storage (flat buffer), else None."""
     base = ts[0]
@@ -155,6 +164,12 @@ class _Embed(torch.autograd.Function):
             dw = None
         else:
             dw = torch.zeros_like(wemb).index_add_(0, rows, dx) if wemb.requires_grad else None
+        glue, maps = _glue_maps(meta, [names["gamma"], names["beta"], names["pos"], names["type"]])
+        if glue is not None:   # all four as slab jobs of the step's one deterministic scatter-add
+            glue.add(slab, glue.map_cat(maps[:2]), slab.shape[0])
+            glue.add(dx.view(S, L * HD), maps[2][:L * HD], S)      # position rows 0 .. L-1
+            glue.add(dx, maps[3][:HD], S * L)                        # token type 0
+            return (None, None, dw, None, None, None, None, None, None, None)
         dpos_L = dx.view(S, L, HD).sum(0)
         dpos = torch.zeros_like(pemb)
         dpos[:L] = dpos_L
@@ -185,10 +200,14 @@ class _LnRes(torch.autograd.Function):
         seed, stream, p, meta, gname, bname, abname, res_sink = ctx.cfg
         dres, da, slab = ops().bert_ln_res_bwd(dy.contiguous(), a.contiguous(), res.contiguous(), gamma.detach(),
                                                stats, seed, stream, p, 0)
-        sl = slab.sum(0)
         if res_sink is not None:
             res_sink.put(dres)
             dres = None
+        glue, maps = _glue_maps(meta, [gname, bname, abname])
+        if glue is not None:   # [blocks][dgamma | dbeta | db] -> one slab job
+            glue.add(slab, glue.map_cat(maps), slab.shape[0])
+            return (da, dres, None, None, None, None, None, None, None, None, None, None, None)
+        sl = slab.sum(0)
         return (da, dres, _route_grad(meta, gname, sl[0]), _route_grad(meta, bname, sl[1]), None, None, None, None,
                 None, None, _route_grad(meta, abname, sl[2]), None, None)
 
@@ -206,6 +225,10 @@ class _BiasGelu(torch.autograd.Function):
         x, b = ctx.saved_tensors
         meta, bname = ctx.cfg
         dx, slab = ops().bert_bias_gelu_bwd(dy.contiguous(), x, b.detach(), 0)
+        glue, maps = _glue_maps(meta, [bname])
+        if glue is not None:
+            glue.add(slab, maps[0], slab.shape[0])
+            return dx, None, None, None
         return dx, _route_grad(meta, bname, slab.sum(0)), None, None
 
 
@@ -226,6 +249,15 @@ class _Mha(torch.autograd.Function):
         qkv, out, lse, inst, mask = ctx.saved_tensors
         L, nh, seed, stream, p, meta, bnames = ctx.cfg
         dqkv, bsum = ops().bert_mha_bwd(qkv, out, dout.contiguous(), lse, inst, mask, L, nh, seed, stream, p)
+        glue, maps = _glue_maps(meta, bnames)
+        if glue is not None:   # bsum [S][nh][3][64] -> q / k / v bias column (h, i, c) -> b_i[h * 64 + c]
+            key = ("mha_bias", nh) + tuple(m.data_ptr() for m in maps)
+            mp = glue._maps.get(key)
+            if mp is None:
+                mp = torch.stack([m.view(nh, 64) for m in maps], 1).reshape(-1).contiguous()
+                glue._maps[key] = mp
+            glue.add(bsum, mp, inst.shape[0])
+            return (dqkv, None, None, None, None, None, None, None, None, None, None, None, None)
         db = bsum.view(inst.shape[0], nh, 3, 64).sum(0).transpose(0, 1).reshape(3, nh * 64)
         return (dqkv, None, None, None, None, None, None, None, None, None) + tuple(
             _route_grad(meta, bnames[i], db[i]) for i in range(3))
@@ -243,10 +275,13 @@ def layer_spans(model, flat_names, offsets, numels):
 
 
 def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
-                grad_views: Optional[Dict[str, torch.Tensor]] = None, overlap=None) -> torch.Tensor:
+                grad_views: Optional[Dict[str, torch.Tensor]] = None, overlap=None, glue=None) -> torch.Tensor:
     """GPU BERT encoder + pooling + projection -> sentence vectors [S, bert_out_dim] fp32.
     ``overlap`` (parallel/dp.py::OverlapAllReduce over layer_spans) gets ``ready(i)`` when layer i's
-    gradients are final, so DP all-reduces run under the rest of backward."""
+    gradients are final, so DP all-reduces run under the rest of backward.  ``glue`` (ops/glue.py::StepGlue,
+    trainer path): the LayerNorm / bias / embedding slab reductions are queued as slab jobs and scattered
+    into the flat gradient by the glue's deterministic slab_scatter (one launch per 8 jobs) instead of a
+    torch reduction + add per parameter (~190 launches per step); the caller flushes after backward."""
     cfg = model.cfg
     ids, mask, e1, e2 = data
     prm = model.params
@@ -258,7 +293,7 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
     pd = cfg.bert_dropout if training else 0.0
     pa = cfg.bert_attn_dropout if training else 0.0
     seed = int(seed) & 0x7FFFFFFF
-    meta = {"grad_views": grad_views}
+    meta = {"grad_views": grad_views, "glue": glue if grad_views is not None else None}
     # ---- bf16 weight copy of all encoder layers: ONE cast of a contiguous flat-buffer region
     layer_names = [n for n in names.values() if n.startswith("bert.encoder.layer.")]
     lparams = [P(n) for n in layer_names]
@@ -290,7 +325,14 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
                              *[P(n) for n in wn], *[P(n) for n in (bn or [])])
 
     # DP overlap: the QKV projection's backward is the last backward op of layer i -> bucket i is final
-    layer_ready = (lambda i: (lambda: overlap.ready(i))) if overlap is not None else (lambda i: None)
+    # (queued slab jobs of the layers above are scattered first: the bucket must hold final gradients)
+    def _ready(i):
+        def f():
+            if meta["glue"] is not None:
+                meta["glue"].flush()
+            overlap.ready(i)
+        return f
+    layer_ready = _ready if overlap is not None else (lambda i: None)
 
     # ---- embeddings
     e = "bert.embeddings."

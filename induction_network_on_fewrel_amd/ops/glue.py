@@ -187,6 +187,28 @@ class StepGlue:
             self._maps[key] = m
         return m
 
+    def map_grad(self, gv: torch.Tensor) -> torch.Tensor:
+        """Identity map of a gradient view of the flat GRADIENT buffer (the trainer's grad_views)."""
+        base = self.flat.grad
+        d = gv.data_ptr() - base.data_ptr()
+        if gv.dtype != torch.float32 or not gv.is_contiguous() or d < 0 or d % 4:
+            raise ValueError("StepGlue.map_grad: not a contiguous view of the flat gradient buffer")
+        key = ("g", d // 4, gv.numel())
+        m = self._maps.get(key)
+        if m is None:
+            m = self._dev_i32(d // 4 + np.arange(gv.numel()))
+            self._maps[key] = m
+        return m
+
+    def map_cat(self, maps) -> torch.Tensor:
+        """Concatenation of maps (one slab job over several parameters' columns), cached."""
+        key = ("cat",) + tuple(m.data_ptr() for m in maps)
+        m = self._maps.get(key)
+        if m is None:
+            m = torch.cat(list(maps)).contiguous()
+            self._maps[key] = m
+        return m
+
     # ------------------------------------------------------------------ slab queue
     def add(self, slab: torch.Tensor, m: torch.Tensor, nblk: int, scale: Optional[torch.Tensor] = None) -> None:
         """Queue sum_b slab[b] (slab viewed as [nblk, m.numel()]) * scale for a scatter-add at map m."""

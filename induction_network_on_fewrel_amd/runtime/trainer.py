@@ -84,8 +84,8 @@ class Trainer:
         self.model = InductionNetwork(cfg, wv, vocab_size=vocab, seed=cfg.seed).to(self.device)
         self.flat = FlatParams(self.model.params.trainable())
         self.grad_views = {n: self.flat.view(self.flat.grad, n) for n in self.flat.names}
-        self.glue = None   # fused step plumbing (ops/glue.py): GPU BiLSTM path
-        if self.device.type == "cuda" and cfg.encoder == "bilstm" and cfg.step_glue:
+        self.glue = None   # fused step plumbing (ops/glue.py): GPU BiLSTM path, BERT gradient slabs
+        if self.device.type == "cuda" and cfg.step_glue:
             from ..ops.glue import StepGlue
             self.glue = StepGlue(self.flat)
         if self.dist.initialized:

@@ -174,3 +174,46 @@ def test_split_k_weight_grad_accumulated_into_flat_span():
         out = torch.empty(o, i, device=dev)
         ops().slab_reduce(part, out, False)
         torch.testing.assert_close(out, part.sum(0), rtol=1e-5, atol=1e-4)
+
+
+def test_bert_glue_slab_jobs_match_direct_routing():
+    """Trainer path: the LayerNorm / bias / embedding slab reductions queued on the StepGlue (one
+    deterministic slab_scatter per 8 jobs) give the same flat gradient as the per-parameter torch
+    reductions routed into the flat buffer."""
+    from induction_network_on_fewrel_amd.config import Config
+    from induction_network_on_fewrel_amd.models import InductionNetwork
+    from induction_network_on_fewrel_amd.ops.bert import bert_encode
+    from induction_network_on_fewrel_amd.ops.glue import StepGlue
+    from induction_network_on_fewrel_amd.ops.optim import FlatParams
+    cfg = Config(encoder="bert", bert_layers=2, bert_hidden=256, bert_heads=4, bert_intermediate=512, bert_vocab=400,
+                 bert_max_position=64, bert_max_length=40, bert_out_dim=64, bert_dropout=0.1, bert_attn_dropout=0.1)
+    torch.manual_seed(4)
+    m = InductionNetwork(cfg, None, vocab_size=10).to(dev)
+    flat = FlatParams(m.params.trainable())
+    views = {n: flat.view(flat.grad, n) for n in flat.names}
+    NI, L = 12, 40
+    ids = torch.randint(9, 400, (NI, L), device=dev, dtype=torch.int32)
+    mask = torch.ones(NI, L, device=dev, dtype=torch.int32)
+    for i in range(NI):
+        mask[i, 10 + 2 * i:] = 0
+        ids[i, 10 + 2 * i:] = 0
+    e1 = torch.randint(1, 8, (NI,), device=dev, dtype=torch.int32)
+    e2 = torch.randint(1, 8, (NI,), device=dev, dtype=torch.int32)
+    inst = torch.tensor([0, 3, 5, 7, 11, 2], device=dev, dtype=torch.int32)
+    w = None
+    grads = []
+    for glue in (None, StepGlue(flat)):
+        for p in m.params.parameters():
+            p.grad = None
+        flat.zero_grad()
+        out = bert_encode(m, inst, (ids, mask, e1, e2), True, 77, views, None, glue)
+        if w is None:
+            w = torch.randn_like(out)
+        (out * w).sum().backward()
+        if glue is not None:
+            assert glue.pending() > 0
+            glue.flush()
+        flat.sync_grads_into_flat()
+        grads.append(flat.grad[:flat.numel].clone())
+    a, b = grads
+    assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max()) + 1e-7
