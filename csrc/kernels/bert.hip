@@ -386,6 +386,10 @@ INA_DEVICE u16x8_t cat44(const u16x4_t& a, const u16x4_t& b) {
   return u16x8_t{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 INA_DEVICE u16x8_t zero8() { return u16x8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
+INA_DEVICE u16x8_t cat_tr(const s16x4_t& a, const s16x4_t& b) {
+  return u16x8_t{(unsigned short)a[0], (unsigned short)a[1], (unsigned short)a[2], (unsigned short)a[3],
+                 (unsigned short)b[0], (unsigned short)b[1], (unsigned short)b[2], (unsigned short)b[3]};
+}
 
 // qkv: [T, 3*HDm] bf16, HDm = nh*64; token row of (s, t) = s*L + t.  ctx: [T, HDm] bf16.
 // lse: [S, nh, LP] fp32 (log2-domain log-sum-exp of the scaled scores).  mask_all: [NI, L] int.
@@ -516,18 +520,21 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
                                                       unsigned short* __restrict__ dqkv, uint32_t salt, uint32_t thr,
                                                       float inv_kp, int drop, float* __restrict__ bsum) {
   constexpr int NT = LP / 16;
-  constexpr int TSTR = LP + 8;       // row stride of the [d][q] / [d][key] transposed images
-  constexpr int SSTR = LP + 8;       // row stride of dS [q][key]
-  // region A: Q^T and dO^T (phase 1), then K^T (phase 2)
-  __shared__ __attribute__((aligned(16))) unsigned short TA[2 * HDIM * TSTR];
-  __shared__ __attribute__((aligned(16))) unsigned short dSl[LP * SSTR];
+  // Every operand image is stored row-major as it arrives (16-byte / 8-byte LDS stores) and the
+  // transposed operands are read with the hardware transpose (tr_read).  Strides: 4 consecutive rows
+  // land in disjoint 8-dword bank windows for the tr_read pattern.
+  constexpr int DSTR = HDIM + 8;     // [q][d] / [key][d] images
+  constexpr int SSTR = LP + 16;      // dS^T [key][q]
+  // region A: Q and dO (phase 1), then K (phase 2)
+  __shared__ __attribute__((aligned(16))) unsigned short TA[2 * LP * DSTR];
+  __shared__ __attribute__((aligned(16))) unsigned short dSt[LP * SSTR];
   __shared__ float delta[LP];
   __shared__ float madd[LP];
   __shared__ float lsel[LP];
   __shared__ float wsum[4][3][HDIM];   // per-wave column sums (dQ | dK | dV), summed in fixed order
-  unsigned short* Qt = TA;
-  unsigned short* dOt = TA + HDIM * TSTR;
-  unsigned short* Kt = TA;
+  unsigned short* Qn = TA;
+  unsigned short* dOn = TA + LP * DSTR;
+  unsigned short* Kn = TA;
   const int s = blockIdx.x / nh, hh = blockIdx.x - s * nh;
   const int HDm = nh * HDIM, ROW = 3 * HDm;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -539,7 +546,7 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
   const unsigned short* ob = ctx + tok0 * HDm + hh * HDIM;
   const unsigned short* gb = dctx + tok0 * HDm + hh * HDIM;
   const float* lrow = lse + ((size_t)s * nh + hh) * LP;
-  // phase 0: Q^T, dO^T images; delta = rowsum(dO * O); key mask.  All loads of a thread are issued
+  // phase 0: Q, dO images; delta = rowsum(dO * O); key mask.  All loads of a thread are issued
   // before any is consumed (one memory latency per phase, not one per row).
   {
     constexpr int NU = LP * 8 / 256;
@@ -566,11 +573,8 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
       d += __shfl_xor(d, 4, 64);
       if ((i & 7) == 0) delta[q] = ok ? d : 0.f;
       if (!ok) qv[u] = dv[u] = zero8();
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        Qt[(c + j) * TSTR + q] = qv[u][j];
-        dOt[(c + j) * TSTR + q] = dv[u][j];
-      }
+      *reinterpret_cast<u16x8_t*>(&Qn[q * DSTR + c]) = qv[u];
+      *reinterpret_cast<u16x8_t*>(&dOn[q * DSTR + c]) = dv[u];
     }
   }
   const int* mrow = mask_all + (size_t)inst[s] * L;
@@ -607,38 +611,19 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
     f32x4_t dV[4], dK[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dV[dt] = dK[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    // A operands (Q and dO rows of the lane's query) of the next q-tile pair are loaded while the
-    // current pair is processed
-    u16x8_t qa8[2][2], ga8[2][2];
-    auto load_pair = [&](int qp, u16x8_t (&qd)[2][2], u16x8_t (&gd)[2][2]) {
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const int qa = 32 * qp + 16 * h2 + n;
-        const int qc = qa < L ? qa : 0;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          qd[h2][ks] = ld8(qb + (size_t)qc * ROW + 32 * ks + 8 * g);
-          gd[h2][ks] = ld8(gb + (size_t)qc * HDm + 32 * ks + 8 * g);
-        }
-      }
-    };
-    load_pair(0, qa8, ga8);
 #pragma unroll 1
     for (int qp = 0; qp < NT / 2; ++qp) {
-      u16x8_t qn8[2][2], gn8[2][2];
-      load_pair(qp + 1 < NT / 2 ? qp + 1 : qp, qn8, gn8);
       float pp[2][4], ds[2][4];
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         const int qt = 2 * qp + h2;
-        const bool qaok = 16 * qt + n < L;
+        // A operands: Q and dO rows of the lane's query from the LDS images (rows >= L are zero)
+        const int ra = (16 * qt + n) * DSTR + 8 * g;
         f32x4_t sacc = {0.f, 0.f, 0.f, 0.f}, pacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          const u16x8_t qv = qaok ? qa8[h2][ks] : zero8();
-          const u16x8_t gv = qaok ? ga8[h2][ks] : zero8();
-          sacc = mfma_bf16(qv, kf[ks], sacc);
-          pacc = mfma_bf16(gv, vf[ks], pacc);
+          sacc = mfma_bf16(ld8(Qn + ra + 32 * ks), kf[ks], sacc);
+          pacc = mfma_bf16(ld8(dOn + ra + 32 * ks), vf[ks], pacc);
         }
         const float4 lq = *reinterpret_cast<const float4*>(&lsel[16 * qt + 4 * g]);
         const float4 dq = *reinterpret_cast<const float4*>(&delta[16 * qt + 4 * g]);
@@ -660,24 +645,20 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
         pf[j] = f2bf(pp[j >> 2][j & 3]);
         sf[j] = f2bf(ds[j >> 2][j & 3]);
       }
-      // dS -> LDS for the dQ phase: dSl[q][key]
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dSl[(32 * qp + 16 * (j >> 2) + 4 * g + (j & 3)) * SSTR + key] = sf[j];
-      // dV^T += dO^T P' ; dK^T += Q^T dS   (A rows = d, k = query in kmap order)
+      // dS^T -> LDS for the dQ phase: row key, the lane's queries 32qp + {4g..4g+3, 16+4g..16+4g+3}
+      {
+        unsigned short* sr = &dSt[key * SSTR + 32 * qp + 4 * g];
+        *reinterpret_cast<u16x4_t*>(sr) = u16x4_t{sf[0], sf[1], sf[2], sf[3]};
+        *reinterpret_cast<u16x4_t*>(sr + 16) = u16x4_t{sf[4], sf[5], sf[6], sf[7]};
+      }
+      // dV^T += dO^T P' ; dK^T += Q^T dS   (A rows = d, k = query in kmap order: two transposed
+      // reads of query rows 32qp + 4g + j and 32qp + 16 + 4g + j)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const unsigned short* gr = &dOt[(16 * dt + n) * TSTR + 32 * qp];
-        const unsigned short* qr = &Qt[(16 * dt + n) * TSTR + 32 * qp];
-        dV[dt] = mfma_bf16(cat44(ld4h(gr + 4 * g), ld4h(gr + 16 + 4 * g)), pf, dV[dt]);
-        dK[dt] = mfma_bf16(cat44(ld4h(qr + 4 * g), ld4h(qr + 16 + 4 * g)), sf, dK[dt]);
+        const int ro = (32 * qp + 4 * g + (n >> 2)) * DSTR + 16 * dt + 4 * (n & 3);
+        dV[dt] = mfma_bf16(cat_tr(tr_read(dOn + ro), tr_read(dOn + ro + 16 * DSTR)), pf, dV[dt]);
+        dK[dt] = mfma_bf16(cat_tr(tr_read(Qn + ro), tr_read(Qn + ro + 16 * DSTR)), sf, dK[dt]);
       }
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          qa8[h2][ks] = qn8[h2][ks];
-          ga8[h2][ks] = gn8[h2][ks];
-        }
     }
     // outputs: dK^T / dV^T tiles -> rows of dqkv (lane: key = 16kt + n, d = 16dt + 4g + r)
     unsigned short* dk = dqkv + (tok0 + key) * ROW + HDm + hh * HDIM;
@@ -697,7 +678,7 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
     }
   }
   __syncthreads();
-  // phase 2: K^T image into region A, then dQ^T = K^T dS^T per query tile
+  // phase 2: K image into region A, then dQ^T = K^T dS^T per query tile
   {
     constexpr int NU = LP * 8 / 256;
     u16x8_t kv[NU];
@@ -712,8 +693,7 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
       const int i = threadIdx.x + 256 * u;
       const int k = i >> 3, c = (i & 7) * 8;
       if (k >= L) kv[u] = zero8();
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Kt[(c + j) * TSTR + k] = kv[u][j];
+      *reinterpret_cast<u16x8_t*>(&Kn[k * DSTR + c]) = kv[u];
     }
   }
   __syncthreads();
@@ -724,9 +704,15 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
     for (int dt = 0; dt < 4; ++dt) acc[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k2 = 0; k2 < NT / 2; ++k2) {
-      const u16x8_t bs = ld8(&dSl[q * SSTR + 32 * k2 + 8 * g]);
+      // standard k order: keys 32k2 + 8g + j, j < 8 (two transposed reads of 4 key rows each)
+      const int rk = 32 * k2 + 8 * g + (n >> 2);
+      const unsigned short* sb = &dSt[rk * SSTR + 16 * qt + 4 * (n & 3)];
+      const u16x8_t bs = cat_tr(tr_read(sb), tr_read(sb + 4 * SSTR));
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma_bf16(ld8(&Kt[(16 * dt + n) * TSTR + 32 * k2 + 8 * g]), bs, acc[dt]);
+      for (int dt = 0; dt < 4; ++dt) {
+        const unsigned short* kr = &Kn[rk * DSTR + 16 * dt + 4 * (n & 3)];
+        acc[dt] = mfma_bf16(cat_tr(tr_read(kr), tr_read(kr + 4 * DSTR)), bs, acc[dt]);
+      }
     }
     unsigned short* dq = dqkv + (tok0 + q) * ROW + hh * HDIM;
 #pragma unroll
