@@ -381,10 +381,6 @@ constexpr int HDIM = 64;
 constexpr int KSTR = HDIM + 8;  // LDS row stride (bf16) of row-major [key][d] images
 
 INA_DEVICE u16x8_t ld8(const unsigned short* p) { return *reinterpret_cast<const u16x8_t*>(p); }
-INA_DEVICE u16x4_t ld4h(const unsigned short* p) { return *reinterpret_cast<const u16x4_t*>(p); }
-INA_DEVICE u16x8_t cat44(const u16x4_t& a, const u16x4_t& b) {
-  return u16x8_t{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-}
 INA_DEVICE u16x8_t zero8() { return u16x8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
 INA_DEVICE u16x8_t cat_tr(const s16x4_t& a, const s16x4_t& b) {
   return u16x8_t{(unsigned short)a[0], (unsigned short)a[1], (unsigned short)a[2], (unsigned short)a[3],
@@ -400,9 +396,8 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const unsigned short* __re
                                                       float* __restrict__ lse, uint32_t salt, uint32_t thr,
                                                       float inv_kp, int drop) {
   constexpr int NT = LP / 16;        // key / query tiles
-  constexpr int VSTR = LP + 8;       // V^T row stride
   __shared__ __attribute__((aligned(16))) unsigned short Ks[LP * KSTR];
-  __shared__ __attribute__((aligned(16))) unsigned short Vt[HDIM * VSTR];
+  __shared__ __attribute__((aligned(16))) unsigned short Vs[LP * KSTR];   // V^T operands via tr_read
   __shared__ float madd[LP];
   const int s = blockIdx.x / nh, hh = blockIdx.x - s * nh;
   const int HDm = nh * HDIM, ROW = 3 * HDm;
@@ -411,7 +406,7 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const unsigned short* __re
   const size_t tok0 = (size_t)s * L;
   const unsigned short* kbase = qkv + tok0 * ROW + HDm + hh * HDIM;
   const unsigned short* vbase = qkv + tok0 * ROW + 2 * HDm + hh * HDIM;
-  // stage K rows and V^T (rows >= L are zero), key mask
+  // stage K and V rows (rows >= L are zero), key mask
   {
     constexpr int NU = LP * 8 / 256;
     u16x8_t kv[NU], vv[NU];
@@ -429,8 +424,7 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const unsigned short* __re
       const int k = i >> 3, c = (i & 7) * 8;
       if (k >= L) kv[u] = vv[u] = zero8();
       *reinterpret_cast<u16x8_t*>(&Ks[k * KSTR + c]) = kv[u];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Vt[(c + j) * VSTR + k] = vv[u][j];
+      *reinterpret_cast<u16x8_t*>(&Vs[k * KSTR + c]) = vv[u];
     }
   }
   const int* mrow = mask_all + (size_t)inst[s] * L;
@@ -495,10 +489,12 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const unsigned short* __re
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-      const unsigned short* vr = &Vt[(16 * dt + n) * VSTR];
 #pragma unroll
-      for (int k2 = 0; k2 < NT / 2; ++k2)
-        acc = mfma_bf16(cat44(ld4h(vr + 32 * k2 + 4 * g), ld4h(vr + 32 * k2 + 16 + 4 * g)), pf[k2], acc);
+      for (int k2 = 0; k2 < NT / 2; ++k2) {
+        // A = V^T rows d = 16dt + n, k = keys in kmap order (32k2 + 4g + j, 32k2 + 16 + 4g + j)
+        const unsigned short* vr = &Vs[(32 * k2 + 4 * g + (n >> 2)) * KSTR + 16 * dt + 4 * (n & 3)];
+        acc = mfma_bf16(cat_tr(tr_read(vr), tr_read(vr + 16 * KSTR)), pf[k2], acc);
+      }
       if (qok) {
         float o[4] = {acc[0] * inv_l, acc[1] * inv_l, acc[2] * inv_l, acc[3] * inv_l};
         st4(orow + 16 * dt + 4 * g, o);
