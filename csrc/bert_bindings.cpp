@@ -200,7 +200,8 @@ std::tuple<Tensor, Tensor> bert_bias_gelu_bwd(const Tensor& dy, const Tensor& x,
               "ina.bert_bias_gelu_bwd: shapes");
   blocks = std::max<int64_t>(1, std::min<int64_t>(blocks > 0 ? blocks : 1024, T));
   auto dx = at::empty_like(x);
-  auto slab = at::zeros({blocks, I}, b.options());
+  // every launched block writes its whole slab row
+  auto slab = T == 0 ? at::zeros({blocks, I}, b.options()) : at::empty({blocks, I}, b.options());
   if (T == 0) return {dx, slab};
   launched(ina::bias_gelu_bwd(dy.data_ptr(), x.data_ptr(), b.data_ptr<float>(), dx.data_ptr(),
                               slab.data_ptr<float>(), (int)T, (int)I, (int)blocks, stream()),

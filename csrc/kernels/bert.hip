@@ -374,6 +374,68 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const unsigned short
   }
 }
 
+// Balanced variant for R * (I/8) == 256 * NPT (I = 3072: R = 2, NPT = 3; I = 768: R = 8, NPT = 3):
+// a block iteration covers R rows as R*I/8 chunks and thread t owns chunks t + 256m, so every thread
+// is busy and issues all 2*NPT 16-byte loads before consuming any.  A thread's chunks keep their
+// columns across iterations (the block strides R rows); the R row-slot partials of a column are
+// summed in fixed slot order through LDS.
+template <int NPT>
+__global__ __launch_bounds__(256) void bias_gelu_bwd_bal_kernel(const unsigned short* __restrict__ dy,
+                                                                const unsigned short* __restrict__ x,
+                                                                const float* __restrict__ b,
+                                                                unsigned short* __restrict__ dx,
+                                                                float* __restrict__ slab, int T, int I, int R) {
+  extern __shared__ float cs[];   // [R][I]
+  const int nch = I / 8;
+  int rin[NPT], col[NPT];
+  float acc[NPT][8], bb[NPT][8];
+#pragma unroll
+  for (int m = 0; m < NPT; ++m) {
+    const int c = threadIdx.x + 256 * m;
+    rin[m] = c / nch;
+    col[m] = (c - rin[m] * nch) * 8;
+    const float4 b0 = ld4f(b + col[m]), b1 = ld4f(b + col[m] + 4);
+    bb[m][0] = b0.x; bb[m][1] = b0.y; bb[m][2] = b0.z; bb[m][3] = b0.w;
+    bb[m][4] = b1.x; bb[m][5] = b1.y; bb[m][6] = b1.z; bb[m][7] = b1.w;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[m][j] = 0.f;
+  }
+  for (int row0 = blockIdx.x * R; row0 < T; row0 += gridDim.x * R) {
+    u16x8_t gv[NPT], xv[NPT];
+#pragma unroll
+    for (int m = 0; m < NPT; ++m) {
+      const int row = row0 + rin[m] < T ? row0 + rin[m] : T - 1;
+      const size_t e0 = (size_t)row * I + col[m];
+      gv[m] = *reinterpret_cast<const u16x8_t*>(dy + e0);
+      xv[m] = *reinterpret_cast<const u16x8_t*>(x + e0);
+    }
+#pragma unroll
+    for (int m = 0; m < NPT; ++m) {
+      if (row0 + rin[m] < T) {
+        u16x8_t o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = bf2f(gv[m][j]) * gelu_grad(bf2f(xv[m][j]) + bb[m][j]);
+          o[j] = f2bf(d);
+          acc[m][j] += d;
+        }
+        *reinterpret_cast<u16x8_t*>(dx + (size_t)(row0 + rin[m]) * I + col[m]) = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < NPT; ++m)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cs[rin[m] * I + col[m] + j] = acc[m][j];
+  __syncthreads();
+  float* o = slab + (size_t)blockIdx.x * I;
+  for (int i = threadIdx.x; i < I; i += 256) {
+    float v = cs[i];
+    for (int r = 1; r < R; ++r) v += cs[r * I + i];
+    o[i] = v;
+  }
+}
+
 // --------------------------------------------------------------------------------------------
 // fused multi-head attention, head dim 64, L <= 128
 // --------------------------------------------------------------------------------------------
@@ -802,7 +864,12 @@ int bias_gelu_fwd(const void* x, const float* b, void* y, long T, int I, hipStre
 int bias_gelu_bwd(const void* dy, const void* x, const float* b, void* dx, float* slab, int T, int I, int blocks,
                   hipStream_t st) {
   const int nch = I / 8;
-  if (nch <= 256) {
+  // balanced variant: R rows per block iteration with R * nch == 3 * 256 and an [R][I] fp32 LDS slab
+  if ((3 * 256) % nch == 0) {   // LDS R * I * 4 = 3 * 256 * 32 bytes
+    const int R = 3 * 256 / nch;
+    hipLaunchKernelGGL(bias_gelu_bwd_bal_kernel<3>, dim3(blocks), dim3(256), (size_t)R * I * sizeof(float), st,
+                       (const unsigned short*)dy, (const unsigned short*)x, b, (unsigned short*)dx, slab, T, I, R);
+  } else if (nch <= 256) {
     hipLaunchKernelGGL(bias_gelu_bwd_kernel<1>, dim3(blocks), dim3(256), 0, st, (const unsigned short*)dy,
                        (const unsigned short*)x, b, (unsigned short*)dx, slab, T, I);
   } else if (nch <= 512) {

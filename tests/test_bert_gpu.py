@@ -76,9 +76,12 @@ def test_embed_ln(p):
     _close(slab.sum(0)[0], gf.grad, rtol=1e-2)
 
 
-def test_bias_gelu():
+@pytest.mark.parametrize("I,blocks", [(3072, 64), (3072, 256), (768, 256), (1000, 64)])
+def test_bias_gelu(I, blocks):
+    # 3072 / 768: the balanced backward (2 / 8 rows per block iteration, ragged tail, blocks with no
+    # rows); 1000: the column-chunk backward
     torch.manual_seed(2)
-    T, I = 333, 3072
+    T = 333
     x = torch.randn(T, I, device=dev).bfloat16()
     b = torch.randn(I, device=dev) * 0.3
     y = _ops().bert_bias_gelu_fwd(x, b)
@@ -87,7 +90,7 @@ def test_bias_gelu():
     _close(y, ref, rtol=1e-2)
     dy = torch.randn(T, I, device=dev).bfloat16()
     ref.backward(dy.float())
-    dx, slab = _ops().bert_bias_gelu_bwd(dy, x, b, 64)
+    dx, slab = _ops().bert_bias_gelu_bwd(dy, x, b, blocks)
     _close(dx, xf.grad, rtol=1e-2)
     _close(slab.sum(0), bf.grad, rtol=1e-2)
 
