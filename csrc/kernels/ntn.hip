@@ -400,7 +400,10 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
           for (int m = 0; m < MTH; ++m) Ps[sl][m] = Z4;
 #pragma unroll
           for (int qt = 0; qt < QT; ++qt) dTs[sl][qt] = Z4;
-          if (s >= h) continue;
+          // a padding slice (odd h, s = h) runs on the zero-padded packs -- all its values are zero -- and
+          // stores into the trash tails: no branch between the pair's two slice chains, so the scheduler
+          // can interleave them
+          const bool sok = s < h;
           // P^T (rows b, cols c) and P (rows c, cols b) from the same fragments (operand swap)
           f32x4_t PT[2 * NKB];
 #pragma unroll
@@ -459,13 +462,14 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
           // per-episode dw contribution
           if (PAPER) {
             dwp = wave_sum(dwp);
-            if (lane == 0) dw_slab[(long)ep * h + s] = dwp;
+            if (lane == 0 && sok) dw_slab[(long)ep * h + s] = dwp;
           } else {
             f32x4_t dw = Z4;
 #pragma unroll
             for (int kq = 0; kq < KQ; ++kq) dw = mfma_bf16(pack2(VT[2 * kq], VT[2 * kq + 1]), dzB[kq], dw);
+            float* const dwt = dw_slab + (long)E * h * N * N;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dwb[r][s * N * N] = dw[r];
+            for (int r = 0; r < 4; ++r) *(sok ? dwb[r] + s * N * N : dwt) = dw[r];
           }
           // dP^T[b, c] = sum_q Q[q, b] dT[c, q]
           f32x4_t dPT[2 * NKB];
@@ -487,9 +491,10 @@ __global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
               dCT[ma] = mfma_bf16(buf[(F1 + (sl * MTH + ma) * NKB + kb) * 64 + lane], dPf, dCT[ma]);
           }
           // dP -> bf16 [E*N][h*H] for the dM reduction GEMM
+          unsigned short* const dpt = dp_out + (long)E * N * hH;
 #pragma unroll
           for (int mb = 0; mb < MTH; ++mb)
-            *reinterpret_cast<u16x4_t*>(dpb[mb] + s * H) =
+            *reinterpret_cast<u16x4_t*>(sok ? dpb[mb] + s * H : dpt) =
                 u16x4_t{f2bf(dPT[mb][0]), f2bf(dPT[mb][1]), f2bf(dPT[mb][2]), f2bf(dPT[mb][3])};
         }
         // dQ^T[b, q] += sum_{s in pair, c} P_s[c, b] dT_s[c, q]

@@ -18,8 +18,8 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _problem(B=3, N=5, K=2, Q=5, L=37, u=20, dtype="fp32", seed=0, E=5, head="reference"):
-    cfg = Config(N=N, K=K, Q=Q, max_length=L, hidden_size=u, dtype=dtype, relation_head=head)
+def _problem(B=3, N=5, K=2, Q=5, L=37, u=20, dtype="fp32", seed=0, E=5, head="reference", slices=100):
+    cfg = Config(N=N, K=K, Q=Q, max_length=L, hidden_size=u, dtype=dtype, relation_head=head, ntn_slices=slices)
     data = make_synthetic(num_relations=max(8, N + 2), instances_per_relation=40, max_length=L, vocab=1000,
                           word_dim=E, seed=seed)
     model = InductionNetwork(cfg, data.word_vec_mat, seed=seed).to(DEV)
@@ -403,12 +403,15 @@ def test_pos_grad_shift_matches_general(B):
 
 
 @pytest.mark.parametrize("head", ["reference", "paper"])
-@pytest.mark.parametrize("shape", [(5, 2, 5), (5, 1, 5), (10, 5, 2), (3, 3, 5)])
+@pytest.mark.parametrize("shape", [(5, 2, 5), (5, 1, 5), (10, 5, 2), (3, 3, 5), (5, 2, 5, 7), (4, 3, 3, 1), (5, 5, 5, 9, 600)])
 def test_head_forward_backward(head, shape):
+    # 4th entry: an odd NTN slice count (the last slice pair holds one zero-padded slice); 5th: episodes
+    # (600: enough workgroups that the NTN runs without the small-batch slice split)
     from induction_network_on_fewrel_amd.ops.head import head as head_fn
-    N, K, Q = shape
-    B = 4
-    cfg, data, model, dd, inst, labels = _problem(B=B, N=N, K=K, Q=Q, head=head)
+    N, K, Q = shape[:3]
+    B = shape[4] if len(shape) > 4 else 4
+    cfg, data, model, dd, inst, labels = _problem(B=B, N=N, K=K, Q=Q, head=head,
+                                                  slices=shape[3] if len(shape) > 3 else 100)
     H = 2 * cfg.hidden_size
     S = inst.shape[0]
     torch.manual_seed(0)
