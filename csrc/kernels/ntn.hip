@@ -64,7 +64,11 @@ constexpr f32x4_t Z4 = {0.f, 0.f, 0.f, 0.f};
 #ifndef INA_NTN_BWD_LD
 #define INA_NTN_BWD_LD 1   // branch-free vectorized prologue loads in ntn_bwd (153 vs 160 us despite 188 B of spills; 0 = the branchy per-element loads)
 #endif
-constexpr int NTN_WAVES = 8;
+#ifndef INA_NTN_WAVES
+#define INA_NTN_WAVES 8   // episodes (waves) per workgroup sharing one staged copy of the slice packs
+// (4: two workgroups per CU, barriers over 4 waves -- measured ntn_bwd 574 -> 1120 us, tools/gpu_ab_ntn.sh)
+#endif
+constexpr int NTN_WAVES = INA_NTN_WAVES;
 constexpr int NTN_THREADS = NTN_WAVES * 64;
 
 // Stage slice pair p straight into LDS with global_load_lds (16 B / lane, one 1-KiB fragment per wave
