@@ -66,7 +66,8 @@ constexpr f32x4_t Z4 = {0.f, 0.f, 0.f, 0.f};
 #endif
 #ifndef INA_NTN_WAVES
 #define INA_NTN_WAVES 8   // episodes (waves) per workgroup sharing one staged copy of the slice packs
-// (4: two workgroups per CU, barriers over 4 waves -- measured ntn_bwd 574 -> 1120 us, tools/gpu_ab_ntn.sh)
+// (4 episodes: ntn_bwd 574 -> 641 us with two workgroups per CU -- twice the pack staging -- and 1120 us
+// without the waves_per_eu(2) bound, which lets it take 331 registers at one wave per SIMD; tools/gpu_ab_ntn.sh)
 #endif
 constexpr int NTN_WAVES = INA_NTN_WAVES;
 constexpr int NTN_THREADS = NTN_WAVES * 64;
@@ -217,7 +218,7 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(4))
 // Outputs: dcls [E,N,H]; de query rows [S,H]; dp_out bf16 [E*N][h*H] (col s*H + b);
 //          dw_slab [E][h][N][N] (reference head) or [E][h] (paper head).
 template <int MTH, int QT, bool PAPER>
-__global__ __launch_bounds__(NTN_THREADS) void ntn_bwd_kernel(
+__global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(2))) void ntn_bwd_kernel(
     const float* __restrict__ cls, const float* __restrict__ e, int E, int N, int K, int Q, int H, int h,
     const u16x8_t* __restrict__ mpack, const u16x8_t* __restrict__ m2pack, const u16x8_t* __restrict__ wtpack,
     const float* __restrict__ wvec, const float* __restrict__ dz, float* __restrict__ dcls, float* __restrict__ de,
