@@ -171,7 +171,9 @@ INA_DEVICE void wave_lds_sync() {
 // x enters the gate MFMAs as bf16 in this mode, so the values are exactly the ones the per-step
 // gather produced.
 // ------------------------------------------------------------------------------------------
-constexpr int XG_T = 16;   // steps per workgroup (16 sequences x 16 steps = 256 threads)
+constexpr int XG_T = 16;   // steps per workgroup pass (16 sequences x 16 steps = 256 threads)
+constexpr int XG_C = 3;    // passes per workgroup (L = 37: one workgroup per tile): the token loads of all
+                           // passes are issued before any is consumed, the pos tables staged once
 // UT / ET / PT: compile-time U, word dim and position dim (0 = the runtime arguments): the reference
 // default (U 20, 5-d words, 5-d positions) gets a fully unrolled, branch-free feature select and keep-bit
 // hash loop
@@ -195,24 +197,40 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
   if constexpr (ET > 0) E = ET;
   if constexpr (PT > 0) PD = PT;
   const int PTN = 2 * L * PD;
-  for (int i = threadIdx.x; i < 2 * PTN; i += 256) ptab[i] = i < PTN ? p1emb[i] : p2emb[i - PTN];
-  __syncthreads();
   // thread = one token (sequence n = tid & 15, step t0 + tid / 16): its id / row loads are runs along
   // t (coalesced), and it writes its NX x 4 features as 4 lane-group chunks; for a fixed step the
   // 16 sequences' chunks of one lane group are one contiguous 16 x 8-byte segment.
   const int tile = blockIdx.x;
-  const int n = threadIdx.x & 15, t = blockIdx.y * XG_T + (threadIdx.x >> 4);
+  const int n = threadIdx.x & 15;
   const int seq = tile * 16 + n;
   const bool valid = seq < S;
-  const long r = (long)inst[valid ? seq : S - 1] * L + min(t, L - 1);   // clamped: unconditional loads
-  const int p1 = pos1[r], p2 = pos2[r];
+  const long rb = (long)inst[valid ? seq : S - 1] * L;
+  int p1c[XG_C], p2c[XG_C], widc[XG_C];
+  u16x8_t wrc[XG_C];
+#pragma unroll
+  for (int c = 0; c < XG_C; ++c) {   // clamped rows: unconditional loads
+    const int t = (blockIdx.y * XG_C + c) * XG_T + (threadIdx.x >> 4);
+    const long r = rb + min(t, L - 1);
+    p1c[c] = pos1[r];
+    p2c[c] = pos2[r];
+    // DIRECT: the token's word row as one 16-byte load of 8 bf16 (E <= 8, zero padded)
+    if constexpr (DIRECT) wrc[c] = *reinterpret_cast<const u16x8_t*>(wrows + r * 8);
+    else widc[c] = word[r];
+  }
+  // (the pos tables are staged while those loads are in flight)
+  for (int i = threadIdx.x; i < 2 * PTN; i += 256) ptab[i] = i < PTN ? p1emb[i] : p2emb[i - PTN];
+  __syncthreads();
+  const int DIN = E + 2 * PD;
+#pragma unroll
+  for (int c = 0; c < XG_C; ++c) {
+  const int t = (blockIdx.y * XG_C + c) * XG_T + (threadIdx.x >> 4);
+  if (t >= L) break;   // t grows with c
+  const int p1 = p1c[c], p2 = p2c[c];
   const float* p1row = ptab + p1 * PD;
   const float* p2row = ptab + PTN + p2 * PD;
-  const int DIN = E + 2 * PD;
-  // DIRECT: the token's word row as one 16-byte load of 8 bf16 (E <= 8, zero padded)
   u16x8_t wr = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-  if constexpr (DIRECT) wr = *reinterpret_cast<const u16x8_t*>(wrows + r * 8);
-  const float* wrow = wemb + (DIRECT ? 0 : (long)word[r] * E);
+  if constexpr (DIRECT) wr = wrc[c];
+  const float* wrow = wemb + (DIRECT ? 0 : (long)widc[c] * E);
   float x[4 * NX];
 #pragma unroll
   for (int f = 0; f < 4 * NX; ++f) {   // E, PD are kernel arguments: the source branches are uniform
@@ -220,7 +238,6 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
     if (f < E) wv = DIRECT ? bf2f(wr[f < 8 ? f : 0]) : wrow[f];
     x[f] = f < E ? wv : (f < E + PD ? p1row[f - E] : (f < DIN ? p2row[f - E - PD] : 0.f));
   }
-  if (t >= L) return;
   unsigned short* dst = xg + (size_t)(tile * L + t) * 64 * NX;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -256,6 +273,7 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
 #pragma unroll
       for (int q = 0; q < 4; ++q) mrow[16 * q] = (unsigned char)by[q];
     }
+  }
   }
 }
 
@@ -1753,7 +1771,7 @@ int x_gather(const LstmArgs& a, int U, int NX, hipStream_t st) {
   if (ntiles <= 0) return 0;
   auto* xg = (unsigned short*)a.xg;
   auto* posb = const_cast<unsigned short*>(a.posb);
-  const dim3 grid(ntiles, (a.L + XG_T - 1) / XG_T);
+  const dim3 grid(ntiles, (a.L + XG_T * XG_C - 1) / (XG_T * XG_C));
   if (2 * a.L * a.PD > 128 * 8) return -1;   // pos tables staged in LDS
   const auto* wr16 = (const unsigned short*)a.wrows;
 #define INA_XG_LAUNCH(NXV, DIR, ...)                                                                     \
