@@ -535,8 +535,13 @@ __global__ __launch_bounds__(256) void wide_x_gather_kernel(const int* __restric
     const int s = (int)(r / L), t = (int)(r - (long)s * L);
     tok[i] = (long)inst[s] * L + t;
   }
+  int p1v[RW], p2v[RW];   // position ids of all RW rows loaded with the word ids (no per-row chains below)
 #pragma unroll
-  for (int i = 0; i < RW; ++i) wbase[i] = (long)word[tok[i]] * E;
+  for (int i = 0; i < RW; ++i) {
+    wbase[i] = (long)word[tok[i]] * E;
+    p1v[i] = pos1[tok[i]];
+    p2v[i] = pos2[tok[i]];
+  }
   int c0 = 0;
   if ((E & 3) == 0) {   // word columns, 4 per lane and pass: all RW rows' loads in flight together
     for (int c = 4 * lane; c < E; c += 256) {
@@ -558,11 +563,32 @@ __global__ __launch_bounds__(256) void wide_x_gather_kernel(const int* __restric
     c0 = E;
   }
   // position columns, the ones column (index D) and zero padding up to DP (and the word columns when E % 4)
+  if (DP - c0 <= 64) {   // one column per lane: the RW rows' table loads all in flight, then the stores
+    const int c = c0 + lane;
+    const int cp = c - E < PD ? c - E : c - E - PD;   // column inside its position table (c in [E, D))
+    float vv[RW];
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+      float wv = 0.f;
+      if (c < E) {
+        if constexpr (WB)
+          wv = bf2f(static_cast<const unsigned short*>(wemb_v)[wbase[i] + c]);
+        else
+          wv = static_cast<const float*>(wemb_v)[wbase[i] + c];
+      }
+      const float pv = (c >= E && c < D) ? (c < E + PD ? p1emb : p2emb)[(long)(c < E + PD ? p1v[i] : p2v[i]) * PD + cp] : 0.f;
+      vv[i] = c < E ? wv : c < D ? pv : c == D ? 1.f : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < RW; ++i)
+      if (c < DP && r0 + i < rows) xb[(r0 + i) * DP + c] = f2bf(vv[i]);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < RW; ++i) {
     if (r0 + i >= rows) break;
-    const float* q1 = p1emb + (long)pos1[tok[i]] * PD;
-    const float* q2 = p2emb + (long)pos2[tok[i]] * PD;
+    const float* q1 = p1emb + (long)p1v[i] * PD;
+    const float* q2 = p2emb + (long)p2v[i] * PD;
     unsigned short* dst = xb + (r0 + i) * DP;
     for (int c = c0 + lane; c < DP; c += 64) {
       float wv = 0.f;
