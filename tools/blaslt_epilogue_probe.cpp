@@ -37,6 +37,8 @@ static int run(hipblasLtHandle_t h, const char* name, hipblasLtEpilogue_t epi, i
     CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux)));
     int64_t ld = m;
     CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &ld, sizeof(ld)));
+    int32_t at = HIP_R_16BF;   // bf16 pre-activation
+    CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_DATA_TYPE, &at, sizeof(at)));
   }
   hipblasLtMatrixLayout_t la, lb, ld;
   const int64_t ar = ta == HIPBLAS_OP_N ? m : k, ac = ta == HIPBLAS_OP_N ? k : m;
@@ -111,6 +113,12 @@ int main() {
       W1, X, Y, b1, HIP_R_32F, Z, ws, wsb, st);
   run(h, "fwd GELU_AUX_BIAS (bf16 bias)", HIPBLASLT_EPILOGUE_GELU_AUX_BIAS, I, T, H, HIPBLAS_OP_T, H, HIPBLAS_OP_N,
       H, W1, X, Y, b1, HIP_R_16BF, Z, ws, wsb, st);
+  run(h, "fwd GELU", HIPBLASLT_EPILOGUE_GELU, I, T, H, HIPBLAS_OP_T, H, HIPBLAS_OP_N, H, W1, X, Y, nullptr, HIP_R_32F,
+      nullptr, ws, wsb, st);
+  run(h, "fwd GELU_BIAS (f32 bias)", HIPBLASLT_EPILOGUE_GELU_BIAS, I, T, H, HIPBLAS_OP_T, H, HIPBLAS_OP_N, H, W1, X,
+      Y, b1, HIP_R_32F, nullptr, ws, wsb, st);
+  run(h, "fwd GELU_AUX", HIPBLASLT_EPILOGUE_GELU_AUX, I, T, H, HIPBLAS_OP_T, H, HIPBLAS_OP_N, H, W1, X, Y, nullptr,
+      HIP_R_32F, Z, ws, wsb, st);
   // bwd: dH[I x T] = W2^T-ish: W2 row-major [H, I] = col-major [I x H] (N op), dY2 row-major [T, H] = col-major [H x T]
   run(h, "bwd plain", HIPBLASLT_EPILOGUE_DEFAULT, I, T, H, HIPBLAS_OP_N, I, HIPBLAS_OP_N, H, W2, dY2, dZ, nullptr,
       HIP_R_32F, nullptr, ws, wsb, st);
