@@ -674,7 +674,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   // K = one step measured 25% slower, half the MFMA rate).
   constexpr int NSLP = (U4 + NX + 1) & ~1;               // XH slots per lane: U4 h, NX x (+1 pad)
   constexpr int FTA = BF16 ? (4 * NSLP + 1 + 15) / 16 : FTMAX;
-  constexpr int GCP = GT * 16 + 4, FCP = FTA * 16 + 4;   // +4 elements: row stride != 0 mod 32 banks
+  // +4 elements: row stride != 0 mod 32 banks.  (A bank-model stride for the dG image, 92 at GT 5, halves
+  // its modelled transposed-read conflicts but measured neutral: tools/gpu_ab_gcp.sh, 1420 vs 1413 us.)
+  constexpr int GCP = GT * 16 + 4, FCP = FTA * 16 + 4;
   static_assert(!BF16 || 32 * (GCP + FCP) <= XROWS * RS, "bf16 dW images exceed the staging region");
   unsigned short* dgI = reinterpret_cast<unsigned short*>(dgT);
   unsigned short* xhI = dgI + 32 * GCP;
