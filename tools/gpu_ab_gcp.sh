@@ -1,4 +1,5 @@
 # A/B on one box: lstm_bwd dG image stride (in-tree) vs GT*16+4 (variants/_ina_kernels_gcp0.so), kernel times
+# (historical: the stride knob INA_LSTM_GCP_PLAIN was removed after this neutral A/B)
 OUT=${1:-gpurun_out/ab_gcp}
 ROOT=$PWD
 mkdir -p $OUT
