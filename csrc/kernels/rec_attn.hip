@@ -298,7 +298,10 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
 // slab per workgroup: [dW1 (H2*H2, row i, col j) | db1 (H2) | dw2 (H2)], the attn_bwd layout.
 // ------------------------------------------------------------------------------------------
 template <int U>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? 3 : 2))) void rec_attn_bwd_kernel(
+#ifndef INA_RA_BWD_WAVES
+#define INA_RA_BWD_WAVES 3   // 2 (197 VGPRs, no spills) measured equal: 596-601 us either way (tools/gpu_ab_ra.sh)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? INA_RA_BWD_WAVES : 2))) void rec_attn_bwd_kernel(
     const unsigned short* __restrict__ rec, const unsigned char* __restrict__ dmask, int S, int L, float inv_kp,
     const u16x8_t* __restrict__ w1r, const u16x8_t* __restrict__ w1rt, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ de, const float* __restrict__ e_fwd,
