@@ -611,12 +611,13 @@ std::tuple<Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tensor& e, c
     TORCH_CHECK(wtpack.numel() == hp * 64 * 8, "ina.ntn_bwd: wtpack size");
   }
   auto dcls = at::empty({E, N, H}, e.options());
-  // dP / dw (reference head) carry a trash tail past the returned view: the kernel's lanes outside
-  // the valid N x N / H ranges store there unconditionally (no exec-mask branches in its slice loop)
+  // dP carries a trash tail past the returned view: the kernel's lanes outside the valid N / H ranges
+  // store there unconditionally (no exec-mask branches in its slice loop)
   auto dp = at::empty({E * N * h * H + h * H + 64}, e.options().dtype(at::kBFloat16))
                 .narrow(0, 0, E * N * h * H).view({E * N, h * H});
-  auto dw = paper ? at::empty({E, h}, e.options())
-                  : at::empty({E * h * N * N + h * N * N + 64}, e.options()).narrow(0, 0, E * h * N * N).view({E, h, N, N});
+  // reference head: one dw row per workgroup group (its episodes summed in the kernel)
+  const int64_t G = ina::ntn_groups((int)E);
+  auto dw = paper ? at::empty({E, h}, e.options()) : at::empty({G, h, N, N}, e.options());
   if (E == 0) return {dcls, dp, dw};
   ina::NtnArgs a{};
   a.cls = cls.data_ptr<float>();

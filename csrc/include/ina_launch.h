@@ -131,6 +131,7 @@ struct NtnArgs {
   float* part2;
 };
 int ntn_split(int E, int h);
+int ntn_groups(int E);   // workgroup groups of episodes (rows of the reference-head dw slab)
 int ntn_fwd(const NtnArgs& a, hipStream_t st);
 
 // step glue (glue.hip)

@@ -216,7 +216,8 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(4))
 
 // ------------------------------------------------------------------------------------------
 // Outputs: dcls [E,N,H]; de query rows [S,H]; dp_out bf16 [E*N][h*H] (col s*H + b);
-//          dw_slab [E][h][N][N] (reference head) or [E][h] (paper head).
+//          dw_slab [ntn_groups(E)][h][N][N] (reference head: the workgroup's 8 episodes summed in fixed wave
+//          order through LDS, one slab row per workgroup group) or [E][h] (paper head).
 template <int MTH, int QT, bool PAPER>
 __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(2))) void ntn_bwd_kernel(
     const float* __restrict__ cls, const float* __restrict__ e, int E, int N, int K, int Q, int H, int h,
@@ -383,17 +384,29 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(2))
       const int b0 = 16 * mb + 4 * q;
       dpb[mb] = dp_out + ((n < N && b0 < H) ? ((long)epc * N + n) * hH + b0 : (long)E * N * hH);
     }
-    float* dwb[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int c = 4 * q + r;
-      dwb[r] = dw_slab + ((!PAPER && c < N && n < N) ? ((long)epc * h * N + c) * N + n : (long)E * h * N * N);
-    }
+    // reference head dw: per (pair parity, wave, slice) an [N*N + 1] LDS slot (the last entry takes the
+    // lanes outside N x N); summed over the group's waves in fixed order one pair later (flush_dw)
+    const int NN1 = N * N + 1;
+    float* const dwl = reinterpret_cast<float*>(ntn_lds + 2 * FR * 64);
+    const int nw = E - g * NTN_WAVES < NTN_WAVES ? E - g * NTN_WAVES : NTN_WAVES;   // active waves of the group
+    auto flush_dw = [&](int pp) {
+      if (PAPER) return;
+      if ((int)threadIdx.x < 2 * N * N) {
+        const int sl = (int)threadIdx.x / (N * N), rem = (int)threadIdx.x - sl * N * N, sv = 2 * pp + sl;
+        if (sv < h) {
+          const float* src = dwl + ((pp & 1) * NTN_WAVES * 2 + sl) * NN1 + rem;
+          float acc = 0.f;
+          for (int w = 0; w < nw; ++w) acc += src[w * 2 * NN1];
+          dw_slab[((long)g * h + sv) * N * N + rem] = acc;
+        }
+      }
+    };
     __syncthreads();
     ntn_stage<MTH, NSW, true>(ntn_lds, p0, mpack, m2pack, wtpack, 2);
     stage_wait();
     __syncthreads();
     for (int p = p0; p < p1; ++p) {
+      if (p > p0) flush_dw(p - 1);   // the previous pair's dw slots are complete (barrier at its end)
       const u16x8_t* buf = ntn_lds + ((p - p0) & 1) * FR * 64;
       if (p + 1 < p1) ntn_stage<MTH, NSW, true>(ntn_lds + ((p + 1 - p0) & 1) * FR * 64, p + 1, mpack, m2pack, wtpack, 2);
       if (act) {
@@ -472,9 +485,9 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(2))
             f32x4_t dw = Z4;
 #pragma unroll
             for (int kq = 0; kq < KQ; ++kq) dw = mfma_bf16(pack2(VT[2 * kq], VT[2 * kq + 1]), dzB[kq], dw);
-            float* const dwt = dw_slab + (long)E * h * N * N;
+            float* const dst = dwl + (((p & 1) * NTN_WAVES + wave) * 2 + sl) * NN1;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) *(sok ? dwb[r] + s * N * N : dwt) = dw[r];
+            for (int r = 0; r < 4; ++r) dst[(4 * q + r < N && n < N) ? (4 * q + r) * N + n : N * N] = dw[r];
           }
           // dP^T[b, c] = sum_q Q[q, b] dT[c, q]
           f32x4_t dPT[2 * NKB];
@@ -513,6 +526,7 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(2))
       stage_wait();
       __syncthreads();
     }
+    if (p1 > p0) flush_dw(p1 - 1);   // read before the next group's first barrier pair
     if (act) {
       const bool split = gridDim.y > 1;
       float* dc_out = split ? pc + (long)blockIdx.y * E * N * H : dcls;
@@ -569,11 +583,15 @@ static int finish_grid(long n) {
   return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
 }
 
-static size_t ntn_lds_bytes(int MTH, bool paper, bool bwd) {
+static size_t ntn_lds_bytes(int MTH, bool paper, bool bwd, int N = 0) {
   const int NKA = (MTH + 1) / 2;
   const int fr = bwd ? (4 * MTH * NKA + (paper ? 0 : 2)) : (2 * MTH * NKA + (paper ? 0 : 1));
-  return (size_t)2 * fr * 64 * 16;
+  // + the reference-head backward's dw slots [2 parities][waves][2 slices][N*N + 1] fp32
+  const size_t dwl = (bwd && !paper) ? (size_t)2 * NTN_WAVES * 2 * (N * N + 1) * 4 : 0;
+  return (size_t)2 * fr * 64 * 16 + dwl;
 }
+
+int ntn_groups(int E) { return (E + NTN_WAVES - 1) / NTN_WAVES; }
 
 template <int MTH, int QT, bool P>
 static int ntn_fwd_t(const NtnArgs& a, hipStream_t st) {
@@ -596,7 +614,12 @@ static int ntn_bwd_t(const NtnArgs& a, hipStream_t st) {
   const int groups = (a.E + NTN_WAVES - 1) / NTN_WAVES;
   const int blocks = groups < a.blocks ? groups : a.blocks;
   const int ny = a.split > 1 ? a.split : 1;
-  hipLaunchKernelGGL((ntn_bwd_kernel<MTH, QT, P>), dim3(blocks, ny), dim3(NTN_THREADS), ntn_lds_bytes(MTH, P, true),
+  const size_t lds = ntn_lds_bytes(MTH, P, true, a.N);
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute((const void*)ntn_bwd_kernel<MTH, QT, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+          hipSuccess)
+    return -1;
+  hipLaunchKernelGGL((ntn_bwd_kernel<MTH, QT, P>), dim3(blocks, ny), dim3(NTN_THREADS), lds,
                      st, a.cls, a.e, a.E, a.N, a.K, a.Q, a.H, a.h, (const u16x8_t*)a.mpack, (const u16x8_t*)a.m2pack,
                      (const u16x8_t*)a.wtpack, a.wvec, a.dz, a.dcls, a.de, (unsigned short*)a.dp_out, a.dw_slab,
                      a.gscale, (unsigned short*)a.cls_bf, a.part, a.part2);

@@ -132,7 +132,7 @@ class HeadLossFn(torch.autograd.Function):
         dMf = torch.bmm(cls_bf.view(ns, -1, H).transpose(1, 2), dp.view(ns, -1, dp.shape[1]),
                         out_dtype=torch.float32)                          # [ns, H, h*H] (col s*H + b)
         slab = o.routing_bwd(e, Ws, dcls, de, E, N, K, Q, R, 0)
-        glue.add(dw_slab, glue.map_identity(p["ntn_w"]), E)
+        glue.add(dw_slab, glue.map_identity(p["ntn_w"]), dw_slab.shape[0])
         glue.add(out[2 + N:3 + N] if paper else out[2:2 + N], glue.map_identity(p["ntn_b"]), 1, scale=g)
         glue.add(slab, glue.map_identity(p["W_s"]), slab.shape[0])
         glue.add(dMf, glue.map_ntn_M(p["M"]), ns)
