@@ -49,45 +49,59 @@ __global__ __launch_bounds__(RS_ROWS) void ragged_hist_kernel(const int* __restr
   }
 }
 
-// exclusive scan of n ints in one 1024-thread workgroup (chunked per thread, then a block scan).  Chunks of
-// up to SC_REG elements are loaded into registers with unconditional (clamped) loads, all in flight at
-// once: the per-element dependent loop took ~16 us at 15 elements per thread (one latency each).
+// exclusive scan of n ints in one 1024-thread workgroup.  n <= 16 * 1024 (the default shapes): the counts
+// go through LDS with coalesced loads / stores (thread-contiguous chunks read straight from global memory
+// touched a different cache line per lane and instruction: ~13 us for 60 KB), each thread scans its
+// contiguous chunk of <= 16 from LDS, and the block scan is a wave-shuffle scan plus the 16 wave totals.
+// Larger n: the same with the chunks read from global memory.
 constexpr int SC_REG = 16;
 __global__ __launch_bounds__(1024) void ragged_scan_kernel(const int* __restrict__ counts, long n,
                                                            int* __restrict__ offsets) {
-  __shared__ int part[1024];
+  __shared__ int buf[SC_REG * 1024];
+  __shared__ int part[16];
   const long chunk = (n + 1023) / 1024;
   const long beg = threadIdx.x * chunk, end = beg + chunk < n ? beg + chunk : n;
+  const bool lds = chunk <= SC_REG;   // uniform
   int v[SC_REG];
-  const bool reg = chunk <= SC_REG;   // uniform
   int s = 0;
-  if (reg) {
+  if (lds) {
+    for (long i = threadIdx.x; i < n; i += 1024) buf[i] = counts[i];
+    __syncthreads();
 #pragma unroll
     for (int j = 0; j < SC_REG; ++j) {
-      const long i = beg + j;
-      const int ok = (j < chunk && i < n) ? 1 : 0;
-      v[j] = counts[i < n ? i : n - 1] * ok;
+      v[j] = (beg + j < end) ? buf[beg + j] : 0;
+      s += v[j];
     }
-#pragma unroll
-    for (int j = 0; j < SC_REG; ++j) s += v[j];
   } else {
     for (long i = beg; i < end; ++i) s += counts[i];
   }
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {   // Hillis-Steele inclusive scan
-    const int x = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
-    __syncthreads();
-    part[threadIdx.x] += x;
-    __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int inc = s;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int x = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += x;
   }
-  int run = threadIdx.x > 0 ? part[threadIdx.x - 1] : 0;
-  if (reg) {
+  if (lane == 63) part[wave] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int w = 0; w < 16; ++w) {
+      const int t = part[w];
+      part[w] = acc;
+      acc += t;
+    }
+  }
+  __syncthreads();
+  int run = part[wave] + inc - s;   // exclusive prefix of this thread's chunk
+  if (lds) {
 #pragma unroll
     for (int j = 0; j < SC_REG; ++j) {
-      if (beg + j < end) offsets[beg + j] = run;
+      if (beg + j < end) buf[beg + j] = run;
       run += v[j];
     }
+    __syncthreads();
+    for (long i = threadIdx.x; i < n; i += 1024) offsets[i] = buf[i];
   } else {
     for (long i = beg; i < end; ++i) {
       offsets[i] = run;

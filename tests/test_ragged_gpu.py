@@ -7,7 +7,7 @@ from induction_network_on_fewrel_amd.ops import ops
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("S,L", [(409600, 37), (1000, 37), (17, 64), (16 * 1025 + 3, 5), (1, 0)])
+@pytest.mark.parametrize("S,L", [(409600, 37), (1000, 37), (17, 64), (16 * 1025 + 3, 5), (1, 0), (1000000, 64)])
 def test_ragged_sort_matches_stable_argsort(S, L):
     g = torch.Generator().manual_seed(S + L)
     NI = 5000
