@@ -79,10 +79,14 @@ __global__ __launch_bounds__(256) void sample_episodes_kernel(const int* __restr
     exhausted |= round == MAX_ROUNDS;
     if (lane == i) my_cls = c;
   }
-  // ---- K + Q distinct instances of each class
+  // ---- K + Q distinct instances of each class (the N classes' scopes loaded at once: one latency)
+  int my_b = 0, my_e = 0;
+  if (lane < N) {
+    my_b = scopes[2 * my_cls];
+    my_e = scopes[2 * my_cls + 1];
+  }
   for (int i = 0; i < N; ++i) {
-    const int ci = __shfl(my_cls, i, 64);
-    const int b = scopes[2 * ci], span = scopes[2 * ci + 1] - b;
+    const int b = __shfl(my_b, i, 64), span = __shfl(my_e, i, 64) - b;
     Rng ri{stream_key(ekey, (uint32_t)(i * 64 + lane)), 0u};
     int x = 0;
     bool need = lane < KQ;
