@@ -286,14 +286,18 @@ std::tuple<Tensor, Tensor> rec_attn_bwd(const Tensor& hlane, const Tensor& dmask
   return {dH, slab};
 }
 
-std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
-                                            const Tensor& pos2, const Tensor& wemb, const Tensor& p1emb,
-                                            const Tensor& p2emb, const Tensor& apack, const Tensor& a2pack,
-                                            const Tensor& bias, const Tensor& hraw, const Tensor& cst, const Tensor& dH,
-                                            const Tensor& dmask, const Tensor& xg, int64_t U, int64_t NX, bool bf16,
-                                            bool word_grad, int64_t blocks, int64_t seed, double keep_prob,
-                                            bool pos_shift, const std::optional<Tensor>& tlen,
-                                            const std::optional<Tensor>& slen) {
+// the self-attention backward fused into lstm_bwd (bf16 record path): packs + the forward's tensors
+struct FaIn {
+  Tensor w1f, w1ft, b1, w2, de, e, alphas;
+  std::optional<Tensor> perm;
+};
+
+static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
+    const Tensor& inst, const Tensor& word, const Tensor& pos1, const Tensor& pos2, const Tensor& wemb,
+    const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack, const Tensor& a2pack, const Tensor& bias,
+    const Tensor& hraw, const Tensor& cst, const Tensor& dH, const Tensor& dmask, const Tensor& xg, int64_t U, int64_t NX,
+    bool bf16, bool word_grad, int64_t blocks, int64_t seed, double keep_prob, bool pos_shift,
+    const std::optional<Tensor>& tlen, const std::optional<Tensor>& slen, const FaIn* fa) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -303,7 +307,7 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   check(p2emb, "p2emb", at::kFloat);
   check(bias, "bias", at::kFloat);
   if (!bf16) check(cst, "cst", at::kFloat);   // bf16: the cell states are packed into hlane
-  check(dH, "dH", bf16 ? at::kBFloat16 : at::kFloat);
+  if (!fa) check(dH, "dH", bf16 ? at::kBFloat16 : at::kFloat);
   check(apack, "apack", bf16 ? at::kBFloat16 : at::kFloat);
   check(a2pack, "a2pack", bf16 ? at::kBFloat16 : at::kFloat);
   check(hraw, "hraw", bf16 ? at::kBFloat16 : at::kFloat);   // bf16: lstm_fwd's step records
@@ -313,10 +317,11 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   TORCH_CHECK(DIN <= 4 * NX, "ina.lstm_bwd: input dim too large");
   TORCH_CHECK(hraw.numel() == ((S + 15) / 16) * 2 * L * U4 * 64 * (bf16 ? 2 : 1), "ina.lstm_bwd: hlane shape");
   // dH: natural [S, L, 2U] (attn_bwd) or, bf16, the step-record lane layout [tiles, 2, L, U/4, 64] (rec_attn_bwd)
-  const bool dh_lane = dH.dim() == 5;
-  TORCH_CHECK(dh_lane ? (bf16 && dH.size(0) == (S + 15) / 16 && dH.size(1) == 2 && dH.size(2) == L &&
-                         dH.size(3) == U / 4 && dH.size(4) == 64)
-                      : (dH.dim() == 3 && dH.size(0) == S && dH.size(1) == L && dH.size(2) == 2 * U),
+  const bool dh_lane = fa ? true : dH.dim() == 5;
+  TORCH_CHECK(fa != nullptr ||
+                  (dh_lane ? (bf16 && dH.size(0) == (S + 15) / 16 && dH.size(1) == 2 && dH.size(2) == L &&
+                              dH.size(3) == U / 4 && dH.size(4) == 64)
+                           : (dH.dim() == 3 && dH.size(0) == S && dH.size(1) == L && dH.size(2) == 2 * U)),
               "ina.lstm_bwd: dH shape");
   TORCH_CHECK(bf16 || cst.numel() == ((S + 15) / 16) * 2 * L * U4 * 64, "ina.lstm_bwd: cst shape");
   const bool drop_ = keep_prob < 1.0;
@@ -351,10 +356,13 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
     TORCH_CHECK(xg.numel() == ntiles * L * (64 * NX + 16), "ina.lstm_bwd: xg (from lstm_fwd) shape");
   }
   Tensor dwemb = word_grad ? at::zeros_like(wemb) : at::empty({0}, opt);
+  const int64_t H2 = 2 * U;
+  Tensor aslab = fa ? at::empty({blocks, 2, U * H2 + H2}, opt) : at::empty({0}, opt);
   if (S == 0) {
     dw_slab.zero_();
     dpos_slab.zero_();
-    return {dw_slab, dpos_slab, dwemb};
+    aslab.zero_();
+    return {dw_slab, dpos_slab, dwemb, aslab};
   }
   ina::LstmArgs a{};
   a.inst = inst.data_ptr<int>();
@@ -373,7 +381,7 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   a.bias = bias.data_ptr<float>();
   a.hraw = hraw.data_ptr();
   a.cst = bf16 ? hraw.data_ptr() : cst.data_ptr();
-  a.dH = dH.data_ptr();
+  a.dH = fa ? nullptr : dH.data_ptr();
   a.dw_slab = dw_slab.data_ptr<float>();
   a.dpos_slab = dpos_slab.data_ptr<float>();
   a.dwemb = word_grad ? dwemb.data_ptr<float>() : nullptr;
@@ -391,6 +399,35 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   a.slen = ragged_arg(slen, S, "slen");
   TORCH_CHECK(!a.tlen || (bf16 && dh_lane), "ina.lstm_bwd: ragged tiles need the bf16 lane-layout dH path");
   TORCH_CHECK(!a.slen || a.tlen, "ina.lstm_bwd: slen needs tlen");
+  if (fa) {
+    TORCH_CHECK(bf16 && (U == 8 || U == 20 || U == 32) && L <= 64, "ina.lstm_attn_bwd: bf16 record path only");
+    check(fa->w1f, "w1f", at::kBFloat16);
+    check(fa->w1ft, "w1ft", at::kBFloat16);
+    check(fa->b1, "b1", at::kFloat);
+    check(fa->w2, "w2", at::kFloat);
+    check(fa->de, "de", at::kFloat);
+    check(fa->e, "e", at::kFloat);
+    check(fa->alphas, "alphas", at::kFloat);
+    const int64_t U4 = U / 4, NV = 2 * U4, MT = (H2 + 15) / 16, NKR = (NV + 7) / 8, NJ = 4 * MT, NKS2 = (NJ + 7) / 8,
+                  NTD = (U4 + 3) / 4;
+    TORCH_CHECK(fa->w1f.numel() == 2 * MT * NKR * 64 * 8 && fa->w1ft.numel() == 2 * NTD * NKS2 * 64 * 8,
+                "ina.lstm_attn_bwd: pack sizes");
+    TORCH_CHECK(fa->b1.numel() == H2 && fa->w2.numel() == H2, "ina.lstm_attn_bwd: b1 / w2 size");
+    TORCH_CHECK(fa->de.size(0) == S && fa->de.size(1) == H2 && fa->e.sizes() == fa->de.sizes() &&
+                    fa->alphas.size(0) == S && fa->alphas.size(1) == L,
+                "ina.lstm_attn_bwd: de / e / alphas shape");
+    TORCH_CHECK(hraw.numel() == ((S + 15) / 16) * 2 * L * 2 * U4 * 64, "ina.lstm_attn_bwd: step records shape");
+    TORCH_CHECK(S * L * 4 < (1LL << 32), "ina.lstm_attn_bwd: alphas too large for a buffer descriptor");
+    a.aw1f = fa->w1f.data_ptr();
+    a.aw1ft = fa->w1ft.data_ptr();
+    a.ab1 = fa->b1.data_ptr<float>();
+    a.aw2 = fa->w2.data_ptr<float>();
+    a.ade = fa->de.data_ptr<float>();
+    a.ae = fa->e.data_ptr<float>();
+    a.aalphas = fa->alphas.data_ptr<float>();
+    a.perm = ragged_arg(fa->perm, S, "perm");
+    a.aslab = aslab.data_ptr<float>();
+  }
   a.xg = bf16 ? xg.data_ptr() : nullptr;
   a.posb = bf16 ? reinterpret_cast<const unsigned short*>(xg.data_ptr<at::BFloat16>() + ntiles * L * 64 * NX)
                 : nullptr;
@@ -402,7 +439,36 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
   } else if (bf16) {
     check_launch(ina::pos_grad(a, (int)pblocks, dpos_slab.data_ptr<float>(), cur_stream()), "pos_grad");
   }
-  return {dw_slab, dpos_slab, dwemb};
+  return {dw_slab, dpos_slab, dwemb, aslab};
+}
+
+std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
+                                            const Tensor& pos2, const Tensor& wemb, const Tensor& p1emb,
+                                            const Tensor& p2emb, const Tensor& apack, const Tensor& a2pack,
+                                            const Tensor& bias, const Tensor& hraw, const Tensor& cst, const Tensor& dH,
+                                            const Tensor& dmask, const Tensor& xg, int64_t U, int64_t NX, bool bf16,
+                                            bool word_grad, int64_t blocks, int64_t seed, double keep_prob,
+                                            bool pos_shift, const std::optional<Tensor>& tlen,
+                                            const std::optional<Tensor>& slen) {
+  auto r = lstm_bwd_impl(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hraw, cst, dH, dmask, xg, U, NX,
+                         bf16, word_grad, blocks, seed, keep_prob, pos_shift, tlen, slen, nullptr);
+  return {std::get<0>(r), std::get<1>(r), std::get<2>(r)};
+}
+
+// bf16 encoder backward with the self-attention backward fused into the BPTT (no dH tensor, no
+// rec_attn_bwd pass over the step records) -> (dw_slab, dpos_slab, dwemb, aslab [blocks, 2, U*2U + 2U]:
+// direction d's own dW1 rows [d U, d U + U) | db1 (d = 0) or dw2 (d = 1))
+std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_attn_bwd(
+    const Tensor& inst, const Tensor& word, const Tensor& pos1, const Tensor& pos2, const Tensor& wemb,
+    const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack, const Tensor& a2pack, const Tensor& bias,
+    const Tensor& hraw, const Tensor& dmask, const Tensor& xg, const Tensor& w1f, const Tensor& w1ft, const Tensor& b1,
+    const Tensor& w2, const Tensor& de, const Tensor& e, const Tensor& alphas, int64_t U, int64_t NX, bool word_grad,
+    int64_t blocks, int64_t seed, double keep_prob, bool pos_shift, const std::optional<Tensor>& tlen,
+    const std::optional<Tensor>& slen, const std::optional<Tensor>& perm) {
+  FaIn fa{w1f, w1ft, b1, w2, de, e, alphas, perm};
+  Tensor none = at::empty({0}, wemb.options());
+  return lstm_bwd_impl(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hraw, none, none, dmask, xg, U,
+                       NX, true, word_grad, blocks, seed, keep_prob, pos_shift, tlen, slen, &fa);
 }
 
 // ------------------------------------------------------------------ attention
@@ -767,6 +833,7 @@ TORCH_LIBRARY(ina, m) {
   m.def("abi_version", &abi_version);
   m.def("lstm_fwd", &lstm_fwd);
   m.def("lstm_bwd", &lstm_bwd);
+  m.def("lstm_attn_bwd", &lstm_attn_bwd);
   m.def("lstm_attn_fwd", &lstm_attn_fwd);
   m.def("rec_attn_ok", &rec_attn_ok);
   m.def("rec_attn_bwd", &rec_attn_bwd);

@@ -8,7 +8,8 @@
 //   * enqueue: an event recorded on the caller's current stream orders the collective after the
 //     kernels that produced the buffer (the backward that wrote a gradient bucket);
 //   * wait:    an event recorded on the comm stream makes the caller's stream wait -- the host never
-//     blocks, so bucket all-reduces overlap the rest of backward (and work inside a captured graph);
+//     blocks, so bucket all-reduces overlap the rest of backward.  (Collectives are not captured into
+//     hipGraphs here: the graphed train step runs its all-reduce eagerly after the replay.)
 //   * the buffer is recorded on the comm stream for the caching allocator (no reuse before the
 //     collective has read it).
 // Linked against the librccl.so that torch itself loads (one RCCL in the process).

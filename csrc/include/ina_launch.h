@@ -46,8 +46,19 @@ struct LstmArgs {
   // lengths; lstm_skip_padding), starts at tlen - 1 and resets each row's state past its own length
   const int* tlen;
   const int* slen;
-  const int* perm;   // x_gather: record row s is original row perm[s] (dropout hash counter)
+  const int* perm;   // x_gather: record row s is original row perm[s] (dropout hash counter); fused bwd: e/de rows
   int wblank;        // bwd with a trained word table: the padding (BLANK) row id, summed in registers (-1: none)
+  // bwd with the self-attention backward fused in (bf16 record path, aslab != nullptr; dH unused):
+  // packs w1f [2][MT][NKR][64][8] / w1ft [2][NTD][NKS2][64][8] (ops/packing.py::_attn_fuse_idx), b1, w2,
+  // de / e [S][2U], alphas [S][L] (original row order) -> aslab [bwd_blocks][2][U*2U + 2U]
+  const void* aw1f;
+  const void* aw1ft;
+  const float* ab1;
+  const float* aw2;
+  const float* ade;
+  const float* ae;
+  const float* aalphas;
+  float* aslab;
 };
 // bf16 mode: gather every token's x features once into a.xg / a.posb, and (a.drop) the dropout keep
 // bits into a.dmask (lstm.hip x_gather_kernel); must run before lstm_fwd in bf16 mode
@@ -66,7 +77,7 @@ int pos_grad(const LstmArgs& a, int blocks, float* slab, hipStream_t st);
 size_t pos_shift_workspace_floats(int S, int L, int PD, int* nchunk, int* kps);
 int pos_grad_shift(const LstmArgs& a, float* gpart, float* out, hipStream_t st);
 bool lstm_supported(int U, int NX);
-size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD);
+size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fused_attn = false);
 
 struct AttnArgs {
   const void* hraw;

@@ -153,6 +153,39 @@ INA_DEVICE void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Self-attention backward fused into the bf16 BPTT (lstm_bwd FA; reference model/layer_module.py:49-98,
+// model/graph.py:36-53).  The direction-d wave recomputes, for each step's PREDECESSOR time tp (one step
+// ahead of the chain: dH_tp does not depend on the BPTT), the attention backward of its 16 sequences:
+//   H_tp = [own h_tp ; other direction's h_tp] (dropped, bf16; lane slots afeat(idx, q, d)),
+//   P = tanh(W1^T H + b1) (MFMA, pack w1f[d]), d(alpha) = de . H, ds = alpha (d(alpha) - de . e),
+//   dP = ds w2 (1 - P^2), dH_own = (W1_own dP + alpha de_own) * keep / keep_prob (MFMA, pack w1ft[d]),
+//   dW1[own rows] += H_own^T dP (16-row LDS images, one v_mfma_f32_16x16x16_bf16 K-step per time step),
+//   db1 += dP (direction 0) / dw2 += ds P (direction 1) in fp32 registers.
+// dH stays in registers: no dH round trip through HBM and no separate pass over the step records
+// (rec_attn_bwd read every h slot and wrote ~0.8 GB of dH per 8192-episode step).
+struct AttnFuse {
+  const u16x8_t* w1f;    // [2][MT][NKR][64]
+  const u16x8_t* w1ft;   // [2][NTD][NKS2][64]
+  const float* b1;
+  const float* w2;
+  const float* de;       // [S][2U] (original row order)
+  const float* e;        // [S][2U] forward output
+  const float* alphas;   // [S][L]
+  const int* perm;       // record row -> original row (ragged tiles) or nullptr
+  float* slab;           // [blocks][2][U 2U + 2U]: own dW1 rows | db1 (dir 0) or dw2 (dir 1)
+};
+template <int U>
+struct FAS {
+  static constexpr int U4 = U / 4, H2 = 2 * U, NV = 2 * U4, NKR = (NV + 7) / 8, MT = (H2 + 15) / 16;
+  static constexpr int NJ = 4 * MT, NKS2 = (NJ + 7) / 8, NTD = (U4 + 3) / 4;
+  static constexpr int NVPO = (U4 + 1) & ~1;            // own H image columns per lane group (even)
+  static constexpr int HTA = (4 * NVPO + 15) / 16;      // dW1 row tiles
+  static constexpr int HCPA = HTA * 16 + 4, JCPA = MT * 16 + 4;
+  static constexpr int NAP = MT * NKR * 64, NAPT = NTD * NKS2 * 64;
+  static constexpr int IMG = 16 * (HCPA + JCPA) * 2;    // bytes of a wave's two images
+  static constexpr int NSA = U * H2 + H2;               // slab floats per (block, dir)
+};
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -620,7 +653,8 @@ struct BwdWaves {
 // PM (bf16 only): dH arrives in the step-record lane layout ALREADY multiplied by the DropoutWrapper
 // scale (rec_attn_bwd), and the BPTT runs the lean step below (raw bf16 operands, no keep bits, no
 // per-lane validity selects, uniform per-step addresses).
-template <int U, int NX, bool BF16, bool WG = false, bool PM = false>
+// FA (with PM): the attention backward runs inside the BPTT (AttnFuse above); dH is not an input.
+template <int U, int NX, bool BF16, bool WG = false, bool PM = false, bool FA = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U, NX>::value))) void lstm_bwd_kernel(
     const int* __restrict__ inst, int S, const int* __restrict__ word, const int* __restrict__ pos1,
     const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
@@ -631,7 +665,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     float* __restrict__ dw_slab,
     float* __restrict__ dpos_slab, float* __restrict__ dwemb, const unsigned char* __restrict__ dmask, uint32_t seed,
     uint32_t thr, float inv_kp, int drop, unsigned short* __restrict__ dxp, const unsigned short* __restrict__ xg,
-    int dh_lane, const int* __restrict__ tlen, const int* __restrict__ slen, int wblank) {
+    int dh_lane, const int* __restrict__ tlen, const int* __restrict__ slen, int wblank, AttnFuse af) {
+  static_assert(!FA || (BF16 && PM), "the fused attention backward runs in the lean bf16 BPTT");
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
   using elem = typename FragT<BF16>::elem;
@@ -681,18 +716,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   unsigned short* dgI = reinterpret_cast<unsigned short*>(dgT);
   unsigned short* xhI = dgI + 32 * GCP;
   const int tcol = 4 * (n & 3);
+  using FS = FAS<U>;
   {
-    size_t xp = (size_t)4 * XROWS * RS * sizeof(elem);
-    const size_t red = (size_t)G4 * (4 * NX + U + 1) * sizeof(float);
+    // FA: the bf16 images at their exact size (the region also holds the final reductions)
+    size_t xp = FA ? (size_t)4 * 32 * (GCP + FCP) * 2 : (size_t)4 * XROWS * RS * sizeof(elem);
+    const size_t red = (size_t)G4 * (4 * NX + U + 1) * sizeof(float) + (FA ? (size_t)FS::NSA * 4 + 16 : 0);
     off += xp > red ? xp : red;
   }
   off = (off + 15) & ~(size_t)15;
   float* dpos_lds = reinterpret_cast<float*>(smem + off);   // [2 tables][2L][PD]
+  // FA: this direction's attention packs, [b1 | w2], and each wave's 16-row dW1 images [H_own | dP]
+  u16x8_t* lAp = reinterpret_cast<u16x8_t*>(smem + off);
+  u16x8_t* lApt = lAp + FS::NAP;
+  float* lbw = reinterpret_cast<float*>(lApt + FS::NAPT);
+  unsigned short* ahI = reinterpret_cast<unsigned short*>(lbw + 2 * FS::MT * 16) + (size_t)wave * (FS::IMG / 2);
+  unsigned short* apI = ahI + 16 * FS::HCPA;
+  if constexpr (FA) {
+    for (int i = threadIdx.x; i < FS::NAP; i += 256) lAp[i] = af.w1f[(size_t)dir * FS::NAP + i];
+    for (int i = threadIdx.x; i < FS::NAPT; i += 256) lApt[i] = af.w1ft[(size_t)dir * FS::NAPT + i];
+    for (int i = threadIdx.x; i < FS::MT * 16; i += 256) {
+      lbw[i] = i < FS::H2 ? af.b1[i] : 0.f;
+      lbw[FS::MT * 16 + i] = i < FS::H2 ? af.w2[i] : 0.f;
+    }
+    // pad columns of the images are never written and must read as zero
+    for (int i = lane; i < FS::IMG / 4; i += 64) reinterpret_cast<uint32_t*>(ahI)[i] = 0u;
+  }
   // gate packs / biases pre-scaled as in the forward (fragment index i -> lane i & 63, gate i & 3);
   // the transposed pack (d[x;h] = W dG) keeps the true weights
   for (int i = threadIdx.x; i < NA; i += 256) lA[i] = fscale(apack[(size_t)dir * NA + i], gate_scale(i & 3));
   for (int i = threadIdx.x; i < NA2; i += 256) lA2[i] = a2pack[(size_t)dir * NA2 + i];
-  for (int i = threadIdx.x; i < 4 * U; i += 256) lbias[i] = gate_bias(bias[dir * 4 * U + i], i / U);
+  // [unit][gate] (16-byte rows: the FA step re-reads a unit's four biases with one ds_read_b128)
+  for (int i = threadIdx.x; i < 4 * U; i += 256) lbias[(i % U) * 4 + i / U] = gate_bias(bias[dir * 4 * U + i], i / U);
   if constexpr (!BF16)
     for (int i = threadIdx.x; i < 2 * P2 * PD; i += 256) dpos_lds[i] = 0.f;
   const int NPF = 2 * PD;   // pos features (bf16 mode: exported to dxp, reduced by pos_grad_kernel)
@@ -710,12 +764,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
 #pragma unroll
   for (int m = 0; m < NMT; ++m)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bm[m][r] = lbias[r * U + 4 * m + q];
+    for (int r = 0; r < 4; ++r) bm[m][r] = lbias[(4 * m + q) * 4 + r];
   f32x4_t accw[GT][FTA];
 #pragma unroll
   for (int a = 0; a < GT; ++a)
 #pragma unroll
     for (int b = 0; b < FTA; ++b) accw[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // FA accumulators: dW1 own rows (image column tiles x projection tiles), db1 (dir 0) / sum ds rr (dir 1)
+  f32x4_t accA[FS::HTA][FS::MT];
+  float a12[FS::MT][4], asds = 0.f;
+  const bool adir = dir != 0;
+#pragma unroll
+  for (int a = 0; a < FS::HTA; ++a)
+#pragma unroll
+    for (int b = 0; b < FS::MT; ++b) accA[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < FS::MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a12[m][r] = 0.f;
 
   XSrc xs[NX];
 #pragma unroll
@@ -968,10 +1034,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       const auto rx = rsrc(xg + (size_t)tu * L * 64 * NX, (uint32_t)L * XSTEPB);
       const auto rdx = rsrc(dxp + ((size_t)dir * ntiles + tu) * L * (NPF + 1) * 16, (uint32_t)L * PSTEPB);
       const int vl2 = lane * 2, vx = lane * NX * 2;
+      // ---- FA: per-tile attention state (de of the lane's slots, sd = de . e) and buffer descriptors
+      const int orow = FA ? (af.perm ? af.perm[seqc] : (int)seqc) : 0;   // e / de / alphas row
+      float dev[FS::NV];   // de of slots [own ; other] (0 for padding rows)
+      float asd = 0.f;
+      if constexpr (FA) {
+#pragma unroll
+        for (int i = 0; i < FS::NV; ++i) {
+          const int f = i < U4 ? dir * U + 4 * i + q : (1 - dir) * U + 4 * (i - U4) + q;
+          const size_t o = (size_t)orow * FS::H2 + f;
+          const float x = valid ? af.de[o] : 0.f;
+          dev[i] = x;
+          asd = fmaf(x, af.e[o], asd);   // same sequential order as d(alpha) below
+        }
+        asd = cross_group_sum(asd);
+      }
+      // the other direction's step records: the descriptor ends at the tile's last valid step (the
+      // forward direction never wrote later ones; alpha is 0 there, loads past the range return 0)
+      const auto rorec = rsrc(reinterpret_cast<const unsigned short*>(hraw) + ((size_t)tu * 2 + (1 - dir)) * L * 2 * U4 * 64,
+                              (uint32_t)Lt * RSTEPB);
+      // keep bytes of both directions (without dropout: any readable bytes, every bit then set by akor)
+      const auto rkb = drop ? rsrc(dmask + (size_t)tu * 2 * L * 64, (uint32_t)(2 * L * 64)) : rrec;
+      const uint32_t akor = drop ? 0u : 0xFFFFu;
+      const int vko = drop ? dir * L * 64 + lane : 0, vkt = drop ? (1 - dir) * L * 64 + lane : 0;
+      const auto ral = rsrc(af.alphas, (uint32_t)((size_t)S * L * 4));
+      const int val = orow * L * 4;
       constexpr int NXW = NX / 2;   // x words (2 features each) per lane and step
       struct Raw {
         uint32_t h[U4], c[U4], d[U4];   // 16-bit loads (upper halves never read)
         uint32_t x[NXW];
+        uint32_t oh[U4], ko, kt, al;    // FA: other direction's h, keep bytes, alpha of the predecessor time
       };
       auto rload = [&](int tau, Raw& o) __attribute__((always_inline)) {
         const int tn = tof(tau), tp = tof(tau >= 1 ? tau - 1 : 0);
@@ -980,7 +1072,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         for (int m = 0; m < U4; ++m) {
           o.h[m] = __builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + m * 128, sr, 0);
           o.c[m] = __builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + (U4 + m) * 128, sr, 0);
-          o.d[m] = __builtin_amdgcn_raw_buffer_load_b16(rdh, vl2 + m * 128, sd, 0);
+          if constexpr (FA)
+            o.oh[m] = __builtin_amdgcn_raw_buffer_load_b16(rorec, vl2 + m * 128, sr, 0);
+          else
+            o.d[m] = __builtin_amdgcn_raw_buffer_load_b16(rdh, vl2 + m * 128, sd, 0);
+        }
+        if constexpr (FA) {
+          o.ko = __builtin_amdgcn_raw_buffer_load_b8(rkb, vko, tp * 64, 0);
+          o.kt = __builtin_amdgcn_raw_buffer_load_b8(rkb, vkt, tp * 64, 0);
+          o.al = __builtin_amdgcn_raw_buffer_load_b32(ral, val, tp * 4, 0);
         }
 #pragma unroll
         for (int k = 0; k < NXW / 2; ++k) {
@@ -997,11 +1097,116 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       // HASP: the step has a predecessor state (else it is zero: the direction's first step in time, or the
       // SKIP backward direction's tile start).  HI: the step stages into image rows 16..31 and completes
       // the pair (rows 0..15 = the previous step), FLUSH: the pair goes into dW after staging.
+      // ---- FA: the attention backward at time tp from its raw inputs -> dha (dH_tp of the own units, the
+      // DropoutWrapper scale applied) and the dW1 image words (own dropped H, dP in accumulator order)
+      float dha[U4];
+#pragma unroll
+      for (int m = 0; m < U4; ++m) dha[m] = 0.f;
+      auto att_math = [&](const uint32_t* ownh, const uint32_t* othh, uint32_t ko, uint32_t kt, uint32_t alraw,
+                          uint32_t* hwo, u16x8_t* B2) __attribute__((always_inline)) {
+        const float alv = valid ? __builtin_bit_cast(float, alraw) : 0.f;
+        const uint32_t kb = (ko | (kt << 8)) | akor;   // bit m: own slot m, bit 8 + m: other slot m
+        auto sc = [&](int i) {
+          const int b = i < U4 ? i : 8 + i - U4;
+          return (float)((kb >> b) & 1u) * inv_kp;
+        };
+        uint32_t bw[FS::NKR * 4];
+#pragma unroll
+        for (int w = 0; w < FS::NKR * 4; ++w) bw[w] = 0u;
+        float d = 0.f;
+#pragma unroll
+        for (int i = 0; i < FS::NV; i += 2) {
+          const uint32_t h0 = i < U4 ? ownh[i] : othh[i - U4];
+          const uint32_t h1 = i + 1 < U4 ? ownh[i + 1] : othh[i + 1 - U4];
+          const float x0 = bf2f((unsigned short)h0) * sc(i), x1 = bf2f((unsigned short)h1) * sc(i + 1);
+          const uint32_t w = (uint32_t)f2bf(x0) | ((uint32_t)f2bf(x1) << 16);
+          bw[i / 2] = w;
+          d = fmaf(dev[i], __builtin_bit_cast(float, w << 16), d);
+          d = fmaf(dev[i + 1], __builtin_bit_cast(float, w & 0xFFFF0000u), d);
+        }
+#pragma unroll
+        for (int w = 0; w < FS::NVPO / 2; ++w) hwo[w] = (2 * w + 1 < U4) ? bw[w] : (bw[w] & 0xFFFFu);
+        const float ds = alv * (cross_group_sum(d) - asd);   // 0 for padding rows (alpha 0)
+        const float ds4 = 4.f * ds;
+        asds += ds;
+        float dp[FS::MT][4];
+#pragma unroll
+        for (int m = 0; m < FS::MT; ++m) {
+          f32x4_t acc;
+          float wv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            acc[r] = lbw[16 * m + 4 * q + r];
+            wv[r] = lbw[FS::MT * 16 + 16 * m + 4 * q + r];
+          }
+#pragma unroll
+          for (int ks = 0; ks < FS::NKR; ++ks)
+            acc = mfma_bf16(lAp[(m * FS::NKR + ks) * 64 + lane],
+                            __builtin_bit_cast(u16x8_t, u32x4_t{bw[4 * ks], bw[4 * ks + 1], bw[4 * ks + 2], bw[4 * ks + 3]}),
+                            acc);
+          const f32x4_t r4 = tanh_r4(acc);   // P = 1 - 2 rr, 1 - P^2 = 4 rr (1 - rr)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float rr = r4[r];
+            dp[m][r] = ds4 * (wv[r] * (rr - rr * rr));
+            a12[m][r] += adir ? ds * rr : dp[m][r];   // dw2 = sum ds P = sum ds - 2 sum ds rr (dir 1); db1 (dir 0)
+          }
+        }
+#pragma unroll
+        for (int ks = 0; ks < FS::NKS2; ++ks) {
+          B2[ks] = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int idx = ks * 8 + j;
+            if (idx < FS::NJ) B2[ks][j] = f2bf(dp[idx >> 2][idx & 3]);
+          }
+        }
+#pragma unroll
+        for (int T = 0; T < FS::NTD; ++T) {
+          f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < FS::NKS2; ++ks) acc = mfma_bf16(lApt[(T * FS::NKS2 + ks) * 64 + lane], B2[ks], acc);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = 4 * T + r;
+            if (m < U4) dha[m] = (acc[r] + alv * dev[m]) * sc(m);
+          }
+        }
+      };
+      // own H / dP into the wave's 16-row images (row = sequence n); the flush contracts the 16 sequences
+      auto att_stage = [&](const uint32_t* hwo, const u16x8_t* B2) __attribute__((always_inline)) {
+        uint32_t* hi = reinterpret_cast<uint32_t*>(ahI + n * FS::HCPA + q * FS::NVPO);
+#pragma unroll
+        for (int w = 0; w < FS::NVPO / 2; ++w) hi[w] = hwo[w];
+        unsigned short* pr = apI + n * FS::JCPA + q * FS::NJ;
+#pragma unroll
+        for (int c = 0; c < FS::NJ / 4; ++c) {
+          const u16x8_t& b = B2[c / 2];
+          const int o = 4 * (c & 1);
+          *reinterpret_cast<u16x4_t*>(pr + 4 * c) = u16x4_t{b[o], b[o + 1], b[o + 2], b[o + 3]};
+        }
+      };
+      auto att_flush = [&]() __attribute__((always_inline)) {
+        s16x4_t fa[FS::HTA], fb[FS::MT];
+#pragma unroll
+        for (int a = 0; a < FS::HTA; ++a) fa[a] = tr_read(ahI + (4 * q + (n >> 2)) * FS::HCPA + 16 * a + 4 * (n & 3));
+#pragma unroll
+        for (int b = 0; b < FS::MT; ++b) fb[b] = tr_read(apI + (4 * q + (n >> 2)) * FS::JCPA + 16 * b + 4 * (n & 3));
+#pragma unroll
+        for (int a = 0; a < FS::HTA; ++a)
+#pragma unroll
+          for (int b = 0; b < FS::MT; ++b) accA[a][b] = mfma16_bf16(fa[a], fb[b], accA[a][b]);
+      };
       auto bstep = [&](auto hasp_c, auto hi_c, auto flush_c, const int tau, const Raw& X0) __attribute__((always_inline)) {
         constexpr bool HASP = decltype(hasp_c)::value, ODD = decltype(hi_c)::value, FLUSH = decltype(flush_c)::value;
         Raw X = X0;
 #pragma unroll
-        for (int m = 0; m < U4; ++m) asm volatile("" : "+v"(X.h[m]), "+v"(X.c[m]), "+v"(X.d[m]));
+        for (int m = 0; m < U4; ++m) {
+          asm volatile("" : "+v"(X.h[m]), "+v"(X.c[m]));
+          if constexpr (FA) asm volatile("" : "+v"(X.oh[m]));
+          else asm volatile("" : "+v"(X.d[m]));
+        }
+        if constexpr (FA) asm volatile("" : "+v"(X.ko), "+v"(X.kt), "+v"(X.al));
 #pragma unroll
         for (int k = 0; k < NXW; ++k) asm volatile("" : "+v"(X.x[k]));
         const int t = tof(tau);
@@ -1037,13 +1242,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
 #pragma unroll
         for (int m = 0; m < U4; ++m) {
           cprev[m] = HASP ? (float)__builtin_bit_cast(_Float16, (unsigned short)X.c[m]) : 0.f;
-          dhin[m] = __builtin_bit_cast(float, X.d[m] << 16);
+          dhin[m] = FA ? dha[m] : __builtin_bit_cast(float, X.d[m] << 16);
+        }
+        // FA: the attention backward of the predecessor time (the next step's dH), off the BPTT chain
+        uint32_t ahw[FS::NVPO / 2];
+        u16x8_t aB2[FS::NKS2];
+        if constexpr (FA && HASP) {
+          att_math(X.h, X.oh, X.ko, X.kt, X.al, ahw, aB2);
+          __builtin_amdgcn_sched_barrier(0);   // the attention's temporaries die before the BPTT's are born
         }
         // ---- recompute gates
         float dg[U4][4];
+        if constexpr (FA) asm volatile("" ::: "memory");   // FA: biases re-read from LDS per step (registers)
 #pragma unroll
         for (int m = 0; m < NMT; ++m) {
           f32x4_t acc = {bm[m][0], bm[m][1], bm[m][2], bm[m][3]};
+          if constexpr (FA) {
+            const float4 b4 = *reinterpret_cast<const float4*>(lbias + (4 * m + q) * 4);
+            acc = f32x4_t{b4.x, b4.y, b4.z, b4.w};
+          }
 #pragma unroll
           for (int ks = 0; ks < NKS; ++ks)
             acc = mma(lA[(m * NKS + ks) * 64 + lane],
@@ -1118,6 +1335,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         uint32_t* xi32 = reinterpret_cast<uint32_t*>(xhI + (RR + n) * FCP + q * NSLP);
 #pragma unroll
         for (int w = 0; w < NSLP / 2; ++w) xi32[w] = w < NW ? bw[w] : 0u;
+        if constexpr (FA && HASP) {   // attention dW1: every step (16-row images)
+          att_stage(ahw, aB2);
+          lds_order();
+          att_flush();
+          if constexpr (!FLUSH) lds_order();
+        }
         if constexpr (FLUSH) {
           lds_order();
           auto tr8 = [&](const unsigned short* img, int stride, int c0) {
@@ -1157,6 +1380,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       for (int m = 0; m < U4; ++m)   // c of the first processed step
         ccur[m] = (float)__builtin_bit_cast(
             _Float16, (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + (U4 + m) * 128, tof(tau_start) * RSTEPB, 0));
+      if constexpr (FA) {   // the attention backward of the first processed time (later ones run one step ahead)
+        const int t0 = tof(tau_start), s0 = t0 * RSTEPB;
+        uint32_t h0[U4], o0[U4];
+#pragma unroll
+        for (int m = 0; m < U4; ++m) {
+          h0[m] = __builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + m * 128, s0, 0);
+          o0[m] = __builtin_amdgcn_raw_buffer_load_b16(rorec, vl2 + m * 128, s0, 0);
+        }
+        const uint32_t k0 = __builtin_amdgcn_raw_buffer_load_b8(rkb, vko, t0 * 64, 0);
+        const uint32_t k1 = __builtin_amdgcn_raw_buffer_load_b8(rkb, vkt, t0 * 64, 0);
+        const uint32_t a0 = __builtin_amdgcn_raw_buffer_load_b32(ral, val, t0 * 4, 0);
+        uint32_t ahw[FS::NVPO / 2];
+        u16x8_t aB2[FS::NKS2];
+        att_math(h0, o0, k0, k1, a0, ahw, aB2);
+        att_stage(ahw, aB2);
+        lds_order();
+        att_flush();
+        lds_order();
+      }
       Raw A, B;
       rload(tau_start, A);
       int k = 0;   // processed steps so far: pairs (k, k + 1) -> image rows 0..15 / 16..31
@@ -1328,7 +1570,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   float* red = reinterpret_cast<float*>(xp_all);
   const int REDN = G4 * NF;
   for (int i = threadIdx.x; i < REDN; i += 256) red[i] = 0.f;
+  float* ared = red + ((REDN + 3) & ~3);   // FA: [U own rows][2U] dW1 | [2U] db1 (dir 0) or dw2 (dir 1)
+  if constexpr (FA)
+    for (int i = threadIdx.x; i < FS::NSA; i += 256) ared[i] = 0.f;
   __syncthreads();
+  float a1s[FS::MT][4];   // cross-lane sums first (every lane takes part in the shuffles)
+  int ajmap[FS::MT];
+  if constexpr (FA) {
+    const float sdsum = group16_sum(asds);
+#pragma unroll
+    for (int m = 0; m < FS::MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float s = group16_sum(a12[m][r]);
+        a1s[m][r] = adir ? sdsum - 2.f * s : s;
+      }
+#pragma unroll
+    for (int b = 0; b < FS::MT; ++b) {   // dP image column -> projection row j
+      const int c = 16 * b + n, qq = c / FS::NJ, idx = c % FS::NJ;
+      const int j = 16 * (idx >> 2) + 4 * qq + (idx & 3);
+      ajmap[b] = (qq < 4 && j < FS::H2) ? j : -1;
+    }
+  }
   // bf16: un-permute the image columns (dG column c -> gate row, XH column -> feature; -1 = pad)
   int fmap[FTA];
 #pragma unroll
@@ -1361,9 +1624,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         for (int b = 0; b < FTA; ++b)
           if (fmap[b] >= 0) red[gc * NF + fmap[b]] += accw[a][b][r];
       }
+    if constexpr (FA) {
+#pragma unroll
+      for (int a = 0; a < FS::HTA; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 16 * a + 4 * q + r, qq = c / FS::NVPO, idx = c % FS::NVPO;
+          if (qq >= 4 || idx >= U4) continue;
+          const int row = (4 * idx + qq) * FS::H2;   // own unit 4 idx + qq
+#pragma unroll
+          for (int b = 0; b < FS::MT; ++b)
+            if (ajmap[b] >= 0) ared[row + ajmap[b]] += accA[a][b][r];
+        }
+#pragma unroll
+      for (int m = 0; m < FS::MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = 16 * m + 4 * q + r;
+          if (n == 0 && j < FS::H2) ared[U * FS::H2 + j] += a1s[m][r];
+        }
+    }
   });
   float* slab = dw_slab + ((size_t)blockIdx.x * 2 + dir) * REDN;
   for (int i = threadIdx.x; i < REDN; i += 256) slab[i] = red[i];
+  if constexpr (FA) {
+    float* as = af.slab + ((size_t)blockIdx.x * 2 + dir) * FS::NSA;
+    for (int i = threadIdx.x; i < FS::NSA; i += 256) as[i] = ared[i];
+  }
   if constexpr (!BF16) {
     float* ps = dpos_slab + ((size_t)blockIdx.x * 2 + dir) * 2 * P2 * PD;
     for (int i = threadIdx.x; i < 2 * P2 * PD; i += 256) ps[i] = dpos_lds[i];
@@ -1581,7 +1868,8 @@ namespace ina {
 
 
 
-size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD) {
+// mirrors the kernel's LDS carve (lstm_bwd_kernel)
+size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fa) {
   const int KPL = bf16 ? 8 : 1;
   const int U4 = U / 4, NSLOT = U4 + NX;
   const int NA = U4 * ((NSLOT + KPL - 1) / KPL) * 64;
@@ -1590,13 +1878,20 @@ size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD) {
   const int GT = (4 * U + 15) / 16;
   const int FTMAX = (4 * NX + U + 1 + 15) / 16;
   const int RS = bf16 ? 40 : 36;
+  // attention (fa): FAS<U>
+  const int H2 = 2 * U, NV = 2 * U4, NKR = (NV + 7) / 8, MT = (H2 + 15) / 16, NJ = 4 * MT, NKS2 = (NJ + 7) / 8;
+  const int NTD = (U4 + 3) / 4, NVPO = (U4 + 1) & ~1, HTA = (4 * NVPO + 15) / 16;
+  const int HCPA = HTA * 16 + 4, JCPA = MT * 16 + 4, NSA = U * H2 + H2;
   size_t off = (size_t)(NA + NA2) * fragb + 4 * U * 4;
   off = (off + 15) & ~(size_t)15;
-  size_t xp = (size_t)4 * (GT * 16 + FTMAX * 16) * RS * (bf16 ? 2 : 4);
-  const size_t red = (size_t)4 * U * (4 * NX + U + 1) * 4;
+  const int NSLP = (U4 + NX + 1) & ~1, FTA = (4 * NSLP + 1 + 15) / 16;
+  const int GCP = GT * 16 + 4, FCP = FTA * 16 + 4;
+  size_t xp = fa ? (size_t)4 * 32 * (GCP + FCP) * 2 : (size_t)4 * (GT * 16 + FTMAX * 16) * RS * (bf16 ? 2 : 4);
+  const size_t red = (size_t)4 * U * (4 * NX + U + 1) * 4 + (fa ? (size_t)NSA * 4 + 16 : 0);
   off += xp > red ? xp : red;
   off = (off + 15) & ~(size_t)15;
   if (!bf16) off += (size_t)2 * 2 * L * PD * 4;   // block pos tables (bf16 mode: pos_grad_kernel)
+  if (fa) off += (size_t)(MT * NKR * 64 + NTD * NKS2 * 64) * 16 + 2 * MT * 16 * 4 + (size_t)4 * 16 * (HCPA + JCPA) * 2;
   return off;
 }
 
@@ -1627,23 +1922,38 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   using frag = typename FragT<BF16>::type;
   using elem = typename FragT<BF16>::elem;
   dim3 grid(a.bwd_blocks, 2);
-  size_t lds = lstm_bwd_lds_bytes(U, NX, BF16, a.L, a.PD);
-  // bf16 + lane-layout dH (rec_attn_bwd, premasked): the lean PM step
-  const bool pm = INA_LSTM_PM && BF16 && a.dh_lane;
+  // bf16 + lane-layout dH (rec_attn_bwd, premasked): the lean PM step; fa: the attention backward fused in
+  const bool fa = BF16 && a.aslab != nullptr;
+  const bool pm = INA_LSTM_PM && BF16 && (a.dh_lane || fa);
+  size_t lds = lstm_bwd_lds_bytes(U, NX, BF16, a.L, a.PD, fa);
   auto kfn = pm ? (a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, BF16> : lstm_bwd_kernel<U, NX, BF16, false, BF16>)
                 : (a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, false> : lstm_bwd_kernel<U, NX, BF16, false, false>);
+  if (fa) kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, BF16, BF16> : lstm_bwd_kernel<U, NX, BF16, false, BF16, BF16>;
   static bool attr_set = false;
   if (!attr_set) {
     for (auto f : {lstm_bwd_kernel<U, NX, BF16, true, false>, lstm_bwd_kernel<U, NX, BF16, false, false>,
-                   lstm_bwd_kernel<U, NX, BF16, true, BF16>, lstm_bwd_kernel<U, NX, BF16, false, BF16>})
+                   lstm_bwd_kernel<U, NX, BF16, true, BF16>, lstm_bwd_kernel<U, NX, BF16, false, BF16>,
+                   lstm_bwd_kernel<U, NX, BF16, true, BF16, BF16>, lstm_bwd_kernel<U, NX, BF16, false, BF16, BF16>})
       hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
+  }
+  AttnFuse af{};
+  if (fa) {
+    af.w1f = (const u16x8_t*)a.aw1f;
+    af.w1ft = (const u16x8_t*)a.aw1ft;
+    af.b1 = a.ab1;
+    af.w2 = a.aw2;
+    af.de = a.ade;
+    af.e = a.ae;
+    af.alphas = a.aalphas;
+    af.perm = a.perm;
+    af.slab = a.aslab;
   }
   hipLaunchKernelGGL(kfn, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, (const frag*)a.a2pack, a.bias,
                      (const elem*)a.hraw, (const typename CT<BF16>::type*)a.cst, (const elem*)a.dH, a.dw_slab, a.dpos_slab, a.dwemb, a.dmask, a.seed, a.thr, a.inv_kp,
                      a.drop, (unsigned short*)a.dxp, (const unsigned short*)a.xg, a.dh_lane, pm ? a.tlen : nullptr,
-                     pm ? a.slen : nullptr, a.wblank);
+                     pm ? a.slen : nullptr, a.wblank, af);
   INA_CHECK_LAUNCH();
   return 0;
 }

@@ -35,19 +35,22 @@ def main(argv=None):
     p.add_argument("--iters", type=int, default=1000)
     p.add_argument("--checkpoint", default="best", choices=["best", "latest"],
                    help="best-val checkpoint (falls back to the latest) or the latest one")
+    p.add_argument("--checkpoint_format", default="safetensors", choices=["safetensors", "tf"],
+                   help="read the safetensors copy or the TF V2 bundle (.index + .data-00000-of-00001); a "
+                        "checkpoint with only one of them loads from that one")
     args = p.parse_args(argv)
     base = Config()
     md = args.model_dir or base.model_dir
     stem = (ckpt.best(md) if args.checkpoint == "best" else None) or ckpt.latest(md)
     if stem is not None:
-        _, meta = ckpt.load(stem)
+        _, meta = ckpt.load(stem, args.checkpoint_format)
         base = Config.from_dict(meta.get("config", {}))
     cfg = config_from_args(args, base).replace(resume=False, episodes_per_step=max(1, base.episodes_per_step))
     tr_data, va_data = T.load_data(cfg, args)
     te = T.load_test(cfg, tr_data) if cfg.test_file else va_data
     trainer = Trainer(cfg, tr_data, va_data, device=cfg.device, log=False)
     if stem is not None:
-        trainer.load(stem)
+        trainer.load(stem, args.checkpoint_format)
     else:
         print(json.dumps({"warning": "no checkpoint found; evaluating the random init"}), file=sys.stderr)
     settings = ([tuple(int(x) for x in s.split("-")) for s in args.settings.split(",") if s]

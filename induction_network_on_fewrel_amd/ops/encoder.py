@@ -18,12 +18,13 @@ model/layer_module.py:49-98 (self_attention).
 """
 from __future__ import annotations
 
+import os
 import weakref
 
 import torch
 
 from ._ext import ops
-from .packing import lstm_shape, pack_attn, pack_attn_rec, pack_lstm
+from .packing import lstm_shape, pack_attn, pack_attn_fuse, pack_attn_rec, pack_lstm
 
 
 def _route_grad(meta, name, g):
@@ -142,9 +143,14 @@ class EncoderFn(torch.autograd.Function):
             hlane, cst, hnat, dmask, xg = o.lstm_fwd(*lstm_args, bf16, bool(need_grad), *tail)
             e, alphas = o.attn_fwd(hnat, inst, mask, w1pack, b1c, w2c, U, bf16, int(meta.get("attn_blocks", 0)))
         if need_grad:
+            # attention backward fused into lstm_bwd (record path): its own per-direction packs
+            fused = rec and meta.get("fuse_attn_bwd", os.environ.get("INA_FUSE_ATTN_BWD", "0") != "0")
+            if fused:
+                w1pack, w1tpack = ((pk["w1fpack"], pk["w1ftpack"]) if pk is not None and "w1fpack" in pk
+                                   else pack_attn_fuse(W1))
             ctx.save_for_backward(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst,
                                   w1pack, w1tpack, b1, w2, alphas, hnat, dmask, xg, e, perm, tlen, slen)
-            ctx.meta = dict(meta, NX=sh["NX"], DIN=DIN, rec=rec)
+            ctx.meta = dict(meta, NX=sh["NX"], DIN=DIN, rec=rec, fused=fused)
         ctx.mark_non_differentiable(alphas)
         ctx.set_materialize_grads(False)   # no zero-fill launch for the alphas gradient
         return e, alphas
@@ -158,33 +164,60 @@ class EncoderFn(torch.autograd.Function):
         U, bf16, DIN = m["U"], m["bf16"], m["DIN"]
         H2 = 2 * U
         b1c, w2c = b1.detach().contiguous(), w2.detach().reshape(-1).contiguous()
+        word_grad = bool(m.get("word_grad", False))
+        if m.get("fused"):
+            # one kernel: BPTT + the attention backward one step ahead of it (no dH tensor)
+            dw_slab, dpos_slab, dwemb, fslab = o.lstm_attn_bwd(
+                inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
+                p2emb.detach().contiguous(), apack, a2pack, bias, hlane, dmask, xg, w1pack, w1tpack, b1c, w2c,
+                de.contiguous().float(), e, alphas, U, m["NX"], word_grad, int(m.get("lstm_blocks", 0)),
+                int(m["seed"]), float(m["keep_prob"]), bool(m.get("pos_shift", False)), tlen, slen, perm)
+            return EncoderFn._grads(ctx, m, None, fslab, dw_slab, dpos_slab, dwemb)
         if m["rec"]:   # dH in lstm_bwd's lane layout [tiles, 2, L, U/4, 64]
             dH, aslab = o.rec_attn_bwd(hlane, dmask, w1pack, w1tpack, b1c, w2c, de.contiguous().float(), e, alphas,
                                        U, float(m["keep_prob"]), int(m.get("attn_blocks", 0)), tlen, perm)
         else:
             dH, aslab = o.attn_bwd(hnat, inst, w1pack, w1tpack, b1c, w2c, de.contiguous().float(), alphas, U, bf16,
                                    int(m.get("attn_blocks", 0)))
-        word_grad = bool(m.get("word_grad", False))
         dw_slab, dpos_slab, dwemb = o.lstm_bwd(inst, word, pos1, pos2, wemb.detach().contiguous(),
                                                p1emb.detach().contiguous(), p2emb.detach().contiguous(), apack, a2pack,
                                                bias, hlane, cst, dH, dmask, xg, U, m["NX"], bf16, word_grad,
                                                int(m.get("lstm_blocks", 0)), int(m["seed"]), float(m["keep_prob"]),
                                                bool(m.get("pos_shift", False)), tlen, slen)
+        return EncoderFn._grads(ctx, m, aslab, None, dw_slab, dpos_slab, dwemb)
+
+    @staticmethod
+    def _grads(ctx, m, aslab, fslab, dw_slab, dpos_slab, dwemb):
+        """Slabs -> parameter gradients.  aslab: [blocks, 2U*2U + 2*2U] (attention kernels); fslab: the fused
+        kernel's [blocks, 2 dir, U*2U + 2U] (own W1 rows | db1 or dw2)."""
+        word, p1emb, p2emb = ctx.saved_tensors[1], ctx.saved_tensors[5], ctx.saved_tensors[6]
+        U, DIN = m["U"], m["DIN"]
+        H2 = 2 * U
+        word_grad = bool(m.get("word_grad", False))
         glue = m.get("glue")
         if glue is not None:
             # slabs -> flat gradient in the step's single slab_scatter_add launch (StepGlue.flush)
             p = m["pdict"]
-            glue.add(aslab, glue.map_attn(p, H2), aslab.shape[0])
+            if fslab is not None:
+                glue.add(fslab, glue.map_attn_fused(p, U), fslab.shape[0])
+            else:
+                glue.add(aslab, glue.map_attn(p, H2), aslab.shape[0])
             glue.add(dw_slab, glue.map_lstm_dw(p, U, DIN), dw_slab.shape[0])
             L, PD = word.shape[1], p1emb.shape[1]
             mp = glue.map_pos(p, L, PD)
             glue.add(dpos_slab, mp, dpos_slab.numel() // mp.numel())
             wg = _route_grad(m, "word_embedding", dwemb) if word_grad else None
             return (None,) * 5 + (wg,) + (None,) * 10
-        a = aslab.sum(0)
-        dW1 = a[: H2 * H2].view(H2, H2)
-        db1 = a[H2 * H2: H2 * H2 + H2]
-        dw2 = a[H2 * H2 + H2:].view(H2, 1)
+        if fslab is not None:
+            f = fslab.sum(0)                       # [2, U*H2 + H2]
+            dW1 = f[:, : U * H2].reshape(H2, H2)
+            db1 = f[0, U * H2:]
+            dw2 = f[1, U * H2:].reshape(H2, 1)
+        else:
+            a = aslab.sum(0)
+            dW1 = a[: H2 * H2].view(H2, H2)
+            db1 = a[H2 * H2: H2 * H2 + H2]
+            dw2 = a[H2 * H2 + H2:].view(H2, 1)
         D = dw_slab.sum(0)                         # [2, 4U, DIN+U+1]
         dKf = D[0, :, : DIN + U].t()
         dKb = D[1, :, : DIN + U].t()

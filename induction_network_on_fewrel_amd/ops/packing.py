@@ -194,6 +194,62 @@ def pack_attn_rec(W1: torch.Tensor):
     return We[_on(pi, dev)].to(torch.bfloat16).contiguous(), We[_on(ti, dev)].to(torch.bfloat16).contiguous()
 
 
+def afeat(idx: int, q: int, d: int, U: int) -> int:
+    """Feature of slot idx of lane group q in direction d's wave of the fused attention backward
+    (lstm.hip, lstm_bwd FA): slots [own direction's units ; the other direction's units]."""
+    U4 = U // 4
+    return d * U + 4 * idx + q if idx < U4 else (1 - d) * U + 4 * (idx - U4) + q
+
+
+@lru_cache(maxsize=None)
+def _attn_fuse_idx(U: int):
+    """Flat indices into [W1 [2U, 2U] | 0] for the attention backward fused into lstm_bwd (one pack per
+    direction; the direction's wave holds its own units first):
+      w1f  [2][MT][NKR][64][8]:  A[row j = 16 m + (l & 15)][k slot (l >> 4, jj)] = W1[afeat(8 ks + jj, l >> 4, d)][j]
+      w1ft [2][NTD][NKS2][64][8]: A[row (qr, rr) = l & 15][k slot (l >> 4, jj)] = W1[d U + 4 (4 T + rr) + qr][j]
+                                 (own units only, 4 T + rr < U/4), j = 16 (idx >> 2) + 4 (l >> 4) + (idx & 3),
+                                 idx = 8 ks + jj (dP accumulator order)."""
+    U4, H2 = U // 4, 2 * U
+    NV, MT = 2 * U4, (H2 + 15) // 16
+    NKR, NJ = (NV + 7) // 8, 4 * MT
+    NKS2, NTD = (NJ + 7) // 8, (U4 + 3) // 4
+    Z = H2 * H2
+    p = np.full((2, MT, NKR, 64, 8), Z, dtype=np.int64)
+    t = np.full((2, NTD, NKS2, 64, 8), Z, dtype=np.int64)
+    for d in range(2):
+        for m in range(MT):
+            for ks in range(NKR):
+                for l in range(64):
+                    j = 16 * m + (l & 15)
+                    for jj in range(8):
+                        idx = 8 * ks + jj
+                        if idx < NV and j < H2:
+                            p[d, m, ks, l, jj] = afeat(idx, l >> 4, d, U) * H2 + j
+        for T in range(NTD):
+            for ks in range(NKS2):
+                for l in range(64):
+                    r16 = l & 15
+                    fi = 4 * T + (r16 & 3)
+                    if fi >= U4:
+                        continue
+                    i = d * U + 4 * fi + (r16 >> 2)
+                    for jj in range(8):
+                        idx = 8 * ks + jj
+                        j = 16 * (idx >> 2) + 4 * (l >> 4) + (idx & 3)
+                        if idx < NJ and j < H2:
+                            t[d, T, ks, l, jj] = i * H2 + j
+    return torch.from_numpy(p), torch.from_numpy(t)
+
+
+def pack_attn_fuse(W1: torch.Tensor):
+    """-> (w1f, w1ft) bf16 packs of the attention backward fused into lstm_bwd (see _attn_fuse_idx)."""
+    U = W1.shape[0] // 2
+    pi, ti = _attn_fuse_idx(U)
+    dev = W1.device
+    We = torch.cat([W1.detach().float().reshape(-1), W1.new_zeros(1, dtype=torch.float32)])
+    return We[_on(pi, dev)].to(torch.bfloat16).contiguous(), We[_on(ti, dev)].to(torch.bfloat16).contiguous()
+
+
 # ------------------------------------------------------------------ NTN (bf16 only)
 def _kmap32(q: int, j: int) -> int:
     return 16 * (j >> 2) + 4 * q + (j & 3)

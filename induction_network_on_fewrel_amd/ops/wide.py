@@ -13,6 +13,8 @@ the two GEMMs of SURVEY K7 -- P = C M, then batched P Q^T) under autograd.
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from ._ext import ops
@@ -106,15 +108,17 @@ _WTAB: dict = {}
 def word_table_bf16(wemb: torch.Tensor) -> torch.Tensor:
     """bf16 copy of a FROZEN word table, cached per (tensor, version): the x rows enter the GEMM as bf16
     anyway, and the wide gather's random row reads are ~2/3 of its traffic at 300-d words.  An in-place
-    update of the table bumps its version counter and refreshes the copy."""
-    key = (wemb.data_ptr(), tuple(wemb.shape), wemb.device)
+    update of the table bumps its version counter and refreshes the copy.  Keyed by tensor identity (a
+    weak reference), not data_ptr: a freed table's address is reused by the caching allocator, and a
+    same-shape table allocated there at version 0 would otherwise get the old table's rows."""
+    key = (id(wemb), wemb._version)
     ent = _WTAB.get(key)
-    if ent is not None and ent[0] == wemb._version:
+    if ent is not None and ent[0]() is wemb:
         return ent[1]
     if len(_WTAB) >= 2:
         _WTAB.pop(next(iter(_WTAB)))
     tab = wemb.detach().to(torch.bfloat16).contiguous()
-    _WTAB[key] = (wemb._version, tab)
+    _WTAB[key] = (weakref.ref(wemb), tab)
     return tab
 
 

@@ -23,6 +23,16 @@ import torch
 import torch.distributed as dist
 
 
+def _native_op(op) -> str:
+    """torch.distributed ReduceOp -> the native communicator's op name (csrc/comm_bindings.cpp); ops it
+    has no equivalent for raise instead of silently becoming a sum."""
+    if op is None or op == dist.ReduceOp.SUM:
+        return "sum"
+    for name in ("MAX", "MIN", "PRODUCT"):
+        if op == getattr(dist.ReduceOp, name):
+            return {"MAX": "max", "MIN": "min", "PRODUCT": "prod"}[name]
+    raise ValueError(f"native communicator: unsupported reduce op {op}")
+
 class DistContext:
     def __init__(self, rank: int = 0, world: int = 1, local_rank: int = 0, device: Optional[torch.device] = None,
                  backend: Optional[str] = None):
@@ -101,7 +111,7 @@ class DistContext:
     def allreduce_(self, t: torch.Tensor, op=None) -> torch.Tensor:
         if self.initialized:
             if self._native_ok(t):
-                self.native.allreduce_(t, "max" if op == dist.ReduceOp.MAX else "sum")
+                self.native.allreduce_(t, _native_op(op))
                 self.native.wait()
             else:
                 dist.all_reduce(t, op=op or dist.ReduceOp.SUM)

@@ -5,9 +5,12 @@ Reference (model/base.py:124,171-178): ``tf.train.Saver()`` (max_to_keep=5) savi
 val accuracy; there is NO restore path in the reference (``curr_iter = 0``, :130). This module keeps
 the directory layout, the file stem and the state file, and the variable names/shapes of SURVEY 2.4
 as tensor keys (params, ``<var>/Adam``, ``<var>/Adam_1``, ``beta1_power``, ``beta2_power``,
-``global_step``), stored as safetensors + a JSON index (TF's binary bundle format is not
-reproducible without TensorFlow). Adds resume: params, optimizer moments, step, sampler/RNG state,
-best accuracy. Rank 0 writes; other ranks receive state by broadcast (parallel/dp.py).
+``global_step``).  Every checkpoint is written twice under the same stem: as TF's V2 tensor bundle
+(``<stem>.index`` + ``<stem>.data-00000-of-00001``, the files ``tf.train.Saver`` writes; runtime/tf_bundle.py
+produces them without TF) and as safetensors (``<stem>.safetensors``) + a JSON index (``<stem>.index.json``:
+resume metadata -- config, sampler states, best accuracy, optimizer counters).  ``load`` reads either
+(safetensors first; a bare TF bundle, e.g. written elsewhere, loads with its metadata if present).
+Rank 0 writes; other ranks receive state by broadcast (parallel/dp.py).
 """
 from __future__ import annotations
 
@@ -19,6 +22,8 @@ from typing import Dict, Optional, Tuple
 
 import torch
 from safetensors.torch import load_file, save_file
+
+from . import tf_bundle
 
 FORMAT = "ina-ckpt-v1"
 
@@ -70,7 +75,7 @@ def best_stem(model_dir: str) -> Optional[str]:
 
 
 def save(model_dir: str, name: str, step: int, tensors: "OrderedDict[str, torch.Tensor]", meta: dict,
-         max_to_keep: int = 5, best: bool = False) -> str:
+         max_to_keep: int = 5, best: bool = False, tf_format: bool = True) -> str:
     """Write ``<model_dir>/checkpoint/<name>-<step>`` and rotate to ``max_to_keep``.  ``best=True`` also
     points ``best_checkpoint`` at it; the best checkpoint is never rotated away (a periodic or resumed
     checkpoint can be newer, so "latest" is not "best")."""
@@ -81,6 +86,8 @@ def save(model_dir: str, name: str, step: int, tensors: "OrderedDict[str, torch.
     tmp = os.path.join(d, stem + ".safetensors.tmp")
     save_file(cpu, tmp)
     os.replace(tmp, os.path.join(d, stem + ".safetensors"))
+    if tf_format:
+        tf_bundle.save_bundle(os.path.join(d, stem), cpu)   # <stem>.index + <stem>.data-00000-of-00001
     index = dict(meta, format=FORMAT, global_step=int(step),
                  variables={k: {"shape": list(v.shape), "dtype": str(v.dtype).replace("torch.", "")}
                             for k, v in cpu.items()})
@@ -107,7 +114,7 @@ def save(model_dir: str, name: str, step: int, tensors: "OrderedDict[str, torch.
 
 
 def _remove(d: str, stem: str) -> None:
-    for ext in (".safetensors", ".index.json"):
+    for ext in (".safetensors", ".index.json", ".index", tf_bundle.DATA_SUFFIX):
         try:
             os.remove(os.path.join(d, stem + ext))
         except FileNotFoundError:
@@ -119,7 +126,11 @@ def latest(model_dir: str) -> Optional[str]:
     if stem is None:
         return None
     p = os.path.join(ckpt_dir(model_dir), stem)
-    return p if os.path.exists(p + ".safetensors") else None
+    return p if _exists(p) else None
+
+
+def _exists(p: str) -> bool:
+    return os.path.exists(p + ".safetensors") or tf_bundle.exists(p)
 
 
 def best(model_dir: str) -> Optional[str]:
@@ -128,13 +139,21 @@ def best(model_dir: str) -> Optional[str]:
     if stem is None:
         return None
     p = os.path.join(ckpt_dir(model_dir), stem)
-    return p if os.path.exists(p + ".safetensors") else None
+    return p if _exists(p) else None
 
 
-def load(path_stem: str) -> Tuple[Dict[str, torch.Tensor], dict]:
-    tensors = load_file(path_stem + ".safetensors")
-    with open(path_stem + ".index.json") as fh:
-        meta = json.load(fh)
-    if meta.get("format") != FORMAT:
-        raise ValueError(f"unknown checkpoint format {meta.get('format')}")
+def load(path_stem: str, prefer: str = "safetensors") -> Tuple[Dict[str, torch.Tensor], dict]:
+    """(tensors by TF variable name, metadata).  ``prefer="tf"`` reads the TF bundle even when the
+    safetensors copy exists; a bundle without our JSON index gets ``{"format": "tf-bundle"}`` metadata."""
+    use_tf = not os.path.exists(path_stem + ".safetensors") or (prefer == "tf" and tf_bundle.exists(path_stem))
+    tensors = dict(tf_bundle.load_bundle(path_stem)) if use_tf else load_file(path_stem + ".safetensors")
+    if os.path.exists(path_stem + ".index.json"):
+        with open(path_stem + ".index.json") as fh:
+            meta = json.load(fh)
+        if meta.get("format") != FORMAT:
+            raise ValueError(f"unknown checkpoint format {meta.get('format')}")
+    elif use_tf:
+        meta = {"format": "tf-bundle", "global_step": int(tensors["global_step"]) if "global_step" in tensors else 0}
+    else:
+        raise FileNotFoundError(path_stem + ".index.json")
     return tensors, meta

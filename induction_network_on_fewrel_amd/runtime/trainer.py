@@ -65,7 +65,8 @@ class Trainer:
         self.cfg = cfg
         if cfg.deterministic:
             from ..utils import make_deterministic
-            make_deterministic(cfg.seed)
+            make_deterministic(cfg.seed, trained_word_table=(cfg.train_word_embedding
+                                                             or train_data.word_vec_mat is None))
         self.dist = dist_ctx or DistContext.from_env(device if device != "auto" else cfg.device)
         if device not in ("auto", None) and self.dist.world == 1 and torch.device(device).type != self.dist.device.type:
             self.dist.device = torch.device(device)   # (keeps from_env's device index for a matching type)
@@ -177,6 +178,10 @@ class Trainer:
         (launch-bound) steps of the fused BiLSTM path."""
         cfg = self.cfg
         if self.device.type != "cuda" or cfg.encoder != "bilstm" or self.glue is None:
+            return False
+        # only the fused BiLSTM kernels read the dropout seed from device memory (seed_dev); the wide /
+        # per-step paths take it as a host int that a captured graph would freeze (same mask every replay)
+        if not self.model.use_fused_lstm(cfg.max_length):
             return False
         return cfg.use_hip_graph or 0 < cfg.episodes_per_step <= cfg.hip_graph_max_episodes
 
@@ -414,8 +419,9 @@ class Trainer:
         return ckpt.save(self.cfg.model_dir, self.cfg.ckpt_name, self.global_step, self.state_tensors(), meta,
                          self.cfg.max_to_keep, best=best)
 
-    def load(self, stem: str) -> None:
-        tensors, meta = ckpt.load(stem)
+    def load(self, stem: str, prefer: str = "safetensors") -> None:
+        """Restore from ``stem`` (either checkpoint format; ``prefer="tf"``: the TF bundle copy)."""
+        tensors, meta = ckpt.load(stem, prefer)
         p = self.model.params
         p.load_tf_state(tensors, strict=False)
         st = self.opt.state_tensors()
@@ -431,9 +437,12 @@ class Trainer:
         self.best_acc = float(meta.get("best_acc", 0.0))
         skipped = int(meta.get("skipped_steps", 0))
         # optimizer_t: applied Adam updates (older checkpoints stored the step count, skips included)
-        t = int(meta["optimizer_t"]) if "optimizer_t" in meta else self.global_step - skipped
-        if meta.get("optimizer_t_counts") != "applied":
-            t -= skipped
+        if "optimizer_t" in meta:
+            t = int(meta["optimizer_t"])
+            if meta.get("optimizer_t_counts") != "applied":   # older checkpoints counted the skipped steps too
+                t -= skipped
+        else:
+            t = self.global_step - skipped
         self.opt.load_counters(max(0, t), skipped)
         self._restore_sampler(meta)
         if self.dist.initialized:

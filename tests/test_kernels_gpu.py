@@ -327,6 +327,35 @@ def test_ragged_tiles_match_full_length(keep_prob):
         assert err < 1e-4, k
 
 
+@pytest.mark.parametrize("u", [8, 20, 32])
+@pytest.mark.parametrize("keep_prob", [1.0, 0.9])
+@pytest.mark.parametrize("skip", [False, True])
+def test_fused_attention_backward_matches_split(keep_prob, u, skip, monkeypatch):
+    """lstm_attn_bwd (the attention backward one step ahead inside the BPTT, dH in registers) against the
+    split rec_attn_bwd -> lstm_bwd path on the same forward: every encoder gradient.  The fused kernel keeps
+    dH in fp32 (the split path rounds it to bf16 in HBM), so they agree to bf16 rounding, not bitwise."""
+    from induction_network_on_fewrel_amd.ops.encoder import encode
+    cfg, data, model, dd, inst, _ = _problem(dtype="bf16", u=u, B=7)
+    out = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("INA_FUSE_ATTN_BWD", fused)
+        p = {k: v.detach().clone().requires_grad_(v.requires_grad) for k, v in model.pdict().items()}
+        meta = dict(U=cfg.hidden_size, bf16=True, keep_prob=keep_prob, seed=5, word_grad=False, ragged_min_rows=0,
+                    skip_padding=skip)
+        e, a = encode(inst, dd.arrays(), p, meta)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        de = torch.randn(e.shape, generator=g, device="cuda")
+        (e * de).sum().backward()
+        torch.cuda.synchronize()
+        out.append((e.detach(), {k: v.grad for k, v in p.items() if v.grad is not None}))
+    (e0, g0), (e1, g1) = out
+    assert torch.equal(e0, e1)
+    for k in g0:
+        err = _relerr(g1[k], g0[k])
+        print(f"  fused u={u} kp={keep_prob} skip={skip} grad {k}: {err:.2e}")
+        assert torch.isfinite(g1[k]).all() and err < 1e-2, k
+
+
 @pytest.mark.parametrize("L", [24, 1, 2])
 def test_encoder_backward_short_and_even_L(L):
     """even L and the 1- and 2-step edge cases of the recurrences' peeled loops."""

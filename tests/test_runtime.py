@@ -57,7 +57,10 @@ def test_checkpoint_layout_and_rotation(tmp_path):
                   {"best_acc": step / 100}, max_to_keep=2)
     d = os.path.join(md, "checkpoint")
     files = sorted(os.listdir(d))
-    assert files == ["checkpoint", "inductionNetwork-20.index.json", "inductionNetwork-20.safetensors",
+    assert files == ["checkpoint",
+                     "inductionNetwork-20.data-00000-of-00001", "inductionNetwork-20.index",
+                     "inductionNetwork-20.index.json", "inductionNetwork-20.safetensors",
+                     "inductionNetwork-30.data-00000-of-00001", "inductionNetwork-30.index",
                      "inductionNetwork-30.index.json", "inductionNetwork-30.safetensors"]
     with open(os.path.join(d, "checkpoint")) as fh:
         txt = fh.read()

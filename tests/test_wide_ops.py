@@ -32,3 +32,21 @@ def test_tall_skinny_mm_gradients():
         (x2 @ w2).backward(dy)
         torch.testing.assert_close(x.grad, x2.grad)
         torch.testing.assert_close(w.grad, w2.grad, rtol=1e-4, atol=1e-3)
+
+
+def test_word_table_cache_follows_identity_not_address():
+    """word_table_bf16 must not hand a new table the rows of a freed one that sat at the same address
+    (the caching allocator reuses addresses; a data_ptr key did exactly that), and must follow in-place
+    updates (version counter)."""
+    import gc
+    from induction_network_on_fewrel_amd.ops.wide import word_table_bf16
+    for i in range(4):
+        a = torch.full((50, 8), float(i + 1))
+        ta = word_table_bf16(a)
+        assert torch.equal(ta.float(), a)
+        del a, ta
+        gc.collect()
+        b = torch.full((50, 8), -float(i + 1))   # same shape, version 0, likely the same storage address
+        assert torch.equal(word_table_bf16(b).float(), b)
+        b.mul_(2.0)
+        assert torch.equal(word_table_bf16(b).float(), b)
