@@ -186,6 +186,18 @@ def main():
     rank_ms = [round(1000 * float(x) / args.steps, 3) for x in dist.all_gather_objects(dt_rank)]
     dt = dist.max_scalar(dt_rank)
     loss = float(loss_t) if loss_t is not None else float("nan")
+    # per-phase GPU time (HIP events at the phase boundaries of the eager train step: device sampling,
+    # forward + backward (incl. the head-span all-reduce overlapped with it), the EXPOSED all-reduce tail,
+    # optimizer), from a few extra steps AFTER the timed region; MAX over ranks per phase
+    phase_ms = None
+    if cuda and not evalm and not tr.graph_step_enabled:
+        tr.cfg = tr.cfg.replace(profile=True)
+        n_prof = max(1, min(5, args.steps))
+        for _ in range(n_prof):
+            tr.train_step_async()
+        sync()
+        ph = tr.drain_phase_events()
+        phase_ms = {k: round(dist.max_scalar(v / n_prof), 3) for k, v in ph.items()}
     in_sync = dist.params_in_sync(tr.flat.flat)
     episodes = args.steps * B * world
     value = episodes / dt
@@ -225,6 +237,7 @@ def main():
             "backend": dist.backend or "none",
             "comm": dist.comm_name,
             "rank_ms_per_step": rank_ms,
+            "phase_ms": phase_ms,
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if cuda else 0.0,
         }
         print(json.dumps(out))

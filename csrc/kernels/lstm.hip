@@ -698,8 +698,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   size_t off = (size_t)(NA + NA2) * sizeof(frag) + 4 * U * sizeof(float);
   off = (off + 15) & ~(size_t)15;
   constexpr int XROWS = GT * 16 + FTMAX * 16;
+  constexpr int NSLP = (U4 + NX + 1) & ~1;               // XH slots per lane: U4 h, NX x (+1 pad)
+  constexpr int FTA = BF16 ? (4 * NSLP + 1 + 15) / 16 : FTMAX;
+  // +4 elements: row stride != 0 mod 32 banks.  (A bank-model stride for the dG image, 92 at GT 5, halves
+  // its modelled transposed-read conflicts but measured neutral, 1420 vs 1413 us.)
+  constexpr int GCP = GT * 16 + 4, FCP = FTA * 16 + 4;
+  // per-wave staging region (elements): FA packs the bf16 images at their exact size (LDS for the attention)
+  constexpr int WSTRIDE = FA ? 32 * (GCP + FCP) : XROWS * RS;
   elem* xp_all = reinterpret_cast<elem*>(smem + off);
-  elem* dgT = xp_all + (size_t)wave * XROWS * RS;
+  elem* dgT = xp_all + (size_t)wave * WSTRIDE;
   elem* xhT = dgT + GT * 16 * RS;
   // bf16 dW staging: a [32 samples][GCP] dG image and a [32 samples][FCP] [x;h;1] image (two steps
   // x 16 sequences), lane-permuted columns so each lane writes its values with a few 8-/4-byte
@@ -707,11 +714,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   // the old [gate row][sample] staging took 20 + 9 ds_write_b16 per step).  Both MFMA operands come
   // back through ds_read_b64_tr_b16 (K = the pair's 32 samples, 16x16x32: the 16x16x16 form with
   // K = one step measured 25% slower, half the MFMA rate).
-  constexpr int NSLP = (U4 + NX + 1) & ~1;               // XH slots per lane: U4 h, NX x (+1 pad)
-  constexpr int FTA = BF16 ? (4 * NSLP + 1 + 15) / 16 : FTMAX;
-  // +4 elements: row stride != 0 mod 32 banks.  (A bank-model stride for the dG image, 92 at GT 5, halves
-  // its modelled transposed-read conflicts but measured neutral: tools/gpu_ab_gcp.sh, 1420 vs 1413 us.)
-  constexpr int GCP = GT * 16 + 4, FCP = FTA * 16 + 4;
   static_assert(!BF16 || 32 * (GCP + FCP) <= XROWS * RS, "bf16 dW images exceed the staging region");
   unsigned short* dgI = reinterpret_cast<unsigned short*>(dgT);
   unsigned short* xhI = dgI + 32 * GCP;
@@ -719,7 +721,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   using FS = FAS<U>;
   {
     // FA: the bf16 images at their exact size (the region also holds the final reductions)
-    size_t xp = FA ? (size_t)4 * 32 * (GCP + FCP) * 2 : (size_t)4 * XROWS * RS * sizeof(elem);
+    size_t xp = (size_t)4 * WSTRIDE * sizeof(elem);
     const size_t red = (size_t)G4 * (4 * NX + U + 1) * sizeof(float) + (FA ? (size_t)FS::NSA * 4 + 16 : 0);
     off += xp > red ? xp : red;
   }
@@ -751,7 +753,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     for (int i = threadIdx.x; i < 2 * P2 * PD; i += 256) dpos_lds[i] = 0.f;
   const int NPF = 2 * PD;   // pos features (bf16 mode: exported to dxp, reduced by pos_grad_kernel)
   // zero the wave's transpose buffers once (pad rows / columns stay zero; bias row = 1)
-  for (int i = lane; i < XROWS * RS; i += 64) dgT[i] = to_elem(0.f, (elem*)nullptr);
+  for (int i = lane; i < WSTRIDE; i += 64) dgT[i] = to_elem(0.f, (elem*)nullptr);
   wave_lds_sync();
   if constexpr (BF16) {
     if (lane < 32) xhI[lane * FCP + 4 * NSLP] = f2bf(1.f);   // bias column

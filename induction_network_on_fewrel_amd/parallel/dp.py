@@ -33,6 +33,7 @@ def _native_op(op) -> str:
             return {"MAX": "max", "MIN": "min", "PRODUCT": "prod"}[name]
     raise ValueError(f"native communicator: unsupported reduce op {op}")
 
+
 class DistContext:
     def __init__(self, rank: int = 0, world: int = 1, local_rank: int = 0, device: Optional[torch.device] = None,
                  backend: Optional[str] = None):

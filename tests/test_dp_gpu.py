@@ -5,7 +5,9 @@ RCCL refuses two ranks on the same device, so the collective backend here is glo
 rank, rank-folded device sampling, the fused kernels writing the flat gradient, the bucketed
 all-reduce + 1/world scaling inside the timed step, the fused Adam, the MAX-over-ranks timing and
 the rank-0 JSON line.  The check is that parameters stay bitwise identical across ranks
-(``params_in_sync``) for the eager step and for the HIP-graph step (all-reduce outside the graph).
+(``params_in_sync``) for the eager step and for the HIP-graph step (all-reduce outside the graph), and --
+the ground truth -- that the all-reduced fused-step gradient / world equals one step over the union of the
+ranks' episodes (tests/dp_grad_check.py).
 """
 import json
 import os
@@ -123,3 +125,36 @@ def test_native_comm_collectives_world1():
         c.sync()
     finally:
         c.destroy()
+
+
+def _dp_check(nproc, extra_env):
+    env = dict(os.environ, OMP_NUM_THREADS="2", **extra_env)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "tests", "dp_grad_check.py")]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=140)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    rows = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(rows) == nproc, r.stdout
+    for row in rows:
+        print(row["rank"], row["comm"], f"{row['max_rel_err']:.2e}")
+        assert row["finite"] and row["world"] == nproc and row["episodes_union"] == nproc * 384
+        assert row["max_rel_err"] < 1e-3, row["per_param"]   # fp32 reduction order + bf16 rounding of the loss gradient
+    return rows
+
+
+def test_dp_gradient_equals_union_step_world2_gloo():
+    """SURVEY 7.4 on the fused GPU path: two ranks on one card (gloo collectives on CUDA tensors), the
+    relation-head span all-reduced under the encoder backward, slabs scattered by the step glue."""
+    _dp_check(2, dict(INA_DIST_BACKEND="gloo"))
+
+
+@pytest.mark.parametrize("comm", ["nccl", "native"])
+def test_dp_gradient_equals_union_step_world1(comm):
+    """The RCCL data planes (torch "nccl" and the native C++ communicator) at world 1: the in-place
+    all-reduce of the overlapped head span must not write a stale bucket back over the flushed gradient."""
+    env = dict(INA_FORCE_DIST="1")
+    if comm == "native":
+        env["INA_COMM"] = "native"
+    os.environ.pop("INA_DIST_BACKEND", None)
+    rows = _dp_check(1, env)
+    assert rows[0]["comm"] == ("rccl-native" if comm == "native" else "nccl")

@@ -350,10 +350,18 @@ def test_fused_attention_backward_matches_split(keep_prob, u, skip, monkeypatch)
         out.append((e.detach(), {k: v.grad for k, v in p.items() if v.grad is not None}))
     (e0, g0), (e1, g1) = out
     assert torch.equal(e0, e1)
-    for k in g0:
-        err = _relerr(g1[k], g0[k])
-        print(f"  fused u={u} kp={keep_prob} skip={skip} grad {k}: {err:.2e}")
-        assert torch.isfinite(g1[k]).all() and err < 1e-2, k
+    errs = {k: _relerr(g1[k], g0[k]) for k in g0}
+    print(f"  fused u={u} kp={keep_prob} skip={skip}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+    for k, v in errs.items():
+        assert torch.isfinite(g1[k]).all() and v < 1e-2, k
+
+
+@pytest.mark.parametrize("u", [8, 20, 32])
+@pytest.mark.parametrize("keep_prob", [1.0, 0.9])
+def test_fused_encoder_backward_vs_oracle(keep_prob, u, monkeypatch):
+    """The fused attention backward against the fp32 oracle (same bounds as test_encoder_backward)."""
+    monkeypatch.setenv("INA_FUSE_ATTN_BWD", "1")
+    test_encoder_backward("bf16", keep_prob, u)
 
 
 @pytest.mark.parametrize("L", [24, 1, 2])

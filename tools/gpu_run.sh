@@ -1,6 +1,6 @@
 # One parametrised GPU-box script (replaces the round-3 one-off lease scripts).
 # usage (on the box, from the repo root):
-#   TESTS="<pytest args>"                      GPU tests (empty: none)
+#   TESTS="<pytest paths / args>"              GPU tests (empty: none); TESTS_K="<-k expression>" (may hold spaces)
 #   BENCH="name|ENV=V ...|bench args;..."      bench.py runs, each with its own env assignments (empty: none)
 #   PROF="name|ENV=V ...|bench args;..."       rocprofv3 --kernel-trace --stats runs of bench.py, summarised by
 #                                              tools/rocpd_summary.py into OUT/<name>_sum.txt
@@ -11,7 +11,11 @@ OUT=${1:-gpurun_out/run}
 ROOT=$PWD
 mkdir -p $OUT
 if [ -n "$TESTS" ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest $TESTS -x -v --timeout 150 --timeout-method thread > $OUT/tests.log 2>&1
+  if [ -n "$TESTS_K" ]; then
+    timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest $TESTS -k "$TESTS_K" -x -v --timeout 150 --timeout-method thread > $OUT/tests.log 2>&1
+  else
+    timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest $TESTS -x -v --timeout 150 --timeout-method thread > $OUT/tests.log 2>&1
+  fi
   rc=$?; echo "tests rc=$rc"; tail -3 $OUT/tests.log
   [ $rc -ne 0 ] && exit $rc
 fi

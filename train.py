@@ -36,6 +36,10 @@ def build_parser():
     p.add_argument("--fold", type=int, default=-1,
                    help="with --split_val (relation mode): hold out relations 5*fold .. 5*fold+4 (JSON order, "
                         "wrapping) and train on the rest -- rotating folds for mean +- std accuracy")
+    p.add_argument("--val_relations", type=int, default=0,
+                   help="with --fold: a THIRD relation-disjoint block -- the V relations after the held-out test "
+                        "block (JSON order, wrapping) are the validation set that selects the checkpoint "
+                        "(--test_best), the fold's 5 relations are only tested, the rest train")
     p.add_argument("--split_mode", default="relation", choices=["relation", "instance"],
                    help="with --split_val: 'relation' = disjoint relations (few-shot transfer); 'instance' = "
                         "every relation in both halves, disjoint sentences (train_fraction of each relation)")
@@ -75,6 +79,15 @@ def load_data(cfg: Config, args):
                     full.subset_relations(rels, "val_split", part=(f, 1.0)))
         if getattr(args, "fold", -1) >= 0:   # rotate: the held-out block of 5 relations goes last
             test = [rels[(5 * args.fold + i) % len(rels)] for i in range(5)]
+            nv = getattr(args, "val_relations", 0)
+            if nv > 0:   # train / val / test, all relation-disjoint: val selects, test only tests
+                val = [rels[(5 * args.fold + 5 + i) % len(rels)] for i in range(nv)]
+                train = [r for r in rels if r not in test and r not in val]
+                print(f"fold {args.fold}: train {len(train)} relations, val {val}, test {test}", flush=True)
+                if cfg.encoder == "bert":
+                    raise SystemExit("--val_relations is implemented for the BiLSTM encoder")
+                args._test_split = full.subset_relations(test, "test_split")
+                return full.subset_relations(train, "train_split"), full.subset_relations(val, "val_split")
             rels = [r for r in rels if r not in test] + test
             half = len(rels) - 5
             print(f"fold {args.fold}: held-out relations {test}", flush=True)
@@ -130,7 +143,7 @@ def main(argv=None):
         raise SystemExit(f"unknown model {cfg.model_name!r} (only 'induction')")
     from induction_network_on_fewrel_amd.runtime.trainer import Trainer
     tr_data, va_data = load_data(cfg, args)
-    te_data = load_test(cfg, tr_data) if cfg.test_file else None
+    te_data = load_test(cfg, tr_data) if cfg.test_file else getattr(args, "_test_split", None)
     trainer = Trainer(cfg, tr_data, va_data, device=cfg.device, test_data=te_data)
     if args.eval_only:
         acc = trainer.evaluate(cfg.test_iter)
