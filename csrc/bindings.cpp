@@ -9,9 +9,14 @@
 #include <hip/hip_runtime.h>
 #include <torch/library.h>
 
+#include <cstdlib>
 #include <tuple>
 
 #include "ina_launch.h"
+
+#ifndef INA_POS_LDS_DEFAULT
+#define INA_POS_LDS_DEFAULT false
+#endif
 
 namespace {
 
@@ -58,6 +63,11 @@ const int* ragged_arg(const std::optional<Tensor>& t, int64_t n, const char* nam
 }
 
 int64_t frag_elems(bool bf16) { return bf16 ? 8 : 1; }
+// LDS position-table gradients in lstm_bwd (shifted ids): INA_POS_LDS=0 disables (A/B, tests)
+bool pos_lds_enabled() {
+  const char* v = std::getenv("INA_POS_LDS");
+  return v == nullptr ? INA_POS_LDS_DEFAULT : (v[0] != '0');
+}
 uint32_t keep_threshold(double kp) {
   const double t = kp * 4294967296.0;
   return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
@@ -332,6 +342,10 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
   const int64_t NSLOT = U4 + NX;
   TORCH_CHECK(a2pack.numel() == 2 * ((NSLOT + 3) / 4) * ((4 * U4 + KPL - 1) / KPL) * 64 * KPL, "ina.lstm_bwd: a2pack");
   TORCH_CHECK(ina::lstm_bwd_lds_bytes((int)U, (int)NX, bf16, (int)L, (int)PD) <= 160 * 1024, "ina.lstm_bwd: LDS budget");
+  // shifted position ids on the lean bf16 BPTT: the position-table gradients are summed in LDS inside lstm_bwd
+  const bool pos_lds = bf16 && pos_shift && (dh_lane || fa != nullptr) && pos_lds_enabled();
+  TORCH_CHECK(!pos_lds || ina::lstm_bwd_lds_bytes((int)U, (int)NX, bf16, (int)L, (int)PD, fa != nullptr, true) <= 160 * 1024,
+              "ina.lstm_bwd: LDS budget (position tables)");
   const int64_t ngroups = ((S + 15) / 16 + 3) / 4;
   // 512 workgroups per direction: ~2 rounds of 3-4 tile groups each, back-filled by the dispatcher.
   // (A grid of exactly the resident workgroups, ina::lstm_bwd_resident_blocks, measured slower:
@@ -346,11 +360,13 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
   const int64_t pblocks = std::max<int64_t>(1, std::min<int64_t>(1024, (pitems + 31) / 32));
   if (bf16) TORCH_CHECK(2 * PD <= 16 && 2 * L <= 128, "ina.lstm_bwd: bf16 path needs pos_dim <= 8 and L <= 64");
   // pos_shift (caller-checked pos[s][t] = pos[s][0] + t, pos[s][0] <= L): per-sequence one-hot GEMM -> ONE slab
-  const bool shift = bf16 && pos_shift && (L + 1 + 15) / 16 <= 5;
+  const bool shift = bf16 && pos_shift && (L + 1 + 15) / 16 <= 5 && !pos_lds;
   auto dpos_slab = shift ? at::empty({1, 1, 2, 2 * L, PD}, opt)
-                         : (bf16 ? at::empty({pblocks, 1, 2, 2 * L, PD}, opt) : at::empty({blocks, 2, 2, 2 * L, PD}, opt));
+                         : ((bf16 && !pos_lds) ? at::empty({pblocks, 1, 2, 2 * L, PD}, opt)
+                                               : at::empty({blocks, 2, 2, 2 * L, PD}, opt));
   // [2 dir][tiles][L][2PD + 1][16] bf16 dx of the pos features (+ a trash row for the other lanes)
-  Tensor dxp = bf16 ? at::empty({2 * (2 * PD + 1) * ntiles * L * 16}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
+  Tensor dxp = (bf16 && !pos_lds) ? at::empty({2 * (2 * PD + 1) * ntiles * L * 16}, opt.dtype(at::kBFloat16))
+                                  : at::empty({0}, opt);
   if (bf16) {
     check(xg, "xg", at::kBFloat16);
     TORCH_CHECK(xg.numel() == ntiles * L * (64 * NX + 16), "ina.lstm_bwd: xg (from lstm_fwd) shape");
@@ -393,7 +409,8 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
   a.thr = keep_threshold(keep_prob);
   a.inv_kp = (float)(1.0 / keep_prob);
   a.drop = keep_prob < 1.0 ? 1 : 0;
-  a.dxp = bf16 ? dxp.data_ptr() : nullptr;
+  a.dxp = (bf16 && !pos_lds) ? dxp.data_ptr() : nullptr;
+  a.pos_lds = pos_lds ? 1 : 0;
   a.dh_lane = dh_lane ? 1 : 0;
   a.tlen = ragged_arg(tlen, ntiles, "tlen");
   a.slen = ragged_arg(slen, S, "slen");
@@ -436,7 +453,7 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
     Tensor gpart = at::empty({(int64_t)ina::pos_shift_workspace_floats((int)S, (int)L, (int)PD, nullptr, nullptr)}, opt);
     check_launch(ina::pos_grad_shift(a, gpart.data_ptr<float>(), dpos_slab.data_ptr<float>(), cur_stream()),
                  "pos_grad_shift");
-  } else if (bf16) {
+  } else if (bf16 && !pos_lds) {
     check_launch(ina::pos_grad(a, (int)pblocks, dpos_slab.data_ptr<float>(), cur_stream()), "pos_grad");
   }
   return {dw_slab, dpos_slab, dwemb, aslab};

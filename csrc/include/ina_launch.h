@@ -59,6 +59,9 @@ struct LstmArgs {
   const float* ae;
   const float* aalphas;
   float* aslab;
+  // bf16 lean BPTT with shifted position ids (pos[s][t] = pos[s][0] + t): the position-table gradients are
+  // summed in LDS inside lstm_bwd -> dpos_slab [bwd_blocks][2 dir][2 tables][2L][PD] (no dxp, no pos_grad)
+  int pos_lds;
 };
 // bf16 mode: gather every token's x features once into a.xg / a.posb, and (a.drop) the dropout keep
 // bits into a.dmask (lstm.hip x_gather_kernel); must run before lstm_fwd in bf16 mode
@@ -77,7 +80,7 @@ int pos_grad(const LstmArgs& a, int blocks, float* slab, hipStream_t st);
 size_t pos_shift_workspace_floats(int S, int L, int PD, int* nchunk, int* kps);
 int pos_grad_shift(const LstmArgs& a, float* gpart, float* out, hipStream_t st);
 bool lstm_supported(int U, int NX);
-size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fused_attn = false);
+size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fused_attn = false, bool pos_lds = false);
 
 struct AttnArgs {
   const void* hraw;

@@ -643,9 +643,12 @@ __global__ __launch_bounds__(256) void h_natural_kernel(const unsigned short* __
 // [tiles][2][L][U4][64] (rec_attn_bwd: coalesced 128-B rows per (step, m))
 // 2 waves/SIMD where the register set fits in 256 without spilling (the default u=20 / 5-d words
 // case); the wider instantiations keep 1 wave and no spills
-template <int U, int NX>
+#ifndef INA_FA_WAVES
+#define INA_FA_WAVES 2   // fused attention backward: waves per SIMD (2 spills ~100 dwords at u = 20; 1 does not)
+#endif
+template <int U, int NX, bool FA = false>
 struct BwdWaves {
-  static constexpr int value = (U <= 20 && NX == 4) ? 2 : 1;
+  static constexpr int value = (U <= 20 && NX == 4) ? (FA ? INA_FA_WAVES : 2) : 1;
 };
 // WG: trained word table (word-row gradients by global atomics).  A template flag rather than a
 // runtime branch: the join after a skipped atomic block made LLVM drain every outstanding load
@@ -654,8 +657,12 @@ struct BwdWaves {
 // scale (rec_attn_bwd), and the BPTT runs the lean step below (raw bf16 operands, no keep bits, no
 // per-lane validity selects, uniform per-step addresses).
 // FA (with PM): the attention backward runs inside the BPTT (AttnFuse above); dH is not an input.
-template <int U, int NX, bool BF16, bool WG = false, bool PM = false, bool FA = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U, NX>::value))) void lstm_bwd_kernel(
+// PL (with PM): position ids are shifted aranges (pos[s][t] = o_s + t, host-checked): each wave adds its
+// pos-feature gradients into its own LDS copy of the two position tables (ds_add_f32 at o_s + t), summed
+// over the workgroup's waves in a fixed order into dpos_slab [blocks][2 dir][2 tables][2L][PD] -- no
+// per-token dx rows in HBM and no separate reduction kernel.
+template <int U, int NX, bool BF16, bool WG = false, bool PM = false, bool FA = false, bool PL = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U, NX, FA>::value))) void lstm_bwd_kernel(
     const int* __restrict__ inst, int S, const int* __restrict__ word, const int* __restrict__ pos1,
     const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
     const float* __restrict__ p1emb, const float* __restrict__ p2emb, int PD,
@@ -667,6 +674,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     uint32_t thr, float inv_kp, int drop, unsigned short* __restrict__ dxp, const unsigned short* __restrict__ xg,
     int dh_lane, const int* __restrict__ tlen, const int* __restrict__ slen, int wblank, AttnFuse af) {
   static_assert(!FA || (BF16 && PM), "the fused attention backward runs in the lean bf16 BPTT");
+  static_assert(!PL || (BF16 && PM), "LDS position-table gradients run in the lean bf16 BPTT");
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
   using elem = typename FragT<BF16>::elem;
@@ -733,6 +741,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   float* lbw = reinterpret_cast<float*>(lApt + FS::NAPT);
   unsigned short* ahI = reinterpret_cast<unsigned short*>(lbw + 2 * FS::MT * 16) + (size_t)wave * (FS::IMG / 2);
   unsigned short* apI = ahI + 16 * FS::HCPA;
+  // PL: per-wave position tables [2 tables][2L][PD] + a trash block [L][PD] (word / padding lanes)
+  const int PLT = 2 * (2 * L) * PD, PLN = PLT + L * PD;
+  const size_t pl_off = (off + (FA ? (size_t)(FS::NAP + FS::NAPT) * 16 + 2 * FS::MT * 16 * 4 + 4 * (size_t)FS::IMG : 0) +
+                         15) & ~(size_t)15;
+  float* plAll = reinterpret_cast<float*>(smem + pl_off);
+  float* plR = plAll + (size_t)wave * PLN;
+  if constexpr (PL)
+    for (int i = lane; i < PLN; i += 64) plR[i] = 0.f;
   if constexpr (FA) {
     for (int i = threadIdx.x; i < FS::NAP; i += 256) lAp[i] = af.w1f[(size_t)dir * FS::NAP + i];
     for (int i = threadIdx.x; i < FS::NAPT; i += 256) lApt[i] = af.w1ft[(size_t)dir * FS::NAPT + i];
@@ -1036,6 +1052,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       const auto rx = rsrc(xg + (size_t)tu * L * 64 * NX, (uint32_t)L * XSTEPB);
       const auto rdx = rsrc(dxp + ((size_t)dir * ntiles + tu) * L * (NPF + 1) * 16, (uint32_t)L * PSTEPB);
       const int vl2 = lane * 2, vx = lane * NX * 2;
+      // ---- PL: the lane's position-table slot at t = 0 per x feature (shifted ids: pos = o + t); word /
+      // padding features and padding rows go to the trash block
+      int plb[NX];
+      if constexpr (PL) {
+        const int o1 = pos1[rowbase], o2 = pos2[rowbase];
+#pragma unroll
+        for (int xi = 0; xi < NX; ++xi) {
+          const int sel = xs[xi].sel;
+          plb[xi] = (valid && sel == 1) ? o1 * PD + xs[xi].col
+                    : (valid && sel == 2) ? (2 * L + o2) * PD + xs[xi].col : PLT;
+        }
+      }
       // ---- FA: per-tile attention state (de of the lane's slots, sd = de . e) and buffer descriptors
       const int orow = FA ? (af.perm ? af.perm[seqc] : (int)seqc) : 0;   // e / de / alphas row
       float dev[FS::NV];   // de of slots [own ; other] (0 for padding rows)
@@ -1310,13 +1338,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
             dc_rec[m] *= k;
           }
         }
-        // pos-feature gradients -> dxp rows (word / padding features: the trash row)
-        const int sp = t * PSTEPB;
+        if constexpr (PL) {   // pos-feature gradients into the wave's LDS position tables (fp32)
+          const int tp = t * PD;
 #pragma unroll
-        for (int xi = 0; xi < NX; xi += 2) {
-          const uint32_t w = pkf(dslot[U4 + xi], xi + 1 < NX ? dslot[U4 + xi + 1] : 0.f);
-          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)w, rdx, 2 * pofs[xi], sp, 0);
-          if (xi + 1 < NX) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(w >> 16), rdx, 2 * pofs[xi + 1], sp, 0);
+          for (int xi = 0; xi < NX; ++xi)
+            __hip_atomic_fetch_add(plR + plb[xi] + tp, dslot[U4 + xi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {   // pos-feature gradients -> dxp rows (word / padding features: the trash row)
+          const int sp = t * PSTEPB;
+#pragma unroll
+          for (int xi = 0; xi < NX; xi += 2) {
+            const uint32_t w = pkf(dslot[U4 + xi], xi + 1 < NX ? dslot[U4 + xi + 1] : 0.f);
+            __builtin_amdgcn_raw_buffer_store_b16((unsigned short)w, rdx, 2 * pofs[xi], sp, 0);
+            if (xi + 1 < NX) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(w >> 16), rdx, 2 * pofs[xi + 1], sp, 0);
+          }
         }
         if constexpr (WG) {   // trained word table: global atomics
           if (valid) {
@@ -1373,7 +1407,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       const int nst = tau_start - tau_end + 1;
       // dxp rows of the steps not processed: zero (the pos-gradient reduction reads every step)
       for (int t = Lt; t < L; ++t) {
-        if (dir == 1 && slen == nullptr) break;
+        if (PL || (dir == 1 && slen == nullptr)) break;
 #pragma unroll
         for (int xi = 0; xi < NX; ++xi)
           __builtin_amdgcn_raw_buffer_store_b16((unsigned short)0, rdx, 2 * pofs[xi], t * PSTEPB, 0);
@@ -1649,6 +1683,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   });
   float* slab = dw_slab + ((size_t)blockIdx.x * 2 + dir) * REDN;
   for (int i = threadIdx.x; i < REDN; i += 256) slab[i] = red[i];
+  if constexpr (PL) {   // the 4 waves' position tables, summed in a fixed order (barriers above)
+    float* ps = dpos_slab + ((size_t)blockIdx.x * 2 + dir) * PLT;
+    for (int i = threadIdx.x; i < PLT; i += 256)
+      ps[i] = (plAll[i] + plAll[PLN + i]) + (plAll[2 * PLN + i] + plAll[3 * PLN + i]);
+  }
   if constexpr (FA) {
     float* as = af.slab + ((size_t)blockIdx.x * 2 + dir) * FS::NSA;
     for (int i = threadIdx.x; i < FS::NSA; i += 256) as[i] = ared[i];
@@ -1871,7 +1910,7 @@ namespace ina {
 
 
 // mirrors the kernel's LDS carve (lstm_bwd_kernel)
-size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fa) {
+size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fa, bool pl) {
   const int KPL = bf16 ? 8 : 1;
   const int U4 = U / 4, NSLOT = U4 + NX;
   const int NA = U4 * ((NSLOT + KPL - 1) / KPL) * 64;
@@ -1894,6 +1933,8 @@ size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fa) {
   off = (off + 15) & ~(size_t)15;
   if (!bf16) off += (size_t)2 * 2 * L * PD * 4;   // block pos tables (bf16 mode: pos_grad_kernel)
   if (fa) off += (size_t)(MT * NKR * 64 + NTD * NKS2 * 64) * 16 + 2 * MT * 16 * 4 + (size_t)4 * 16 * (HCPA + JCPA) * 2;
+  off = (off + 15) & ~(size_t)15;
+  if (pl) off += (size_t)4 * (2 * 2 * L * PD + L * PD) * 4;   // per-wave position tables + trash block
   return off;
 }
 
@@ -1927,15 +1968,22 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   // bf16 + lane-layout dH (rec_attn_bwd, premasked): the lean PM step; fa: the attention backward fused in
   const bool fa = BF16 && a.aslab != nullptr;
   const bool pm = INA_LSTM_PM && BF16 && (a.dh_lane || fa);
-  size_t lds = lstm_bwd_lds_bytes(U, NX, BF16, a.L, a.PD, fa);
-  auto kfn = pm ? (a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, BF16> : lstm_bwd_kernel<U, NX, BF16, false, BF16>)
+  const bool pl = pm && a.pos_lds;
+  size_t lds = lstm_bwd_lds_bytes(U, NX, BF16, a.L, a.PD, fa, pl);
+  constexpr bool P = BF16;   // the PM / FA / PL kernels exist in bf16 mode only
+  auto kfn = pm ? (a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, P> : lstm_bwd_kernel<U, NX, BF16, false, P>)
                 : (a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, false> : lstm_bwd_kernel<U, NX, BF16, false, false>);
-  if (fa) kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, BF16, BF16> : lstm_bwd_kernel<U, NX, BF16, false, BF16, BF16>;
+  if (fa) kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, P, P> : lstm_bwd_kernel<U, NX, BF16, false, P, P>;
+  if (pl && !fa)
+    kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, P, false, P> : lstm_bwd_kernel<U, NX, BF16, false, P, false, P>;
+  if (pl && fa) kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, P, P, P> : lstm_bwd_kernel<U, NX, BF16, false, P, P, P>;
   static bool attr_set = false;
   if (!attr_set) {
     for (auto f : {lstm_bwd_kernel<U, NX, BF16, true, false>, lstm_bwd_kernel<U, NX, BF16, false, false>,
-                   lstm_bwd_kernel<U, NX, BF16, true, BF16>, lstm_bwd_kernel<U, NX, BF16, false, BF16>,
-                   lstm_bwd_kernel<U, NX, BF16, true, BF16, BF16>, lstm_bwd_kernel<U, NX, BF16, false, BF16, BF16>})
+                   lstm_bwd_kernel<U, NX, BF16, true, P>, lstm_bwd_kernel<U, NX, BF16, false, P>,
+                   lstm_bwd_kernel<U, NX, BF16, true, P, P>, lstm_bwd_kernel<U, NX, BF16, false, P, P>,
+                   lstm_bwd_kernel<U, NX, BF16, true, P, false, P>, lstm_bwd_kernel<U, NX, BF16, false, P, false, P>,
+                   lstm_bwd_kernel<U, NX, BF16, true, P, P, P>, lstm_bwd_kernel<U, NX, BF16, false, P, P, P>})
       hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
@@ -1954,8 +2002,8 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(kfn, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, (const frag*)a.a2pack, a.bias,
                      (const elem*)a.hraw, (const typename CT<BF16>::type*)a.cst, (const elem*)a.dH, a.dw_slab, a.dpos_slab, a.dwemb, a.dmask, a.seed, a.thr, a.inv_kp,
-                     a.drop, (unsigned short*)a.dxp, (const unsigned short*)a.xg, a.dh_lane, pm ? a.tlen : nullptr,
-                     pm ? a.slen : nullptr, a.wblank, af);
+                     a.drop, pl ? nullptr : (unsigned short*)a.dxp, (const unsigned short*)a.xg, a.dh_lane,
+                     pm ? a.tlen : nullptr, pm ? a.slen : nullptr, a.wblank, af);
   INA_CHECK_LAUNCH();
   return 0;
 }

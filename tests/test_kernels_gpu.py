@@ -364,6 +364,37 @@ def test_fused_encoder_backward_vs_oracle(keep_prob, u, monkeypatch):
     test_encoder_backward("bf16", keep_prob, u)
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
+@pytest.mark.parametrize("skip", [False, True])
+@pytest.mark.parametrize("u", [8, 20, 32])
+def test_pos_lds_matches_dxp_path(u, skip, fused, monkeypatch):
+    """Position-table gradients summed in LDS inside lstm_bwd (shifted ids, ds_add_f32 per wave, fixed-order
+    workgroup sum) against the per-token dx rows + one-hot GEMM reduction; all other gradients bitwise equal."""
+    from induction_network_on_fewrel_amd.ops.encoder import encode
+    cfg, data, model, dd, inst, _ = _problem(dtype="bf16", u=u, B=7)
+    assert dd.pos_shift
+    monkeypatch.setenv("INA_FUSE_ATTN_BWD", fused)
+    out = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("INA_POS_LDS", on)
+        p = {k: v.detach().clone().requires_grad_(v.requires_grad) for k, v in model.pdict().items()}
+        meta = dict(U=cfg.hidden_size, bf16=True, keep_prob=0.9, seed=5, word_grad=False, ragged_min_rows=0,
+                    skip_padding=skip)
+        e, _ = encode(inst, dd.arrays(), p, meta)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        (e * torch.randn(e.shape, generator=g, device="cuda")).sum().backward()
+        torch.cuda.synchronize()
+        out.append({k: v.grad for k, v in p.items() if v.grad is not None})
+    g0, g1 = out
+    for k in g0:
+        err = _relerr(g1[k], g0[k])
+        print(f"  pos-lds u={u} skip={skip} fused={fused} {k}: {err:.2e}")
+        if k.startswith("pos"):
+            assert err < 1e-2, k
+        else:
+            assert torch.equal(g1[k], g0[k]), k
+
+
 @pytest.mark.parametrize("L", [24, 1, 2])
 def test_encoder_backward_short_and_even_L(L):
     """even L and the 1- and 2-step edge cases of the recurrences' peeled loops."""
