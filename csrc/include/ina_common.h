@@ -49,6 +49,17 @@ INA_DEVICE f32x4_t mfma16_bf16(const s16x4_t& a, const s16x4_t& b, const f32x4_t
 INA_DEVICE s16x4_t tr_read(const unsigned short* lds_addr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)lds_addr);
 }
+// 16x16x32 operand fragment from a row-major LDS image [k rows][cols] (two ds_read_b64_tr_b16):
+// element j of lane (q = l >> 4, n = l & 15) = image[8 q + j][c0 + n] -- the B operand B[k][c0 + n], or
+// the A operand A[c0 + n][k] of the transposed block.  stride (elements) * 2 and c0 * 2 must be 8-byte
+// multiples; EXEC must be all ones.
+INA_DEVICE u16x8_t tr_read8(const unsigned short* img, int stride, int c0, int q, int n) {
+  const s16x4_t lo = tr_read(img + (8 * q + (n >> 2)) * stride + c0 + 4 * (n & 3));
+  const s16x4_t hi = tr_read(img + (8 * q + 4 + (n >> 2)) * stride + c0 + 4 * (n & 3));
+  return u16x8_t{(unsigned short)lo[0], (unsigned short)lo[1], (unsigned short)lo[2], (unsigned short)lo[3],
+                 (unsigned short)hi[0], (unsigned short)hi[1], (unsigned short)hi[2], (unsigned short)hi[3]};
+}
+
 // order this wave's LDS accesses without a memory fence: a wave's own LDS operations execute in
 // order in hardware, and a fence would also wait for every in-flight global load (vmcnt(0))
 INA_DEVICE void lds_order() {

@@ -741,8 +741,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   float* lbw = reinterpret_cast<float*>(lApt + FS::NAPT);
   unsigned short* ahI = reinterpret_cast<unsigned short*>(lbw + 2 * FS::MT * 16) + (size_t)wave * (FS::IMG / 2);
   unsigned short* apI = ahI + 16 * FS::HCPA;
-  // PL: per-wave position tables [2 tables][2L][PD] + a trash block [L][PD] (word / padding lanes)
-  const int PLT = 2 * (2 * L) * PD, PLN = PLT + L * PD;
+  // PL: per-wave position tables [2 tables][2L][PD] + a trash block of 64 per-lane slots (word / padding lanes)
+  const int PLT = 2 * (2 * L) * PD, PLN = PLT + 64;
   const size_t pl_off = (off + (FA ? (size_t)(FS::NAP + FS::NAPT) * 16 + 2 * FS::MT * 16 * 4 + 4 * (size_t)FS::IMG : 0) +
                          15) & ~(size_t)15;
   float* plAll = reinterpret_cast<float*>(smem + pl_off);
@@ -1054,14 +1054,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       const int vl2 = lane * 2, vx = lane * NX * 2;
       // ---- PL: the lane's position-table slot at t = 0 per x feature (shifted ids: pos = o + t); word /
       // padding features and padding rows go to the trash block
-      int plb[NX];
+      // (a shared trash address made every instruction a ~25-way same-address LDS atomic: each lane has its
+      // own trash slot, and plm = 0 keeps it fixed over the steps)
+      int plb[NX], plm[NX];
       if constexpr (PL) {
         const int o1 = pos1[rowbase], o2 = pos2[rowbase];
 #pragma unroll
         for (int xi = 0; xi < NX; ++xi) {
           const int sel = xs[xi].sel;
-          plb[xi] = (valid && sel == 1) ? o1 * PD + xs[xi].col
-                    : (valid && sel == 2) ? (2 * L + o2) * PD + xs[xi].col : PLT;
+          const bool pos = valid && (sel == 1 || sel == 2);
+          plb[xi] = pos ? (sel == 1 ? o1 : 2 * L + o2) * PD + xs[xi].col : PLT + lane;
+          plm[xi] = pos ? 1 : 0;
         }
       }
       // ---- FA: per-tile attention state (de of the lane's slots, sd = de . e) and buffer descriptors
@@ -1342,7 +1345,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
           const int tp = t * PD;
 #pragma unroll
           for (int xi = 0; xi < NX; ++xi)
-            __hip_atomic_fetch_add(plR + plb[xi] + tp, dslot[U4 + xi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(plR + plb[xi] + plm[xi] * tp, dslot[U4 + xi], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
         } else {   // pos-feature gradients -> dxp rows (word / padding features: the trash row)
           const int sp = t * PSTEPB;
 #pragma unroll
@@ -1934,7 +1938,7 @@ size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fa, bool
   if (!bf16) off += (size_t)2 * 2 * L * PD * 4;   // block pos tables (bf16 mode: pos_grad_kernel)
   if (fa) off += (size_t)(MT * NKR * 64 + NTD * NKS2 * 64) * 16 + 2 * MT * 16 * 4 + (size_t)4 * 16 * (HCPA + JCPA) * 2;
   off = (off + 15) & ~(size_t)15;
-  if (pl) off += (size_t)4 * (2 * 2 * L * PD + L * PD) * 4;   // per-wave position tables + trash block
+  if (pl) off += (size_t)4 * (2 * 2 * L * PD + 64) * 4;   // per-wave position tables + per-lane trash slots
   return off;
 }
 

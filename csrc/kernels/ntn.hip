@@ -64,6 +64,11 @@ constexpr f32x4_t Z4 = {0.f, 0.f, 0.f, 0.f};
 #ifndef INA_NTN_BWD_LD
 #define INA_NTN_BWD_LD 1   // branch-free vectorized prologue loads in ntn_bwd (153 vs 160 us despite 188 B of spills; 0 = the branchy per-element loads)
 #endif
+#ifndef INA_NTN_TR
+#define INA_NTN_TR 1   // ntn_bwd: P^T -> P, T -> T^T and dT -> dT^T through wave-private LDS images read back with
+                       // ds_read_b64_tr_b16, instead of recomputing each product in the other layout (37 -> 25 MFMAs
+                       // per slice and episode)
+#endif
 #ifndef INA_NTN_WAVES
 #define INA_NTN_WAVES 8   // episodes (waves) per workgroup sharing one staged copy of the slice packs
 // (4 episodes: ntn_bwd 574 -> 641 us with two workgroups per CU -- twice the pack staging -- and 1120 us
@@ -272,6 +277,7 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(2))
         }
     // Q^T as the A operand over queries: A[i = b][k = query (kmap32)]
     __builtin_amdgcn_sched_barrier(0);   // load groups in turn: bounded registers in flight
+    // (TR: natural query order k = q -- the dT^T operand then comes from a row-major LDS image)
     u16x8_t QTf[MTH][KQ];
 #pragma unroll
     for (int mb = 0; mb < MTH; ++mb)
@@ -279,7 +285,7 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(2))
       for (int kq = 0; kq < KQ; ++kq)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int b = 16 * mb + n, qi = 32 * kq + kmap32(q, j);
+          const int b = 16 * mb + n, qi = 32 * kq + (INA_NTN_TR ? 8 * q + j : kmap32(q, j));
           QTf[mb][kq][j] = f2bf(ldz(e, qi < NQ && b < H, (rq0 + qi) * H + b));
         }
     __builtin_amdgcn_sched_barrier(0);
@@ -305,11 +311,12 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(2))
     for (int kq = 0; kq < KQ; ++kq)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int qi = 32 * kq + kmap32(q, j);
+        const int qi = 32 * kq + (INA_NTN_TR ? 8 * q + j : kmap32(q, j));
         dzB[kq][j] = f2bf(gs * ldz(dze, qi < NQ && n < N, qi * N + n));
       }
     __builtin_amdgcn_sched_barrier(0);
 #else
+    static_assert(!INA_NTN_TR, "the LDS-transpose backward needs the vectorized prologue (INA_NTN_BWD_LD)");
     u16x8_t Cf[NKA];
 #pragma unroll
     for (int ka = 0; ka < NKA; ++ka)
@@ -388,6 +395,19 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(2))
     // lanes outside N x N); summed over the group's waves in fixed order one pair later (flush_dw)
     const int NN1 = N * N + 1;
     float* const dwl = reinterpret_cast<float*>(ntn_lds + 2 * FR * 64);
+    // TR: wave-private bf16 images (after the dw slots): I_P [32 rows (slice, class)][PS] = the pair's P^T
+    // transposed; I_V / I_dT [32 KQ rows (query)][VS] = relu(T) / dT with the queries on the rows
+    constexpr int PS = 16 * MTH + 4, VS = 20, IPN = 32 * PS, IVN = 32 * KQ * VS;
+    // (byte offset arithmetic on the __shared__ pointer: a uintptr_t round trip would turn these accesses
+    // into FLAT instructions)
+    unsigned short* const imgP =
+        reinterpret_cast<unsigned short*>(reinterpret_cast<unsigned char*>(dwl) +
+                                          (((PAPER ? 0 : 2 * NTN_WAVES * 2 * NN1) * 4 + 15) & ~15)) +
+        (size_t)wave * (IPN + 2 * IVN);
+    unsigned short* const imgV = imgP + IPN;
+    unsigned short* const imgD = imgV + IVN;
+    if (INA_NTN_TR && g == (int)blockIdx.x)   // once: rows / columns a shape never writes must read as zero
+      for (int i = lane; i < (IPN + 2 * IVN) / 2; i += 64) reinterpret_cast<uint32_t*>(imgP)[i] = 0u;
     const int nw = E - g * NTN_WAVES < NTN_WAVES ? E - g * NTN_WAVES : NTN_WAVES;   // active waves of the group
     auto flush_dw = [&](int pp) {
       if (PAPER) return;
@@ -409,6 +429,120 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(2))
       if (p > p0) flush_dw(p - 1);   // the previous pair's dw slots are complete (barrier at its end)
       const u16x8_t* buf = ntn_lds + ((p - p0) & 1) * FR * 64;
       if (p + 1 < p1) ntn_stage<MTH, NSW, true>(ntn_lds + ((p + 1 - p0) & 1) * FR * 64, p + 1, mpack, m2pack, wtpack, 2);
+#if INA_NTN_TR
+      if (act) {
+        f32x4_t dTs[2][QT];
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+          const int s = 2 * p + sl;
+          const bool sok = s < h;   // (a padding slice runs on zero packs and stores into the trash tails)
+          f32x4_t PT[2 * NKB];
+#pragma unroll
+          for (int mb = 0; mb < 2 * NKB; ++mb) {
+            PT[mb] = Z4;
+            if (mb < MTH) {
+#pragma unroll
+              for (int ka = 0; ka < NKA; ++ka) PT[mb] = mfma_bf16(buf[((sl * MTH + mb) * NKA + ka) * 64 + lane], Cf[ka], PT[mb]);
+            }
+          }
+          u16x8_t PTf[NKB];
+#pragma unroll
+          for (int kb = 0; kb < NKB; ++kb) PTf[kb] = pack2(PT[2 * kb], PT[2 * kb + 1]);
+          // P^T [b][c = n] -> I_P row (slice sl, class n) in the pair-fragment k order 8 (c >> 2) + 4 sl + (c & 3)
+          {
+            unsigned short* row = imgP + (8 * (n >> 2) + 4 * sl + (n & 3)) * PS + 4 * q;
+#pragma unroll
+            for (int mb = 0; mb < MTH; ++mb) {
+              const u16x8_t& f = PTf[mb >> 1];
+              const int o = 4 * (mb & 1);
+              *reinterpret_cast<u16x4_t*>(row + 16 * mb) = u16x4_t{f[o], f[o + 1], f[o + 2], f[o + 3]};
+            }
+          }
+          u16x8_t wt = {0, 0, 0, 0, 0, 0, 0, 0};
+          float ws = 0.f;
+          if (PAPER) ws = wvec[s];
+          else wt = buf[(F1 + F2 + sl) * 64 + lane];
+          float dwp = 0.f;
+#pragma unroll
+          for (int qt = 0; qt < QT; ++qt) {
+            f32x4_t T = Z4;
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) T = mfma_bf16(PTf[kb], Qf[qt][kb], T);   // rows c, cols query
+            f32x4_t dV;
+            if (PAPER) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                dV[r] = ws * dzC[qt][r];
+                dwp += fmaxf(T[r], 0.f) * dzC[qt][r];
+              }
+            } else {
+              dV = mfma_bf16(wt, dzA[qt], Z4);   // rows c, cols query
+            }
+            f32x4_t V;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              dTs[sl][qt][r] = T[r] > 0.f ? dV[r] : 0.f;
+              V[r] = fmaxf(T[r], 0.f);
+            }
+            // rows c = 4q + r, cols query 16 qt + n -> I_V / I_dT row = query, cols c
+            const int ro = (16 * qt + n) * VS + 4 * q;
+            if (!PAPER)
+              *reinterpret_cast<u16x4_t*>(imgV + ro) = u16x4_t{f2bf(V[0]), f2bf(V[1]), f2bf(V[2]), f2bf(V[3])};
+            *reinterpret_cast<u16x4_t*>(imgD + ro) =
+                u16x4_t{f2bf(dTs[sl][qt][0]), f2bf(dTs[sl][qt][1]), f2bf(dTs[sl][qt][2]), f2bf(dTs[sl][qt][3])};
+          }
+          lds_order();
+          if (PAPER) {
+            dwp = wave_sum(dwp);
+            if (lane == 0 && sok) dw_slab[(long)ep * h + s] = dwp;
+          } else {
+            f32x4_t dw = Z4;   // dw[c][c'] = sum_q relu(T)[c][q] dz[q][c']
+#pragma unroll
+            for (int kq = 0; kq < KQ; ++kq) dw = mfma_bf16(tr_read8(imgV + kq * 32 * VS, VS, 0, q, n), dzB[kq], dw);
+            float* const dst = dwl + (((p & 1) * NTN_WAVES + wave) * 2 + sl) * NN1;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dst[(4 * q + r < N && n < N) ? (4 * q + r) * N + n : N * N] = dw[r];
+          }
+          // dP^T[b, c] = sum_q Q[q, b] dT[c, q]  (B = dT^T from I_dT)
+          u16x8_t dTB[KQ];
+#pragma unroll
+          for (int kq = 0; kq < KQ; ++kq) dTB[kq] = tr_read8(imgD + kq * 32 * VS, VS, 0, q, n);
+          lds_order();   // the next slice's image stores come after these reads
+          f32x4_t dPT[2 * NKB];
+#pragma unroll
+          for (int mb = 0; mb < 2 * NKB; ++mb) {
+            dPT[mb] = Z4;
+            if (mb < MTH) {
+#pragma unroll
+              for (int kq = 0; kq < KQ; ++kq) dPT[mb] = mfma_bf16(QTf[mb][kq], dTB[kq], dPT[mb]);
+            }
+          }
+          // dC^T[a, c] += sum_b M[a, b, s] dP[c, b]
+#pragma unroll
+          for (int kb = 0; kb < NKB; ++kb) {
+            const u16x8_t dPf = pack2(dPT[2 * kb], dPT[2 * kb + 1]);
+#pragma unroll
+            for (int ma = 0; ma < MTH; ++ma)
+              dCT[ma] = mfma_bf16(buf[(F1 + (sl * MTH + ma) * NKB + kb) * 64 + lane], dPf, dCT[ma]);
+          }
+          // dP -> bf16 [E*N][h*H] for the dM reduction GEMM
+          unsigned short* const dpt = dp_out + (long)E * N * hH;
+#pragma unroll
+          for (int mb = 0; mb < MTH; ++mb)
+            *reinterpret_cast<u16x4_t*>(sok ? dpb[mb] + s * H : dpt) =
+                u16x4_t{f2bf(dPT[mb][0]), f2bf(dPT[mb][1]), f2bf(dPT[mb][2]), f2bf(dPT[mb][3])};
+        }
+        // dQ^T[b, q] += sum_{s in pair, c} P_s[c, b] dT_s[c, q]  (A = the pair's P from I_P)
+        lds_order();
+#pragma unroll
+        for (int nb = 0; nb < MTH; ++nb) {
+          const u16x8_t Pf = tr_read8(imgP, PS, 16 * nb, q, n);
+#pragma unroll
+          for (int qt = 0; qt < QT; ++qt) dQT[nb][qt] = mfma_bf16(Pf, pack2(dTs[0][qt], dTs[1][qt]), dQT[nb][qt]);
+        }
+        lds_order();
+      }
+#else
       if (act) {
         f32x4_t Ps[2][MTH], dTs[2][QT];
 #pragma unroll
@@ -523,6 +657,7 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(2))
           for (int qt = 0; qt < QT; ++qt) dQT[nb][qt] = mfma_bf16(Pf, pack2(dTs[0][qt], dTs[1][qt]), dQT[nb][qt]);
         }
       }
+#endif
       stage_wait();
       __syncthreads();
     }
@@ -588,7 +723,10 @@ static size_t ntn_lds_bytes(int MTH, bool paper, bool bwd, int N = 0) {
   const int fr = bwd ? (4 * MTH * NKA + (paper ? 0 : 2)) : (2 * MTH * NKA + (paper ? 0 : 1));
   // + the reference-head backward's dw slots [2 parities][waves][2 slices][N*N + 1] fp32
   const size_t dwl = (bwd && !paper) ? (size_t)2 * NTN_WAVES * 2 * (N * N + 1) * 4 : 0;
-  return (size_t)2 * fr * 64 * 16 + dwl;
+  // + (TR) the wave-private transpose images, 16-byte aligned after the dw slots
+  const int KQ = 2;   // upper bound over the instantiated QT (<= 4)
+  const size_t img = (bwd && INA_NTN_TR) ? 16 + (size_t)NTN_WAVES * (32 * (16 * MTH + 4) + 2 * 32 * KQ * 20) * 2 : 0;
+  return (size_t)2 * fr * 64 * 16 + dwl + img;
 }
 
 int ntn_groups(int E) { return (E + NTN_WAVES - 1) / NTN_WAVES; }
