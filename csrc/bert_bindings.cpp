@@ -209,6 +209,44 @@ std::tuple<Tensor, Tensor> bert_bias_gelu_bwd(const Tensor& dy, const Tensor& x,
   return {dx, slab};
 }
 
+// ------------------------------------------------------------------ own GEMM (gemm.hip)
+// y = x W^T with epilogue epi: 0 -> (y [+ b]), 1 -> (gelu(y + b), pre-activation aux), 2 -> (y * gelu'(aux),
+// bias-gradient column-sum slab [2 ceil(M/256)][N])
+std::tuple<Tensor, Tensor> bert_gemm(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& b,
+                                     const c10::optional<Tensor>& aux, int64_t epi) {
+  chk(x, "x", at::kBFloat16);
+  chk(w, "w", at::kBFloat16);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "ina.bert_gemm: x [M, K], w [N, K]");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(N % 256 == 0 && K % 64 == 0 && K >= 64, "ina.bert_gemm: N must be a multiple of 256, K of 64");
+  TORCH_CHECK(M * K * 2 < (1LL << 31) && N * K * 2 < (1LL << 31), "ina.bert_gemm: operand too large");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "ina.bert_gemm: epi must be 0, 1 or 2");
+  const float* bp = nullptr;
+  if (b.has_value() && b->defined()) {
+    chk(*b, "b", at::kFloat);
+    TORCH_CHECK(b->numel() == N, "ina.bert_gemm: b must be [N]");
+    bp = b->data_ptr<float>();
+  }
+  TORCH_CHECK(epi != 1 || bp != nullptr, "ina.bert_gemm: epi 1 needs the bias");
+  auto y = at::empty({M, N}, x.options());
+  Tensor ax, slab;
+  if (epi == 0) ax = at::empty({0}, x.options());
+  if (epi == 1) ax = at::empty({M, N}, x.options());
+  if (epi == 2) {
+    TORCH_CHECK(aux.has_value() && aux->defined(), "ina.bert_gemm: epi 2 needs aux");
+    ax = *aux;
+    chk(ax, "aux", at::kBFloat16);
+    TORCH_CHECK(ax.size(0) == M && ax.size(1) == N, "ina.bert_gemm: aux must be [M, N]");
+    slab = at::empty({2 * ((M + 255) / 256), N}, x.options().dtype(at::kFloat));
+  }
+  if (M == 0) return {y, epi == 2 ? slab.zero_() : ax};
+  launched(ina::gemm_bf16_nt(x.data_ptr(), (int)K, w.data_ptr(), (int)K, (int)M, (int)N, (int)K, bp, y.data_ptr(),
+                             (int)N, epi != 0 ? ax.data_ptr() : nullptr, (int)N,
+                             slab.defined() ? slab.data_ptr<float>() : nullptr, (int)epi, stream()),
+           "gemm_bf16_nt");
+  return {y, epi == 2 ? slab : ax};
+}
+
 // ------------------------------------------------------------------ fused attention
 void mha_checks(const Tensor& qkv, const Tensor& inst, const Tensor& mask, int64_t L, int64_t nh) {
   chk(qkv, "qkv", at::kBFloat16);
@@ -289,6 +327,7 @@ TORCH_LIBRARY_FRAGMENT(ina, m) {
   m.def("bert_ln_res_bwd", &bert_ln_res_bwd);
   m.def("bert_bias_gelu_fwd", &bert_bias_gelu_fwd);
   m.def("bert_bias_gelu_bwd", &bert_bias_gelu_bwd);
+  m.def("bert_gemm", &bert_gemm);
   m.def("bert_mha_fwd", &bert_mha_fwd);
   m.def("bert_mha_bwd", &bert_mha_bwd);
 }

@@ -316,6 +316,10 @@ int embed_ln_fwd(const BertEmbArgs& a, hipStream_t st);
 int embed_ln_bwd(const BertEmbArgs& a, hipStream_t st);
 
 int bias_gelu_fwd(const void* x, const float* b, void* y, long T, int I, hipStream_t st);
+// gemm.hip: C = A B^T (bf16, A [M][K] / B [N][K] K-contiguous), epi 0 plain (+bias), 1 bias+GELU with the
+// pre-activation in aux, 2 C * GELU'(aux) with column-sum slab [2 ceil(M/256)][N].  N % 256 == 0, K % 64 == 0.
+int gemm_bf16_nt(const void* A, int lda, const void* B, int ldb, int M, int N, int K, const float* bias, void* out,
+                 int ldo, void* aux, int ldx, float* slab, int epi, hipStream_t st);
 int bias_gelu_bwd(const void* dy, const void* x, const float* b, void* dx, float* slab, int T, int I, int blocks,
                   hipStream_t st);
 

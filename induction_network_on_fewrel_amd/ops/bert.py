@@ -5,7 +5,8 @@ Per layer (post-LN BERT, models/bert.py is the oracle):
                                      flat bf16 weight copy (q/k/v are adjacent in the flat buffer)
     ctx = MHA(qkv)                   ina.bert_mha_fwd / _bwd   (fused, sequence in LDS, MFMA)
     x1  = LN(x + drop(ctx Wo^T+bo))  addmm + ina.bert_ln_res_fwd / _bwd
-    h   = gelu(x1 W1^T + b1)         mm + ina.bert_bias_gelu_fwd / _bwd
+    h   = gelu(x1 W1^T + b1)         mm + ina.bert_bias_gelu_fwd / _bwd, or (INA_BERT_OWN_GEMM=1) _Ffn: the
+                                     own gemm.hip kernel with bias + GELU / GELU' + db in its epilogues
     x2  = LN(x1 + drop(h W2^T+b2))   addmm + ina.bert_ln_res_fwd / _bwd
 Embeddings: ina.bert_embed_ln_fwd / _bwd (gather by instance index, no host copies); the word-table
 gradient is scattered with index_add_ straight into the flat gradient buffer.
@@ -17,6 +18,7 @@ accumulation).  LayerNorm / GELU-bias / embedding tables stay fp32.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -122,6 +124,62 @@ class _Linear(torch.autograd.Function):
         if on_done is not None:   # last backward op of a layer: its gradient bucket is final
             on_done()
         return (dx, None, None, None, None, None, None, None, None) + tuple(outs)
+
+
+def _add_wgrad(gW, dy, x, shape):
+    """dW = dy^T x (fp32) added into the flat gradient span gW, or returned (plain autograd)."""
+    part = _wgrad_parts(dy, x) if gW is not None and gW.is_contiguous() else None
+    if part is not None:
+        ops().slab_reduce(part, gW, True)
+        return None
+    if gW is not None:
+        gW.add_(_wgrad(dy, x).view(gW.shape))
+        return None
+    return _wgrad(dy, x).view(shape)
+
+
+class _Ffn(torch.autograd.Function):
+    """o = gelu(x W1^T + b1) W2^T + b2 on the own gfx950 GEMM (csrc/kernels/gemm.hip):
+
+    forward : ONE kernel for x W1^T with bias + GELU + the bf16 pre-activation (aux) in its epilogue (replaces
+              hipBLASLt mm + bert_bias_gelu_fwd), then h W2^T + b2 (hipBLASLt addmm).
+    backward: ONE kernel for dh = do W2 with dpre = dh * GELU'(aux) and the b1 column-sum slab in its epilogue
+              (replaces hipBLASLt mm + bert_bias_gelu_bwd); dx = dpre W1 (+ the residual gradient, as _Linear);
+              dW1 / dW2 as _Linear's split-K fp32 GEMMs.
+    b2's gradient comes from the following _LnRes (db_ext), as for the unfused path."""
+
+    @staticmethod
+    def forward(ctx, x, W1b, W2b, bb2, gW1, gW2, dx_acc, meta, b1name, W1, b1, W2):
+        h, aux = ops().bert_gemm(x, W1b, b1.detach(), None, 1)
+        o = torch.addmm(bb2, h, W2b.t())
+        ctx.save_for_backward(x, W1b, W2b, h, aux)
+        ctx.cfg = (gW1, gW2, dx_acc, meta, b1name, tuple(W1.shape), tuple(W2.shape))
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        x, W1b, W2b, h, aux = ctx.saved_tensors
+        gW1, gW2, dx_acc, meta, b1name, s1, s2 = ctx.cfg
+        do = do.contiguous()
+        dpre, slab = ops().bert_gemm(do, W2b.t().contiguous(), None, aux, 2)
+        dW2 = _add_wgrad(gW2, do, h, s2)
+        res = dx_acc.take() if dx_acc is not None else None
+        dx = res.addmm_(dpre, W1b) if res is not None else torch.mm(dpre, W1b)
+        dW1 = _add_wgrad(gW1, dpre, x, s1)
+        glue, maps = _glue_maps(meta, [b1name])
+        db1 = None
+        if glue is not None:
+            glue.add(slab, maps[0], slab.shape[0])
+        else:
+            db1 = _route_grad(meta, b1name, slab.sum(0))
+        return dx, None, None, None, None, None, None, None, None, dW1, db1, dW2
+
+
+def own_ffn_enabled(I: int, Hd: int) -> bool:
+    """The own-GEMM FFN (INA_BERT_OWN_GEMM=1; default off: measured at parity with hipBLASLt + the separate
+    bias / GELU passes -- BERT 10w5s 108.9 / 109.2 vs 109.6 / 110.0 episodes/s, profiles/r4_own_gemm).
+    Needs N = I a multiple of 256 and K = Hd a multiple of 64."""
+    return os.environ.get("INA_BERT_OWN_GEMM", "0") != "0" and I % 256 == 0 and Hd % 64 == 0
 
 
 class _ResGrad:
@@ -343,6 +401,7 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
                      P(e + "token_type_embeddings.weight"), P(e + "LayerNorm.weight"), P(e + "LayerNorm.bias"),
                      seed, pd, dict(meta, names=emb_names))
     # ---- layers
+    own_ffn = own_ffn_enabled(cfg.bert_intermediate, Hd)
     for i in range(nl):
         pre = f"bert.encoder.layer.{i}."
         a = pre + "attention."
@@ -357,9 +416,15 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
                          meta, by_name[a + "output.LayerNorm.weight"], by_name[a + "output.LayerNorm.bias"],
                          P(a + "output.dense.bias"), by_name[a + "output.dense.bias"], r1)
         I = cfg.bert_intermediate
-        hpre = linear(x, [pre + "intermediate.dense.weight"], None, I, Hd, dx_acc=r2)
-        h = _BiasGelu.apply(hpre, P(pre + "intermediate.dense.bias"), meta, by_name[pre + "intermediate.dense.bias"])
-        o = linear(h, [pre + "output.dense.weight"], [pre + "output.dense.bias"], Hd, I, db_ext=True)
+        w1n, b1n, w2n, b2n = (pre + "intermediate.dense.weight", pre + "intermediate.dense.bias",
+                              pre + "output.dense.weight", pre + "output.dense.bias")
+        if own_ffn:
+            o = _Ffn.apply(x, wspan([w1n], (I, Hd)), wspan([w2n], (Hd, I)), wspan([b2n], (Hd,)), gspan([w1n]),
+                           gspan([w2n]), r2, meta, by_name[b1n], P(w1n), P(b1n), P(w2n))
+        else:
+            hpre = linear(x, [w1n], None, I, Hd, dx_acc=r2)
+            h = _BiasGelu.apply(hpre, P(b1n), meta, by_name[b1n])
+            o = linear(h, [w2n], [b2n], Hd, I, db_ext=True)
         x = _LnRes.apply(o, x, P(pre + "output.LayerNorm.weight"), P(pre + "output.LayerNorm.bias"), seed, 19 + 3 * i,
                          pd, meta, by_name[pre + "output.LayerNorm.weight"], by_name[pre + "output.LayerNorm.bias"],
                          P(pre + "output.dense.bias"), by_name[pre + "output.dense.bias"], r2)

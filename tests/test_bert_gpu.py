@@ -123,8 +123,11 @@ def test_mha(L, p):
     torch.testing.assert_close(db, dqkv.float().sum(0), rtol=1e-4, atol=1e-3)
 
 
-def test_bert_encoder_end_to_end():
-    """ops.bert.bert_encode (kernels + hipBLASLt GEMMs) vs encode_ref: forward and parameter grads."""
+@pytest.mark.parametrize("own_gemm", ["1", "0"])
+def test_bert_encoder_end_to_end(own_gemm, monkeypatch):
+    """ops.bert.bert_encode (kernels + GEMMs) vs encode_ref: forward and parameter grads; own_gemm "1" runs
+    the FFN on the own gemm.hip kernels (fused bias + GELU / GELU' epilogues), "0" on hipBLASLt + bias_gelu."""
+    monkeypatch.setenv("INA_BERT_OWN_GEMM", own_gemm)
     from induction_network_on_fewrel_amd.config import Config
     from induction_network_on_fewrel_amd.models import InductionNetwork
     from induction_network_on_fewrel_amd.ops.bert import bert_encode
@@ -153,7 +156,8 @@ def test_bert_encoder_end_to_end():
     (ref * w).sum().backward()
     for n in ("bert.encoder.layer.0.attention.self.query.weight", "bert.encoder.layer.1.output.dense.weight",
               "bert.encoder.layer.1.output.LayerNorm.weight", "bert.embeddings.position_embeddings.weight",
-              "bert.embeddings.word_embeddings.weight", "bert.encoder.layer.0.intermediate.dense.bias"):
+              "bert.embeddings.word_embeddings.weight", "bert.encoder.layer.0.intermediate.dense.bias",
+              "bert.encoder.layer.0.intermediate.dense.weight", "bert.encoder.layer.1.intermediate.dense.bias"):
         assert n in got, n
         _close(got[n], p[n].grad, rtol=8e-2)
 
@@ -179,10 +183,12 @@ def test_split_k_weight_grad_accumulated_into_flat_span():
         torch.testing.assert_close(out, part.sum(0), rtol=1e-5, atol=1e-4)
 
 
-def test_bert_glue_slab_jobs_match_direct_routing():
+@pytest.mark.parametrize("own_gemm", ["1", "0"])
+def test_bert_glue_slab_jobs_match_direct_routing(own_gemm, monkeypatch):
     """Trainer path: the LayerNorm / bias / embedding slab reductions queued on the StepGlue (one
     deterministic slab_scatter per 8 jobs) give the same flat gradient as the per-parameter torch
     reductions routed into the flat buffer."""
+    monkeypatch.setenv("INA_BERT_OWN_GEMM", own_gemm)
     from induction_network_on_fewrel_amd.config import Config
     from induction_network_on_fewrel_amd.models import InductionNetwork
     from induction_network_on_fewrel_amd.ops.bert import bert_encode

@@ -1,0 +1,92 @@
+"""Own gfx950 bf16 GEMM (csrc/kernels/gemm.hip, ina.bert_gemm) vs a plain PyTorch fp32 GEMM of the same
+bf16 inputs: plain / bias, bias + GELU with the pre-activation aux, and GELU' * C with the bias-gradient
+column-sum slab.  Shapes include the BERT-base FFN (K = 768 / 3072, N = 768 / 3072) and ragged M tails."""
+import pytest
+import torch
+
+from induction_network_on_fewrel_amd.models import bert as B
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda")
+
+
+def _ops():
+    from induction_network_on_fewrel_amd.ops._ext import ops
+    return ops()
+
+
+def _close(a, b, rtol):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err / scale < rtol, f"max err {err} vs scale {scale}"
+
+
+def _gelu_grad(u):
+    return 0.5 * (1.0 + torch.erf(u * 0.7071067811865476)) + u * 0.3989422804014327 * torch.exp(-0.5 * u * u)
+
+
+SHAPES = [(256, 256, 64), (300, 512, 192), (1000, 768, 768), (4133, 3072, 768), (2048 + 37, 768, 3072), (97, 256, 128),
+          (8292, 3072, 768), (17000, 1024, 192)]   # the last two: more tiles than CUs (persistent blocks), odd K-step count
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("bias", [False, True])
+def test_gemm_plain(M, N, K, bias):
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device=dev) if bias else None
+    y, _ = _ops().bert_gemm(x, w, b, None, 0)
+    ref = x.float() @ w.float().t()
+    if bias:
+        ref = ref + b
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    _close(y, ref, 1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_gemm_bias_gelu(M, N, K):
+    torch.manual_seed(1 + M)
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device=dev) * 0.5
+    y, aux = _ops().bert_gemm(x, w, b, None, 1)
+    pre = x.float() @ w.float().t() + b
+    _close(aux, pre, 1e-2)
+    _close(y, B.gelu(pre), 1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_gemm_dgelu_slab(M, N, K):
+    torch.manual_seed(2 + M)
+    dy = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
+    aux = (torch.randn(M, N, device=dev) * 2).bfloat16()
+    d, slab = _ops().bert_gemm(dy, w, None, aux, 2)
+    ref = (dy.float() @ w.float().t()) * _gelu_grad(aux.float())
+    _close(d, ref, 1e-2)
+    assert slab.shape == (2 * ((M + 255) // 256), N)
+    _close(slab.sum(0), ref.sum(0), 1e-2)
+
+
+def test_gemm_deterministic():
+    torch.manual_seed(5)
+    M, N, K = 1500, 3072, 768
+    dy = torch.randn(M, K, device=dev).bfloat16()
+    w = torch.randn(N, K, device=dev).bfloat16()
+    aux = torch.randn(M, N, device=dev).bfloat16()
+    a1, s1 = _ops().bert_gemm(dy, w, None, aux, 2)
+    a2, s2 = _ops().bert_gemm(dy, w, None, aux, 2)
+    assert torch.equal(a1, a2) and torch.equal(s1, s2)
+
+
+def test_gemm_rejects_bad_shapes():
+    x = torch.randn(64, 100, device=dev).bfloat16()
+    w = torch.randn(256, 100, device=dev).bfloat16()
+    with pytest.raises(RuntimeError):
+        _ops().bert_gemm(x, w, None, None, 0)   # K % 64 != 0
+    x = torch.randn(64, 128, device=dev).bfloat16()
+    w = torch.randn(200, 128, device=dev).bfloat16()
+    with pytest.raises(RuntimeError):
+        _ops().bert_gemm(x, w, None, None, 0)   # N % 256 != 0
