@@ -161,8 +161,9 @@ class Config:
     def validate(self) -> None:
         if self.N < 1 or self.K < 1 or self.Q < 1:
             raise ValueError("N, K, Q must be >= 1")
-        if self.hidden_size % 4 != 0:
-            raise ValueError("hidden_size must be a multiple of 4 (lane-ownership layout of the LSTM kernel)")
+        if self.hidden_size < 1:
+            raise ValueError("hidden_size must be >= 1 (widths between the kernel instantiations run zero-padded, "
+                             "models/padding.py)")
         if self.relation_head not in ("reference", "paper"):
             raise ValueError(f"unknown relation_head {self.relation_head}")
         if self.dtype not in ("bf16", "fp32"):

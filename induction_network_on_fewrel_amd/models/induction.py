@@ -18,6 +18,7 @@ from torch import nn
 
 from ..config import Config
 from . import reference as ref
+from .padding import SMALL_U, WIDE_U, next_width, padded_params, padding_enabled
 from .params import InductionParams
 
 GPU_SUPPORTED_U = (8, 20, 32)   # fused BiLSTM kernel instantiations; other widths use ops/wide.py
@@ -39,16 +40,31 @@ class InductionNetwork(nn.Module):
         """HF name -> tensor view of the BERT encoder + projection parameters."""
         return {n: getattr(self.params, a) for a, n in self.params.names().items() if a.startswith("bert__")}
 
+    def lstm_plan(self, L: int) -> Tuple[str, int]:
+        """(path, width) of the GPU encoder: "small" = the fused lane-ownership BiLSTM+attention kernels
+        (lstm.hip, u in {8, 20, 32}, input <= 64, L <= 64, pos dim <= 8), "wide" = ops/wide.py (persistent
+        lstm_wide.hip kernels at u in {64, 100, 128}, the per-step GEMM loop otherwise).  A width between the
+        instantiations runs exactly on the next one up with zero-padded parameters (models/padding.py;
+        INA_LSTM_PAD=0 disables).  ``lstm_impl`` "fused" / "wide" forces the path."""
+        cfg = self.cfg
+        u, impl = cfg.hidden_size, cfg.lstm_impl
+        small_ok = self.params.input_dim <= 64 and L <= 64 and cfg.pos_embedding_dim <= 8
+        pad = padding_enabled()
+        if impl != "wide":
+            if small_ok and u in SMALL_U:
+                return "small", u
+            if small_ok and pad and u < SMALL_U[-1]:
+                return "small", next_width(u, SMALL_U)
+            if impl == "fused":
+                raise NotImplementedError(f"fused BiLSTM kernels need u <= {SMALL_U[-1]} (instantiated for "
+                                          f"{SMALL_U}), input dim <= 64, L <= 64, pos dim <= 8")
+        if pad and u <= WIDE_U[-1] and u not in WIDE_U:
+            return "wide", next_width(u, WIDE_U)
+        return "wide", u
+
     def use_fused_lstm(self, L: int) -> bool:
-        """Fused lane-ownership BiLSTM+attention kernels (u in GPU_SUPPORTED_U, input <= 64, L <= 64,
-        pos dim <= 8) or the wide GEMM path (``lstm_impl`` forces either)."""
-        impl = self.cfg.lstm_impl
-        ok = (self.cfg.hidden_size in GPU_SUPPORTED_U and self.params.input_dim <= 64 and L <= 64
-              and self.cfg.pos_embedding_dim <= 8)
-        if impl == "fused" and not ok:
-            raise NotImplementedError(f"fused BiLSTM kernels need u in {GPU_SUPPORTED_U}, input dim <= 64, L <= 64, "
-                                      "pos dim <= 8")
-        return ok if impl == "auto" else impl == "fused"
+        """The fused small-width kernels at the model's own width (the fused training step, graph capture)."""
+        return self.lstm_plan(L) == ("small", self.cfg.hidden_size)
 
     def _head(self, e, p, B, N, K, Q, grad_views):
         """Fused routing + NTN kernels when instantiated for (H, N, Q), else the GEMM formulation."""
@@ -107,19 +123,24 @@ class InductionNetwork(nn.Module):
                                       embeddings_only, glue)
         if inst.is_cuda:
             word, pos1, pos2, mask = data
-            if self.use_fused_lstm(word.shape[1]):
+            path, up = self.lstm_plan(word.shape[1])
+            u = cfg.hidden_size
+            pe, real = (p, None) if up == u else padded_params(p, u, up, self.params.input_dim)
+            if path == "small":
                 from ..ops.encoder import encode
-                meta = dict(U=cfg.hidden_size, bf16=(cfg.dtype == "bf16"), keep_prob=kp, seed=int(dropout_seed),
+                meta = dict(U=up, bf16=(cfg.dtype == "bf16"), keep_prob=kp, seed=int(dropout_seed),
                             ragged=cfg.ragged_tiles, skip_padding=cfg.lstm_skip_padding,
                             word_grad=bool(isinstance(p["word_embedding"], nn.Parameter)
-                                           and p["word_embedding"].requires_grad), grad_views=grad_views,
-                            seed_dev=seed_dev)
-                e, alphas = encode(inst, data, p, meta)
-            else:   # wide layers (e.g. the paper's u=128, E=300): GEMM + fused-cell path
+                                           and p["word_embedding"].requires_grad),
+                            grad_views=grad_views if real is None else None, seed_dev=seed_dev)
+                e, alphas = encode(inst, data, pe, meta)
+            else:   # wide layers (e.g. the paper's u=128, E=300): persistent kernels or the GEMM loop
                 from ..ops.wide import encode_wide
                 if cfg.lstm_skip_padding:
                     raise NotImplementedError("lstm_skip_padding: the wide GPU path runs the reference's full L")
-                e, alphas = encode_wide(inst, data, p, cfg.hidden_size, kp, int(dropout_seed))
+                e, alphas = encode_wide(inst, data, pe, up, kp, int(dropout_seed))
+            if real is not None:   # the real units of the zero-padded encoder
+                e = e[:, real]
             if embeddings_only:
                 return e, alphas
             return self._head(e, p, B, N, K, Q, grad_views), alphas

@@ -57,7 +57,9 @@ def test_paper_config_forward_backward_vs_oracle(keep_prob, u):
         assert _relerr(got[k], p[k].grad) < 8e-2, k
 
 
-def test_wide_matches_fused_at_u20():
+def test_wide_matches_fused_at_u20(monkeypatch):
+    """the per-step GEMM loop of ops/wide.py (padding off) against the fused kernels at u = 20."""
+    monkeypatch.setenv("INA_LSTM_PAD", "0")
     outs = []
     for impl in ("fused", "wide"):
         cfg, model, inst, arrays, lab, (B, N, K, Q) = _setup(20, 5, impl)
@@ -68,6 +70,39 @@ def test_wide_matches_fused_at_u20():
     assert _relerr(p1, p0) < 2e-2
     assert _relerr(g1, g0) < 6e-2
     assert _relerr(a1, a0) < 6e-2
+
+
+@pytest.mark.parametrize("u,E,path", [(10, 5, "small"), (16, 5, "small"), (50, 50, "wide"), (80, 50, "wide"),
+                                      (24, 300, "wide")])
+@pytest.mark.parametrize("keep_prob", [1.0, 0.9])
+def test_padded_width_vs_oracle(u, E, path, keep_prob):
+    """hidden_size between the kernel instantiations (models/padding.py): the encoder runs on the next
+    instantiated width with zero-padded parameters.  keep_prob 1: against the fp32 oracle at the model's own
+    width (exact semantics); keep_prob 0.9: against the oracle run on the padded parameters (the dropout
+    stream is drawn over the padded width), sliced back to the real units."""
+    from induction_network_on_fewrel_amd.models.padding import padded_params
+    cfg, model, inst, arrays, lab, (B, N, K, Q) = _setup(u, E, "auto", shifted=keep_prob == 1.0)
+    cfg.keep_prob = keep_prob
+    plan = model.lstm_plan(37)
+    assert plan[0] == path and plan[1] > u, plan
+    probs, _ = model(inst, arrays, B, N, K, Q, training=True, dropout_seed=5)
+    model.loss(probs, lab).backward()
+    got = {k: v.grad.clone() for k, v in model.pdict().items() if v.grad is not None}
+    p = {k: v.detach().clone().requires_grad_(v.requires_grad) for k, v in model.pdict().items()}
+    w, a1, a2, m = (t[inst.long()] for t in arrays)
+    if keep_prob == 1.0:
+        pr, _ = ref.forward(p, w.long(), a1.long(), a2.long(), m, B, N, K, Q, 3, "reference", 1.0, 5, bf16=False)
+    else:
+        pp, real = padded_params(p, u, plan[1], model.params.input_dim)
+        e, _ = ref.encode(pp, w.long(), a1.long(), a2.long(), m, keep_prob, 5)
+        pr = ref.head_forward(p, e[:, real], B, N, K, Q, 3, "reference")
+    model.loss(pr, lab).backward()
+    assert probs.shape == pr.shape
+    assert _relerr(probs.detach(), pr.detach()) < 3e-2
+    tol = 8e-2 if path == "wide" else 1.2e-1   # the small kernels keep the BPTT stash / dH in bf16
+    for k in ("lstm_fw_kernel", "lstm_bw_bias", "pos1_embedding", "attn_kernel", "W_s", "M"):
+        assert got[k].shape == p[k].shape, k
+        assert _relerr(got[k], p[k].grad) < tol, k
 
 
 @pytest.mark.parametrize("H,L,S", [(256, 37, 101), (200, 37, 64), (128, 37, 33), (256, 90, 5)])
