@@ -92,6 +92,12 @@ class EventWriter:
     def scalars(self, step: int, values: Dict[str, float]) -> None:
         self.fh.write(tfrecord(encode_event(step, time.time(), values)))
 
+    def graph(self, graph_def: bytes) -> None:
+        """Event{graph_def = 4}: the model graph for TensorBoard's graph dashboard (runtime/tb_graph.py)."""
+        ev = _key(1, 1) + struct.pack("<d", time.time()) + _key(2, 0) + _varint(0) + _ld(4, graph_def)
+        self.fh.write(tfrecord(ev))
+        self.fh.flush()
+
     def flush(self) -> None:
         self.fh.flush()
 
@@ -193,6 +199,10 @@ class MetricsLogger:
         if self.tb is not None and kind == "train":
             self.tb.scalars(step, {k: v for k, v in values.items()
                                    if k in ("loss", "accuracy", "learning_rate") or k.startswith(TB_PREFIXES)})
+
+    def graph(self, graph_def: bytes) -> None:
+        if self.enabled and self.tb is not None:
+            self.tb.graph(graph_def)
 
     def print(self, msg: str) -> None:
         if self.enabled and self.stdout:

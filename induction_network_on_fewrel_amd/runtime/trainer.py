@@ -30,6 +30,7 @@ from ..ops.optim import FlatParams, FusedOptimizer, lr_at
 from ..parallel.dp import DistContext
 from . import checkpoint as ckpt
 from .metrics import MetricsLogger
+from .tb_graph import model_graph
 
 
 class _HostEpisodes:
@@ -104,6 +105,8 @@ class Trainer:
         self.val_eps = self._make_sampler(self.val_data, rank_seed + 1, self.eval_nota)
         self.nota_threshold: Optional[float] = cfg.nota_threshold if cfg.nota_threshold >= 0 else None
         self.log = MetricsLogger(cfg.model_dir, enabled=log and self.dist.is_main)
+        # the model graph for TensorBoard (the reference's FileWriter(..., sess.graph), model/base.py:125)
+        self.log.graph(model_graph(self.model, cfg.N, cfg.K, cfg.Q))
         self.timers = {"sample": 0.0, "fwd_bwd": 0.0, "allreduce": 0.0, "optim": 0.0}   # host (launch) time
         self.gpu_phase_ms = {k: 0.0 for k in self.timers}                                # HIP-event time
         self._pending_events = []

@@ -227,6 +227,31 @@ def test_gradient_norm_summaries(tmp_path):
     assert {"loss", "learning_rate", "global_norm/gradient_norm", "gradient_norm/M"} <= tags
 
 
+def test_tensorboard_graph(tmp_path):
+    """The model graph event (reference: FileWriter(..., sess.graph), model/base.py:125): the reference's
+    placeholders, every variable under its TF name with its shape, and the module scopes."""
+    import glob
+    from induction_network_on_fewrel_amd.runtime.tb_graph import read_graph
+    from induction_network_on_fewrel_amd.runtime.trainer import Trainer
+    data = make_synthetic(num_relations=10, instances_per_relation=40, vocab=500, seed=0)
+    cfg = Config(N=5, K=2, Q=3, episodes_per_step=2, model_dir=str(tmp_path / "run"), seed=3, resume=False,
+                 train_iter=1, val_step=1000, test_iter=2, log_every=1)
+    tr = Trainer(cfg, data, None, device="cpu", log=True)
+    tr.log.flush()
+    nodes = read_graph(glob.glob(str(tmp_path / "run" / "train" / "events.out.tfevents.*"))[0])
+    by = {n["name"]: n for n in nodes}
+    for ph in ("input_words", "input_pos1", "input_pos2", "mask_padding", "query_label", "keep_probx"):
+        assert by[ph]["op"] == "Placeholder", ph
+    for attr, name in tr.model.params.names().items():
+        assert by[name]["op"] == "VariableV2" and by[name + "/read"]["inputs"] == [name], name
+        assert "shape" in by[name]["attrs"]
+    scopes = {n["name"].split("/")[0] for n in nodes}
+    assert {"embedding", "EncoderModule", "InductionModule", "RelationModule", "loss"} <= scopes
+    names = set(by)
+    for n in nodes:   # every input is a node of the graph
+        assert all(i in names for i in n["inputs"]), n["name"]
+
+
 def test_legacy_single_sampler_checkpoint_resumes_exactly(tmp_path):
     """Advisor finding: an older checkpoint with one 'train_sampler' entry must restore the CPU
     sampler's RNG in full at world size 1 (not restart it and replay episodes)."""
