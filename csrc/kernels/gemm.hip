@@ -60,6 +60,9 @@ enum { EPI_PLAIN = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_PLAIN_B = 3 };  // 3: pla
 #define INA_GEMM_LGKM_AFTER 0  // 1: retire the phase's LDS reads after its first barrier (A/B only: needs
                                // the 2-phase WAR distance, which the staging schedule does not give)
 #endif
+#ifndef INA_GEMM_SCHED
+#define INA_GEMM_SCHED 1  // operand staging schedule (kstep): 1 balanced, 0 front-loaded (A/B)
+#endif
 #ifndef INA_GEMM_DIAG
 #define INA_GEMM_DIAG 0  // 1: no operand staging inside the K loop (diagnostic of the MFMA/LDS/barrier skeleton)
 #endif
@@ -172,11 +175,22 @@ INA_DEVICE void wait_vm() {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// One K-step (4 phases) on buffer BUF.  full: steps s+1 and s+2 exist (steady-state counted waits);
-// otherwise every wait is vmcnt(0).  (m2, n2, kt2): the tile / K-step staged now (step s+2), valid if st2.
+// Staging position of a later K-step of this block's stream: its tile's (m0, n0) and K-step.
+struct StagePos {
+  int m, n, k;
+};
+
+// One K-step (4 phases) on buffer BUF.  full: step s+2 exists (steady-state counted waits); otherwise every
+// wait is vmcnt(0).  p1 / p2: the staging positions of steps s+1 / s+2, valid if st1 / st2.
+// INA_GEMM_SCHED 1 (balanced, default): p0 stages A1 of s+1, p1 A0, p2 B0, p3 B1 of s+2 -- one half-tile
+//   (2 DMAs per thread) per phase; waits vmcnt(10) in p0 (B1 of s), p1 (A1 of s), p3 (A0 + B0 of s+1): every
+//   half-tile has 5-6 phases between its issue and its wait.
+// INA_GEMM_SCHED 0 (front-loaded): p1 A0 + B0, p2 B1, p3 A1 of s+2; waits vmcnt(10 / 12 / 12).
 template <int BUF>
-INA_DEVICE void kstep(f32x4_t (&acc)[8][4], Frags& f, const Stager& sg, bool full, bool st2, int m2, int n2, int kt2,
-                      uint32_t rdA0, uint32_t rdA1, uint32_t rdB0, uint32_t rdB1) {
+INA_DEVICE void kstep(f32x4_t (&acc)[8][4], Frags& f, const Stager& sg, bool full, bool st1, bool st2,
+                      const StagePos& p1, const StagePos& p2, uint32_t rdA0, uint32_t rdA1, uint32_t rdB0,
+                      uint32_t rdB1) {
+  constexpr int OTHER = BUF ^ 1;
   const unsigned char* buf = gemm_lds + BUF * G_BUF;
   auto read_a = [&](u16x8_t (&fa)[4][2], int H) {
     const unsigned char* img = buf + H * G_HALF;
@@ -197,32 +211,33 @@ INA_DEVICE void kstep(f32x4_t (&acc)[8][4], Frags& f, const Stager& sg, bool ful
   // p0: A0 / B0 subtiles; B1 of this step must have landed before p1 reads it
   read_b(f.b0, 0);
   read_a(f.a0, 0);
+  if (INA_GEMM_SCHED && st1) sg.stage(OTHER, 1, p1.m, p1.n, p1.k);
   wait_lgkm0();
   if (full) wait_vm<10>(); else wait_vm<0>();
   barrier();
   mma_quadrant<0, 0>(acc, f.a0, f.b0);
   barrier();
-  // p1: B1 subtile; restage A0 + B0 (read in p0) with step s+2; A1 must land before p2
+  // p1: B1 subtile; restage A0 (+ B0) (read in p0) with step s+2; A1 must land before p2
   read_b(f.b1, 1);
   if (st2) {
-    sg.stage(BUF, 0, m2, n2, kt2);
-    sg.stage(BUF, 2, m2, n2, kt2);
+    sg.stage(BUF, 0, p2.m, p2.n, p2.k);
+    if (!INA_GEMM_SCHED) sg.stage(BUF, 2, p2.m, p2.n, p2.k);
   }
   wait_lgkm0();
-  if (full) wait_vm<12>(); else wait_vm<0>();
+  if (full) wait_vm<INA_GEMM_SCHED ? 10 : 12>(); else wait_vm<0>();
   barrier();
   mma_quadrant<0, 1>(acc, f.a0, f.b1);
   barrier();
-  // p2: A1 subtile; restage B1 (read in p1)
+  // p2: A1 subtile; restage B0 (read in p0) / B1 (read in p1)
   read_a(f.a1, 1);
-  if (st2) sg.stage(BUF, 3, m2, n2, kt2);
+  if (st2) sg.stage(BUF, INA_GEMM_SCHED ? 2 : 3, p2.m, p2.n, p2.k);
   wait_lgkm0();
   barrier();
   mma_quadrant<1, 1>(acc, f.a1, f.b1);
   barrier();
-  // p3: no reads; restage A1 (read in p2); A0 + B0 of step s+1 must land before its p0
-  if (st2) sg.stage(BUF, 1, m2, n2, kt2);
-  if (full) wait_vm<12>(); else wait_vm<0>();
+  // p3: no reads; restage B1 (read in p1) / A1 (read in p2); A0 + B0 of step s+1 must land before its p0
+  if (st2) sg.stage(BUF, INA_GEMM_SCHED ? 3 : 1, p2.m, p2.n, p2.k);
+  if (full) wait_vm<INA_GEMM_SCHED ? 10 : 12>(); else wait_vm<0>();
   barrier();
   mma_quadrant<1, 0>(acc, f.a1, f.b0);
   barrier();
@@ -344,26 +359,29 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_bf16_nt_kernel(GemmArgs g) 
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   Frags f;
 
-  // current tile (compute) and the stream position two steps ahead (staging)
+  // current tile (compute) and the stream positions one and two steps ahead (staging)
   int jt = 0, kt = 0, m0, n0;
   tile_coords(b, NT, NB, m0, n0);
-  int j2 = 0, k2 = 0, m2 = m0, n2 = n0;
-  auto adv2 = [&]() {
-    if (++k2 == T) {
-      k2 = 0;
+  StagePos p1{m0, n0, 0}, p2{m0, n0, 0};
+  int j2 = 0;
+  auto adv2 = [&]() {   // p1 <- p2, p2 <- the next K-step of the stream
+    p1 = p2;
+    if (++p2.k == T) {
+      p2.k = 0;
       ++j2;
-      if (j2 < ntile) tile_coords(b + j2 * G, NT, NB, m2, n2);
+      if (j2 < ntile) tile_coords(b + j2 * G, NT, NB, p2.m, p2.n);
     }
   };
-  // prologue: steps 0 and 1, half-tiles in the order the waits count them (A0 B0 B1 A1)
+  // prologue: step 0 (A0 B0 B1 A1) and step 1 (SCHED 1: A0 B0 B1, its A1 is staged in step 0's p0;
+  // SCHED 0: A0 B0 B1 A1), in the order the counted waits assume
   for (int p = 0; p < 2 && p < S; ++p) {
-    sg.stage(p, 0, m2, n2, k2);
-    sg.stage(p, 2, m2, n2, k2);
-    sg.stage(p, 3, m2, n2, k2);
-    sg.stage(p, 1, m2, n2, k2);
+    sg.stage(p, 0, p2.m, p2.n, p2.k);
+    sg.stage(p, 2, p2.m, p2.n, p2.k);
+    sg.stage(p, 3, p2.m, p2.n, p2.k);
+    if (!INA_GEMM_SCHED || p == 0) sg.stage(p, 1, p2.m, p2.n, p2.k);
     adv2();
   }
-  if (S > 1) wait_vm<12>(); else wait_vm<0>();
+  if (S > 1) wait_vm<INA_GEMM_SCHED ? 10 : 12>(); else wait_vm<0>();
   barrier();
   if (INA_GEMM_STAGGER && wr == 1) barrier();  // ping-pong: row group 1 runs one barrier behind row group 0
 
@@ -372,12 +390,12 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_bf16_nt_kernel(GemmArgs g) 
     for (int u = 0; u < 2; ++u) {
       const int ss = s + u;
       if (ss < S) {
-        const bool st2 = ss + 2 < S;
+        const bool st1 = ss + 1 < S, st2 = ss + 2 < S;
         if (u == 0)
-          kstep<0>(acc, f, sg, st2, st2, m2, n2, k2, rdA0, rdA1, rdB0, rdB1);
+          kstep<0>(acc, f, sg, st2, st1, st2, p1, p2, rdA0, rdA1, rdB0, rdB1);
         else
-          kstep<1>(acc, f, sg, st2, st2, m2, n2, k2, rdA0, rdA1, rdB0, rdB1);
-        if (st2) adv2();
+          kstep<1>(acc, f, sg, st2, st1, st2, p1, p2, rdA0, rdA1, rdB0, rdB1);
+        adv2();
         if (++kt == T) {
           epilogue<EPI>(acc, g, m0, n0, wr, wc, fr, fq);
 #pragma unroll

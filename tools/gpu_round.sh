@@ -4,7 +4,7 @@ set -o pipefail
 OUT=${1:-gpurun_out/round}
 ROOT=$PWD
 mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 && \
+timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 && \
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
 timeout -k 10 200 python bench.py --steps 30 --warmup 5 > $OUT/b5.log 2>&1 && \
 timeout -k 10 200 python bench.py --steps 30 --warmup 5 --graph 1 > $OUT/b5g.log 2>&1 && \
