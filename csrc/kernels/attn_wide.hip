@@ -35,7 +35,8 @@ template <int HP>
 struct AttnCfg {
   static constexpr int NW = HP / 32;   // waves: two 16-feature M-tiles each
   static constexpr int KS = HP / 32;   // K-steps over the features
-  static constexpr int HS = HP + 8;    // LDS row stride (elements)
+  static constexpr int HS = HP + 16;   // LDS row stride (elements): rows 2 bank slots apart, so the MFMA
+                                       // B-operand reads are conflict-free (lstm_wide.hip WideCfg)
   static constexpr int NTH = NW * 64;  // = 2 HP
   static constexpr int CP = HP / 8;    // 16-byte chunks per padded row
   static constexpr int PFH = 6;        // prefetched H chunks per thread: blocks of <= 96 tokens
@@ -458,7 +459,7 @@ int wide_attn_hp(int H) { return (H == 128 || H == 200 || H == 256) ? (H + 31) /
 int wide_attn_sb(int L) { return L >= 80 ? 1 : min(4, 80 / L); }   // ~80 tokens, <= 4 sequences per block
 
 size_t wide_attn_smem(int H, int L, bool bwd) {
-  const int HP = wide_attn_hp(H), HS = HP + 8, SB = wide_attn_sb(L), R = (SB * L + 15) / 16 * 16;
+  const int HP = wide_attn_hp(H), HS = HP + 16, SB = wide_attn_sb(L), R = (SB * L + 15) / 16 * 16;
   if (!bwd) return (size_t)R * HS * 2 + (size_t)(HP / 32) * R * 4 + (size_t)R * 4;
   return 2 * (size_t)R * HS * 2 + 2 * 16 * (size_t)HS * 2 + 2 * (size_t)SB * HP * 4 + 3 * (size_t)R * 4 +
          2 * (size_t)HP * 4;

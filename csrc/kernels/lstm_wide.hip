@@ -181,8 +181,14 @@ struct WideCfg {
   static constexpr int G4 = 4 * UP;      // permuted gate columns
   static constexpr int KS2 = G4 / 32;    // backward K-steps (gate columns)
   static constexpr int NT = 2;           // 16-sequence tiles per workgroup
-  static constexpr int HS = UP + 8;      // h image row stride (elements; +16 B against bank aliasing)
-  static constexpr int GS = G4 + 8;      // dG image row stride
+  // LDS image row strides: +32 bytes, i.e. consecutive rows 2 bank slots (of 16 B) apart.  The MFMA B
+  // operand reads (ds_read_b128: 16 rows n x chunk 4 ks + q per lane group {0-3,12-15 | q} u {4-11 | q+1})
+  // then land rows of one q parity on even and the other on odd slots, pairwise distinct: conflict-free.
+  // (+16 bytes put lane 12 and lane 27 on one slot: a 2-way conflict in every lane group, 44-46% of the
+  // LDS cycles at the paper configuration, verdict r3 #5; an XOR swizzle costs per-lane addresses and
+  // spilled the backward.)
+  static constexpr int HS = UP + 16;     // h image row stride (elements)
+  static constexpr int GS = G4 + 16;     // dG image row stride
   static constexpr int SEQ = NT * 16;
 };
 
