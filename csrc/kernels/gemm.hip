@@ -61,7 +61,8 @@ enum { EPI_PLAIN = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_PLAIN_B = 3 };  // 3: pla
                                // the 2-phase WAR distance, which the staging schedule does not give)
 #endif
 #ifndef INA_GEMM_SCHED
-#define INA_GEMM_SCHED 1  // operand staging schedule (kstep): 1 balanced, 0 front-loaded (A/B)
+#define INA_GEMM_SCHED 2  // operand staging schedule (kstep): 2 two phases per K-step (default: 4-8% over 1),
+                          // 1 balanced four phases, 0 front-loaded four phases
 #endif
 #ifndef INA_GEMM_DIAG
 #define INA_GEMM_DIAG 0  // 1: no operand staging inside the K loop (diagnostic of the MFMA/LDS/barrier skeleton)
@@ -171,6 +172,7 @@ struct Stager {
 template <int N>
 INA_DEVICE void wait_vm() {
   if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -208,6 +210,35 @@ INA_DEVICE void kstep(f32x4_t (&acc)[8][4], Frags& f, const Stager& sg, bool ful
       fb[j][1] = ldsr(img + rdB1 + j * 16 * 128);
     }
   };
+  if constexpr (INA_GEMM_SCHED == 2) {
+    // two phases of 32 MFMAs (4 barriers per K-step instead of 8):
+    // X: A0 / B0 / B1 subtiles, quadrants (A0,B0) (A0,B1); stage A1 of s+1; A1 of s must land before Y
+    read_b(f.b0, 0);
+    read_b(f.b1, 1);
+    read_a(f.a0, 0);
+    if (st1) sg.stage(OTHER, 1, p1.m, p1.n, p1.k);
+    wait_lgkm0();
+    if (full) wait_vm<8>(); else wait_vm<0>();
+    barrier();
+    mma_quadrant<0, 0>(acc, f.a0, f.b0);
+    mma_quadrant<0, 1>(acc, f.a0, f.b1);
+    barrier();
+    // Y: A1 subtile, quadrants (A1,B1) (A1,B0); restage A0 / B0 / B1 (read in X) with s+2; A0 / B0 / B1 of
+    // s+1 must land before its X
+    read_a(f.a1, 1);
+    if (st2) {
+      sg.stage(BUF, 0, p2.m, p2.n, p2.k);
+      sg.stage(BUF, 2, p2.m, p2.n, p2.k);
+      sg.stage(BUF, 3, p2.m, p2.n, p2.k);
+    }
+    wait_lgkm0();
+    if (full) wait_vm<8>(); else wait_vm<0>();
+    barrier();
+    mma_quadrant<1, 1>(acc, f.a1, f.b1);
+    mma_quadrant<1, 0>(acc, f.a1, f.b0);
+    barrier();
+    return;
+  }
   // p0: A0 / B0 subtiles; B1 of this step must have landed before p1 reads it
   read_b(f.b0, 0);
   read_a(f.a0, 0);
@@ -381,7 +412,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_bf16_nt_kernel(GemmArgs g) 
     if (!INA_GEMM_SCHED || p == 0) sg.stage(p, 1, p2.m, p2.n, p2.k);
     adv2();
   }
-  if (S > 1) wait_vm<INA_GEMM_SCHED ? 10 : 12>(); else wait_vm<0>();
+  if (S > 1) wait_vm<INA_GEMM_SCHED == 2 ? 8 : (INA_GEMM_SCHED ? 10 : 12)>(); else wait_vm<0>();
   barrier();
   if (INA_GEMM_STAGGER && wr == 1) barrier();  // ping-pong: row group 1 runs one barrier behind row group 0
 
