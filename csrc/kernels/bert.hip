@@ -29,6 +29,15 @@ using namespace ina;
 namespace {
 
 constexpr float LN_EPS = 1e-12f;
+
+#define INA_PRAGMA(x) _Pragma(#x)
+#define INA_UNROLL(n) INA_PRAGMA(unroll n)
+#ifndef INA_MHA_KTU
+#define INA_MHA_KTU 1   // mha_bwd key-tile loop unroll (A/B)
+#endif
+#ifndef INA_MHA_QPU
+#define INA_MHA_QPU 1   // mha_bwd query-pair loop unroll (A/B)
+#endif
 constexpr float LOG2E = 1.4426950408889634f;
 
 INA_DEVICE void ld4(const unsigned short* p, float* v) {
@@ -654,7 +663,7 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
   const float c2 = 0.125f * LOG2E;
   const float scale = 0.125f;
   // phase 1: each wave owns key tiles kt = wave, wave + 4
-#pragma unroll 1
+INA_UNROLL(INA_MHA_KTU)
   for (int kt = wave; kt < NT; kt += 4) {
     const int key = 16 * kt + n;
     const bool kok = key < L;
@@ -669,7 +678,7 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
     f32x4_t dV[4], dK[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dV[dt] = dK[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
+INA_UNROLL(INA_MHA_QPU)
     for (int qp = 0; qp < NT / 2; ++qp) {
       float pp[2][4], ds[2][4];
 #pragma unroll
