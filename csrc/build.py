@@ -43,7 +43,11 @@ ARCH = os.environ.get("INA_OFFLOAD_ARCH", "gfx950")
 # vectoriser there: its v_pk_fma_f32 broadcasts pair a scalar with whatever register sits next to it,
 # and the wait-count pass then treats a prefetch landing in that neighbour as a dependency (a
 # vmcnt(0) in the middle of the backward's step); 444 vs 464 us forward, 746 vs 756 us backward.
-FILE_FLAGS = {"rec_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"]}
+# lstm.hip: no SLP vectoriser either -- its packed v_pk_mul / v_pk_fma f32 next to the recurrences' MFMAs
+# cost more issue cycles than the scalar forms (MI355X_MICROARCH: packed f32 beside MFMAs is an
+# anti-lever): 1,925,812 / 1,897,512 vs 1,886,461 / 1,885,572 episodes/s same box (profiles/r4_noslp).
+FILE_FLAGS = {"rec_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"],
+              "lstm.hip": ["-fno-slp-vectorize"]}
 
 
 def _torch_paths():
