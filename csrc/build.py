@@ -46,8 +46,10 @@ ARCH = os.environ.get("INA_OFFLOAD_ARCH", "gfx950")
 # lstm.hip: no SLP vectoriser either -- its packed v_pk_mul / v_pk_fma f32 next to the recurrences' MFMAs
 # cost more issue cycles than the scalar forms (MI355X_MICROARCH: packed f32 beside MFMAs is an
 # anti-lever): 1,925,812 / 1,897,512 vs 1,886,461 / 1,885,572 episodes/s same box (profiles/r4_noslp).
+# routing.hip likewise (fwd 31 -> 26 us, bwd 87 -> 80 us; ntn.hip measured mixed: fwd -8, bwd +16 us, kept;
+# profiles/r4_noslp/noslp2).
 FILE_FLAGS = {"rec_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"],
-              "lstm.hip": ["-fno-slp-vectorize"]}
+              "lstm.hip": ["-fno-slp-vectorize"], "routing.hip": ["-fno-slp-vectorize"]}
 
 
 def _torch_paths():
