@@ -49,7 +49,8 @@ ARCH = os.environ.get("INA_OFFLOAD_ARCH", "gfx950")
 # routing.hip likewise (fwd 31 -> 26 us, bwd 87 -> 80 us; ntn.hip measured mixed: fwd -8, bwd +16 us, kept;
 # profiles/r4_noslp/noslp2).
 FILE_FLAGS = {"rec_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"],
-              "lstm.hip": ["-fno-slp-vectorize"], "routing.hip": ["-fno-slp-vectorize"]}
+              "lstm.hip": ["-fno-slp-vectorize"], "routing.hip": ["-fno-slp-vectorize"],
+              "bert.hip": ["-fno-slp-vectorize"]}   # BERT 108.75 / 108.75 vs 108.37 / 108.29 (r4_noslp/noslp3)
 
 
 def _torch_paths():
