@@ -85,7 +85,8 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd_impl(
     const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U, int64_t NX, bool bf16,
     bool store_c, int64_t seed, double keep_prob, const std::optional<Tensor>& seed_dev,
     const std::optional<Tensor>& wrows, bool natural, const std::optional<Tensor>& tlen = std::nullopt,
-    const std::optional<Tensor>& slen = std::nullopt, const std::optional<Tensor>& perm = std::nullopt) {
+    const std::optional<Tensor>& slen = std::nullopt, const std::optional<Tensor>& perm = std::nullopt,
+    bool direct_x = false) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -127,7 +128,12 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd_impl(
   Tensor dmask = want_mask ? at::empty({ntiles, 2, L, 64}, word.options().dtype(at::kByte))
                            : at::empty({0}, word.options().dtype(at::kByte));
   TORCH_CHECK(ntiles * L * (64 * NX + 16) < (1LL << 31), "ina.lstm_fwd: batch too large for the x rows");
-  Tensor xg = bf16 ? at::empty({ntiles * L * (64 * NX + 16)}, word.options().dtype(at::kBFloat16))
+  // direct x (record path, NX == 4, shifted position ids, word rows): the recurrences read the word rows and
+  // LDS position tables themselves; xg then holds only x_gather's position ids [tiles][L][16]
+  const bool has_wrows = wrows.has_value() && wrows->defined() && wrows->numel() > 0;
+  TORCH_CHECK(!direct_x || (bf16 && !natural && NX == 4 && has_wrows),
+              "ina.lstm_fwd: direct x needs the bf16 record path, NX == 4 and word rows");
+  Tensor xg = bf16 ? at::empty({ntiles * L * ((direct_x ? 0 : 64 * NX) + 16)}, word.options().dtype(at::kBFloat16))
                    : at::empty({0}, word.options().dtype(at::kBFloat16));
   if (S == 0) return {hlane, cst, hnat, dmask, xg};
   ina::LstmArgs a{};
@@ -156,19 +162,22 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd_impl(
   a.inv_kp = (float)(1.0 / keep_prob);
   a.drop = drop ? 1 : 0;
   a.wrows = nullptr;
-  if (wrows.has_value() && wrows->defined() && wrows->numel() > 0) {
+  if (has_wrows) {
     check(*wrows, "wrows", at::kBFloat16);
     TORCH_CHECK(wrows->numel() == word.numel() * 8 && E <= 8, "ina.lstm_fwd: wrows must be bf16 [NI * L, 8] (E <= 8)");
+    TORCH_CHECK(wrows->numel() * 2 < (1LL << 31), "ina.lstm_fwd: word rows exceed a buffer descriptor");
     a.wrows = wrows->data_ptr();
+    a.wbytes = (uint32_t)(wrows->numel() * 2);
   }
+  a.xd = direct_x ? 1 : 0;
   a.tlen = ragged_arg(tlen, ntiles, "tlen");
   a.slen = ragged_arg(slen, S, "slen");
   a.perm = ragged_arg(perm, S, "perm");
   TORCH_CHECK(!a.tlen || (bf16 && !natural), "ina.lstm_fwd: ragged tiles need the bf16 record path");
   TORCH_CHECK(!a.slen || a.tlen, "ina.lstm_fwd: slen needs tlen");
   if (bf16) {
-    a.xg = xg.data_ptr();
-    a.posb = reinterpret_cast<const unsigned short*>(xg.data_ptr<at::BFloat16>() + ntiles * L * 64 * NX);
+    a.xg = direct_x ? nullptr : xg.data_ptr();
+    a.posb = reinterpret_cast<const unsigned short*>(xg.data_ptr<at::BFloat16>() + (direct_x ? 0 : ntiles * L * 64 * NX));
     check_launch(ina::x_gather(a, (int)U, (int)NX, cur_stream()), "x_gather");
   }
   check_launch(ina::lstm_fwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_fwd");
@@ -198,7 +207,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> lstm_attn_fwd
     const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack, const Tensor& bias, int64_t U, int64_t NX,
     bool store_c, int64_t seed, double keep_prob, const std::optional<Tensor>& seed_dev,
     const std::optional<Tensor>& wrows, const Tensor& mask, const Tensor& w1r, const Tensor& b1, const Tensor& w2,
-    const std::optional<Tensor>& tlen, const std::optional<Tensor>& perm, const std::optional<Tensor>& slen) {
+    const std::optional<Tensor>& tlen, const std::optional<Tensor>& perm, const std::optional<Tensor>& slen,
+    bool direct_x) {
   check(mask, "mask", at::kInt);
   check(w1r, "w1r", at::kBFloat16);
   check(b1, "b1", at::kFloat);
@@ -211,7 +221,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> lstm_attn_fwd
   TORCH_CHECK(w1r.numel() == MT * NKR * 64 * 8, "ina.lstm_attn_fwd: w1r pack size");
   const bool drop = keep_prob < 1.0;
   auto r = lstm_fwd_impl(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, bias, U, NX, true, store_c, seed, keep_prob,
-                         seed_dev, wrows, false, tlen, slen, perm);
+                         seed_dev, wrows, false, tlen, slen, perm, direct_x);
   auto e = at::empty({S, 2 * U}, b1.options());
   auto alphas = at::empty({S, L}, b1.options());
   if (S == 0) return {std::get<0>(r), std::get<1>(r), std::get<2>(r), std::get<3>(r), std::get<4>(r), e, alphas};
@@ -307,7 +317,8 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
     const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack, const Tensor& a2pack, const Tensor& bias,
     const Tensor& hraw, const Tensor& cst, const Tensor& dH, const Tensor& dmask, const Tensor& xg, int64_t U, int64_t NX,
     bool bf16, bool word_grad, int64_t blocks, int64_t seed, double keep_prob, bool pos_shift,
-    const std::optional<Tensor>& tlen, const std::optional<Tensor>& slen, const FaIn* fa) {
+    const std::optional<Tensor>& tlen, const std::optional<Tensor>& slen, const FaIn* fa,
+    const std::optional<Tensor>& wrows = std::nullopt) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -367,9 +378,18 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
   // [2 dir][tiles][L][2PD + 1][16] bf16 dx of the pos features (+ a trash row for the other lanes)
   Tensor dxp = (bf16 && !pos_lds) ? at::empty({2 * (2 * PD + 1) * ntiles * L * 16}, opt.dtype(at::kBFloat16))
                                   : at::empty({0}, opt);
+  // direct x (lstm_attn_fwd with direct_x): xg holds only the position ids, x comes from the word rows
+  const bool direct_x = bf16 && xg.numel() == ntiles * L * 16;
   if (bf16) {
     check(xg, "xg", at::kBFloat16);
-    TORCH_CHECK(xg.numel() == ntiles * L * (64 * NX + 16), "ina.lstm_bwd: xg (from lstm_fwd) shape");
+    TORCH_CHECK(direct_x || xg.numel() == ntiles * L * (64 * NX + 16), "ina.lstm_bwd: xg (from lstm_fwd) shape");
+  }
+  if (direct_x) {
+    TORCH_CHECK(wrows.has_value() && wrows->defined() && wrows->numel() == word.numel() * 8,
+                "ina.lstm_bwd: direct x needs the forward's word rows");
+    check(*wrows, "wrows", at::kBFloat16);
+    TORCH_CHECK(fa == nullptr && !pos_lds && dh_lane && NX == 4 && wrows->numel() * 2 < (1LL << 31),
+                "ina.lstm_bwd: direct x runs in the lean lane-layout BPTT only");
   }
   Tensor dwemb = word_grad ? at::zeros_like(wemb) : at::empty({0}, opt);
   const int64_t H2 = 2 * U;
@@ -445,9 +465,12 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
     a.perm = ragged_arg(fa->perm, S, "perm");
     a.aslab = aslab.data_ptr<float>();
   }
-  a.xg = bf16 ? xg.data_ptr() : nullptr;
-  a.posb = bf16 ? reinterpret_cast<const unsigned short*>(xg.data_ptr<at::BFloat16>() + ntiles * L * 64 * NX)
+  a.xg = (bf16 && !direct_x) ? xg.data_ptr() : nullptr;
+  a.posb = bf16 ? reinterpret_cast<const unsigned short*>(xg.data_ptr<at::BFloat16>() + (direct_x ? 0 : ntiles * L * 64 * NX))
                 : nullptr;
+  a.xd = direct_x ? 1 : 0;
+  a.wrows = direct_x ? wrows->data_ptr() : nullptr;
+  a.wbytes = direct_x ? (uint32_t)(wrows->numel() * 2) : 0u;
   check_launch(ina::lstm_bwd(a, (int)U, (int)NX, bf16, cur_stream()), "lstm_bwd");
   if (shift) {
     Tensor gpart = at::empty({(int64_t)ina::pos_shift_workspace_floats((int)S, (int)L, (int)PD, nullptr, nullptr)}, opt);
@@ -466,9 +489,9 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& wo
                                             const Tensor& dmask, const Tensor& xg, int64_t U, int64_t NX, bool bf16,
                                             bool word_grad, int64_t blocks, int64_t seed, double keep_prob,
                                             bool pos_shift, const std::optional<Tensor>& tlen,
-                                            const std::optional<Tensor>& slen) {
+                                            const std::optional<Tensor>& slen, const std::optional<Tensor>& wrows) {
   auto r = lstm_bwd_impl(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hraw, cst, dH, dmask, xg, U, NX,
-                         bf16, word_grad, blocks, seed, keep_prob, pos_shift, tlen, slen, nullptr);
+                         bf16, word_grad, blocks, seed, keep_prob, pos_shift, tlen, slen, nullptr, wrows);
   return {std::get<0>(r), std::get<1>(r), std::get<2>(r)};
 }
 

@@ -62,6 +62,12 @@ struct LstmArgs {
   // bf16 lean BPTT with shifted position ids (pos[s][t] = pos[s][0] + t): the position-table gradients are
   // summed in LDS inside lstm_bwd -> dpos_slab [bwd_blocks][2 dir][2 tables][2L][PD] (no dxp, no pos_grad)
   int pos_lds;
+  // direct x (bf16 record path, NX == 4, shifted position ids, wrows given): lstm_fwd / lstm_bwd read each
+  // token's word features straight from wrows (q-interleaved rows [f0 f4 f1 f5 f2 f6 f3 f7], one dword per
+  // lane-step) and its position features from block-resident LDS tables at o_s + t; x_gather then writes
+  // only posb / dmask (no xg record).  wbytes = wrows' size in bytes (buffer range: rows past it read 0)
+  int xd;
+  uint32_t wbytes;
 };
 // bf16 mode: gather every token's x features once into a.xg / a.posb, and (a.drop) the dropout keep
 // bits into a.dmask (lstm.hip x_gather_kernel); must run before lstm_fwd in bf16 mode
@@ -80,7 +86,10 @@ int pos_grad(const LstmArgs& a, int blocks, float* slab, hipStream_t st);
 size_t pos_shift_workspace_floats(int S, int L, int PD, int* nchunk, int* kps);
 int pos_grad_shift(const LstmArgs& a, float* gpart, float* out, hipStream_t st);
 bool lstm_supported(int U, int NX);
-size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fused_attn = false, bool pos_lds = false);
+size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fused_attn = false, bool pos_lds = false,
+                          bool direct_x = false);
+// direct-x position tables in LDS: [4 lane groups q][2 tables][3L rows][4 slots] bf16 (rows >= 2L zero)
+inline size_t xd_table_bytes(int L) { return (size_t)4 * 2 * 3 * L * 4 * 2; }
 
 struct AttnArgs {
   const void* hraw;

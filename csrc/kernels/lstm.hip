@@ -246,7 +246,9 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
     const long r = rb + min(t, L - 1);
     p1c[c] = pos1[r];
     p2c[c] = pos2[r];
-    // DIRECT: the token's word row as one 16-byte load of 8 bf16 (E <= 8, zero padded)
+    // DIRECT: the token's word row as one 16-byte load of 8 bf16 (E <= 8, zero padded, q-interleaved:
+    // feature f at 2 (f & 3) + (f >> 2)).  xg == nullptr (direct-x recurrences): ids / keep bits only
+    if (xg == nullptr) continue;
     if constexpr (DIRECT) wrc[c] = *reinterpret_cast<const u16x8_t*>(wrows + r * 8);
     else widc[c] = word[r];
   }
@@ -259,6 +261,7 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
   const int t = (blockIdx.y * XG_C + c) * XG_T + (threadIdx.x >> 4);
   if (t >= L) break;   // t grows with c
   const int p1 = p1c[c], p2 = p2c[c];
+  if (xg != nullptr) {   // uniform
   const float* p1row = ptab + p1 * PD;
   const float* p2row = ptab + PTN + p2 * PD;
   u16x8_t wr = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
 #pragma unroll
   for (int f = 0; f < 4 * NX; ++f) {   // E, PD are kernel arguments: the source branches are uniform
     float wv = 0.f;
-    if (f < E) wv = DIRECT ? bf2f(wr[f < 8 ? f : 0]) : wrow[f];
+    if (f < E) wv = DIRECT ? bf2f(wr[f < 8 ? 2 * (f & 3) + (f >> 2) : 0]) : wrow[f];
     x[f] = f < E ? wv : (f < E + PD ? p1row[f - E] : (f < DIN ? p2row[f - E - PD] : 0.f));
   }
   unsigned short* dst = xg + (size_t)(tile * L + t) * 64 * NX;
@@ -281,6 +284,7 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
     for (int c = 0; c < NX / 4; ++c)
       *reinterpret_cast<u16x4_t*>(dst + (q * 16 + n) * NX + 4 * c) =
           u16x4_t{v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
+  }
   }
   posb[(size_t)(tile * L + t) * 16 + n] = (unsigned short)(p1 | (p2 << 8));
   if (dmask) {   // uniform
@@ -311,13 +315,36 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
 }
 
 // ------------------------------------------------------------------------------------------
+// direct x (LstmArgs::xd; verdict r3 #6: x_gather's 485 MB xg record and its four re-reads per step go
+// away).  The word features come from the per-token word rows (ops/encoder.py::word_rows, q-interleaved
+// [f0 f4 f1 f5 f2 f6 f3 f7]: lane group q's two slots xi = 0, 1 are ONE dword at byte 4q of the token's
+// 16-byte row; a sequence's rows are contiguous, so a 128-byte line serves 8 steps).  The position
+// features come from block-resident LDS tables, since the ids are shifted aranges (pos = o_s + t):
+//   T[(q * 2 + tb) * 3L + r][xi] = bf16 of feature 4 xi + q if it is a column of position table tb, row r
+//                                  (else 0); rows 2L .. 3L-1 are zero (padding sequences: o = 2L)
+// A lane reads its two 8-byte entries at rows o1 + t / o2 + t and ORs them into the word dword: every slot
+// is nonzero in at most one of the three sources, so the operand bits equal x_gather's.
+// ------------------------------------------------------------------------------------------
+__device__ inline void xd_build(unsigned short* T, int L, int E, int PD, const float* __restrict__ p1emb,
+                                const float* __restrict__ p2emb) {
+  const int R = 3 * L, N = 4 * 2 * R * 4;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    const int xi = i & 3, r = (i >> 2) % R, qt = (i >> 2) / R, tb = qt & 1, q = qt >> 1;
+    const int c = 4 * xi + q - E - tb * PD;
+    float v = 0.f;
+    if (r < 2 * L && c >= 0 && c < PD) v = (tb ? p2emb : p1emb)[r * PD + c];
+    T[i] = f2bf(v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------
 // DROP / STORE are compile-time so the step loop has no branches: the waitcnt pass can then count
 // the stores issued after each prefetch and wait only for the prefetched loads.
 // SKIP (bf16): sequence_length semantics for the backward direction (lstm_skip_padding): it starts at the
 // tile's longest length and each row's state is reset to zero past its own length (TF dynamic_rnn)
-template <int U, int NX, bool BF16, bool DROP, bool STORE, bool SKIP = false>
+template <int U, int NX, bool BF16, bool DROP, bool STORE, bool SKIP = false, bool XD = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void lstm_fwd_kernel(
     const int* __restrict__ inst, int S, const int* __restrict__ word, const int* __restrict__ pos1,
     const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
@@ -326,7 +353,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     typename FragT<BF16>::elem* __restrict__ hlane, typename CT<BF16>::type* __restrict__ cst,
     typename FragT<BF16>::elem* __restrict__ hnat, unsigned char* __restrict__ dmask, uint32_t seed, uint32_t thr,
     float inv_kp, int drop, const int* __restrict__ seed_dev, const unsigned short* __restrict__ xg,
-    const int* __restrict__ tlen, const int* __restrict__ slen) {
+    const int* __restrict__ tlen, const int* __restrict__ slen, const unsigned short* __restrict__ wrows,
+    uint32_t wbytes) {
+  static_assert(!XD || (BF16 && NX == 4), "direct x: bf16, 4 x slots per lane");
   if (seed_dev) seed = (uint32_t)seed_dev[0];   // device-resident dropout seed (HIP-graph replay)
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
@@ -339,6 +368,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   const int ntiles = (S + 15) / 16;
   const int tile = blockIdx.x * 4 + wave;
   int2* ids = ids_all + wave * 16 * L;
+  if constexpr (XD) {   // the block's position tables (before any wave leaves)
+    xd_build(reinterpret_cast<unsigned short*>(ids_all), L, E, PD, p1emb, p2emb);
+    __syncthreads();
+  }
   constexpr bool FG = !BF16;   // fp32 mode gathers x per step
   if constexpr (FG) {
     // fp32 mode gathers x per step: stage (word, pos1 | pos2 << 16) of the wave's 16 sequences into LDS
@@ -501,6 +534,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   // bf16: the ping-pong buffers hold the RAW x_gather rows, converted inside the step: converting at
   // the load made the compiler wait for it right there (s_waitcnt vmcnt(0), which also drained the
   // previous step's record stores), i.e. no prefetch at all
+  if constexpr (XD) {
+    // direct x: per step one dword of the token's word row (buffer load; padding sequences read past the
+    // range -> 0) and two 8-byte LDS table entries, prefetched one step ahead like the xg rows below
+    const bool valid = seq < S;
+    const int rb0 = inst[valid ? seq : S - 1] * L;
+    const uint32_t wvo = valid ? (uint32_t)rb0 * 16u + 4u * (uint32_t)q : 0x80000000u;
+    const int R = 3 * L;
+    const int o1 = valid ? pos1[rb0] : 2 * L, o2 = valid ? pos2[rb0] : 2 * L;
+    const char* tb1 = reinterpret_cast<const char*>(ids_all) + ((q * 2) * R + o1) * 8;
+    const char* tb2 = reinterpret_cast<const char*>(ids_all) + ((q * 2 + 1) * R + o2) * 8;
+    const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(wrows), (short)0, (int)wbytes,
+                                                      0x00020000);
+    struct XR {
+      uint32_t w;
+      uint64_t a, b;
+    };
+    XR ra, rb;
+    auto load_xr = [&](int t, XR& r) __attribute__((always_inline)) {
+      // (t is wave-uniform but derived from the wave index: without readfirstlane the soffset operand got a
+      // waterfall loop per load)
+      r.w = __builtin_amdgcn_raw_buffer_load_b32(rw, wvo, __builtin_amdgcn_readfirstlane(t * 16), 0);
+      r.a = *reinterpret_cast<const uint64_t*>(tb1 + t * 8);
+      r.b = *reinterpret_cast<const uint64_t*>(tb2 + t * 8);
+    };
+    auto step_xr = [&](const int tau, const XR& r0) __attribute__((always_inline)) {
+      XR r = r0;
+      asm volatile("" : "+v"(r.w), "+v"(r.a), "+v"(r.b));
+      const uint32_t w0 = r.w | (uint32_t)r.a | (uint32_t)r.b;
+      const uint32_t w1 = (uint32_t)(r.a >> 32) | (uint32_t)(r.b >> 32);
+      float xv[4] = {bf2f((unsigned short)w0), bf2f((unsigned short)(w0 >> 16)), bf2f((unsigned short)w1),
+                     bf2f((unsigned short)(w1 >> 16))};
+      step(tau, xv);
+    };
+    auto xpair = [&](int tau) __attribute__((always_inline)) {
+      load_xr(tof(tau + 1), rb);
+      __builtin_amdgcn_sched_barrier(0);
+      step_xr(tau, ra);
+      __builtin_amdgcn_sched_barrier(0);
+      load_xr(tof(min(tau + 2, te - 1)), ra);
+      __builtin_amdgcn_sched_barrier(0);
+      step_xr(tau + 1, rb);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    load_xr(tof(tb), ra);
+    int tau = tb;
+    if (te - tb >= 2) {
+      xpair(tb);
+      tau = tb + 2;
+    }
+    for (; tau + 1 < te; tau += 2) xpair(tau);
+    if (tau < te) step_xr(tau, ra);
+    return;
+  }
   if constexpr (!FG) {
     u16x4_t ra[NX / 4], rb[NX / 4];
     auto load_raw = [&](int t, u16x4_t* r) {
@@ -661,7 +747,9 @@ struct BwdWaves {
 // pos-feature gradients into its own LDS copy of the two position tables (ds_add_f32 at o_s + t), summed
 // over the workgroup's waves in a fixed order into dpos_slab [blocks][2 dir][2 tables][2L][PD] -- no
 // per-token dx rows in HBM and no separate reduction kernel.
-template <int U, int NX, bool BF16, bool WG = false, bool PM = false, bool FA = false, bool PL = false>
+// XD (with PM, not FA / PL): direct x -- word features from the word rows, position features from LDS
+// tables (see xd_build); no xg record.
+template <int U, int NX, bool BF16, bool WG = false, bool PM = false, bool FA = false, bool PL = false, bool XD = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U, NX, FA>::value))) void lstm_bwd_kernel(
     const int* __restrict__ inst, int S, const int* __restrict__ word, const int* __restrict__ pos1,
     const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
@@ -672,9 +760,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     float* __restrict__ dw_slab,
     float* __restrict__ dpos_slab, float* __restrict__ dwemb, const unsigned char* __restrict__ dmask, uint32_t seed,
     uint32_t thr, float inv_kp, int drop, unsigned short* __restrict__ dxp, const unsigned short* __restrict__ xg,
-    int dh_lane, const int* __restrict__ tlen, const int* __restrict__ slen, int wblank, AttnFuse af) {
+    int dh_lane, const int* __restrict__ tlen, const int* __restrict__ slen, int wblank, AttnFuse af,
+    const unsigned short* __restrict__ wrows, uint32_t wbytes) {
   static_assert(!FA || (BF16 && PM), "the fused attention backward runs in the lean bf16 BPTT");
   static_assert(!PL || (BF16 && PM), "LDS position-table gradients run in the lean bf16 BPTT");
+  static_assert(!XD || (BF16 && PM && !FA && !PL && NX == 4), "direct x runs in the lean bf16 BPTT (4 x slots)");
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
   using elem = typename FragT<BF16>::elem;
@@ -749,6 +839,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   float* plR = plAll + (size_t)wave * PLN;
   if constexpr (PL)
     for (int i = lane; i < PLN; i += 64) plR[i] = 0.f;
+  // XD: the block's direct-x position tables (lstm_bwd_lds_bytes mirrors this offset)
+  char* xdT = reinterpret_cast<char*>(smem) + ((pl_off + (PL ? (size_t)4 * PLN * 4 : 0) + 15) & ~(size_t)15);
+  if constexpr (XD) xd_build(reinterpret_cast<unsigned short*>(xdT), L, E, PD, p1emb, p2emb);
   if constexpr (FA) {
     for (int i = threadIdx.x; i < FS::NAP; i += 256) lAp[i] = af.w1f[(size_t)dir * FS::NAP + i];
     for (int i = threadIdx.x; i < FS::NAPT; i += 256) lApt[i] = af.w1ft[(size_t)dir * FS::NAPT + i];
@@ -1049,7 +1142,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
                             (uint32_t)Lt * DSTEPB);
       const bool lane_reset = slen != nullptr && dir == 1;   // sequence_length semantics (backward direction)
       const int mylen = slen != nullptr ? (valid ? slen[seq] : 0) : L;
-      const auto rx = rsrc(xg + (size_t)tu * L * 64 * NX, (uint32_t)L * XSTEPB);
+      const auto rx = rsrc(XD ? (const unsigned short*)wrows : xg + (size_t)tu * L * 64 * NX,
+                           XD ? wbytes : (uint32_t)L * XSTEPB);
+      // XD: the lane's word-row dword (padding rows: past the range -> 0) and position-table entries
+      const uint32_t wvo = valid ? (uint32_t)rowbase * 16u + 4u * (uint32_t)q : 0x80000000u;
+      const char* xtb1 = xdT + ((q * 2) * 3 * L + (valid ? pos1[rowbase] : 2 * L)) * 8;
+      const char* xtb2 = xdT + ((q * 2 + 1) * 3 * L + (valid ? pos2[rowbase] : 2 * L)) * 8;
       const auto rdx = rsrc(dxp + ((size_t)dir * ntiles + tu) * L * (NPF + 1) * 16, (uint32_t)L * PSTEPB);
       const int vl2 = lane * 2, vx = lane * NX * 2;
       // ---- PL: the lane's position-table slot at t = 0 per x feature (shifted ids: pos = o + t); word /
@@ -1096,6 +1194,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       struct Raw {
         uint32_t h[U4], c[U4], d[U4];   // 16-bit loads (upper halves never read)
         uint32_t x[NXW];
+        uint64_t pa, pb;                // XD: position-table entries (x[0] = the word dword until bstep)
         uint32_t oh[U4], ko, kt, al;    // FA: other direction's h, keep bytes, alpha of the predecessor time
       };
       auto rload = [&](int tau, Raw& o) __attribute__((always_inline)) {
@@ -1115,11 +1214,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
           o.kt = __builtin_amdgcn_raw_buffer_load_b8(rkb, vkt, tp * 64, 0);
           o.al = __builtin_amdgcn_raw_buffer_load_b32(ral, val, tp * 4, 0);
         }
+        if constexpr (XD) {
+          o.x[0] = __builtin_amdgcn_raw_buffer_load_b32(rx, wvo, tn * 16, 0);
+          o.pa = *reinterpret_cast<const uint64_t*>(xtb1 + tn * 8);
+          o.pb = *reinterpret_cast<const uint64_t*>(xtb2 + tn * 8);
+        } else {
 #pragma unroll
-        for (int k = 0; k < NXW / 2; ++k) {
-          const auto v = __builtin_amdgcn_raw_buffer_load_b64(rx, vx + 8 * k, sx, 0);
-          o.x[2 * k] = (uint32_t)v[0];
-          o.x[2 * k + 1] = (uint32_t)v[1];
+          for (int k = 0; k < NXW / 2; ++k) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rx, vx + 8 * k, sx, 0);
+            o.x[2 * k] = (uint32_t)v[0];
+            o.x[2 * k + 1] = (uint32_t)v[1];
+          }
         }
       };
       auto pkf = [](float a, float b) {   // two floats -> packed bf16 pair (one v_cvt_pk_bf16_f32)
@@ -1240,8 +1345,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
           else asm volatile("" : "+v"(X.d[m]));
         }
         if constexpr (FA) asm volatile("" : "+v"(X.ko), "+v"(X.kt), "+v"(X.al));
+        if constexpr (XD) {   // word dword | the two table entries (disjoint nonzero slots)
+          asm volatile("" : "+v"(X.x[0]), "+v"(X.pa), "+v"(X.pb));
+          X.x[0] |= (uint32_t)X.pa | (uint32_t)X.pb;
+          X.x[1] = (uint32_t)(X.pa >> 32) | (uint32_t)(X.pb >> 32);
+        } else {
 #pragma unroll
-        for (int k = 0; k < NXW; ++k) asm volatile("" : "+v"(X.x[k]));
+          for (int k = 0; k < NXW; ++k) asm volatile("" : "+v"(X.x[k]));
+        }
         const int t = tof(tau);
         // slot words [h (U4) ; x (NX slots) ; 0]: the gate B operand and the dW image row.  Slot s is the
         // 16-bit half `off` (byte 0 or 2, -1 = zero) of register word `wd`; a pair word is ONE v_perm.
@@ -1914,7 +2025,7 @@ namespace ina {
 
 
 // mirrors the kernel's LDS carve (lstm_bwd_kernel)
-size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fa, bool pl) {
+size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fa, bool pl, bool xd) {
   const int KPL = bf16 ? 8 : 1;
   const int U4 = U / 4, NSLOT = U4 + NX;
   const int NA = U4 * ((NSLOT + KPL - 1) / KPL) * 64;
@@ -1939,6 +2050,7 @@ size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fa, bool
   if (fa) off += (size_t)(MT * NKR * 64 + NTD * NKS2 * 64) * 16 + 2 * MT * 16 * 4 + (size_t)4 * 16 * (HCPA + JCPA) * 2;
   off = (off + 15) & ~(size_t)15;
   if (pl) off += (size_t)4 * (2 * 2 * L * PD + 64) * 4;   // per-wave position tables + per-lane trash slots
+  if (xd) off = ((off + 15) & ~(size_t)15) + xd_table_bytes(L);   // direct-x position tables
   return off;
 }
 
@@ -1948,7 +2060,10 @@ static int launch_fwd_t(const LstmArgs& a, hipStream_t st) {
   using elem = typename FragT<BF16>::elem;
   const int ntiles = (a.S + 15) / 16;
   dim3 grid((ntiles + 3) / 4, 2);
-  size_t lds = BF16 ? 0 : (size_t)4 * 16 * a.L * sizeof(int2);   // fp32: token ids
+  constexpr bool XDC = BF16 && NX == 4;   // the direct-x kernels exist for 4 x slots per lane only
+  const bool xd = XDC && a.xd;
+  if (a.xd && !xd) return -1;
+  size_t lds = xd ? xd_table_bytes(a.L) : (BF16 ? 0 : (size_t)4 * 16 * a.L * sizeof(int2));   // fp32: token ids
   const bool store = a.hraw != nullptr && a.cst != nullptr;
   // bf16: the keep bits come from x_gather_kernel (x_gather must run first); fp32 hashes them here
   const bool drop = a.drop && !BF16;
@@ -1956,10 +2071,16 @@ static int launch_fwd_t(const LstmArgs& a, hipStream_t st) {
                    : (store ? lstm_fwd_kernel<U, NX, BF16, false, true> : lstm_fwd_kernel<U, NX, BF16, false, false>);
   if (BF16 && a.slen)   // sequence_length semantics (lstm_skip_padding)
     kern = store ? lstm_fwd_kernel<U, NX, BF16, false, true, BF16> : lstm_fwd_kernel<U, NX, BF16, false, false, BF16>;
+  if (xd)
+    kern = a.slen ? (store ? lstm_fwd_kernel<U, NX, BF16, false, true, BF16, XDC>
+                           : lstm_fwd_kernel<U, NX, BF16, false, false, BF16, XDC>)
+                  : (store ? lstm_fwd_kernel<U, NX, BF16, false, true, false, XDC>
+                           : lstm_fwd_kernel<U, NX, BF16, false, false, false, XDC>);
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, a.bias, (elem*)a.hraw,
                      (typename CT<BF16>::type*)a.cst, (elem*)a.hdrop, a.dmask, a.seed, a.thr, a.inv_kp, a.drop, a.seed_dev,
-                     (const unsigned short*)a.xg, BF16 ? a.tlen : nullptr, BF16 ? a.slen : nullptr);
+                     (const unsigned short*)a.xg, BF16 ? a.tlen : nullptr, BF16 ? a.slen : nullptr,
+                     (const unsigned short*)a.wrows, a.wbytes);
   INA_CHECK_LAUNCH();
   return 0;
 }
@@ -1973,7 +2094,10 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   const bool fa = BF16 && a.aslab != nullptr;
   const bool pm = INA_LSTM_PM && BF16 && (a.dh_lane || fa);
   const bool pl = pm && a.pos_lds;
-  size_t lds = lstm_bwd_lds_bytes(U, NX, BF16, a.L, a.PD, fa, pl);
+  constexpr bool XDC = BF16 && NX == 4;   // the direct-x kernels exist for 4 x slots per lane only
+  const bool xd = XDC && pm && !fa && !pl && a.xd;
+  if (a.xd && !xd) return -1;
+  size_t lds = lstm_bwd_lds_bytes(U, NX, BF16, a.L, a.PD, fa, pl, xd);
   constexpr bool P = BF16;   // the PM / FA / PL kernels exist in bf16 mode only
   auto kfn = pm ? (a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, P> : lstm_bwd_kernel<U, NX, BF16, false, P>)
                 : (a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, false> : lstm_bwd_kernel<U, NX, BF16, false, false>);
@@ -1981,13 +2105,18 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   if (pl && !fa)
     kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, P, false, P> : lstm_bwd_kernel<U, NX, BF16, false, P, false, P>;
   if (pl && fa) kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, P, P, P> : lstm_bwd_kernel<U, NX, BF16, false, P, P, P>;
+  if (xd)
+    kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, P, false, false, XDC>
+                  : lstm_bwd_kernel<U, NX, BF16, false, P, false, false, XDC>;
   static bool attr_set = false;
   if (!attr_set) {
     for (auto f : {lstm_bwd_kernel<U, NX, BF16, true, false>, lstm_bwd_kernel<U, NX, BF16, false, false>,
                    lstm_bwd_kernel<U, NX, BF16, true, P>, lstm_bwd_kernel<U, NX, BF16, false, P>,
                    lstm_bwd_kernel<U, NX, BF16, true, P, P>, lstm_bwd_kernel<U, NX, BF16, false, P, P>,
                    lstm_bwd_kernel<U, NX, BF16, true, P, false, P>, lstm_bwd_kernel<U, NX, BF16, false, P, false, P>,
-                   lstm_bwd_kernel<U, NX, BF16, true, P, P, P>, lstm_bwd_kernel<U, NX, BF16, false, P, P, P>})
+                   lstm_bwd_kernel<U, NX, BF16, true, P, P, P>, lstm_bwd_kernel<U, NX, BF16, false, P, P, P>,
+                   lstm_bwd_kernel<U, NX, BF16, true, P, false, false, XDC>,
+                   lstm_bwd_kernel<U, NX, BF16, false, P, false, false, XDC>})
       hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
@@ -2007,7 +2136,8 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, (const frag*)a.a2pack, a.bias,
                      (const elem*)a.hraw, (const typename CT<BF16>::type*)a.cst, (const elem*)a.dH, a.dw_slab, a.dpos_slab, a.dwemb, a.dmask, a.seed, a.thr, a.inv_kp,
                      a.drop, pl ? nullptr : (unsigned short*)a.dxp, (const unsigned short*)a.xg, a.dh_lane,
-                     pm ? a.tlen : nullptr, pm ? a.slen : nullptr, a.wblank, af);
+                     pm ? a.tlen : nullptr, pm ? a.slen : nullptr, a.wblank, af, (const unsigned short*)a.wrows,
+                     a.wbytes);
   INA_CHECK_LAUNCH();
   return 0;
 }

@@ -40,12 +40,19 @@ def _route_grad(meta, name, g):
 
 
 _WROWS: dict = {}
+_QI = [0, 4, 1, 5, 2, 6, 3, 7]   # word_rows column order (feature q, q + 4 per lane group q)
+
+
+def direct_x_enabled() -> bool:
+    """Direct-x recurrences (lstm.hip xd_build): INA_DIRECT_X=0 keeps the x_gather record (A/B, tests)."""
+    return os.environ.get("INA_DIRECT_X", "1") != "0" and os.environ.get("INA_POS_LDS", "0") == "0"
 
 
 def word_rows(word: torch.Tensor, wemb: torch.Tensor, fresh: bool):
     """Word-table rows per dataset token, bf16 [NI * L, 8] (zero padded; the gate MFMAs take x in bf16
     anyway), for lstm_fwd's x gather: one 16-byte load per token from a per-instance contiguous run
-    instead of a random row of the 400k-row table.
+    instead of a random row of the 400k-row table.  Columns are q-interleaved, [f0 f4 f1 f5 f2 f6 f3 f7]:
+    the recurrences' lane group q holds features q and q + 4, ONE dword at byte 4q (direct x, lstm.hip).
     A frozen table (the reference default, model/base.py:55-59) is gathered once per (ids, table
     version); ``fresh`` (trained word table, updated in place by the fused optimizer) gathers every
     step.  None for word vectors wider than 8 (the kernel then gathers from the table itself)."""
@@ -60,7 +67,7 @@ def word_rows(word: torch.Tensor, wemb: torch.Tensor, fresh: bool):
             return hit[2]
     E = wemb.shape[1]
     rows = torch.nn.functional.pad(wemb.detach().float().index_select(0, word.reshape(-1).long()), (0, 8 - E))
-    rows = rows.to(torch.bfloat16).contiguous()
+    rows = rows[:, _QI].to(torch.bfloat16).contiguous()
     if not fresh:
         if len(_WROWS) >= 4:
             _WROWS.pop(next(iter(_WROWS)))
@@ -116,8 +123,8 @@ class EncoderFn(torch.autograd.Function):
         kp = float(meta["keep_prob"])
         lstm_args = (inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
                      p2emb.detach().contiguous(), apack, bias, U, sh["NX"])
-        tail = (int(meta["seed"]), kp, meta.get("seed_dev"),
-                word_rows(word, wemb, bool(meta.get("word_grad", False))) if bf16 else None)
+        wrows = word_rows(word, wemb, bool(meta.get("word_grad", False))) if bf16 else None
+        tail = (int(meta["seed"]), kp, meta.get("seed_dev"), wrows)
         b1c, w2c = b1.detach().contiguous(), w2.detach().reshape(-1).contiguous()
         rec = bf16 and meta.get("fuse_rec_attn", True) and o.rec_attn_ok(U, word.shape[1])
         skip = bool(meta.get("skip_padding", False))
@@ -126,6 +133,10 @@ class EncoderFn(torch.autograd.Function):
             raise NotImplementedError("lstm_skip_padding on the GPU needs the bf16 record path (u in {8, 20, 32}, "
                                       "L <= 64) and device lengths")
         perm = tlen = slen = None
+        fused = rec and bool(need_grad) and meta.get("fuse_attn_bwd", os.environ.get("INA_FUSE_ATTN_BWD", "0") != "0")
+        # direct x: the recurrences read the word rows + LDS position tables (shifted ids), no xg record
+        direct = (rec and wrows is not None and sh["NX"] == 4 and bool(meta.get("pos_shift", False)) and not fused
+                  and direct_x_enabled())
         if rec:
             # attention straight from the step records (no natural-layout copy of H)
             w1pack, w1tpack = ((pk["w1rpack"], pk["w1rtpack"]) if pk is not None and "w1rpack" in pk
@@ -137,19 +148,20 @@ class EncoderFn(torch.autograd.Function):
                 inst, perm, tlen, slen = ragged_plan(inst, lengths, skip, int(word.shape[1]))
                 lstm_args = (inst,) + lstm_args[1:]
             hlane, cst, hnat, dmask, xg, e, alphas = o.lstm_attn_fwd(*lstm_args, bool(need_grad), *tail,
-                                                                     mask, w1pack, b1c, w2c, tlen, perm, slen)
+                                                                     mask, w1pack, b1c, w2c, tlen, perm, slen,
+                                                                     direct)
         else:
             w1pack, w1tpack = (pk["w1pack"], pk["w1tpack"]) if pk is not None else pack_attn(W1, bf16)
             hlane, cst, hnat, dmask, xg = o.lstm_fwd(*lstm_args, bf16, bool(need_grad), *tail)
             e, alphas = o.attn_fwd(hnat, inst, mask, w1pack, b1c, w2c, U, bf16, int(meta.get("attn_blocks", 0)))
         if need_grad:
             # attention backward fused into lstm_bwd (record path): its own per-direction packs
-            fused = rec and meta.get("fuse_attn_bwd", os.environ.get("INA_FUSE_ATTN_BWD", "0") != "0")
             if fused:
                 w1pack, w1tpack = ((pk["w1fpack"], pk["w1ftpack"]) if pk is not None and "w1fpack" in pk
                                    else pack_attn_fuse(W1))
             ctx.save_for_backward(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst,
-                                  w1pack, w1tpack, b1, w2, alphas, hnat, dmask, xg, e, perm, tlen, slen)
+                                  w1pack, w1tpack, b1, w2, alphas, hnat, dmask, xg, e, perm, tlen, slen,
+                                  wrows if direct else None)
             ctx.meta = dict(meta, NX=sh["NX"], DIN=DIN, rec=rec, fused=fused)
         ctx.mark_non_differentiable(alphas)
         ctx.set_materialize_grads(False)   # no zero-fill launch for the alphas gradient
@@ -159,7 +171,7 @@ class EncoderFn(torch.autograd.Function):
     def backward(ctx, de, _dalpha):
         o = ops()
         (inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst, w1pack, w1tpack, b1, w2,
-         alphas, hnat, dmask, xg, e, perm, tlen, slen) = ctx.saved_tensors
+         alphas, hnat, dmask, xg, e, perm, tlen, slen, wrows) = ctx.saved_tensors
         m = ctx.meta
         U, bf16, DIN = m["U"], m["bf16"], m["DIN"]
         H2 = 2 * U
@@ -183,7 +195,7 @@ class EncoderFn(torch.autograd.Function):
                                                p1emb.detach().contiguous(), p2emb.detach().contiguous(), apack, a2pack,
                                                bias, hlane, cst, dH, dmask, xg, U, m["NX"], bf16, word_grad,
                                                int(m.get("lstm_blocks", 0)), int(m["seed"]), float(m["keep_prob"]),
-                                               bool(m.get("pos_shift", False)), tlen, slen)
+                                               bool(m.get("pos_shift", False)), tlen, slen, wrows)
         return EncoderFn._grads(ctx, m, aslab, None, dw_slab, dpos_slab, dwemb)
 
     @staticmethod

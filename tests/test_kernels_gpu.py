@@ -193,7 +193,7 @@ def test_rec_attention_forward_matches_natural(keep_prob, store, tail, u):
     hl0, _, hn0, dm0, _ = ops().lstm_fwd(*args, True, True, 77, keep_prob, None, None)
     e0, a0 = ops().attn_fwd(hn0, inst, mask, P["packs"][0], P["b1"], P["w2"], U, True, 0)
     hl1, _, hn1, dm1, _, e1, a1 = ops().lstm_attn_fwd(*args, store, 77, keep_prob, None, None, mask, P["rpacks"][0],
-                                                      P["b1"], P["w2"], None, None, None)
+                                                      P["b1"], P["w2"], None, None, None, False)
     torch.cuda.synchronize()
     assert hn1.numel() == 0 and e1.shape == e0.shape and a1.shape == a0.shape
     # h slots always; the c slots only when stored (the no-backward kernel leaves them unwritten)
@@ -395,6 +395,38 @@ def test_pos_lds_matches_dxp_path(u, skip, fused, monkeypatch):
             assert torch.equal(g1[k], g0[k]), k
 
 
+@pytest.mark.parametrize("u", [8, 20, 32])
+@pytest.mark.parametrize("keep_prob", [1.0, 0.9])
+@pytest.mark.parametrize("skip,word_grad", [(False, False), (True, False), (False, True)])
+def test_direct_x_matches_xg_record(u, keep_prob, skip, word_grad, monkeypatch):
+    """Direct x (the recurrences read the word rows and LDS position tables, no x_gather record) gives the
+    recurrences bit-identical x operands: e, alphas and every gradient bitwise equal to the xg-record path
+    (incl. the padding rows of a partial last tile, ragged tiles, sequence_length resets, trained words)."""
+    from induction_network_on_fewrel_amd.ops.encoder import encode
+    cfg, data, model, dd, inst, _ = _problem(dtype="bf16", u=u, B=7)
+    assert dd.pos_shift and inst.shape[0] % 16 != 0
+    out = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("INA_DIRECT_X", on)
+        p = {k: v.detach().clone().requires_grad_(v.requires_grad or (word_grad and k == "word_embedding"))
+             for k, v in model.pdict().items()}
+        meta = dict(U=cfg.hidden_size, bf16=True, keep_prob=keep_prob, seed=5, word_grad=word_grad,
+                    ragged_min_rows=0, skip_padding=skip)
+        e, a = encode(inst, dd.arrays(), p, meta)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        (e * torch.randn(e.shape, generator=g, device="cuda")).sum().backward()
+        torch.cuda.synchronize()
+        out.append((e.detach(), a, {k: v.grad for k, v in p.items() if v.grad is not None}))
+    (e0, a0, g0), (e1, a1, g1) = out
+    assert torch.equal(e0, e1) and torch.equal(a0, a1)
+    assert set(g0) == set(g1) and (not word_grad or "word_embedding" in g0)
+    for k in g0:
+        if word_grad and k == "word_embedding":   # global float atomics: order-dependent roundoff
+            assert _relerr(g1[k], g0[k]) < 1e-5, k
+        else:
+            assert torch.equal(g1[k], g0[k]), k
+
+
 @pytest.mark.parametrize("L", [24, 1, 2])
 def test_encoder_backward_short_and_even_L(L):
     """even L and the 1- and 2-step edge cases of the recurrences' peeled loops."""
@@ -462,7 +494,7 @@ def test_pos_grad_shift_matches_general(B):
     outs = []
     for shift in (False, True):
         _, dpos, _ = ops().lstm_bwd(inst, word, pos1, pos2, *tabs, apack, a2pack, bias, hlane, cst, dH, dmask, xg, U, NX,
-                                    True, False, 0, 5, 0.9, shift, None, None)
+                                    True, False, 0, 5, 0.9, shift, None, None, None)
         outs.append(dpos.sum((0, 1)))
     torch.cuda.synchronize()
     err = _relerr(outs[1], outs[0])
@@ -755,3 +787,19 @@ def test_small_steps_run_as_hip_graph(tmp_path):
         loss, _ = tr.train_step()
         assert loss == loss
     assert tr._graph is not None and tr._graph.graph is not None and tr.global_step == 3
+
+
+@pytest.mark.parametrize("hidden,E", [(128, 50), (12, 5)])
+def test_small_steps_stay_eager_off_the_fused_width(tmp_path, hidden, E):
+    """The wide path (u = 128) and zero-padded widths take the dropout seed as a host int: a captured
+    graph would replay one mask, so small steps stay eager there and every step draws a new mask."""
+    from induction_network_on_fewrel_amd.runtime.trainer import Trainer
+    data = make_synthetic(num_relations=8, instances_per_relation=30, vocab=300, word_dim=E, seed=0)
+    cfg = Config(N=5, K=5, Q=5, episodes_per_step=1, model_dir=str(tmp_path / "w"), seed=1, resume=False,
+                 hidden_size=hidden)
+    tr = Trainer(cfg, data, None, device="cuda", log=False)
+    assert not tr.graph_step_enabled
+    for _ in range(2):
+        loss, _ = tr.train_step()
+        assert loss == loss
+    assert tr._graph is None and tr.global_step == 2

@@ -81,14 +81,14 @@ def main():
     t, (dH, aslab) = timed(lambda: o.attn_bwd(hnat, inst, w1pack, w1tpack, b1, w2, de, alphas, U, True, 0))
     res["attn_bwd"] = t
     t, _ = timed(lambda: o.lstm_bwd(inst, word, pos1, pos2, wemb, p1, p2, apack, a2pack, bias, hlane, cst, dH, dmask, xg, U,
-                                    sh["NX"], True, False, 0, 7, 0.9, False, None, None))
+                                    sh["NX"], True, False, 0, 7, 0.9, False, None, None, None))
     res["lstm_bwd"] = t
     if hasattr(o, "lstm_attn_fwd"):
         t, _ = timed(lambda: o.lstm_attn_fwd(inst, word, pos1, pos2, wemb, p1, p2, apack, bias, U, sh["NX"], True, 7,
-                                             0.9, None, wrows, mask, w1pack, b1, w2, None, None, None))
+                                             0.9, None, wrows, mask, w1pack, b1, w2, None, None, None, False))
         res["lstm_attn_fwd"] = t
         t, _ = timed(lambda: o.lstm_attn_fwd(inst, word, pos1, pos2, wemb, p1, p2, apack, bias, U, sh["NX"], False, 7,
-                                             1.0, None, wrows, mask, w1pack, b1, w2, None, None, None))
+                                             1.0, None, wrows, mask, w1pack, b1, w2, None, None, None, False))
         res["lstm_attn_fwd_infer"] = t
     res["encoder_total"] = res["lstm_fwd"] + res["attn_fwd"] + res["attn_bwd"] + res["lstm_bwd"]
     print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in res.items()}))
