@@ -68,6 +68,7 @@ struct LstmArgs {
   // only posb / dmask (no xg record).  wbytes = wrows' size in bytes (buffer range: rows past it read 0)
   int xd;
   uint32_t wbytes;
+  void* xdtab;   // direct x: the position tables (x_gather writes them, the recurrences copy them into LDS)
 };
 // bf16 mode: gather every token's x features once into a.xg / a.posb, and (a.drop) the dropout keep
 // bits into a.dmask (lstm.hip x_gather_kernel); must run before lstm_fwd in bf16 mode

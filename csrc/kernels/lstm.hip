@@ -189,6 +189,36 @@ struct FAS {
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
+// direct x (LstmArgs::xd; verdict r3 #6: x_gather's 485 MB xg record and its four re-reads per step go
+// away).  The word features come from the per-token word rows (ops/encoder.py::word_rows, q-interleaved
+// [f0 f4 f1 f5 f2 f6 f3 f7]: lane group q's two slots xi = 0, 1 are ONE dword at byte 4q of the token's
+// 16-byte row; a sequence's rows are contiguous, so a 128-byte line serves 8 steps).  The position
+// features come from block-resident LDS tables, since the ids are shifted aranges (pos = o_s + t):
+//   T[(q * 2 + tb) * 3L + r][xi] = bf16 of feature 4 xi + q if it is a column of position table tb, row r
+//                                  (else 0); rows 2L .. 3L-1 are zero (padding sequences: o = 2L)
+// A lane reads its two 8-byte entries at rows o1 + t / o2 + t and ORs them into the word dword: every slot
+// is nonzero in at most one of the three sources, so the operand bits equal x_gather's.
+// ------------------------------------------------------------------------------------------
+__device__ inline void xd_build(unsigned short* T, int L, int E, int PD, const float* __restrict__ p1emb,
+                                const float* __restrict__ p2emb) {
+  const int R = 3 * L, N = 4 * 2 * R * 4;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    const int xi = i & 3, r = (i >> 2) % R, qt = (i >> 2) / R, tb = qt & 1, q = qt >> 1;
+    const int c = 4 * xi + q - E - tb * PD;
+    float v = 0.f;
+    if (r < 2 * L && c >= 0 && c < PD) v = (tb ? p2emb : p1emb)[r * PD + c];
+    T[i] = f2bf(v);
+  }
+}
+// a block's copy of the tables (built once per forward by x_gather block (0, 0) into global memory: building
+// them in every recurrence block cost ~50 us of lstm_fwd prologue at 12,800 blocks); 16-byte chunks
+__device__ inline void xd_copy(void* lds, const unsigned short* __restrict__ g, int L) {
+  const uint4* s = reinterpret_cast<const uint4*>(g);
+  uint4* d = reinterpret_cast<uint4*>(lds);
+  for (int i = threadIdx.x; i < 12 * L; i += blockDim.x) d[i] = s[i];   // 4 * 2 * 3L * 4 * 2 bytes / 16
+}
+
+// ------------------------------------------------------------------------------------------
 // encoder input gather (bf16 mode; K1 of SURVEY 2.3).  The recurrences used to gather their x
 // features per step (a random 20-byte word-table row per token, 2 directions x fwd + bwd = 4 times
 // per token, one step of prefetch): latency-bound on L2/MALL misses (kbench: 0.44 -> 0.29 ms
@@ -222,10 +252,14 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
                                                       unsigned short* __restrict__ posb,
                                                       unsigned char* __restrict__ dmask, int U, uint32_t seed,
                                                       const int* __restrict__ seed_dev, uint32_t thr,
-                                                      const int* __restrict__ perm) {
+                                                      const int* __restrict__ perm, unsigned short* __restrict__ xdtab) {
+  // direct x: block (0, 0) also builds the recurrences' position tables (xd_build) in global memory
+  if (xdtab != nullptr && blockIdx.x == 0 && blockIdx.y == 0) xd_build(xdtab, L, E, PD, p1emb, p2emb);
   // the two position tables ([2L, PD] each, tiny) in LDS: per-feature loads from them were most of
   // this kernel's vector-memory instructions
   __shared__ float ptab[2 * 128 * 8];
+  __shared__ uint32_t kst[2 * XG_C * XG_T * 16];   // keep bytes [dir][step - t0][64 lanes]
+  const int t0 = blockIdx.y * XG_C * XG_T;
   if constexpr (UT > 0) U = UT;
   if constexpr (ET > 0) E = ET;
   if constexpr (PT > 0) PD = PT;
@@ -240,21 +274,26 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
   const long rb = (long)inst[valid ? seq : S - 1] * L;
   int p1c[XG_C], p2c[XG_C], widc[XG_C];
   u16x8_t wrc[XG_C];
+  // direct x: only the t = 0 position ids are consumed (pos_shift_gemm's per-sequence offsets); every
+  // thread loads its sequence's first ids (16 distinct rows per wave) and no x features are written
+  const bool xd = xg == nullptr;
 #pragma unroll
   for (int c = 0; c < XG_C; ++c) {   // clamped rows: unconditional loads
     const int t = (blockIdx.y * XG_C + c) * XG_T + (threadIdx.x >> 4);
-    const long r = rb + min(t, L - 1);
+    const long r = rb + (xd ? 0 : min(t, L - 1));
     p1c[c] = pos1[r];
     p2c[c] = pos2[r];
     // DIRECT: the token's word row as one 16-byte load of 8 bf16 (E <= 8, zero padded, q-interleaved:
     // feature f at 2 (f & 3) + (f >> 2)).  xg == nullptr (direct-x recurrences): ids / keep bits only
-    if (xg == nullptr) continue;
+    if (xd) continue;
     if constexpr (DIRECT) wrc[c] = *reinterpret_cast<const u16x8_t*>(wrows + r * 8);
     else widc[c] = word[r];
   }
   // (the pos tables are staged while those loads are in flight)
-  for (int i = threadIdx.x; i < 2 * PTN; i += 256) ptab[i] = i < PTN ? p1emb[i] : p2emb[i - PTN];
-  __syncthreads();
+  if (!xd) {
+    for (int i = threadIdx.x; i < 2 * PTN; i += 256) ptab[i] = i < PTN ? p1emb[i] : p2emb[i - PTN];
+    __syncthreads();
+  }
   const int DIN = E + 2 * PD;
 #pragma unroll
   for (int c = 0; c < XG_C; ++c) {
@@ -286,7 +325,7 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
           u16x4_t{v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
   }
   }
-  posb[(size_t)(tile * L + t) * 16 + n] = (unsigned short)(p1 | (p2 << 8));
+  if (!xd || t == 0) posb[(size_t)(tile * L + t) * 16 + n] = (unsigned short)(p1 | (p2 << 8));
   if (dmask) {   // uniform
     const uint32_t sd = seed_dev ? (uint32_t)seed_dev[0] : seed;
     const uint32_t thr16 = thr >> 16;
@@ -306,34 +345,21 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
         by[u0 & 3] |= ((x & 0xFFFFu) < thr16 ? 1u : 0u) << (u0 >> 2);
         by[u1 & 3] |= ((x >> 16) < thr16 ? 1u : 0u) << (u1 >> 2);
       }
-      unsigned char* mrow = dmask + (size_t)((tile * 2 + d) * L + t) * 64 + n;
+      // staged in LDS, stored below as coalesced dwords (per-lane byte stores to global were most of
+      // this kernel's time once direct x removed its x rows)
+      unsigned char* mrow = reinterpret_cast<unsigned char*>(kst) + (d * XG_C * XG_T + t - t0) * 64 + n;
 #pragma unroll
       for (int q = 0; q < 4; ++q) mrow[16 * q] = (unsigned char)by[q];
     }
   }
   }
-}
-
-// ------------------------------------------------------------------------------------------
-// direct x (LstmArgs::xd; verdict r3 #6: x_gather's 485 MB xg record and its four re-reads per step go
-// away).  The word features come from the per-token word rows (ops/encoder.py::word_rows, q-interleaved
-// [f0 f4 f1 f5 f2 f6 f3 f7]: lane group q's two slots xi = 0, 1 are ONE dword at byte 4q of the token's
-// 16-byte row; a sequence's rows are contiguous, so a 128-byte line serves 8 steps).  The position
-// features come from block-resident LDS tables, since the ids are shifted aranges (pos = o_s + t):
-//   T[(q * 2 + tb) * 3L + r][xi] = bf16 of feature 4 xi + q if it is a column of position table tb, row r
-//                                  (else 0); rows 2L .. 3L-1 are zero (padding sequences: o = 2L)
-// A lane reads its two 8-byte entries at rows o1 + t / o2 + t and ORs them into the word dword: every slot
-// is nonzero in at most one of the three sources, so the operand bits equal x_gather's.
-// ------------------------------------------------------------------------------------------
-__device__ inline void xd_build(unsigned short* T, int L, int E, int PD, const float* __restrict__ p1emb,
-                                const float* __restrict__ p2emb) {
-  const int R = 3 * L, N = 4 * 2 * R * 4;
-  for (int i = threadIdx.x; i < N; i += blockDim.x) {
-    const int xi = i & 3, r = (i >> 2) % R, qt = (i >> 2) / R, tb = qt & 1, q = qt >> 1;
-    const int c = 4 * xi + q - E - tb * PD;
-    float v = 0.f;
-    if (r < 2 * L && c >= 0 && c < PD) v = (tb ? p2emb : p1emb)[r * PD + c];
-    T[i] = f2bf(v);
+  if (dmask) {   // uniform: the block's keep bytes, rows [t0, t0 + rows) of both directions
+    __syncthreads();
+    const int rows = min(XG_C * XG_T, L - t0), nw = rows * 16;
+    for (int i = threadIdx.x; i < 2 * nw; i += 256) {
+      const int d = i >= nw ? 1 : 0, r = i - d * nw;
+      reinterpret_cast<uint32_t*>(dmask + (size_t)((tile * 2 + d) * L + t0) * 64)[r] = kst[d * XG_C * XG_T * 16 + r];
+    }
   }
 }
 
@@ -368,8 +394,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   const int ntiles = (S + 15) / 16;
   const int tile = blockIdx.x * 4 + wave;
   int2* ids = ids_all + wave * 16 * L;
-  if constexpr (XD) {   // the block's position tables (before any wave leaves)
-    xd_build(reinterpret_cast<unsigned short*>(ids_all), L, E, PD, p1emb, p2emb);
+  if constexpr (XD) {   // the block's position tables (xg = x_gather's global copy; before any wave leaves)
+    xd_copy(ids_all, xg, L);
     __syncthreads();
   }
   constexpr bool FG = !BF16;   // fp32 mode gathers x per step
@@ -841,7 +867,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     for (int i = lane; i < PLN; i += 64) plR[i] = 0.f;
   // XD: the block's direct-x position tables (lstm_bwd_lds_bytes mirrors this offset)
   char* xdT = reinterpret_cast<char*>(smem) + ((pl_off + (PL ? (size_t)4 * PLN * 4 : 0) + 15) & ~(size_t)15);
-  if constexpr (XD) xd_build(reinterpret_cast<unsigned short*>(xdT), L, E, PD, p1emb, p2emb);
+  if constexpr (XD) xd_copy(xdT, xg, L);   // (xg = x_gather's global copy of the tables)
   if constexpr (FA) {
     for (int i = threadIdx.x; i < FS::NAP; i += 256) lAp[i] = af.w1f[(size_t)dir * FS::NAP + i];
     for (int i = threadIdx.x; i < FS::NAPT; i += 256) lApt[i] = af.w1ft[(size_t)dir * FS::NAPT + i];
@@ -2079,7 +2105,7 @@ static int launch_fwd_t(const LstmArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, a.bias, (elem*)a.hraw,
                      (typename CT<BF16>::type*)a.cst, (elem*)a.hdrop, a.dmask, a.seed, a.thr, a.inv_kp, a.drop, a.seed_dev,
-                     (const unsigned short*)a.xg, BF16 ? a.tlen : nullptr, BF16 ? a.slen : nullptr,
+                     (const unsigned short*)(xd ? a.xdtab : a.xg), BF16 ? a.tlen : nullptr, BF16 ? a.slen : nullptr,
                      (const unsigned short*)a.wrows, a.wbytes);
   INA_CHECK_LAUNCH();
   return 0;
@@ -2135,7 +2161,7 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(kfn, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, (const frag*)a.a2pack, a.bias,
                      (const elem*)a.hraw, (const typename CT<BF16>::type*)a.cst, (const elem*)a.dH, a.dw_slab, a.dpos_slab, a.dwemb, a.dmask, a.seed, a.thr, a.inv_kp,
-                     a.drop, pl ? nullptr : (unsigned short*)a.dxp, (const unsigned short*)a.xg, a.dh_lane,
+                     a.drop, pl ? nullptr : (unsigned short*)a.dxp, (const unsigned short*)(xd ? a.xdtab : a.xg), a.dh_lane,
                      pm ? a.tlen : nullptr, pm ? a.slen : nullptr, a.wblank, af, (const unsigned short*)a.wrows,
                      a.wbytes);
   INA_CHECK_LAUNCH();
@@ -2273,7 +2299,7 @@ int x_gather(const LstmArgs& a, int U, int NX, hipStream_t st) {
 #define INA_XG_LAUNCH(NXV, DIR, ...)                                                                     \
   hipLaunchKernelGGL((x_gather_kernel<NXV, DIR, ##__VA_ARGS__>), grid, dim3(256), 0, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, \
                      a.wemb, wr16, a.E, a.p1emb, a.p2emb, a.PD, xg, posb, a.drop ? a.dmask : nullptr, U, a.seed, \
-                     a.seed_dev, a.thr, a.perm)
+                     a.seed_dev, a.thr, a.perm, a.xd ? (unsigned short*)a.xdtab : nullptr)
   if (NX == 4 && a.wrows && U == 20 && a.E == 5 && a.PD == 5)
     INA_XG_LAUNCH(4, true, 20, 5, 5);
   else if (NX == 4 && a.wrows)
