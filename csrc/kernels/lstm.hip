@@ -272,6 +272,12 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
   const int seq = tile * 16 + n;
   const bool valid = seq < S;
   const long rb = (long)inst[valid ? seq : S - 1] * L;
+  // dropout hash inputs, loaded once (inside the pass / direction loops they were 6 dependent load round
+  // trips per thread): the counter uses the row's ORIGINAL index (ragged tiles sort the rows), so the mask
+  // equals the unsorted run's and the oracle's
+  const uint32_t sd = seed_dev ? (uint32_t)seed_dev[0] : seed;
+  const uint32_t pv = perm ? (uint32_t)perm[valid ? seq : S - 1] : 0u;   // (clamped: no lane-dependent branch)
+  const uint32_t oseq = (perm && valid) ? pv : (uint32_t)seq;
   int p1c[XG_C], p2c[XG_C], widc[XG_C];
   u16x8_t wrc[XG_C];
   // direct x: only the t = 0 position ids are consumed (pos_shift_gemm's per-sequence offsets); every
@@ -327,14 +333,10 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
   }
   if (!xd || t == 0) posb[(size_t)(tile * L + t) * 16 + n] = (unsigned short)(p1 | (p2 << 8));
   if (dmask) {   // uniform
-    const uint32_t sd = seed_dev ? (uint32_t)seed_dev[0] : seed;
     const uint32_t thr16 = thr >> 16;
 #pragma unroll
     for (int d = 0; d < 2; ++d) {
       const uint32_t salt = dropout_salt(sd, (uint32_t)d);
-      // the hash counter uses the row's ORIGINAL index (ragged tiles sort the rows): the same mask as
-      // the unsorted run and the oracle
-      const uint32_t oseq = (perm && valid) ? (uint32_t)perm[seq] : (uint32_t)seq;
       const uint32_t pbase = ((oseq * L + t) * U) >> 1;   // U even: the row's first unit pair
       uint32_t by[4] = {0u, 0u, 0u, 0u};                            // keep byte of lane group q
 #pragma unroll
