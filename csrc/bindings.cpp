@@ -133,8 +133,8 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> lstm_fwd_impl(
   const bool has_wrows = wrows.has_value() && wrows->defined() && wrows->numel() > 0;
   TORCH_CHECK(!direct_x || (bf16 && !natural && NX == 4 && has_wrows),
               "ina.lstm_fwd: direct x needs the bf16 record path, NX == 4 and word rows");
-  // (direct x: [position ids][position tables 4 x 2 x 3L x 4 bf16], see lstm.hip xd_build)
-  Tensor xg = bf16 ? at::empty({ntiles * L * ((direct_x ? 0 : 64 * NX) + 16) + (direct_x ? 96 * L : 0)},
+  // (direct x: [position ids][position tables 4 x 2 x 2L x 4 bf16], see lstm.hip xd_build)
+  Tensor xg = bf16 ? at::empty({ntiles * L * ((direct_x ? 0 : 64 * NX) + 16) + (direct_x ? 64 * L : 0)},
                                word.options().dtype(at::kBFloat16))
                    : at::empty({0}, word.options().dtype(at::kBFloat16));
   if (S == 0) return {hlane, cst, hnat, dmask, xg};
@@ -376,7 +376,7 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
   // pos_shift (caller-checked pos[s][t] = pos[s][0] + t, pos[s][0] <= L): per-sequence one-hot GEMM -> ONE slab
   const bool shift = bf16 && pos_shift && (L + 1 + 15) / 16 <= 5 && !pos_lds;
   // (direct x: x_gather wrote only the t = 0 position ids -- the shifted-form reduction's per-sequence offsets)
-  TORCH_CHECK(!(bf16 && xg.numel() == ((S + 15) / 16) * L * 16 + 96 * L) || shift,
+  TORCH_CHECK(!(bf16 && xg.numel() == ((S + 15) / 16) * L * 16 + 64 * L) || shift,
               "ina.lstm_bwd: direct x needs the shifted-position gradient path");
   auto dpos_slab = shift ? at::empty({1, 1, 2, 2 * L, PD}, opt)
                          : ((bf16 && !pos_lds) ? at::empty({pblocks, 1, 2, 2 * L, PD}, opt)
@@ -385,7 +385,7 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
   Tensor dxp = (bf16 && !pos_lds) ? at::empty({2 * (2 * PD + 1) * ntiles * L * 16}, opt.dtype(at::kBFloat16))
                                   : at::empty({0}, opt);
   // direct x (lstm_attn_fwd with direct_x): xg holds only the position ids, x comes from the word rows
-  const bool direct_x = bf16 && xg.numel() == ntiles * L * 16 + 96 * L;
+  const bool direct_x = bf16 && xg.numel() == ntiles * L * 16 + 64 * L;
   if (bf16) {
     check(xg, "xg", at::kBFloat16);
     TORCH_CHECK(direct_x || xg.numel() == ntiles * L * (64 * NX + 16), "ina.lstm_bwd: xg (from lstm_fwd) shape");

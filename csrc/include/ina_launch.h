@@ -89,8 +89,8 @@ int pos_grad_shift(const LstmArgs& a, float* gpart, float* out, hipStream_t st);
 bool lstm_supported(int U, int NX);
 size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fused_attn = false, bool pos_lds = false,
                           bool direct_x = false);
-// direct-x position tables in LDS: [4 lane groups q][2 tables][3L rows][4 slots] bf16 (rows >= 2L zero)
-inline size_t xd_table_bytes(int L) { return (size_t)4 * 2 * 3 * L * 4 * 2; }
+// direct-x position tables in LDS: [4 lane groups q][2 tables][2L rows][4 slots] bf16
+inline size_t xd_table_bytes(int L) { return (size_t)4 * 2 * 2 * L * 4 * 2; }
 
 struct AttnArgs {
   const void* hraw;

@@ -194,14 +194,14 @@ struct FAS {
 // [f0 f4 f1 f5 f2 f6 f3 f7]: lane group q's two slots xi = 0, 1 are ONE dword at byte 4q of the token's
 // 16-byte row; a sequence's rows are contiguous, so a 128-byte line serves 8 steps).  The position
 // features come from block-resident LDS tables, since the ids are shifted aranges (pos = o_s + t):
-//   T[(q * 2 + tb) * 3L + r][xi] = bf16 of feature 4 xi + q if it is a column of position table tb, row r
-//                                  (else 0); rows 2L .. 3L-1 are zero (padding sequences: o = 2L)
+//   T[(q * 2 + tb) * 2L + r][xi] = bf16 of feature 4 xi + q if it is a column of position table tb, row r
+//                                  (else 0); padding sequences read rows 0.. and mask the result to 0
 // A lane reads its two 8-byte entries at rows o1 + t / o2 + t and ORs them into the word dword: every slot
 // is nonzero in at most one of the three sources, so the operand bits equal x_gather's.
 // ------------------------------------------------------------------------------------------
 __device__ inline void xd_build(unsigned short* T, int L, int E, int PD, const float* __restrict__ p1emb,
                                 const float* __restrict__ p2emb) {
-  const int R = 3 * L, N = 4 * 2 * R * 4;
+  const int R = 2 * L, N = 4 * 2 * R * 4;
   for (int i = threadIdx.x; i < N; i += blockDim.x) {
     const int xi = i & 3, r = (i >> 2) % R, qt = (i >> 2) / R, tb = qt & 1, q = qt >> 1;
     const int c = 4 * xi + q - E - tb * PD;
@@ -215,7 +215,7 @@ __device__ inline void xd_build(unsigned short* T, int L, int E, int PD, const f
 __device__ inline void xd_copy(void* lds, const unsigned short* __restrict__ g, int L) {
   const uint4* s = reinterpret_cast<const uint4*>(g);
   uint4* d = reinterpret_cast<uint4*>(lds);
-  for (int i = threadIdx.x; i < 12 * L; i += blockDim.x) d[i] = s[i];   // 4 * 2 * 3L * 4 * 2 bytes / 16
+  for (int i = threadIdx.x; i < 8 * L; i += blockDim.x) d[i] = s[i];   // 4 * 2 * 2L * 4 * 2 bytes / 16
 }
 
 // ------------------------------------------------------------------------------------------
@@ -564,12 +564,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   // previous step's record stores), i.e. no prefetch at all
   if constexpr (XD) {
     // direct x: per step one dword of the token's word row (buffer load; padding sequences read past the
-    // range -> 0) and two 8-byte LDS table entries, prefetched one step ahead like the xg rows below
+    // range -> 0) and two 8-byte LDS table entries, prefetched one step ahead like the xg rows below.
+    // (The word loads two steps ahead, a 4-step loop, measured equal: 765 vs 768 us, profiles/r4_direct_x/pf2.)
     const bool valid = seq < S;
     const int rb0 = inst[valid ? seq : S - 1] * L;
     const uint32_t wvo = valid ? (uint32_t)rb0 * 16u + 4u * (uint32_t)q : 0x80000000u;
-    const int R = 3 * L;
-    const int o1 = valid ? pos1[rb0] : 2 * L, o2 = valid ? pos2[rb0] : 2 * L;
+    const int R = 2 * L;
+    const uint32_t vm = valid ? 0xFFFFFFFFu : 0u;   // padding sequences: x = 0
+    const int o1 = valid ? pos1[rb0] : 0, o2 = valid ? pos2[rb0] : 0;
     const char* tb1 = reinterpret_cast<const char*>(ids_all) + ((q * 2) * R + o1) * 8;
     const char* tb2 = reinterpret_cast<const char*>(ids_all) + ((q * 2 + 1) * R + o2) * 8;
     const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(wrows), (short)0, (int)wbytes,
@@ -589,8 +591,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     auto step_xr = [&](const int tau, const XR& r0) __attribute__((always_inline)) {
       XR r = r0;
       asm volatile("" : "+v"(r.w), "+v"(r.a), "+v"(r.b));
-      const uint32_t w0 = r.w | (uint32_t)r.a | (uint32_t)r.b;
-      const uint32_t w1 = (uint32_t)(r.a >> 32) | (uint32_t)(r.b >> 32);
+      const uint32_t w0 = (r.w | (uint32_t)r.a | (uint32_t)r.b) & vm;
+      const uint32_t w1 = ((uint32_t)(r.a >> 32) | (uint32_t)(r.b >> 32)) & vm;
       float xv[4] = {bf2f((unsigned short)w0), bf2f((unsigned short)(w0 >> 16)), bf2f((unsigned short)w1),
                      bf2f((unsigned short)(w1 >> 16))};
       step(tau, xv);
@@ -1174,8 +1176,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
                            XD ? wbytes : (uint32_t)L * XSTEPB);
       // XD: the lane's word-row dword (padding rows: past the range -> 0) and position-table entries
       const uint32_t wvo = valid ? (uint32_t)rowbase * 16u + 4u * (uint32_t)q : 0x80000000u;
-      const char* xtb1 = xdT + ((q * 2) * 3 * L + (valid ? pos1[rowbase] : 2 * L)) * 8;
-      const char* xtb2 = xdT + ((q * 2 + 1) * 3 * L + (valid ? pos2[rowbase] : 2 * L)) * 8;
+      const char* xtb1 = xdT + ((q * 2) * 2 * L + (valid ? pos1[rowbase] : 0)) * 8;
+      const char* xtb2 = xdT + ((q * 2 + 1) * 2 * L + (valid ? pos2[rowbase] : 0)) * 8;
+      const uint32_t xvm = valid ? 0xFFFFFFFFu : 0u;   // padding sequences: x = 0
       const auto rdx = rsrc(dxp + ((size_t)dir * ntiles + tu) * L * (NPF + 1) * 16, (uint32_t)L * PSTEPB);
       const int vl2 = lane * 2, vx = lane * NX * 2;
       // ---- PL: the lane's position-table slot at t = 0 per x feature (shifted ids: pos = o + t); word /
@@ -1375,8 +1378,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         if constexpr (FA) asm volatile("" : "+v"(X.ko), "+v"(X.kt), "+v"(X.al));
         if constexpr (XD) {   // word dword | the two table entries (disjoint nonzero slots)
           asm volatile("" : "+v"(X.x[0]), "+v"(X.pa), "+v"(X.pb));
-          X.x[0] |= (uint32_t)X.pa | (uint32_t)X.pb;
-          X.x[1] = (uint32_t)(X.pa >> 32) | (uint32_t)(X.pb >> 32);
+          X.x[0] = (X.x[0] | (uint32_t)X.pa | (uint32_t)X.pb) & xvm;
+          X.x[1] = ((uint32_t)(X.pa >> 32) | (uint32_t)(X.pb >> 32)) & xvm;
         } else {
 #pragma unroll
           for (int k = 0; k < NXW; ++k) asm volatile("" : "+v"(X.x[k]));
