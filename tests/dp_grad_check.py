@@ -74,7 +74,10 @@ def main():
         per[name] = float((a - b).abs().max()) / den
     out = dict(rank=dist.rank, world=dist.world, comm=dist.comm_name, episodes_union=Bt,
                max_rel_err=max(per.values()), per_param=per, finite=bool(torch.isfinite(g_dp).all()))
-    print(json.dumps(out), flush=True)
+    # one write() per line: the ranks share the launcher's stdout, and print()'s separate newline write let
+    # two ranks' lines interleave into one
+    sys.stdout.write(json.dumps(out) + "\n")
+    sys.stdout.flush()
     dist.destroy()
 
 

@@ -127,13 +127,28 @@ def test_native_comm_collectives_world1():
         c.destroy()
 
 
+def _json_objects(text):
+    """Every top-level JSON object in the ranks' merged stdout (robust to lines of two ranks run together)."""
+    dec, out, i = json.JSONDecoder(), [], text.find("{")
+    while i >= 0:
+        try:
+            obj, end = dec.raw_decode(text, i)
+        except json.JSONDecodeError:
+            i = text.find("{", i + 1)
+            continue
+        if isinstance(obj, dict) and "rank" in obj:
+            out.append(obj)
+        i = text.find("{", end)
+    return out
+
+
 def _dp_check(nproc, extra_env):
     env = dict(os.environ, OMP_NUM_THREADS="2", **extra_env)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "tests", "dp_grad_check.py")]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=140)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    rows = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    rows = _json_objects(r.stdout)
     assert len(rows) == nproc, r.stdout
     for row in rows:
         print(row["rank"], row["comm"], f"{row['max_rel_err']:.2e}")
