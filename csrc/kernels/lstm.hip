@@ -565,7 +565,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   if constexpr (XD) {
     // direct x: per step one dword of the token's word row (buffer load; padding sequences read past the
     // range -> 0) and two 8-byte LDS table entries, prefetched one step ahead like the xg rows below.
-    // (The word loads two steps ahead, a 4-step loop, measured equal: 765 vs 768 us, profiles/r4_direct_x/pf2.)
+    // (The word loads two steps ahead, a 4-step loop, measured equal: 765 vs 768 us, profiles/r4_direct_x/pf2;
+    // the tables read from x_gather's global copy through L1 instead of LDS, slower: 793 vs 766 us, gtab/.)
     const bool valid = seq < S;
     const int rb0 = inst[valid ? seq : S - 1] * L;
     const uint32_t wvo = valid ? (uint32_t)rb0 * 16u + 4u * (uint32_t)q : 0x80000000u;
