@@ -43,6 +43,9 @@ _WROWS: dict = {}
 _QI = [0, 4, 1, 5, 2, 6, 3, 7]   # word_rows column order (feature q, q + 4 per lane group q)
 
 
+DIRECT_X_CALLS = [0]   # forwards that ran direct x (tests assert the path engaged)
+
+
 def direct_x_enabled() -> bool:
     """Direct-x recurrences (lstm.hip xd_build): INA_DIRECT_X=0 keeps the x_gather record (A/B, tests)."""
     return os.environ.get("INA_DIRECT_X", "1") != "0" and os.environ.get("INA_POS_LDS", "0") == "0"
@@ -134,9 +137,12 @@ class EncoderFn(torch.autograd.Function):
                                       "L <= 64) and device lengths")
         perm = tlen = slen = None
         fused = rec and bool(need_grad) and meta.get("fuse_attn_bwd", os.environ.get("INA_FUSE_ATTN_BWD", "0") != "0")
-        # direct x: the recurrences read the word rows + LDS position tables (shifted ids), no xg record
+        # direct x: the recurrences read the word rows + LDS position tables (shifted ids), no xg record.  It
+        # pays once the kernels are throughput-bound (same row threshold as the ragged tiles): 1,616,764 vs
+        # 1,588,243 episodes/s at 2048 episodes, 3,543 vs 3,569 at 1 episode (profiles/r4_direct_x/small)
         direct = (rec and wrows is not None and sh["NX"] == 4 and bool(meta.get("pos_shift", False)) and not fused
-                  and direct_x_enabled())
+                  and direct_x_enabled() and inst.shape[0] >= meta.get("direct_x_min_rows", RAGGED_MIN_ROWS))
+        DIRECT_X_CALLS[0] += int(direct)
         if rec:
             # attention straight from the step records (no natural-layout copy of H)
             w1pack, w1tpack = ((pk["w1rpack"], pk["w1rtpack"]) if pk is not None and "w1rpack" in pk

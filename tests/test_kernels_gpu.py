@@ -255,7 +255,8 @@ def test_encoder_backward(dtype, keep_prob, u, L=37):
     cfg, data, model, dd, inst, _ = _problem(dtype=dtype, u=u, L=L)
     bf16 = dtype == "bf16"
     seed = 99
-    meta = dict(U=cfg.hidden_size, bf16=bf16, keep_prob=keep_prob, seed=seed, word_grad=False, ragged_min_rows=0)
+    meta = dict(U=cfg.hidden_size, bf16=bf16, keep_prob=keep_prob, seed=seed, word_grad=False, ragged_min_rows=0,
+                direct_x_min_rows=0)
     p = model.pdict()
     e, alphas = encode(inst, dd.arrays(), p, meta)
     de = torch.randn_like(e)
@@ -402,20 +403,23 @@ def test_direct_x_matches_xg_record(u, keep_prob, skip, word_grad, monkeypatch):
     """Direct x (the recurrences read the word rows and LDS position tables, no x_gather record) gives the
     recurrences bit-identical x operands: e, alphas and every gradient bitwise equal to the xg-record path
     (incl. the padding rows of a partial last tile, ragged tiles, sequence_length resets, trained words)."""
+    from induction_network_on_fewrel_amd.ops import encoder as enc
     from induction_network_on_fewrel_amd.ops.encoder import encode
     cfg, data, model, dd, inst, _ = _problem(dtype="bf16", u=u, B=7)
     assert dd.pos_shift and inst.shape[0] % 16 != 0
     out = []
     for on in ("0", "1"):
         monkeypatch.setenv("INA_DIRECT_X", on)
+        n0 = enc.DIRECT_X_CALLS[0]
         p = {k: v.detach().clone().requires_grad_(v.requires_grad or (word_grad and k == "word_embedding"))
              for k, v in model.pdict().items()}
         meta = dict(U=cfg.hidden_size, bf16=True, keep_prob=keep_prob, seed=5, word_grad=word_grad,
-                    ragged_min_rows=0, skip_padding=skip)
+                    ragged_min_rows=0, direct_x_min_rows=0, skip_padding=skip)
         e, a = encode(inst, dd.arrays(), p, meta)
         g = torch.Generator(device="cuda").manual_seed(1)
         (e * torch.randn(e.shape, generator=g, device="cuda")).sum().backward()
         torch.cuda.synchronize()
+        assert enc.DIRECT_X_CALLS[0] - n0 == (1 if on == "1" else 0)   # the path under test really ran
         out.append((e.detach(), a, {k: v.grad for k, v in p.items() if v.grad is not None}))
     (e0, a0, g0), (e1, a1, g1) = out
     assert torch.equal(e0, e1) and torch.equal(a0, a1)
