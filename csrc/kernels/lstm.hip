@@ -24,6 +24,9 @@ using namespace ina;
 #ifndef INA_FWD_PIPE
 #define INA_FWD_PIPE 1
 #endif
+#ifndef INA_DG_SHARED
+#define INA_DG_SHARED 1   // lean BPTT gate gradients with shared products (0: the direct formulas, A/B)
+#endif
 #ifndef INA_LSTM_PM
 #define INA_LSTM_PM 1   // 0: timing-only A/B build -- lane-layout dH through the generic step (double-masked)
 #endif
@@ -1444,12 +1447,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
           const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
           const float tc = tanh_l2(ccur[m] * (2.f * LOG2E_F));
           const float dh = dh_rec[m] + dhin[m];
+#if INA_DG_SHARED
+          // (shared products: the step is VALU-issue bound -- README "ISA budget"; 14 instead of 16 ops per unit)
+          const float dho = dh * og;
+          const float dc = fmaf(dho, fmaf(-tc, tc, 1.f), dc_rec[m]);
+          dc_rec[m] = dc * fg;
+          const float dci = dc * ig;
+          dg[m][0] = dci * fmaf(-jg, ig, jg);          // dc jg ig (1 - ig)
+          dg[m][1] = dci * fmaf(-jg, jg, 1.f);         // dc ig (1 - jg^2)
+          dg[m][2] = dc * cprev[m] * fmaf(-fg, fg, fg);
+          const float dot = dho * tc;
+          dg[m][3] = fmaf(-dot, og, dot);              // dh tc og (1 - og)
+#else
           const float dc = dc_rec[m] + dh * og * (1.f - tc * tc);
           dc_rec[m] = dc * fg;
           dg[m][0] = dc * jg * (ig - ig * ig);
           dg[m][1] = dc * ig * (1.f - jg * jg);
           dg[m][2] = dc * cprev[m] * (fg - fg * fg);
           dg[m][3] = dh * tc * (og - og * og);
+#endif
           ccur[m] = cprev[m];
         }
         uint32_t dgw[2 * U4];   // packed bf16 dG pairs: the W dG operand and the dW image row
