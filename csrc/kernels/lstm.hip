@@ -221,6 +221,20 @@ __device__ inline void xd_copy(void* lds, const unsigned short* __restrict__ g, 
   for (int i = threadIdx.x; i < 8 * L; i += blockDim.x) d[i] = s[i];   // 4 * 2 * 2L * 4 * 2 bytes / 16
 }
 
+// direct x without dropout (eval / keep_prob = 1): x_gather has nothing left but the recurrences' position
+// tables and pos_shift_gemm's t = 0 ids -- one thread per sequence instead of one per token (the full
+// gather grid was ~100 us of block launches for an eval step of 16,384 episodes)
+__global__ __launch_bounds__(256) void xd_ids_kernel(const int* __restrict__ inst, int S, const int* __restrict__ pos1,
+                                                     const int* __restrict__ pos2, int L, int E, int PD,
+                                                     const float* __restrict__ p1emb, const float* __restrict__ p2emb,
+                                                     unsigned short* __restrict__ posb, unsigned short* __restrict__ xdtab) {
+  if (blockIdx.x == 0) xd_build(xdtab, L, E, PD, p1emb, p2emb);
+  const int seq = blockIdx.x * 256 + threadIdx.x;
+  if (seq >= ((S + 15) / 16) * 16) return;   // (padding rows of the last tile: the clamped row, as x_gather)
+  const long r = (long)inst[seq < S ? seq : S - 1] * L;
+  posb[(size_t)(seq >> 4) * L * 16 + (seq & 15)] = (unsigned short)(pos1[r] | (pos2[r] << 8));
+}
+
 // ------------------------------------------------------------------------------------------
 // encoder input gather (bf16 mode; K1 of SURVEY 2.3).  The recurrences used to gather their x
 // features per step (a random 20-byte word-table row per token, 2 directions x fwd + bwd = 4 times
@@ -2318,6 +2332,12 @@ int x_gather(const LstmArgs& a, int U, int NX, hipStream_t st) {
   const dim3 grid(ntiles, (a.L + XG_T * XG_C - 1) / (XG_T * XG_C));
   if (2 * a.L * a.PD > 128 * 8) return -1;   // pos tables staged in LDS
   const auto* wr16 = (const unsigned short*)a.wrows;
+  if (a.xd && !a.drop) {
+    hipLaunchKernelGGL(xd_ids_kernel, dim3((ntiles * 16 + 255) / 256), dim3(256), 0, st, a.inst, a.S, a.pos1, a.pos2,
+                       a.L, a.E, a.PD, a.p1emb, a.p2emb, posb, (unsigned short*)a.xdtab);
+    INA_CHECK_LAUNCH();
+    return 0;
+  }
 #define INA_XG_LAUNCH(NXV, DIR, ...)                                                                     \
   hipLaunchKernelGGL((x_gather_kernel<NXV, DIR, ##__VA_ARGS__>), grid, dim3(256), 0, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, \
                      a.wemb, wr16, a.E, a.p1emb, a.p2emb, a.PD, xg, posb, a.drop ? a.dmask : nullptr, U, a.seed, \
