@@ -15,6 +15,7 @@
 // wave-private LDS every 2 steps to accumulate dW with MFMAs (32 samples per K-step).
 #include <type_traits>
 
+#include <cstdlib>
 #include "ina_common.h"
 #include "ina_launch.h"
 
@@ -284,7 +285,9 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
   // thread = one token (sequence n = tid & 15, step t0 + tid / 16): its id / row loads are runs along
   // t (coalesced), and it writes its NX x 4 features as 4 lane-group chunks; for a fixed step the
   // 16 sequences' chunks of one lane group are one contiguous 16 x 8-byte segment.
-  const int tile = blockIdx.x;
+  const int ntiles = (S + 15) / 16;
+  // grid-stride over tiles (the launcher may cap the grid: fewer, longer-lived workgroups)
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   const int n = threadIdx.x & 15;
   const int seq = tile * 16 + n;
   const bool valid = seq < S;
@@ -379,6 +382,8 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
       const int d = i >= nw ? 1 : 0, r = i - d * nw;
       reinterpret_cast<uint32_t*>(dmask + (size_t)((tile * 2 + d) * L + t0) * 64)[r] = kst[d * XG_C * XG_T * 16 + r];
     }
+    __syncthreads();   // kst is rewritten by the next tile
+  }
   }
 }
 
@@ -2329,9 +2334,14 @@ int x_gather(const LstmArgs& a, int U, int NX, hipStream_t st) {
   if (ntiles <= 0) return 0;
   auto* xg = (unsigned short*)a.xg;
   auto* posb = const_cast<unsigned short*>(a.posb);
-  const dim3 grid(ntiles, (a.L + XG_T * XG_C - 1) / (XG_T * XG_C));
+  dim3 grid(ntiles, (a.L + XG_T * XG_C - 1) / (XG_T * XG_C));
   if (2 * a.L * a.PD > 128 * 8) return -1;   // pos tables staged in LDS
   const auto* wr16 = (const unsigned short*)a.wrows;
+  // INA_XG_GRID caps the gather grid (grid-stride over tiles; 0 / unset: one workgroup per tile).  Capped grids
+  // measured slower -- the direct-x gather is bound by its keep-bit hash (two quarter-rate multiplies per unit
+  // pair), not by workgroup launches: 163 / 179 us at 2048 / 1024 workgroups vs 148 (profiles/r4_xgather_grid)
+  static const int xg_cap = [] { const char* v = std::getenv("INA_XG_GRID"); return v ? std::atoi(v) : 0; }();
+  if (xg_cap > 0 && (int)grid.x > xg_cap) grid.x = xg_cap;
   if (a.xd && !a.drop) {
     hipLaunchKernelGGL(xd_ids_kernel, dim3((ntiles * 16 + 255) / 256), dim3(256), 0, st, a.inst, a.S, a.pos1, a.pos2,
                        a.L, a.E, a.PD, a.p1emb, a.p2emb, posb, (unsigned short*)a.xdtab);
