@@ -4,6 +4,7 @@
 // that the kernel grid does not assume never reaches the GPU.  Launches go to the current HIP
 // stream (capturable into hipGraphs by the caller).  No op has a CPU implementation: the CPU path
 // of the framework is the pure-PyTorch oracle in models/reference.py.
+#include <map>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
@@ -647,29 +648,27 @@ Tensor routing_bwd(const Tensor& e, const Tensor& Ws, const Tensor& dcls, Tensor
 }
 
 // ------------------------------------------------------------------ NTN
-Tensor ntn_fwd(const Tensor& cls, const Tensor& e, const Tensor& mpack, const Tensor& wpack, const Tensor& wvec,
-               const Tensor& bias, int64_t E, int64_t N, int64_t K, int64_t Q, int64_t h, bool paper, int64_t blocks) {
+// tile pack geometry (must match ops/packing.py::ntn_tile_geometry)
+static void ntn_geometry(int64_t N, int64_t H, int64_t h, int64_t& SG, int64_t& ntile, int64_t& tpb) {
+  const int64_t MTH = (H + 15) / 16;
+  SG = ina::ntn_slices_per_tile((int)N);
+  ntile = (h + SG - 1) / SG;
+  tpb = SG * MTH * 16 * 128 + 1024;
+}
+
+static ina::NtnArgs ntn_args(const Tensor& cls, const Tensor& e, const Tensor& tiles, int64_t E, int64_t N, int64_t K,
+                             int64_t Q, int64_t h, bool paper, int64_t blocks, const char* who) {
   check(cls, "cls", at::kFloat);
   check(e, "e", at::kFloat);
-  check(mpack, "mpack", at::kBFloat16);
-  check(bias, "bias", at::kFloat);
-  check_episode_rows(e, E, N, K, Q, "ina.ntn_fwd");
-  const int64_t H = e.size(1), MTH = (H + 15) / 16, NKA = (MTH + 1) / 2;
-  TORCH_CHECK(N <= 16 && N * Q <= 64, "ina.ntn_fwd: needs N <= 16 and N*Q <= 64");
-  TORCH_CHECK((MTH == 1 || MTH == 3 || MTH == 4) && H % 8 == 0, "ina.ntn_fwd: unsupported H ", H);
-  TORCH_CHECK(cls.numel() == E * N * H, "ina.ntn_fwd: cls shape");
-  const int64_t hp = 2 * ((h + 1) / 2);  // packs are padded to an even number of slices
-  TORCH_CHECK(mpack.numel() == hp * MTH * NKA * 64 * 8, "ina.ntn_fwd: mpack size");
-  if (paper) {
-    check(wvec, "wvec", at::kFloat);
-    TORCH_CHECK(wvec.numel() == h, "ina.ntn_fwd: paper head w must be [h]");
-  } else {
-    check(wpack, "wpack", at::kBFloat16);
-    TORCH_CHECK(wpack.numel() == ((h + 1) / 2) * 64 * 8, "ina.ntn_fwd: wpack size");
-    TORCH_CHECK(bias.numel() == N, "ina.ntn_fwd: bias must be [N]");
-  }
-  auto probs = at::empty({E, N * Q, N}, e.options());
-  if (E == 0) return probs;
+  check(tiles, "tiles", at::kBFloat16);
+  check_episode_rows(e, E, N, K, Q, who);
+  const int64_t H = e.size(1), MTH = (H + 15) / 16;
+  TORCH_CHECK(N >= 1 && N <= 16 && N * Q <= 64, who, ": needs 1 <= N <= 16 and N*Q <= 64");
+  TORCH_CHECK((MTH == 1 || MTH == 3 || MTH == 4) && H % 8 == 0, who, ": unsupported H ", H);
+  TORCH_CHECK(cls.numel() == E * N * H, who, ": cls shape");
+  int64_t SG, ntile, tpb;
+  ntn_geometry(N, H, h, SG, ntile, tpb);
+  TORCH_CHECK(tiles.numel() * 2 == ntile * tpb, who, ": tile pack size ", tiles.numel(), " != ", ntile * tpb / 2);
   ina::NtnArgs a{};
   a.cls = cls.data_ptr<float>();
   a.e = e.data_ptr<float>();
@@ -679,15 +678,27 @@ Tensor ntn_fwd(const Tensor& cls, const Tensor& e, const Tensor& mpack, const Te
   a.Q = (int)Q;
   a.H = (int)H;
   a.h = (int)h;
-  a.mpack = mpack.data_ptr();
-  a.wpack = paper ? nullptr : wpack.data_ptr();
-  a.wvec = paper ? wvec.data_ptr<float>() : nullptr;
+  a.tiles = tiles.data_ptr();
+  a.G = ina::ntn_episodes_per_wave((int)N, (int)Q);
+  a.SG = (int)SG;
+  a.ntile = (int)ntile;
+  a.tpb = (int)tpb;
+  a.paper = paper ? 1 : 0;
+  if (blocks <= 0) blocks = 65535;   // one workgroup per 8 waves x G episodes (grid-stride beyond)
+  a.blocks = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, 65535));
+  a.split = ina::ntn_split((int)E, (int)N, (int)Q, (int)h);
+  return a;
+}
+
+Tensor ntn_fwd(const Tensor& cls, const Tensor& e, const Tensor& tiles, const Tensor& bias, int64_t E, int64_t N,
+               int64_t K, int64_t Q, int64_t h, bool paper, int64_t blocks) {
+  check(bias, "bias", at::kFloat);
+  TORCH_CHECK(bias.numel() == (paper ? 1 : N), "ina.ntn_fwd: bias must be [", paper ? 1 : N, "]");
+  auto a = ntn_args(cls, e, tiles, E, N, K, Q, h, paper, blocks, "ina.ntn_fwd");
+  auto probs = at::empty({E, N * Q, N}, e.options());
+  if (E == 0) return probs;
   a.bias = bias.data_ptr<float>();
   a.probs = probs.data_ptr<float>();
-  a.paper = paper ? 1 : 0;
-  if (blocks <= 0) blocks = 1024;  // workgroups of 8 episodes (grid-stride beyond)
-  a.blocks = (int)std::max<int64_t>(1, blocks);
-  a.split = ina::ntn_split((int)E, (int)h);
   Tensor part;
   if (a.split > 1) {
     part = at::empty({a.split * E * N * Q * N}, e.options());
@@ -697,69 +708,40 @@ Tensor ntn_fwd(const Tensor& cls, const Tensor& e, const Tensor& mpack, const Te
   return probs;
 }
 
-std::tuple<Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tensor& e, const Tensor& mpack,
-                                           const Tensor& m2pack, const Tensor& wtpack, const Tensor& wvec,
-                                           const Tensor& dz, Tensor de, int64_t E, int64_t N, int64_t K, int64_t Q,
-                                           int64_t h, bool paper, int64_t blocks,
-                                           const std::optional<Tensor>& gscale, const std::optional<Tensor>& cls_bf) {
-  check(cls, "cls", at::kFloat);
-  check(e, "e", at::kFloat);
-  check(mpack, "mpack", at::kBFloat16);
-  check(m2pack, "m2pack", at::kBFloat16);
+// -> (dcls [E, N, H], dP bf16 [Kp, h H], dw slab [ngroups, ntile * (SG N N | SG)], C bf16 [Kp, H]) with the
+// class rows padded to Kp = E N rounded up to 64 (zero rows): dP and C are the operands of the dM reduction
+// GEMM (gemm_tn_slab)
+std::tuple<Tensor, Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tensor& e, const Tensor& tiles,
+                                                   const Tensor& dz, Tensor de, int64_t E, int64_t N, int64_t K,
+                                                   int64_t Q, int64_t h, bool paper, int64_t blocks,
+                                                   const std::optional<Tensor>& gscale) {
+  auto a = ntn_args(cls, e, tiles, E, N, K, Q, h, paper, blocks, "ina.ntn_bwd");
   check(dz, "dz", at::kFloat);
   check(de, "de", at::kFloat);
-  check_episode_rows(e, E, N, K, Q, "ina.ntn_bwd");
-  const int64_t H = e.size(1), MTH = (H + 15) / 16, NKB = (MTH + 1) / 2;
-  TORCH_CHECK(N <= 16 && N * Q <= 64, "ina.ntn_bwd: needs N <= 16 and N*Q <= 64");
-  TORCH_CHECK(MTH == 1 || MTH == 3 || MTH == 4, "ina.ntn_bwd: unsupported H");
-  TORCH_CHECK(H % 8 == 0, "ina.ntn_bwd: H must be a multiple of 8 (float4 row loads)");
+  const int64_t H = e.size(1), hH = h * H, rows = E * N, Kp = (rows + 63) / 64 * 64;
   TORCH_CHECK(dz.numel() == E * N * Q * N, "ina.ntn_bwd: dz shape");
   TORCH_CHECK(de.sizes() == e.sizes(), "ina.ntn_bwd: de shape");
-  const int64_t hp = 2 * ((h + 1) / 2);
-  TORCH_CHECK(m2pack.numel() == hp * MTH * NKB * 64 * 8 && mpack.numel() == m2pack.numel(), "ina.ntn_bwd: pack size");
-  if (paper) {
-    check(wvec, "wvec", at::kFloat);
-  } else {
-    check(wtpack, "wtpack", at::kBFloat16);
-    TORCH_CHECK(wtpack.numel() == hp * 64 * 8, "ina.ntn_bwd: wtpack size");
-  }
   auto dcls = at::empty({E, N, H}, e.options());
-  // dP carries a trash tail past the returned view: the kernel's lanes outside the valid N / H ranges
-  // store there unconditionally (no exec-mask branches in its slice loop)
-  auto dp = at::empty({E * N * h * H + h * H + 64}, e.options().dtype(at::kBFloat16))
-                .narrow(0, 0, E * N * h * H).view({E * N, h * H});
-  // reference head: one dw row per workgroup group (its episodes summed in the kernel)
-  const int64_t G = ina::ntn_groups((int)E);
-  auto dw = paper ? at::empty({E, h}, e.options()) : at::empty({G, h, N, N}, e.options());
-  if (E == 0) return {dcls, dp, dw};
-  ina::NtnArgs a{};
-  a.cls = cls.data_ptr<float>();
-  a.e = e.data_ptr<float>();
-  a.E = (int)E;
-  a.N = (int)N;
-  a.K = (int)K;
-  a.Q = (int)Q;
-  a.H = (int)H;
-  a.h = (int)h;
-  a.mpack = mpack.data_ptr();
-  a.m2pack = m2pack.data_ptr();
-  a.wtpack = paper ? nullptr : wtpack.data_ptr();
-  a.wvec = paper ? wvec.data_ptr<float>() : nullptr;
+  // dP: a trash tail past the padded rows takes the stores of lanes outside the valid (slice, class) / H
+  // ranges (no exec-mask branches in the tile loop)
+  auto dpf = at::empty({Kp * hH + 64}, e.options().dtype(at::kBFloat16));
+  auto dp = dpf.narrow(0, 0, Kp * hH).view({Kp, hH});
+  auto cbf = at::empty({Kp, H}, e.options().dtype(at::kBFloat16));
+  if (Kp > rows) {
+    dp.narrow(0, rows, Kp - rows).zero_();
+    cbf.narrow(0, rows, Kp - rows).zero_();
+  }
+  const int64_t groups = ina::ntn_groups((int)E, (int)N, (int)Q);
+  const int64_t dwe = paper ? a.SG : a.SG * N * N;
+  auto dw = at::empty({groups, a.ntile * dwe}, e.options());
+  if (E == 0) return {dcls, dp, dw, cbf};
   a.dz = dz.data_ptr<float>();
   a.dcls = dcls.data_ptr<float>();
   a.de = de.data_ptr<float>();
   a.dp_out = dp.data_ptr();
   a.dw_slab = dw.data_ptr<float>();
-  a.paper = paper ? 1 : 0;
   a.gscale = dev_float(gscale, "gscale");
-  if (cls_bf.has_value() && cls_bf->defined()) {
-    check(*cls_bf, "cls_bf", at::kBFloat16);
-    TORCH_CHECK(cls_bf->numel() == E * N * H, "ina.ntn_bwd: cls_bf must be [E*N, H]");
-    a.cls_bf = cls_bf->data_ptr();
-  }
-  if (blocks <= 0) blocks = 1024;
-  a.blocks = (int)std::max<int64_t>(1, blocks);
-  a.split = ina::ntn_split((int)E, (int)h);
+  a.cls_bf = cbf.data_ptr();
   Tensor pc, pq;
   if (a.split > 1) {
     pc = at::empty({a.split * E * N * H}, e.options());
@@ -768,7 +750,29 @@ std::tuple<Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tensor& e, c
     a.part2 = pq.data_ptr<float>();
   }
   check_launch(ina::ntn_bwd(a, cur_stream()), "ntn_bwd");
-  return {dcls, dp, dw};
+  return {dcls, dp, dw, cbf};
+}
+
+int64_t ntn_slices_per_tile(int64_t N) { return ina::ntn_slices_per_tile((int)N); }
+
+// slab [splits, MI, NJ] fp32 = per-split sums over k of A[k, :MI]^T B[k, :] (A [K, lda], B [K, NJ] bf16; K % 64 == 0)
+Tensor gemm_tn_slab(const Tensor& A, const Tensor& B, int64_t MI, int64_t splits) {
+  check(A, "A", at::kBFloat16);
+  check(B, "B", at::kBFloat16);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(0) == B.size(0), "ina.gemm_tn_slab: A [K, lda], B [K, NJ]");
+  const int64_t K = A.size(0), NJ = B.size(1);
+  TORCH_CHECK(K % 64 == 0 && MI % 8 == 0 && MI > 0 && MI <= 64 && MI <= A.size(1) && NJ % 8 == 0 && NJ >= 8,
+              "ina.gemm_tn_slab: needs K % 64 == 0, MI % 8 == 0, MI <= 64, NJ % 8 == 0");
+  if (splits <= 0) splits = ina::gemm_tn_splits((int)K, (int)MI, (int)NJ);
+  auto slab = at::empty({splits, MI, NJ}, A.options().dtype(at::kFloat));
+  static thread_local std::map<int, Tensor> zeros;
+  const int dev = A.get_device();
+  auto it = zeros.find(dev);
+  if (it == zeros.end()) it = zeros.emplace(dev, at::zeros({64}, A.options())).first;
+  check_launch(ina::gemm_tn_slab(A.data_ptr(), (int)A.size(1), B.data_ptr(), (int)NJ, (int)K, (int)MI, (int)NJ,
+                                 it->second.data_ptr(), slab.data_ptr<float>(), (int)splits, cur_stream()),
+               "gemm_tn_slab");
+  return slab;
 }
 
 // ------------------------------------------------------------------ optim / misc
@@ -890,6 +894,8 @@ TORCH_LIBRARY(ina, m) {
   m.def("routing_bwd", &routing_bwd);
   m.def("ntn_fwd", &ntn_fwd);
   m.def("ntn_bwd", &ntn_bwd);
+  m.def("ntn_slices_per_tile", &ntn_slices_per_tile);
+  m.def("gemm_tn_slab", &gemm_tn_slab);
   m.def("adam_step", &adam_step);
   m.def("adagrad_step", &adagrad_step);
   m.def("nonfinite_flag", &nonfinite_flag);

@@ -36,6 +36,7 @@ _VFILE = {f: fl.split(",") for f, fl in (e.split(":", 1) for e in os.environ.get
 OUT_DIR = os.path.join(ROOT, "build", "obj" + (f"_{_TAG}" if _TAG else ""))
 LIB = (os.path.join(ROOT, "variants", f"_ina_kernels_{_TAG}.so") if _TAG
        else os.path.join(ROOT, "induction_network_on_fewrel_amd", "_ina_kernels.so"))
+HOST_LIB = os.path.join(ROOT, "induction_network_on_fewrel_amd", "_ina_host" + sysconfig.get_config_var("EXT_SUFFIX"))
 ARCH = os.environ.get("INA_OFFLOAD_ARCH", "gfx950")
 # Per-file code generation flags.  rec_attn.hip: MFMA results in VGPRs (gfx950's unified register
 # file allows it); the default AGPR form cost 12 v_accvgpr_read per token step of the attention
@@ -112,6 +113,11 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
         for out in ex.map(_run, tasks):
             if verbose and out.strip():
                 print(out)
+    # host-only CPython extension (no torch / HIP): checkpoint CRC32C on any host
+    hsrc = os.path.join(CSRC, "host", "ina_host.c")
+    if _newer(HOST_LIB, [hsrc, __file__]):
+        _run([shutil.which("gcc") or "cc", "-O2", "-fPIC", "-shared", "-I" + sysconfig.get_paths()["include"], hsrc,
+              "-o", HOST_LIB])
     if tasks or not os.path.exists(LIB) or _newer(LIB, objs):
         cmd = [hipcc, "-shared", "-fPIC", "-o", LIB, *objs, f"-L{tlib}", "-ltorch", "-ltorch_cpu", "-lc10",
                "-lc10_hip", "-ltorch_hip", "-lrccl", f"-Wl,-rpath,{tlib}"]

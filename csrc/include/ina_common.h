@@ -60,6 +60,23 @@ INA_DEVICE u16x8_t tr_read8(const unsigned short* img, int stride, int c0, int q
                  (unsigned short)hi[0], (unsigned short)hi[1], (unsigned short)hi[2], (unsigned short)hi[3]};
 }
 
+// LDS-DMA of 16 B per lane (lane-linear from the wave-uniform LDS byte address lds_dst) as inline asm
+// (cdna_hip_programming.md 5.7 recipe: M0 saved / set / restored in the statement).  hipcc does not see it,
+// so it does not make later ds_read_b64_tr_b16 wait for it (with the builtin it cannot prove the transposed
+// reads disjoint from the DMA target and drains vmcnt before every one); the caller counts the completion
+// (s_waitcnt vmcnt + a workgroup barrier before the data is read).
+INA_DEVICE void glds16_asm(const void* gsrc_lane, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc_lane), "s"(lds_dst)
+               : "memory");
+}
+// 32-bit LDS byte address of a __shared__ pointer
+INA_DEVICE uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p;
+}
+
 // order this wave's LDS accesses without a memory fence: a wave's own LDS operations execute in
 // order in hardware, and a fence would also wait for every in-flight global load (vmcnt(0))
 INA_DEVICE void lds_order() {

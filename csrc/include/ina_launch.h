@@ -128,34 +128,38 @@ int routing_bwd(const float* e, const float* Ws, int E, int N, int K, int Q, int
 size_t routing_lds_bytes(int N, int K, int H, int R, bool bwd);
 int routing_bwd_default_blocks(int N, int K, int H, int R);
 
+// Neural tensor layer (ntn.hip).  The weights come as ONE per-step "tile pack" (ops/packing.py::pack_ntn_tiles):
+// slice tile t (SG = ntn_slices_per_tile(N) slices, rows (slice, class) of the MFMA tiles) = SG swizzled bf16
+// images of M[:, :, s] [16 MTH rows a][64 cols b] + the 16x16x16 fragments W [(s,c)][c'] and Wt [c'][(s,c)]
+// of the relation FC (reference head: w[s N + c][c']; paper head: w[s] on the diagonal c == c').
 struct NtnArgs {
-  const float* cls;
-  const float* e;
+  const float* cls;      // [E][N][H] class vectors
+  const float* e;        // [E * (N K + N Q)][H] sentence vectors (query rows used)
   int E, N, K, Q, H, h;
-  const void* mpack;
-  const void* m2pack;
-  const void* wpack;
-  const void* wtpack;
-  const float* wvec;
-  const float* bias;
-  float* probs;
-  const float* dz;
-  float* dcls;
-  float* de;
-  void* dp_out;
-  float* dw_slab;
-  int blocks;
+  const void* tiles;     // [ntile][tpb bytes] tile pack
+  int G;                 // episodes stacked per wave (class rows (g, c) of the P / dC tiles), ntn_episodes_per_wave
+  int SG, ntile, tpb;    // slices per tile, tiles, bytes per tile
   int paper;
+  const float* bias;
+  float* probs;          // fwd: [E][NQ][N]
+  const float* dz;       // bwd: dL/dlogit [E][NQ][N]
   const float* gscale;   // bwd: optional device scalar multiplying dz (upstream loss gradient)
-  void* cls_bf;          // bwd: optional bf16 copy of cls [E*N][H] (operand of the dM GEMM)
-  // slice split (small E, ntn_split): grid.y = split workgroup rows over the slice pairs; partials in
-  // part (fwd: [split][E][NQ][N] logits; bwd: dC [split][E][N][H]) and part2 (bwd: dQ [split][E][NQ][H])
+  float* dcls;           // bwd: [E][N][H]
+  float* de;             // bwd: query rows of [E * (N K + N Q)][H]
+  void* dp_out;          // bwd: bf16 dP [Kp][h H] (Kp = E N padded to 64; operand of the dM GEMM), + trash tail
+  float* dw_slab;        // bwd: [ngroups][ntile][SG N][N] (reference) / [ngroups][ntile][SG] (paper)
+  void* cls_bf;          // bwd: bf16 copy of cls [Kp][H] (the dM GEMM's other operand)
+  int blocks;
+  // slice split (small E, ntn_split): grid.y workgroup rows over the tiles; partials in part (fwd: logits
+  // [split][E][NQ][N]; bwd: dC [split][E][N][H]) and part2 (bwd: dQ [split][E][NQ][H])
   int split;
   float* part;
   float* part2;
 };
-int ntn_split(int E, int h);
-int ntn_groups(int E);   // workgroup groups of episodes (rows of the reference-head dw slab)
+int ntn_slices_per_tile(int N);
+int ntn_episodes_per_wave(int N, int Q);
+int ntn_split(int E, int N, int Q, int h);
+int ntn_groups(int E, int N, int Q);   // workgroup groups of episodes (rows of the dw slab)
 int ntn_fwd(const NtnArgs& a, hipStream_t st);
 
 // step glue (glue.hip)
@@ -328,6 +332,10 @@ int embed_ln_bwd(const BertEmbArgs& a, hipStream_t st);
 int bias_gelu_fwd(const void* x, const float* b, void* y, long T, int I, hipStream_t st);
 // gemm.hip: C = A B^T (bf16, A [M][K] / B [N][K] K-contiguous), epi 0 plain (+bias), 1 bias+GELU with the
 // pre-activation in aux, 2 C * GELU'(aux) with column-sum slab [2 ceil(M/256)][N].  N % 256 == 0, K % 64 == 0.
+// reduction GEMM slab[s][i][j] = sum_{k in split s} A[k][i] B[k][j] (gemm_tn.hip): K % 64 == 0, MI <= 64, MI % 8 == 0
+int gemm_tn_splits(int K, int MI, int NJ);
+int gemm_tn_slab(const void* A, int lda, const void* B, int ldb, int K, int MI, int NJ, const void* zero, float* slab,
+                 int splits, hipStream_t st);
 int gemm_bf16_nt(const void* A, int lda, const void* B, int ldb, int M, int N, int K, const float* bias, void* out,
                  int ldo, void* aux, int ldx, float* slab, int epi, hipStream_t st);
 int bias_gelu_bwd(const void* dy, const void* x, const float* b, void* dx, float* slab, int T, int I, int blocks,

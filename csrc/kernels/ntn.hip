@@ -6,21 +6,27 @@
 //   probs = sigmoid(V @ w + b),  w [h*N, N], b [N]        ("reference" head)
 // "paper" head (paper Eq.11): probs[q, c] = sigmoid(sum_s w_s relu(T[q, s, c]) + b).
 //
-// One wave per episode; the 200 tiny GEMMs of the reference become one chained MFMA pipeline per
-// slice pair, entirely in registers:
-//   P_s^T[b, c] = M_s^T[b, a] C^T[a, c]                          (M pre-packed per step)
-//   T_s[c, q]   = P_s[c, b] Q^T[b, q]      P^T accumulator reused as the A operand
-//   logits[q,c']+= relu(T)[(s,c), q]^T w[(s,c), c']   relu(T) accumulators of TWO slices form one
-//                                                      32-deep K step
-// An accumulator tile X (rows 4*(l>>4)+r, column l&15) used as an operand contracts over X's ROW
-// index; two tiles are paired into one K=32 fragment with k = 8q + j <-> row 16*(j>>2) + 4q + (j&3)
-// ("kmap32").  Every memory operand that meets such a fragment is packed with the same map.
-// The backward recomputes P/T and produces dC, dQ (registers, summed over slices), the per-episode
-// dw contribution and dP (bf16, for the dM = C^T dP reduction GEMM across episodes).
+// Tile formulation.  The h slices are cut into tiles of SG = 16 / N slices (<= 4) so that the rows
+// (slice, class) of one tile fill a 16-row MFMA operand (N = 5: 3 slices, 15 rows); a wave owns G = 2
+// episodes (<= 16 / N) whose class rows (g, c) are stacked the same way.  Per tile:
+//   P^T_s[b, (g,c)] = M_s^T C^T                 stacked over the wave's episodes (the dense product: 2x fewer
+//                                               MFMAs than one episode per wave), written to a per-episode
+//                                               LDS image P_g[(s,c)][b]
+//   T^T_g[(s,c), q] = P_g Q_g^T                 A = P image rows (ds_read_b128), B = Q rows (registers)
+//   fwd: logits^T[c', q] += Wt[c', (s,c)] relu(T^T)        16x16x16: the T^T accumulator IS the B operand
+//   bwd: dV^T = W[(s,c), c'] dz^T; dT^T = [T > 0] dV^T      16x16x16: dz^T is the B operand
+//        dw[(s,c), c'] += V dz                 A = V through a wave-private LDS image + ds_read_b64_tr_b16
+//        dQ^T_g[b, q] += P_g^T dT^T             A = the P image read transposed (tr_b16), B = dT^T accumulator
+//        dP^T_g[b, (s,c)] = Q^T dT              B = dT through an LDS image (tr_b16); dP -> global (dM GEMM)
+//                                               and -> the P image's rows (the P image is dead by then)
+//        dC^T[a, (g,c)] += M_s D_s              stacked over the wave's episodes again, B = the dP images
+// Compared with one wave per episode and the rows (c) of every product padded to 16 this is 11 MFMAs per
+// (slice, episode) in the backward instead of 25 (4 instead of 11 in the forward).
 //
-// A workgroup is 8 waves = 8 episodes; the packed M / w fragments of each slice pair are staged ONCE
-// per workgroup into LDS (double buffered, one barrier per pair) and shared by the 8 episodes, so the
-// L2 traffic for M is 1/8 of a wave-per-episode design (which measured 76 % SQ_WAIT_ANY).
+// A workgroup is 8 waves = 16 episodes.  The tile pack (M images + FC fragments, ops/packing.py::
+// pack_ntn_tiles) is staged once per workgroup with global_load_lds (double buffered, one barrier per tile).
+// LDS images are XOR-swizzled in 8-byte chunks (M: chunk ^ ((a & 2) << 1 | (a & 8)); P: chunk ^ ((r & 6) << 1);
+// V / dT: a row-slot rotation), which makes the fragment reads of every product conflict-free.
 #include "ina_common.h"
 #include "ina_launch.h"
 
@@ -28,25 +34,36 @@ using namespace ina;
 
 namespace {
 
-INA_DEVICE u16x8_t pack2(const f32x4_t& x0, const f32x4_t& x1) {
-  u16x8_t f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    f[j] = f2bf(x0[j]);
-    f[4 + j] = f2bf(x1[j]);
-  }
-  return f;
+constexpr int NW = 8;                // waves (each G episodes) per workgroup
+constexpr int NT_THREADS = NW * 64;
+constexpr int IMG_ROW = 128;         // bytes per LDS image row: 64 bf16
+constexpr int PIMG = 16 * IMG_ROW;   // per-episode P image [16 rows (slice, class)][64 b]
+constexpr int ZERO_BYTES = 256;      // zero block: the fragment reads of rows outside an image
+constexpr int DW_SLOT = 256;         // floats per wave of the dw tile exchange
+constexpr f32x4_t Z4 = {0.f, 0.f, 0.f, 0.f};
+constexpr s16x4_t Z4S = {0, 0, 0, 0};
+
+INA_DEVICE int mask_m(int a) { return ((a & 2) << 1) | (a & 8); }
+INA_DEVICE int mask_p(int r) { return (r & 6) << 1; }
+INA_DEVICE int vslot(int r) { return (r & ~15) | (r & 8) | ((r + ((r & 8) >> 1)) & 7); }
+
+INA_DEVICE s16x4_t trr(const unsigned char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p);
 }
-INA_DEVICE f32x4_t relu4(const f32x4_t& x) {
-  return f32x4_t{fmaxf(x[0], 0.f), fmaxf(x[1], 0.f), fmaxf(x[2], 0.f), fmaxf(x[3], 0.f)};
+INA_DEVICE u16x8_t cat8(const s16x4_t& lo, const s16x4_t& hi) {
+  return u16x8_t{(unsigned short)lo[0], (unsigned short)lo[1], (unsigned short)lo[2], (unsigned short)lo[3],
+                 (unsigned short)hi[0], (unsigned short)hi[1], (unsigned short)hi[2], (unsigned short)hi[3]};
 }
-INA_DEVICE int kmap32(int q, int j) { return 16 * (j >> 2) + 4 * q + (j & 3); }
-// Unconditional load from a clamped index, zero outside: a lane-dependent branch around each load
-// made hipcc wait vmcnt(0) per element (60-400 serialized L2 round trips in the prologues).
-// (multiply by 0/1 rather than select: a select lets LLVM sink the load back under a branch)
-INA_DEVICE float ldz(const float* __restrict__ p, bool ok, long idx) {
-  return p[ok ? idx : 0] * (ok ? 1.f : 0.f);
+INA_DEVICE s16x4_t bf4(const f32x4_t& x) {
+  return s16x4_t{(short)f2bf(x[0]), (short)f2bf(x[1]), (short)f2bf(x[2]), (short)f2bf(x[3])};
 }
+INA_DEVICE s16x4_t bf4relu(const f32x4_t& x) {
+  return s16x4_t{(short)f2bf(fmaxf(x[0], 0.f)), (short)f2bf(fmaxf(x[1], 0.f)), (short)f2bf(fmaxf(x[2], 0.f)),
+                 (short)f2bf(fmaxf(x[3], 0.f))};
+}
+// Unconditional load from a clamped index, zero outside (a lane-dependent branch around each load made
+// hipcc wait vmcnt(0) per element); multiply rather than select so LLVM cannot sink the load under a branch
+INA_DEVICE float ldz(const float* __restrict__ p, bool ok, long idx) { return p[ok ? idx : 0] * (ok ? 1.f : 0.f); }
 // 4 consecutive floats p[idx .. idx + 3] (idx % 4 == 0) -> bf16 elements j0 .. j0 + 3 of f (zeros if !ok)
 INA_DEVICE void ld4bf(const float* __restrict__ p, bool ok, long idx, u16x8_t& f, int j0) {
   const float4 v = *reinterpret_cast<const float4*>(p + (ok ? idx : 0));
@@ -56,163 +73,184 @@ INA_DEVICE void ld4bf(const float* __restrict__ p, bool ok, long idx, u16x8_t& f
   f[j0 + 2] = f2bf(v.z * z);
   f[j0 + 3] = f2bf(v.w * z);
 }
-constexpr f32x4_t Z4 = {0.f, 0.f, 0.f, 0.f};
 
-}  // namespace
-
-
-#ifndef INA_NTN_BWD_LD
-#define INA_NTN_BWD_LD 1   // branch-free vectorized prologue loads in ntn_bwd (153 vs 160 us despite 188 B of spills; 0 = the branchy per-element loads)
-#endif
-#ifndef INA_NTN_TR
-#define INA_NTN_TR 1   // ntn_bwd: P^T -> P, T -> T^T and dT -> dT^T through wave-private LDS images read back with
-                       // ds_read_b64_tr_b16, instead of recomputing each product in the other layout (37 -> 25 MFMAs
-                       // per slice and episode)
-#endif
-#ifndef INA_NTN_WAVES
-#define INA_NTN_WAVES 8   // episodes (waves) per workgroup sharing one staged copy of the slice packs
-// (4 episodes: ntn_bwd 574 -> 641 us with two workgroups per CU -- twice the pack staging -- and 1120 us
-// without the waves_per_eu(2) bound, which lets it take 331 registers at one wave per SIMD; tools/gpu_ab_ntn.sh)
-#endif
-constexpr int NTN_WAVES = INA_NTN_WAVES;
-constexpr int NTN_THREADS = NTN_WAVES * 64;
-
-// Stage slice pair p straight into LDS with global_load_lds (16 B / lane, one 1-KiB fragment per wave
-// instruction, no staging registers).  Staged pair layout (fragments of 64 lanes x 16 B):
-// [mpack: 2*MTH*NKA][m2pack: 2*MTH*NKB (backward only)][w: NSW].  The host pads every packed array to
-// an even number of slices, so no lane needs a bounds check.
-INA_DEVICE void glds16(const u16x8_t* gsrc_lane, u16x8_t* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc_lane,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
-}
-template <int MTH, int NSW, bool WITH_M2>
-INA_DEVICE void ntn_stage(u16x8_t* buf, int p, const u16x8_t* __restrict__ mpack, const u16x8_t* __restrict__ m2pack,
-                          const u16x8_t* __restrict__ wsrc, int w_per_pair) {
-  constexpr int NKA = (MTH + 1) / 2, NKB = (MTH + 1) / 2;
-  constexpr int F1 = 2 * MTH * NKA, F2 = WITH_M2 ? 2 * MTH * NKB : 0, FR = F1 + F2 + NSW;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int f = wave; f < FR; f += NTN_WAVES) {
-    const u16x8_t* src;
-    if (f < F1)
-      src = mpack + ((long)2 * p * MTH * NKA + f) * 64;
-    else if (f < F1 + F2)
-      src = m2pack + ((long)2 * p * MTH * NKB + (f - F1)) * 64;
-    else
-      src = wsrc + ((long)p * w_per_pair + (f - F1 - F2)) * 64;
-    glds16(src + lane, buf + f * 64);
-  }
+// tile pack -> LDS: 1-KiB fragments, wave w takes fragments w, w + NW, ...
+INA_DEVICE void stage_tile(unsigned char* dst, const unsigned char* __restrict__ src, int nfrag) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(dst));
+  for (int f = wave; f < nfrag; f += NW) glds16_asm(src + (long)f * 1024 + lane * 16, base + f * 1024);
 }
 INA_DEVICE void stage_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Order point of a wave's own cross-lane LDS traffic (lanes read what other lanes wrote): the wave's image
+// base offset goes through an empty asm, so the compiler can prove no access after it disjoint from one
+// before it.  No "memory" clobber: with one (or a fence) hipcc waits for the in-flight tile DMA (vmcnt(0))
+// before every later LDS read.  The hardware runs a wave's LDS instructions in order.
+// The lane index through an empty asm at the top of each tile: the lane-dependent LDS / global addresses
+// are recomputed per tile (a few VALU) instead of being hoisted out of both loops into ~100 live registers.
+INA_DEVICE int opaque_lane() {
+  int l = threadIdx.x & 63;
+  asm volatile("" : "+v"(l));
+  return l;
+}
+INA_DEVICE void wave_order(uint32_t& off) {
+  asm volatile("" : "+v"(off));
+  __builtin_amdgcn_wave_barrier();
+}
 
-// ------------------------------------------------------------------------------------------
-template <int MTH, int QT, bool PAPER>
-__global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void ntn_fwd_kernel(const float* __restrict__ cls, const float* __restrict__ e,
-                                                              int E, int N, int K, int Q, int H, int h,
-                                                              const u16x8_t* __restrict__ mpack,
-                                                              const u16x8_t* __restrict__ wpack,
-                                                              const float* __restrict__ wvec,
-                                                              const float* __restrict__ bias, float* __restrict__ probs,
-                                                              float* __restrict__ part) {
-  constexpr int NKA = (MTH + 1) / 2;  // K steps over a (32 each)
-  constexpr int NKB = (MTH + 1) / 2;  // K steps over b (pairs of accumulator tiles)
-  constexpr int NSW = PAPER ? 0 : 1;
-  constexpr int FR = 2 * MTH * NKA + NSW;
-  extern __shared__ __attribute__((aligned(16))) u16x8_t ntn_lds[];
-  const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15, wave = threadIdx.x >> 6;
-  const int NQ = N * Q;
-  const int npair = (h + 1) / 2;
-  // slice split (small episode batches): workgroup row blockIdx.y takes slice pairs [p0, p1) and writes
-  // raw logit partials; ntn_fwd_finish sums them in split order (deterministic)
-  const int p0 = (int)((long)npair * blockIdx.y / gridDim.y), p1 = (int)((long)npair * (blockIdx.y + 1) / gridDim.y);
-  for (int g = blockIdx.x; g * NTN_WAVES < E; g += gridDim.x) {
-    const int ep = g * NTN_WAVES + wave;
-    const bool act = ep < E;
-    const int epc = act ? ep : E - 1;
-    const long rq0 = (long)epc * (N * K + NQ) + N * K;
-    // H % 8 == 0 (host check): every 4-feature run is in or out of range as a whole -> float4 loads
-    u16x8_t Cf[NKA];
+struct Geo {   // per-launch geometry shared by both kernels
+  int N, NQ, G, SG, H, lg, lc;
+  bool lrow;   // this lane's stacked class row (g, c) = (lg, lc) exists
+};
+INA_DEVICE Geo geo(const NtnArgs& k, int n) {
+  Geo g;
+  g.N = k.N;
+  g.NQ = k.N * k.Q;
+  g.G = k.G;
+  g.SG = k.SG;
+  g.H = k.H;
+  g.lg = n / k.N;
+  g.lc = n - g.lg * k.N;
+  g.lrow = n < k.G * k.N;
+  return g;
+}
+
+// C^T as the B operand of P^T (k = a, 2 K-steps; col = the lane's stacked row (g, c))
+INA_DEVICE void load_cf(const NtnArgs& k, const Geo& g, int epw, int q, u16x8_t (&Cf)[2]) {
+  const int ep = epw + g.lg;
+  const bool ok = g.lrow && ep < k.E;
+  const long row = (long)(ok ? ep : 0) * g.N + g.lc;
 #pragma unroll
-    for (int ka = 0; ka < NKA; ++ka)
+  for (int ka = 0; ka < 2; ++ka)
+#pragma unroll
+    for (int h4 = 0; h4 < 2; ++h4) {
+      const int a = 32 * ka + 8 * q + 4 * h4;
+      ld4bf(k.cls, ok && a < g.H, row * g.H + a, Cf[ka], 4 * h4);
+    }
+}
+// Q^T as the B operand of T^T: B[k = b][col = query 16 qt + n]
+template <int QT>
+INA_DEVICE void load_qf(const NtnArgs& k, const Geo& g, int ep, bool oke, int q, int n, u16x8_t (&Qf)[QT][2]) {
+  const long rq0 = (long)(oke ? ep : 0) * (g.N * k.K + g.NQ) + g.N * k.K;
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int h4 = 0; h4 < 2; ++h4) {
-        const int a = 32 * ka + 8 * q + 4 * h4;
-        ld4bf(cls, n < N && a < H, ((long)epc * N + n) * H + a, Cf[ka], 4 * h4);
+        const int qi = 16 * qt + n, b = 32 * kb + 8 * q + 4 * h4;
+        ld4bf(k.e, oke && qi < g.NQ && b < g.H, (rq0 + qi) * g.H + b, Qf[qt][kb], 4 * h4);
       }
-    u16x8_t Qf[QT][NKB];
+}
+
+// P^T_s for the SG slices of the staged tile (stacked over the wave's episodes) -> the P images
+template <int MTH>
+INA_DEVICE void p_images(const unsigned char* buf, const unsigned char* zero, unsigned char* pimg, const Geo& g,
+                         const u16x8_t (&Cf)[2], int q, int n) {
+  constexpr int RA = 16 * MTH;
+  for (int sl = 0; sl < g.SG; ++sl) {
+    const unsigned char* mimg = buf + sl * (RA * IMG_ROW);
+    f32x4_t PT[MTH];
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt)
+    for (int mb = 0; mb < MTH; ++mb) PT[mb] = Z4;
 #pragma unroll
-      for (int kb = 0; kb < NKB; ++kb)
+    for (int ka = 0; ka < 2; ++ka) {
+      const int a0 = 32 * ka + 8 * q + (n >> 2), a1 = a0 + 4;
 #pragma unroll
-        for (int h4 = 0; h4 < 2; ++h4) {   // kmap32: elements 4 h4 .. +3 = features 32 kb + 16 h4 + 4q .. +3
-          const int qi = 16 * qt + n, b = 32 * kb + 16 * h4 + 4 * q;
-          ld4bf(e, qi < NQ && b < H, (rq0 + qi) * H + b, Qf[qt][kb], 4 * h4);
-        }
-    f32x4_t Lg[QT];
+      for (int mb = 0; mb < MTH; ++mb) {
+        const int c8 = 4 * mb + (n & 3);
+        const unsigned char* p0 = a0 < RA ? mimg + a0 * IMG_ROW + ((c8 ^ mask_m(a0)) << 3) : zero;
+        const unsigned char* p1 = a1 < RA ? mimg + a1 * IMG_ROW + ((c8 ^ mask_m(a1)) << 3) : zero;
+        PT[mb] = mfma_bf16(cat8(trr(p0), trr(p1)), Cf[ka], PT[mb]);
+      }
+    }
+    if (g.lrow) {
+      const int row = sl * g.N + g.lc;
+      unsigned char* dst = pimg + g.lg * PIMG + row * IMG_ROW;
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt) Lg[qt] = Z4;
-    __syncthreads();  // previous group's readers are done with buffer 0
-    ntn_stage<MTH, NSW, false>(ntn_lds, p0, mpack, nullptr, wpack, 1);
+      for (int mb = 0; mb < MTH; ++mb)
+        *reinterpret_cast<s16x4_t*>(dst + (((4 * mb + q) ^ mask_p(row)) << 3)) = bf4(PT[mb]);
+    }
+  }
+}
+
+// A = P_g[i = (s,c) = n][k = b], the two 32-deep K-steps
+INA_DEVICE void p_rows(const unsigned char* img, int q, int n, u16x8_t (&Pa)[2]) {
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+    Pa[kb] = *reinterpret_cast<const u16x8_t*>(img + n * IMG_ROW + (((8 * kb + 2 * q) ^ mask_p(n)) << 3));
+}
+
+// ------------------------------------------------------------------------------------------
+template <int MTH, int QT>
+__global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void ntn_fwd_kernel(NtnArgs k) {
+  constexpr int GM = QT <= 2 ? 2 : 1;
+  extern __shared__ __attribute__((aligned(16))) unsigned char ntn_lds[];
+  const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15, wave = threadIdx.x >> 6;
+  const Geo g = geo(k, n);
+  const int t0 = (int)((long)k.ntile * blockIdx.y / gridDim.y), t1 = (int)((long)k.ntile * (blockIdx.y + 1) / gridDim.y);
+  unsigned char* const zero = ntn_lds + 2 * k.tpb;
+  uint32_t woff = 2 * k.tpb + ZERO_BYTES + wave * (GM * PIMG);   // the wave's P images
+  for (int i = lane; i < GM * PIMG / 16; i += 64) reinterpret_cast<u32x4_t*>(ntn_lds + woff)[i] = u32x4_t{0u, 0u, 0u, 0u};
+  if (wave == 0)
+    for (int i = lane; i < ZERO_BYTES / 16; i += 64) reinterpret_cast<u32x4_t*>(zero)[i] = u32x4_t{0u, 0u, 0u, 0u};
+  const int nfrag = k.tpb >> 10;
+  const unsigned char* tiles = reinterpret_cast<const unsigned char*>(k.tiles);
+  const int fo = g.SG * MTH * 16 * IMG_ROW;   // FC fragments after the M images
+  for (int grp = blockIdx.x; grp * NW * g.G < k.E; grp += gridDim.x) {
+    const int epw = (grp * NW + wave) * g.G;
+    u16x8_t Cf[2];
+    load_cf(k, g, epw, q, Cf);
+    u16x8_t Qf[GM][QT][2];
+    f32x4_t Lg[GM][QT];
+#pragma unroll
+    for (int gi = 0; gi < GM; ++gi) {
+      load_qf<QT>(k, g, epw + gi, gi < g.G && epw + gi < k.E, q, n, Qf[gi]);
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) Lg[gi][qt] = Z4;
+    }
+    __syncthreads();   // the previous group's readers are done with the stage buffers
+    stage_tile(ntn_lds, tiles + (long)t0 * k.tpb, nfrag);
     stage_wait();
     __syncthreads();
-    for (int p = p0; p < p1; ++p) {
-      const u16x8_t* buf = ntn_lds + ((p - p0) & 1) * FR * 64;
-      if (p + 1 < p1) ntn_stage<MTH, NSW, false>(ntn_lds + ((p + 1 - p0) & 1) * FR * 64, p + 1, mpack, nullptr, wpack, 1);
-      if (act) {
-        f32x4_t V[2][QT];
+    for (int t = t0; t < t1; ++t) {
+      const unsigned char* buf = ntn_lds + ((t - t0) & 1) * k.tpb;
+      if (t + 1 < t1) stage_tile(ntn_lds + ((t + 1 - t0) & 1) * k.tpb, tiles + (long)(t + 1) * k.tpb, nfrag);
+      const int lt = opaque_lane(), q = lt >> 4, n = lt & 15;
+      const Geo g = geo(k, n);
+      p_images<MTH>(buf, zero, ntn_lds + woff, g, Cf, q, n);
+      wave_order(woff);
+      const s16x4_t wt = *reinterpret_cast<const s16x4_t*>(buf + fo + 512 + lt * 8);
 #pragma unroll
-        for (int sl = 0; sl < 2; ++sl) {
-          const int s = 2 * p + sl;
-          f32x4_t PT[2 * NKB];
-#pragma unroll
-          for (int mb = 0; mb < 2 * NKB; ++mb) {
-            PT[mb] = Z4;
-            if (mb < MTH) {
-#pragma unroll
-              for (int ka = 0; ka < NKA; ++ka)
-                PT[mb] = mfma_bf16(buf[((sl * MTH + mb) * NKA + ka) * 64 + lane], Cf[ka], PT[mb]);
-            }
-          }
-          u16x8_t PTf[NKB];
-#pragma unroll
-          for (int kb = 0; kb < NKB; ++kb) PTf[kb] = pack2(PT[2 * kb], PT[2 * kb + 1]);
+      for (int gi = 0; gi < GM; ++gi) {
+        if (gi < g.G) {
+          u16x8_t Pa[2];
+          p_rows(ntn_lds + woff + gi * PIMG, q, n, Pa);
 #pragma unroll
           for (int qt = 0; qt < QT; ++qt) {
-            f32x4_t T = Z4;
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) T = mfma_bf16(PTf[kb], Qf[qt][kb], T);
-            if (PAPER) {
-              const float ws = s < h ? wvec[s < h ? s : 0] : 0.f;
-              const f32x4_t Rl = relu4(T);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) Lg[qt][r] += ws * Rl[r];
-            } else {
-              V[sl][qt] = relu4(T);  // zero M for s >= h -> T = 0
-            }
+            f32x4_t T = mfma_bf16(Pa[0], Qf[gi][qt][0], Z4);
+            T = mfma_bf16(Pa[1], Qf[gi][qt][1], T);   // rows (s, c), cols query
+            Lg[gi][qt] = mfma16_bf16(wt, bf4relu(T), Lg[gi][qt]);
           }
-        }
-        if (!PAPER) {
-          const u16x8_t wf = buf[(2 * MTH * NKA) * 64 + lane];
-#pragma unroll
-          for (int qt = 0; qt < QT; ++qt) Lg[qt] = mfma_bf16(pack2(V[0][qt], V[1][qt]), wf, Lg[qt]);
         }
       }
       stage_wait();
       __syncthreads();
     }
-    if (act) {
+#pragma unroll
+    for (int gi = 0; gi < GM; ++gi) {
+      const int ep = epw + gi;
+      if (gi >= g.G || ep >= k.E) continue;
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          // PAPER: rows c, cols query; reference head: rows query, cols c'
-          const int c = PAPER ? 4 * q + r : n, qi = PAPER ? 16 * qt + n : 16 * qt + 4 * q + r;
-          if (c < N && qi < NQ) {
-            const long o = ((long)ep * NQ + qi) * N + c;
+          const int c = 4 * q + r, qi = 16 * qt + n;   // logits^T: rows class c', cols query
+          if (c < g.N && qi < g.NQ) {
+            const long o = ((long)ep * g.NQ + qi) * g.N + c;
             if (gridDim.y == 1)
-              probs[o] = sigmoidf_(Lg[qt][r] + bias[PAPER ? 0 : c]);
+              k.probs[o] = sigmoidf_(Lg[gi][qt][r] + k.bias[k.paper ? 0 : c]);
             else
-              part[(long)blockIdx.y * E * NQ * N + o] = Lg[qt][r];
+              k.part[(long)blockIdx.y * k.E * g.NQ * g.N + o] = Lg[gi][qt][r];
           }
         }
     }
@@ -220,470 +258,265 @@ __global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(4))
 }
 
 // ------------------------------------------------------------------------------------------
-// Outputs: dcls [E,N,H]; de query rows [S,H]; dp_out bf16 [E*N][h*H] (col s*H + b);
-//          dw_slab [ntn_groups(E)][h][N][N] (reference head: the workgroup's 8 episodes summed in fixed wave
-//          order through LDS, one slab row per workgroup group) or [E][h] (paper head).
-template <int MTH, int QT, bool PAPER>
-__global__ __launch_bounds__(NTN_THREADS) __attribute__((amdgpu_waves_per_eu(2))) void ntn_bwd_kernel(
-    const float* __restrict__ cls, const float* __restrict__ e, int E, int N, int K, int Q, int H, int h,
-    const u16x8_t* __restrict__ mpack, const u16x8_t* __restrict__ m2pack, const u16x8_t* __restrict__ wtpack,
-    const float* __restrict__ wvec, const float* __restrict__ dz, float* __restrict__ dcls, float* __restrict__ de,
-    unsigned short* __restrict__ dp_out, float* __restrict__ dw_slab, const float* __restrict__ gscale,
-    unsigned short* __restrict__ cls_bf, float* __restrict__ pc, float* __restrict__ pq) {
-  constexpr int NKA = (MTH + 1) / 2, NKB = (MTH + 1) / 2, KQ = (QT + 1) / 2;
-  const float gs = gscale ? gscale[0] : 1.f;   // upstream scale of dz (loss.backward(g))
-  constexpr int NSW = PAPER ? 0 : 2;
-  constexpr int F1 = 2 * MTH * NKA, F2 = 2 * MTH * NKB;
-  constexpr int FR = F1 + F2 + NSW;
-  extern __shared__ __attribute__((aligned(16))) u16x8_t ntn_lds[];
+template <int MTH, int QT>
+__global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(2))) void ntn_bwd_kernel(NtnArgs k) {
+  constexpr int GM = QT <= 2 ? 2 : 1;
+  constexpr int KQ = (QT + 1) / 2;     // 32-deep K-steps over the queries
+  constexpr int VIMG = KQ * 32 * 32;   // V / dT image [32 KQ rows (query)][16 cols (slice, class)] bf16
+  constexpr int RA = 16 * MTH;
+  extern __shared__ __attribute__((aligned(16))) unsigned char ntn_lds[];
   const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15, wave = threadIdx.x >> 6;
-  const int NQ = N * Q;
-  const long hH = (long)h * H;
-  const int npair = (h + 1) / 2;
-  // slice split: pairs [p0, p1) of workgroup row blockIdx.y; dC / dQ partials -> pc / pq (ntn_bwd_finish)
-  const int p0 = (int)((long)npair * blockIdx.y / gridDim.y), p1 = (int)((long)npair * (blockIdx.y + 1) / gridDim.y);
-  if (gridDim.y > 1 && blockIdx.y > 0) cls_bf = nullptr;   // one writer of the bf16 class vectors
-  for (int g = blockIdx.x; g * NTN_WAVES < E; g += gridDim.x) {
-    const int ep = g * NTN_WAVES + wave;
-    const bool act = ep < E;
-    const int epc = act ? ep : E - 1;
-    const long rq0 = (long)epc * (N * K + NQ) + N * K;
-    const float* dze = dz + (long)epc * NQ * N;
-#if INA_NTN_BWD_LD
-    u16x8_t Cf[NKA];
+  const Geo g = geo(k, n);
+  const int t0 = (int)((long)k.ntile * blockIdx.y / gridDim.y), t1 = (int)((long)k.ntile * (blockIdx.y + 1) / gridDim.y);
+  const bool split = gridDim.y > 1;
+  unsigned char* const zero = ntn_lds + 2 * k.tpb;
+  // the wave's images [P_0 .. P_{GM-1} | V | dT] at byte offset woff (laundered at every order point)
+  uint32_t woff = 2 * k.tpb + ZERO_BYTES + wave * (GM * PIMG + 2 * VIMG);
+  float* const dwl = reinterpret_cast<float*>(zero + ZERO_BYTES + NW * (GM * PIMG + 2 * VIMG));
+  // zero once: rows / columns of the images no product writes (query rows >= 16 QT of V / dT, P columns >= H)
+  for (int i = lane; i < (GM * PIMG + 2 * VIMG) / 16; i += 64)
+    reinterpret_cast<u32x4_t*>(ntn_lds + woff)[i] = u32x4_t{0u, 0u, 0u, 0u};
+  if (wave == 0)
+    for (int i = lane; i < ZERO_BYTES / 16; i += 64) reinterpret_cast<u32x4_t*>(zero)[i] = u32x4_t{0u, 0u, 0u, 0u};
+  const int nfrag = k.tpb >> 10;
+  const unsigned char* tiles = reinterpret_cast<const unsigned char*>(k.tiles);
+  const int fo = g.SG * MTH * 16 * IMG_ROW;
+  const float gs = k.gscale ? k.gscale[0] : 1.f;
+  const int SGN = g.SG * g.N;
+  const int dwe = k.paper ? g.SG : SGN * g.N;   // dw slab entries per tile
+  const long hH = (long)k.h * g.H;
+  unsigned short* const dp = reinterpret_cast<unsigned short*>(k.dp_out);
+  unsigned short* const dp_trash = dp + ((long)k.E * g.N + 63) / 64 * 64 * hH;   // past the zero pad rows
+  for (int grp = blockIdx.x; grp * NW * g.G < k.E; grp += gridDim.x) {
+    const int epw = (grp * NW + wave) * g.G;
+    u16x8_t Cf[2];
+    load_cf(k, g, epw, q, Cf);
+    if (k.cls_bf && !blockIdx.y && g.lrow && epw + g.lg < k.E) {
 #pragma unroll
-    for (int ka = 0; ka < NKA; ++ka)
-#pragma unroll
-      for (int h4 = 0; h4 < 2; ++h4) {
-        const int a = 32 * ka + 8 * q + 4 * h4;
-        ld4bf(cls, n < N && a < H, ((long)epc * N + n) * H + a, Cf[ka], 4 * h4);
-      }
-    if (cls_bf && act && n < N) {
-#pragma unroll
-      for (int ka = 0; ka < NKA; ++ka) {
+      for (int ka = 0; ka < 2; ++ka) {
         const int a = 32 * ka + 8 * q;
-        if (a < H) *reinterpret_cast<u16x8_t*>(cls_bf + ((long)ep * N + n) * H + a) = Cf[ka];
+        if (a < g.H)
+          *reinterpret_cast<u16x8_t*>(reinterpret_cast<unsigned short*>(k.cls_bf) +
+                                      ((long)(epw + g.lg) * g.N + g.lc) * g.H + a) = Cf[ka];
       }
     }
-    u16x8_t Qf[QT][NKB];
+    u16x8_t Qf[GM][QT][2];
+    u16x8_t QB[GM][MTH][KQ];   // A = Q^T[i = b][k = query]
+    s16x4_t dzT[GM][QT];       // B[k = c'][col = query] (16x16x16)
+    u16x8_t dzB[GM][KQ];       // B[k = query][col = c']
+    f32x4_t dQ[GM][MTH][QT];   // dQ^T[b][query]
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt)
+    for (int gi = 0; gi < GM; ++gi) {
+      const int ep = epw + gi;
+      const bool oke = gi < g.G && ep < k.E;
+      load_qf<QT>(k, g, ep, oke, q, n, Qf[gi]);
+      const long rq0 = (long)(oke ? ep : 0) * (g.N * k.K + g.NQ) + g.N * k.K;
+      const float* dze = k.dz + (long)(oke ? ep : 0) * g.NQ * g.N;
 #pragma unroll
-      for (int kb = 0; kb < NKB; ++kb)
+      for (int mb = 0; mb < MTH; ++mb)
 #pragma unroll
-        for (int h4 = 0; h4 < 2; ++h4) {
-          const int qi = 16 * qt + n, b = 32 * kb + 16 * h4 + 4 * q;
-          ld4bf(e, qi < NQ && b < H, (rq0 + qi) * H + b, Qf[qt][kb], 4 * h4);
+        for (int kq = 0; kq < KQ; ++kq)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int b = 16 * mb + n, qi = 32 * kq + 8 * q + j;
+            QB[gi][mb][kq][j] = f2bf(ldz(k.e, oke && qi < g.NQ && b < g.H, (rq0 + qi) * g.H + b));
+          }
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int qi = 16 * qt + n, cp = 4 * q + j;
+          dzT[gi][qt][j] = (short)f2bf(gs * ldz(dze, oke && qi < g.NQ && cp < g.N, qi * g.N + cp));
         }
-    // Q^T as the A operand over queries: A[i = b][k = query (kmap32)]
-    __builtin_amdgcn_sched_barrier(0);   // load groups in turn: bounded registers in flight
-    // (TR: natural query order k = q -- the dT^T operand then comes from a row-major LDS image)
-    u16x8_t QTf[MTH][KQ];
-#pragma unroll
-    for (int mb = 0; mb < MTH; ++mb)
 #pragma unroll
       for (int kq = 0; kq < KQ; ++kq)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int b = 16 * mb + n, qi = 32 * kq + (INA_NTN_TR ? 8 * q + j : kmap32(q, j));
-          QTf[mb][kq][j] = f2bf(ldz(e, qi < NQ && b < H, (rq0 + qi) * H + b));
+          const int qi = 32 * kq + 8 * q + j;
+          dzB[gi][kq][j] = f2bf(gs * ldz(dze, oke && qi < g.NQ && n < g.N, qi * g.N + n));
         }
-    __builtin_amdgcn_sched_barrier(0);
-    u16x8_t dzA[QT];           // A[i = query][k = c']
-    u16x8_t dzB[KQ];           // B[k = query (kmap32)][j = c']
-    f32x4_t dzC[QT], dzR[QT];  // accumulator layouts: dzC rows c / cols query, dzR rows query / cols c
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
+      for (int mb = 0; mb < MTH; ++mb)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int qi = 16 * qt + n, cp = 8 * q + j;
-        dzA[qt][j] = f2bf(gs * ldz(dze, qi < NQ && cp < N, qi * N + cp));
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = 4 * q + r, qi = 16 * qt + n;
-        dzC[qt][r] = gs * ldz(dze, c < N && qi < NQ, qi * N + c);
-        const int qr = 16 * qt + 4 * q + r;
-        dzR[qt][r] = gs * ldz(dze, n < N && qr < NQ, qr * N + n);
-      }
+        for (int qt = 0; qt < QT; ++qt) dQ[gi][mb][qt] = Z4;
     }
+    f32x4_t dC[MTH];   // dC^T[a][(g, c)]
 #pragma unroll
-    for (int kq = 0; kq < KQ; ++kq)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int qi = 32 * kq + (INA_NTN_TR ? 8 * q + j : kmap32(q, j));
-        dzB[kq][j] = f2bf(gs * ldz(dze, qi < NQ && n < N, qi * N + n));
-      }
-    __builtin_amdgcn_sched_barrier(0);
-#else
-    static_assert(!INA_NTN_TR, "the LDS-transpose backward needs the vectorized prologue (INA_NTN_BWD_LD)");
-    u16x8_t Cf[NKA];
-#pragma unroll
-    for (int ka = 0; ka < NKA; ++ka)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int a = 32 * ka + 8 * q + j;
-        Cf[ka][j] = (n < N && a < H) ? f2bf(cls[((long)epc * N + n) * H + a]) : (unsigned short)0;
-        if (cls_bf && act && n < N && a < H) cls_bf[((long)ep * N + n) * H + a] = Cf[ka][j];
-      }
-    u16x8_t Qf[QT][NKB];
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int qi = 16 * qt + n, b = 32 * kb + kmap32(q, j);
-          Qf[qt][kb][j] = (qi < NQ && b < H) ? f2bf(e[(rq0 + qi) * H + b]) : (unsigned short)0;
-        }
-    // Q^T as the A operand over queries: A[i = b][k = query (kmap32)]
-    u16x8_t QTf[MTH][KQ];
-#pragma unroll
-    for (int mb = 0; mb < MTH; ++mb)
-#pragma unroll
-      for (int kq = 0; kq < KQ; ++kq)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int b = 16 * mb + n, qi = 32 * kq + kmap32(q, j);
-          QTf[mb][kq][j] = (qi < NQ && b < H) ? f2bf(e[(rq0 + qi) * H + b]) : (unsigned short)0;
-        }
-    u16x8_t dzA[QT];           // A[i = query][k = c']
-    u16x8_t dzB[KQ];           // B[k = query (kmap32)][j = c']
-    f32x4_t dzC[QT], dzR[QT];  // accumulator layouts: dzC rows c / cols query, dzR rows query / cols c
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int qi = 16 * qt + n, cp = 8 * q + j;
-        dzA[qt][j] = (qi < NQ && cp < N) ? f2bf(gs * dze[qi * N + cp]) : (unsigned short)0;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = 4 * q + r, qi = 16 * qt + n;
-        dzC[qt][r] = (c < N && qi < NQ) ? gs * dze[qi * N + c] : 0.f;
-        const int qr = 16 * qt + 4 * q + r;
-        dzR[qt][r] = (n < N && qr < NQ) ? gs * dze[qr * N + n] : 0.f;
-      }
-    }
-#pragma unroll
-    for (int kq = 0; kq < KQ; ++kq)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int qi = 32 * kq + kmap32(q, j);
-        dzB[kq][j] = (qi < NQ && n < N) ? f2bf(gs * dze[qi * N + n]) : (unsigned short)0;
-      }
-#endif
-    f32x4_t dCT[MTH], dQT[MTH][QT];
-#pragma unroll
-    for (int m = 0; m < MTH; ++m) {
-      dCT[m] = Z4;
-#pragma unroll
-      for (int qt = 0; qt < QT; ++qt) dQT[m][qt] = Z4;
-    }
-    // Per-lane store bases of the per-slice dP / dw outputs, chosen once per group: lanes outside
-    // the N x N / H ranges point into the trash tail the host allocates past each buffer, so the
-    // slice loop's stores are unconditional.  (Guarded stores split the loop into ~15 basic
-    // blocks -- exec-mask branches the scheduler cannot move MFMAs across -- and re-derived the
-    // 64-bit row offsets with v_mul_lo_u32 per slice.)
-    unsigned short* dpb[MTH];
-#pragma unroll
-    for (int mb = 0; mb < MTH; ++mb) {
-      const int b0 = 16 * mb + 4 * q;
-      dpb[mb] = dp_out + ((n < N && b0 < H) ? ((long)epc * N + n) * hH + b0 : (long)E * N * hH);
-    }
-    // reference head dw: per (pair parity, wave, slice) an [N*N + 1] LDS slot (the last entry takes the
-    // lanes outside N x N); summed over the group's waves in fixed order one pair later (flush_dw)
-    const int NN1 = N * N + 1;
-    float* const dwl = reinterpret_cast<float*>(ntn_lds + 2 * FR * 64);
-    // TR: wave-private bf16 images (after the dw slots): I_P [32 rows (slice, class)][PS] = the pair's P^T
-    // transposed; I_V / I_dT [32 KQ rows (query)][VS] = relu(T) / dT with the queries on the rows
-    constexpr int PS = 16 * MTH + 4, VS = 20, IPN = 32 * PS, IVN = 32 * KQ * VS;
-    // (byte offset arithmetic on the __shared__ pointer: a uintptr_t round trip would turn these accesses
-    // into FLAT instructions)
-    unsigned short* const imgP =
-        reinterpret_cast<unsigned short*>(reinterpret_cast<unsigned char*>(dwl) +
-                                          (((PAPER ? 0 : 2 * NTN_WAVES * 2 * NN1) * 4 + 15) & ~15)) +
-        (size_t)wave * (IPN + 2 * IVN);
-    unsigned short* const imgV = imgP + IPN;
-    unsigned short* const imgD = imgV + IVN;
-    if (INA_NTN_TR && g == (int)blockIdx.x)   // once: rows / columns a shape never writes must read as zero
-      for (int i = lane; i < (IPN + 2 * IVN) / 2; i += 64) reinterpret_cast<uint32_t*>(imgP)[i] = 0u;
-    const int nw = E - g * NTN_WAVES < NTN_WAVES ? E - g * NTN_WAVES : NTN_WAVES;   // active waves of the group
-    auto flush_dw = [&](int pp) {
-      if (PAPER) return;
-      if ((int)threadIdx.x < 2 * N * N) {
-        const int sl = (int)threadIdx.x / (N * N), rem = (int)threadIdx.x - sl * N * N, sv = 2 * pp + sl;
-        if (sv < h) {
-          const float* src = dwl + ((pp & 1) * NTN_WAVES * 2 + sl) * NN1 + rem;
-          float acc = 0.f;
-          for (int w = 0; w < nw; ++w) acc += src[w * 2 * NN1];
-          dw_slab[((long)g * h + sv) * N * N + rem] = acc;
-        }
-      }
-    };
+    for (int ma = 0; ma < MTH; ++ma) dC[ma] = Z4;
     __syncthreads();
-    ntn_stage<MTH, NSW, true>(ntn_lds, p0, mpack, m2pack, wtpack, 2);
+    stage_tile(ntn_lds, tiles + (long)t0 * k.tpb, nfrag);
     stage_wait();
     __syncthreads();
-    for (int p = p0; p < p1; ++p) {
-      if (p > p0) flush_dw(p - 1);   // the previous pair's dw slots are complete (barrier at its end)
-      const u16x8_t* buf = ntn_lds + ((p - p0) & 1) * FR * 64;
-      if (p + 1 < p1) ntn_stage<MTH, NSW, true>(ntn_lds + ((p + 1 - p0) & 1) * FR * 64, p + 1, mpack, m2pack, wtpack, 2);
-#if INA_NTN_TR
-      if (act) {
-        f32x4_t dTs[2][QT];
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl) {
-          const int s = 2 * p + sl;
-          const bool sok = s < h;   // (a padding slice runs on zero packs and stores into the trash tails)
-          f32x4_t PT[2 * NKB];
-#pragma unroll
-          for (int mb = 0; mb < 2 * NKB; ++mb) {
-            PT[mb] = Z4;
-            if (mb < MTH) {
-#pragma unroll
-              for (int ka = 0; ka < NKA; ++ka) PT[mb] = mfma_bf16(buf[((sl * MTH + mb) * NKA + ka) * 64 + lane], Cf[ka], PT[mb]);
-            }
-          }
-          u16x8_t PTf[NKB];
-#pragma unroll
-          for (int kb = 0; kb < NKB; ++kb) PTf[kb] = pack2(PT[2 * kb], PT[2 * kb + 1]);
-          // P^T [b][c = n] -> I_P row (slice sl, class n) in the pair-fragment k order 8 (c >> 2) + 4 sl + (c & 3)
-          {
-            unsigned short* row = imgP + (8 * (n >> 2) + 4 * sl + (n & 3)) * PS + 4 * q;
-#pragma unroll
-            for (int mb = 0; mb < MTH; ++mb) {
-              const u16x8_t& f = PTf[mb >> 1];
-              const int o = 4 * (mb & 1);
-              *reinterpret_cast<u16x4_t*>(row + 16 * mb) = u16x4_t{f[o], f[o + 1], f[o + 2], f[o + 3]};
-            }
-          }
-          u16x8_t wt = {0, 0, 0, 0, 0, 0, 0, 0};
-          float ws = 0.f;
-          if (PAPER) ws = wvec[s];
-          else wt = buf[(F1 + F2 + sl) * 64 + lane];
-          float dwp = 0.f;
-#pragma unroll
-          for (int qt = 0; qt < QT; ++qt) {
-            f32x4_t T = Z4;
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) T = mfma_bf16(PTf[kb], Qf[qt][kb], T);   // rows c, cols query
-            f32x4_t dV;
-            if (PAPER) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                dV[r] = ws * dzC[qt][r];
-                dwp += fmaxf(T[r], 0.f) * dzC[qt][r];
-              }
-            } else {
-              dV = mfma_bf16(wt, dzA[qt], Z4);   // rows c, cols query
-            }
-            f32x4_t V;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              dTs[sl][qt][r] = T[r] > 0.f ? dV[r] : 0.f;
-              V[r] = fmaxf(T[r], 0.f);
-            }
-            // rows c = 4q + r, cols query 16 qt + n -> I_V / I_dT row = query, cols c
-            const int ro = (16 * qt + n) * VS + 4 * q;
-            if (!PAPER)
-              *reinterpret_cast<u16x4_t*>(imgV + ro) = u16x4_t{f2bf(V[0]), f2bf(V[1]), f2bf(V[2]), f2bf(V[3])};
-            *reinterpret_cast<u16x4_t*>(imgD + ro) =
-                u16x4_t{f2bf(dTs[sl][qt][0]), f2bf(dTs[sl][qt][1]), f2bf(dTs[sl][qt][2]), f2bf(dTs[sl][qt][3])};
-          }
-          lds_order();
-          if (PAPER) {
-            dwp = wave_sum(dwp);
-            if (lane == 0 && sok) dw_slab[(long)ep * h + s] = dwp;
-          } else {
-            f32x4_t dw = Z4;   // dw[c][c'] = sum_q relu(T)[c][q] dz[q][c']
-#pragma unroll
-            for (int kq = 0; kq < KQ; ++kq) dw = mfma_bf16(tr_read8(imgV + kq * 32 * VS, VS, 0, q, n), dzB[kq], dw);
-            float* const dst = dwl + (((p & 1) * NTN_WAVES + wave) * 2 + sl) * NN1;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dst[(4 * q + r < N && n < N) ? (4 * q + r) * N + n : N * N] = dw[r];
-          }
-          // dP^T[b, c] = sum_q Q[q, b] dT[c, q]  (B = dT^T from I_dT)
-          u16x8_t dTB[KQ];
-#pragma unroll
-          for (int kq = 0; kq < KQ; ++kq) dTB[kq] = tr_read8(imgD + kq * 32 * VS, VS, 0, q, n);
-          lds_order();   // the next slice's image stores come after these reads
-          f32x4_t dPT[2 * NKB];
-#pragma unroll
-          for (int mb = 0; mb < 2 * NKB; ++mb) {
-            dPT[mb] = Z4;
-            if (mb < MTH) {
-#pragma unroll
-              for (int kq = 0; kq < KQ; ++kq) dPT[mb] = mfma_bf16(QTf[mb][kq], dTB[kq], dPT[mb]);
-            }
-          }
-          // dC^T[a, c] += sum_b M[a, b, s] dP[c, b]
-#pragma unroll
-          for (int kb = 0; kb < NKB; ++kb) {
-            const u16x8_t dPf = pack2(dPT[2 * kb], dPT[2 * kb + 1]);
-#pragma unroll
-            for (int ma = 0; ma < MTH; ++ma)
-              dCT[ma] = mfma_bf16(buf[(F1 + (sl * MTH + ma) * NKB + kb) * 64 + lane], dPf, dCT[ma]);
-          }
-          // dP -> bf16 [E*N][h*H] for the dM reduction GEMM
-          unsigned short* const dpt = dp_out + (long)E * N * hH;
-#pragma unroll
-          for (int mb = 0; mb < MTH; ++mb)
-            *reinterpret_cast<u16x4_t*>(sok ? dpb[mb] + s * H : dpt) =
-                u16x4_t{f2bf(dPT[mb][0]), f2bf(dPT[mb][1]), f2bf(dPT[mb][2]), f2bf(dPT[mb][3])};
+    for (int t = t0; t < t1; ++t) {
+      const int par = (t - t0) & 1;
+      const unsigned char* buf = ntn_lds + par * k.tpb;
+      if (t + 1 < t1) stage_tile(ntn_lds + (par ^ 1) * k.tpb, tiles + (long)(t + 1) * k.tpb, nfrag);
+      const int lt = opaque_lane(), q = lt >> 4, n = lt & 15;
+      const Geo g = geo(k, n);
+      const int dsl = n / g.N, dcl = n - dsl * g.N;
+      if (t > t0 && (int)threadIdx.x < dwe) {   // flush the previous tile's dw (slots complete: barrier)
+        const float* src = dwl + (par ^ 1) * NW * DW_SLOT;
+        float acc = 0.f;
+        if (k.paper) {
+          for (int w = 0; w < NW; ++w)
+            for (int c = 0; c < g.N; ++c) acc += src[w * DW_SLOT + (threadIdx.x * g.N + c) * 16 + c];
+        } else {
+          const int row = threadIdx.x / g.N, cp = threadIdx.x - row * g.N;
+          for (int w = 0; w < NW; ++w) acc += src[w * DW_SLOT + row * 16 + cp];
         }
-        // dQ^T[b, q] += sum_{s in pair, c} P_s[c, b] dT_s[c, q]  (A = the pair's P from I_P)
-        lds_order();
-#pragma unroll
-        for (int nb = 0; nb < MTH; ++nb) {
-          const u16x8_t Pf = tr_read8(imgP, PS, 16 * nb, q, n);
-#pragma unroll
-          for (int qt = 0; qt < QT; ++qt) dQT[nb][qt] = mfma_bf16(Pf, pack2(dTs[0][qt], dTs[1][qt]), dQT[nb][qt]);
-        }
-        lds_order();
+        k.dw_slab[((long)grp * k.ntile + t - 1) * dwe + threadIdx.x] = acc;
       }
-#else
-      if (act) {
-        f32x4_t Ps[2][MTH], dTs[2][QT];
+      p_images<MTH>(buf, zero, ntn_lds + woff, g, Cf, q, n);
+      wave_order(woff);
+      const s16x4_t wA = *reinterpret_cast<const s16x4_t*>(buf + fo + lt * 8);
+      f32x4_t dw = Z4;
 #pragma unroll
-        for (int sl = 0; sl < 2; ++sl) {
-          const int s = 2 * p + sl;
+      for (int gi = 0; gi < GM; ++gi) {
+        if (gi >= g.G) continue;
+        const int ep = epw + gi;
+        unsigned char* pg = ntn_lds + woff + gi * PIMG;
+        unsigned char* vimg = ntn_lds + woff + GM * PIMG;
+        unsigned char* dtimg = vimg + VIMG;
+        u16x8_t Pa[2];
+        p_rows(pg, q, n, Pa);
+        f32x4_t dT[QT];
 #pragma unroll
-          for (int m = 0; m < MTH; ++m) Ps[sl][m] = Z4;
+        for (int qt = 0; qt < QT; ++qt) {
+          f32x4_t T = mfma_bf16(Pa[0], Qf[gi][qt][0], Z4);
+          T = mfma_bf16(Pa[1], Qf[gi][qt][1], T);                 // rows (s, c), cols query
+          const f32x4_t dV = mfma16_bf16(wA, dzT[gi][qt], Z4);   // rows (s, c), cols query
 #pragma unroll
-          for (int qt = 0; qt < QT; ++qt) dTs[sl][qt] = Z4;
-          // a padding slice (odd h, s = h) runs on the zero-padded packs -- all its values are zero -- and
-          // stores into the trash tails: no branch between the pair's two slice chains, so the scheduler
-          // can interleave them
-          const bool sok = s < h;
-          // P^T (rows b, cols c) and P (rows c, cols b) from the same fragments (operand swap)
-          f32x4_t PT[2 * NKB];
-#pragma unroll
-          for (int mb = 0; mb < 2 * NKB; ++mb) {
-            PT[mb] = Z4;
-            if (mb < MTH) {
-#pragma unroll
-              for (int ka = 0; ka < NKA; ++ka) {
-                const u16x8_t mf = buf[((sl * MTH + mb) * NKA + ka) * 64 + lane];
-                PT[mb] = mfma_bf16(mf, Cf[ka], PT[mb]);
-                Ps[sl][mb] = mfma_bf16(Cf[ka], mf, Ps[sl][mb]);
-              }
-            }
-          }
-          u16x8_t PTf[NKB];
-#pragma unroll
-          for (int kb = 0; kb < NKB; ++kb) PTf[kb] = pack2(PT[2 * kb], PT[2 * kb + 1]);
-          u16x8_t wt = {0, 0, 0, 0, 0, 0, 0, 0};
-          float ws = 0.f;
-          if (PAPER) {
-            ws = wvec[s];
-          } else {
-            wt = buf[(F1 + F2 + sl) * 64 + lane];
-          }
-          f32x4_t VT[2 * KQ], dTT[2 * KQ];
-#pragma unroll
-          for (int i = 0; i < 2 * KQ; ++i) VT[i] = dTT[i] = Z4;
-          float dwp = 0.f;
-#pragma unroll
-          for (int qt = 0; qt < QT; ++qt) {
-            f32x4_t T = Z4, TT = Z4;
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) {
-              T = mfma_bf16(PTf[kb], Qf[qt][kb], T);    // rows c, cols query
-              TT = mfma_bf16(Qf[qt][kb], PTf[kb], TT);  // rows query, cols c
-            }
-            f32x4_t dV, dVT;
-            if (PAPER) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                dV[r] = ws * dzC[qt][r];
-                dVT[r] = ws * dzR[qt][r];
-                dwp += fmaxf(TT[r], 0.f) * dzR[qt][r];
-              }
-            } else {
-              dV = mfma_bf16(wt, dzA[qt], Z4);   // rows c, cols query
-              dVT = mfma_bf16(dzA[qt], wt, Z4);  // rows query, cols c
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              dTs[sl][qt][r] = T[r] > 0.f ? dV[r] : 0.f;
-              dTT[qt][r] = TT[r] > 0.f ? dVT[r] : 0.f;
-            }
-            VT[qt] = relu4(TT);
-          }
-          // per-episode dw contribution
-          if (PAPER) {
-            dwp = wave_sum(dwp);
-            if (lane == 0 && sok) dw_slab[(long)ep * h + s] = dwp;
-          } else {
-            f32x4_t dw = Z4;
-#pragma unroll
-            for (int kq = 0; kq < KQ; ++kq) dw = mfma_bf16(pack2(VT[2 * kq], VT[2 * kq + 1]), dzB[kq], dw);
-            float* const dst = dwl + (((p & 1) * NTN_WAVES + wave) * 2 + sl) * NN1;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dst[(4 * q + r < N && n < N) ? (4 * q + r) * N + n : N * N] = dw[r];
-          }
-          // dP^T[b, c] = sum_q Q[q, b] dT[c, q]
-          f32x4_t dPT[2 * NKB];
-#pragma unroll
-          for (int mb = 0; mb < 2 * NKB; ++mb) {
-            dPT[mb] = Z4;
-            if (mb < MTH) {
-#pragma unroll
-              for (int kq = 0; kq < KQ; ++kq)
-                dPT[mb] = mfma_bf16(QTf[mb][kq], pack2(dTT[2 * kq], dTT[2 * kq + 1]), dPT[mb]);
-            }
-          }
-          // dC^T[a, c] += sum_b M[a, b, s] dP[c, b]
-#pragma unroll
-          for (int kb = 0; kb < NKB; ++kb) {
-            const u16x8_t dPf = pack2(dPT[2 * kb], dPT[2 * kb + 1]);
-#pragma unroll
-            for (int ma = 0; ma < MTH; ++ma)
-              dCT[ma] = mfma_bf16(buf[(F1 + (sl * MTH + ma) * NKB + kb) * 64 + lane], dPf, dCT[ma]);
-          }
-          // dP -> bf16 [E*N][h*H] for the dM reduction GEMM
-          unsigned short* const dpt = dp_out + (long)E * N * hH;
-#pragma unroll
-          for (int mb = 0; mb < MTH; ++mb)
-            *reinterpret_cast<u16x4_t*>(sok ? dpb[mb] + s * H : dpt) =
-                u16x4_t{f2bf(dPT[mb][0]), f2bf(dPT[mb][1]), f2bf(dPT[mb][2]), f2bf(dPT[mb][3])};
+          for (int r = 0; r < 4; ++r) dT[qt][r] = T[r] > 0.f ? dV[r] : 0.f;
+          // images [query row][(s, c) col]: the lane writes its query row's 4 (s, c) columns
+          const int off = vslot(16 * qt + n) * 32 + q * 8;
+          *reinterpret_cast<s16x4_t*>(vimg + off) = bf4relu(T);
+          *reinterpret_cast<s16x4_t*>(dtimg + off) = bf4(dT[qt]);
         }
-        // dQ^T[b, q] += sum_{s in pair, c} P_s[c, b] dT_s[c, q]
+        wave_order(woff);
+        pg = ntn_lds + woff + gi * PIMG;
+        vimg = ntn_lds + woff + GM * PIMG;
+        dtimg = vimg + VIMG;
+        // transposed image reads: lane (q, n) gets image[32 kq + 8 q + j][col n], j < 8
+        u16x8_t Vt[KQ], dTt[KQ];
 #pragma unroll
-        for (int nb = 0; nb < MTH; ++nb) {
-          const u16x8_t Pf = pack2(Ps[0][nb], Ps[1][nb]);
+        for (int kq = 0; kq < KQ; ++kq) {
+          const int r0 = 32 * kq + 8 * q + (n >> 2);
+          const int o0 = vslot(r0) * 32 + (n & 3) * 8, o1 = vslot(r0 + 4) * 32 + (n & 3) * 8;
+          Vt[kq] = cat8(trr(vimg + o0), trr(vimg + o1));
+          dTt[kq] = cat8(trr(dtimg + o0), trr(dtimg + o1));
+        }
+        // dw[(s, c)][c'] += sum_q V[(s, c), q] dz[q, c']
 #pragma unroll
-          for (int qt = 0; qt < QT; ++qt) dQT[nb][qt] = mfma_bf16(Pf, pack2(dTs[0][qt], dTs[1][qt]), dQT[nb][qt]);
+        for (int kq = 0; kq < KQ; ++kq) dw = mfma_bf16(Vt[kq], dzB[gi][kq], dw);
+        // dQ^T[b][q] += sum_(s,c) P^T[b, (s,c)] dT^T[(s,c), q]   (A: the P image read transposed)
+#pragma unroll
+        for (int mb = 0; mb < MTH; ++mb) {
+          const int pr = 4 * q + (n >> 2);
+          const s16x4_t Pt = trr(pg + pr * IMG_ROW + (((4 * mb + (n & 3)) ^ mask_p(pr)) << 3));
+#pragma unroll
+          for (int qt = 0; qt < QT; ++qt) dQ[gi][mb][qt] = mfma16_bf16(Pt, bf4(dT[qt]), dQ[gi][mb][qt]);
+        }
+        // dP^T[b][(s, c)] = sum_q Q^T[b, q] dT[q, (s, c)]
+        f32x4_t dPT[MTH];
+#pragma unroll
+        for (int mb = 0; mb < MTH; ++mb) {
+          dPT[mb] = Z4;
+#pragma unroll
+          for (int kq = 0; kq < KQ; ++kq) dPT[mb] = mfma_bf16(QB[gi][mb][kq], dTt[kq], dPT[mb]);
+        }
+        // dP -> global bf16 [(e, c)][s H + b] (lanes outside the valid ranges store into the trash tail)
+        {
+          const int s = t * g.SG + dsl;
+          const bool okc = n < SGN && s < k.h && ep < k.E;
+          unsigned short* const drow = dp + ((long)(okc ? ep : 0) * g.N + dcl) * hH + (long)(okc ? s : 0) * g.H;
+#pragma unroll
+          for (int mb = 0; mb < MTH; ++mb) {
+            const int b0 = 16 * mb + 4 * q;
+            unsigned short* dst = (okc && b0 < g.H) ? drow + b0 : dp_trash;
+            *reinterpret_cast<s16x4_t*>(dst) = bf4(dPT[mb]);
+          }
+        }
+        wave_order(woff);   // this episode's P image reads are done: it becomes the dP image D[(s,c)][b]
+        pg = ntn_lds + woff + gi * PIMG;
+#pragma unroll
+        for (int mb = 0; mb < MTH; ++mb)
+          *reinterpret_cast<s16x4_t*>(pg + n * IMG_ROW + (((4 * mb + q) ^ mask_p(n)) << 3)) = bf4(dPT[mb]);
+        wave_order(woff);   // (the next episode's V / dT image writes come after this one's reads)
+      }
+      wave_order(woff);
+      const unsigned char* const pimg = ntn_lds + woff;
+      // dC^T[a][(g, c)] += sum_b M_s[a, b] D_s[b, (g, c)], stacked over the wave's episodes
+      for (int sl = 0; sl < g.SG; ++sl) {
+        const unsigned char* mimg = buf + sl * (RA * IMG_ROW);
+        const int row = sl * g.N + g.lc;
+        u16x8_t Bd[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+          Bd[kb] = *reinterpret_cast<const u16x8_t*>(
+              g.lrow ? pimg + g.lg * PIMG + row * IMG_ROW + (((8 * kb + 2 * q) ^ mask_p(row)) << 3) : zero);
+#pragma unroll
+        for (int ma = 0; ma < MTH; ++ma) {
+          const int a = 16 * ma + n;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) {
+            const u16x8_t Ma =
+                *reinterpret_cast<const u16x8_t*>(mimg + a * IMG_ROW + (((8 * kb + 2 * q) ^ mask_m(a)) << 3));
+            dC[ma] = mfma_bf16(Ma, Bd[kb], dC[ma]);
+          }
         }
       }
-#endif
+      {   // this wave's dw tile -> its exchange slot (summed over the workgroup's waves after the barrier)
+        float* slot = dwl + par * NW * DW_SLOT + wave * DW_SLOT;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) slot[(4 * q + r) * 16 + n] = dw[r];
+      }
       stage_wait();
       __syncthreads();
     }
-    if (p1 > p0) flush_dw(p1 - 1);   // read before the next group's first barrier pair
-    if (act) {
-      const bool split = gridDim.y > 1;
-      float* dc_out = split ? pc + (long)blockIdx.y * E * N * H : dcls;
-#pragma unroll
-      for (int ma = 0; ma < MTH; ++ma) {
-        const int a0 = 16 * ma + 4 * q;
-        if (n < N && a0 < H) *reinterpret_cast<f32x4_t*>(dc_out + ((long)ep * N + n) * H + a0) = dCT[ma];
+    if (t1 > t0 && (int)threadIdx.x < dwe) {   // flush the last tile's dw
+      const float* src = dwl + ((t1 - 1 - t0) & 1) * NW * DW_SLOT;
+      float acc = 0.f;
+      if (k.paper) {
+        for (int w = 0; w < NW; ++w)
+          for (int c = 0; c < g.N; ++c) acc += src[w * DW_SLOT + (threadIdx.x * g.N + c) * 16 + c];
+      } else {
+        const int row = threadIdx.x / g.N, cp = threadIdx.x - row * g.N;
+        for (int w = 0; w < NW; ++w) acc += src[w * DW_SLOT + row * 16 + cp];
       }
-      // query-row gradients: straight into de, or this split's compact [E][NQ][H] partial
-      float* dq_base = split ? pq + ((long)blockIdx.y * E + ep) * NQ * H : de + rq0 * H;
+      k.dw_slab[((long)grp * k.ntile + t1 - 1) * dwe + threadIdx.x] = acc;
+    }
+    // dC^T: rows a, col (g, c)
+    {
+      const int ep = epw + g.lg;
+      if (g.lrow && ep < k.E) {
+        float* dc_out = split ? k.part + (long)blockIdx.y * k.E * g.N * g.H : k.dcls;
 #pragma unroll
-      for (int nb = 0; nb < MTH; ++nb)
+        for (int ma = 0; ma < MTH; ++ma) {
+          const int a0 = 16 * ma + 4 * q;
+          if (a0 < g.H) *reinterpret_cast<f32x4_t*>(dc_out + ((long)ep * g.N + g.lc) * g.H + a0) = dC[ma];
+        }
+      }
+    }
+    // dQ^T: rows b, cols query -> the query rows of de (or this split's [E][NQ][H] partial)
+#pragma unroll
+    for (int gi = 0; gi < GM; ++gi) {
+      const int ep = epw + gi;
+      if (gi >= g.G || ep >= k.E) continue;
+      const long rq0 = (long)ep * (g.N * k.K + g.NQ) + g.N * k.K;
+      float* dq_base = split ? k.part2 + ((long)blockIdx.y * k.E + ep) * g.NQ * g.H : k.de + rq0 * g.H;
+#pragma unroll
+      for (int mb = 0; mb < MTH; ++mb)
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
-          const int b0 = 16 * nb + 4 * q, qi = 16 * qt + n;
-          if (qi < NQ && b0 < H) *reinterpret_cast<f32x4_t*>(dq_base + (long)qi * H + b0) = dQT[nb][qt];
+          const int b0 = 16 * mb + 4 * q, qi = 16 * qt + n;
+          if (qi < g.NQ && b0 < g.H) *reinterpret_cast<f32x4_t*>(dq_base + (long)qi * g.H + b0) = dQ[gi][mb][qt];
         }
     }
+    // (the next group's first barrier orders these dw-slot reads before its writes)
   }
 }
 
-// sums of the slice-split partials, in split order (deterministic)
+// sums of the split partials, in split order (deterministic)
 __global__ __launch_bounds__(256) void ntn_fwd_finish_kernel(const float* __restrict__ part, int ny, long n, int N,
                                                              int paper, const float* __restrict__ bias,
                                                              float* __restrict__ probs) {
@@ -710,102 +543,95 @@ __global__ __launch_bounds__(256) void ntn_bwd_finish_kernel(const float* __rest
   }
 }
 
-// ------------------------------------------------------------------------------------------
-namespace ina {
-
-static int finish_grid(long n) {
+int finish_grid(long n) {
   const long g = (n + 255) / 256;
   return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
 }
 
-static size_t ntn_lds_bytes(int MTH, bool paper, bool bwd, int N = 0) {
-  const int NKA = (MTH + 1) / 2;
-  const int fr = bwd ? (4 * MTH * NKA + (paper ? 0 : 2)) : (2 * MTH * NKA + (paper ? 0 : 1));
-  // + the reference-head backward's dw slots [2 parities][waves][2 slices][N*N + 1] fp32
-  const size_t dwl = (bwd && !paper) ? (size_t)2 * NTN_WAVES * 2 * (N * N + 1) * 4 : 0;
-  // + (TR) the wave-private transpose images, 16-byte aligned after the dw slots
-  const int KQ = 2;   // upper bound over the instantiated QT (<= 4)
-  const size_t img = (bwd && INA_NTN_TR) ? 16 + (size_t)NTN_WAVES * (32 * (16 * MTH + 4) + 2 * 32 * KQ * 20) * 2 : 0;
-  return (size_t)2 * fr * 64 * 16 + dwl + img;
+int qt_of(int N, int Q) {
+  const int need = (N * Q + 15) / 16;
+  return need <= 1 ? 1 : (need <= 2 ? 2 : (need <= 4 ? 4 : 0));
 }
 
-int ntn_groups(int E) { return (E + NTN_WAVES - 1) / NTN_WAVES; }
-
-template <int MTH, int QT, bool P>
-static int ntn_fwd_t(const NtnArgs& a, hipStream_t st) {
-  const int groups = (a.E + NTN_WAVES - 1) / NTN_WAVES;
-  const int blocks = groups < a.blocks ? groups : a.blocks;
-  const int ny = a.split > 1 ? a.split : 1;
-  hipLaunchKernelGGL((ntn_fwd_kernel<MTH, QT, P>), dim3(blocks, ny), dim3(NTN_THREADS), ntn_lds_bytes(MTH, P, false),
-                     st, a.cls, a.e, a.E, a.N, a.K, a.Q, a.H, a.h, (const u16x8_t*)a.mpack, (const u16x8_t*)a.wpack,
-                     a.wvec, a.bias, a.probs, a.part);
-  if (ny > 1) {
-    const long n = (long)a.E * a.N * a.Q * a.N;
-    hipLaunchKernelGGL(ntn_fwd_finish_kernel, dim3(finish_grid(n)), dim3(256), 0, st, a.part, ny, n, a.N, a.paper,
-                       a.bias, a.probs);
-  }
-  INA_CHECK_LAUNCH();
-  return 0;
+size_t lds_bytes(const NtnArgs& a, int QT, bool bwd) {
+  const int GM = QT <= 2 ? 2 : 1;
+  const size_t per_wave = (size_t)GM * PIMG + (bwd ? 2 * ((QT + 1) / 2) * 32 * 32 : 0);
+  return (size_t)2 * a.tpb + ZERO_BYTES + NW * per_wave + (bwd ? (size_t)2 * NW * DW_SLOT * 4 : 0);
 }
-template <int MTH, int QT, bool P>
-static int ntn_bwd_t(const NtnArgs& a, hipStream_t st) {
-  const int groups = (a.E + NTN_WAVES - 1) / NTN_WAVES;
+
+template <int MTH, int QT, bool BWD>
+int launch(const NtnArgs& a, hipStream_t st) {
+  const int groups = ina::ntn_groups(a.E, a.N, a.Q);
   const int blocks = groups < a.blocks ? groups : a.blocks;
   const int ny = a.split > 1 ? a.split : 1;
-  const size_t lds = ntn_lds_bytes(MTH, P, true, a.N);
-  if (lds > 64 * 1024 &&
-      hipFuncSetAttribute((const void*)ntn_bwd_kernel<MTH, QT, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-          hipSuccess)
+  const size_t lds = lds_bytes(a, QT, BWD);
+  const void* fn = BWD ? (const void*)ntn_bwd_kernel<MTH, QT> : (const void*)ntn_fwd_kernel<MTH, QT>;
+  if (lds > 64 * 1024 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -1;
-  hipLaunchKernelGGL((ntn_bwd_kernel<MTH, QT, P>), dim3(blocks, ny), dim3(NTN_THREADS), lds,
-                     st, a.cls, a.e, a.E, a.N, a.K, a.Q, a.H, a.h, (const u16x8_t*)a.mpack, (const u16x8_t*)a.m2pack,
-                     (const u16x8_t*)a.wtpack, a.wvec, a.dz, a.dcls, a.de, (unsigned short*)a.dp_out, a.dw_slab,
-                     a.gscale, (unsigned short*)a.cls_bf, a.part, a.part2);
+  if (BWD) {
+    hipLaunchKernelGGL((ntn_bwd_kernel<MTH, QT>), dim3(blocks, ny), dim3(NT_THREADS), lds, st, a);
+  } else {
+    hipLaunchKernelGGL((ntn_fwd_kernel<MTH, QT>), dim3(blocks, ny), dim3(NT_THREADS), lds, st, a);
+  }
   if (ny > 1) {
-    const long n = (long)a.E * a.N * a.H * (1 + a.Q);
-    hipLaunchKernelGGL(ntn_bwd_finish_kernel, dim3(finish_grid(n)), dim3(256), 0, st, a.part, a.part2, ny, a.E, a.N,
-                       a.K, a.Q, a.H, a.dcls, a.de);
+    if (BWD) {
+      const long n = (long)a.E * a.N * a.H * (1 + a.Q);
+      hipLaunchKernelGGL(ntn_bwd_finish_kernel, dim3(finish_grid(n)), dim3(256), 0, st, a.part, a.part2, ny, a.E, a.N,
+                         a.K, a.Q, a.H, a.dcls, a.de);
+    } else {
+      const long n = (long)a.E * a.N * a.Q * a.N;
+      hipLaunchKernelGGL(ntn_fwd_finish_kernel, dim3(finish_grid(n)), dim3(256), 0, st, a.part, ny, n, a.N, a.paper,
+                         a.bias, a.probs);
+    }
   }
   INA_CHECK_LAUNCH();
   return 0;
 }
 
-#define INA_NTN_QT(FN, MTH, P)                       \
-  if (QT == 1) return FN<MTH, 1, P>(a, st);          \
-  if (QT == 2) return FN<MTH, 2, P>(a, st);          \
-  if (QT == 4) return FN<MTH, 4, P>(a, st);
-#define INA_NTN_DISPATCH(FN)                                              \
-  const int QT = qt_needed <= 1 ? 1 : (qt_needed <= 2 ? 2 : (qt_needed <= 4 ? 4 : 0)); \
-  if (QT == 0) return -1;                                                 \
-  if (a.paper) {                                                          \
-    if (MTH == 1) { INA_NTN_QT(FN, 1, true) }                             \
-    if (MTH == 3) { INA_NTN_QT(FN, 3, true) }                             \
-    if (MTH == 4) { INA_NTN_QT(FN, 4, true) }                             \
-  } else {                                                                \
-    if (MTH == 1) { INA_NTN_QT(FN, 1, false) }                            \
-    if (MTH == 3) { INA_NTN_QT(FN, 3, false) }                            \
-    if (MTH == 4) { INA_NTN_QT(FN, 4, false) }                            \
-  }                                                                       \
+template <bool BWD>
+int dispatch(const NtnArgs& a, hipStream_t st) {
+  const int MTH = (a.H + 15) / 16, QT = qt_of(a.N, a.Q);
+  if (a.N < 1 || a.N > 16 || QT == 0 || a.H % 8 != 0 || a.H > 64) return -1;
+  if (a.SG != ina::ntn_slices_per_tile(a.N) || a.G != ina::ntn_episodes_per_wave(a.N, a.Q)) return -1;
+  if (lds_bytes(a, QT, BWD) > 160 * 1024) return -1;
+#define INA_NTN_QT(M)                                  \
+  if (QT == 1) return launch<M, 1, BWD>(a, st);        \
+  if (QT == 2) return launch<M, 2, BWD>(a, st);        \
+  if (QT == 4) return launch<M, 4, BWD>(a, st);
+  if (MTH == 1) { INA_NTN_QT(1) }
+  if (MTH == 3) { INA_NTN_QT(3) }
+  if (MTH == 4) { INA_NTN_QT(4) }
+#undef INA_NTN_QT
   return -1;
+}
 
-// slice-split factor for small episode batches: fill ~256 workgroups, >= 2 slice pairs per split
-int ntn_split(int E, int h) {
-  const int groups = (E + NTN_WAVES - 1) / NTN_WAVES, npair = (h + 1) / 2;
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+namespace ina {
+
+int ntn_slices_per_tile(int N) {
+  const int s = 16 / (N > 0 ? N : 1);
+  return s < 4 ? (s > 0 ? s : 1) : 4;
+}
+int ntn_episodes_per_wave(int N, int Q) {
+  const int gm = qt_of(N, Q) <= 2 ? 2 : 1;
+  const int s = 16 / (N > 0 ? N : 1);
+  return s < gm ? (s > 0 ? s : 1) : gm;
+}
+int ntn_groups(int E, int N, int Q) {
+  const int per = NW * ntn_episodes_per_wave(N, Q);
+  return (E + per - 1) / per;
+}
+// tile-split factor for small episode batches: fill ~256 workgroups, >= 2 tiles per split
+int ntn_split(int E, int N, int Q, int h) {
+  const int groups = ntn_groups(E, N, Q), ntile = (h + ntn_slices_per_tile(N) - 1) / ntn_slices_per_tile(N);
   if (groups >= 64) return 1;
   int ny = 256 / groups;
-  if (ny > npair / 2) ny = npair / 2;
+  if (ny > ntile / 2) ny = ntile / 2;
   return ny > 1 ? ny : 1;
 }
-
-int ntn_fwd(const NtnArgs& a, hipStream_t st) {
-  const int MTH = (a.H + 15) / 16, qt_needed = (a.N * a.Q + 15) / 16;
-  if (a.N > 16) return -1;
-  INA_NTN_DISPATCH(ntn_fwd_t)
-}
-int ntn_bwd(const NtnArgs& a, hipStream_t st) {
-  const int MTH = (a.H + 15) / 16, qt_needed = (a.N * a.Q + 15) / 16;
-  if (a.N > 16) return -1;
-  INA_NTN_DISPATCH(ntn_bwd_t)
-}
+int ntn_fwd(const NtnArgs& a, hipStream_t st) { return dispatch<false>(a, st); }
+int ntn_bwd(const NtnArgs& a, hipStream_t st) { return dispatch<true>(a, st); }
 
 }  // namespace ina

@@ -100,6 +100,7 @@ class Config:
     model_dir: str = "checkpoints/inductionNetwork_test"
     ckpt_name: str = "inductionNetwork"
     max_to_keep: int = 5
+    tf_checkpoint: bool = True         # also write the TF V2 bundle (.index / .data) + .meta next to safetensors
     resume: bool = True
 
     # ---------------- execution ----------------

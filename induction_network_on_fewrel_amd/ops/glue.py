@@ -26,7 +26,7 @@ import numpy as np
 import torch
 
 from ._ext import ops
-from .packing import _attn_fuse_idx, _attn_idx, _attn_rec_idx, _lstm_idx, _ntn_m_idx, _ntn_w_idx, lstm_shape
+from .packing import _attn_fuse_idx, _attn_idx, _attn_rec_idx, _lstm_idx, _ntn_dw_idx, _ntn_tile_idx, lstm_shape
 
 
 class StepGlue:
@@ -58,10 +58,10 @@ class StepGlue:
     # ------------------------------------------------------------------ packs
     def packs(self, p: Dict[str, torch.Tensor], U: int, DIN: int, bf16: bool, head: Optional[tuple]):
         """All per-step weight packs in one launch.  head = (H, h, N, paper) or None.
-        Returns dict(apack, a2pack, bias2, w1pack, w1tpack[, mpack, m2pack, wpack, wtpack])."""
+        Returns dict(apack, a2pack, bias2, w1pack, w1tpack[, ntn_tiles])."""
         names = ["lstm_fw_kernel", "lstm_bw_kernel", "lstm_fw_bias", "lstm_bw_bias", "attn_kernel"]
         if head is not None:
-            names += ["M"] + ([] if head[3] else ["ntn_w"])
+            names += ["M", "ntn_w"]
         offs = tuple(self.off(p[n]) for n in names)
         key = (U, DIN, bf16, head, offs)
         ent = self._idx.get(key)
@@ -119,15 +119,8 @@ class StepGlue:
             put("w1ftpack", np.where(fti < Z, off["attn_kernel"] + fti, -1), True)
         if head is not None:
             H, h, N, paper = head
-            mi, m2i = (t.numpy() for t in _ntn_m_idx(H, h))
-            ZM = H * H * h
-            put("mpack", np.where(mi < ZM, off["M"] + mi, -1), True)
-            put("m2pack", np.where(m2i < ZM, off["M"] + m2i, -1), True)
-            if not paper:
-                wi, wti = (t.numpy() for t in _ntn_w_idx(h, N))
-                ZW = h * N * N
-                put("wpack", np.where(wi < ZW, off["ntn_w"] + wi, -1), True)
-                put("wtpack", np.where(wti < ZW, off["ntn_w"] + wti, -1), True)
+            mi, wi = (t.numpy() for t in _ntn_tile_idx(H, h, N, bool(paper)))
+            put("ntn_tiles", np.where(mi >= 0, off["M"] + mi, np.where(wi >= 0, off["ntn_w"] + wi, -1)), True)
         allidx = np.concatenate(parts_b + parts_f) if (parts_b or parts_f) else np.zeros(0)
         return self._dev_i32(allidx), layout, nb, nf
 
@@ -203,6 +196,16 @@ class StepGlue:
         if m is None:
             a, s, b = np.meshgrid(np.arange(H), np.arange(h), np.arange(H), indexing="ij")
             m = self._dev_i32(self.off(Mt) + (a * H + b) * h + s)
+            self._maps[key] = m
+        return m
+
+    def map_ntn_dw(self, w: torch.Tensor, h: int, N: int, paper: bool) -> torch.Tensor:
+        """ntn_bwd dw slab row ([ntile][SG N][N] / [ntile][SG], ops/packing.py::_ntn_dw_idx) -> ntn_w."""
+        key = ("ntn_dw", self.off(w), h, N, bool(paper))
+        m = self._maps.get(key)
+        if m is None:
+            di = _ntn_dw_idx(h, N, bool(paper)).numpy()
+            m = self._dev_i32(np.where(di >= 0, self.off(w) + di, -1))
             self._maps[key] = m
         return m
 

@@ -1,7 +1,7 @@
 """Induction + relation head on the GPU path: dynamic routing -> neural tensor layer -> sigmoid.
 
-forward:  routing_fwd (one wave / episode) -> ntn_fwd (one wave / episode, chained bf16 MFMAs)
-backward: ntn_bwd (dC, dQ, per-episode dw, dP) -> dM = C^T dP (library GEMM over E*N)
+forward:  routing_fwd -> ntn_fwd (slice tiles x stacked episodes, bf16 MFMA; csrc/kernels/ntn.hip)
+backward: ntn_bwd (dC, dQ, dw slab, dP) -> dM = C^T dP (reduction GEMM over the E*N class rows)
           -> routing_bwd (exact reverse through all routing iterations, dW_s slab)
 The gradient wrt the sentence embeddings is written by ntn_bwd (query rows) and routing_bwd
 (support rows) into ONE buffer -- no zero-fill and no add of two sparse gradients.
@@ -14,7 +14,7 @@ import torch
 
 from ._ext import ops
 from .encoder import _route_grad
-from .packing import pack_ntn_M, pack_ntn_w
+from .packing import _ntn_dw_idx, _on, pack_ntn_tiles
 
 
 class HeadFn(torch.autograd.Function):
@@ -28,36 +28,34 @@ class HeadFn(torch.autograd.Function):
         e = e.contiguous()
         Wsd = Ws.detach().contiguous()
         cls = o.routing_fwd(e, Wsd, E, N, K, Q, R, 0)
-        mpack, m2pack = pack_ntn_M(M)
-        if paper:
-            wpack = wtpack = torch.empty(0, dtype=torch.bfloat16, device=e.device)
-            wvec = w.detach().reshape(-1).float().contiguous()
-        else:
-            wpack, wtpack = pack_ntn_w(w, h, N)
-            wvec = torch.empty(0, dtype=torch.float32, device=e.device)
-        probs = o.ntn_fwd(cls, e, mpack, wpack, wvec, b.detach().float().contiguous(), E, N, K, Q, h, paper, 0)
-        ctx.save_for_backward(e, Wsd, cls, mpack, m2pack, wtpack, wvec, probs)
+        tiles = pack_ntn_tiles(M, w, N, paper)
+        probs = o.ntn_fwd(cls, e, tiles, b.detach().float().contiguous(), E, N, K, Q, h, paper, 0)
+        ctx.save_for_backward(e, Wsd, cls, tiles, probs)
         ctx.meta = dict(meta, H=H, h=h)
         return probs
 
     @staticmethod
     def backward(ctx, dprobs):
         o = ops()
-        e, Ws, cls, mpack, m2pack, wtpack, wvec, probs = ctx.saved_tensors
+        e, Ws, cls, tiles, probs = ctx.saved_tensors
         m = ctx.meta
         E, N, K, Q, R, H, h = m["E"], m["N"], m["K"], m["Q"], m["iters"], m["H"], m["h"]
         paper = bool(m["paper"])
         dz = (dprobs * probs * (1.0 - probs)).float().contiguous()
         de = torch.empty_like(e)
-        dcls, dp, dw_slab = o.ntn_bwd(cls, e, mpack, m2pack, wtpack, wvec, dz, de, E, N, K, Q, h, paper, 0, None, None)
-        # dM[a][b][s] = sum_{(e,c)} C[(e,c)][a] dP[(e,c)][s*H + b]
-        dMf = torch.matmul(cls.reshape(E * N, H).t().to(torch.bfloat16), dp).float()   # [H, h*H]
+        dcls, dp, dw_slab, cls_bf = o.ntn_bwd(cls, e, tiles, dz, de, E, N, K, Q, h, paper, 0, None)
+        # dM[a][b][s] = sum_{(e,c)} C[(e,c)][a] dP[(e,c)][s*H + b]   (gemm_tn.hip, split slabs)
+        dMf = o.gemm_tn_slab(cls_bf, dp, H, 0).sum(0)   # [H, h*H]
         dM = dMf.view(H, h, H).permute(0, 2, 1).contiguous()
+        di = _on(_ntn_dw_idx(h, N, paper), e.device)
+        ok = di >= 0
+        dw = torch.zeros(h if paper else h * N * N, dtype=torch.float32, device=e.device)
+        dw.index_add_(0, di[ok], dw_slab.sum(0)[ok])
         if paper:
-            dw = dw_slab.sum(0).view(h, 1)
+            dw = dw.view(h, 1)
             db = dz.sum().view(1)
         else:
-            dw = dw_slab.sum(0).reshape(h * N, N)
+            dw = dw.view(h * N, N)
             db = dz.sum((0, 1))
         slab = o.routing_bwd(e, Ws, dcls, de, E, N, K, Q, R, 0)
         dWs = slab.sum(0)
@@ -75,8 +73,8 @@ class HeadLossFn(torch.autograd.Function):
     forward:  routing_fwd -> ntn_fwd -> ina.head_loss (loss, accuracy, dz = dL/dlogit and its row
               sum = the NTN bias gradient, all in one launch; reference model/graph.py:88-95)
     backward: ntn_bwd scales dz by the upstream loss gradient on the device and also emits the bf16
-              copy of the class vectors for the dM GEMM (fp32 output); every parameter gradient is
-              queued on the StepGlue for the step's single slab_scatter_add.
+              class vectors and dP for the dM reduction GEMM (gemm_tn.hip, fp32 split slabs); every
+              parameter gradient is queued on the StepGlue for the step's single slab_scatter_add.
     Returns (loss, accuracy, probs); accuracy and probs are not differentiable."""
 
     @staticmethod
@@ -89,14 +87,8 @@ class HeadLossFn(torch.autograd.Function):
         e = e.contiguous()
         Wsd = Ws.detach().contiguous()
         cls = o.routing_fwd(e, Wsd, E, N, K, Q, R, 0)
-        mpack, m2pack = pk["mpack"], pk["m2pack"]
-        if paper:
-            wpack = wtpack = torch.empty(0, dtype=torch.bfloat16, device=e.device)
-            wvec = w.detach().reshape(-1).float().contiguous()
-        else:
-            wpack, wtpack = pk["wpack"], pk["wtpack"]
-            wvec = torch.empty(0, dtype=torch.float32, device=e.device)
-        probs = o.ntn_fwd(cls, e, mpack, wpack, wvec, b.detach().float().contiguous(), E, N, K, Q, h, paper, 0)
+        tiles = pk["ntn_tiles"]
+        probs = o.ntn_fwd(cls, e, tiles, b.detach().float().contiguous(), E, N, K, Q, h, paper, 0)
         rows = E * N * Q
         ce = meta.get("loss_type", "mse") == "ce"
         if meta.get("reduction", "mean") == "mean":
@@ -106,7 +98,7 @@ class HeadLossFn(torch.autograd.Function):
         dz = torch.empty_like(probs)
         out = torch.empty(N + 3, dtype=torch.float32, device=e.device)
         o.head_loss(probs, labels.reshape(-1), scale, dz, out, glue.loss_part, _loss_blocks(glue, rows), ce)
-        ctx.save_for_backward(e, Wsd, cls, mpack, m2pack, wtpack, wvec, dz, out)
+        ctx.save_for_backward(e, Wsd, cls, tiles, dz, out)
         ctx.meta = dict(meta, H=H, h=h)
         ctx.set_materialize_grads(False)   # no zero-fill launches for the non-differentiable outputs
         loss, acc = out[0], out[1]
@@ -116,23 +108,20 @@ class HeadLossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gloss, _gacc, _gprobs):
         o = ops()
-        e, Ws, cls, mpack, m2pack, wtpack, wvec, dz, out = ctx.saved_tensors
+        e, Ws, cls, tiles, dz, out = ctx.saved_tensors
         m = ctx.meta
         E, N, K, Q, R, H, h = m["E"], m["N"], m["K"], m["Q"], m["iters"], m["H"], m["h"]
         paper = bool(m["paper"])
         glue, p = m["glue"], m["pdict"]
         g = gloss.reshape(1).float().contiguous()
         de = torch.empty_like(e)
-        cls_bf = torch.empty(E * N, H, dtype=torch.bfloat16, device=e.device)
-        dcls, dp, dw_slab = o.ntn_bwd(cls, e, mpack, m2pack, wtpack, wvec, dz, de, E, N, K, Q, h, paper, 0, g, cls_bf)
-        # dM = C^T dP over K = E*N rows: split-K as a batched GEMM [ns, H, h*H] (a plain [H=40] x
-        # [h*H=4000] GEMM has only ~63 output tiles -- a quarter of the CUs streaming the 82 MB dP); the
-        # ns partial slabs are summed by the glue's deterministic slab scatter-add
-        ns = _dm_splits(E * N)
-        dMf = torch.bmm(cls_bf.view(ns, -1, H).transpose(1, 2), dp.view(ns, -1, dp.shape[1]),
-                        out_dtype=torch.float32)                          # [ns, H, h*H] (col s*H + b)
+        dcls, dp, dw_slab, cls_bf = o.ntn_bwd(cls, e, tiles, dz, de, E, N, K, Q, h, paper, 0, g)
+        # dM = C^T dP over the E*N class rows: the split-K reduction GEMM of gemm_tn.hip -> slabs [ns, H, h*H]
+        # (col s*H + b), summed by the glue's deterministic slab scatter-add
+        dMf = o.gemm_tn_slab(cls_bf, dp, H, 0)
+        ns = dMf.shape[0]
         slab = o.routing_bwd(e, Ws, dcls, de, E, N, K, Q, R, 0)
-        glue.add(dw_slab, glue.map_identity(p["ntn_w"]), dw_slab.shape[0])
+        glue.add(dw_slab, glue.map_ntn_dw(p["ntn_w"], h, N, paper), dw_slab.shape[0])
         glue.add(out[2 + N:3 + N] if paper else out[2:2 + N], glue.map_identity(p["ntn_b"]), 1, scale=g)
         glue.add(slab, glue.map_identity(p["W_s"]), slab.shape[0])
         glue.add(dMf, glue.map_ntn_M(p["M"]), ns)
@@ -141,14 +130,6 @@ class HeadLossFn(torch.autograd.Function):
             glue.flush()
             ov.ready(0)
         return de, None, None, None, None, None, None
-
-
-def _dm_splits(rows: int) -> int:
-    """Split-K factor of the dM GEMM: >= 1024 (episode, class) rows per split, dividing ``rows``."""
-    for ns in (8, 4, 2):
-        if rows % ns == 0 and rows // ns >= 1024:
-            return ns
-    return 1
 
 
 def _loss_blocks(glue, rows: int) -> int:

@@ -251,71 +251,78 @@ def pack_attn_fuse(W1: torch.Tensor):
 
 
 # ------------------------------------------------------------------ NTN (bf16 only)
-def _kmap32(q: int, j: int) -> int:
-    return 16 * (j >> 2) + 4 * q + (j & 3)
+def ntn_slices_per_tile(N: int) -> int:
+    """Slices per NTN tile: the rows (slice, class) of a tile fill one 16-row MFMA operand (csrc/kernels/ntn.hip)."""
+    return max(1, min(4, 16 // max(1, N)))
 
 
-@lru_cache(maxsize=None)
-def _ntn_m_idx(H: int, h: int):
-    """Packed M fragments for h_pad = 2*ceil(h/2) slices (the pad slice is zero): the NTN kernels
-    stage whole slice pairs with global_load_lds and need no per-lane bounds checks."""
+def ntn_tile_geometry(H: int, h: int, N: int):
+    """-> (MTH, SG, ntile, tile elements (bf16)).  A tile = SG swizzled M images [16 MTH rows a][64 cols b]
+    + the 16x16x16 FC fragments W [(s,c)][c'] and Wt [c'][(s,c)] (256 elements each)."""
     MTH = (H + 15) // 16
-    NKA = (MTH + 1) // 2
-    Z = H * H * h
-    hp = 2 * ((h + 1) // 2)
-    mp = np.full((hp, MTH, NKA, 64, 8), Z, dtype=np.int64)
-    m2 = np.full((hp, MTH, NKA, 64, 8), Z, dtype=np.int64)
-    ls = np.arange(64)
-    js = np.arange(8)
-    for s in range(h):
-        for mb in range(MTH):
-            for ka in range(NKA):
-                a = 32 * ka + 8 * (ls[:, None] >> 4) + js[None, :]
-                b = 16 * mb + (ls[:, None] & 15) + 0 * js[None, :]
-                ok = (a < H) & (b < H)
-                mp[s, mb, ka] = np.where(ok, (a * H + b) * h + s, Z)
-                a2 = 16 * mb + (ls[:, None] & 15) + 0 * js[None, :]
-                b2 = 32 * ka + 16 * (js[None, :] >> 2) + 4 * (ls[:, None] >> 4) + (js[None, :] & 3)
-                ok2 = (a2 < H) & (b2 < H)
-                m2[s, mb, ka] = np.where(ok2, (a2 * H + b2) * h + s, Z)
-    return torch.from_numpy(mp), torch.from_numpy(m2)
+    SG = ntn_slices_per_tile(N)
+    ntile = (h + SG - 1) // SG
+    return MTH, SG, ntile, SG * MTH * 16 * 64 + 512
 
 
 @lru_cache(maxsize=None)
-def _ntn_w_idx(h: int, N: int):
-    Z = h * N * N
-    npair = (h + 1) // 2
-    wp = np.empty((npair, 64, 8), dtype=np.int64)
-    wt = np.full((2 * npair, 64, 8), Z, dtype=np.int64)
-    for p in range(npair):
-        for l in range(64):
-            for j in range(8):
-                s = 2 * p + (j >> 2)
-                c = 4 * (l >> 4) + (j & 3)
-                cp = l & 15
-                wp[p, l, j] = (s * N + c) * N + cp if (s < h and c < N and cp < N) else Z
-    for s in range(h):
-        for l in range(64):
-            for j in range(8):
-                c = l & 15
-                cp = 8 * (l >> 4) + j
-                wt[s, l, j] = (s * N + c) * N + cp if (c < N and cp < N) else Z
-    return torch.from_numpy(wp), torch.from_numpy(wt)
+def _ntn_tile_idx(H: int, h: int, N: int, paper: bool):
+    """Index tables of the per-step NTN tile pack (csrc/kernels/ntn.hip), element by element:
+      mi  [ntile, TE]: (a * H + b) * h + s into M [H, H, h] (-1: zero)
+      wi  [ntile, TE]: index into w ([h N, N] reference head, [h, 1] paper head) (-1: zero)
+    M image of slice sl: element (a, b) at sl * RA * 64 + a * 64 + 4 (chunk ^ ((a & 2) << 1 | (a & 8))) + (b & 3),
+    chunk = b >> 2 (8-byte chunks XOR-swizzled by row: conflict-free row and transposed fragment reads).
+    W fragment (A[i = (s,c)][k = c'], lane l holds row l & 15, k = 4 (l >> 4) + j) and Wt fragment
+    (A[i = c'][k = (s,c)]): row (s_loc, c) = divmod(r, N) of the tile; reference head w[(s N + c)][c'],
+    paper head w[s] where c == c'."""
+    MTH, SG, NT, TE = ntn_tile_geometry(H, h, N)
+    RA = 16 * MTH
+    mi = np.full((NT, TE), -1, dtype=np.int64)
+    wi = np.full((NT, TE), -1, dtype=np.int64)
+    t, sl, a, b = np.meshgrid(np.arange(NT), np.arange(SG), np.arange(RA), np.arange(64), indexing="ij")
+    s = t * SG + sl
+    phys = (((b >> 2) ^ (((a & 2) << 1) | (a & 8))) << 2) | (b & 3)
+    pos = sl * RA * 64 + a * 64 + phys
+    ok = (s < h) & (a < H) & (b < H)
+    mi[t, pos] = np.where(ok, (a * H + b) * h + s, -1)
+    l, j = np.meshgrid(np.arange(64), np.arange(4), indexing="ij")
+    for which, (row, cp) in enumerate(((l & 15, 4 * (l >> 4) + j), (4 * (l >> 4) + j, l & 15))):
+        for tt in range(NT):
+            sl_, c = row // N, row % N
+            ss = tt * SG + sl_
+            ok = (row < SG * N) & (ss < h) & (cp < N)
+            if paper:
+                ok &= c == cp
+                idx = ss
+            else:
+                idx = (ss * N + c) * N + cp
+            wi[tt, SG * RA * 64 + 256 * which + l * 4 + j] = np.where(ok, idx, -1)
+    return torch.from_numpy(mi), torch.from_numpy(wi)
 
 
-def pack_ntn_M(M: torch.Tensor):
+def pack_ntn_tiles(M: torch.Tensor, w: torch.Tensor, N: int, paper: bool) -> torch.Tensor:
+    """M [H, H, h] and the relation FC weight w -> the NTN tile pack (bf16 [ntile, TE])."""
     H, _, h = M.shape
-    mi, m2i = _ntn_m_idx(H, h)
+    mi, wi = _ntn_tile_idx(H, h, N, bool(paper))
     dev = M.device
-    Me = torch.cat([M.detach().float().reshape(-1), M.new_zeros(1, dtype=torch.float32)])
-    return Me[_on(mi, dev)].to(torch.bfloat16).contiguous(), Me[_on(m2i, dev)].to(torch.bfloat16).contiguous()
+    nm = M.numel()
+    flat = torch.cat([M.detach().float().reshape(-1), w.detach().float().reshape(-1), M.new_zeros(1, dtype=torch.float32)])
+    mi, wi = _on(mi, dev), _on(wi, dev)
+    idx = torch.where(mi >= 0, mi, torch.where(wi >= 0, wi + nm, torch.full_like(mi, flat.numel() - 1)))
+    return flat[idx].to(torch.bfloat16).contiguous()
 
 
-def pack_ntn_w(w: torch.Tensor, h: int, N: int):
-    wi, wti = _ntn_w_idx(h, N)
-    dev = w.device
-    we = torch.cat([w.detach().float().reshape(-1), w.new_zeros(1, dtype=torch.float32)])
-    return we[_on(wi, dev)].to(torch.bfloat16).contiguous(), we[_on(wti, dev)].to(torch.bfloat16).contiguous()
+@lru_cache(maxsize=None)
+def _ntn_dw_idx(h: int, N: int, paper: bool):
+    """dw slab row of ntn_bwd ([ntile][SG N][N] reference / [ntile][SG] paper) -> index into w (-1: dropped)."""
+    SG = ntn_slices_per_tile(N)
+    NT = (h + SG - 1) // SG
+    if paper:
+        s = np.arange(NT * SG)
+        return torch.from_numpy(np.where(s < h, s, -1))
+    t, r, cp = np.meshgrid(np.arange(NT), np.arange(SG * N), np.arange(N), indexing="ij")
+    s = t * SG + r // N
+    return torch.from_numpy(np.where(s < h, (s * N + r % N) * N + cp, -1).reshape(-1))
 
 
 # ------------------------------------------------------------------ wide BiLSTM (lstm_wide.hip persistent kernels)

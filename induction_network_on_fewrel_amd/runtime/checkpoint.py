@@ -75,7 +75,7 @@ def best_stem(model_dir: str) -> Optional[str]:
 
 
 def save(model_dir: str, name: str, step: int, tensors: "OrderedDict[str, torch.Tensor]", meta: dict,
-         max_to_keep: int = 5, best: bool = False, tf_format: bool = True) -> str:
+         max_to_keep: int = 5, best: bool = False, tf_format: bool = True, meta_graph: Optional[bytes] = None) -> str:
     """Write ``<model_dir>/checkpoint/<name>-<step>`` and rotate to ``max_to_keep``.  ``best=True`` also
     points ``best_checkpoint`` at it; the best checkpoint is never rotated away (a periodic or resumed
     checkpoint can be newer, so "latest" is not "best")."""
@@ -88,6 +88,10 @@ def save(model_dir: str, name: str, step: int, tensors: "OrderedDict[str, torch.
     os.replace(tmp, os.path.join(d, stem + ".safetensors"))
     if tf_format:
         tf_bundle.save_bundle(os.path.join(d, stem), cpu)   # <stem>.index + <stem>.data-00000-of-00001
+        if meta_graph is not None:   # <stem>.meta: the serialized MetaGraphDef (runtime/tb_graph.py::meta_graph)
+            with open(os.path.join(d, stem + ".meta.tmp"), "wb") as fh:
+                fh.write(meta_graph)
+            os.replace(os.path.join(d, stem + ".meta.tmp"), os.path.join(d, stem + ".meta"))
     index = dict(meta, format=FORMAT, global_step=int(step),
                  variables={k: {"shape": list(v.shape), "dtype": str(v.dtype).replace("torch.", "")}
                             for k, v in cpu.items()})
@@ -114,7 +118,7 @@ def save(model_dir: str, name: str, step: int, tensors: "OrderedDict[str, torch.
 
 
 def _remove(d: str, stem: str) -> None:
-    for ext in (".safetensors", ".index.json", ".index", tf_bundle.DATA_SUFFIX):
+    for ext in (".safetensors", ".index.json", ".index", ".meta", tf_bundle.DATA_SUFFIX):
         try:
             os.remove(os.path.join(d, stem + ext))
         except FileNotFoundError:

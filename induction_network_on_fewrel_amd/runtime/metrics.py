@@ -29,6 +29,11 @@ for _i in range(256):
 
 
 def crc32c(data: bytes) -> int:
+    try:
+        from .. import _ina_host   # host-only native CRC32C (csrc/host/ina_host.c)
+        return _ina_host.crc32c(data)
+    except ImportError:
+        pass
     c = 0xFFFFFFFF
     for b in data:
         c = _TABLE[(c ^ b) & 0xFF] ^ (c >> 8)

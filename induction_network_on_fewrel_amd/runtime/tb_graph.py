@@ -133,6 +133,97 @@ def model_graph(model, N: int, K: int, Q: int) -> bytes:
     return graph_def(nodes)
 
 
+# ------------------------------------------------------------------ MetaGraphDef (<stem>.meta)
+def _var_def(name: str, trainable: bool) -> bytes:
+    """VariableDef{variable_name=1, initializer_name=2, snapshot_name=3, initial_value_name=6, trainable=7}."""
+    return (_ld(1, f"{name}:0".encode()) + _ld(2, f"{name}/Assign".encode()) + _ld(3, f"{name}/read:0".encode()) +
+            _ld(6, f"{name}/Initializer:0".encode()) + (_key(7, 0) + _varint(1) if trainable else b""))
+
+
+def _collection(name: str, kind: int, values: Sequence[bytes]) -> bytes:
+    """map<string, CollectionDef> entry; CollectionDef{node_list=1 | bytes_list=2 {value=1}}."""
+    inner = b"".join(_ld(1, v) for v in values)
+    return _ld(4, _ld(1, name.encode()) + _ld(2, _ld(kind, inner)))
+
+
+def meta_graph(model, N: int, K: int, Q: int, max_to_keep: int = 5) -> bytes:
+    """Serialized MetaGraphDef, as ``tf.train.Saver.save`` writes next to the bundle
+    (/root/reference/model/base.py:124,177): meta_info_def {meta_graph_version "v0", tags}, the model's
+    GraphDef plus the Saver's nodes (save/Const filename, save/SaveV2, save/control_dependency,
+    save/RestoreV2, save/Assign_i, save/restore_all), a V2 SaverDef (tensor / op names as TF1's Saver names
+    them, max_to_keep, keep_checkpoint_every_n_hours 10000) and the variables / trainable_variables /
+    train_op / global_step collections (VariableDef entries under the checkpoint's variable names).
+    Parity with TF's own bytes is unpinned (TF is not installed); tests/test_tf_bundle.py parses it back.
+
+    Fields (tensorflow/core/protobuf/meta_graph.proto, saver.proto): MetaGraphDef{meta_info_def=1,
+    graph_def=2, saver_def=3, collection_def=4}; MetaInfoDef{meta_graph_version=1, tags=4,
+    tensorflow_version=5}; SaverDef{filename_tensor_name=1, save_tensor_name=2, restore_op_name=3,
+    max_to_keep=4, sharded=5, keep_checkpoint_every_n_hours=6 (float), version=7 (V2 = 2)}."""
+    import struct
+    g = model_graph(model, N, K, Q)
+    prm = model.params
+    names = [prm.tf_name(a) for a in prm.names()]
+    trainable = {prm.tf_name(a) for a in prm.trainable()}
+    save_nodes = [node("save/Const", "Const", attrs={"dtype": _key(6, 0) + _varint(7)})]   # DT_STRING
+    save_nodes.append(node("save/SaveV2", "SaveV2", ["save/Const"] + [f"{n}" for n in names] + ["global_step"]))
+    save_nodes.append(node("save/control_dependency", "Identity", ["save/Const", "^save/SaveV2"]))
+    save_nodes.append(node("save/RestoreV2", "RestoreV2", ["save/Const"]))
+    for i, n in enumerate(names + ["global_step"]):
+        save_nodes.append(node(f"save/Assign_{i}" if i else "save/Assign", "Assign", [n, f"save/RestoreV2:{i}"]))
+    save_nodes.append(node("save/restore_all", "NoOp",
+                           [f"^save/Assign_{i}" if i else "^save/Assign" for i in range(len(names) + 1)]))
+    g = g + b"".join(_ld(1, n) for n in save_nodes)
+    info = _ld(1, b"v0") + _ld(4, b"train") + _ld(5, b"ina-mi355x (TF1 layout)")
+    saver = (_ld(1, b"save/Const:0") + _ld(2, b"save/control_dependency:0") + _ld(3, b"save/restore_all") +
+             _key(4, 0) + _varint(int(max_to_keep)) + _key(6, 5) + struct.pack("<f", 10000.0) + _key(7, 0) + _varint(2))
+    var_all = [_var_def(n, n in trainable) for n in names] + [_var_def("global_step", False)]
+    var_tr = [_var_def(n, True) for n in names if n in trainable]
+    opt = "Adam" if model.cfg.optimizer == "adam" else "Adagrad"
+    return (_ld(1, info) + _ld(2, g) + _ld(3, saver) +
+            _collection("global_step", 2, [_var_def("global_step", False)]) +
+            _collection("train_op", 1, [f"OptimizeLoss/{opt}".encode()]) +
+            _collection("trainable_variables", 2, var_tr) +
+            _collection("variables", 2, var_all))
+
+
+def parse_meta_graph(b: bytes) -> dict:
+    """Minimal MetaGraphDef reader (tests): -> {meta_info: raw, nodes: parse_graph(...), saver: {field: value},
+    collections: {name: (kind, [values])}}."""
+    import struct
+    from .metrics import _read_varint
+
+    def fields(buf):
+        i, out = 0, []
+        while i < len(buf):
+            key, i = _read_varint(buf, i)
+            f, wt = key >> 3, key & 7
+            if wt == 0:
+                v, i = _read_varint(buf, i)
+            elif wt == 5:
+                v = struct.unpack_from("<f", buf, i)[0]
+                i += 4
+            else:
+                ln, i = _read_varint(buf, i)
+                v = buf[i:i + ln]
+                i += ln
+            out.append((f, v))
+        return out
+
+    res = {"nodes": [], "saver": {}, "collections": {}, "meta_info": b""}
+    for f, v in fields(b):
+        if f == 1:
+            res["meta_info"] = v
+        elif f == 2:
+            res["nodes"] = parse_graph(v)
+        elif f == 3:
+            res["saver"] = dict(fields(v))
+        elif f == 4:
+            ent = dict(fields(v))
+            (kind, inner), = fields(ent[2])
+            res["collections"][ent[1].decode()] = (kind, [x for _, x in fields(inner)])
+    return res
+
+
 def parse_graph(b: bytes) -> List[dict]:
     """Minimal GraphDef reader (tests): -> [{name, op, inputs, attrs: {key: raw bytes}}]."""
     from .metrics import _read_varint

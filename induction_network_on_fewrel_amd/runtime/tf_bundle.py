@@ -9,8 +9,9 @@ The reference saves with ``tf.train.Saver().save(sess, <dir>/checkpoint/inductio
   bytewise order; blocks = prefix-compressed entries + restart array + (type byte, masked CRC32C);
   metaindex and index blocks; a 48-byte footer ending in the table magic 0xdb4775248b80fb57;
 * ``inductionNetwork-<step>.data-00000-of-00001`` -- the tensors' raw little-endian bytes back to back;
-* ``inductionNetwork-<step>.meta`` -- the serialized MetaGraphDef.  There is no TF graph here, so no .meta
-  is written (``tf.train.load_checkpoint`` / ``NewCheckpointReader`` need only .index + .data).
+* ``inductionNetwork-<step>.meta`` -- the serialized MetaGraphDef (runtime/tb_graph.py::meta_graph): the
+  model's GraphDef (the same one the summary writer puts in the event file) with the Saver's save / restore
+  nodes, a V2 SaverDef and the variables / trainable_variables / train_op / global_step collections.
 
 The tensor keys are the reference's TF variable names, so a TF ``CheckpointReader`` sees the
 same variables, shapes and dtypes.  Parity with TensorFlow itself is unpinned (TF is not installed and
@@ -39,18 +40,17 @@ _DT_INV = {v: k for k, v in _DT.items()}
 
 
 # ------------------------------------------------------------------ CRC32C
-def crc32c(data: bytes, crc: int = 0) -> int:
-    """CRC-32C; the native host implementation (csrc/io_bindings.cpp) when the library loads."""
+def crc32c(data, crc: int = 0) -> int:
+    """CRC-32C of a bytes-like object; the host-only native module (csrc/host/ina_host.c, no torch / HIP
+    dependency) when it is built, else a table loop."""
     try:
-        from ..ops._ext import available
-        if available():
-            buf = torch.frombuffer(bytearray(data), dtype=torch.uint8) if len(data) else torch.empty(0, dtype=torch.uint8)
-            return int(torch.ops.ina.crc32c(buf, crc)) & 0xFFFFFFFF
-    except Exception:
+        from .. import _ina_host
+        return _ina_host.crc32c(data, crc)
+    except ImportError:
         pass
     from .metrics import _TABLE
     c = crc ^ 0xFFFFFFFF
-    for b in data:
+    for b in bytes(data):
         c = _TABLE[(c ^ b) & 0xFF] ^ (c >> 8)
     return c ^ 0xFFFFFFFF
 
@@ -246,7 +246,7 @@ def save_bundle(prefix: str, tensors: "OrderedDict[str, torch.Tensor]") -> None:
             t = tensors[name].detach().to("cpu").contiguous()
             if t.dtype not in _DT:
                 raise TypeError(f"{name}: dtype {t.dtype} has no TF DataType here")
-            raw = t.reshape(-1).view(torch.uint8).numpy().tobytes() if t.numel() else b""
+            raw = t.reshape(-1).view(torch.uint8).numpy() if t.numel() else b""   # no copy (buffer protocol)
             f.write(raw)
             items.append((name.encode(), entry_proto(_DT[t.dtype], list(t.shape), off, len(raw), mask(crc32c(raw)))))
             off += len(raw)

@@ -30,7 +30,7 @@ from ..ops.optim import FlatParams, FusedOptimizer, lr_at
 from ..parallel.dp import DistContext
 from . import checkpoint as ckpt
 from .metrics import MetricsLogger
-from .tb_graph import model_graph
+from .tb_graph import meta_graph, model_graph
 
 
 class _HostEpisodes:
@@ -419,8 +419,13 @@ class Trainer:
         meta = {"best_acc": self.best_acc, "optimizer_t": self.opt.t, "optimizer_t_counts": "applied",
                 "config": self.cfg.to_dict(),
                 "train_samplers": samplers, "skipped_steps": skipped, "world_size": self.dist.world}
+        mg = None
+        if self.cfg.tf_checkpoint:
+            if getattr(self, "_meta_graph", None) is None:   # built once (the graph does not change)
+                self._meta_graph = meta_graph(self.model, self.cfg.N, self.cfg.K, self.cfg.Q, self.cfg.max_to_keep)
+            mg = self._meta_graph
         return ckpt.save(self.cfg.model_dir, self.cfg.ckpt_name, self.global_step, self.state_tensors(), meta,
-                         self.cfg.max_to_keep, best=best)
+                         self.cfg.max_to_keep, best=best, tf_format=self.cfg.tf_checkpoint, meta_graph=mg)
 
     def load(self, stem: str, prefer: str = "safetensors") -> None:
         """Restore from ``stem`` (either checkpoint format; ``prefer="tf"``: the TF bundle copy)."""

@@ -90,3 +90,23 @@ def test_gemm_rejects_bad_shapes():
     w = torch.randn(200, 128, device=dev).bfloat16()
     with pytest.raises(RuntimeError):
         _ops().bert_gemm(x, w, None, None, 0)   # N % 256 != 0
+
+
+@pytest.mark.parametrize("K,MI,NJ,splits", [(64, 40, 4000, 0), (40960, 40, 4000, 0), (1280, 64, 1000, 3), (640, 16, 8, 0),
+                                            (4096, 48, 2056, 7), (192, 8, 264, 5)])
+def test_gemm_tn_slab(K, MI, NJ, splits):
+    """Reduction GEMM (csrc/kernels/gemm_tn.hip): slab[s] summed = A[:, :MI]^T B over all K, vs fp32 torch.
+    Includes the headline dM shape (K = 8192 episodes x 5 classes, MI = H = 40, NJ = h H = 4000), column tails
+    past the last 256-wide tile, more splits than K-steps per split divides, and an A wider than MI."""
+    torch.manual_seed(K + MI + NJ)
+    lda = MI + (8 if MI < 64 else 0)
+    A = torch.randn(K, lda, device=dev).bfloat16()
+    Bm = torch.randn(K, NJ, device=dev).bfloat16()
+    slab = _ops().gemm_tn_slab(A, Bm, MI, splits)
+    torch.cuda.synchronize()
+    ref = A[:, :MI].float().t() @ Bm.float()
+    got = slab.sum(0)
+    assert slab.shape[1:] == (MI, NJ)
+    err = (got - ref).abs()
+    # fp32 accumulation of exact bf16 products: only summation-order differences
+    assert (err / (ref.abs() + (K ** 0.5))).max().item() < 1e-4, err.max().item()

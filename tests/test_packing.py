@@ -242,3 +242,46 @@ def test_fused_attention_packs(U):
                         np.testing.assert_allclose(D[4 * q + r], dH[:, d * U + 4 * m + q], rtol=1e-10, atol=1e-10)
                     else:
                         assert np.all(D[4 * q + r] == 0)
+
+
+@pytest.mark.parametrize("H,h,N,paper", [(40, 100, 5, False), (40, 7, 5, True), (64, 9, 10, False), (16, 5, 3, True),
+                                         (40, 1, 4, False)])
+def test_ntn_tile_pack_layout(H, h, N, paper):
+    """The NTN tile pack (csrc/kernels/ntn.hip) read back through the kernel's addressing: M images
+    with the 8-byte-chunk XOR swizzle and the two 16x16x16 FC fragments of every tile."""
+    from induction_network_on_fewrel_amd.ops.packing import ntn_tile_geometry, pack_ntn_tiles, _ntn_dw_idx
+    g = torch.Generator().manual_seed(0)
+    M = torch.randn(H, H, h, generator=g)
+    w = torch.randn(h, 1, generator=g) if paper else torch.randn(h * N, N, generator=g)
+    pk = pack_ntn_tiles(M, w, N, paper).float()
+    MTH, SG, NT, TE = ntn_tile_geometry(H, h, N)
+    assert pk.shape == (NT, TE) and (TE * 2) % 1024 == 0
+    RA = 16 * MTH
+    Mb = M.to(torch.bfloat16).float()
+    wb = w.to(torch.bfloat16).float().reshape(-1)
+    for t in range(NT):
+        for sl in range(SG):
+            s = t * SG + sl
+            for a in range(RA):
+                mask = ((a & 2) << 1) | (a & 8)
+                for b in range(64):
+                    v = pk[t, sl * RA * 64 + a * 64 + ((((b >> 2) ^ mask) << 2) | (b & 3))]
+                    ref = Mb[a, b, s] if (s < h and a < H and b < H) else 0.0
+                    assert v == ref, (t, sl, a, b)
+        base = SG * RA * 64
+        for l in range(64):
+            for j in range(4):
+                for which, (row, cp) in enumerate(((l & 15, 4 * (l >> 4) + j), (4 * (l >> 4) + j, l & 15))):
+                    sl, c = divmod(row, N)
+                    s = t * SG + sl
+                    if row >= SG * N or s >= h or cp >= N:
+                        ref = 0.0
+                    elif paper:
+                        ref = wb[s] if c == cp else 0.0
+                    else:
+                        ref = wb[(s * N + c) * N + cp]
+                    assert pk[t, base + 256 * which + 4 * l + j] == ref
+    di = _ntn_dw_idx(h, N, paper)
+    assert di.numel() == NT * (SG if paper else SG * N * N)
+    valid = di[di >= 0]
+    assert valid.unique().numel() == valid.numel() == (h if paper else h * N * N)

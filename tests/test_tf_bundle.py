@@ -145,3 +145,36 @@ def test_fewrel_eval_reads_tf_bundle_only_checkpoint(tmp_path):
         assert r.returncode == 0, r.stderr
         outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
     assert outs[0]["accuracy"] == outs[1]["accuracy"] and outs[0]["step"] == outs[1]["step"]
+
+
+def test_meta_graph_written_and_parsed(tmp_path):
+    """<stem>.meta (tf.train.Saver.save writes it next to .index / .data, reference model/base.py:124,177):
+    a MetaGraphDef with the model GraphDef + Saver nodes, a V2 SaverDef and the variable collections."""
+    from induction_network_on_fewrel_amd.config import Config
+    from induction_network_on_fewrel_amd.data import make_synthetic
+    from induction_network_on_fewrel_amd.runtime.tb_graph import parse_meta_graph
+    from induction_network_on_fewrel_amd.runtime.trainer import Trainer
+    cfg = Config(N=5, K=1, Q=2, hidden_size=8, max_length=12, train_iter=1, val_iter=1, val_step=1000,
+                 model_dir=str(tmp_path / "m"), resume=False, device="cpu", dtype="fp32")
+    data = make_synthetic(num_relations=8, instances_per_relation=10, vocab=100, seed=0, max_length=12)
+    tr = Trainer(cfg, data, None, device="cpu")
+    stem = tr.save()
+    with open(stem + ".meta", "rb") as fh:
+        mg = parse_meta_graph(fh.read())
+    assert b"v0" in mg["meta_info"]
+    names = {n["name"] for n in mg["nodes"]}
+    assert {"save/Const", "save/SaveV2", "save/control_dependency", "save/RestoreV2", "save/restore_all", "M",
+            "global_step"} <= names
+    sv = mg["saver"]
+    assert sv[1] == b"save/Const:0" and sv[2] == b"save/control_dependency:0" and sv[3] == b"save/restore_all"
+    assert sv[4] == cfg.max_to_keep and sv[7] == 2 and abs(sv[6] - 10000.0) < 1e-3
+    kind, vals = mg["collections"]["trainable_variables"]
+    assert kind == 2 and any(v.startswith(b"\n\x03M:0") for v in vals)
+    kind, vals = mg["collections"]["variables"]
+    assert len(vals) == len(tr.model.params.names()) + 1
+    assert mg["collections"]["train_op"] == (1, [b"OptimizeLoss/Adam"])
+    # the rotation removes .meta with the rest of a checkpoint
+    cfg2 = Config(**dict(cfg.to_dict(), tf_checkpoint=False, model_dir=str(tmp_path / "n")))
+    tr2 = Trainer(cfg2, data, None, device="cpu")
+    s2 = tr2.save()
+    assert os.path.exists(s2 + ".safetensors") and not os.path.exists(s2 + ".meta") and not os.path.exists(s2 + ".index")
