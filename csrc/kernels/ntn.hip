@@ -37,15 +37,25 @@ namespace {
 constexpr int NW = 8;                // waves (each G episodes) per workgroup
 constexpr int NT_THREADS = NW * 64;
 constexpr int IMG_ROW = 128;         // bytes per LDS image row: 64 bf16
-constexpr int PIMG = 16 * IMG_ROW;   // per-episode P image [16 rows (slice, class)][64 b]
+constexpr int PIMG = 16 * IMG_ROW + 64;   // per-episode P image [16 rows (slice, class)][64 b], + 64 B: the
+                                         // two episodes' images sit 16 banks apart (their rows meet in one
+                                         // write / read instruction)
 constexpr int ZERO_BYTES = 256;      // zero block: the fragment reads of rows outside an image
 constexpr int DW_SLOT = 256;         // floats per wave of the dw tile exchange
 constexpr f32x4_t Z4 = {0.f, 0.f, 0.f, 0.f};
 constexpr s16x4_t Z4S = {0, 0, 0, 0};
 
 INA_DEVICE int mask_m(int a) { return ((a & 2) << 1) | (a & 8); }
-INA_DEVICE int mask_p(int r) { return (r & 6) << 1; }
+// P image row r: 8-byte chunk XOR {0,4,12,2,10,14,6,8}[r & 7] (searched with an LDS bank model -- reads 64 banks,
+// writes 32 banks per 16-lane group: the row reads, the transposed reads and the per-row stores are
+// conflict-free, the stacked-episode stores 2-way; the (r & 6) << 1 mask had 4-way stores)
+INA_DEVICE int mask_p(int r) { return (int)((0x86EA2C40u >> (4 * (r & 7))) & 15u); }
 INA_DEVICE int vslot(int r) { return (r & ~15) | (r & 8) | ((r + ((r & 8) >> 1)) & 7); }
+// V / dT image: byte offset of 8-byte chunk c of row r (row slots rotated, chunks XOR-ed by slot >> 2)
+INA_DEVICE int voff(int r, int c) {
+  const int sl = vslot(r);
+  return sl * 32 + ((c ^ ((sl >> 2) & 3)) << 3);
+}
 
 INA_DEVICE s16x4_t trr(const unsigned char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)p);
@@ -143,11 +153,12 @@ INA_DEVICE void load_qf(const NtnArgs& k, const Geo& g, int ep, bool oke, int q,
 }
 
 // P^T_s for the SG slices of the staged tile (stacked over the wave's episodes) -> the P images
-template <int MTH>
+template <int MTH, int SG>
 INA_DEVICE void p_images(const unsigned char* buf, const unsigned char* zero, unsigned char* pimg, const Geo& g,
                          const u16x8_t (&Cf)[2], int q, int n) {
   constexpr int RA = 16 * MTH;
-  for (int sl = 0; sl < g.SG; ++sl) {
+#pragma unroll
+  for (int sl = 0; sl < SG; ++sl) {
     const unsigned char* mimg = buf + sl * (RA * IMG_ROW);
     f32x4_t PT[MTH];
 #pragma unroll
@@ -181,7 +192,7 @@ INA_DEVICE void p_rows(const unsigned char* img, int q, int n, u16x8_t (&Pa)[2])
 }
 
 // ------------------------------------------------------------------------------------------
-template <int MTH, int QT>
+template <int MTH, int QT, int SG>
 __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void ntn_fwd_kernel(NtnArgs k) {
   constexpr int GM = QT <= 2 ? 2 : 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char ntn_lds[];
@@ -195,7 +206,7 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     for (int i = lane; i < ZERO_BYTES / 16; i += 64) reinterpret_cast<u32x4_t*>(zero)[i] = u32x4_t{0u, 0u, 0u, 0u};
   const int nfrag = k.tpb >> 10;
   const unsigned char* tiles = reinterpret_cast<const unsigned char*>(k.tiles);
-  const int fo = g.SG * MTH * 16 * IMG_ROW;   // FC fragments after the M images
+  constexpr int fo = SG * MTH * 16 * IMG_ROW;   // FC fragments after the M images
   for (int grp = blockIdx.x; grp * NW * g.G < k.E; grp += gridDim.x) {
     const int epw = (grp * NW + wave) * g.G;
     u16x8_t Cf[2];
@@ -217,7 +228,7 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       if (t + 1 < t1) stage_tile(ntn_lds + ((t + 1 - t0) & 1) * k.tpb, tiles + (long)(t + 1) * k.tpb, nfrag);
       const int lt = opaque_lane(), q = lt >> 4, n = lt & 15;
       const Geo g = geo(k, n);
-      p_images<MTH>(buf, zero, ntn_lds + woff, g, Cf, q, n);
+      p_images<MTH, SG>(buf, zero, ntn_lds + woff, g, Cf, q, n);
       wave_order(woff);
       const s16x4_t wt = *reinterpret_cast<const s16x4_t*>(buf + fo + 512 + lt * 8);
 #pragma unroll
@@ -258,7 +269,7 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
 }
 
 // ------------------------------------------------------------------------------------------
-template <int MTH, int QT>
+template <int MTH, int QT, int SG>
 __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(2))) void ntn_bwd_kernel(NtnArgs k) {
   constexpr int GM = QT <= 2 ? 2 : 1;
   constexpr int KQ = (QT + 1) / 2;     // 32-deep K-steps over the queries
@@ -280,10 +291,10 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
     for (int i = lane; i < ZERO_BYTES / 16; i += 64) reinterpret_cast<u32x4_t*>(zero)[i] = u32x4_t{0u, 0u, 0u, 0u};
   const int nfrag = k.tpb >> 10;
   const unsigned char* tiles = reinterpret_cast<const unsigned char*>(k.tiles);
-  const int fo = g.SG * MTH * 16 * IMG_ROW;
+  constexpr int fo = SG * MTH * 16 * IMG_ROW;
   const float gs = k.gscale ? k.gscale[0] : 1.f;
-  const int SGN = g.SG * g.N;
-  const int dwe = k.paper ? g.SG : SGN * g.N;   // dw slab entries per tile
+  const int SGN = SG * g.N;
+  const int dwe = k.paper ? SG : SGN * g.N;   // dw slab entries per tile
   const long hH = (long)k.h * g.H;
   unsigned short* const dp = reinterpret_cast<unsigned short*>(k.dp_out);
   unsigned short* const dp_trash = dp + ((long)k.E * g.N + 63) / 64 * 64 * hH;   // past the zero pad rows
@@ -366,7 +377,7 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         }
         k.dw_slab[((long)grp * k.ntile + t - 1) * dwe + threadIdx.x] = acc;
       }
-      p_images<MTH>(buf, zero, ntn_lds + woff, g, Cf, q, n);
+      p_images<MTH, SG>(buf, zero, ntn_lds + woff, g, Cf, q, n);
       wave_order(woff);
       const s16x4_t wA = *reinterpret_cast<const s16x4_t*>(buf + fo + lt * 8);
       f32x4_t dw = Z4;
@@ -388,7 +399,7 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
 #pragma unroll
           for (int r = 0; r < 4; ++r) dT[qt][r] = T[r] > 0.f ? dV[r] : 0.f;
           // images [query row][(s, c) col]: the lane writes its query row's 4 (s, c) columns
-          const int off = vslot(16 * qt + n) * 32 + q * 8;
+          const int off = voff(16 * qt + n, q);
           *reinterpret_cast<s16x4_t*>(vimg + off) = bf4relu(T);
           *reinterpret_cast<s16x4_t*>(dtimg + off) = bf4(dT[qt]);
         }
@@ -401,7 +412,7 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
 #pragma unroll
         for (int kq = 0; kq < KQ; ++kq) {
           const int r0 = 32 * kq + 8 * q + (n >> 2);
-          const int o0 = vslot(r0) * 32 + (n & 3) * 8, o1 = vslot(r0 + 4) * 32 + (n & 3) * 8;
+          const int o0 = voff(r0, n & 3), o1 = voff(r0 + 4, n & 3);
           Vt[kq] = cat8(trr(vimg + o0), trr(vimg + o1));
           dTt[kq] = cat8(trr(dtimg + o0), trr(dtimg + o1));
         }
@@ -426,7 +437,7 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         }
         // dP -> global bf16 [(e, c)][s H + b] (lanes outside the valid ranges store into the trash tail)
         {
-          const int s = t * g.SG + dsl;
+          const int s = t * SG + dsl;
           const bool okc = n < SGN && s < k.h && ep < k.E;
           unsigned short* const drow = dp + ((long)(okc ? ep : 0) * g.N + dcl) * hH + (long)(okc ? s : 0) * g.H;
 #pragma unroll
@@ -446,7 +457,8 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
       wave_order(woff);
       const unsigned char* const pimg = ntn_lds + woff;
       // dC^T[a][(g, c)] += sum_b M_s[a, b] D_s[b, (g, c)], stacked over the wave's episodes
-      for (int sl = 0; sl < g.SG; ++sl) {
+#pragma unroll
+      for (int sl = 0; sl < SG; ++sl) {
         const unsigned char* mimg = buf + sl * (RA * IMG_ROW);
         const int row = sl * g.N + g.lc;
         u16x8_t Bd[2];
@@ -559,19 +571,19 @@ size_t lds_bytes(const NtnArgs& a, int QT, bool bwd) {
   return (size_t)2 * a.tpb + ZERO_BYTES + NW * per_wave + (bwd ? (size_t)2 * NW * DW_SLOT * 4 : 0);
 }
 
-template <int MTH, int QT, bool BWD>
+template <int MTH, int QT, int SG, bool BWD>
 int launch(const NtnArgs& a, hipStream_t st) {
   const int groups = ina::ntn_groups(a.E, a.N, a.Q);
   const int blocks = groups < a.blocks ? groups : a.blocks;
   const int ny = a.split > 1 ? a.split : 1;
   const size_t lds = lds_bytes(a, QT, BWD);
-  const void* fn = BWD ? (const void*)ntn_bwd_kernel<MTH, QT> : (const void*)ntn_fwd_kernel<MTH, QT>;
+  const void* fn = BWD ? (const void*)ntn_bwd_kernel<MTH, QT, SG> : (const void*)ntn_fwd_kernel<MTH, QT, SG>;
   if (lds > 64 * 1024 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -1;
   if (BWD) {
-    hipLaunchKernelGGL((ntn_bwd_kernel<MTH, QT>), dim3(blocks, ny), dim3(NT_THREADS), lds, st, a);
+    hipLaunchKernelGGL((ntn_bwd_kernel<MTH, QT, SG>), dim3(blocks, ny), dim3(NT_THREADS), lds, st, a);
   } else {
-    hipLaunchKernelGGL((ntn_fwd_kernel<MTH, QT>), dim3(blocks, ny), dim3(NT_THREADS), lds, st, a);
+    hipLaunchKernelGGL((ntn_fwd_kernel<MTH, QT, SG>), dim3(blocks, ny), dim3(NT_THREADS), lds, st, a);
   }
   if (ny > 1) {
     if (BWD) {
@@ -594,14 +606,20 @@ int dispatch(const NtnArgs& a, hipStream_t st) {
   if (a.N < 1 || a.N > 16 || QT == 0 || a.H % 8 != 0 || a.H > 64) return -1;
   if (a.SG != ina::ntn_slices_per_tile(a.N) || a.G != ina::ntn_episodes_per_wave(a.N, a.Q)) return -1;
   if (lds_bytes(a, QT, BWD) > 160 * 1024) return -1;
-#define INA_NTN_QT(M)                                  \
-  if (QT == 1) return launch<M, 1, BWD>(a, st);        \
-  if (QT == 2) return launch<M, 2, BWD>(a, st);        \
-  if (QT == 4) return launch<M, 4, BWD>(a, st);
+#define INA_NTN_SG(M, Q)                                  \
+  if (a.SG == 1) return launch<M, Q, 1, BWD>(a, st);      \
+  if (a.SG == 2) return launch<M, Q, 2, BWD>(a, st);      \
+  if (a.SG == 3) return launch<M, Q, 3, BWD>(a, st);      \
+  if (a.SG == 4) return launch<M, Q, 4, BWD>(a, st);
+#define INA_NTN_QT(M)                   \
+  if (QT == 1) { INA_NTN_SG(M, 1) }     \
+  if (QT == 2) { INA_NTN_SG(M, 2) }     \
+  if (QT == 4) { INA_NTN_SG(M, 4) }
   if (MTH == 1) { INA_NTN_QT(1) }
   if (MTH == 3) { INA_NTN_QT(3) }
   if (MTH == 4) { INA_NTN_QT(4) }
 #undef INA_NTN_QT
+#undef INA_NTN_SG
   return -1;
 }
 
