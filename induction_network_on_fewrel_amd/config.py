@@ -43,6 +43,11 @@ class Config:
     synthetic_instances: int = 700
     synthetic_vocab: int = 400000
     synthetic_word_dim: int = 5
+    synthetic_task: str = "lexical"    # "lexical": per-relation trigger words anywhere (benchmarks); "transfer":
+                                       # relation-disjoint train / val / test splits, relations told apart only by
+                                       # the span between the entities (data/synthetic.py::make_transfer_splits)
+    synthetic_val_relations: int = 8   # transfer task: validation (checkpoint selection) relations
+    synthetic_test_relations: int = 8  # transfer task: held-out test relations
 
     # ---------------- model (model/base.py:12-27, train.py:31-37) ----------------
     hidden_size: int = 20              # LSTM units per direction (u); BiLSTM out = 2u
@@ -175,6 +180,8 @@ class Config:
             raise ValueError(f"unknown optimizer {self.optimizer}")
         if self.encoder not in ("bilstm", "bert"):
             raise ValueError(f"unknown encoder {self.encoder}")
+        if self.synthetic_task not in ("lexical", "transfer"):
+            raise ValueError(f"unknown synthetic_task {self.synthetic_task}")
         if self.encoder == "bert":
             if self.bert_hidden % self.bert_heads != 0 or self.bert_hidden // self.bert_heads != 64:
                 raise ValueError("BERT heads must be 64 wide (bert_hidden = 64 * bert_heads)")

@@ -77,3 +77,72 @@ def make_synthetic(num_relations: int = 64, instances_per_relation: int = 700, m
     rel2scope = OrderedDict((f"S{r}", [r * I, (r + 1) * I]) for r in range(R))
     mat = random_word_vectors(vocab, word_dim, seed + 1) if with_word_vectors else None
     return FewRelDataset(word, pos1, pos2, mask, lengths, rel2scope, mat, None, "synthetic")
+
+
+def make_transfer_splits(train_relations: int = 48, val_relations: int = 8, test_relations: int = 8,
+                         instances_per_relation: int = 300, max_length: int = 37, vocab: int = 20000,
+                         word_dim: int = 50, triggers_per_relation: int = 4, triggers_in_span: int = 2,
+                         distractors: int = 4, min_gap: int = 3, max_gap: int = 7, seed: int = 0):
+    """Few-shot RELATION-TRANSFER task (verdict r4 #5): three relation-disjoint splits (train / val / test)
+    whose relations the encoder can only tell apart by what lies BETWEEN the two entities.
+
+    * Relation r owns ``triggers_per_relation`` trigger tokens (disjoint across ALL relations of all splits,
+      so val / test relations bring trigger tokens never seen in training).
+    * A sentence (length from val.json's histogram) has head / tail entities ``min_gap .. max_gap`` tokens
+      apart (random order); ``triggers_in_span`` of r's triggers sit between them, the rest of the span is
+      filler.
+    * Outside the span sit ``distractors`` triggers of OTHER relations of the same split -- in a test episode
+      often of the episode's other classes -- plus filler.  A bag of words (mean-pooled word vectors:
+      tools/control_baseline.py --task transfer) therefore sees more wrong-class than right-class triggers;
+      a model that learned (on the training relations) to read the span between the entities through the
+      position features transfers to the unseen relations.
+    -> (train, val, test) FewRelDatasets sharing one frozen random word table (``word_dim``-d)."""
+    rng = np.random.default_rng(seed)
+    L = max_length
+    R = train_relations + val_relations + test_relations
+    T = triggers_per_relation
+    if R * T >= vocab // 2:
+        raise ValueError("vocab too small for the trigger tokens")
+    blank = vocab + 1
+    mat = random_word_vectors(vocab, word_dim, seed + 1)
+    ls_all = np.array([k for k in FEWREL_VAL_LENGTH_HIST if max_gap + 4 <= k <= min(36, L)], dtype=np.int32)
+    w_all = np.array([FEWREL_VAL_LENGTH_HIST[k] for k in ls_all], dtype=np.float64)
+    bounds = np.cumsum([0, train_relations, val_relations, test_relations])
+    out = []
+    for part, name in enumerate(("train", "val", "test")):
+        rels = np.arange(bounds[part], bounds[part + 1])
+        nr, I = len(rels), instances_per_relation
+        tot = nr * I
+        lengths = rng.choice(ls_all, size=tot, p=w_all / w_all.sum()).astype(np.int32)
+        word = rng.integers(R * T, vocab, size=(tot, L)).astype(np.int32)   # filler (never a trigger)
+        p1 = np.zeros(tot, dtype=np.int32)
+        p2 = np.zeros(tot, dtype=np.int32)
+        for i in range(tot):
+            r = rels[i // I]
+            n = lengths[i]
+            gap = int(rng.integers(min_gap, max_gap + 1))
+            a = int(rng.integers(0, n - gap - 1))
+            b = a + gap + 1
+            if rng.random() < 0.5:
+                p1[i], p2[i] = a, b
+            else:
+                p1[i], p2[i] = b, a
+            span = np.arange(a + 1, b)
+            for pos in rng.choice(span, size=min(triggers_in_span, len(span)), replace=False):
+                word[i, pos] = r * T + int(rng.integers(0, T))
+            outside = np.concatenate([np.arange(0, a), np.arange(b + 1, n)])
+            others = rels[rels != r]
+            if len(others) and len(outside):
+                for pos in rng.choice(outside, size=min(distractors, len(outside)), replace=False):
+                    word[i, pos] = int(rng.choice(others)) * T + int(rng.integers(0, T))
+        j = np.arange(L, dtype=np.int32)[None, :]
+        word[j >= lengths[:, None]] = blank
+        pos1 = (j - p1[:, None] + L).astype(np.int32)
+        pos2 = (j - p2[:, None] + L).astype(np.int32)
+        lo = np.minimum(p1, p2)[:, None]
+        hi = np.maximum(p1, p2)[:, None]
+        mask = np.where(j <= lo, 1, np.where(j <= hi, 2, 3)).astype(np.int32)
+        mask[j >= lengths[:, None]] = 0
+        rel2scope = OrderedDict((f"T{r}", [k * I, (k + 1) * I]) for k, r in enumerate(rels))
+        out.append(FewRelDataset(word, pos1, pos2, mask, lengths, rel2scope, mat, None, f"transfer_{name}"))
+    return tuple(out)

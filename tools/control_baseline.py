@@ -28,6 +28,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def _meanpool_accuracy(ds, W, K, episodes, seed, N=5, Q=5):
+    """Mean of the frozen word vectors over the valid tokens -> nearest class prototype (cosine)."""
+    from induction_network_on_fewrel_amd.data import EpisodeSampler
+    valid = (ds.data_mask > 0).astype(np.float32)
+    vec = (W[ds.data_word] * valid[..., None]).sum(1) / np.maximum(valid.sum(1, keepdims=True), 1.0)
+    vec /= np.maximum(np.linalg.norm(vec, axis=1, keepdims=True), 1e-12)
+    s = EpisodeSampler(ds, seed=seed)
+    idx, labels = s.next_batch_indices(episodes, N, K, Q)
+    sup = vec[idx[:, : N * K]].reshape(episodes, N, K, -1).mean(2)
+    sup /= np.maximum(np.linalg.norm(sup, axis=-1, keepdims=True), 1e-12)
+    pred = np.einsum("bqd,bnd->bqn", vec[idx[:, N * K:]], sup).argmax(-1)
+    return float((pred == labels).mean())
+
+
 def main():
     from induction_network_on_fewrel_amd.config import Config
     from induction_network_on_fewrel_amd.data import EpisodeSampler, FewRelDataset, vocab_from_fewrel
@@ -38,9 +52,34 @@ def main():
     ap.add_argument("--shots", default="1,5")
     ap.add_argument("--episodes", type=int, default=3000)
     ap.add_argument("--out", default="")
+    ap.add_argument("--task", default="val", choices=["val", "transfer"],
+                    help="transfer: the synthetic relation-transfer task's held-out test relations "
+                         "(data/synthetic.py::make_transfer_splits with train.py's --synthetic_task transfer defaults)")
+    ap.add_argument("--relations", type=int, default=48, help="transfer: training relations (--synthetic_relations)")
+    ap.add_argument("--instances", type=int, default=300, help="transfer: instances per relation")
+    ap.add_argument("--vocab", type=int, default=20000, help="transfer: --synthetic_vocab")
+    ap.add_argument("--seed", type=int, default=None, help="transfer: --seed (default Config.seed)")
     args = ap.parse_args()
     cfg = Config()
     rows = []
+    if args.task == "transfer":
+        from induction_network_on_fewrel_amd.data.synthetic import make_transfer_splits
+        seed = cfg.seed if args.seed is None else args.seed
+        for dim in (int(x) for x in args.dims.split(",")):
+            _, va, te = make_transfer_splits(args.relations, cfg.synthetic_val_relations, cfg.synthetic_test_relations,
+                                             args.instances, cfg.max_length, args.vocab, dim, seed=seed)
+            for split in (va, te):
+                for K in (int(x) for x in args.shots.split(",")):
+                    acc = _meanpool_accuracy(split, split.word_vec_mat, K, args.episodes, cfg.seed)
+                    r = dict(control="meanpool-nearest-prototype", task="transfer", split=split.name, dim=dim, N=5,
+                             K=K, episodes=args.episodes, relations=split.relations(), accuracy=round(acc, 4))
+                    rows.append(r)
+                    print(json.dumps(r), flush=True)
+        if args.out:
+            with open(args.out, "w") as fh:
+                for r in rows:
+                    fh.write(json.dumps(r) + "\n")
+        return
     for dim in (int(x) for x in args.dims.split(",")):
         # the word table train.py --vocab_from_data builds (processed-data cache bypassed: written to /tmp)
         wv = f"/tmp/ina_control_vocab_{dim}.json"

@@ -8,6 +8,7 @@ hidden_size=20, ``./data/glove.6B.5d.json`` and ``checkpoints/inductionNetwork_t
 Examples
   python train.py induction 5 2                          # reference defaults (needs data files)
   python train.py induction 5 1 --synthetic true         # synthetic FewRel-shaped data
+  python train.py induction 5 1 --synthetic true --synthetic_task transfer --test_best true   # unseen relations
   python train.py induction 5 5 --val_file data/val.json --split_val true   # relation-disjoint val split
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 train.py induction 5 5 --episodes_per_step 64
 """
@@ -52,6 +53,15 @@ def build_parser():
 
 def load_data(cfg: Config, args):
     from induction_network_on_fewrel_amd.data import FewRelDataset, make_synthetic, vocab_from_fewrel
+    if cfg.synthetic and cfg.synthetic_task == "transfer":   # relation-disjoint train / val / test
+        from induction_network_on_fewrel_amd.data.synthetic import make_transfer_splits
+        tr, va, te = make_transfer_splits(cfg.synthetic_relations, cfg.synthetic_val_relations,
+                                          cfg.synthetic_test_relations, cfg.synthetic_instances, cfg.max_length,
+                                          cfg.synthetic_vocab, cfg.synthetic_word_dim, seed=cfg.seed)
+        print(f"transfer task: {len(tr.relations())} train / {len(va.relations())} val / {len(te.relations())} test "
+              "relations (disjoint trigger tokens)", flush=True)
+        args._test_split = te
+        return tr, va
     if cfg.synthetic:
         tr = make_synthetic(cfg.synthetic_relations, cfg.synthetic_instances, cfg.max_length, cfg.synthetic_vocab,
                             cfg.synthetic_word_dim, seed=cfg.seed)
