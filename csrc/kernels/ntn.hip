@@ -45,7 +45,10 @@ constexpr int DW_SLOT = 256;         // floats per wave of the dw tile exchange
 constexpr f32x4_t Z4 = {0.f, 0.f, 0.f, 0.f};
 constexpr s16x4_t Z4S = {0, 0, 0, 0};
 
-INA_DEVICE int mask_m(int a) { return ((a & 2) << 1) | (a & 8); }
+// M image row a: 8-byte chunk XOR {0,0,4,4,8,8,12,12,10,10,14,14,2,2,6,6}[a & 15] -- linear in the row bits,
+// found exhaustively with the bank model (tools/lds_probe/mimage_search.py): the transposed full-K reads, the
+// transposed 16-deep tail reads and the dC row reads are all conflict-free
+INA_DEVICE int mask_m(int a) { return (int)((0x6622EEAACC884400ull >> (4 * (a & 15))) & 15u); }
 // P image row r: 8-byte chunk XOR {0,4,12,2,10,14,6,8}[r & 7] (searched with an LDS bank model -- reads 64 banks,
 // writes 32 banks per 16-lane group: the row reads, the transposed reads and the per-row stores are
 // conflict-free, the stacked-episode stores 2-way; the (r & 6) << 1 mask had 4-way stores)
@@ -64,12 +67,21 @@ INA_DEVICE u16x8_t cat8(const s16x4_t& lo, const s16x4_t& hi) {
   return u16x8_t{(unsigned short)lo[0], (unsigned short)lo[1], (unsigned short)lo[2], (unsigned short)lo[3],
                  (unsigned short)hi[0], (unsigned short)hi[1], (unsigned short)hi[2], (unsigned short)hi[3]};
 }
+// A 16-deep K tail accumulated onto 16x16x32 results: v_mfma_f32_16x16x32_bf16 with the upper half of both
+// operands zero (same k relabelling on A and B, so the sum is the 16x16x16 product).  A back-to-back
+// v_mfma_f32_16x16x32_bf16 -> v_mfma_f32_16x16x16_bf16 accumulate chain gets no wait states from hipcc (ROCm
+// 7.2) and reads a stale SrcC on gfx950 (tools/lds_probe/mfma_chain.hip); the 16x16x16 form is no faster here
+// (tools/lds_probe/mfma_rate.hip), so every chain keeps one opcode.
+INA_DEVICE f32x4_t mfma_tail(const s16x4_t& a, const s16x4_t& b, const f32x4_t& c) {
+  return mfma_bf16(cat8(a, Z4S), cat8(b, Z4S), c);
+}
 INA_DEVICE s16x4_t bf4(const f32x4_t& x) {
   return s16x4_t{(short)f2bf(x[0]), (short)f2bf(x[1]), (short)f2bf(x[2]), (short)f2bf(x[3])};
 }
+// relu on the packed bf16 values: a negative bf16 is a negative int16, so one v_pk_max_i16 per pair (fmaxf on
+// the fp32 values costs a canonicalizing v_max plus the v_max per element)
 INA_DEVICE s16x4_t bf4relu(const f32x4_t& x) {
-  return s16x4_t{(short)f2bf(fmaxf(x[0], 0.f)), (short)f2bf(fmaxf(x[1], 0.f)), (short)f2bf(fmaxf(x[2], 0.f)),
-                 (short)f2bf(fmaxf(x[3], 0.f))};
+  return __builtin_elementwise_max(bf4(x), Z4S);
 }
 // Unconditional load from a clamped index, zero outside (a lane-dependent branch around each load made
 // hipcc wait vmcnt(0) per element); multiply rather than select so LLVM cannot sink the load under a branch
@@ -124,39 +136,79 @@ INA_DEVICE Geo geo(const NtnArgs& k, int n) {
   return g;
 }
 
-// C^T as the B operand of P^T (k = a, 2 K-steps; col = the lane's stacked row (g, c))
-INA_DEVICE void load_cf(const NtnArgs& k, const Geo& g, int epw, int q, u16x8_t (&Cf)[2]) {
+// C^T as the B operand of P^T (col = the lane's stacked row (g, c)): KF = MTH / 2 32-deep K-steps over a
+// (16x16x32) and, for odd MTH, a 16-deep tail a = 32 KF .. + 15 (16x16x16; same cycles, half the LDS reads,
+// and no reads of image rows past 16 MTH)
+template <int MTH>
+struct CFrag {
+  static constexpr int KF = MTH / 2, TAIL = MTH & 1;
+  u16x8_t f[KF > 0 ? KF : 1];
+  s16x4_t t;
+};
+template <int MTH>
+INA_DEVICE void load_cf(const NtnArgs& k, const Geo& g, int epw, int q, CFrag<MTH>& C) {
   const int ep = epw + g.lg;
   const bool ok = g.lrow && ep < k.E;
   const long row = (long)(ok ? ep : 0) * g.N + g.lc;
 #pragma unroll
-  for (int ka = 0; ka < 2; ++ka)
+  for (int ka = 0; ka < CFrag<MTH>::KF; ++ka)
 #pragma unroll
     for (int h4 = 0; h4 < 2; ++h4) {
       const int a = 32 * ka + 8 * q + 4 * h4;
-      ld4bf(k.cls, ok && a < g.H, row * g.H + a, Cf[ka], 4 * h4);
+      ld4bf(k.cls, ok && a < g.H, row * g.H + a, C.f[ka], 4 * h4);
     }
+  if (CFrag<MTH>::TAIL) {
+    u16x8_t t8;
+    const int a = 32 * CFrag<MTH>::KF + 4 * q;
+    ld4bf(k.cls, ok && a < g.H, row * g.H + a, t8, 0);
+    C.t = s16x4_t{(short)t8[0], (short)t8[1], (short)t8[2], (short)t8[3]};
+  } else {
+    C.t = Z4S;
+  }
 }
-// Q^T as the B operand of T^T: B[k = b][col = query 16 qt + n]
-template <int QT>
-INA_DEVICE void load_qf(const NtnArgs& k, const Geo& g, int ep, bool oke, int q, int n, u16x8_t (&Qf)[QT][2]) {
+// Q^T as the B operand of T^T: B[k = b][col = query 16 qt + n]; K over b as in CFrag (full steps + 16-deep tail)
+template <int MTH, int QT>
+struct QFrag {
+  static constexpr int KF = MTH / 2, TAIL = MTH & 1;
+  u16x8_t f[QT][KF > 0 ? KF : 1];
+  s16x4_t t[QT];
+};
+template <int MTH, int QT>
+INA_DEVICE void load_qf(const NtnArgs& k, const Geo& g, int ep, bool oke, int q, int n, QFrag<MTH, QT>& Qf) {
   const long rq0 = (long)(oke ? ep : 0) * (g.N * k.K + g.NQ) + g.N * k.K;
 #pragma unroll
-  for (int qt = 0; qt < QT; ++qt)
+  for (int qt = 0; qt < QT; ++qt) {
+    const int qi = 16 * qt + n;
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int kb = 0; kb < QFrag<MTH, QT>::KF; ++kb)
 #pragma unroll
       for (int h4 = 0; h4 < 2; ++h4) {
-        const int qi = 16 * qt + n, b = 32 * kb + 8 * q + 4 * h4;
-        ld4bf(k.e, oke && qi < g.NQ && b < g.H, (rq0 + qi) * g.H + b, Qf[qt][kb], 4 * h4);
+        const int b = 32 * kb + 8 * q + 4 * h4;
+        ld4bf(k.e, oke && qi < g.NQ && b < g.H, (rq0 + qi) * g.H + b, Qf.f[qt][kb], 4 * h4);
       }
+    if (QFrag<MTH, QT>::TAIL) {
+      u16x8_t t8;
+      const int b = 32 * QFrag<MTH, QT>::KF + 4 * q;
+      ld4bf(k.e, oke && qi < g.NQ && b < g.H, (rq0 + qi) * g.H + b, t8, 0);
+      Qf.t[qt] = s16x4_t{(short)t8[0], (short)t8[1], (short)t8[2], (short)t8[3]};
+    } else {
+      Qf.t[qt] = Z4S;
+    }
+  }
 }
 
 // P^T_s for the SG slices of the staged tile (stacked over the wave's episodes) -> the P images
 template <int MTH, int SG>
-INA_DEVICE void p_images(const unsigned char* buf, const unsigned char* zero, unsigned char* pimg, const Geo& g,
-                         const u16x8_t (&Cf)[2], int q, int n) {
-  constexpr int RA = 16 * MTH;
+INA_DEVICE void p_images(const unsigned char* buf, unsigned char* pimg, const Geo& g, const CFrag<MTH>& C, int q,
+                         int n) {
+  constexpr int RA = 16 * MTH, KF = CFrag<MTH>::KF;
+  // lane offsets: the full steps read rows 32 ka + 8 q + (n >> 2) (lo) and + 4 (hi), the tail rows
+  // 32 KF + 4 q + (n >> 2).  mask_m depends on the row bits 1..3 only (same for every ka / sl); the chunk
+  // (4 mb + (n & 3)) ^ m splits into the 32-byte block mb ^ (m >> 2) and the 8-byte chunk (n & 3) ^ (m & 3)
+  const int af = 8 * q + (n >> 2), at = 32 * KF + 4 * q + (n >> 2);
+  const int ml = mask_m(af), mh = mask_m(af + 4), mt = mask_m(at);
+  const int bl = af * IMG_ROW + (((n & 3) ^ (ml & 3)) << 3), bh = (af + 4) * IMG_ROW + (((n & 3) ^ (mh & 3)) << 3);
+  const int bt = at * IMG_ROW + (((n & 3) ^ (mt & 3)) << 3);
 #pragma unroll
   for (int sl = 0; sl < SG; ++sl) {
     const unsigned char* mimg = buf + sl * (RA * IMG_ROW);
@@ -164,15 +216,13 @@ INA_DEVICE void p_images(const unsigned char* buf, const unsigned char* zero, un
 #pragma unroll
     for (int mb = 0; mb < MTH; ++mb) PT[mb] = Z4;
 #pragma unroll
-    for (int ka = 0; ka < 2; ++ka) {
-      const int a0 = 32 * ka + 8 * q + (n >> 2), a1 = a0 + 4;
+    for (int mb = 0; mb < MTH; ++mb) {
+      const unsigned char* pl = mimg + bl + 32 * (mb ^ (ml >> 2));
+      const unsigned char* ph = mimg + bh + 32 * (mb ^ (mh >> 2));
 #pragma unroll
-      for (int mb = 0; mb < MTH; ++mb) {
-        const int c8 = 4 * mb + (n & 3);
-        const unsigned char* p0 = a0 < RA ? mimg + a0 * IMG_ROW + ((c8 ^ mask_m(a0)) << 3) : zero;
-        const unsigned char* p1 = a1 < RA ? mimg + a1 * IMG_ROW + ((c8 ^ mask_m(a1)) << 3) : zero;
-        PT[mb] = mfma_bf16(cat8(trr(p0), trr(p1)), Cf[ka], PT[mb]);
-      }
+      for (int ka = 0; ka < KF; ++ka)
+        PT[mb] = mfma_bf16(cat8(trr(pl + ka * 32 * IMG_ROW), trr(ph + ka * 32 * IMG_ROW)), C.f[ka], PT[mb]);
+      if (CFrag<MTH>::TAIL) PT[mb] = mfma_tail(trr(mimg + bt + 32 * (mb ^ (mt >> 2))), C.t, PT[mb]);
     }
     if (g.lrow) {
       const int row = sl * g.N + g.lc;
@@ -184,11 +234,30 @@ INA_DEVICE void p_images(const unsigned char* buf, const unsigned char* zero, un
   }
 }
 
-// A = P_g[i = (s,c) = n][k = b], the two 32-deep K-steps
-INA_DEVICE void p_rows(const unsigned char* img, int q, int n, u16x8_t (&Pa)[2]) {
+// A = P_g[i = (s,c) = n][k = b]: the full 32-deep K-steps (ds_read_b128) and the 16-deep tail (ds_read_b64)
+template <int MTH>
+struct PRow {
+  static constexpr int KF = MTH / 2, TAIL = MTH & 1;
+  u16x8_t f[KF > 0 ? KF : 1];
+  s16x4_t t;
+};
+template <int MTH>
+INA_DEVICE void p_rows(const unsigned char* img, int q, int n, PRow<MTH>& P) {
+  const int m = mask_p(n);
+  const unsigned char* row = img + n * IMG_ROW;
 #pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
-    Pa[kb] = *reinterpret_cast<const u16x8_t*>(img + n * IMG_ROW + (((8 * kb + 2 * q) ^ mask_p(n)) << 3));
+  for (int kb = 0; kb < PRow<MTH>::KF; ++kb)
+    P.f[kb] = *reinterpret_cast<const u16x8_t*>(row + (((8 * kb + 2 * q) ^ m) << 3));
+  if (PRow<MTH>::TAIL) P.t = *reinterpret_cast<const s16x4_t*>(row + (((8 * PRow<MTH>::KF + q) ^ m) << 3));
+}
+// T^T[(s,c)][query 16 qt + n] = P_g Q_g^T
+template <int MTH, int QT>
+INA_DEVICE f32x4_t tt(const PRow<MTH>& P, const QFrag<MTH, QT>& Qf, int qt) {
+  f32x4_t T = Z4;
+#pragma unroll
+  for (int kb = 0; kb < PRow<MTH>::KF; ++kb) T = mfma_bf16(P.f[kb], Qf.f[qt][kb], T);
+  if (PRow<MTH>::TAIL) T = mfma_tail(P.t, Qf.t[qt], T);
+  return T;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -209,13 +278,13 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
   constexpr int fo = SG * MTH * 16 * IMG_ROW;   // FC fragments after the M images
   for (int grp = blockIdx.x; grp * NW * g.G < k.E; grp += gridDim.x) {
     const int epw = (grp * NW + wave) * g.G;
-    u16x8_t Cf[2];
-    load_cf(k, g, epw, q, Cf);
-    u16x8_t Qf[GM][QT][2];
+    CFrag<MTH> Cf;
+    load_cf<MTH>(k, g, epw, q, Cf);
+    QFrag<MTH, QT> Qf[GM];
     f32x4_t Lg[GM][QT];
 #pragma unroll
     for (int gi = 0; gi < GM; ++gi) {
-      load_qf<QT>(k, g, epw + gi, gi < g.G && epw + gi < k.E, q, n, Qf[gi]);
+      load_qf<MTH, QT>(k, g, epw + gi, gi < g.G && epw + gi < k.E, q, n, Qf[gi]);
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt) Lg[gi][qt] = Z4;
     }
@@ -228,18 +297,17 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       if (t + 1 < t1) stage_tile(ntn_lds + ((t + 1 - t0) & 1) * k.tpb, tiles + (long)(t + 1) * k.tpb, nfrag);
       const int lt = opaque_lane(), q = lt >> 4, n = lt & 15;
       const Geo g = geo(k, n);
-      p_images<MTH, SG>(buf, zero, ntn_lds + woff, g, Cf, q, n);
+      p_images<MTH, SG>(buf, ntn_lds + woff, g, Cf, q, n);
       wave_order(woff);
       const s16x4_t wt = *reinterpret_cast<const s16x4_t*>(buf + fo + 512 + lt * 8);
 #pragma unroll
       for (int gi = 0; gi < GM; ++gi) {
         if (gi < g.G) {
-          u16x8_t Pa[2];
-          p_rows(ntn_lds + woff + gi * PIMG, q, n, Pa);
+          PRow<MTH> Pa;
+          p_rows<MTH>(ntn_lds + woff + gi * PIMG, q, n, Pa);
 #pragma unroll
           for (int qt = 0; qt < QT; ++qt) {
-            f32x4_t T = mfma_bf16(Pa[0], Qf[gi][qt][0], Z4);
-            T = mfma_bf16(Pa[1], Qf[gi][qt][1], T);   // rows (s, c), cols query
+            const f32x4_t T = tt<MTH, QT>(Pa, Qf[gi], qt);   // rows (s, c), cols query
             Lg[gi][qt] = mfma16_bf16(wt, bf4relu(T), Lg[gi][qt]);
           }
         }
@@ -300,18 +368,21 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
   unsigned short* const dp_trash = dp + ((long)k.E * g.N + 63) / 64 * 64 * hH;   // past the zero pad rows
   for (int grp = blockIdx.x; grp * NW * g.G < k.E; grp += gridDim.x) {
     const int epw = (grp * NW + wave) * g.G;
-    u16x8_t Cf[2];
-    load_cf(k, g, epw, q, Cf);
+    CFrag<MTH> Cf;
+    load_cf<MTH>(k, g, epw, q, Cf);
     if (k.cls_bf && !blockIdx.y && g.lrow && epw + g.lg < k.E) {
+      unsigned short* crow = reinterpret_cast<unsigned short*>(k.cls_bf) + ((long)(epw + g.lg) * g.N + g.lc) * g.H;
 #pragma unroll
-      for (int ka = 0; ka < 2; ++ka) {
+      for (int ka = 0; ka < CFrag<MTH>::KF; ++ka) {
         const int a = 32 * ka + 8 * q;
-        if (a < g.H)
-          *reinterpret_cast<u16x8_t*>(reinterpret_cast<unsigned short*>(k.cls_bf) +
-                                      ((long)(epw + g.lg) * g.N + g.lc) * g.H + a) = Cf[ka];
+        if (a < g.H) *reinterpret_cast<u16x8_t*>(crow + a) = Cf.f[ka];
+      }
+      if (CFrag<MTH>::TAIL) {
+        const int a = 32 * CFrag<MTH>::KF + 4 * q;
+        if (a < g.H) *reinterpret_cast<s16x4_t*>(crow + a) = Cf.t;
       }
     }
-    u16x8_t Qf[GM][QT][2];
+    QFrag<MTH, QT> Qf[GM];
     u16x8_t QB[GM][MTH][KQ];   // A = Q^T[i = b][k = query]
     s16x4_t dzT[GM][QT];       // B[k = c'][col = query] (16x16x16)
     u16x8_t dzB[GM][KQ];       // B[k = query][col = c']
@@ -320,7 +391,7 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
     for (int gi = 0; gi < GM; ++gi) {
       const int ep = epw + gi;
       const bool oke = gi < g.G && ep < k.E;
-      load_qf<QT>(k, g, ep, oke, q, n, Qf[gi]);
+      load_qf<MTH, QT>(k, g, ep, oke, q, n, Qf[gi]);
       const long rq0 = (long)(oke ? ep : 0) * (g.N * k.K + g.NQ) + g.N * k.K;
       const float* dze = k.dz + (long)(oke ? ep : 0) * g.NQ * g.N;
 #pragma unroll
@@ -377,7 +448,7 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         }
         k.dw_slab[((long)grp * k.ntile + t - 1) * dwe + threadIdx.x] = acc;
       }
-      p_images<MTH, SG>(buf, zero, ntn_lds + woff, g, Cf, q, n);
+      p_images<MTH, SG>(buf, ntn_lds + woff, g, Cf, q, n);
       wave_order(woff);
       const s16x4_t wA = *reinterpret_cast<const s16x4_t*>(buf + fo + lt * 8);
       f32x4_t dw = Z4;
@@ -388,20 +459,21 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         unsigned char* pg = ntn_lds + woff + gi * PIMG;
         unsigned char* vimg = ntn_lds + woff + GM * PIMG;
         unsigned char* dtimg = vimg + VIMG;
-        u16x8_t Pa[2];
-        p_rows(pg, q, n, Pa);
-        f32x4_t dT[QT];
+        PRow<MTH> Pa;
+        p_rows<MTH>(pg, q, n, Pa);
+        s16x4_t dT[QT];   // bf16 dT^T: rows (s, c), cols query (the dQ B operand and the dT image)
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
-          f32x4_t T = mfma_bf16(Pa[0], Qf[gi][qt][0], Z4);
-          T = mfma_bf16(Pa[1], Qf[gi][qt][1], T);                 // rows (s, c), cols query
+          const f32x4_t T = tt<MTH, QT>(Pa, Qf[gi], qt);          // rows (s, c), cols query
           const f32x4_t dV = mfma16_bf16(wA, dzT[gi][qt], Z4);   // rows (s, c), cols query
+          f32x4_t d;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dT[qt][r] = T[r] > 0.f ? dV[r] : 0.f;
+          for (int r = 0; r < 4; ++r) d[r] = T[r] > 0.f ? dV[r] : 0.f;
+          dT[qt] = bf4(d);
           // images [query row][(s, c) col]: the lane writes its query row's 4 (s, c) columns
           const int off = voff(16 * qt + n, q);
           *reinterpret_cast<s16x4_t*>(vimg + off) = bf4relu(T);
-          *reinterpret_cast<s16x4_t*>(dtimg + off) = bf4(dT[qt]);
+          *reinterpret_cast<s16x4_t*>(dtimg + off) = dT[qt];
         }
         wave_order(woff);
         pg = ntn_lds + woff + gi * PIMG;
@@ -425,7 +497,7 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
           const int pr = 4 * q + (n >> 2);
           const s16x4_t Pt = trr(pg + pr * IMG_ROW + (((4 * mb + (n & 3)) ^ mask_p(pr)) << 3));
 #pragma unroll
-          for (int qt = 0; qt < QT; ++qt) dQ[gi][mb][qt] = mfma16_bf16(Pt, bf4(dT[qt]), dQ[gi][mb][qt]);
+          for (int qt = 0; qt < QT; ++qt) dQ[gi][mb][qt] = mfma16_bf16(Pt, dT[qt], dQ[gi][mb][qt]);
         }
         // dP^T[b][(s, c)] = sum_q Q^T[b, q] dT[q, (s, c)]
         f32x4_t dPT[MTH];
@@ -456,25 +528,29 @@ __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
       }
       wave_order(woff);
       const unsigned char* const pimg = ntn_lds + woff;
-      // dC^T[a][(g, c)] += sum_b M_s[a, b] D_s[b, (g, c)], stacked over the wave's episodes
+      // dC^T[a][(g, c)] += sum_b M_s[a, b] D_s[b, (g, c)], stacked over the wave's episodes (K over b: full
+      // 32-deep steps + the 16-deep tail, as for P)
 #pragma unroll
       for (int sl = 0; sl < SG; ++sl) {
         const unsigned char* mimg = buf + sl * (RA * IMG_ROW);
-        const int row = sl * g.N + g.lc;
-        u16x8_t Bd[2];
+        const int row = sl * g.N + g.lc, mpr = mask_p(row);
+        const unsigned char* drow = g.lrow ? pimg + g.lg * PIMG + row * IMG_ROW : zero;
+        PRow<MTH> Bd;
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-          Bd[kb] = *reinterpret_cast<const u16x8_t*>(
-              g.lrow ? pimg + g.lg * PIMG + row * IMG_ROW + (((8 * kb + 2 * q) ^ mask_p(row)) << 3) : zero);
+        for (int kb = 0; kb < PRow<MTH>::KF; ++kb)
+          Bd.f[kb] = *reinterpret_cast<const u16x8_t*>(g.lrow ? drow + (((8 * kb + 2 * q) ^ mpr) << 3) : zero);
+        if (PRow<MTH>::TAIL)
+          Bd.t = *reinterpret_cast<const s16x4_t*>(g.lrow ? drow + (((8 * PRow<MTH>::KF + q) ^ mpr) << 3) : zero);
 #pragma unroll
         for (int ma = 0; ma < MTH; ++ma) {
-          const int a = 16 * ma + n;
+          const int a = 16 * ma + n, mma = mask_m(a);
+          const unsigned char* arow = mimg + a * IMG_ROW;
 #pragma unroll
-          for (int kb = 0; kb < 2; ++kb) {
-            const u16x8_t Ma =
-                *reinterpret_cast<const u16x8_t*>(mimg + a * IMG_ROW + (((8 * kb + 2 * q) ^ mask_m(a)) << 3));
-            dC[ma] = mfma_bf16(Ma, Bd[kb], dC[ma]);
-          }
+          for (int kb = 0; kb < PRow<MTH>::KF; ++kb)
+            dC[ma] = mfma_bf16(*reinterpret_cast<const u16x8_t*>(arow + (((8 * kb + 2 * q) ^ mma) << 3)), Bd.f[kb], dC[ma]);
+          if (PRow<MTH>::TAIL)
+            dC[ma] = mfma_tail(*reinterpret_cast<const s16x4_t*>(arow + (((8 * PRow<MTH>::KF + q) ^ mma) << 3)), Bd.t,
+                               dC[ma]);
         }
       }
       {   // this wave's dw tile -> its exchange slot (summed over the workgroup's waves after the barrier)

@@ -194,62 +194,6 @@ def pack_attn_rec(W1: torch.Tensor):
     return We[_on(pi, dev)].to(torch.bfloat16).contiguous(), We[_on(ti, dev)].to(torch.bfloat16).contiguous()
 
 
-def afeat(idx: int, q: int, d: int, U: int) -> int:
-    """Feature of slot idx of lane group q in direction d's wave of the fused attention backward
-    (lstm.hip, lstm_bwd FA): slots [own direction's units ; the other direction's units]."""
-    U4 = U // 4
-    return d * U + 4 * idx + q if idx < U4 else (1 - d) * U + 4 * (idx - U4) + q
-
-
-@lru_cache(maxsize=None)
-def _attn_fuse_idx(U: int):
-    """Flat indices into [W1 [2U, 2U] | 0] for the attention backward fused into lstm_bwd (one pack per
-    direction; the direction's wave holds its own units first):
-      w1f  [2][MT][NKR][64][8]:  A[row j = 16 m + (l & 15)][k slot (l >> 4, jj)] = W1[afeat(8 ks + jj, l >> 4, d)][j]
-      w1ft [2][NTD][NKS2][64][8]: A[row (qr, rr) = l & 15][k slot (l >> 4, jj)] = W1[d U + 4 (4 T + rr) + qr][j]
-                                 (own units only, 4 T + rr < U/4), j = 16 (idx >> 2) + 4 (l >> 4) + (idx & 3),
-                                 idx = 8 ks + jj (dP accumulator order)."""
-    U4, H2 = U // 4, 2 * U
-    NV, MT = 2 * U4, (H2 + 15) // 16
-    NKR, NJ = (NV + 7) // 8, 4 * MT
-    NKS2, NTD = (NJ + 7) // 8, (U4 + 3) // 4
-    Z = H2 * H2
-    p = np.full((2, MT, NKR, 64, 8), Z, dtype=np.int64)
-    t = np.full((2, NTD, NKS2, 64, 8), Z, dtype=np.int64)
-    for d in range(2):
-        for m in range(MT):
-            for ks in range(NKR):
-                for l in range(64):
-                    j = 16 * m + (l & 15)
-                    for jj in range(8):
-                        idx = 8 * ks + jj
-                        if idx < NV and j < H2:
-                            p[d, m, ks, l, jj] = afeat(idx, l >> 4, d, U) * H2 + j
-        for T in range(NTD):
-            for ks in range(NKS2):
-                for l in range(64):
-                    r16 = l & 15
-                    fi = 4 * T + (r16 & 3)
-                    if fi >= U4:
-                        continue
-                    i = d * U + 4 * fi + (r16 >> 2)
-                    for jj in range(8):
-                        idx = 8 * ks + jj
-                        j = 16 * (idx >> 2) + 4 * (l >> 4) + (idx & 3)
-                        if idx < NJ and j < H2:
-                            t[d, T, ks, l, jj] = i * H2 + j
-    return torch.from_numpy(p), torch.from_numpy(t)
-
-
-def pack_attn_fuse(W1: torch.Tensor):
-    """-> (w1f, w1ft) bf16 packs of the attention backward fused into lstm_bwd (see _attn_fuse_idx)."""
-    U = W1.shape[0] // 2
-    pi, ti = _attn_fuse_idx(U)
-    dev = W1.device
-    We = torch.cat([W1.detach().float().reshape(-1), W1.new_zeros(1, dtype=torch.float32)])
-    return We[_on(pi, dev)].to(torch.bfloat16).contiguous(), We[_on(ti, dev)].to(torch.bfloat16).contiguous()
-
-
 # ------------------------------------------------------------------ NTN (bf16 only)
 def ntn_slices_per_tile(N: int) -> int:
     """Slices per NTN tile: the rows (slice, class) of a tile fill one 16-row MFMA operand (csrc/kernels/ntn.hip)."""
@@ -270,8 +214,9 @@ def _ntn_tile_idx(H: int, h: int, N: int, paper: bool):
     """Index tables of the per-step NTN tile pack (csrc/kernels/ntn.hip), element by element:
       mi  [ntile, TE]: (a * H + b) * h + s into M [H, H, h] (-1: zero)
       wi  [ntile, TE]: index into w ([h N, N] reference head, [h, 1] paper head) (-1: zero)
-    M image of slice sl: element (a, b) at sl * RA * 64 + a * 64 + 4 (chunk ^ ((a & 2) << 1 | (a & 8))) + (b & 3),
-    chunk = b >> 2 (8-byte chunks XOR-swizzled by row: conflict-free row and transposed fragment reads).
+    M image of slice sl: element (a, b) at sl * RA * 64 + a * 64 + 4 (chunk ^ mask_m(a)) + (b & 3), chunk = b >> 2,
+    mask_m(a) = {0,0,4,4,8,8,12,12,10,10,14,14,2,2,6,6}[a & 15] (8-byte chunks XOR-swizzled by row: conflict-free
+    row and transposed fragment reads; tools/lds_probe/mimage_search.py).
     W fragment (A[i = (s,c)][k = c'], lane l holds row l & 15, k = 4 (l >> 4) + j) and Wt fragment
     (A[i = c'][k = (s,c)]): row (s_loc, c) = divmod(r, N) of the tile; reference head w[(s N + c)][c'],
     paper head w[s] where c == c'."""
@@ -281,7 +226,8 @@ def _ntn_tile_idx(H: int, h: int, N: int, paper: bool):
     wi = np.full((NT, TE), -1, dtype=np.int64)
     t, sl, a, b = np.meshgrid(np.arange(NT), np.arange(SG), np.arange(RA), np.arange(64), indexing="ij")
     s = t * SG + sl
-    phys = (((b >> 2) ^ (((a & 2) << 1) | (a & 8))) << 2) | (b & 3)
+    mask = (0x6622EEAACC884400 >> (4 * (a & 15))) & 15   # csrc/kernels/ntn.hip mask_m
+    phys = (((b >> 2) ^ mask) << 2) | (b & 3)
     pos = sl * RA * 64 + a * 64 + phys
     ok = (s < h) & (a < H) & (b < H)
     mi[t, pos] = np.where(ok, (a * H + b) * h + s, -1)

@@ -195,55 +195,6 @@ def test_narrow_and_wide_attention_index_helpers_coexist():
     assert HP == 256 and it.numel() == iw.numel() == 256 * 256
 
 
-@pytest.mark.parametrize("U", [8, 20, 32])
-def test_fused_attention_packs(U):
-    """w1f / w1ft (the attention backward fused into lstm_bwd): direction d's wave holds its own units in
-    slots [0, U/4) and the other direction's after them; the dH pack produces only the own units."""
-    from induction_network_on_fewrel_amd.ops.packing import _attn_fuse_idx, afeat
-    rng = np.random.default_rng(200 + U)
-    H2, U4 = 2 * U, U // 4
-    NV, MT = 2 * U4, (H2 + 15) // 16
-    NKR, NJ = (NV + 7) // 8, 4 * MT
-    NKS2, NTD = (NJ + 7) // 8, (U4 + 3) // 4
-    W1 = rng.standard_normal((H2, H2))
-    H = rng.standard_normal((16, H2))
-    dP = rng.standard_normal((16, H2))
-    pi, ti = _attn_fuse_idx(U)
-    A, At = _gather(W1, pi), _gather(W1, ti)
-    P, dH = H @ W1, dP @ W1.T
-    for d in range(2):
-        for m in range(MT):
-            D = np.zeros((16, 16))
-            for ks in range(NKR):
-                B = np.zeros((64, 8))
-                for l in range(64):
-                    for j in range(8):
-                        if 8 * ks + j < NV:
-                            B[l, j] = H[l & 15, afeat(8 * ks + j, l >> 4, d, U)]
-                D += _mfma(A[d, m, ks], B)
-            for row in range(16):
-                if 16 * m + row < H2:
-                    np.testing.assert_allclose(D[row], P[:, 16 * m + row], rtol=1e-10, atol=1e-10)
-        for T in range(NTD):
-            D = np.zeros((16, 16))
-            for ks in range(NKS2):
-                B = np.zeros((64, 8))
-                for l in range(64):
-                    for j in range(8):
-                        idx = 8 * ks + j
-                        jj = 16 * (idx >> 2) + 4 * (l >> 4) + (idx & 3)
-                        if idx < NJ and jj < H2:
-                            B[l, j] = dP[l & 15, jj]
-                D += _mfma(At[d, T, ks], B)
-            for q in range(4):
-                for r in range(4):
-                    m = 4 * T + r
-                    if m < U4:
-                        np.testing.assert_allclose(D[4 * q + r], dH[:, d * U + 4 * m + q], rtol=1e-10, atol=1e-10)
-                    else:
-                        assert np.all(D[4 * q + r] == 0)
-
-
 @pytest.mark.parametrize("H,h,N,paper", [(40, 100, 5, False), (40, 7, 5, True), (64, 9, 10, False), (16, 5, 3, True),
                                          (40, 1, 4, False)])
 def test_ntn_tile_pack_layout(H, h, N, paper):
@@ -263,7 +214,7 @@ def test_ntn_tile_pack_layout(H, h, N, paper):
         for sl in range(SG):
             s = t * SG + sl
             for a in range(RA):
-                mask = ((a & 2) << 1) | (a & 8)
+                mask = (0x6622EEAACC884400 >> (4 * (a & 15))) & 15
                 for b in range(64):
                     v = pk[t, sl * RA * 64 + a * 64 + ((((b >> 2) ^ mask) << 2) | (b & 3))]
                     ref = Mb[a, b, s] if (s < h and a < H and b < H) else 0.0
