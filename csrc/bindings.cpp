@@ -15,10 +15,6 @@
 
 #include "ina_launch.h"
 
-#ifndef INA_POS_LDS_DEFAULT
-#define INA_POS_LDS_DEFAULT false
-#endif
-
 namespace {
 
 using at::Tensor;
@@ -64,11 +60,6 @@ const int* ragged_arg(const std::optional<Tensor>& t, int64_t n, const char* nam
 }
 
 int64_t frag_elems(bool bf16) { return bf16 ? 8 : 1; }
-// LDS position-table gradients in lstm_bwd (shifted ids): INA_POS_LDS=0 disables (A/B, tests)
-bool pos_lds_enabled() {
-  const char* v = std::getenv("INA_POS_LDS");
-  return v == nullptr ? INA_POS_LDS_DEFAULT : (v[0] != '0');
-}
 uint32_t keep_threshold(double kp) {
   const double t = kp * 4294967296.0;
   return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
@@ -310,19 +301,12 @@ std::tuple<Tensor, Tensor> rec_attn_bwd(const Tensor& hlane, const Tensor& dmask
   return {dH, slab};
 }
 
-// the self-attention backward fused into lstm_bwd (bf16 record path): packs + the forward's tensors
-struct FaIn {
-  Tensor w1f, w1ft, b1, w2, de, e, alphas;
-  std::optional<Tensor> perm;
-};
-
-static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
+std::tuple<Tensor, Tensor, Tensor> lstm_bwd(
     const Tensor& inst, const Tensor& word, const Tensor& pos1, const Tensor& pos2, const Tensor& wemb,
     const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack, const Tensor& a2pack, const Tensor& bias,
     const Tensor& hraw, const Tensor& cst, const Tensor& dH, const Tensor& dmask, const Tensor& xg, int64_t U, int64_t NX,
     bool bf16, bool word_grad, int64_t blocks, int64_t seed, double keep_prob, bool pos_shift,
-    const std::optional<Tensor>& tlen, const std::optional<Tensor>& slen, const FaIn* fa,
-    const std::optional<Tensor>& wrows = std::nullopt) {
+    const std::optional<Tensor>& tlen, const std::optional<Tensor>& slen, const std::optional<Tensor>& wrows) {
   check(inst, "inst", at::kInt);
   check(word, "word", at::kInt);
   check(pos1, "pos1", at::kInt);
@@ -332,7 +316,7 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
   check(p2emb, "p2emb", at::kFloat);
   check(bias, "bias", at::kFloat);
   if (!bf16) check(cst, "cst", at::kFloat);   // bf16: the cell states are packed into hlane
-  if (!fa) check(dH, "dH", bf16 ? at::kBFloat16 : at::kFloat);
+  check(dH, "dH", bf16 ? at::kBFloat16 : at::kFloat);
   check(apack, "apack", bf16 ? at::kBFloat16 : at::kFloat);
   check(a2pack, "a2pack", bf16 ? at::kBFloat16 : at::kFloat);
   check(hraw, "hraw", bf16 ? at::kBFloat16 : at::kFloat);   // bf16: lstm_fwd's step records
@@ -342,11 +326,10 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
   TORCH_CHECK(DIN <= 4 * NX, "ina.lstm_bwd: input dim too large");
   TORCH_CHECK(hraw.numel() == ((S + 15) / 16) * 2 * L * U4 * 64 * (bf16 ? 2 : 1), "ina.lstm_bwd: hlane shape");
   // dH: natural [S, L, 2U] (attn_bwd) or, bf16, the step-record lane layout [tiles, 2, L, U/4, 64] (rec_attn_bwd)
-  const bool dh_lane = fa ? true : dH.dim() == 5;
-  TORCH_CHECK(fa != nullptr ||
-                  (dh_lane ? (bf16 && dH.size(0) == (S + 15) / 16 && dH.size(1) == 2 && dH.size(2) == L &&
-                              dH.size(3) == U / 4 && dH.size(4) == 64)
-                           : (dH.dim() == 3 && dH.size(0) == S && dH.size(1) == L && dH.size(2) == 2 * U)),
+  const bool dh_lane = dH.dim() == 5;
+  TORCH_CHECK(dh_lane ? (bf16 && dH.size(0) == (S + 15) / 16 && dH.size(1) == 2 && dH.size(2) == L &&
+                         dH.size(3) == U / 4 && dH.size(4) == 64)
+                      : (dH.dim() == 3 && dH.size(0) == S && dH.size(1) == L && dH.size(2) == 2 * U),
               "ina.lstm_bwd: dH shape");
   TORCH_CHECK(bf16 || cst.numel() == ((S + 15) / 16) * 2 * L * U4 * 64, "ina.lstm_bwd: cst shape");
   const bool drop_ = keep_prob < 1.0;
@@ -357,10 +340,6 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
   const int64_t NSLOT = U4 + NX;
   TORCH_CHECK(a2pack.numel() == 2 * ((NSLOT + 3) / 4) * ((4 * U4 + KPL - 1) / KPL) * 64 * KPL, "ina.lstm_bwd: a2pack");
   TORCH_CHECK(ina::lstm_bwd_lds_bytes((int)U, (int)NX, bf16, (int)L, (int)PD) <= 160 * 1024, "ina.lstm_bwd: LDS budget");
-  // shifted position ids on the lean bf16 BPTT: the position-table gradients are summed in LDS inside lstm_bwd
-  const bool pos_lds = bf16 && pos_shift && (dh_lane || fa != nullptr) && pos_lds_enabled();
-  TORCH_CHECK(!pos_lds || ina::lstm_bwd_lds_bytes((int)U, (int)NX, bf16, (int)L, (int)PD, fa != nullptr, true) <= 160 * 1024,
-              "ina.lstm_bwd: LDS budget (position tables)");
   const int64_t ngroups = ((S + 15) / 16 + 3) / 4;
   // 512 workgroups per direction: ~2 rounds of 3-4 tile groups each, back-filled by the dispatcher.
   // (A grid of exactly the resident workgroups, ina::lstm_bwd_resident_blocks, measured slower:
@@ -375,16 +354,14 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
   const int64_t pblocks = std::max<int64_t>(1, std::min<int64_t>(1024, (pitems + 31) / 32));
   if (bf16) TORCH_CHECK(2 * PD <= 16 && 2 * L <= 128, "ina.lstm_bwd: bf16 path needs pos_dim <= 8 and L <= 64");
   // pos_shift (caller-checked pos[s][t] = pos[s][0] + t, pos[s][0] <= L): per-sequence one-hot GEMM -> ONE slab
-  const bool shift = bf16 && pos_shift && (L + 1 + 15) / 16 <= 5 && !pos_lds;
+  const bool shift = bf16 && pos_shift && (L + 1 + 15) / 16 <= 5;
   // (direct x: x_gather wrote only the t = 0 position ids -- the shifted-form reduction's per-sequence offsets)
   TORCH_CHECK(!(bf16 && xg.numel() == ((S + 15) / 16) * L * 16 + 64 * L) || shift,
               "ina.lstm_bwd: direct x needs the shifted-position gradient path");
   auto dpos_slab = shift ? at::empty({1, 1, 2, 2 * L, PD}, opt)
-                         : ((bf16 && !pos_lds) ? at::empty({pblocks, 1, 2, 2 * L, PD}, opt)
-                                               : at::empty({blocks, 2, 2, 2 * L, PD}, opt));
+                         : (bf16 ? at::empty({pblocks, 1, 2, 2 * L, PD}, opt) : at::empty({blocks, 2, 2, 2 * L, PD}, opt));
   // [2 dir][tiles][L][2PD + 1][16] bf16 dx of the pos features (+ a trash row for the other lanes)
-  Tensor dxp = (bf16 && !pos_lds) ? at::empty({2 * (2 * PD + 1) * ntiles * L * 16}, opt.dtype(at::kBFloat16))
-                                  : at::empty({0}, opt);
+  Tensor dxp = bf16 ? at::empty({2 * (2 * PD + 1) * ntiles * L * 16}, opt.dtype(at::kBFloat16)) : at::empty({0}, opt);
   // direct x (lstm_attn_fwd with direct_x): xg holds only the position ids, x comes from the word rows
   const bool direct_x = bf16 && xg.numel() == ntiles * L * 16 + 64 * L;
   if (bf16) {
@@ -395,17 +372,14 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
     TORCH_CHECK(wrows.has_value() && wrows->defined() && wrows->numel() == word.numel() * 8,
                 "ina.lstm_bwd: direct x needs the forward's word rows");
     check(*wrows, "wrows", at::kBFloat16);
-    TORCH_CHECK(fa == nullptr && !pos_lds && dh_lane && NX == 4 && wrows->numel() * 2 < (1LL << 31),
+    TORCH_CHECK(dh_lane && NX == 4 && wrows->numel() * 2 < (1LL << 31),
                 "ina.lstm_bwd: direct x runs in the lean lane-layout BPTT only");
   }
   Tensor dwemb = word_grad ? at::zeros_like(wemb) : at::empty({0}, opt);
-  const int64_t H2 = 2 * U;
-  Tensor aslab = fa ? at::empty({blocks, 2, U * H2 + H2}, opt) : at::empty({0}, opt);
   if (S == 0) {
     dw_slab.zero_();
     dpos_slab.zero_();
-    aslab.zero_();
-    return {dw_slab, dpos_slab, dwemb, aslab};
+    return {dw_slab, dpos_slab, dwemb};
   }
   ina::LstmArgs a{};
   a.inst = inst.data_ptr<int>();
@@ -424,7 +398,7 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
   a.bias = bias.data_ptr<float>();
   a.hraw = hraw.data_ptr();
   a.cst = bf16 ? hraw.data_ptr() : cst.data_ptr();
-  a.dH = fa ? nullptr : dH.data_ptr();
+  a.dH = dH.data_ptr();
   a.dw_slab = dw_slab.data_ptr<float>();
   a.dpos_slab = dpos_slab.data_ptr<float>();
   a.dwemb = word_grad ? dwemb.data_ptr<float>() : nullptr;
@@ -436,42 +410,12 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
   a.thr = keep_threshold(keep_prob);
   a.inv_kp = (float)(1.0 / keep_prob);
   a.drop = keep_prob < 1.0 ? 1 : 0;
-  a.dxp = (bf16 && !pos_lds) ? dxp.data_ptr() : nullptr;
-  a.pos_lds = pos_lds ? 1 : 0;
+  a.dxp = bf16 ? dxp.data_ptr() : nullptr;
   a.dh_lane = dh_lane ? 1 : 0;
   a.tlen = ragged_arg(tlen, ntiles, "tlen");
   a.slen = ragged_arg(slen, S, "slen");
   TORCH_CHECK(!a.tlen || (bf16 && dh_lane), "ina.lstm_bwd: ragged tiles need the bf16 lane-layout dH path");
   TORCH_CHECK(!a.slen || a.tlen, "ina.lstm_bwd: slen needs tlen");
-  if (fa) {
-    TORCH_CHECK(bf16 && (U == 8 || U == 20 || U == 32) && L <= 64, "ina.lstm_attn_bwd: bf16 record path only");
-    check(fa->w1f, "w1f", at::kBFloat16);
-    check(fa->w1ft, "w1ft", at::kBFloat16);
-    check(fa->b1, "b1", at::kFloat);
-    check(fa->w2, "w2", at::kFloat);
-    check(fa->de, "de", at::kFloat);
-    check(fa->e, "e", at::kFloat);
-    check(fa->alphas, "alphas", at::kFloat);
-    const int64_t U4 = U / 4, NV = 2 * U4, MT = (H2 + 15) / 16, NKR = (NV + 7) / 8, NJ = 4 * MT, NKS2 = (NJ + 7) / 8,
-                  NTD = (U4 + 3) / 4;
-    TORCH_CHECK(fa->w1f.numel() == 2 * MT * NKR * 64 * 8 && fa->w1ft.numel() == 2 * NTD * NKS2 * 64 * 8,
-                "ina.lstm_attn_bwd: pack sizes");
-    TORCH_CHECK(fa->b1.numel() == H2 && fa->w2.numel() == H2, "ina.lstm_attn_bwd: b1 / w2 size");
-    TORCH_CHECK(fa->de.size(0) == S && fa->de.size(1) == H2 && fa->e.sizes() == fa->de.sizes() &&
-                    fa->alphas.size(0) == S && fa->alphas.size(1) == L,
-                "ina.lstm_attn_bwd: de / e / alphas shape");
-    TORCH_CHECK(hraw.numel() == ((S + 15) / 16) * 2 * L * 2 * U4 * 64, "ina.lstm_attn_bwd: step records shape");
-    TORCH_CHECK(S * L * 4 < (1LL << 32), "ina.lstm_attn_bwd: alphas too large for a buffer descriptor");
-    a.aw1f = fa->w1f.data_ptr();
-    a.aw1ft = fa->w1ft.data_ptr();
-    a.ab1 = fa->b1.data_ptr<float>();
-    a.aw2 = fa->w2.data_ptr<float>();
-    a.ade = fa->de.data_ptr<float>();
-    a.ae = fa->e.data_ptr<float>();
-    a.aalphas = fa->alphas.data_ptr<float>();
-    a.perm = ragged_arg(fa->perm, S, "perm");
-    a.aslab = aslab.data_ptr<float>();
-  }
   a.xg = (bf16 && !direct_x) ? xg.data_ptr() : nullptr;
   a.posb = bf16 ? reinterpret_cast<const unsigned short*>(xg.data_ptr<at::BFloat16>() + (direct_x ? 0 : ntiles * L * 64 * NX))
                 : nullptr;
@@ -484,40 +428,12 @@ static std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_bwd_impl(
     Tensor gpart = at::empty({(int64_t)ina::pos_shift_workspace_floats((int)S, (int)L, (int)PD, nullptr, nullptr)}, opt);
     check_launch(ina::pos_grad_shift(a, gpart.data_ptr<float>(), dpos_slab.data_ptr<float>(), cur_stream()),
                  "pos_grad_shift");
-  } else if (bf16 && !pos_lds) {
+  } else if (bf16) {
     check_launch(ina::pos_grad(a, (int)pblocks, dpos_slab.data_ptr<float>(), cur_stream()), "pos_grad");
   }
-  return {dw_slab, dpos_slab, dwemb, aslab};
+  return {dw_slab, dpos_slab, dwemb};
 }
 
-std::tuple<Tensor, Tensor, Tensor> lstm_bwd(const Tensor& inst, const Tensor& word, const Tensor& pos1,
-                                            const Tensor& pos2, const Tensor& wemb, const Tensor& p1emb,
-                                            const Tensor& p2emb, const Tensor& apack, const Tensor& a2pack,
-                                            const Tensor& bias, const Tensor& hraw, const Tensor& cst, const Tensor& dH,
-                                            const Tensor& dmask, const Tensor& xg, int64_t U, int64_t NX, bool bf16,
-                                            bool word_grad, int64_t blocks, int64_t seed, double keep_prob,
-                                            bool pos_shift, const std::optional<Tensor>& tlen,
-                                            const std::optional<Tensor>& slen, const std::optional<Tensor>& wrows) {
-  auto r = lstm_bwd_impl(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hraw, cst, dH, dmask, xg, U, NX,
-                         bf16, word_grad, blocks, seed, keep_prob, pos_shift, tlen, slen, nullptr, wrows);
-  return {std::get<0>(r), std::get<1>(r), std::get<2>(r)};
-}
-
-// bf16 encoder backward with the self-attention backward fused into the BPTT (no dH tensor, no
-// rec_attn_bwd pass over the step records) -> (dw_slab, dpos_slab, dwemb, aslab [blocks, 2, U*2U + 2U]:
-// direction d's own dW1 rows [d U, d U + U) | db1 (d = 0) or dw2 (d = 1))
-std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_attn_bwd(
-    const Tensor& inst, const Tensor& word, const Tensor& pos1, const Tensor& pos2, const Tensor& wemb,
-    const Tensor& p1emb, const Tensor& p2emb, const Tensor& apack, const Tensor& a2pack, const Tensor& bias,
-    const Tensor& hraw, const Tensor& dmask, const Tensor& xg, const Tensor& w1f, const Tensor& w1ft, const Tensor& b1,
-    const Tensor& w2, const Tensor& de, const Tensor& e, const Tensor& alphas, int64_t U, int64_t NX, bool word_grad,
-    int64_t blocks, int64_t seed, double keep_prob, bool pos_shift, const std::optional<Tensor>& tlen,
-    const std::optional<Tensor>& slen, const std::optional<Tensor>& perm) {
-  FaIn fa{w1f, w1ft, b1, w2, de, e, alphas, perm};
-  Tensor none = at::empty({0}, wemb.options());
-  return lstm_bwd_impl(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hraw, none, none, dmask, xg, U,
-                       NX, true, word_grad, blocks, seed, keep_prob, pos_shift, tlen, slen, &fa);
-}
 
 // ------------------------------------------------------------------ attention
 
@@ -884,7 +800,6 @@ TORCH_LIBRARY(ina, m) {
   m.def("abi_version", &abi_version);
   m.def("lstm_fwd", &lstm_fwd);
   m.def("lstm_bwd", &lstm_bwd);
-  m.def("lstm_attn_bwd", &lstm_attn_bwd);
   m.def("lstm_attn_fwd", &lstm_attn_fwd);
   m.def("rec_attn_ok", &rec_attn_ok);
   m.def("rec_attn_bwd", &rec_attn_bwd);

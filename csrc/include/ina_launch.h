@@ -46,22 +46,8 @@ struct LstmArgs {
   // lengths; lstm_skip_padding), starts at tlen - 1 and resets each row's state past its own length
   const int* tlen;
   const int* slen;
-  const int* perm;   // x_gather: record row s is original row perm[s] (dropout hash counter); fused bwd: e/de rows
+  const int* perm;   // x_gather: record row s is original row perm[s] (dropout hash counter)
   int wblank;        // bwd with a trained word table: the padding (BLANK) row id, summed in registers (-1: none)
-  // bwd with the self-attention backward fused in (bf16 record path, aslab != nullptr; dH unused):
-  // packs w1f [2][MT][NKR][64][8] / w1ft [2][NTD][NKS2][64][8] (ops/packing.py::_attn_fuse_idx), b1, w2,
-  // de / e [S][2U], alphas [S][L] (original row order) -> aslab [bwd_blocks][2][U*2U + 2U]
-  const void* aw1f;
-  const void* aw1ft;
-  const float* ab1;
-  const float* aw2;
-  const float* ade;
-  const float* ae;
-  const float* aalphas;
-  float* aslab;
-  // bf16 lean BPTT with shifted position ids (pos[s][t] = pos[s][0] + t): the position-table gradients are
-  // summed in LDS inside lstm_bwd -> dpos_slab [bwd_blocks][2 dir][2 tables][2L][PD] (no dxp, no pos_grad)
-  int pos_lds;
   // direct x (bf16 record path, NX == 4, shifted position ids, wrows given): lstm_fwd / lstm_bwd read each
   // token's word features straight from wrows (q-interleaved rows [f0 f4 f1 f5 f2 f6 f3 f7], one dword per
   // lane-step) and its position features from block-resident LDS tables at o_s + t; x_gather then writes
@@ -87,8 +73,7 @@ int pos_grad(const LstmArgs& a, int blocks, float* slab, hipStream_t st);
 size_t pos_shift_workspace_floats(int S, int L, int PD, int* nchunk, int* kps);
 int pos_grad_shift(const LstmArgs& a, float* gpart, float* out, hipStream_t st);
 bool lstm_supported(int U, int NX);
-size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fused_attn = false, bool pos_lds = false,
-                          bool direct_x = false);
+size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool direct_x = false);
 // direct-x position tables in LDS: [4 lane groups q][2 tables][2L rows][4 slots] bf16
 inline size_t xd_table_bytes(int L) { return (size_t)4 * 2 * 2 * L * 4 * 2; }
 

@@ -25,12 +25,6 @@ using namespace ina;
 #ifndef INA_FWD_PIPE
 #define INA_FWD_PIPE 1
 #endif
-#ifndef INA_DG_SHARED
-#define INA_DG_SHARED 1   // lean BPTT gate gradients with shared products (0: the direct formulas, A/B)
-#endif
-#ifndef INA_LSTM_PM
-#define INA_LSTM_PM 1   // 0: timing-only A/B build -- lane-layout dH through the generic step (double-masked)
-#endif
 namespace {
 
 template <int U, int NX, bool BF16>
@@ -157,38 +151,6 @@ INA_DEVICE void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// Self-attention backward fused into the bf16 BPTT (lstm_bwd FA; reference model/layer_module.py:49-98,
-// model/graph.py:36-53).  The direction-d wave recomputes, for each step's PREDECESSOR time tp (one step
-// ahead of the chain: dH_tp does not depend on the BPTT), the attention backward of its 16 sequences:
-//   H_tp = [own h_tp ; other direction's h_tp] (dropped, bf16; lane slots afeat(idx, q, d)),
-//   P = tanh(W1^T H + b1) (MFMA, pack w1f[d]), d(alpha) = de . H, ds = alpha (d(alpha) - de . e),
-//   dP = ds w2 (1 - P^2), dH_own = (W1_own dP + alpha de_own) * keep / keep_prob (MFMA, pack w1ft[d]),
-//   dW1[own rows] += H_own^T dP (16-row LDS images, one v_mfma_f32_16x16x16_bf16 K-step per time step),
-//   db1 += dP (direction 0) / dw2 += ds P (direction 1) in fp32 registers.
-// dH stays in registers: no dH round trip through HBM and no separate pass over the step records
-// (rec_attn_bwd read every h slot and wrote ~0.8 GB of dH per 8192-episode step).
-struct AttnFuse {
-  const u16x8_t* w1f;    // [2][MT][NKR][64]
-  const u16x8_t* w1ft;   // [2][NTD][NKS2][64]
-  const float* b1;
-  const float* w2;
-  const float* de;       // [S][2U] (original row order)
-  const float* e;        // [S][2U] forward output
-  const float* alphas;   // [S][L]
-  const int* perm;       // record row -> original row (ragged tiles) or nullptr
-  float* slab;           // [blocks][2][U 2U + 2U]: own dW1 rows | db1 (dir 0) or dw2 (dir 1)
-};
-template <int U>
-struct FAS {
-  static constexpr int U4 = U / 4, H2 = 2 * U, NV = 2 * U4, NKR = (NV + 7) / 8, MT = (H2 + 15) / 16;
-  static constexpr int NJ = 4 * MT, NKS2 = (NJ + 7) / 8, NTD = (U4 + 3) / 4;
-  static constexpr int NVPO = (U4 + 1) & ~1;            // own H image columns per lane group (even)
-  static constexpr int HTA = (4 * NVPO + 15) / 16;      // dW1 row tiles
-  static constexpr int HCPA = HTA * 16 + 4, JCPA = MT * 16 + 4;
-  static constexpr int NAP = MT * NKR * 64, NAPT = NTD * NKS2 * 64;
-  static constexpr int IMG = 16 * (HCPA + JCPA) * 2;    // bytes of a wave's two images
-  static constexpr int NSA = U * H2 + H2;               // slab floats per (block, dir)
-};
 
 }  // namespace
 
@@ -782,12 +744,9 @@ __global__ __launch_bounds__(256) void h_natural_kernel(const unsigned short* __
 // [tiles][2][L][U4][64] (rec_attn_bwd: coalesced 128-B rows per (step, m))
 // 2 waves/SIMD where the register set fits in 256 without spilling (the default u=20 / 5-d words
 // case); the wider instantiations keep 1 wave and no spills
-#ifndef INA_FA_WAVES
-#define INA_FA_WAVES 2   // fused attention backward: waves per SIMD (2 spills ~100 dwords at u = 20; 1 does not)
-#endif
-template <int U, int NX, bool FA = false>
+template <int U, int NX>
 struct BwdWaves {
-  static constexpr int value = (U <= 20 && NX == 4) ? (FA ? INA_FA_WAVES : 2) : 1;
+  static constexpr int value = (U <= 20 && NX == 4) ? 2 : 1;
 };
 // WG: trained word table (word-row gradients by global atomics).  A template flag rather than a
 // runtime branch: the join after a skipped atomic block made LLVM drain every outstanding load
@@ -795,15 +754,12 @@ struct BwdWaves {
 // PM (bf16 only): dH arrives in the step-record lane layout ALREADY multiplied by the DropoutWrapper
 // scale (rec_attn_bwd), and the BPTT runs the lean step below (raw bf16 operands, no keep bits, no
 // per-lane validity selects, uniform per-step addresses).
-// FA (with PM): the attention backward runs inside the BPTT (AttnFuse above); dH is not an input.
-// PL (with PM): position ids are shifted aranges (pos[s][t] = o_s + t, host-checked): each wave adds its
-// pos-feature gradients into its own LDS copy of the two position tables (ds_add_f32 at o_s + t), summed
-// over the workgroup's waves in a fixed order into dpos_slab [blocks][2 dir][2 tables][2L][PD] -- no
-// per-token dx rows in HBM and no separate reduction kernel.
-// XD (with PM, not FA / PL): direct x -- word features from the word rows, position features from LDS
+// (The attention backward fused into this kernel and per-wave LDS position tables were built and measured
+// slower -- profiles/r4_fused_attn, README "negative results"; removed.)
+// XD (with PM): direct x -- word features from the word rows, position features from LDS
 // tables (see xd_build); no xg record.
-template <int U, int NX, bool BF16, bool WG = false, bool PM = false, bool FA = false, bool PL = false, bool XD = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U, NX, FA>::value))) void lstm_bwd_kernel(
+template <int U, int NX, bool BF16, bool WG = false, bool PM = false, bool XD = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U, NX>::value))) void lstm_bwd_kernel(
     const int* __restrict__ inst, int S, const int* __restrict__ word, const int* __restrict__ pos1,
     const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
     const float* __restrict__ p1emb, const float* __restrict__ p2emb, int PD,
@@ -813,11 +769,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
     float* __restrict__ dw_slab,
     float* __restrict__ dpos_slab, float* __restrict__ dwemb, const unsigned char* __restrict__ dmask, uint32_t seed,
     uint32_t thr, float inv_kp, int drop, unsigned short* __restrict__ dxp, const unsigned short* __restrict__ xg,
-    int dh_lane, const int* __restrict__ tlen, const int* __restrict__ slen, int wblank, AttnFuse af,
+    int dh_lane, const int* __restrict__ tlen, const int* __restrict__ slen, int wblank,
     const unsigned short* __restrict__ wrows, uint32_t wbytes) {
-  static_assert(!FA || (BF16 && PM), "the fused attention backward runs in the lean bf16 BPTT");
-  static_assert(!PL || (BF16 && PM), "LDS position-table gradients run in the lean bf16 BPTT");
-  static_assert(!XD || (BF16 && PM && !FA && !PL && NX == 4), "direct x runs in the lean bf16 BPTT (4 x slots)");
+  static_assert(!XD || (BF16 && PM && NX == 4), "direct x runs in the lean bf16 BPTT (4 x slots)");
   using Sh = Shape<U, NX, BF16>;
   using frag = typename FragT<BF16>::type;
   using elem = typename FragT<BF16>::elem;
@@ -854,8 +808,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   // +4 elements: row stride != 0 mod 32 banks.  (A bank-model stride for the dG image, 92 at GT 5, halves
   // its modelled transposed-read conflicts but measured neutral, 1420 vs 1413 us.)
   constexpr int GCP = GT * 16 + 4, FCP = FTA * 16 + 4;
-  // per-wave staging region (elements): FA packs the bf16 images at their exact size (LDS for the attention)
-  constexpr int WSTRIDE = FA ? 32 * (GCP + FCP) : XROWS * RS;
+  constexpr int WSTRIDE = XROWS * RS;   // per-wave staging region (elements)
   elem* xp_all = reinterpret_cast<elem*>(smem + off);
   elem* dgT = xp_all + (size_t)wave * WSTRIDE;
   elem* xhT = dgT + GT * 16 * RS;
@@ -869,47 +822,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   unsigned short* dgI = reinterpret_cast<unsigned short*>(dgT);
   unsigned short* xhI = dgI + 32 * GCP;
   const int tcol = 4 * (n & 3);
-  using FS = FAS<U>;
   {
-    // FA: the bf16 images at their exact size (the region also holds the final reductions)
+    // (the region also holds the final reductions)
     size_t xp = (size_t)4 * WSTRIDE * sizeof(elem);
-    const size_t red = (size_t)G4 * (4 * NX + U + 1) * sizeof(float) + (FA ? (size_t)FS::NSA * 4 + 16 : 0);
+    const size_t red = (size_t)G4 * (4 * NX + U + 1) * sizeof(float);
     off += xp > red ? xp : red;
   }
   off = (off + 15) & ~(size_t)15;
   float* dpos_lds = reinterpret_cast<float*>(smem + off);   // [2 tables][2L][PD]
-  // FA: this direction's attention packs, [b1 | w2], and each wave's 16-row dW1 images [H_own | dP]
-  u16x8_t* lAp = reinterpret_cast<u16x8_t*>(smem + off);
-  u16x8_t* lApt = lAp + FS::NAP;
-  float* lbw = reinterpret_cast<float*>(lApt + FS::NAPT);
-  unsigned short* ahI = reinterpret_cast<unsigned short*>(lbw + 2 * FS::MT * 16) + (size_t)wave * (FS::IMG / 2);
-  unsigned short* apI = ahI + 16 * FS::HCPA;
-  // PL: per-wave position tables [2 tables][2L][PD] + a trash block of 64 per-lane slots (word / padding lanes)
-  const int PLT = 2 * (2 * L) * PD, PLN = PLT + 64;
-  const size_t pl_off = (off + (FA ? (size_t)(FS::NAP + FS::NAPT) * 16 + 2 * FS::MT * 16 * 4 + 4 * (size_t)FS::IMG : 0) +
-                         15) & ~(size_t)15;
-  float* plAll = reinterpret_cast<float*>(smem + pl_off);
-  float* plR = plAll + (size_t)wave * PLN;
-  if constexpr (PL)
-    for (int i = lane; i < PLN; i += 64) plR[i] = 0.f;
   // XD: the block's direct-x position tables (lstm_bwd_lds_bytes mirrors this offset)
-  char* xdT = reinterpret_cast<char*>(smem) + ((pl_off + (PL ? (size_t)4 * PLN * 4 : 0) + 15) & ~(size_t)15);
+  char* xdT = reinterpret_cast<char*>(smem) + ((off + 15) & ~(size_t)15);
   if constexpr (XD) xd_copy(xdT, xg, L);   // (xg = x_gather's global copy of the tables)
-  if constexpr (FA) {
-    for (int i = threadIdx.x; i < FS::NAP; i += 256) lAp[i] = af.w1f[(size_t)dir * FS::NAP + i];
-    for (int i = threadIdx.x; i < FS::NAPT; i += 256) lApt[i] = af.w1ft[(size_t)dir * FS::NAPT + i];
-    for (int i = threadIdx.x; i < FS::MT * 16; i += 256) {
-      lbw[i] = i < FS::H2 ? af.b1[i] : 0.f;
-      lbw[FS::MT * 16 + i] = i < FS::H2 ? af.w2[i] : 0.f;
-    }
-    // pad columns of the images are never written and must read as zero
-    for (int i = lane; i < FS::IMG / 4; i += 64) reinterpret_cast<uint32_t*>(ahI)[i] = 0u;
-  }
   // gate packs / biases pre-scaled as in the forward (fragment index i -> lane i & 63, gate i & 3);
   // the transposed pack (d[x;h] = W dG) keeps the true weights
   for (int i = threadIdx.x; i < NA; i += 256) lA[i] = fscale(apack[(size_t)dir * NA + i], gate_scale(i & 3));
   for (int i = threadIdx.x; i < NA2; i += 256) lA2[i] = a2pack[(size_t)dir * NA2 + i];
-  // [unit][gate] (16-byte rows: the FA step re-reads a unit's four biases with one ds_read_b128)
+  // [unit][gate]
   for (int i = threadIdx.x; i < 4 * U; i += 256) lbias[(i % U) * 4 + i / U] = gate_bias(bias[dir * 4 * U + i], i / U);
   if constexpr (!BF16)
     for (int i = threadIdx.x; i < 2 * P2 * PD; i += 256) dpos_lds[i] = 0.f;
@@ -934,18 +862,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   for (int a = 0; a < GT; ++a)
 #pragma unroll
     for (int b = 0; b < FTA; ++b) accw[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  // FA accumulators: dW1 own rows (image column tiles x projection tiles), db1 (dir 0) / sum ds rr (dir 1)
-  f32x4_t accA[FS::HTA][FS::MT];
-  float a12[FS::MT][4], asds = 0.f;
-  const bool adir = dir != 0;
-#pragma unroll
-  for (int a = 0; a < FS::HTA; ++a)
-#pragma unroll
-    for (int b = 0; b < FS::MT; ++b) accA[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int m = 0; m < FS::MT; ++m)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) a12[m][r] = 0.f;
 
   XSrc xs[NX];
 #pragma unroll
@@ -1204,52 +1120,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       const uint32_t xvm = valid ? 0xFFFFFFFFu : 0u;   // padding sequences: x = 0
       const auto rdx = rsrc(dxp + ((size_t)dir * ntiles + tu) * L * (NPF + 1) * 16, (uint32_t)L * PSTEPB);
       const int vl2 = lane * 2, vx = lane * NX * 2;
-      // ---- PL: the lane's position-table slot at t = 0 per x feature (shifted ids: pos = o + t); word /
-      // padding features and padding rows go to the trash block
-      // (a shared trash address made every instruction a ~25-way same-address LDS atomic: each lane has its
-      // own trash slot, and plm = 0 keeps it fixed over the steps)
-      int plb[NX], plm[NX];
-      if constexpr (PL) {
-        const int o1 = pos1[rowbase], o2 = pos2[rowbase];
-#pragma unroll
-        for (int xi = 0; xi < NX; ++xi) {
-          const int sel = xs[xi].sel;
-          const bool pos = valid && (sel == 1 || sel == 2);
-          plb[xi] = pos ? (sel == 1 ? o1 : 2 * L + o2) * PD + xs[xi].col : PLT + lane;
-          plm[xi] = pos ? 1 : 0;
-        }
-      }
-      // ---- FA: per-tile attention state (de of the lane's slots, sd = de . e) and buffer descriptors
-      const int orow = FA ? (af.perm ? af.perm[seqc] : (int)seqc) : 0;   // e / de / alphas row
-      float dev[FS::NV];   // de of slots [own ; other] (0 for padding rows)
-      float asd = 0.f;
-      if constexpr (FA) {
-#pragma unroll
-        for (int i = 0; i < FS::NV; ++i) {
-          const int f = i < U4 ? dir * U + 4 * i + q : (1 - dir) * U + 4 * (i - U4) + q;
-          const size_t o = (size_t)orow * FS::H2 + f;
-          const float x = valid ? af.de[o] : 0.f;
-          dev[i] = x;
-          asd = fmaf(x, af.e[o], asd);   // same sequential order as d(alpha) below
-        }
-        asd = cross_group_sum(asd);
-      }
-      // the other direction's step records: the descriptor ends at the tile's last valid step (the
-      // forward direction never wrote later ones; alpha is 0 there, loads past the range return 0)
-      const auto rorec = rsrc(reinterpret_cast<const unsigned short*>(hraw) + ((size_t)tu * 2 + (1 - dir)) * L * 2 * U4 * 64,
-                              (uint32_t)Lt * RSTEPB);
-      // keep bytes of both directions (without dropout: any readable bytes, every bit then set by akor)
-      const auto rkb = drop ? rsrc(dmask + (size_t)tu * 2 * L * 64, (uint32_t)(2 * L * 64)) : rrec;
-      const uint32_t akor = drop ? 0u : 0xFFFFu;
-      const int vko = drop ? dir * L * 64 + lane : 0, vkt = drop ? (1 - dir) * L * 64 + lane : 0;
-      const auto ral = rsrc(af.alphas, (uint32_t)((size_t)S * L * 4));
-      const int val = orow * L * 4;
       constexpr int NXW = NX / 2;   // x words (2 features each) per lane and step
       struct Raw {
         uint32_t h[U4], c[U4], d[U4];   // 16-bit loads (upper halves never read)
         uint32_t x[NXW];
         uint64_t pa, pb;                // XD: position-table entries (x[0] = the word dword until bstep)
-        uint32_t oh[U4], ko, kt, al;    // FA: other direction's h, keep bytes, alpha of the predecessor time
       };
       auto rload = [&](int tau, Raw& o) __attribute__((always_inline)) {
         const int tn = tof(tau), tp = tof(tau >= 1 ? tau - 1 : 0);
@@ -1258,15 +1133,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         for (int m = 0; m < U4; ++m) {
           o.h[m] = __builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + m * 128, sr, 0);
           o.c[m] = __builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + (U4 + m) * 128, sr, 0);
-          if constexpr (FA)
-            o.oh[m] = __builtin_amdgcn_raw_buffer_load_b16(rorec, vl2 + m * 128, sr, 0);
-          else
-            o.d[m] = __builtin_amdgcn_raw_buffer_load_b16(rdh, vl2 + m * 128, sd, 0);
-        }
-        if constexpr (FA) {
-          o.ko = __builtin_amdgcn_raw_buffer_load_b8(rkb, vko, tp * 64, 0);
-          o.kt = __builtin_amdgcn_raw_buffer_load_b8(rkb, vkt, tp * 64, 0);
-          o.al = __builtin_amdgcn_raw_buffer_load_b32(ral, val, tp * 4, 0);
+          o.d[m] = __builtin_amdgcn_raw_buffer_load_b16(rdh, vl2 + m * 128, sd, 0);
         }
         if constexpr (XD) {
           o.x[0] = __builtin_amdgcn_raw_buffer_load_b32(rx, wvo, tn * 16, 0);
@@ -1289,116 +1156,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       // HASP: the step has a predecessor state (else it is zero: the direction's first step in time, or the
       // SKIP backward direction's tile start).  HI: the step stages into image rows 16..31 and completes
       // the pair (rows 0..15 = the previous step), FLUSH: the pair goes into dW after staging.
-      // ---- FA: the attention backward at time tp from its raw inputs -> dha (dH_tp of the own units, the
-      // DropoutWrapper scale applied) and the dW1 image words (own dropped H, dP in accumulator order)
-      float dha[U4];
-#pragma unroll
-      for (int m = 0; m < U4; ++m) dha[m] = 0.f;
-      auto att_math = [&](const uint32_t* ownh, const uint32_t* othh, uint32_t ko, uint32_t kt, uint32_t alraw,
-                          uint32_t* hwo, u16x8_t* B2) __attribute__((always_inline)) {
-        const float alv = valid ? __builtin_bit_cast(float, alraw) : 0.f;
-        const uint32_t kb = (ko | (kt << 8)) | akor;   // bit m: own slot m, bit 8 + m: other slot m
-        auto sc = [&](int i) {
-          const int b = i < U4 ? i : 8 + i - U4;
-          return (float)((kb >> b) & 1u) * inv_kp;
-        };
-        uint32_t bw[FS::NKR * 4];
-#pragma unroll
-        for (int w = 0; w < FS::NKR * 4; ++w) bw[w] = 0u;
-        float d = 0.f;
-#pragma unroll
-        for (int i = 0; i < FS::NV; i += 2) {
-          const uint32_t h0 = i < U4 ? ownh[i] : othh[i - U4];
-          const uint32_t h1 = i + 1 < U4 ? ownh[i + 1] : othh[i + 1 - U4];
-          const float x0 = bf2f((unsigned short)h0) * sc(i), x1 = bf2f((unsigned short)h1) * sc(i + 1);
-          const uint32_t w = (uint32_t)f2bf(x0) | ((uint32_t)f2bf(x1) << 16);
-          bw[i / 2] = w;
-          d = fmaf(dev[i], __builtin_bit_cast(float, w << 16), d);
-          d = fmaf(dev[i + 1], __builtin_bit_cast(float, w & 0xFFFF0000u), d);
-        }
-#pragma unroll
-        for (int w = 0; w < FS::NVPO / 2; ++w) hwo[w] = (2 * w + 1 < U4) ? bw[w] : (bw[w] & 0xFFFFu);
-        const float ds = alv * (cross_group_sum(d) - asd);   // 0 for padding rows (alpha 0)
-        const float ds4 = 4.f * ds;
-        asds += ds;
-        float dp[FS::MT][4];
-#pragma unroll
-        for (int m = 0; m < FS::MT; ++m) {
-          f32x4_t acc;
-          float wv[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            acc[r] = lbw[16 * m + 4 * q + r];
-            wv[r] = lbw[FS::MT * 16 + 16 * m + 4 * q + r];
-          }
-#pragma unroll
-          for (int ks = 0; ks < FS::NKR; ++ks)
-            acc = mfma_bf16(lAp[(m * FS::NKR + ks) * 64 + lane],
-                            __builtin_bit_cast(u16x8_t, u32x4_t{bw[4 * ks], bw[4 * ks + 1], bw[4 * ks + 2], bw[4 * ks + 3]}),
-                            acc);
-          const f32x4_t r4 = tanh_r4(acc);   // P = 1 - 2 rr, 1 - P^2 = 4 rr (1 - rr)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float rr = r4[r];
-            dp[m][r] = ds4 * (wv[r] * (rr - rr * rr));
-            a12[m][r] += adir ? ds * rr : dp[m][r];   // dw2 = sum ds P = sum ds - 2 sum ds rr (dir 1); db1 (dir 0)
-          }
-        }
-#pragma unroll
-        for (int ks = 0; ks < FS::NKS2; ++ks) {
-          B2[ks] = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int idx = ks * 8 + j;
-            if (idx < FS::NJ) B2[ks][j] = f2bf(dp[idx >> 2][idx & 3]);
-          }
-        }
-#pragma unroll
-        for (int T = 0; T < FS::NTD; ++T) {
-          f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int ks = 0; ks < FS::NKS2; ++ks) acc = mfma_bf16(lApt[(T * FS::NKS2 + ks) * 64 + lane], B2[ks], acc);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = 4 * T + r;
-            if (m < U4) dha[m] = (acc[r] + alv * dev[m]) * sc(m);
-          }
-        }
-      };
-      // own H / dP into the wave's 16-row images (row = sequence n); the flush contracts the 16 sequences
-      auto att_stage = [&](const uint32_t* hwo, const u16x8_t* B2) __attribute__((always_inline)) {
-        uint32_t* hi = reinterpret_cast<uint32_t*>(ahI + n * FS::HCPA + q * FS::NVPO);
-#pragma unroll
-        for (int w = 0; w < FS::NVPO / 2; ++w) hi[w] = hwo[w];
-        unsigned short* pr = apI + n * FS::JCPA + q * FS::NJ;
-#pragma unroll
-        for (int c = 0; c < FS::NJ / 4; ++c) {
-          const u16x8_t& b = B2[c / 2];
-          const int o = 4 * (c & 1);
-          *reinterpret_cast<u16x4_t*>(pr + 4 * c) = u16x4_t{b[o], b[o + 1], b[o + 2], b[o + 3]};
-        }
-      };
-      auto att_flush = [&]() __attribute__((always_inline)) {
-        s16x4_t fa[FS::HTA], fb[FS::MT];
-#pragma unroll
-        for (int a = 0; a < FS::HTA; ++a) fa[a] = tr_read(ahI + (4 * q + (n >> 2)) * FS::HCPA + 16 * a + 4 * (n & 3));
-#pragma unroll
-        for (int b = 0; b < FS::MT; ++b) fb[b] = tr_read(apI + (4 * q + (n >> 2)) * FS::JCPA + 16 * b + 4 * (n & 3));
-#pragma unroll
-        for (int a = 0; a < FS::HTA; ++a)
-#pragma unroll
-          for (int b = 0; b < FS::MT; ++b) accA[a][b] = mfma16_bf16(fa[a], fb[b], accA[a][b]);
-      };
       auto bstep = [&](auto hasp_c, auto hi_c, auto flush_c, const int tau, const Raw& X0) __attribute__((always_inline)) {
         constexpr bool HASP = decltype(hasp_c)::value, ODD = decltype(hi_c)::value, FLUSH = decltype(flush_c)::value;
         Raw X = X0;
 #pragma unroll
         for (int m = 0; m < U4; ++m) {
-          asm volatile("" : "+v"(X.h[m]), "+v"(X.c[m]));
-          if constexpr (FA) asm volatile("" : "+v"(X.oh[m]));
-          else asm volatile("" : "+v"(X.d[m]));
+          asm volatile("" : "+v"(X.h[m]), "+v"(X.c[m]), "+v"(X.d[m]));
         }
-        if constexpr (FA) asm volatile("" : "+v"(X.ko), "+v"(X.kt), "+v"(X.al));
         if constexpr (XD) {   // word dword | the two table entries (disjoint nonzero slots)
           asm volatile("" : "+v"(X.x[0]), "+v"(X.pa), "+v"(X.pb));
           X.x[0] = (X.x[0] | (uint32_t)X.pa | (uint32_t)X.pb) & xvm;
@@ -1440,25 +1204,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
 #pragma unroll
         for (int m = 0; m < U4; ++m) {
           cprev[m] = HASP ? (float)__builtin_bit_cast(_Float16, (unsigned short)X.c[m]) : 0.f;
-          dhin[m] = FA ? dha[m] : __builtin_bit_cast(float, X.d[m] << 16);
-        }
-        // FA: the attention backward of the predecessor time (the next step's dH), off the BPTT chain
-        uint32_t ahw[FS::NVPO / 2];
-        u16x8_t aB2[FS::NKS2];
-        if constexpr (FA && HASP) {
-          att_math(X.h, X.oh, X.ko, X.kt, X.al, ahw, aB2);
-          __builtin_amdgcn_sched_barrier(0);   // the attention's temporaries die before the BPTT's are born
+          dhin[m] = __builtin_bit_cast(float, X.d[m] << 16);
         }
         // ---- recompute gates
         float dg[U4][4];
-        if constexpr (FA) asm volatile("" ::: "memory");   // FA: biases re-read from LDS per step (registers)
 #pragma unroll
         for (int m = 0; m < NMT; ++m) {
           f32x4_t acc = {bm[m][0], bm[m][1], bm[m][2], bm[m][3]};
-          if constexpr (FA) {
-            const float4 b4 = *reinterpret_cast<const float4*>(lbias + (4 * m + q) * 4);
-            acc = f32x4_t{b4.x, b4.y, b4.z, b4.w};
-          }
 #pragma unroll
           for (int ks = 0; ks < NKS; ++ks)
             acc = mma(lA[(m * NKS + ks) * 64 + lane],
@@ -1466,7 +1218,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
           const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
           const float tc = tanh_l2(ccur[m] * (2.f * LOG2E_F));
           const float dh = dh_rec[m] + dhin[m];
-#if INA_DG_SHARED
           // (shared products: the step is VALU-issue bound -- README "ISA budget"; 14 instead of 16 ops per unit)
           const float dho = dh * og;
           const float dc = fmaf(dho, fmaf(-tc, tc, 1.f), dc_rec[m]);
@@ -1477,14 +1228,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
           dg[m][2] = dc * cprev[m] * fmaf(-fg, fg, fg);
           const float dot = dho * tc;
           dg[m][3] = fmaf(-dot, og, dot);              // dh tc og (1 - og)
-#else
-          const float dc = dc_rec[m] + dh * og * (1.f - tc * tc);
-          dc_rec[m] = dc * fg;
-          dg[m][0] = dc * jg * (ig - ig * ig);
-          dg[m][1] = dc * ig * (1.f - jg * jg);
-          dg[m][2] = dc * cprev[m] * (fg - fg * fg);
-          dg[m][3] = dh * tc * (og - og * og);
-#endif
           ccur[m] = cprev[m];
         }
         uint32_t dgw[2 * U4];   // packed bf16 dG pairs: the W dG operand and the dW image row
@@ -1519,13 +1262,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
             dc_rec[m] *= k;
           }
         }
-        if constexpr (PL) {   // pos-feature gradients into the wave's LDS position tables (fp32)
-          const int tp = t * PD;
-#pragma unroll
-          for (int xi = 0; xi < NX; ++xi)
-            __hip_atomic_fetch_add(plR + plb[xi] + plm[xi] * tp, dslot[U4 + xi], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {   // pos-feature gradients -> dxp rows (word / padding features: the trash row)
+        {   // pos-feature gradients -> dxp rows (word / padding features: the trash row)
           const int sp = t * PSTEPB;
 #pragma unroll
           for (int xi = 0; xi < NX; xi += 2) {
@@ -1553,12 +1290,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         uint32_t* xi32 = reinterpret_cast<uint32_t*>(xhI + (RR + n) * FCP + q * NSLP);
 #pragma unroll
         for (int w = 0; w < NSLP / 2; ++w) xi32[w] = w < NW ? bw[w] : 0u;
-        if constexpr (FA && HASP) {   // attention dW1: every step (16-row images)
-          att_stage(ahw, aB2);
-          lds_order();
-          att_flush();
-          if constexpr (!FLUSH) lds_order();
-        }
         if constexpr (FLUSH) {
           lds_order();
           auto tr8 = [&](const unsigned short* img, int stride, int c0) {
@@ -1589,7 +1320,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       const int nst = tau_start - tau_end + 1;
       // dxp rows of the steps not processed: zero (the pos-gradient reduction reads every step)
       for (int t = Lt; t < L; ++t) {
-        if (PL || (dir == 1 && slen == nullptr)) break;
+        if (dir == 1 && slen == nullptr) break;
 #pragma unroll
         for (int xi = 0; xi < NX; ++xi)
           __builtin_amdgcn_raw_buffer_store_b16((unsigned short)0, rdx, 2 * pofs[xi], t * PSTEPB, 0);
@@ -1598,25 +1329,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
       for (int m = 0; m < U4; ++m)   // c of the first processed step
         ccur[m] = (float)__builtin_bit_cast(
             _Float16, (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + (U4 + m) * 128, tof(tau_start) * RSTEPB, 0));
-      if constexpr (FA) {   // the attention backward of the first processed time (later ones run one step ahead)
-        const int t0 = tof(tau_start), s0 = t0 * RSTEPB;
-        uint32_t h0[U4], o0[U4];
-#pragma unroll
-        for (int m = 0; m < U4; ++m) {
-          h0[m] = __builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + m * 128, s0, 0);
-          o0[m] = __builtin_amdgcn_raw_buffer_load_b16(rorec, vl2 + m * 128, s0, 0);
-        }
-        const uint32_t k0 = __builtin_amdgcn_raw_buffer_load_b8(rkb, vko, t0 * 64, 0);
-        const uint32_t k1 = __builtin_amdgcn_raw_buffer_load_b8(rkb, vkt, t0 * 64, 0);
-        const uint32_t a0 = __builtin_amdgcn_raw_buffer_load_b32(ral, val, t0 * 4, 0);
-        uint32_t ahw[FS::NVPO / 2];
-        u16x8_t aB2[FS::NKS2];
-        att_math(h0, o0, k0, k1, a0, ahw, aB2);
-        att_stage(ahw, aB2);
-        lds_order();
-        att_flush();
-        lds_order();
-      }
       Raw A, B;
       rload(tau_start, A);
       int k = 0;   // processed steps so far: pairs (k, k + 1) -> image rows 0..15 / 16..31
@@ -1788,28 +1500,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   float* red = reinterpret_cast<float*>(xp_all);
   const int REDN = G4 * NF;
   for (int i = threadIdx.x; i < REDN; i += 256) red[i] = 0.f;
-  float* ared = red + ((REDN + 3) & ~3);   // FA: [U own rows][2U] dW1 | [2U] db1 (dir 0) or dw2 (dir 1)
-  if constexpr (FA)
-    for (int i = threadIdx.x; i < FS::NSA; i += 256) ared[i] = 0.f;
   __syncthreads();
-  float a1s[FS::MT][4];   // cross-lane sums first (every lane takes part in the shuffles)
-  int ajmap[FS::MT];
-  if constexpr (FA) {
-    const float sdsum = group16_sum(asds);
-#pragma unroll
-    for (int m = 0; m < FS::MT; ++m)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float s = group16_sum(a12[m][r]);
-        a1s[m][r] = adir ? sdsum - 2.f * s : s;
-      }
-#pragma unroll
-    for (int b = 0; b < FS::MT; ++b) {   // dP image column -> projection row j
-      const int c = 16 * b + n, qq = c / FS::NJ, idx = c % FS::NJ;
-      const int j = 16 * (idx >> 2) + 4 * qq + (idx & 3);
-      ajmap[b] = (qq < 4 && j < FS::H2) ? j : -1;
-    }
-  }
   // bf16: un-permute the image columns (dG column c -> gate row, XH column -> feature; -1 = pad)
   int fmap[FTA];
 #pragma unroll
@@ -1842,38 +1533,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         for (int b = 0; b < FTA; ++b)
           if (fmap[b] >= 0) red[gc * NF + fmap[b]] += accw[a][b][r];
       }
-    if constexpr (FA) {
-#pragma unroll
-      for (int a = 0; a < FS::HTA; ++a)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = 16 * a + 4 * q + r, qq = c / FS::NVPO, idx = c % FS::NVPO;
-          if (qq >= 4 || idx >= U4) continue;
-          const int row = (4 * idx + qq) * FS::H2;   // own unit 4 idx + qq
-#pragma unroll
-          for (int b = 0; b < FS::MT; ++b)
-            if (ajmap[b] >= 0) ared[row + ajmap[b]] += accA[a][b][r];
-        }
-#pragma unroll
-      for (int m = 0; m < FS::MT; ++m)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = 16 * m + 4 * q + r;
-          if (n == 0 && j < FS::H2) ared[U * FS::H2 + j] += a1s[m][r];
-        }
-    }
   });
   float* slab = dw_slab + ((size_t)blockIdx.x * 2 + dir) * REDN;
   for (int i = threadIdx.x; i < REDN; i += 256) slab[i] = red[i];
-  if constexpr (PL) {   // the 4 waves' position tables, summed in a fixed order (barriers above)
-    float* ps = dpos_slab + ((size_t)blockIdx.x * 2 + dir) * PLT;
-    for (int i = threadIdx.x; i < PLT; i += 256)
-      ps[i] = (plAll[i] + plAll[PLN + i]) + (plAll[2 * PLN + i] + plAll[3 * PLN + i]);
-  }
-  if constexpr (FA) {
-    float* as = af.slab + ((size_t)blockIdx.x * 2 + dir) * FS::NSA;
-    for (int i = threadIdx.x; i < FS::NSA; i += 256) as[i] = ared[i];
-  }
   if constexpr (!BF16) {
     float* ps = dpos_slab + ((size_t)blockIdx.x * 2 + dir) * 2 * P2 * PD;
     for (int i = threadIdx.x; i < 2 * P2 * PD; i += 256) ps[i] = dpos_lds[i];
@@ -2092,7 +1754,7 @@ namespace ina {
 
 
 // mirrors the kernel's LDS carve (lstm_bwd_kernel)
-size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fa, bool pl, bool xd) {
+size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool xd) {
   const int KPL = bf16 ? 8 : 1;
   const int U4 = U / 4, NSLOT = U4 + NX;
   const int NA = U4 * ((NSLOT + KPL - 1) / KPL) * 64;
@@ -2101,22 +1763,13 @@ size_t lstm_bwd_lds_bytes(int U, int NX, bool bf16, int L, int PD, bool fa, bool
   const int GT = (4 * U + 15) / 16;
   const int FTMAX = (4 * NX + U + 1 + 15) / 16;
   const int RS = bf16 ? 40 : 36;
-  // attention (fa): FAS<U>
-  const int H2 = 2 * U, NV = 2 * U4, NKR = (NV + 7) / 8, MT = (H2 + 15) / 16, NJ = 4 * MT, NKS2 = (NJ + 7) / 8;
-  const int NTD = (U4 + 3) / 4, NVPO = (U4 + 1) & ~1, HTA = (4 * NVPO + 15) / 16;
-  const int HCPA = HTA * 16 + 4, JCPA = MT * 16 + 4, NSA = U * H2 + H2;
   size_t off = (size_t)(NA + NA2) * fragb + 4 * U * 4;
   off = (off + 15) & ~(size_t)15;
-  const int NSLP = (U4 + NX + 1) & ~1, FTA = (4 * NSLP + 1 + 15) / 16;
-  const int GCP = GT * 16 + 4, FCP = FTA * 16 + 4;
-  size_t xp = fa ? (size_t)4 * 32 * (GCP + FCP) * 2 : (size_t)4 * (GT * 16 + FTMAX * 16) * RS * (bf16 ? 2 : 4);
-  const size_t red = (size_t)4 * U * (4 * NX + U + 1) * 4 + (fa ? (size_t)NSA * 4 + 16 : 0);
+  size_t xp = (size_t)4 * (GT * 16 + FTMAX * 16) * RS * (bf16 ? 2 : 4);
+  const size_t red = (size_t)4 * U * (4 * NX + U + 1) * 4;
   off += xp > red ? xp : red;
   off = (off + 15) & ~(size_t)15;
   if (!bf16) off += (size_t)2 * 2 * L * PD * 4;   // block pos tables (bf16 mode: pos_grad_kernel)
-  if (fa) off += (size_t)(MT * NKR * 64 + NTD * NKS2 * 64) * 16 + 2 * MT * 16 * 4 + (size_t)4 * 16 * (HCPA + JCPA) * 2;
-  off = (off + 15) & ~(size_t)15;
-  if (pl) off += (size_t)4 * (2 * 2 * L * PD + 64) * 4;   // per-wave position tables + per-lane trash slots
   if (xd) off = ((off + 15) & ~(size_t)15) + xd_table_bytes(L);   // direct-x position tables
   return off;
 }
@@ -2157,53 +1810,29 @@ static int launch_bwd_t(const LstmArgs& a, hipStream_t st) {
   using frag = typename FragT<BF16>::type;
   using elem = typename FragT<BF16>::elem;
   dim3 grid(a.bwd_blocks, 2);
-  // bf16 + lane-layout dH (rec_attn_bwd, premasked): the lean PM step; fa: the attention backward fused in
-  const bool fa = BF16 && a.aslab != nullptr;
-  const bool pm = INA_LSTM_PM && BF16 && (a.dh_lane || fa);
-  const bool pl = pm && a.pos_lds;
+  // bf16 + lane-layout dH (rec_attn_bwd, premasked): the lean PM step
+  const bool pm = BF16 && a.dh_lane;
   constexpr bool XDC = BF16 && NX == 4;   // the direct-x kernels exist for 4 x slots per lane only
-  const bool xd = XDC && pm && !fa && !pl && a.xd;
+  const bool xd = XDC && pm && a.xd;
   if (a.xd && !xd) return -1;
-  size_t lds = lstm_bwd_lds_bytes(U, NX, BF16, a.L, a.PD, fa, pl, xd);
-  constexpr bool P = BF16;   // the PM / FA / PL kernels exist in bf16 mode only
+  size_t lds = lstm_bwd_lds_bytes(U, NX, BF16, a.L, a.PD, xd);
+  constexpr bool P = BF16;   // the PM / XD kernels exist in bf16 mode only
   auto kfn = pm ? (a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, P> : lstm_bwd_kernel<U, NX, BF16, false, P>)
                 : (a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, false> : lstm_bwd_kernel<U, NX, BF16, false, false>);
-  if (fa) kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, P, P> : lstm_bwd_kernel<U, NX, BF16, false, P, P>;
-  if (pl && !fa)
-    kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, P, false, P> : lstm_bwd_kernel<U, NX, BF16, false, P, false, P>;
-  if (pl && fa) kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, P, P, P> : lstm_bwd_kernel<U, NX, BF16, false, P, P, P>;
-  if (xd)
-    kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, P, false, false, XDC>
-                  : lstm_bwd_kernel<U, NX, BF16, false, P, false, false, XDC>;
+  if (xd) kfn = a.dwemb ? lstm_bwd_kernel<U, NX, BF16, true, P, XDC> : lstm_bwd_kernel<U, NX, BF16, false, P, XDC>;
   static bool attr_set = false;
   if (!attr_set) {
     for (auto f : {lstm_bwd_kernel<U, NX, BF16, true, false>, lstm_bwd_kernel<U, NX, BF16, false, false>,
                    lstm_bwd_kernel<U, NX, BF16, true, P>, lstm_bwd_kernel<U, NX, BF16, false, P>,
-                   lstm_bwd_kernel<U, NX, BF16, true, P, P>, lstm_bwd_kernel<U, NX, BF16, false, P, P>,
-                   lstm_bwd_kernel<U, NX, BF16, true, P, false, P>, lstm_bwd_kernel<U, NX, BF16, false, P, false, P>,
-                   lstm_bwd_kernel<U, NX, BF16, true, P, P, P>, lstm_bwd_kernel<U, NX, BF16, false, P, P, P>,
-                   lstm_bwd_kernel<U, NX, BF16, true, P, false, false, XDC>,
-                   lstm_bwd_kernel<U, NX, BF16, false, P, false, false, XDC>})
+                   lstm_bwd_kernel<U, NX, BF16, true, P, XDC>, lstm_bwd_kernel<U, NX, BF16, false, P, XDC>})
       hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
-  }
-  AttnFuse af{};
-  if (fa) {
-    af.w1f = (const u16x8_t*)a.aw1f;
-    af.w1ft = (const u16x8_t*)a.aw1ft;
-    af.b1 = a.ab1;
-    af.w2 = a.aw2;
-    af.de = a.ade;
-    af.e = a.ae;
-    af.alphas = a.aalphas;
-    af.perm = a.perm;
-    af.slab = a.aslab;
   }
   hipLaunchKernelGGL(kfn, grid, dim3(256), lds, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, a.wemb, a.E,
                      a.p1emb, a.p2emb, a.PD, (const frag*)a.apack, (const frag*)a.a2pack, a.bias,
                      (const elem*)a.hraw, (const typename CT<BF16>::type*)a.cst, (const elem*)a.dH, a.dw_slab, a.dpos_slab, a.dwemb, a.dmask, a.seed, a.thr, a.inv_kp,
-                     a.drop, pl ? nullptr : (unsigned short*)a.dxp, (const unsigned short*)(xd ? a.xdtab : a.xg), a.dh_lane,
-                     pm ? a.tlen : nullptr, pm ? a.slen : nullptr, a.wblank, af, (const unsigned short*)a.wrows,
+                     a.drop, (unsigned short*)a.dxp, (const unsigned short*)(xd ? a.xdtab : a.xg), a.dh_lane,
+                     pm ? a.tlen : nullptr, pm ? a.slen : nullptr, a.wblank, (const unsigned short*)a.wrows,
                      a.wbytes);
   INA_CHECK_LAUNCH();
   return 0;
@@ -2337,11 +1966,8 @@ int x_gather(const LstmArgs& a, int U, int NX, hipStream_t st) {
   dim3 grid(ntiles, (a.L + XG_T * XG_C - 1) / (XG_T * XG_C));
   if (2 * a.L * a.PD > 128 * 8) return -1;   // pos tables staged in LDS
   const auto* wr16 = (const unsigned short*)a.wrows;
-  // INA_XG_GRID caps the gather grid (grid-stride over tiles; 0 / unset: one workgroup per tile).  Capped grids
-  // measured slower -- the direct-x gather is bound by its keep-bit hash (two quarter-rate multiplies per unit
-  // pair), not by workgroup launches: 163 / 179 us at 2048 / 1024 workgroups vs 148 (profiles/r4_xgather_grid)
-  static const int xg_cap = [] { const char* v = std::getenv("INA_XG_GRID"); return v ? std::atoi(v) : 0; }();
-  if (xg_cap > 0 && (int)grid.x > xg_cap) grid.x = xg_cap;
+  // one workgroup per tile (capped grid-stride grids measured slower: the direct-x gather is bound by its
+  // keep-bit hash, not by workgroup launches -- profiles/r4_xgather_grid)
   if (a.xd && !a.drop) {
     hipLaunchKernelGGL(xd_ids_kernel, dim3((ntiles * 16 + 255) / 256), dim3(256), 0, st, a.inst, a.S, a.pos1, a.pos2,
                        a.L, a.E, a.PD, a.p1emb, a.p2emb, posb, (unsigned short*)a.xdtab);

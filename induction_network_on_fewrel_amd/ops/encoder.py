@@ -24,7 +24,7 @@ import weakref
 import torch
 
 from ._ext import ops
-from .packing import lstm_shape, pack_attn, pack_attn_fuse, pack_attn_rec, pack_lstm
+from .packing import lstm_shape, pack_attn, pack_attn_rec, pack_lstm
 
 
 def _route_grad(meta, name, g):
@@ -48,7 +48,7 @@ DIRECT_X_CALLS = [0]   # forwards that ran direct x (tests assert the path engag
 
 def direct_x_enabled() -> bool:
     """Direct-x recurrences (lstm.hip xd_build): INA_DIRECT_X=0 keeps the x_gather record (A/B, tests)."""
-    return os.environ.get("INA_DIRECT_X", "1") != "0" and os.environ.get("INA_POS_LDS", "0") == "0"
+    return os.environ.get("INA_DIRECT_X", "1") != "0"
 
 
 def word_rows(word: torch.Tensor, wemb: torch.Tensor, fresh: bool):
@@ -136,11 +136,10 @@ class EncoderFn(torch.autograd.Function):
             raise NotImplementedError("lstm_skip_padding on the GPU needs the bf16 record path (u in {8, 20, 32}, "
                                       "L <= 64) and device lengths")
         perm = tlen = slen = None
-        fused = rec and bool(need_grad) and meta.get("fuse_attn_bwd", os.environ.get("INA_FUSE_ATTN_BWD", "0") != "0")
         # direct x: the recurrences read the word rows + LDS position tables (shifted ids), no xg record.  It
         # pays once the kernels are throughput-bound (same row threshold as the ragged tiles): 1,616,764 vs
         # 1,588,243 episodes/s at 2048 episodes, 3,543 vs 3,569 at 1 episode (profiles/r4_direct_x/small)
-        direct = (rec and wrows is not None and sh["NX"] == 4 and bool(meta.get("pos_shift", False)) and not fused
+        direct = (rec and wrows is not None and sh["NX"] == 4 and bool(meta.get("pos_shift", False))
                   and direct_x_enabled() and inst.shape[0] >= meta.get("direct_x_min_rows", RAGGED_MIN_ROWS))
         DIRECT_X_CALLS[0] += int(direct)
         if rec:
@@ -161,14 +160,10 @@ class EncoderFn(torch.autograd.Function):
             hlane, cst, hnat, dmask, xg = o.lstm_fwd(*lstm_args, bf16, bool(need_grad), *tail)
             e, alphas = o.attn_fwd(hnat, inst, mask, w1pack, b1c, w2c, U, bf16, int(meta.get("attn_blocks", 0)))
         if need_grad:
-            # attention backward fused into lstm_bwd (record path): its own per-direction packs
-            if fused:
-                w1pack, w1tpack = ((pk["w1fpack"], pk["w1ftpack"]) if pk is not None and "w1fpack" in pk
-                                   else pack_attn_fuse(W1))
             ctx.save_for_backward(inst, word, pos1, pos2, wemb, p1emb, p2emb, apack, a2pack, bias, hlane, cst,
                                   w1pack, w1tpack, b1, w2, alphas, hnat, dmask, xg, e, perm, tlen, slen,
                                   wrows if direct else None)
-            ctx.meta = dict(meta, NX=sh["NX"], DIN=DIN, rec=rec, fused=fused)
+            ctx.meta = dict(meta, NX=sh["NX"], DIN=DIN, rec=rec)
         ctx.mark_non_differentiable(alphas)
         ctx.set_materialize_grads(False)   # no zero-fill launch for the alphas gradient
         return e, alphas
@@ -183,14 +178,6 @@ class EncoderFn(torch.autograd.Function):
         H2 = 2 * U
         b1c, w2c = b1.detach().contiguous(), w2.detach().reshape(-1).contiguous()
         word_grad = bool(m.get("word_grad", False))
-        if m.get("fused"):
-            # one kernel: BPTT + the attention backward one step ahead of it (no dH tensor)
-            dw_slab, dpos_slab, dwemb, fslab = o.lstm_attn_bwd(
-                inst, word, pos1, pos2, wemb.detach().contiguous(), p1emb.detach().contiguous(),
-                p2emb.detach().contiguous(), apack, a2pack, bias, hlane, dmask, xg, w1pack, w1tpack, b1c, w2c,
-                de.contiguous().float(), e, alphas, U, m["NX"], word_grad, int(m.get("lstm_blocks", 0)),
-                int(m["seed"]), float(m["keep_prob"]), bool(m.get("pos_shift", False)), tlen, slen, perm)
-            return EncoderFn._grads(ctx, m, None, fslab, dw_slab, dpos_slab, dwemb)
         if m["rec"]:   # dH in lstm_bwd's lane layout [tiles, 2, L, U/4, 64]
             dH, aslab = o.rec_attn_bwd(hlane, dmask, w1pack, w1tpack, b1c, w2c, de.contiguous().float(), e, alphas,
                                        U, float(m["keep_prob"]), int(m.get("attn_blocks", 0)), tlen, perm)
@@ -202,12 +189,11 @@ class EncoderFn(torch.autograd.Function):
                                                bias, hlane, cst, dH, dmask, xg, U, m["NX"], bf16, word_grad,
                                                int(m.get("lstm_blocks", 0)), int(m["seed"]), float(m["keep_prob"]),
                                                bool(m.get("pos_shift", False)), tlen, slen, wrows)
-        return EncoderFn._grads(ctx, m, aslab, None, dw_slab, dpos_slab, dwemb)
+        return EncoderFn._grads(ctx, m, aslab, dw_slab, dpos_slab, dwemb)
 
     @staticmethod
-    def _grads(ctx, m, aslab, fslab, dw_slab, dpos_slab, dwemb):
-        """Slabs -> parameter gradients.  aslab: [blocks, 2U*2U + 2*2U] (attention kernels); fslab: the fused
-        kernel's [blocks, 2 dir, U*2U + 2U] (own W1 rows | db1 or dw2)."""
+    def _grads(ctx, m, aslab, dw_slab, dpos_slab, dwemb):
+        """Slabs -> parameter gradients.  aslab: [blocks, 2U*2U + 2*2U] (attention kernels)."""
         word, p1emb, p2emb = ctx.saved_tensors[1], ctx.saved_tensors[5], ctx.saved_tensors[6]
         U, DIN = m["U"], m["DIN"]
         H2 = 2 * U
@@ -216,26 +202,17 @@ class EncoderFn(torch.autograd.Function):
         if glue is not None:
             # slabs -> flat gradient in the step's single slab_scatter_add launch (StepGlue.flush)
             p = m["pdict"]
-            if fslab is not None:
-                glue.add(fslab, glue.map_attn_fused(p, U), fslab.shape[0])
-            else:
-                glue.add(aslab, glue.map_attn(p, H2), aslab.shape[0])
+            glue.add(aslab, glue.map_attn(p, H2), aslab.shape[0])
             glue.add(dw_slab, glue.map_lstm_dw(p, U, DIN), dw_slab.shape[0])
             L, PD = word.shape[1], p1emb.shape[1]
             mp = glue.map_pos(p, L, PD)
             glue.add(dpos_slab, mp, dpos_slab.numel() // mp.numel())
             wg = _route_grad(m, "word_embedding", dwemb) if word_grad else None
             return (None,) * 5 + (wg,) + (None,) * 10
-        if fslab is not None:
-            f = fslab.sum(0)                       # [2, U*H2 + H2]
-            dW1 = f[:, : U * H2].reshape(H2, H2)
-            db1 = f[0, U * H2:]
-            dw2 = f[1, U * H2:].reshape(H2, 1)
-        else:
-            a = aslab.sum(0)
-            dW1 = a[: H2 * H2].view(H2, H2)
-            db1 = a[H2 * H2: H2 * H2 + H2]
-            dw2 = a[H2 * H2 + H2:].view(H2, 1)
+        a = aslab.sum(0)
+        dW1 = a[: H2 * H2].view(H2, H2)
+        db1 = a[H2 * H2: H2 * H2 + H2]
+        dw2 = a[H2 * H2 + H2:].view(H2, 1)
         D = dw_slab.sum(0)                         # [2, 4U, DIN+U+1]
         dKf = D[0, :, : DIN + U].t()
         dKb = D[1, :, : DIN + U].t()

@@ -26,7 +26,7 @@ import numpy as np
 import torch
 
 from ._ext import ops
-from .packing import _attn_fuse_idx, _attn_idx, _attn_rec_idx, _lstm_idx, _ntn_dw_idx, _ntn_tile_idx, lstm_shape
+from .packing import _attn_idx, _attn_rec_idx, _lstm_idx, _ntn_dw_idx, _ntn_tile_idx, lstm_shape
 
 
 class StepGlue:
@@ -114,9 +114,6 @@ class StepGlue:
             ri, rti = (t.numpy() for t in _attn_rec_idx(U))
             put("w1rpack", np.where(ri < Z, off["attn_kernel"] + ri, -1), True)
             put("w1rtpack", np.where(rti < Z, off["attn_kernel"] + rti, -1), True)
-            fi_, fti = (t.numpy() for t in _attn_fuse_idx(U))   # attention backward fused into lstm_bwd
-            put("w1fpack", np.where(fi_ < Z, off["attn_kernel"] + fi_, -1), True)
-            put("w1ftpack", np.where(fti < Z, off["attn_kernel"] + fti, -1), True)
         if head is not None:
             H, h, N, paper = head
             mi, wi = (t.numpy() for t in _ntn_tile_idx(H, h, N, bool(paper)))
@@ -169,22 +166,6 @@ class StepGlue:
         m = self._maps.get(key)
         if m is None:
             m = self._dev_i32(np.concatenate([o[0] + np.arange(H2 * H2), o[1] + np.arange(H2), o[2] + np.arange(H2)]))
-            self._maps[key] = m
-        return m
-
-    def map_attn_fused(self, p, U: int) -> torch.Tensor:
-        """lstm_attn_bwd slab row [2 dir][U own W1 rows x 2U | 2U]: direction d holds W1 rows [d U, d U + U)
-        and db1 (d = 0) / dw2 (d = 1)."""
-        o = (self.off(p["attn_kernel"]), self.off(p["attn_bias"]), self.off(p["attn_w2"]))
-        key = ("attn_fused", U, o)
-        m = self._maps.get(key)
-        if m is None:
-            H2 = 2 * U
-            parts = []
-            for d in range(2):
-                parts.append(o[0] + d * U * H2 + np.arange(U * H2))
-                parts.append((o[1] if d == 0 else o[2]) + np.arange(H2))
-            m = self._dev_i32(np.concatenate(parts))
             self._maps[key] = m
         return m
 
