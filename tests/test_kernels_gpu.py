@@ -41,6 +41,16 @@ def _relerr(a, b):
     return float((a - b).abs().max() / (b.abs().max() + 1e-12))
 
 
+def _elem(a, b, atol_frac, rtol):
+    """(max-relative error, fraction of entries with |a - b| <= atol_frac * max|b| + rtol * |b|): the element-wise
+    criterion catches a systematic error confined to a slice of a tensor (one gate's columns, one slice of M) that
+    a max-relative bound sized for bf16 rounding would let through."""
+    a, b = a.double().flatten(), b.double().flatten()
+    scale = float(b.abs().max()) + 1e-30
+    d = (a - b).abs()
+    return float(d.max()) / scale, float((d <= atol_frac * scale + rtol * b.abs()).double().mean())
+
+
 def _gathered(dd, inst):
     return [t[inst.long()] for t in dd.arrays()]
 
@@ -268,11 +278,20 @@ def test_encoder_backward(dtype, keep_prob, u, L=37):
     ee = _relerr(e.detach(), e_ref)
     print(f"encoder {dtype} kp={keep_prob}: e {ee:.2e}")
     assert ee < tol_e
+    # bf16: also against the oracle with the kernels' bf16 rounding points (ref.encode bf16=True), tightly and
+    # element-wise (>= 99.9 % of entries within 1e-2 max + 5e-2 |g|); measured (round 5): <= 1.02e-2 max-relative,
+    # 100 % of entries within, over u in {8, 20, 32} and keep_prob in {1, 0.9}
+    g_b = _encoder_grads_ref(model, dd, inst, de, keep_prob, seed, bf16=True)[1] if bf16 else None
     for k in ("pos1_embedding", "pos2_embedding", "lstm_fw_kernel", "lstm_fw_bias", "lstm_bw_kernel", "lstm_bw_bias",
               "attn_kernel", "attn_bias", "attn_w2"):
         g = getattr(model.params, k).grad
         err = _relerr(g, g_ref[k])
-        print(f"  grad {k}: {err:.2e}")
+        msg = f"  grad {k}: {err:.2e}"
+        if bf16:
+            mb, fb = _elem(g, g_b[k], 1e-2, 5e-2)
+            msg += f" | vs bf16 oracle {mb:.2e}, {100 * fb:.2f}% within"
+            assert mb < 3e-2 and fb >= 0.999, (k, mb, fb)
+        print(msg)
         assert err < tol_g, k
 
 
@@ -474,12 +493,13 @@ def test_head_forward_backward(head, shape):
     (probs_r * dp).sum().backward()
     ep = _relerr(probs.detach(), probs_r.detach())
     print(f"head {head} {shape}: probs {ep:.2e}")
-    assert ep < 2e-2
+    assert ep < 5e-3
+    # measured (round 5): probs <= 9e-4, every gradient <= 6.5e-3 max-relative
     for k, t in (("e", (e.grad, er.grad)), ("W_s", (p["W_s"].grad, pr["W_s"].grad)), ("M", (p["M"].grad, pr["M"].grad)),
                  ("w", (p["ntn_w"].grad, pr["ntn_w"].grad)), ("b", (p["ntn_b"].grad, pr["ntn_b"].grad))):
-        err = _relerr(*t)
-        print(f"  grad {k}: {err:.2e}")
-        assert err < 6e-2, k
+        err, frac = _elem(*t, 5e-3, 2e-2)
+        print(f"  grad {k}: {err:.2e}, {100 * frac:.2f}% within 5e-3 max + 2e-2 |g|")
+        assert err < 2e-2 and frac >= 0.999, k
 
 
 @pytest.mark.parametrize("N,K,H,R", [(5, 3, 40, 3), (10, 5, 64, 3), (5, 1, 40, 3), (5, 10, 40, 3), (3, 2, 16, 2),
