@@ -451,6 +451,18 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_bal_kernel(const unsigned s
 constexpr int HDIM = 64;
 constexpr int KSTR = HDIM + 8;  // LDS row stride (bf16) of row-major [key][d] images
 
+// Attention-probability dropout: ONE hash per pair of adjacent keys.  Element (row, key), row = (s nh + h) L + q,
+// keeps iff 16-bit half (key & 1) of mix(pidx * C + salt), pidx = (row << 6) | (key >> 1), is < thr >> 16 (keep
+// rate floor(kp 2^16) / 2^16; L <= 128).  pidx * C splits into a per-row / per-lane base plus compile-time
+// multiples of C, so the forward costs one add + the mix per PAIR.  Bit-identical to models/bert.py::attn_keep_mask.
+constexpr uint32_t ATTN_C = 0x6C8E9CF5u;
+INA_DEVICE uint32_t attn_mix(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  return x;
+}
+
 INA_DEVICE u16x8_t ld8(const unsigned short* p) { return *reinterpret_cast<const u16x8_t*>(p); }
 INA_DEVICE u16x8_t zero8() { return u16x8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
 INA_DEVICE u16x8_t cat_tr(const s16x4_t& a, const s16x4_t& b) {
@@ -535,19 +547,23 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const unsigned short* __re
     for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        sc[kt][r] = exp2f(sc[kt][r] - m);
+        sc[kt][r] = __builtin_amdgcn_exp2f(sc[kt][r] - m);   // arguments <= 0: v_exp_f32, no range fix-up
         l += sc[kt][r];
       }
     l = cross_group_sum(l);
-    const float inv_l = 1.f / l;
+    // the dropout scale 1 / kp goes into the output scaling with 1 / l
+    const float inv_l = (drop ? inv_kp : 1.f) / l;
     if (drop) {
-      const uint32_t rowidx = ((uint32_t)(s * nh + hh) * L + q) * L;
+      // pairs (4g + 2hr, +1) of key tile kt: pidx = (row << 6) + 8 kt + 2 g + hr
+      const uint32_t thr16 = thr >> 16;
+      const uint32_t hb = ((((uint32_t)(s * nh + hh) * L + q) << 6) + 2 * g) * ATTN_C + salt;
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = 16 * kt + 4 * g + r;
-          sc[kt][r] = dropout_keep_salted(salt, rowidx + key, thr) ? sc[kt][r] * inv_kp : 0.f;
+        for (int hr = 0; hr < 2; ++hr) {
+          const uint32_t x = attn_mix(hb + (uint32_t)(8 * kt + hr) * ATTN_C);
+          if ((x & 0xFFFFu) >= thr16) sc[kt][2 * hr] = 0.f;
+          if ((x >> 16) >= thr16) sc[kt][2 * hr + 1] = 0.f;
         }
     }
     // O^T = V^T P^T: B operand = P^T accumulators (k-step ks2 covers key tiles 2ks2, 2ks2+1)
@@ -651,14 +667,27 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
   }
   for (int i = threadIdx.x; i < 4 * 3 * HDIM; i += 256) (&wsum[0][0][0])[i] = 0.f;
   __syncthreads();
-  // add the column sums (over the 16 lanes n) of one 16-row output tile into this wave's partials
-  // (the rounded bf16 values that are stored; lanes of rows >= L pass zeros)
+  // column sums (the rounded bf16 values that are stored; rows >= L add zeros): per-lane partials in registers
+  // over all of the wave's tiles, then ONE 16-lane reduction per column into this wave's slot
+  float csum[3][4][4];
+#pragma unroll
+  for (int part = 0; part < 3; ++part)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) csum[part][dt][r] = 0.f;
   auto colsum = [&](int part, int dt, const float (&v)[4], bool ok) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float t = group16_sum(ok ? round_bf(v[r]) : 0.f);
-      if (n == 0) wsum[wave][part][16 * dt + 4 * g + r] += t;
-    }
+    for (int r = 0; r < 4; ++r) csum[part][dt][r] += ok ? round_bf(v[r]) : 0.f;
+  };
+  auto colsum_flush = [&](int part) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float t = group16_sum(csum[part][dt][r]);
+        if (n == 0) wsum[wave][part][16 * dt + 4 * g + r] = t;
+      }
   };
   const float c2 = 0.125f * LOG2E;
   const float scale = 0.125f;
@@ -675,6 +704,9 @@ INA_UNROLL(INA_MHA_KTU)
       if (!kok) kf[ks] = vf[ks] = zero8();
     }
     const float ma = madd[key];
+    // dropout hash base of the lane: (((s nh + h) L + 4 g) << 6) + (key >> 1), times C, plus the salt
+    const uint32_t thr16 = thr >> 16, kshift = 16u * (uint32_t)(key & 1);
+    const uint32_t kbase_h = ((((uint32_t)(s * nh + hh) * L + 4 * g) << 6) + (uint32_t)(key >> 1)) * ATTN_C + salt;
     f32x4_t dV[4], dK[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dV[dt] = dK[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -698,9 +730,12 @@ INA_UNROLL(INA_MHA_QPU)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = 16 * qt + 4 * g + r;
-          const float p = (q < L) ? exp2f(sacc[r] * c2 + ma - lqa[r]) : 0.f;
+          const float p = (q < L) ? __builtin_amdgcn_exp2f(sacc[r] * c2 + ma - lqa[r]) : 0.f;
           float z = 1.f;
-          if (drop) z = dropout_keep_salted(salt, ((uint32_t)(s * nh + hh) * L + q) * L + key, thr) ? inv_kp : 0.f;
+          if (drop) {   // the lane's key is fixed: pidx = ((row0 + q) << 6) + (key >> 1)
+            const uint32_t x = attn_mix(kbase_h + (uint32_t)(16 * qt + r) * (64u * ATTN_C));
+            z = ((x >> kshift) & 0xFFFFu) < thr16 ? inv_kp : 0.f;
+          }
           const float dp = pacc[r] * z;
           pp[h2][r] = p * z;
           ds[h2][r] = p * (dp - dqa[r]);
@@ -743,6 +778,10 @@ INA_UNROLL(INA_MHA_QPU)
         colsum(2, dt, b, kok);
       }
     }
+  }
+  if (bsum) {
+    colsum_flush(1);
+    colsum_flush(2);
   }
   __syncthreads();
   // phase 2: K image into region A, then dQ^T = K^T dS^T per query tile
@@ -790,6 +829,7 @@ INA_UNROLL(INA_MHA_QPU)
     }
   }
   if (bsum) {
+    colsum_flush(0);
     __syncthreads();
     for (int i = threadIdx.x; i < 3 * HDIM; i += 256) {
       const float* w = &wsum[0][0][0] + i;

@@ -95,6 +95,23 @@ def keep_mask(seed: int, stream: int, numel: int, keep_prob: float, device=None)
     return (x < thr).to(torch.float32)
 
 
+def attn_keep_mask(seed: int, stream: int, S: int, nh: int, L: int, keep_prob: float, device=None) -> torch.Tensor:
+    """Attention-probability keep mask [S, nh, L, L] (float 0/1): ONE hash per pair of adjacent keys.  Element
+    (row, j), row = (s nh + h) L + i, keeps iff 16-bit half (j & 1) of mix(((row << 6) | (j >> 1)) * C + salt) is
+    below floor(kp 2^32) >> 16 (csrc/kernels/bert.hip attn_mix; L <= 128)."""
+    salt = ((seed & 0x7FFFFFFF) * 0x2545F491 + stream * 0x3C6EF372 + 0x1234567) & _M32
+    row = torch.arange(S * nh * L, dtype=torch.int64, device=device)[:, None]
+    j = torch.arange(L, dtype=torch.int64, device=device)[None, :]
+    x = ((((row << 6) | (j >> 1)) * 0x6C8E9CF5) & _M32) + salt
+    x = x & _M32
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    v = torch.where((j & 1) == 1, x >> 16, x & 0xFFFF)
+    thr16 = min(int(keep_prob * 4294967296.0), 0xFFFFFFFF) >> 16
+    return (v < thr16).to(torch.float32).view(S, nh, L, L)
+
+
 def _dropout(x: torch.Tensor, seed: int, stream: int, p: float, training: bool) -> torch.Tensor:
     if not training or p <= 0.0:
         return x
@@ -115,7 +132,7 @@ def layer_norm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor) -> torch.Tenso
 
 
 def attention(q, k, v, mask, nh: int, seed: int, stream: int, p: float, training: bool):
-    """q/k/v [S, L, Hd]; mask [S, L] (1 = real key).  Dropout index ((s*nh+h)*L + i)*L + j."""
+    """q/k/v [S, L, Hd]; mask [S, L] (1 = real key).  Dropout: attn_keep_mask (one hash per key pair)."""
     S, L, Hd = q.shape
     d = Hd // nh
     qh = q.view(S, L, nh, d).transpose(1, 2)
@@ -124,7 +141,8 @@ def attention(q, k, v, mask, nh: int, seed: int, stream: int, p: float, training
     sc = qh @ kh.transpose(-1, -2) / math.sqrt(d)
     sc = sc.masked_fill(mask[:, None, None, :] == 0, float("-inf"))
     pr = torch.softmax(sc, -1)
-    pr = _dropout(pr, seed, stream, p, training)
+    if training and p > 0.0:
+        pr = pr * attn_keep_mask(seed, stream, S, nh, L, 1.0 - p, pr.device) / (1.0 - p)
     return (pr @ vh).transpose(1, 2).reshape(S, L, Hd)
 
 
