@@ -57,6 +57,32 @@ def test_paper_config_forward_backward_vs_oracle(keep_prob, u):
         assert _relerr(got[k], p[k].grad) < 8e-2, k
 
 
+@pytest.mark.parametrize("u", [129, 130])
+def test_odd_and_unaligned_width_per_step_loop_vs_oracle(u):
+    """Widths above the last kernel instantiation that are odd or not multiples of 4 run the
+    per-step GEMM loop (ops/wide.py WideBiLSTM + lstm_wide_fwd_step / _bwd_step) with dropout on: the pair hash
+    over the flat (sequence, step, unit) index is the oracle's for any u, odd included."""
+    cfg, model, inst, arrays, lab, (B, N, K, Q) = _setup(u, 50, "auto")
+    cfg.keep_prob = 0.9
+    assert not model.use_fused_lstm(37)
+    probs, _ = model(inst, arrays, B, N, K, Q, training=True, dropout_seed=7)
+    loss = model.loss(probs, lab)
+    loss.backward()
+    got = {k: v.grad.clone() for k, v in model.pdict().items() if v.grad is not None}
+    p = {k: v.detach().clone().requires_grad_(v.requires_grad) for k, v in model.pdict().items()}
+    w, a1, a2, m = (t[inst.long()] for t in arrays)
+    pr, _ = ref.forward(p, w.long(), a1.long(), a2.long(), m, B, N, K, Q, 3, "reference", 0.9, 7, bf16=False)
+    model.loss(pr, lab).backward()
+    ep = _relerr(probs.detach(), pr.detach())
+    print(f"u={u}: probs {ep:.2e}")
+    assert ep < 3e-2
+    for k in ("lstm_fw_kernel", "lstm_fw_bias", "lstm_bw_kernel", "lstm_bw_bias", "pos1_embedding", "attn_kernel",
+              "W_s", "M"):
+        err = _relerr(got[k], p[k].grad)
+        print(f"  grad {k}: {err:.2e}")
+        assert err < 8e-2, k
+
+
 def test_wide_matches_fused_at_u20(monkeypatch):
     """the per-step GEMM loop of ops/wide.py (padding off) against the fused kernels at u = 20."""
     monkeypatch.setenv("INA_LSTM_PAD", "0")

@@ -91,11 +91,16 @@ def load_data(cfg: Config, args):
             test = [rels[(5 * args.fold + i) % len(rels)] for i in range(5)]
             nv = getattr(args, "val_relations", 0)
             if nv > 0:   # train / val / test, all relation-disjoint: val selects, test only tests
-                val = [rels[(5 * args.fold + 5 + i) % len(rels)] for i in range(nv)]
-                train = [r for r in rels if r not in test and r not in val]
-                print(f"fold {args.fold}: train {len(train)} relations, val {val}, test {test}", flush=True)
                 if cfg.encoder == "bert":
                     raise SystemExit("--val_relations is implemented for the BiLSTM encoder")
+                # the val block must not wrap into the test block, and N relations must remain for training
+                if 5 + nv > len(rels) - cfg.N:
+                    raise SystemExit(f"--val_relations {nv}: {len(rels)} relations leave no disjoint train / val / "
+                                     f"test split with >= {cfg.N} training relations (need 5 + val <= {len(rels) - cfg.N})")
+                val = [rels[(5 * args.fold + 5 + i) % len(rels)] for i in range(nv)]
+                assert not set(val) & set(test)
+                train = [r for r in rels if r not in test and r not in val]
+                print(f"fold {args.fold}: train {len(train)} relations, val {val}, test {test}", flush=True)
                 args._test_split = full.subset_relations(test, "test_split")
                 return full.subset_relations(train, "train_split"), full.subset_relations(val, "val_split")
             rels = [r for r in rels if r not in test] + test
