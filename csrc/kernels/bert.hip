@@ -21,6 +21,8 @@
 //  backward ("key on the lane"): each wave owns key tiles; S = Q K^T and dP = dO V^T have the key
 //    on the lane, so dV^T = dO^T P' and dK^T = Q^T dS take P'/dS accumulators as B operands (q in
 //    kmap order, dO^T / Q^T from LDS); dS crosses LDS once for dQ^T = K^T dS^T.
+#include <cstdlib>
+
 #include "ina_common.h"
 #include "ina_launch.h"
 
@@ -472,8 +474,8 @@ INA_DEVICE u16x8_t cat_tr(const s16x4_t& a, const s16x4_t& b) {
 
 // qkv: [T, 3*HDm] bf16, HDm = nh*64; token row of (s, t) = s*L + t.  ctx: [T, HDm] bf16.
 // lse: [S, nh, LP] fp32 (log2-domain log-sum-exp of the scaled scores).  mask_all: [NI, L] int.
-template <int LP>
-__global__ __launch_bounds__(256) void mha_fwd_kernel(const unsigned short* __restrict__ qkv,
+template <int LP, int NWV>
+__global__ __launch_bounds__(64 * NWV) void mha_fwd_kernel(const unsigned short* __restrict__ qkv,
                                                       const int* __restrict__ inst, const int* __restrict__ mask_all,
                                                       int S, int L, int nh, unsigned short* __restrict__ ctx,
                                                       float* __restrict__ lse, uint32_t salt, uint32_t thr,
@@ -490,12 +492,13 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const unsigned short* __re
   const unsigned short* kbase = qkv + tok0 * ROW + HDm + hh * HDIM;
   const unsigned short* vbase = qkv + tok0 * ROW + 2 * HDm + hh * HDIM;
   // stage K and V rows (rows >= L are zero), key mask
+  constexpr int NTH = 64 * NWV;
   {
-    constexpr int NU = LP * 8 / 256;
+    constexpr int NU = (LP * 8 + NTH - 1) / NTH;
     u16x8_t kv[NU], vv[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
-      const int i = threadIdx.x + 256 * u;
+      const int i = min(threadIdx.x + NTH * u, LP * 8 - 1);
       const int k = i >> 3, c = (i & 7) * 8;
       const size_t off = (size_t)(k < L ? k : 0) * ROW + c;
       kv[u] = ld8(kbase + off);
@@ -503,7 +506,8 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const unsigned short* __re
     }
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
-      const int i = threadIdx.x + 256 * u;
+      const int i = threadIdx.x + NTH * u;
+      if (i >= LP * 8) break;
       const int k = i >> 3, c = (i & 7) * 8;
       if (k >= L) kv[u] = vv[u] = zero8();
       *reinterpret_cast<u16x8_t*>(&Ks[k * KSTR + c]) = kv[u];
@@ -511,11 +515,11 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const unsigned short* __re
     }
   }
   const int* mrow = mask_all + (size_t)inst[s] * L;
-  for (int k = threadIdx.x; k < LP; k += 256) madd[k] = (k < L && mrow[k < L ? k : 0] > 0) ? 0.f : -INFINITY;
+  for (int k = threadIdx.x; k < LP; k += NTH) madd[k] = (k < L && mrow[k < L ? k : 0] > 0) ? 0.f : -INFINITY;
   __syncthreads();
   const float c2 = 0.125f * LOG2E;  // 1/sqrt(64) in the log2 domain
 #pragma unroll 1
-  for (int qt = wave; qt < NT; qt += 4) {
+  for (int qt = wave; qt < NT; qt += NWV) {
     const int q = 16 * qt + n;
     const bool qok = q < L;
     const unsigned short* qrow = qkv + (tok0 + (qok ? q : 0)) * ROW + hh * HDIM;
@@ -594,8 +598,8 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(const unsigned short* __re
 // dqkv: [T, 3*HDm] bf16 (dQ | dK | dV), fully written (rows of tokens < L).
 // bsum (optional): [S * nh][3][64] column sums of this block's stored dQ / dK / dV (the QKV bias
 // gradient before the sum over sequences; one small slab instead of a [T, 3*HDm] reduction).
-template <int LP>
-__global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __restrict__ qkv,
+template <int LP, int NWV>
+__global__ __launch_bounds__(64 * NWV) void mha_bwd_kernel(const unsigned short* __restrict__ qkv,
                                                       const unsigned short* __restrict__ ctx,
                                                       const unsigned short* __restrict__ dctx,
                                                       const float* __restrict__ lse, const int* __restrict__ inst,
@@ -614,7 +618,8 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
   __shared__ float delta[LP];
   __shared__ float madd[LP];
   __shared__ float lsel[LP];
-  __shared__ float wsum[4][3][HDIM];   // per-wave column sums (dQ | dK | dV), summed in fixed order
+  __shared__ float wsum[NWV][3][HDIM];   // per-wave column sums (dQ | dK | dV), summed in fixed order
+  constexpr int NTH = 64 * NWV;
   unsigned short* Qn = TA;
   unsigned short* dOn = TA + LP * DSTR;
   unsigned short* Kn = TA;
@@ -632,11 +637,11 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
   // phase 0: Q, dO images; delta = rowsum(dO * O); key mask.  All loads of a thread are issued
   // before any is consumed (one memory latency per phase, not one per row).
   {
-    constexpr int NU = LP * 8 / 256;
+    constexpr int NU = (LP * 8 + NTH - 1) / NTH;   // chunk i >= 8 LP: clamped load, no store
     u16x8_t qv[NU], dv[NU], ov[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
-      const int i = threadIdx.x + 256 * u;
+      const int i = min(threadIdx.x + NTH * u, LP * 8 - 1);
       const int q = i >> 3, c = (i & 7) * 8;
       const int qc = q < L ? q : 0;
       qv[u] = ld8(qb + (size_t)qc * ROW + c);
@@ -645,7 +650,8 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
     }
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
-      const int i = threadIdx.x + 256 * u;
+      const int i = threadIdx.x + NTH * u;
+      if (i >= LP * 8) break;   // (wave-uniform for NTH <= 8 LP; else the tail wave's lanes)
       const int q = i >> 3, c = (i & 7) * 8;
       const bool ok = q < L;
       float d = 0.f;
@@ -661,11 +667,11 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
     }
   }
   const int* mrow = mask_all + (size_t)inst[s] * L;
-  for (int k = threadIdx.x; k < LP; k += 256) {
+  for (int k = threadIdx.x; k < LP; k += NTH) {
     madd[k] = (k < L && mrow[k < L ? k : 0] > 0) ? 0.f : -INFINITY;
     lsel[k] = lrow[k];
   }
-  for (int i = threadIdx.x; i < 4 * 3 * HDIM; i += 256) (&wsum[0][0][0])[i] = 0.f;
+  for (int i = threadIdx.x; i < NWV * 3 * HDIM; i += NTH) (&wsum[0][0][0])[i] = 0.f;
   __syncthreads();
   // column sums (the rounded bf16 values that are stored; rows >= L add zeros): per-lane partials in registers
   // over all of the wave's tiles, then ONE 16-lane reduction per column into this wave's slot
@@ -693,7 +699,7 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(const unsigned short* __re
   const float scale = 0.125f;
   // phase 1: each wave owns key tiles kt = wave, wave + 4
 INA_UNROLL(INA_MHA_KTU)
-  for (int kt = wave; kt < NT; kt += 4) {
+  for (int kt = wave; kt < NT; kt += NWV) {
     const int key = 16 * kt + n;
     const bool kok = key < L;
     u16x8_t kf[2], vf[2];
@@ -786,24 +792,25 @@ INA_UNROLL(INA_MHA_QPU)
   __syncthreads();
   // phase 2: K image into region A, then dQ^T = K^T dS^T per query tile
   {
-    constexpr int NU = LP * 8 / 256;
+    constexpr int NU = (LP * 8 + NTH - 1) / NTH;   // chunk i >= 8 LP: clamped load, no store
     u16x8_t kv[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
-      const int i = threadIdx.x + 256 * u;
+      const int i = min(threadIdx.x + NTH * u, LP * 8 - 1);
       const int k = i >> 3, c = (i & 7) * 8;
       kv[u] = ld8(kb + (size_t)(k < L ? k : 0) * ROW + c);
     }
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
-      const int i = threadIdx.x + 256 * u;
+      const int i = threadIdx.x + NTH * u;
+      if (i >= LP * 8) break;
       const int k = i >> 3, c = (i & 7) * 8;
       if (k >= L) kv[u] = zero8();
       *reinterpret_cast<u16x8_t*>(&Kn[k * DSTR + c]) = kv[u];
     }
   }
   __syncthreads();
-  for (int qt = wave; qt < NT; qt += 4) {
+  for (int qt = wave; qt < NT; qt += NWV) {
     const int q = 16 * qt + n;
     f32x4_t acc[4];
 #pragma unroll
@@ -831,9 +838,12 @@ INA_UNROLL(INA_MHA_QPU)
   if (bsum) {
     colsum_flush(0);
     __syncthreads();
-    for (int i = threadIdx.x; i < 3 * HDIM; i += 256) {
+    for (int i = threadIdx.x; i < 3 * HDIM; i += NTH) {
       const float* w = &wsum[0][0][0] + i;
-      bsum[(size_t)blockIdx.x * 3 * HDIM + i] = ((w[0] + w[3 * HDIM]) + w[6 * HDIM]) + w[9 * HDIM];
+      float acc = 0.f;
+#pragma unroll
+      for (int v = 0; v < NWV; ++v) acc += w[v * 3 * HDIM];   // fixed order
+      bsum[(size_t)blockIdx.x * 3 * HDIM + i] = acc;
     }
   }
 }
@@ -938,9 +948,15 @@ int mha_lp(int L) { return L <= 32 ? 32 : (L <= 64 ? 64 : (L <= 96 ? 96 : (L <= 
 
 int mha_fwd(const BertMhaArgs& a, hipStream_t st) {
   const dim3 grid(a.S * a.nh);
+  // INA_MHA_FWD_WAVES = 4 / 8 waves per (sequence, head) block (A/B)
+  static const int nwv = [] { const char* v = std::getenv("INA_MHA_FWD_WAVES"); return v ? std::atoi(v) : 4; }();
 #define CALL(LP)                                                                                          \
-  hipLaunchKernelGGL(mha_fwd_kernel<LP>, grid, dim3(256), 0, st, (const unsigned short*)a.qkv, a.inst,   \
-                     a.mask, a.S, a.L, a.nh, (unsigned short*)a.ctx, a.lse, a.salt, a.thr, a.inv_kp, a.drop)
+  if (nwv == 8)                                                                                           \
+    hipLaunchKernelGGL((mha_fwd_kernel<LP, 8>), grid, dim3(512), 0, st, (const unsigned short*)a.qkv, a.inst, \
+                       a.mask, a.S, a.L, a.nh, (unsigned short*)a.ctx, a.lse, a.salt, a.thr, a.inv_kp, a.drop); \
+  else                                                                                                    \
+    hipLaunchKernelGGL((mha_fwd_kernel<LP, 4>), grid, dim3(256), 0, st, (const unsigned short*)a.qkv, a.inst, \
+                       a.mask, a.S, a.L, a.nh, (unsigned short*)a.ctx, a.lse, a.salt, a.thr, a.inv_kp, a.drop)
   switch (mha_lp(a.L)) {
     case 32: CALL(32); break;
     case 64: CALL(64); break;
@@ -955,8 +971,16 @@ int mha_fwd(const BertMhaArgs& a, hipStream_t st) {
 
 int mha_bwd(const BertMhaArgs& a, hipStream_t st) {
   const dim3 grid(a.S * a.nh);
+  // INA_MHA_BWD_WAVES = 4 / 8: waves per (sequence, head) block (default 8: one key / query tile per wave at
+  // L = 128, 16 waves per CU at the 2 blocks the LDS allows; 379 vs 453 us per layer, profiles/r5_mha)
+  static const int nwv = [] { const char* v = std::getenv("INA_MHA_BWD_WAVES"); return v ? std::atoi(v) : 8; }();
 #define CALL(LP)                                                                                              \
-  hipLaunchKernelGGL(mha_bwd_kernel<LP>, grid, dim3(256), 0, st, (const unsigned short*)a.qkv,               \
+  if (nwv == 8)                                                                                               \
+    hipLaunchKernelGGL((mha_bwd_kernel<LP, 8>), grid, dim3(512), 0, st, (const unsigned short*)a.qkv,         \
+                       (const unsigned short*)a.ctx, (const unsigned short*)a.dctx, a.lse, a.inst, a.mask, a.S, \
+                       a.L, a.nh, (unsigned short*)a.dqkv, a.salt, a.thr, a.inv_kp, a.drop, a.bsum);           \
+  else                                                                                                        \
+  hipLaunchKernelGGL((mha_bwd_kernel<LP, 4>), grid, dim3(256), 0, st, (const unsigned short*)a.qkv,          \
                      (const unsigned short*)a.ctx, (const unsigned short*)a.dctx, a.lse, a.inst, a.mask, a.S, \
                      a.L, a.nh, (unsigned short*)a.dqkv, a.salt, a.thr, a.inv_kp, a.drop, a.bsum)
   switch (mha_lp(a.L)) {
