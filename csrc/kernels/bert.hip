@@ -948,15 +948,11 @@ int mha_lp(int L) { return L <= 32 ? 32 : (L <= 64 ? 64 : (L <= 96 ? 96 : (L <= 
 
 int mha_fwd(const BertMhaArgs& a, hipStream_t st) {
   const dim3 grid(a.S * a.nh);
-  // INA_MHA_FWD_WAVES = 4 / 8 waves per (sequence, head) block (A/B)
-  static const int nwv = [] { const char* v = std::getenv("INA_MHA_FWD_WAVES"); return v ? std::atoi(v) : 4; }();
+  // 4 waves per (sequence, head) block: the forward is HBM-bound (q/k/v in, ctx out); 8 waves measured the
+  // same (149 vs 151 us per layer, profiles/r5_mha/bert_sum_fwd8.txt)
 #define CALL(LP)                                                                                          \
-  if (nwv == 8)                                                                                           \
-    hipLaunchKernelGGL((mha_fwd_kernel<LP, 8>), grid, dim3(512), 0, st, (const unsigned short*)a.qkv, a.inst, \
-                       a.mask, a.S, a.L, a.nh, (unsigned short*)a.ctx, a.lse, a.salt, a.thr, a.inv_kp, a.drop); \
-  else                                                                                                    \
-    hipLaunchKernelGGL((mha_fwd_kernel<LP, 4>), grid, dim3(256), 0, st, (const unsigned short*)a.qkv, a.inst, \
-                       a.mask, a.S, a.L, a.nh, (unsigned short*)a.ctx, a.lse, a.salt, a.thr, a.inv_kp, a.drop)
+  hipLaunchKernelGGL((mha_fwd_kernel<LP, 4>), grid, dim3(256), 0, st, (const unsigned short*)a.qkv, a.inst, \
+                     a.mask, a.S, a.L, a.nh, (unsigned short*)a.ctx, a.lse, a.salt, a.thr, a.inv_kp, a.drop)
   switch (mha_lp(a.L)) {
     case 32: CALL(32); break;
     case 64: CALL(64); break;
@@ -971,16 +967,10 @@ int mha_fwd(const BertMhaArgs& a, hipStream_t st) {
 
 int mha_bwd(const BertMhaArgs& a, hipStream_t st) {
   const dim3 grid(a.S * a.nh);
-  // INA_MHA_BWD_WAVES = 4 / 8: waves per (sequence, head) block (default 8: one key / query tile per wave at
-  // L = 128, 16 waves per CU at the 2 blocks the LDS allows; 379 vs 453 us per layer, profiles/r5_mha)
-  static const int nwv = [] { const char* v = std::getenv("INA_MHA_BWD_WAVES"); return v ? std::atoi(v) : 8; }();
+  // 8 waves per (sequence, head) block: one key / query tile per wave at L = 128, 16 waves per CU at the two
+  // blocks the LDS allows (4 waves: 453 vs 379 us per layer, profiles/r5_mha/bert_sum_bwd4.txt / _bwd8.txt)
 #define CALL(LP)                                                                                              \
-  if (nwv == 8)                                                                                               \
-    hipLaunchKernelGGL((mha_bwd_kernel<LP, 8>), grid, dim3(512), 0, st, (const unsigned short*)a.qkv,         \
-                       (const unsigned short*)a.ctx, (const unsigned short*)a.dctx, a.lse, a.inst, a.mask, a.S, \
-                       a.L, a.nh, (unsigned short*)a.dqkv, a.salt, a.thr, a.inv_kp, a.drop, a.bsum);           \
-  else                                                                                                        \
-  hipLaunchKernelGGL((mha_bwd_kernel<LP, 4>), grid, dim3(256), 0, st, (const unsigned short*)a.qkv,          \
+  hipLaunchKernelGGL((mha_bwd_kernel<LP, 8>), grid, dim3(512), 0, st, (const unsigned short*)a.qkv,          \
                      (const unsigned short*)a.ctx, (const unsigned short*)a.dctx, a.lse, a.inst, a.mask, a.S, \
                      a.L, a.nh, (unsigned short*)a.dqkv, a.salt, a.thr, a.inv_kp, a.drop, a.bsum)
   switch (mha_lp(a.L)) {
