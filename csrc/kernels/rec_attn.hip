@@ -298,8 +298,13 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
 // slab per workgroup: [dW1 (H2*H2, row i, col j) | db1 (H2) | dw2 (H2)], the attn_bwd layout.
 // ------------------------------------------------------------------------------------------
 template <int U>
+#ifndef INA_RA_PF_BWD
+#define INA_RA_PF_BWD 2   // backward prefetch distance in token steps (1: two buffers, 2: three)
+#endif
 #ifndef INA_RA_BWD_WAVES
-#define INA_RA_BWD_WAVES 3   // 2 (197 VGPRs, no spills) measured equal: 596-601 us either way (tools/gpu_ab_ra.sh)
+// 2 waves per SIMD with the 2-step prefetch (256 VGPRs, no spills): 5w5s 2,081,185 - 2,083,673 vs 2,064,695 -
+// 2,072,628 episodes/s for 3 waves + 1 step (which spilled 18; 3 waves + 2 steps spills 270), profiles/r5_rapf
+#define INA_RA_BWD_WAVES 2
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? INA_RA_BWD_WAVES : 2))) void rec_attn_bwd_kernel(
     const unsigned short* __restrict__ rec, const unsigned char* __restrict__ dmask, int S, int L, float inv_kp,
@@ -369,7 +374,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? I
       rec_load<U>(r0, r1, k0, k1, kor, t, o);
       o.al = arow[t];
     };
-    rec_steps<U, 1>(Lt, load, [&](int t, RecStep<U>& cur) {
+    rec_steps<U, INA_RA_PF_BWD>(Lt, load, [&](int t, RecStep<U>& cur) {
       rec_pin<U, true>(cur, kor);
       const float alv = valid ? cur.al : 0.f;
       float dev[DEPC];
