@@ -25,6 +25,11 @@ using namespace ina;
 #ifndef INA_FWD_PIPE
 #define INA_FWD_PIPE 1
 #endif
+#ifndef INA_BWD_TC_FROM_H
+// lean BPTT: tanh(c_t) = h_t / o_t = h_t (1 + 2^-z_o) from the step record's h_t and the o gate's exp (no
+// exp / rcp pair per unit and step for tanh(c_t); h_t is the forward's bf16 h, relative error <= 2^-9)
+#define INA_BWD_TC_FROM_H 1
+#endif
 namespace {
 
 template <int U, int NX, bool BF16>
@@ -1153,6 +1158,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
         const bf2_t v = {(__bf16)a, (__bf16)b};
         return __builtin_bit_cast(uint32_t, v);
       };
+      float hcv[U4];   // h_t (bf16 record) of the step being processed: tanh(c_t) = h_t / o_t
       // HASP: the step has a predecessor state (else it is zero: the direction's first step in time, or the
       // SKIP backward direction's tile start).  HI: the step stages into image rows 16..31 and completes
       // the pair (rows 0..15 = the previous step), FLUSH: the pair goes into dW after staging.
@@ -1215,8 +1221,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
           for (int ks = 0; ks < NKS; ++ks)
             acc = mma(lA[(m * NKS + ks) * 64 + lane],
                       __builtin_bit_cast(u16x8_t, u32x4_t{bw[4 * ks], bw[4 * ks + 1], bw[4 * ks + 2], bw[4 * ks + 3]}), acc);
-          const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
+          const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]);
+#if INA_BWD_TC_FROM_H
+          // o = 1 / (1 + e), e = 2^-z_o (z clamped: e stays finite, and where o ~ 0 every use of tc is scaled by o)
+          const float eo = __builtin_amdgcn_exp2f(fminf(-acc[3], 126.f));
+          const float og = fast_rcp(1.f + eo);
+          const float tc = hcv[m] * (1.f + eo);
+#else
+          const float og = sigmoid_l2(acc[3]);
           const float tc = tanh_l2(ccur[m] * (2.f * LOG2E_F));
+#endif
           const float dh = dh_rec[m] + dhin[m];
           // (shared products: the step is VALU-issue bound -- README "ISA budget"; 14 instead of 16 ops per unit)
           const float dho = dh * og;
@@ -1229,6 +1243,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
           const float dot = dho * tc;
           dg[m][3] = fmaf(-dot, og, dot);              // dh tc og (1 - og)
           ccur[m] = cprev[m];
+          hcv[m] = HASP ? bf2f((unsigned short)X.h[m]) : 0.f;   // h_t of the next processed step (time tp)
         }
         uint32_t dgw[2 * U4];   // packed bf16 dG pairs: the W dG operand and the dW image row
 #pragma unroll
@@ -1326,9 +1341,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
           __builtin_amdgcn_raw_buffer_store_b16((unsigned short)0, rdx, 2 * pofs[xi], t * PSTEPB, 0);
       }
 #pragma unroll
-      for (int m = 0; m < U4; ++m)   // c of the first processed step
+      for (int m = 0; m < U4; ++m) {   // c and h of the first processed step
         ccur[m] = (float)__builtin_bit_cast(
             _Float16, (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + (U4 + m) * 128, tof(tau_start) * RSTEPB, 0));
+        hcv[m] = bf2f((unsigned short)__builtin_amdgcn_raw_buffer_load_b16(rrec, vl2 + m * 128, tof(tau_start) * RSTEPB, 0));
+      }
       Raw A, B;
       rload(tau_start, A);
       int k = 0;   // processed steps so far: pairs (k, k + 1) -> image rows 0..15 / 16..31
