@@ -218,6 +218,9 @@ struct WideSeqArgs {
   void* hout;             // [S][L][2U] bf16: DropoutWrapper output (attention input)
   const void* dH;         // [S][L][2U] bf16: gradient w.r.t. hout
   void* dG;               // [S*L][2][G4] bf16: pre-activation gate gradients (both directions)
+  const void* wpk;        // [2][KS2][64] x 8 bf16 W_pos^T fragments (backward dX_pos; with dxp)
+  float* dxp;             // [2][S*L][np] fp32: dX_pos = dG W_pos^T per direction (nullptr: not computed)
+  int np;                 // position columns (2 PD <= 16)
   uint32_t salt0, salt1, thr;
   float inv_kp;
   int drop;
@@ -228,7 +231,7 @@ int wide_x_gather(const int* inst, int S, int L, const int* word, const int* pos
                   bool wemb_bf16, int E, const float* p1emb, const float* p2emb, int PD, int DP, void* xb,
                   hipStream_t st);
 int wide_pos_grad(const float* dxp, const int* inst, const int* pos1, const int* pos2, int S, int L, int PD, int P2,
-                  int chunks, float* part, hipStream_t st);
+                  int chunks, int planes, float* part, hipStream_t st);
 int lstm_wide_seq_fwd(const WideSeqArgs& a, hipStream_t st);
 int lstm_wide_seq_bwd(const WideSeqArgs& a, hipStream_t st);
 

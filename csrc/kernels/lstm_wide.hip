@@ -164,7 +164,11 @@ int lstm_wide_bwd_step(const LstmWideArgs& a, int tau, hipStream_t st) {
 //   * the activation / cell stash is tile-major (WideStash): 512 contiguous bytes per wave access;
 //   * backward: dG (bf16) goes to an LDS image [32][4 UP] and is contracted with the backward W_h
 //     fragments, whose rows land dh of unit 16w + 4q + r in accumulator register r of lane group q --
-//     the lane that owns that unit's gates.
+//     the lane that owns that unit's gates;
+//   * backward, optional (dxp): the input gradient's position columns dX_pos = dG W_pos^T (<= 16 columns)
+//     from the same LDS image -- wave w contracts 16-sequence tile w & 1 over 128 of the gate columns
+//     (4 MFMAs per step), the UP / 32 partials per tile are summed in a fixed order through LDS one step
+//     later.  This replaces a separate GEMM pass over the whole 2.4 GB dG at the paper configuration.
 // Gate columns are permuted to c = 4u + g (unit-major, the 4 gates of a unit adjacent).
 // ops/packing.py::pack_lstm_wide builds the fragments and is checked by tests/test_packing.py's
 // MFMA-layout emulation.
@@ -347,11 +351,14 @@ template <int U>
 __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_bwd_kernel(
     const unsigned short* __restrict__ dH, const uint2* __restrict__ acts, const uint2* __restrict__ cst,
     const u16x8_t* __restrict__ a2pk, unsigned short* __restrict__ dG, int S, int L, uint32_t salt0, uint32_t salt1,
-    uint32_t thr, float inv_kp, int drop) {
+    uint32_t thr, float inv_kp, int drop, const u16x8_t* __restrict__ wpk, float* __restrict__ dxp, int np) {
   using C = WideCfg<U>;
   using Z = WideStash<U>;
   constexpr int UP = C::UP, NW = C::NW, M = C::M, G4 = C::G4, KS2 = C::KS2, NT = C::NT, GS = C::GS, SEQ = C::SEQ;
+  constexpr int NTH = NW * 64, NG = NW / 2;   // NG dX_pos partials per 16-sequence tile (4 K-steps each)
+  static_assert(NW % 2 == 0 && 4 * NG == KS2, "dX_pos: NW / 2 wave pairs x 4 K-steps cover the gate columns");
   __shared__ __attribute__((aligned(16))) unsigned short gimg[2][SEQ * GS];
+  __shared__ __attribute__((aligned(16))) float pimg[2][NG * NT * 16 * 16];   // [buf][kg][nt][seq][16 cols]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4, n = lane & 15;
   const int dir = blockIdx.y, s0 = blockIdx.x * SEQ;
   const uint32_t salt = dir ? salt1 : salt0;
@@ -361,6 +368,31 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_bwd_kernel(
 #pragma unroll
     for (int ks = 0; ks < KS2; ++ks) A2[ks] = ap[ks * 64];
   }
+  const int ntw = w & 1, kg = w >> 1;   // dX_pos: this wave's tile and K-step group
+  u16x8_t Wp[4];                        // W_pos^T fragments (rows = position columns, zero rows >= np)
+  if (dxp != nullptr) {
+    const u16x8_t* wp = wpk + ((size_t)dir * KS2 + 4 * kg) * 64 + lane;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Wp[k] = wp[k * 64];
+  }
+  // sum of the NG partials of one processed step (buffer buf, time t) -> dxp[dir][s*L + t][0 .. np)
+  auto pos_reduce = [&](int buf, int t) {
+    for (int i = threadIdx.x; i < SEQ * 16; i += NTH) {
+      const int sl = i >> 4, j = i & 15, s = s0 + sl;
+      if (s < S && j < np) {
+        float v = 0.f;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) v += pimg[buf][((g * NT + (sl >> 4)) * 16 + (sl & 15)) * 16 + j];
+        dxp[(((size_t)dir * S + s) * L + t) * np + j] = v;
+      }
+    }
+  };
+  // a step's partial is stored one step later, just before that step's barrier: the store does not wait
+  // on its MFMA chain, and the sum still runs right after that barrier
+  f32x4_t pacc = {0.f, 0.f, 0.f, 0.f};
+  auto pos_store = [&](int buf) {
+    *reinterpret_cast<f32x4_t*>(&pimg[buf][((kg * NT + ntw) * 16 + n) * 16 + 4 * q]) = pacc;
+  };
   int srow[NT];
   bool sval[NT];
 #pragma unroll
@@ -447,7 +479,8 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_bwd_kernel(
       li[1] = g_hi;
       cn2[nt] = cur.cp[nt];
     }
-    __syncthreads();   // the dG image of this step is complete
+    if (dxp != nullptr && tau + 1 < L) pos_store((tau + 1) & 1);
+    __syncthreads();   // the dG image of this step is complete (and the previous step's dX_pos partials)
     if (tau > 0) {     // dh_{t-1} = dG W_h^T: two accumulators per tile (shorter dependent MFMA chains)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
@@ -460,6 +493,13 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_bwd_kernel(
         dhr[nt] = a0 + a1;
       }
     }
+    if (dxp != nullptr) {
+      if (tau + 1 < L) pos_reduce((tau + 1) & 1, dir ? L - 2 - tau : tau + 1);
+      const unsigned short* br = gcur + (ntw * 16 + n) * GS + 128 * kg + 8 * q;
+      pacc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pacc = mfma_bf16(Wp[k], *reinterpret_cast<const u16x8_t*>(br + 32 * k), pacc);
+    }
   };
   In b0, b1;   // ping-pong prefetch buffers (loop unrolled by two)
   load_in(L - 1, b0);
@@ -469,6 +509,11 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_bwd_kernel(
     step(tau - 1, b1, b0);
   }
   if (tau == 0) step(0, b0, b1);
+  if (dxp != nullptr) {
+    pos_store(0);
+    __syncthreads();   // the last processed step's (tau = 0) partials
+    pos_reduce(0, dir ? L - 1 : 0);
+  }
 }
 
 namespace ina {
@@ -492,7 +537,7 @@ static int wide_seq_bwd_t(const WideSeqArgs& a, hipStream_t st) {
   const dim3 grid((a.S + C::SEQ - 1) / C::SEQ, 2);
   hipLaunchKernelGGL(lstm_wide_seq_bwd_kernel<U>, grid, dim3(C::NW * 64), 0, st, (const unsigned short*)a.dH,
                      (const uint2*)a.acts, (const uint2*)a.cst, (const u16x8_t*)a.a2pk, (unsigned short*)a.dG, a.S, a.L,
-                     a.salt0, a.salt1, a.thr, a.inv_kp, a.drop);
+                     a.salt0, a.salt1, a.thr, a.inv_kp, a.drop, (const u16x8_t*)a.wpk, a.dxp, a.np);
   INA_CHECK_LAUNCH();
   return 0;
 }
@@ -614,10 +659,11 @@ __global__ __launch_bounds__(256) void wide_x_gather_kernel(const int* __restric
 // ids (pos[i][t] = pos[i][0] + t, ops/sampler.py::positions_are_shifted): table tb row p collects
 // dX[s][p - p0(s)][E + tb PD + c] over the sequences s with 0 <= p - p0(s) < L.  Thread = one output
 // (tb, p, c), grid.y = sequence chunks -> partials [chunks][2][P2][PD] (summed in order by the caller:
-// deterministic, no atomics).  dxp = dX's position columns, [S*L][2PD] fp32.
+// deterministic, no atomics).  dxp = dX's position columns, [planes][S*L][2PD] fp32 (planes = 2: the two
+// directions' contributions as the fused BiLSTM backward writes them, summed here).
 __global__ __launch_bounds__(256) void wide_pos_grad_kernel(const float* __restrict__ dxp, const int* __restrict__ inst,
                                                             const int* __restrict__ pos1, const int* __restrict__ pos2,
-                                                            int S, int L, int PD, int P2, int chunk,
+                                                            int S, int L, int PD, int P2, int chunk, int planes,
                                                             float* __restrict__ part) {
   const int o = blockIdx.x * 256 + threadIdx.x;
   const int nout = 2 * P2 * PD;
@@ -628,7 +674,10 @@ __global__ __launch_bounds__(256) void wide_pos_grad_kernel(const float* __restr
   float acc = 0.f;
   for (int s = s0; s < s1; ++s) {
     const int t = p - pos[(long)inst[s] * L];
-    if (t >= 0 && t < L) acc += dxp[((long)s * L + t) * 2 * PD + tb * PD + c];
+    if (t >= 0 && t < L) {
+      const long i = ((long)s * L + t) * 2 * PD + tb * PD + c;
+      acc += planes == 2 ? dxp[i] + dxp[i + (long)S * L * 2 * PD] : dxp[i];
+    }
   }
   part[(long)blockIdx.y * nout + o] = acc;
 }
@@ -654,11 +703,11 @@ int wide_x_gather(const int* inst, int S, int L, const int* word, const int* pos
 }
 
 int wide_pos_grad(const float* dxp, const int* inst, const int* pos1, const int* pos2, int S, int L, int PD, int P2,
-                  int chunks, float* part, hipStream_t st) {
+                  int chunks, int planes, float* part, hipStream_t st) {
   const int nout = 2 * P2 * PD;
   const int chunk = (S + chunks - 1) / chunks;
   hipLaunchKernelGGL(wide_pos_grad_kernel, dim3((nout + 255) / 256, chunks), dim3(256), 0, st, dxp, inst, pos1, pos2, S,
-                     L, PD, P2, chunk, part);
+                     L, PD, P2, chunk, planes, part);
   INA_CHECK_LAUNCH();
   return 0;
 }

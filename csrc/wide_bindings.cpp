@@ -141,9 +141,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_wide_seq_fwd(const Tensor& gx, c
   return {hout, hprev, acts, cst};
 }
 
-// dH [S, L, 2U] bf16 (gradient w.r.t. hout) + the forward's stash -> dG [S*L, 2 * 4UP] bf16 (both directions, permuted columns)
-Tensor lstm_wide_seq_bwd(const Tensor& dH, const Tensor& acts, const Tensor& cst, const Tensor& a2pk, int64_t S,
-                         int64_t L, int64_t U, int64_t seed, double keep_prob) {
+// dH [S, L, 2U] bf16 (gradient w.r.t. hout) + the forward's stash -> dG [S*L, 2 * 4UP] bf16 (both directions, permuted
+// columns) and, with wpk ([2][4UP/32][64][8] bf16 W_pos^T fragments, ops/wide.py::pos_frags; empty: none), the
+// input gradient's np position columns per direction dxp [2, S*L, np] fp32
+std::tuple<Tensor, Tensor> lstm_wide_seq_bwd(const Tensor& dH, const Tensor& acts, const Tensor& cst, const Tensor& a2pk,
+                                             int64_t S, int64_t L, int64_t U, int64_t seed, double keep_prob,
+                                             const Tensor& wpk, int64_t np) {
   TORCH_CHECK(ina::lstm_wide_seq_supported((int)U), "ina.lstm_wide_seq_bwd: U must be 64, 100 or 128");
   const int64_t UP = wide_up(U), G4 = 4 * UP, NW = UP / 16;
   chk(dH, "dH", at::kBFloat16, S * L * 2 * U);
@@ -151,7 +154,13 @@ Tensor lstm_wide_seq_bwd(const Tensor& dH, const Tensor& acts, const Tensor& cst
   chk(cst, "cst", at::kHalf, 2 * wide_seq_pad(S) * L * UP);
   chk(a2pk, "a2pk", at::kBFloat16, 2 * NW * (G4 / 32) * 64 * 8);
   auto dG = at::empty({S * L, 2 * G4}, dH.options());
-  if (S == 0) return dG;
+  const bool pg = wpk.numel() > 0;
+  if (pg) {
+    chk(wpk, "wpk", at::kBFloat16, 2 * (G4 / 32) * 64 * 8);
+    TORCH_CHECK(np >= 1 && np <= 16, "ina.lstm_wide_seq_bwd: 1 <= np <= 16 position columns");
+  }
+  auto dxp = at::empty({pg ? 2 : 0, S * L, pg ? np : 0}, dH.options().dtype(at::kFloat));
+  if (S == 0) return {dG, dxp};
   ina::WideSeqArgs a{};
   a.S = (int)S;
   a.L = (int)L;
@@ -161,6 +170,9 @@ Tensor lstm_wide_seq_bwd(const Tensor& dH, const Tensor& acts, const Tensor& cst
   a.cst = cst.data_ptr();
   a.a2pk = a2pk.data_ptr();
   a.dG = dG.data_ptr();
+  a.wpk = pg ? wpk.data_ptr() : nullptr;
+  a.dxp = pg ? dxp.data_ptr<float>() : nullptr;
+  a.np = pg ? (int)np : 0;
   ina::LstmWideArgs d{};
   fill_drop(d, seed, keep_prob);
   a.salt0 = d.salt0;
@@ -170,7 +182,7 @@ Tensor lstm_wide_seq_bwd(const Tensor& dH, const Tensor& acts, const Tensor& cst
   a.drop = d.drop;
   TORCH_CHECK(ina::lstm_wide_seq_bwd(a, c10::hip::getCurrentHIPStream().stream()) == 0,
               "ina.lstm_wide_seq_bwd: launch failed");
-  return dG;
+  return {dG, dxp};
 }
 
 bool lstm_wide_seq_ok(int64_t U) { return ina::lstm_wide_seq_supported((int)U); }
@@ -204,18 +216,21 @@ Tensor wide_x_gather(const Tensor& inst, const Tensor& word, const Tensor& pos1,
   return xb;
 }
 
-// position-table gradients [2, P2, PD] from dX's position columns dxp [S*L, 2PD] fp32 (shifted-arange ids)
+// position-table gradients [2, P2, PD] from dX's position columns dxp [S*L, 2PD] or [2, S*L, 2PD] (the two
+// directions' parts, summed) fp32 (shifted-arange ids)
 Tensor wide_pos_grad(const Tensor& dxp, const Tensor& inst, const Tensor& pos1, const Tensor& pos2, int64_t P2) {
   chk_ids(inst, "inst");
   chk_ids(pos1, "pos1");
   chk_ids(pos2, "pos2");
-  const int64_t S = inst.size(0), L = pos1.size(1), PD = dxp.size(1) / 2;
-  chk(dxp, "dxp", at::kFloat, S * L * 2 * PD);
+  TORCH_CHECK(dxp.dim() == 2 || (dxp.dim() == 3 && dxp.size(0) == 2), "ina.wide_pos_grad: dxp [S*L, 2PD] or [2, S*L, 2PD]");
+  const int64_t planes = dxp.dim() == 3 ? 2 : 1;
+  const int64_t S = inst.size(0), L = pos1.size(1), PD = dxp.size(-1) / 2;
+  chk(dxp, "dxp", at::kFloat, planes * S * L * 2 * PD);
   const int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(256, S / 64));
   auto part = at::empty({chunks, 2, P2, PD}, dxp.options());
   if (S == 0) return part.sum(0);
   TORCH_CHECK(ina::wide_pos_grad(dxp.data_ptr<float>(), inst.data_ptr<int>(), pos1.data_ptr<int>(), pos2.data_ptr<int>(),
-                                 (int)S, (int)L, (int)PD, (int)P2, (int)chunks, part.data_ptr<float>(),
+                                 (int)S, (int)L, (int)PD, (int)P2, (int)chunks, (int)planes, part.data_ptr<float>(),
                                  c10::hip::getCurrentHIPStream().stream()) == 0,
               "ina.wide_pos_grad: launch failed");
   return part.sum(0);

@@ -22,11 +22,15 @@ from ._ext import ops
 
 def _wgrad(a: torch.Tensor, b: torch.Tensor, split: int = 16) -> torch.Tensor:
     """a^T b in fp32 for tall bf16 a [T, m], b [T, n] (K = T split into `split` chunks: hipBLASLt runs a
-    single K = 1.2 M GEMM on a handful of output tiles; tools/gemm_probe.py measured 16-64 best)."""
+    single K = 1.2 M GEMM on a handful of output tiles; tools/gemm_probe.py measured 16-64 best for the
+    x-projection, 128 for the 256 x 256 attention weight).  A T that `split` does not divide takes the
+    largest smaller power-of-two split that does."""
     T = a.shape[0]
-    if T % split == 0 and T >= 256 * split:
-        part = torch.bmm(a.view(split, T // split, -1).transpose(1, 2), b.view(split, T // split, -1),
-                         out_dtype=torch.float32)
+    sp = split
+    while sp > 1 and (T % sp or T < 256 * sp):
+        sp //= 2
+    if sp > 1:
+        part = torch.bmm(a.view(sp, T // sp, -1).transpose(1, 2), b.view(sp, T // sp, -1), out_dtype=torch.float32)
         return part.sum(0)
     return torch.mm(a.t(), b, out_dtype=torch.float32)
 
@@ -165,7 +169,13 @@ class WideSeqBiLSTM(torch.autograd.Function):
         inst, word, pos1, pos2, Xb, wxtc, a2pk, hprev, acts, cst = ctx.saved_tensors
         S, L, E, P, U, seed, kp, shift, P2, V = ctx.cfg
         D = E + 2 * P
-        dG = o.lstm_wide_seq_bwd(dout.contiguous().to(torch.bfloat16), acts, cst, a2pk, S, L, U, seed, kp)
+        need_w = ctx.needs_input_grad[4]
+        # the position columns of the input gradient straight from the BPTT kernel (dG W_pos^T on the LDS
+        # image of each step's dG); the word columns only for a trainable word table, as a GEMM
+        fuse = not need_w and 2 * P <= 16
+        wpk = pos_frags(wxtc, E, D) if fuse else wxtc.new_empty(0)
+        dG, dxpd = o.lstm_wide_seq_bwd(dout.contiguous().to(torch.bfloat16), acts, cst, a2pk, S, L, U, seed, kp,
+                                       wpk, 2 * P)
         UP, G4 = hprev.shape[-1], dG.shape[1] // 2
         # ONE GEMM for both directions' x-kernel gradients; Xb's ones column (row D) makes it the bias
         # gradient as well (no separate column-sum pass over dG)
@@ -176,14 +186,18 @@ class WideSeqBiLSTM(torch.autograd.Function):
             dK, db = unpack_wide_grads(dwx[:D, c], _wgrad(hprev[d].reshape(S * L, UP), dG[:, c], 64), dwx[D, c], U)
             dKs.append(dK)
             dbs.append(db)
-        need_w = ctx.needs_input_grad[4]
-        cols = slice(0, D) if need_w else slice(E, D)
-        dX = torch.mm(dG, wxtc[cols].t(), out_dtype=torch.float32)      # both directions: K = 2 G4
-        dxp = dX[:, -2 * P:].contiguous()
+        if fuse:
+            dxp = dxpd                                                    # [2, S*L, 2P]: per direction
+        else:
+            cols = slice(0, D) if need_w else slice(E, D)
+            dX = torch.mm(dG, wxtc[cols].t(), out_dtype=torch.float32)  # both directions: K = 2 G4
+            dxp = dX[:, -2 * P:].contiguous()
         if shift:
-            tp = o.wide_pos_grad(dxp, inst, pos1, pos2, P2)
+            tp = o.wide_pos_grad(dxp, inst, pos1, pos2, P2)             # sums the direction planes
             dp1, dp2 = tp[0], tp[1]
         else:
+            if dxp.dim() == 3:
+                dxp = dxp.sum(0)
             il = inst.long()
             dp1 = table_grad(pos1[il].reshape(-1).long(), dxp[:, :P], P2)
             dp2 = table_grad(pos2[il].reshape(-1).long(), dxp[:, P:], P2)
@@ -191,6 +205,16 @@ class WideSeqBiLSTM(torch.autograd.Function):
         if need_w:
             dw = table_grad(word[inst.long()].reshape(-1).long(), dX[:, :E], V)
         return (None, None, None, None, dw, dp1, dp2, dKs[0], dbs[0], dKs[1], dbs[1], None, None, None, None, None)
+
+
+def pos_frags(wxtc: torch.Tensor, E: int, D: int) -> torch.Tensor:
+    """MFMA A fragments of W_pos^T for the BPTT kernel's fused dX_pos (csrc/kernels/lstm_wide.hip): rows
+    E .. D of wxtc [D, 2 G4] (the position columns' x-projection weights, permuted gate columns, unscaled)
+    zero-padded to 16 rows -> [2 dirs][G4 / 32 K-steps][64 lanes][8] bf16, lane = 16 q + n holding row n,
+    gate columns 32 ks + 8 q .. + 8 of its direction."""
+    G4 = wxtc.shape[1] // 2
+    wp = torch.nn.functional.pad(wxtc[E:D], (0, 0, 0, 16 - (D - E)))                # [16, 2 G4]
+    return wp.view(16, 2, G4 // 32, 4, 8).permute(1, 2, 3, 0, 4).contiguous().to(torch.bfloat16)
 
 
 def table_grad(idx: torch.Tensor, d: torch.Tensor, rows: int) -> torch.Tensor:
@@ -278,7 +302,7 @@ class WideAttn(torch.autograd.Function):
         H = Hb.shape[-1]
         dH, dZ, part = ops().wide_attn_bwd(Hb, inst, mask, pk["w1t"], pk["w1"], pk["b1"], pk["w2"], alpha,
                                            de.contiguous().float())
-        dW1 = _wgrad(Hb.reshape(-1, H), dZ) if ctx.needs_input_grad[3] else None
+        dW1 = _wgrad(Hb.reshape(-1, H), dZ, 128) if ctx.needs_input_grad[3] else None
         ps = part.sum(0)
         return dH, None, None, dW1, ps[1, :H], ps[0, :H].unsqueeze(1), None
 

@@ -57,6 +57,36 @@ def test_paper_config_forward_backward_vs_oracle(keep_prob, u):
         assert _relerr(got[k], p[k].grad) < 8e-2, k
 
 
+@pytest.mark.parametrize("U", [128, 100, 64])
+def test_bwd_fused_position_columns_match_gemm(U):
+    """The BPTT kernel's fused dX_pos (dG W_pos^T from each step's LDS dG image, per direction) against the
+    GEMM over the dG it writes; dG itself is unchanged by the fusion.  S = 77: a partial 32-sequence tile."""
+    from induction_network_on_fewrel_amd.ops._ext import ops
+    from induction_network_on_fewrel_amd.ops.packing import pack_lstm_wide, wide_x_cols
+    from induction_network_on_fewrel_amd.ops.wide import pos_frags
+    o = ops()
+    g = torch.Generator().manual_seed(0)
+    S, L, E, P = 77, 37, 50, 5
+    D = E + 2 * P
+    Kf, Kb = (torch.randn(D + U, 4 * U, generator=g) * 0.1 for _ in range(2))
+    bf, bb = (torch.randn(4 * U, generator=g) * 0.1 for _ in range(2))
+    pk = pack_lstm_wide(Kf.to(DEV), bf.to(DEV), Kb.to(DEV), bb.to(DEV), U, D)
+    X = torch.randn(S * L, wide_x_cols(D), generator=g).to(DEV).bfloat16()
+    gx = torch.mm(X, pk["wxc"])
+    _, _, acts, cst = o.lstm_wide_seq_fwd(gx, pk["bx"], pk["apk"], S, L, U, True, 7, 0.9)
+    dH = torch.randn(S, L, 2 * U, generator=g).to(DEV).bfloat16()
+    dG0, none = o.lstm_wide_seq_bwd(dH, acts, cst, pk["a2pk"], S, L, U, 7, 0.9, X.new_empty(0), 2 * P)
+    dG, dxp = o.lstm_wide_seq_bwd(dH, acts, cst, pk["a2pk"], S, L, U, 7, 0.9, pos_frags(pk["wxtc"], E, D), 2 * P)
+    torch.cuda.synchronize()
+    assert none.numel() == 0 and dxp.shape == (2, S * L, 2 * P)
+    assert torch.equal(dG, dG0)
+    G4 = dG.shape[1] // 2
+    for d in range(2):
+        c = slice(d * G4, (d + 1) * G4)
+        want = torch.mm(dG[:, c].float(), pk["wxtc"][E:D, c].float().t())
+        assert float((dxp[d] - want).abs().max()) <= 1e-5 * float(want.abs().max()), d
+
+
 @pytest.mark.parametrize("u", [129, 130])
 def test_odd_and_unaligned_width_per_step_loop_vs_oracle(u):
     """Widths above the last kernel instantiation that are odd or not multiples of 4 run the

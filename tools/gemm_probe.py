@@ -44,3 +44,16 @@ bench("dX pos mm(G, W[1024,10])", lambda: torch.mm(G, Wp, out_dtype=torch.float3
 Wp16 = torch.randn(1024, 16, device=dev, dtype=bf)
 bench("dX pos mm(G, W[1024,16])", lambda: torch.mm(G, Wp16, out_dtype=torch.float32))
 bench("dX pos mm(G, W16) bf16 out", lambda: torch.mm(G, Wp16))
+# round 5: the attention weight gradient dW1 = H^T dZ (H = 2u = 256) and split counts that fill 256 CUs
+Hb = torch.randn(T, 256, device=dev, dtype=bf)
+dZ = torch.randn(T, 256, device=dev, dtype=bf)
+for sp in (16, 32, 50, 64, 100, 128):
+    bench(f"dW1 split{sp} bmm [256x256]", lambda: torch.bmm(Hb.view(sp, T // sp, 256).transpose(1, 2),
+                                                             dZ.view(sp, T // sp, 256), out_dtype=torch.float32).sum(0))
+X = torch.randn(T, 320, device=dev, dtype=bf)
+for sp in (16, 20, 25, 32, 40):
+    bench(f"dwx split{sp} bmm K=320", lambda: torch.bmm(X.view(sp, T // sp, 320).transpose(1, 2), G.view(sp, T // sp, 1024),
+                                                        out_dtype=torch.float32).sum(0))
+for sp in (32, 50, 100, 128):
+    bench(f"dwh strided split{sp}", lambda: torch.bmm(Hp[0].view(sp, T // sp, 128).transpose(1, 2),
+                                                      G[:, :512].view(sp, T // sp, 512), out_dtype=torch.float32).sum(0))

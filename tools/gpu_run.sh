@@ -4,6 +4,7 @@
 #   BENCH="name|ENV=V ...|bench args;..."      bench.py runs, each with its own env assignments (empty: none)
 #   PROF="name|ENV=V ...|bench args;..."       rocprofv3 --kernel-trace --stats runs of bench.py, summarised by
 #                                              tools/rocpd_summary.py into OUT/<name>_sum.txt
+#   SEQ="<kernel-name substring>"              also OUT/<name>_seq.txt: the last profiled step's kernel sequence
 #   bash tools/gpu_run.sh OUT
 # Every step has its own time limit; the script stops at the first failure (no GPU step after a fault).
 set -o pipefail
@@ -37,5 +38,6 @@ for r in "${PRUNS[@]}"; do
   [ $rc -ne 0 ] && { tail -5 $OUT/${name}_prof.log; exit $rc; }
   db=$(ls /tmp/prof_$name/*/*.db /tmp/prof_$name/*.db 2>/dev/null | head -1)
   python tools/rocpd_summary.py $db --steps ${PROF_STEPS:-25} --top 30 > $OUT/${name}_sum.txt 2>&1
+  [ -n "$SEQ" ] && python tools/rocpd_summary.py $db --sequence "$SEQ" > $OUT/${name}_seq.txt 2>&1
   head -14 $OUT/${name}_sum.txt
 done

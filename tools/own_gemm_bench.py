@@ -2,7 +2,9 @@
 """Own gfx950 GEMM (ina.bert_gemm, csrc/kernels/gemm.hip) vs hipBLASLt (torch.mm / addmm) + the separate
 bias+GELU passes at the BERT-base FFN shapes, T = 102,400 tokens (10-way 5-shot Q=5, 8 episodes, L=128).
 
-Prints one JSON line per case: us per call and TFLOP/s (2 M N K / t, random operands)."""
+Prints one JSON line per case: us per call and TFLOP/s (2 M N K / t, random operands).
+usage: own_gemm_bench.py [T] [N,K ...]   (other shapes, e.g. the paper configuration's x-projection:
+       own_gemm_bench.py 1184000 1024,320)"""
 import json
 import sys
 
@@ -28,7 +30,8 @@ def main():
     o = ops()
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 102400
     dev = torch.device("cuda")
-    for (N, K) in ((3072, 768), (768, 3072), (2304, 768), (768, 768)):
+    shapes = [tuple(int(v) for v in a.split(",")) for a in sys.argv[2:]] or [(3072, 768), (768, 3072), (2304, 768), (768, 768)]
+    for (N, K) in shapes:
         x = torch.randn(T, K, device=dev).bfloat16()
         w = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
         b = torch.randn(N, device=dev)
