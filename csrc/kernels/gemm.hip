@@ -67,6 +67,9 @@ enum { EPI_PLAIN = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_PLAIN_B = 3 };  // 3: pla
 #ifndef INA_GEMM_DIAG
 #define INA_GEMM_DIAG 0  // 1: no operand staging inside the K loop (diagnostic of the MFMA/LDS/barrier skeleton)
 #endif
+#ifndef INA_GEMM_NOSTORE
+#define INA_GEMM_NOSTORE 0  // 1: the epilogue stores nothing (diagnostic: the K loop + staging without the C writes)
+#endif
 
 struct GemmArgs {
   const unsigned short* A;
@@ -274,6 +277,26 @@ INA_DEVICE void kstep(f32x4_t (&acc)[8][4], Frags& f, const Stager& sg, bool ful
   barrier();
 }
 
+// Store widening: lane group fq holds X = columns 4 fq .. 4 fq + 3 of tile nt = 2h and Y = columns 16 + 4 fq ..
+// of tile 2h + 1 (4 bf16 each, one row).  permlane32_swap (upper half of X <-> lower half of Y) then
+// permlane16_swap (odd 16-lane rows of X <-> even rows of Y) leave lane group fq with columns 8 fq .. 8 fq + 7
+// as (X, Y): one 16-byte store per lane, 16 rows x 64 B per instruction instead of two of 16 rows x 32 B
+// (the C write of a short-K GEMM is store-issue bound: cdna_hip_programming.md T21).
+INA_DEVICE void widen(uint2& X, uint2& Y) {
+  auto r = __builtin_amdgcn_permlane32_swap(X.x, Y.x, false, false);
+  X.x = r[0];
+  Y.x = r[1];
+  r = __builtin_amdgcn_permlane32_swap(X.y, Y.y, false, false);
+  X.y = r[0];
+  Y.y = r[1];
+  r = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
+  X.x = r[0];
+  Y.x = r[1];
+  r = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
+  X.y = r[0];
+  Y.y = r[1];
+}
+
 // acc[mt][nt][r] = C[m0 + mrow(mt) + fr][n0 + ncol(nt) + 4 fq + r]
 template <int EPI>
 INA_DEVICE void epilogue(f32x4_t (&acc)[8][4], const GemmArgs& g, int m0, int n0, int wr, int wc, int fr, int fq) {
@@ -304,9 +327,9 @@ INA_DEVICE void epilogue(f32x4_t (&acc)[8][4], const GemmArgs& g, int m0, int n0
         xv[nt] = *reinterpret_cast<const u16x4_t*>(g.aux + mrow * g.ldx + n);
       }
     }
+    u16x4_t ov[4], axv[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const int n = n0 + (nt >> 1) * 128 + wc * 32 + (nt & 1) * 16 + 4 * fq;
       const float bv[4] = {bb[nt][0], bb[nt][1], bb[nt][2], bb[nt][3]};
       u16x4_t o, ax;
 #pragma unroll
@@ -324,9 +347,20 @@ INA_DEVICE void epilogue(f32x4_t (&acc)[8][4], const GemmArgs& g, int m0, int n0
           cs[nt][r] += d;
         }
       }
-      if (ok) {
-        *reinterpret_cast<u16x4_t*>(g.out + mrow * g.ldo + n) = o;
-        if constexpr (EPI == EPI_GELU) *reinterpret_cast<u16x4_t*>(g.aux + mrow * g.ldx + n) = ax;
+      ov[nt] = o;
+      axv[nt] = ax;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int n = n0 + h * 128 + wc * 32 + 8 * fq;
+      uint2 X = __builtin_bit_cast(uint2, ov[2 * h]), Y = __builtin_bit_cast(uint2, ov[2 * h + 1]);
+      widen(X, Y);
+      if (ok && (!INA_GEMM_NOSTORE || X.x == 0x7FC17FC1u))   // (diagnostic: a never-true use keeps the MFMAs)
+        *reinterpret_cast<uint4*>(g.out + mrow * g.ldo + n) = uint4{X.x, X.y, Y.x, Y.y};
+      if constexpr (EPI == EPI_GELU) {
+        uint2 Xa = __builtin_bit_cast(uint2, axv[2 * h]), Ya = __builtin_bit_cast(uint2, axv[2 * h + 1]);
+        widen(Xa, Ya);
+        if (ok) *reinterpret_cast<uint4*>(g.aux + mrow * g.ldx + n) = uint4{Xa.x, Xa.y, Ya.x, Ya.y};
       }
     }
   }
@@ -473,10 +507,12 @@ namespace ina {
 int gemm_bf16_nt(const void* A, int lda, const void* B, int ldb, int M, int N, int K, const float* bias, void* out,
                  int ldo, void* aux, int ldx, float* slab, int epi, hipStream_t st) {
   if (M <= 0 || N <= 0 || N % G_BN != 0 || K < G_BK || K % G_BK != 0) return 1;
-  if (lda % 8 != 0 || ldb % 8 != 0 || ldo % 4 != 0 || lda < K || ldb < K || ldo < N) return 1;
+  // 16-byte epilogue stores (widen): ldo / ldx multiples of 8 elements, 16-byte aligned bases
+  if (lda % 8 != 0 || ldb % 8 != 0 || ldo % 8 != 0 || lda < K || ldb < K || ldo < N) return 1;
+  if (((uintptr_t)out & 15) != 0 || ((uintptr_t)aux & 15) != 0) return 1;
   // 32-bit byte offsets of the DMA sources
   if ((long)M * lda * 2 >= (1L << 31) || (long)N * ldb * 2 >= (1L << 31)) return 1;
-  if (epi != EPI_PLAIN && (aux == nullptr || ldx % 4 != 0 || ldx < N)) return 1;
+  if (epi != EPI_PLAIN && (aux == nullptr || ldx % 8 != 0 || ldx < N)) return 1;
   if (epi == EPI_GELU && bias == nullptr) return 1;
   if (epi == EPI_DGELU && slab == nullptr) return 1;
   GemmArgs a{(const unsigned short*)A, (const unsigned short*)B, bias, (unsigned short*)out, (unsigned short*)aux,

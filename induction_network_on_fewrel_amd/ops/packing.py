@@ -350,6 +350,7 @@ def pack_lstm_wide(Kf: torch.Tensor, bf: torch.Tensor, Kb: torch.Tensor, bb: tor
     column dir * G4 + c, so ONE GEMM covers them):
       wxc  [DP, 2 G4] bf16  x-projection, exp2-pre-scaled, zero rows D .. DP (the ones / pad columns
                             of Xb: the fp32 bias is added in-kernel)
+      wxcT [2 G4, DP] bf16  wxc transposed (the own GEMM's K-contiguous B operand)
       wxtc [D, 2 G4]  bf16  the same columns UNscaled (dX = dG wxtc^T)
       wxt  [2, D, G4] bf16  per-direction view of wxtc
       bx   [2, G4]    fp32  bias (+1 on the forget gate), pre-scaled
@@ -385,7 +386,8 @@ def pack_lstm_wide(Kf: torch.Tensor, bf: torch.Tensor, Kb: torch.Tensor, bb: tor
         outs["a2pk"].append(bfl(Wh[bwd_i]))
     wxtc = bfl(torch.cat(outs["wxt"], 1))
     G4 = wxtc.shape[1] // 2
-    return {"wxc": bfl(torch.cat(outs["wx"], 1)), "wxtc": wxtc,
+    wxc = bfl(torch.cat(outs["wx"], 1))
+    return {"wxc": wxc, "wxcT": wxc.t().contiguous(), "wxtc": wxtc,
             "wxt": wxtc.view(D, 2, G4).transpose(0, 1),
             "bx": torch.stack(outs["bx"]).contiguous(), "apk": torch.stack(outs["apk"]).contiguous(),
             "a2pk": torch.stack(outs["a2pk"]).contiguous()}

@@ -126,6 +126,17 @@ def word_table_bf16(wemb: torch.Tensor) -> torch.Tensor:
     return tab
 
 
+def x_projection(Xb: torch.Tensor, pk: dict) -> torch.Tensor:
+    """Xb [T, DP] x wxc [DP, 2 G4] -> bf16 [T, 2 G4] on the own GEMM (csrc/kernels/gemm.hip; its widened
+    16-byte epilogue stores: 1.12 ms against hipBLASLt's 1.23 ms at the paper configuration,
+    profiles/r5_widen) where its limits hold (N % 256, K % 64, 32-bit operand offsets), else hipBLASLt."""
+    M, K = Xb.shape
+    wt = pk.get("wxcT")
+    if wt is not None and wt.shape[0] % 256 == 0 and K % 64 == 0 and M * K * 2 < (1 << 31) and Xb.is_contiguous():
+        return ops().bert_gemm(Xb, wt, None, None, 0)[0]
+    return torch.mm(Xb, pk["wxc"])
+
+
 class WideSeqBiLSTM(torch.autograd.Function):
     """Embedding + BiLSTM of the wide path on hand-written kernels (lstm_wide.hip, U in {64, 100, 128}):
       wide_x_gather     the encoder input rows Xb [S*L, DP] bf16 in one pass (E + 2PD embedding columns,
@@ -153,7 +164,7 @@ class WideSeqBiLSTM(torch.autograd.Function):
                              p2emb.detach().float().contiguous())
         # x W_x for both directions as ONE bf16-output GEMM (the kernel adds the fp32 biases): an fp32 output
         # plus a separate bias pass moved ~15 GB per step at the paper configuration
-        gx = torch.mm(Xb, pk["wxc"])
+        gx = x_projection(Xb, pk)
         need = any(ctx.needs_input_grad[4:11])
         hout, hprev, acts, cst = o.lstm_wide_seq_fwd(gx, pk["bx"], pk["apk"], S, L, U, bool(need), int(seed),
                                                      float(keep_prob))

@@ -22,7 +22,7 @@ from .packing import pack_attn_wide, pack_lstm_wide
 
 _LSTM = ("Kf", "bf", "Kb", "bb")
 _ATTN = ("W1", "b1", "w2")
-_BF16 = ("wxc", "wxtc", "apk", "a2pk", "w1t", "w1")     # output order, bf16 region
+_BF16 = ("wxc", "wxcT", "wxtc", "apk", "a2pk", "w1t", "w1")     # output order, bf16 region
 _F32 = ("bx", "b1", "w2")                               # fp32 region
 _PLANS: Dict[tuple, tuple] = {}
 
@@ -43,7 +43,7 @@ def _flat_of(ts) -> Optional[Tuple[torch.Tensor, Tuple[int, ...]]]:
 def _packs(vals, U: int, D: int, scaled: bool):
     lw = pack_lstm_wide(*vals[:4], U, D, scaled=scaled, cast=False)
     aw = pack_attn_wide(*vals[4:], cast=False)
-    out = {k: lw[k] for k in ("wxc", "wxtc", "apk", "a2pk", "bx")}
+    out = {k: lw[k] for k in ("wxc", "wxcT", "wxtc", "apk", "a2pk", "bx")}
     out.update({k: aw[k] for k in ("w1t", "w1", "b1", "w2")})
     return out
 

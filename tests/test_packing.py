@@ -156,6 +156,7 @@ def test_wide_lstm_packs_emulated_mfma():
             wxt = p["wxt"][d].float()
             assert torch.equal(p["wxtc"][:, d * G4:(d + 1) * G4], p["wxt"][d])
             assert p["wxc"].shape == (-(-(D + 1) // 32) * 32, 2 * G4) and float(p["wxc"][D:].abs().sum()) == 0.0
+            assert torch.equal(p["wxcT"], p["wxc"].t())
             assert torch.allclose(wxt[:, 4 * 3 + 2], K[:D, 2 * U + 3].bfloat16().float())
             assert abs(float(p["bx"][d][4 * 5 + 2]) - (float(b[2 * U + 5]) + 1.0) * LOG2E) < 1e-5
             dK, db = unpack_wide_grads(wxt, torch.nn.functional.pad(K[D:].bfloat16().float()[:, :0], (0, G4)),
