@@ -5,7 +5,7 @@ Per layer (post-LN BERT, models/bert.py is the oracle):
                                      flat bf16 weight copy (q/k/v are adjacent in the flat buffer)
     ctx = MHA(qkv)                   ina.bert_mha_fwd / _bwd   (fused, sequence in LDS, MFMA)
     x1  = LN(x + drop(ctx Wo^T+bo))  addmm + ina.bert_ln_res_fwd / _bwd
-    h   = gelu(x1 W1^T + b1)         mm + ina.bert_bias_gelu_fwd / _bwd, or (INA_BERT_OWN_GEMM=1) _Ffn: the
+    h   = gelu(x1 W1^T + b1)         _Ffn (default; INA_BERT_OWN_GEMM=0: mm + ina.bert_bias_gelu_fwd / _bwd): the
                                      own gemm.hip kernel with bias + GELU / GELU' + db in its epilogues
     x2  = LN(x1 + drop(h W2^T+b2))   addmm + ina.bert_ln_res_fwd / _bwd
 Embeddings: ina.bert_embed_ln_fwd / _bwd (gather by instance index, no host copies); the word-table
@@ -176,10 +176,11 @@ class _Ffn(torch.autograd.Function):
 
 
 def own_ffn_enabled(I: int, Hd: int) -> bool:
-    """The own-GEMM FFN (INA_BERT_OWN_GEMM=1; default off: measured at parity with hipBLASLt + the separate
-    bias / GELU passes -- BERT 10w5s 108.9 / 109.2 vs 109.6 / 110.0 episodes/s, profiles/r4_own_gemm).
-    Needs N = I a multiple of 256 and K = Hd a multiple of 64."""
-    return os.environ.get("INA_BERT_OWN_GEMM", "0") != "0" and I % 256 == 0 and Hd % 64 == 0
+    """The own-GEMM FFN (default on since its 16-byte epilogue stores, round 5: BERT 10w5s 108.72 / 108.70 vs
+    108.57 / 108.38 episodes/s with hipBLASLt + the separate bias / GELU passes, profiles/r5_widen/bert_ab;
+    round 4 measured it at parity).  INA_BERT_OWN_GEMM=0 selects the hipBLASLt path.  Needs N = I a
+    multiple of 256 and K = Hd a multiple of 64."""
+    return os.environ.get("INA_BERT_OWN_GEMM", "1") != "0" and I % 256 == 0 and Hd % 64 == 0
 
 
 class _ResGrad:
