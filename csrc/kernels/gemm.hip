@@ -297,9 +297,87 @@ INA_DEVICE void widen(uint2& X, uint2& Y) {
   Y.y = r[1];
 }
 
+// The inverse exchange (each swap is an involution): a 16-byte row chunk loaded in the widened layout (lane
+// group fq: columns 8 fq .. 8 fq + 7) back to the accumulator layout (X: tile 2h columns 4 fq .., Y: tile 2h + 1).
+// (The widening is applied to VALU results only: a permlane swap reading an MFMA accumulator directly gets no
+// MFMA -> VALU wait states from hipcc and read stale values.)
+INA_DEVICE void unwiden(uint2& X, uint2& Y) {
+  auto r = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
+  X.x = r[0];
+  Y.x = r[1];
+  r = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
+  X.y = r[0];
+  Y.y = r[1];
+  r = __builtin_amdgcn_permlane32_swap(X.x, Y.x, false, false);
+  X.x = r[0];
+  Y.x = r[1];
+  r = __builtin_amdgcn_permlane32_swap(X.y, Y.y, false, false);
+  X.y = r[0];
+  Y.y = r[1];
+}
+
+// EPI_DGELU: per (row tile mt, half h) ONE 16-byte aux load per lane (the widened layout, unwidened in
+// registers) instead of two 8-byte ones, all 16 of the wave's aux loads issued before the first use; d in the
+// accumulator layout (bias-gradient column sums as before), stored widened.
+INA_DEVICE void epilogue_dgelu(const f32x4_t (&acc)[8][4], const GemmArgs& g, int m0, int n0, int wr, int wc, int fr,
+                               int fq) {
+  uint4 xa[8][2];
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) {
+    const int m = m0 + (mt >> 2) * 128 + wr * 64 + (mt & 3) * 16 + fr;
+    const size_t mrow = (size_t)(m < g.M ? m : 0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      xa[mt][h] = *reinterpret_cast<const uint4*>(g.aux + mrow * g.ldx + n0 + h * 128 + wc * 32 + 8 * fq);
+  }
+  float cs[4][4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cs[nt][r] = 0.f;
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) {
+    const int m = m0 + (mt >> 2) * 128 + wr * 64 + (mt & 3) * 16 + fr;
+    const bool ok = m < g.M;
+    const size_t mrow = (size_t)(ok ? m : 0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint2 ax = uint2{xa[mt][h].x, xa[mt][h].y}, ay = uint2{xa[mt][h].z, xa[mt][h].w};
+      unwiden(ax, ay);
+      const u16x4_t xv[2] = {__builtin_bit_cast(u16x4_t, ax), __builtin_bit_cast(u16x4_t, ay)};
+      u16x4_t o[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = ok ? acc[mt][2 * h + j][r] * gelu_d(bf2f(xv[j][r])) : 0.f;
+          o[j][r] = f2bf(d);
+          cs[2 * h + j][r] += d;
+        }
+      uint2 X = __builtin_bit_cast(uint2, o[0]), Y = __builtin_bit_cast(uint2, o[1]);
+      widen(X, Y);
+      if (ok) *reinterpret_cast<uint4*>(g.out + mrow * g.ldo + n0 + h * 128 + wc * 32 + 8 * fq) = uint4{X.x, X.y, Y.x, Y.y};
+    }
+  }
+  float* srow = g.slab + (size_t)(2 * (m0 / G_BM) + wr) * g.N;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    float4 sv;
+    sv.x = group16_sum(cs[nt][0]);
+    sv.y = group16_sum(cs[nt][1]);
+    sv.z = group16_sum(cs[nt][2]);
+    sv.w = group16_sum(cs[nt][3]);
+    if (fr == 0) *reinterpret_cast<float4*>(srow + n0 + (nt >> 1) * 128 + wc * 32 + (nt & 1) * 16 + 4 * fq) = sv;
+  }
+}
+
 // acc[mt][nt][r] = C[m0 + mrow(mt) + fr][n0 + ncol(nt) + 4 fq + r]
 template <int EPI>
 INA_DEVICE void epilogue(f32x4_t (&acc)[8][4], const GemmArgs& g, int m0, int n0, int wr, int wc, int fr, int fq) {
+  if constexpr (EPI == EPI_DGELU) {
+    epilogue_dgelu(acc, g, m0, n0, wr, wc, fr, fq);
+    return;
+  }
   float cs[4][4];
   f32x4_t bb[4];
 #pragma unroll
