@@ -211,6 +211,47 @@ INA_DEVICE float cross_group_max(float v) {
   return fmaxf(a, b);
 }
 INA_DEVICE float wave_sum(float v) { return cross_group_sum(group16_sum(v)); }
+
+// Store widening: lane group fq holds X = columns 4 fq .. 4 fq + 3 of tile nt = 2h and Y = columns 16 + 4 fq ..
+// of tile 2h + 1 (4 bf16 each, one row).  permlane32_swap (upper half of X <-> lower half of Y) then
+// permlane16_swap (odd 16-lane rows of X <-> even rows of Y) leave lane group fq with columns 8 fq .. 8 fq + 7
+// as (X, Y): one 16-byte store per lane, 16 rows x 64 B per instruction instead of two of 16 rows x 32 B
+// (the C write of a short-K GEMM is store-issue bound: cdna_hip_programming.md T21; used by gemm.hip and
+// attn_wide.hip).  Semantics checked by tools/lds_probe/permlane_probe.hip.
+INA_DEVICE void widen(uint2& X, uint2& Y) {
+  auto r = __builtin_amdgcn_permlane32_swap(X.x, Y.x, false, false);
+  X.x = r[0];
+  Y.x = r[1];
+  r = __builtin_amdgcn_permlane32_swap(X.y, Y.y, false, false);
+  X.y = r[0];
+  Y.y = r[1];
+  r = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
+  X.x = r[0];
+  Y.x = r[1];
+  r = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
+  X.y = r[0];
+  Y.y = r[1];
+}
+
+// The inverse exchange (each swap is an involution): a 16-byte row chunk loaded in the widened layout (lane
+// group fq: columns 8 fq .. 8 fq + 7) back to the accumulator layout (X: tile 2h columns 4 fq .., Y: tile 2h + 1).
+// (The widening is applied to VALU results only: a permlane swap reading an MFMA accumulator directly gets no
+// MFMA -> VALU wait states from hipcc and read stale values.)
+INA_DEVICE void unwiden(uint2& X, uint2& Y) {
+  auto r = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
+  X.x = r[0];
+  Y.x = r[1];
+  r = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
+  X.y = r[0];
+  Y.y = r[1];
+  r = __builtin_amdgcn_permlane32_swap(X.x, Y.x, false, false);
+  X.x = r[0];
+  Y.x = r[1];
+  r = __builtin_amdgcn_permlane32_swap(X.y, Y.y, false, false);
+  X.y = r[0];
+  Y.y = r[1];
+}
+
 INA_DEVICE float wave_max(float v) { return cross_group_max(group16_max(v)); }
 
 // Deterministic workgroup reduction: the waves add their contributions into a shared LDS buffer one

@@ -257,19 +257,24 @@ __global__ __launch_bounds__(AttnCfg<HP>::NTH) void wide_attn_fwd_kernel(WideAtt
       }
     }
     __syncthreads();
-    // e = sum_t alpha_t H_t (fp32), two features per thread
-    const int H2 = H / 2;
-    for (int i = threadIdx.x; i < b.nseq * H2; i += NTH) {
-      const int sl = i / H2, f = 2 * (i - sl * H2);
-      float e0 = 0.f, e1 = 0.f;
-      for (int t = 0; t < L; ++t) {
-        const int tok = sl * L + t;
-        const float al = alp[tok];
-        const uint32_t hv = *reinterpret_cast<const uint32_t*>(hb + tok * HS + f);
-        e0 += al * bf2f((unsigned short)hv);
-        e1 += al * bf2f((unsigned short)(hv >> 16));
+    // e = sum_t alpha_t H_t (fp32): one feature per thread (every wave busy: SB H = 512 at the paper
+    // configuration), the token loop unrolled by 4 into independent partial sums so 4 tokens' LDS reads are
+    // in flight (the two-features-per-thread serial loop left half the waves idle on a 37-step LDS-latency
+    // chain per block)
+    for (int i = threadIdx.x; i < b.nseq * H; i += NTH) {
+      const int sl = i / H, f = i - sl * H;
+      const unsigned short* hp = hb + (sl * L) * HS + f;
+      const float* ap = alp + sl * L;
+      float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;
+      int t = 0;
+      for (; t + 4 <= L; t += 4) {
+        e0 += ap[t] * bf2f(hp[t * HS]);
+        e1 += ap[t + 1] * bf2f(hp[(t + 1) * HS]);
+        e2 += ap[t + 2] * bf2f(hp[(t + 2) * HS]);
+        e3 += ap[t + 3] * bf2f(hp[(t + 3) * HS]);
       }
-      *reinterpret_cast<float2*>(a.e + (size_t)(b.s0 + sl) * H + f) = float2{e0, e1};
+      for (; t < L; ++t) e0 += ap[t] * bf2f(hp[t * HS]);
+      a.e[(size_t)(b.s0 + sl) * H + f] = (e0 + e1) + (e2 + e3);
     }
   }
 }
@@ -407,18 +412,19 @@ __global__ __launch_bounds__(AttnCfg<HP>::NTH) void wide_attn_bwd_kernel(WideAtt
         acc[0] = mfma_bf16(A2[0][ks], B, acc[0]);
         acc[1] = mfma_bf16(A2[1][ks], B, acc[1]);
       }
-      if (tok < b.Tv) {
-        const int sl = tok / L;
+      {   // dH rows widened (ina_common.h widen: lane group q ends up with features 32w + 8q .. + 7 of its
+          // token): one 16-byte store per lane, 16 tokens x 64 B per instruction instead of two 8-byte stores
+          // per lane; all lanes take part in the swaps, padded tokens are not stored
+        const int sl = min(tok / L, SB - 1);
         const float al = alp[tok];
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          const int k0 = 32 * w + 16 * mt + 4 * q;
-          if (k0 < H) {
-            const float4 dv = *reinterpret_cast<const float4*>(deL + sl * HP + k0);
-            *reinterpret_cast<uint2*>(dHg + (g0 + tok) * H + k0) =
-                pack4_bf16(acc[mt][0] + al * dv.x, acc[mt][1] + al * dv.y, acc[mt][2] + al * dv.z, acc[mt][3] + al * dv.w);
-          }
-        }
+        const int k0 = 32 * w + 4 * q;
+        const float4 d0 = *reinterpret_cast<const float4*>(deL + sl * HP + k0);
+        const float4 d1 = *reinterpret_cast<const float4*>(deL + sl * HP + k0 + 16);
+        uint2 X = pack4_bf16(acc[0][0] + al * d0.x, acc[0][1] + al * d0.y, acc[0][2] + al * d0.z, acc[0][3] + al * d0.w);
+        uint2 Y = pack4_bf16(acc[1][0] + al * d1.x, acc[1][1] + al * d1.y, acc[1][2] + al * d1.z, acc[1][3] + al * d1.w);
+        widen(X, Y);
+        const int kw = 32 * w + 8 * q;
+        if (tok < b.Tv && kw < H) *reinterpret_cast<uint4*>(dHg + (g0 + tok) * H + kw) = uint4{X.x, X.y, Y.x, Y.y};
       }
 #pragma unroll
       for (int k = 0; k < 2; ++k) {

@@ -277,45 +277,6 @@ INA_DEVICE void kstep(f32x4_t (&acc)[8][4], Frags& f, const Stager& sg, bool ful
   barrier();
 }
 
-// Store widening: lane group fq holds X = columns 4 fq .. 4 fq + 3 of tile nt = 2h and Y = columns 16 + 4 fq ..
-// of tile 2h + 1 (4 bf16 each, one row).  permlane32_swap (upper half of X <-> lower half of Y) then
-// permlane16_swap (odd 16-lane rows of X <-> even rows of Y) leave lane group fq with columns 8 fq .. 8 fq + 7
-// as (X, Y): one 16-byte store per lane, 16 rows x 64 B per instruction instead of two of 16 rows x 32 B
-// (the C write of a short-K GEMM is store-issue bound: cdna_hip_programming.md T21).
-INA_DEVICE void widen(uint2& X, uint2& Y) {
-  auto r = __builtin_amdgcn_permlane32_swap(X.x, Y.x, false, false);
-  X.x = r[0];
-  Y.x = r[1];
-  r = __builtin_amdgcn_permlane32_swap(X.y, Y.y, false, false);
-  X.y = r[0];
-  Y.y = r[1];
-  r = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
-  X.x = r[0];
-  Y.x = r[1];
-  r = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
-  X.y = r[0];
-  Y.y = r[1];
-}
-
-// The inverse exchange (each swap is an involution): a 16-byte row chunk loaded in the widened layout (lane
-// group fq: columns 8 fq .. 8 fq + 7) back to the accumulator layout (X: tile 2h columns 4 fq .., Y: tile 2h + 1).
-// (The widening is applied to VALU results only: a permlane swap reading an MFMA accumulator directly gets no
-// MFMA -> VALU wait states from hipcc and read stale values.)
-INA_DEVICE void unwiden(uint2& X, uint2& Y) {
-  auto r = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
-  X.x = r[0];
-  Y.x = r[1];
-  r = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
-  X.y = r[0];
-  Y.y = r[1];
-  r = __builtin_amdgcn_permlane32_swap(X.x, Y.x, false, false);
-  X.x = r[0];
-  Y.x = r[1];
-  r = __builtin_amdgcn_permlane32_swap(X.y, Y.y, false, false);
-  X.y = r[0];
-  Y.y = r[1];
-}
-
 // EPI_DGELU: per (row tile mt, half h) ONE 16-byte aux load per lane (the widened layout, unwidened in
 // registers) instead of two 8-byte ones, all 16 of the wave's aux loads issued before the first use; d in the
 // accumulator layout (bias-gradient column sums as before), stored widened.
