@@ -54,6 +54,21 @@ INA_DEVICE void st4(unsigned short* p, const float* v) {
   *reinterpret_cast<u16x4_t*>(p) = x;
 }
 INA_DEVICE float4 ld4f(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// One row's 4-column groups of two 16-column tiles (a0: columns 4g .. 4g+3 of tile dt, a1: the same of tile dt+1)
+// -> ONE 16-byte store per lane of columns 8g .. 8g+7 (ina_common.h widen; all lanes must call it, ok masks the
+// store): 16 rows x 64 B per instruction instead of two instructions of 16 rows x 32 B.  p = the row's base + 32
+// columns per tile pair.
+INA_DEVICE void st8w(unsigned short* p, int g, const float* a0, const float* a1, bool ok) {
+  u16x4_t x, y;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    x[r] = f2bf(a0[r]);
+    y[r] = f2bf(a1[r]);
+  }
+  uint2 X = __builtin_bit_cast(uint2, x), Y = __builtin_bit_cast(uint2, y);
+  widen(X, Y);
+  if (ok) *reinterpret_cast<uint4*>(p + 8 * g) = uint4{X.x, X.y, Y.x, Y.y};
+}
 
 // --------------------------------------------------------------------------------------------
 // LN(res + dropout(a))
@@ -577,6 +592,7 @@ __global__ __launch_bounds__(64 * NWV) void mha_fwd_kernel(const unsigned short*
 #pragma unroll
       for (int j = 0; j < 8; ++j) pf[k2][j] = f2bf(sc[2 * k2 + (j >> 2)][j & 3]);
     unsigned short* orow = ctx + (tok0 + (qok ? q : 0)) * HDm + hh * HDIM;
+    float o[4][4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
@@ -586,11 +602,11 @@ __global__ __launch_bounds__(64 * NWV) void mha_fwd_kernel(const unsigned short*
         const unsigned short* vr = &Vs[(32 * k2 + 4 * g + (n >> 2)) * KSTR + 16 * dt + 4 * (n & 3)];
         acc = mfma_bf16(cat_tr(tr_read(vr), tr_read(vr + 16 * KSTR)), pf[k2], acc);
       }
-      if (qok) {
-        float o[4] = {acc[0] * inv_l, acc[1] * inv_l, acc[2] * inv_l, acc[3] * inv_l};
-        st4(orow + 16 * dt + 4 * g, o);
-      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[dt][r] = acc[r] * inv_l;
     }
+    st8w(orow, g, o[0], o[1], qok);
+    st8w(orow + 32, g, o[2], o[3], qok);
     if (g == 0) lse[((size_t)s * nh + hh) * LP + q] = m + __log2f(l);
   }
 }
@@ -771,19 +787,23 @@ INA_UNROLL(INA_MHA_QPU)
     // outputs: dK^T / dV^T tiles -> rows of dqkv (lane: key = 16kt + n, d = 16dt + 4g + r)
     unsigned short* dk = dqkv + (tok0 + key) * ROW + HDm + hh * HDIM;
     unsigned short* dv = dk + HDm;
+    float a[4][4], b[4][4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      float a[4] = {dK[dt][0] * scale, dK[dt][1] * scale, dK[dt][2] * scale, dK[dt][3] * scale};
-      float b[4] = {dV[dt][0], dV[dt][1], dV[dt][2], dV[dt][3]};
-      if (kok) {
-        st4(dk + 16 * dt + 4 * g, a);
-        st4(dv + 16 * dt + 4 * g, b);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a[dt][r] = dK[dt][r] * scale;
+        b[dt][r] = dV[dt][r];
       }
       if (bsum) {   // uniform
-        colsum(1, dt, a, kok);
-        colsum(2, dt, b, kok);
+        colsum(1, dt, a[dt], kok);
+        colsum(2, dt, b[dt], kok);
       }
     }
+    st8w(dk, g, a[0], a[1], kok);
+    st8w(dk + 32, g, a[2], a[3], kok);
+    st8w(dv, g, b[0], b[1], kok);
+    st8w(dv + 32, g, b[2], b[3], kok);
   }
   if (bsum) {
     colsum_flush(1);
@@ -828,12 +848,15 @@ INA_UNROLL(INA_MHA_QPU)
       }
     }
     unsigned short* dq = dqkv + (tok0 + q) * ROW + hh * HDIM;
+    float a[4][4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      float a[4] = {acc[dt][0] * scale, acc[dt][1] * scale, acc[dt][2] * scale, acc[dt][3] * scale};
-      if (q < L) st4(dq + 16 * dt + 4 * g, a);
-      if (bsum) colsum(0, dt, a, q < L);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[dt][r] = acc[dt][r] * scale;
+      if (bsum) colsum(0, dt, a[dt], q < L);
     }
+    st8w(dq, g, a[0], a[1], q < L);
+    st8w(dq + 32, g, a[2], a[3], q < L);
   }
   if (bsum) {
     colsum_flush(0);
