@@ -214,12 +214,15 @@ std::tuple<Tensor, Tensor> bert_bias_gelu_bwd(const Tensor& dy, const Tensor& x,
 // bias-gradient column-sum slab [2 ceil(M/256)][N])
 std::tuple<Tensor, Tensor> bert_gemm(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& b,
                                      const c10::optional<Tensor>& aux, int64_t epi) {
-  chk(x, "x", at::kBFloat16);
+  // x may be a column slice of wider rows (stride(1) == 1, row stride = lda)
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1 &&
+                  x.stride(0) >= x.size(1),
+              "ina.bert_gemm: x must be a bf16 GPU matrix with unit column stride");
   chk(w, "w", at::kBFloat16);
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "ina.bert_gemm: x [M, K], w [N, K]");
-  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && x.size(1) == w.size(1), "ina.bert_gemm: x [M, K], w [N, K]");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0), lda = x.stride(0);
   TORCH_CHECK(N % 256 == 0 && K % 64 == 0 && K >= 64, "ina.bert_gemm: N must be a multiple of 256, K of 64");
-  TORCH_CHECK(M * K * 2 < (1LL << 31) && N * K * 2 < (1LL << 31), "ina.bert_gemm: operand too large");
+  TORCH_CHECK(M * lda * 2 < (1LL << 31) && N * K * 2 < (1LL << 31), "ina.bert_gemm: operand too large");
   TORCH_CHECK(epi >= 0 && epi <= 2, "ina.bert_gemm: epi must be 0, 1 or 2");
   const float* bp = nullptr;
   if (b.has_value() && b->defined()) {
@@ -240,7 +243,7 @@ std::tuple<Tensor, Tensor> bert_gemm(const Tensor& x, const Tensor& w, const c10
     slab = at::empty({2 * ((M + 255) / 256), N}, x.options().dtype(at::kFloat));
   }
   if (M == 0) return {y, epi == 2 ? slab.zero_() : ax};
-  launched(ina::gemm_bf16_nt(x.data_ptr(), (int)K, w.data_ptr(), (int)K, (int)M, (int)N, (int)K, bp, y.data_ptr(),
+  launched(ina::gemm_bf16_nt(x.data_ptr(), (int)lda, w.data_ptr(), (int)K, (int)M, (int)N, (int)K, bp, y.data_ptr(),
                              (int)N, epi != 0 ? ax.data_ptr() : nullptr, (int)N,
                              slab.defined() ? slab.data_ptr<float>() : nullptr, (int)epi, stream()),
            "gemm_bf16_nt");

@@ -212,7 +212,11 @@ struct WideSeqArgs {
   const float* bx;        // [2][G4] fp32: pre-scaled biases (forget gate +1)
   const void* apk;        // [2][NW][4][KS][64] x 8 bf16 forward W_h fragments (pre-scaled)
   const void* a2pk;       // [2][NW][KS2][64] x 8 bf16 backward W_h fragments
-  void* hprev;            // [2][S][L][UP] bf16: each step's recurrent input h_{t-1} (dW_h GEMM operand)
+  void* hprev;            // bf16 each step's recurrent input h_{t-1} (dW_h GEMM operand): direction d, row s L + t at
+                          // hprev + d hdo + (s L + t) hld ([2][S][L][UP]: hld = UP, hdo = S L UP; or columns of
+                          // the x rows [S L][DP + 2 UP]: hld = DP + 2 UP, hdo = UP)
+  int hld;
+  long hdo;
   void* acts;             // i, j, f, o activations, bf16, tile-major (lstm_wide.hip WideStash)
   void* cst;              // cell states, fp16, tile-major (lstm_wide.hip WideStash)
   void* hout;             // [S][L][2U] bf16: DropoutWrapper output (attention input)
@@ -228,7 +232,7 @@ struct WideSeqArgs {
 };
 bool lstm_wide_seq_supported(int U);
 int wide_x_gather(const int* inst, int S, int L, const int* word, const int* pos1, const int* pos2, const void* wemb,
-                  bool wemb_bf16, int E, const float* p1emb, const float* p2emb, int PD, int DP, void* xb,
+                  bool wemb_bf16, int E, const float* p1emb, const float* p2emb, int PD, int DP, void* xb, int ldx,
                   hipStream_t st);
 int wide_pos_grad(const float* dxp, const int* inst, const int* pos1, const int* pos2, int S, int L, int PD, int P2,
                   int chunks, int planes, float* part, hipStream_t st);

@@ -230,7 +230,7 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_fwd_kernel(
     const unsigned short* __restrict__ gx, const float* __restrict__ bx, const u16x8_t* __restrict__ apk, int S, int L,
     unsigned short* __restrict__ hprev, uint2* __restrict__ acts, uint2* __restrict__ cst,
     unsigned short* __restrict__ hout, uint32_t salt0, uint32_t salt1, uint32_t thr, float inv_kp, int drop,
-    int stash) {
+    int stash, int hld, long hdo) {
   using C = WideCfg<U>;
   using Z = WideStash<U>;
   constexpr int UP = C::UP, NW = C::NW, M = C::M, KS = C::KS, G4 = C::G4, NT = C::NT, HS = C::HS, SEQ = C::SEQ;
@@ -283,11 +283,12 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_fwd_kernel(
     load_gx(tn, gnx);
     const unsigned short* hin = himg[tau & 1];
     unsigned short* hnx = himg[(tau + 1) & 1];
-    if (stash) {   // this step's recurrent input h_{t-1} -> hprev[dir][s][t] (the dW_h GEMM's rows)
+    if (stash) {   // this step's recurrent input h_{t-1} -> hprev row s L + t of direction dir (the dW_h GEMM's
+                   // rows: row stride hld, direction offset hdo elements)
       for (int i = threadIdx.x; i < NCH; i += NTH) {
         const int r = i / CH, ch = i - r * CH, s = s0 + r;
         if (s < S)
-          *reinterpret_cast<u16x8_t*>(hprev + (((size_t)dir * S + s) * L + t) * UP + 8 * ch) =
+          *reinterpret_cast<u16x8_t*>(hprev + dir * hdo + ((size_t)s * L + t) * hld + 8 * ch) =
               *reinterpret_cast<const u16x8_t*>(hin + r * HS + 8 * ch);
       }
     }
@@ -527,7 +528,7 @@ static int wide_seq_fwd_t(const WideSeqArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(lstm_wide_seq_fwd_kernel<U>, grid, dim3(C::NW * 64), 0, st, (const unsigned short*)a.gx, a.bx,
                      (const u16x8_t*)a.apk, a.S, a.L, (unsigned short*)a.hprev, (uint2*)a.acts,
                      (uint2*)a.cst, (unsigned short*)a.hout, a.salt0,
-                     a.salt1, a.thr, a.inv_kp, a.drop, a.stash);
+                     a.salt1, a.thr, a.inv_kp, a.drop, a.stash, a.hld, a.hdo);
   INA_CHECK_LAUNCH();
   return 0;
 }
@@ -572,7 +573,7 @@ __global__ __launch_bounds__(256) void wide_x_gather_kernel(const int* __restric
                                                             const int* __restrict__ pos2, const void* __restrict__ wemb_v,
                                                             int E, const float* __restrict__ p1emb,
                                                             const float* __restrict__ p2emb, int PD, int DP,
-                                                            unsigned short* __restrict__ xb) {
+                                                            unsigned short* __restrict__ xb, int ldx) {
   const int lane = threadIdx.x & 63;
   const int D = E + 2 * PD;
   const long rows = (long)S * L;
@@ -609,7 +610,7 @@ __global__ __launch_bounds__(256) void wide_x_gather_kernel(const int* __restric
       }
 #pragma unroll
       for (int i = 0; i < RW; ++i)
-        if (r0 + i < rows) *reinterpret_cast<uint2*>(xb + (r0 + i) * DP + c) = v[i];
+        if (r0 + i < rows) *reinterpret_cast<uint2*>(xb + (r0 + i) * ldx + c) = v[i];
     }
     c0 = E;
   }
@@ -632,7 +633,7 @@ __global__ __launch_bounds__(256) void wide_x_gather_kernel(const int* __restric
     }
 #pragma unroll
     for (int i = 0; i < RW; ++i)
-      if (c < DP && r0 + i < rows) xb[(r0 + i) * DP + c] = f2bf(vv[i]);
+      if (c < DP && r0 + i < rows) xb[(r0 + i) * ldx + c] = f2bf(vv[i]);
     return;
   }
 #pragma unroll
@@ -640,7 +641,7 @@ __global__ __launch_bounds__(256) void wide_x_gather_kernel(const int* __restric
     if (r0 + i >= rows) break;
     const float* q1 = p1emb + (long)p1v[i] * PD;
     const float* q2 = p2emb + (long)p2v[i] * PD;
-    unsigned short* dst = xb + (r0 + i) * DP;
+    unsigned short* dst = xb + (r0 + i) * ldx;
     for (int c = c0 + lane; c < DP; c += 64) {
       float wv = 0.f;
       if (c < E) {
@@ -685,7 +686,7 @@ __global__ __launch_bounds__(256) void wide_pos_grad_kernel(const float* __restr
 namespace ina {
 
 int wide_x_gather(const int* inst, int S, int L, const int* word, const int* pos1, const int* pos2, const void* wemb,
-                  bool wemb_bf16, int E, const float* p1emb, const float* p2emb, int PD, int DP, void* xb,
+                  bool wemb_bf16, int E, const float* p1emb, const float* p2emb, int PD, int DP, void* xb, int ldx,
                   hipStream_t st) {
 #ifndef INA_WXG_RW
 #define INA_WXG_RW 4   // rows per wave: 4 -> 383 us, 8 -> 415 us, 16 -> 477 us at the paper configuration (profiles/r5_rw)
@@ -697,10 +698,10 @@ int wide_x_gather(const int* inst, int S, int L, const int* word, const int* pos
   if (blocks >= (1L << 31)) return -1;
   if (wemb_bf16)
     hipLaunchKernelGGL((wide_x_gather_kernel<true, RW>), dim3((int)blocks), dim3(256), 0, st, inst, S, L, word, pos1,
-                       pos2, wemb, E, p1emb, p2emb, PD, DP, (unsigned short*)xb);
+                       pos2, wemb, E, p1emb, p2emb, PD, DP, (unsigned short*)xb, ldx);
   else
     hipLaunchKernelGGL((wide_x_gather_kernel<false, RW>), dim3((int)blocks), dim3(256), 0, st, inst, S, L, word, pos1,
-                       pos2, wemb, E, p1emb, p2emb, PD, DP, (unsigned short*)xb);
+                       pos2, wemb, E, p1emb, p2emb, PD, DP, (unsigned short*)xb, ldx);
   INA_CHECK_LAUNCH();
   return 0;
 }

@@ -101,9 +101,11 @@ int64_t wide_up(int64_t U) { return (U + 31) / 32 * 32; }
 // pack_lstm_wide's forward fragments -> (hout [S, L, 2U] bf16, hprev [2, S, L, UP] bf16,
 // acts [2, Sp*L, 4UP] bf16, cst [2, Sp*L, UP] fp16: tile-major, Sp = S rounded up to 32);
 // the last three only when stash (training), else empty
+// hdst (optional, stash only): the x rows [S*L, W] whose columns hcol .. hcol + 2 UP take the h_{t-1} stash (direction
+// d at hcol + d UP), so one weight-gradient GEMM covers x and both directions' h; then hprev is returned empty
 std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_wide_seq_fwd(const Tensor& gx, const Tensor& bx, const Tensor& apk,
                                                              int64_t S, int64_t L, int64_t U, bool stash, int64_t seed,
-                                                             double keep_prob) {
+                                                             double keep_prob, const Tensor& hdst, int64_t hcol) {
   TORCH_CHECK(ina::lstm_wide_seq_supported((int)U), "ina.lstm_wide_seq_fwd: U must be 64, 100 or 128");
   const int64_t UP = wide_up(U), G4 = 4 * UP, NW = UP / 16;
   chk(gx, "gx", at::kBFloat16, 2 * S * L * G4);
@@ -112,7 +114,15 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_wide_seq_fwd(const Tensor& gx, c
   TORCH_CHECK(S * L * G4 < (1LL << 31) * 2, "ina.lstm_wide_seq_fwd: batch too large");
   auto bopt = gx.options().dtype(at::kBFloat16), hopt = gx.options().dtype(at::kHalf);
   auto hout = at::empty({S, L, 2 * U}, bopt);
-  auto hprev = stash ? at::empty({2, S, L, UP}, bopt) : at::empty({0}, bopt);
+  const bool into_x = stash && hdst.numel() > 0;
+  if (into_x) {
+    TORCH_CHECK(hdst.is_cuda() && hdst.is_contiguous() && hdst.scalar_type() == at::kBFloat16 && hdst.dim() == 2 &&
+                    hdst.size(0) == S * L && hcol >= 0 && hcol % 8 == 0 && hcol + 2 * UP <= hdst.size(1) &&
+                    hdst.size(1) % 8 == 0,
+                "ina.lstm_wide_seq_fwd: hdst must be contiguous bf16 [S*L, W] with room for 2 UP columns at hcol");
+    TORCH_CHECK(S * L * hdst.size(1) < (1LL << 31) * 2, "ina.lstm_wide_seq_fwd: hdst too large");
+  }
+  auto hprev = stash && !into_x ? at::empty({2, S, L, UP}, bopt) : at::empty({0}, bopt);
   const int64_t Sp = wide_seq_pad(S);   // tile-major stash: whole 32-sequence tiles
   auto acts = stash ? at::empty({2, Sp * L, G4}, bopt) : at::empty({0}, bopt);
   auto cst = stash ? at::empty({2, Sp * L, UP}, hopt) : at::empty({0}, hopt);
@@ -124,7 +134,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lstm_wide_seq_fwd(const Tensor& gx, c
   a.gx = gx.data_ptr();
   a.bx = bx.data_ptr<float>();
   a.apk = apk.data_ptr();
-  a.hprev = stash ? hprev.data_ptr() : nullptr;
+  a.hprev = !stash ? nullptr : into_x ? (void*)((unsigned short*)hdst.data_ptr() + hcol) : hprev.data_ptr();
+  a.hld = into_x ? (int)hdst.size(1) : (int)UP;
+  a.hdo = into_x ? (long)UP : (long)(S * L * UP);
   a.acts = stash ? acts.data_ptr() : nullptr;
   a.cst = stash ? cst.data_ptr() : nullptr;
   a.hout = hout.data_ptr();
@@ -193,8 +205,10 @@ void chk_ids(const Tensor& t, const char* name) {
 }
 
 // Xb [S*L, E + 2PD] bf16 = [word row ; pos1 row ; pos2 row] of every token of the rows inst
+// extra: columns appended to each row after the DP gathered ones (not written here: the BiLSTM forward's h_{t-1}
+// stash, lstm_wide_seq_fwd hdst)
 Tensor wide_x_gather(const Tensor& inst, const Tensor& word, const Tensor& pos1, const Tensor& pos2,
-                     const Tensor& wemb, const Tensor& p1emb, const Tensor& p2emb) {
+                     const Tensor& wemb, const Tensor& p1emb, const Tensor& p2emb, int64_t extra) {
   chk_ids(inst, "inst");
   chk_ids(word, "word");
   chk_ids(pos1, "pos1");
@@ -207,10 +221,11 @@ Tensor wide_x_gather(const Tensor& inst, const Tensor& word, const Tensor& pos1,
   TORCH_CHECK(pos1.sizes() == word.sizes() && pos2.sizes() == word.sizes() && p2emb.size(1) == PD,
               "ina.wide_x_gather: shapes");
   const int64_t DP = (E + 2 * PD + 1 + 31) / 32 * 32;   // + the ones column, K padded to 32 (packing.wide_x_cols)
-  auto xb = at::empty({S * L, DP}, p1emb.options().dtype(at::kBFloat16));
+  TORCH_CHECK(extra >= 0 && extra % 8 == 0, "ina.wide_x_gather: extra columns must be a multiple of 8");
+  auto xb = at::empty({S * L, DP + extra}, p1emb.options().dtype(at::kBFloat16));
   TORCH_CHECK(ina::wide_x_gather(inst.data_ptr<int>(), (int)S, (int)L, word.data_ptr<int>(), pos1.data_ptr<int>(),
                                  pos2.data_ptr<int>(), wemb.data_ptr(), wb, (int)E, p1emb.data_ptr<float>(),
-                                 p2emb.data_ptr<float>(), (int)PD, (int)DP, xb.data_ptr(),
+                                 p2emb.data_ptr<float>(), (int)PD, (int)DP, xb.data_ptr(), (int)(DP + extra),
                                  c10::hip::getCurrentHIPStream().stream()) == 0,
               "ina.wide_x_gather: launch failed");
   return xb;

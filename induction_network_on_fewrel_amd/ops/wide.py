@@ -132,8 +132,10 @@ def x_projection(Xb: torch.Tensor, pk: dict) -> torch.Tensor:
     profiles/r5_widen) where its limits hold (N % 256, K % 64, 32-bit operand offsets), else hipBLASLt."""
     M, K = Xb.shape
     wt = pk.get("wxcT")
-    if wt is not None and wt.shape[0] % 256 == 0 and K % 64 == 0 and M * K * 2 < (1 << 31) and Xb.is_contiguous():
-        return ops().bert_gemm(Xb, wt, None, None, 0)[0]
+    lda = Xb.stride(0)
+    if (wt is not None and wt.shape[0] % 256 == 0 and K % 64 == 0 and Xb.stride(1) == 1 and lda % 8 == 0
+            and M * lda * 2 < (1 << 31)):
+        return ops().bert_gemm(Xb, wt, None, None, 0)[0]   # (Xb may be the x columns of wider rows)
     return torch.mm(Xb, pk["wxc"])
 
 
@@ -160,16 +162,22 @@ class WideSeqBiLSTM(torch.autograd.Function):
         D = E + 2 * P
         pk = packs if packs is not None else pack_lstm_wide(Kf, bf, Kb, bb, U, D)
         wtab = word_table_bf16(wemb) if not wemb.requires_grad else wemb.detach().float().contiguous()
-        Xb = o.wide_x_gather(inst, word, pos1, pos2, wtab, p1emb.detach().float().contiguous(),
-                             p2emb.detach().float().contiguous())
+        need = any(ctx.needs_input_grad[4:11])
+        UP = (U + 31) // 32 * 32
+        DP = (D + 1 + 31) // 32 * 32
+        # training: each x row is followed by the two directions' h_{t-1} stash columns (written by the forward
+        # kernel), so ONE split-K GEMM over [x | h_fw | h_bw] rows gives dW_x, db and both dW_h reading dG once
+        # (1,385 vs 1,506 us for the three GEMMs at the paper configuration, tools/gemm_probe.py)
+        Xw = o.wide_x_gather(inst, word, pos1, pos2, wtab, p1emb.detach().float().contiguous(),
+                             p2emb.detach().float().contiguous(), 2 * UP if need else 0)
+        Xb = Xw[:, :DP]
         # x W_x for both directions as ONE bf16-output GEMM (the kernel adds the fp32 biases): an fp32 output
         # plus a separate bias pass moved ~15 GB per step at the paper configuration
         gx = x_projection(Xb, pk)
-        need = any(ctx.needs_input_grad[4:11])
-        hout, hprev, acts, cst = o.lstm_wide_seq_fwd(gx, pk["bx"], pk["apk"], S, L, U, bool(need), int(seed),
-                                                     float(keep_prob))
+        hout, _, acts, cst = o.lstm_wide_seq_fwd(gx, pk["bx"], pk["apk"], S, L, U, bool(need), int(seed),
+                                                 float(keep_prob), Xw if need else Xw.new_empty(0), DP)
         if need:
-            ctx.save_for_backward(inst, word, pos1, pos2, Xb, pk["wxtc"], pk["a2pk"], hprev, acts, cst)
+            ctx.save_for_backward(inst, word, pos1, pos2, Xw, pk["wxtc"], pk["a2pk"], acts, cst)
             ctx.cfg = (S, L, E, P, U, int(seed), float(keep_prob), bool(pos_shift), p1emb.shape[0], wemb.shape[0])
         return hout
 
@@ -177,7 +185,7 @@ class WideSeqBiLSTM(torch.autograd.Function):
     def backward(ctx, dout):
         from .packing import unpack_wide_grads
         o = ops()
-        inst, word, pos1, pos2, Xb, wxtc, a2pk, hprev, acts, cst = ctx.saved_tensors
+        inst, word, pos1, pos2, Xw, wxtc, a2pk, acts, cst = ctx.saved_tensors
         S, L, E, P, U, seed, kp, shift, P2, V = ctx.cfg
         D = E + 2 * P
         need_w = ctx.needs_input_grad[4]
@@ -187,14 +195,18 @@ class WideSeqBiLSTM(torch.autograd.Function):
         wpk = pos_frags(wxtc, E, D) if fuse else wxtc.new_empty(0)
         dG, dxpd = o.lstm_wide_seq_bwd(dout.contiguous().to(torch.bfloat16), acts, cst, a2pk, S, L, U, seed, kp,
                                        wpk, 2 * P)
-        UP, G4 = hprev.shape[-1], dG.shape[1] // 2
-        # ONE GEMM for both directions' x-kernel gradients; Xb's ones column (row D) makes it the bias
-        # gradient as well (no separate column-sum pass over dG)
-        dwx = _wgrad(Xb, dG)                                              # [DP, 2 G4]
+        G4 = dG.shape[1] // 2
+        UP = G4 // 4
+        DP = Xw.shape[1] - 2 * UP
+        # ONE GEMM for both directions' x- and h-kernel gradients over the rows [x | h_fw | h_bw] (the two
+        # cross-direction blocks h_fw^T dG_bw / h_bw^T dG_fw are computed and dropped: 12% more FLOPs, dG read
+        # once); x's ones column (row D) makes it the bias gradient as well
+        dwall = _wgrad(Xw, dG, 64)                                        # [DP + 2 UP, 2 G4]
         dKs, dbs = [], []
         for d in range(2):
             c = slice(d * G4, (d + 1) * G4)
-            dK, db = unpack_wide_grads(dwx[:D, c], _wgrad(hprev[d].reshape(S * L, UP), dG[:, c], 64), dwx[D, c], U)
+            dwh = dwall[DP + d * UP:DP + (d + 1) * UP, c]
+            dK, db = unpack_wide_grads(dwall[:D, c], dwh, dwall[D, c], U)
             dKs.append(dK)
             dbs.append(db)
         if fuse:

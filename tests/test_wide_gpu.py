@@ -73,7 +73,7 @@ def test_bwd_fused_position_columns_match_gemm(U):
     pk = pack_lstm_wide(Kf.to(DEV), bf.to(DEV), Kb.to(DEV), bb.to(DEV), U, D)
     X = torch.randn(S * L, wide_x_cols(D), generator=g).to(DEV).bfloat16()
     gx = torch.mm(X, pk["wxc"])
-    _, _, acts, cst = o.lstm_wide_seq_fwd(gx, pk["bx"], pk["apk"], S, L, U, True, 7, 0.9)
+    _, _, acts, cst = o.lstm_wide_seq_fwd(gx, pk["bx"], pk["apk"], S, L, U, True, 7, 0.9, X.new_empty(0), 0)
     dH = torch.randn(S, L, 2 * U, generator=g).to(DEV).bfloat16()
     dG0, none = o.lstm_wide_seq_bwd(dH, acts, cst, pk["a2pk"], S, L, U, 7, 0.9, X.new_empty(0), 2 * P)
     dG, dxp = o.lstm_wide_seq_bwd(dH, acts, cst, pk["a2pk"], S, L, U, 7, 0.9, pos_frags(pk["wxtc"], E, D), 2 * P)
@@ -235,7 +235,7 @@ def test_wide_x_gather_rows(E, table_bf16):
     wemb = torch.randn(V, E, generator=g).to(DEV)
     p1, p2 = torch.randn(2 * L, PD, generator=g).to(DEV), torch.randn(2 * L, PD, generator=g).to(DEV)
     tab = wemb.to(torch.bfloat16) if table_bf16 else wemb
-    xb = ops().wide_x_gather(inst, word, pos1, pos2, tab, p1, p2)
+    xb = ops().wide_x_gather(inst, word, pos1, pos2, tab, p1, p2, 0)
     il = inst.long()
     ref = torch.cat([wemb[word[il].long()], p1[pos1[il].long()], p2[pos2[il].long()],
                      torch.ones(S, L, 1, device=DEV)], -1).reshape(S * L, -1)

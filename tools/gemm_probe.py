@@ -57,3 +57,13 @@ for sp in (16, 20, 25, 32, 40):
 for sp in (32, 50, 100, 128):
     bench(f"dwh strided split{sp}", lambda: torch.bmm(Hp[0].view(sp, T // sp, 128).transpose(1, 2),
                                                       G[:, :512].view(sp, T // sp, 512), out_dtype=torch.float32).sum(0))
+# round 5: dW_x and both directions' dW_h as ONE split-K GEMM over [x | h_prev fw | h_prev bw] rows (reads dG once;
+# 12% extra FLOPs for the two cross-direction blocks) vs the current three GEMMs
+XA = torch.randn(T, 576, device=dev, dtype=bf)
+for sp in (16, 32, 64):
+    bench(f"merged [T,576]^T [T,1024] split{sp}", lambda: torch.bmm(XA.view(sp, T // sp, 576).transpose(1, 2),
+                                                                   G.view(sp, T // sp, 1024), out_dtype=torch.float32).sum(0))
+bench("current dwx split16 + 2 x dwh split64", lambda: (
+    torch.bmm(X.view(16, T // 16, 320).transpose(1, 2), G.view(16, T // 16, 1024), out_dtype=torch.float32).sum(0),
+    torch.bmm(Hp[0].view(64, T // 64, 128).transpose(1, 2), G[:, :512].view(64, T // 64, 512), out_dtype=torch.float32).sum(0),
+    torch.bmm(Hp[1].view(64, T // 64, 128).transpose(1, 2), G[:, 512:].view(64, T // 64, 512), out_dtype=torch.float32).sum(0)))
