@@ -201,7 +201,7 @@ class WideSeqBiLSTM(torch.autograd.Function):
         # ONE GEMM for both directions' x- and h-kernel gradients over the rows [x | h_fw | h_bw] (the two
         # cross-direction blocks h_fw^T dG_bw / h_bw^T dG_fw are computed and dropped: 12% more FLOPs, dG read
         # once); x's ones column (row D) makes it the bias gradient as well
-        dwall = _wgrad(Xw, dG, 64)                                        # [DP + 2 UP, 2 G4]
+        dwall = _wgrad(Xw, dG, 64)                                        # [DP + 2 UP, 2 G4] (split 64; 128 measured slower in the step: 1,325 vs 1,227 us, profiles/r5_merged)
         dKs, dbs = [], []
         for d in range(2):
             c = slice(d * G4, (d + 1) * G4)
