@@ -1,0 +1,20 @@
+"""The paper configuration head's dM = C^T dP GEMM (ops/wide.py _wide_head_backward): split-K vs one GEMM.
+usage (GPU box): python tools/dm_wide_probe.py"""
+import torch
+def bench(name, fn, it=20):
+    for _ in range(3): fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it): fn()
+    e.record(); torch.cuda.synchronize()
+    print(f"{s.elapsed_time(e) / it * 1000:9.1f} us  {name}", flush=True)
+R, H, hH = 1280, 256, 25600
+c = torch.randn(R, H, device="cuda").bfloat16()
+d = torch.randn(R, hH, device="cuda").bfloat16()
+bench("mm fp32 out (no split)", lambda: torch.mm(c.t(), d, out_dtype=torch.float32))
+for ns in (2, 4):
+    bench(f"split {ns} + sum", lambda: torch.bmm(c.view(ns, R // ns, H).transpose(1, 2), d.view(ns, R // ns, hH), out_dtype=torch.float32).sum(0))
+bench("mm bf16 out", lambda: torch.mm(c.t(), d))
+Mt = torch.randn(H, hH, device="cuda")
+bench("permute-back copy (dM view permute contiguous)", lambda: Mt.view(H, 100, H).permute(0, 2, 1).contiguous())
