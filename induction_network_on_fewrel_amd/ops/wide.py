@@ -417,6 +417,20 @@ def _split_sum_mm(a: torch.Tensor, b: torch.Tensor, nb: int = 64) -> torch.Tenso
     return torch.bmm(a.view(nb, T // nb, -1).transpose(1, 2), b.view(nb, T // nb, -1)).sum(0)
 
 
+def _splitk_nt(a: torch.Tensor, b: torch.Tensor, ns: int) -> torch.Tensor:
+    """a b^T in fp32 for a [M, K], b [N, K] with a long K and a small output: K split into ns chunks as ONE
+    strided batched GEMM + an ordered sum (deterministic).  The head's dcls = dP M'^T (K = h H = 25,600, a
+    [1280, 256] output at the paper configuration) ran as one GEMM on ~44 workgroups: 104 -> 32 us with
+    ns = 8 (tools/dm_wide_probe.py)."""
+    M, K = a.shape
+    N = b.shape[0]
+    if ns <= 1 or K % ns or not (a.is_cuda and a.is_contiguous() and b.is_contiguous()):
+        return torch.mm(a, b.t(), out_dtype=torch.float32)
+    c = K // ns
+    return torch.bmm(a.view(M, ns, c).transpose(0, 1), b.view(N, ns, c).permute(1, 2, 0),
+                     out_dtype=torch.float32).sum(0)
+
+
 def _wide_head_forward(e, Ws, M, w, b, E, N, K, Q, R, paper):
     """Routing (e_hat GEMM + routing_wide_fwd) -> NTN (P = C M', T = Q P^T as bf16 GEMMs) -> epilogue.
     M' = M permuted to [a, (s, b')] so that P [E*N, h*H] viewed [E, N*h, H] is each episode's
@@ -451,7 +465,7 @@ def _wide_head_backward(ctx, saved, dz, g):
     dQ = torch.bmm(dT, P.view(E, N * h, H), out_dtype=torch.float32)           # [E, NQ, H]
     dP = torch.bmm(dT.transpose(1, 2), qb)                                      # [E, N*h, H] bf16
     dPf = dP.view(E * N, h * H)
-    dcls = torch.mm(dPf, Mt.t(), out_dtype=torch.float32)                       # [E*N, H]
+    dcls = _splitk_nt(dPf, Mt, 8)                                              # [E*N, H]
     dMt = torch.mm(cls_bf.t(), dPf, out_dtype=torch.float32)                   # [H, h*H] fp32 (one GEMM: 30 us
     # vs 69 us split 4 + sum at the paper configuration, tools/dm_wide_probe.py)
     dM = dMt.view(H, h, H).permute(0, 2, 1)

@@ -18,3 +18,12 @@ for ns in (2, 4):
 bench("mm bf16 out", lambda: torch.mm(c.t(), d))
 Mt = torch.randn(H, hH, device="cuda")
 bench("permute-back copy (dM view permute contiguous)", lambda: Mt.view(H, 100, H).permute(0, 2, 1).contiguous())
+# dcls = dP M'^T: [E*N, h*H] x [h*H, H] with K = h*H = 25,600 and a [1280, 256] output (few tiles for one GEMM)
+P = torch.randn(R, hH, device="cuda").bfloat16()
+Mtb = torch.randn(H, hH, device="cuda").bfloat16()
+bench("dcls mm fp32 out", lambda: torch.mm(P, Mtb.t(), out_dtype=torch.float32))
+for ns in (4, 8, 16, 32):
+    c_ = hH // ns
+    bench(f"dcls split-K {ns} (strided bmm) + sum", lambda: torch.bmm(P.view(R, ns, c_).transpose(0, 1),
+                                                                   Mtb.view(H, ns, c_).permute(1, 2, 0),
+                                                                   out_dtype=torch.float32).sum(0))
