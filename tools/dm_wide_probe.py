@@ -27,3 +27,12 @@ for ns in (4, 8, 16, 32):
     bench(f"dcls split-K {ns} (strided bmm) + sum", lambda: torch.bmm(P.view(R, ns, c_).transpose(0, 1),
                                                                    Mtb.view(H, ns, c_).permute(1, 2, 0),
                                                                    out_dtype=torch.float32).sum(0))
+# dWs = S^T dE_hat (fp32, [6400, 256]^T [6400, 256]): one fp32 GEMM vs split-K fp32
+S_ = torch.randn(6400, H, device="cuda")
+D_ = torch.randn(6400, H, device="cuda")
+bench("dWs mm fp32", lambda: torch.mm(S_.t(), D_))
+for ns in (4, 8, 16):
+    bench(f"dWs split-K {ns} fp32 + sum", lambda: torch.bmm(S_.view(ns, 6400 // ns, H).transpose(1, 2), D_.view(ns, 6400 // ns, H)).sum(0))
+Mf = torch.randn(H, H, 100, device="cuda")
+bench("Mt = M.permute(0,2,1).reshape.to(bf16)", lambda: Mf.permute(0, 2, 1).reshape(H, 100 * H).to(torch.bfloat16))
+bench("Mt via transpose(1,2).contiguous then cast", lambda: Mf.transpose(1, 2).contiguous().to(torch.bfloat16))
