@@ -21,6 +21,18 @@ void need(const Tensor& t, const char* op, const char* name, at::ScalarType dt) 
 }
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// in [A, B, C] fp32 contiguous -> [A, C, B] (bf16 if bf16 else fp32): the last two dims transposed
+Tensor transpose12(const Tensor& in, bool bf16) {
+  TORCH_CHECK(in.is_cuda() && in.is_contiguous() && in.scalar_type() == at::kFloat && in.dim() == 3,
+              "ina.transpose12: in must be a contiguous fp32 [A, B, C] GPU tensor");
+  const int64_t A = in.size(0), B = in.size(1), C = in.size(2);
+  auto out = at::empty({A, C, B}, in.options().dtype(bf16 ? at::kBFloat16 : at::kFloat));
+  TORCH_CHECK(ina::transpose12(in.data_ptr<float>(), out.data_ptr(), (int)A, (int)B, (int)C, bf16,
+                               c10::hip::getCurrentHIPStream().stream()) == 0,
+              "ina.transpose12: launch failed");
+  return out;
+}
+
 void gather_pack(const Tensor& src, const Tensor& idx, int64_t nb, Tensor out_bf16, Tensor out_f32) {
   const char* op = "ina.gather_pack";
   need(src, op, "src", at::kFloat);
@@ -146,6 +158,7 @@ int64_t slab_scatter_add(Tensor dst, const std::vector<Tensor>& srcs, const std:
 
 TORCH_LIBRARY_FRAGMENT(ina, m) {
   m.def("gather_pack", &gather_pack);
+  m.def("transpose12", &transpose12);
   m.def("head_loss", &head_loss);
   m.def("ragged_sort", &ragged_sort);
   m.def("gather_pack_affine", &gather_pack_affine);

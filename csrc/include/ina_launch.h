@@ -161,6 +161,8 @@ struct SlabJobs {   // passed by value as a kernel argument (no per-step host->d
   long fbase[SLAB_MAX_JOBS + 1];      // prefix sums of ceil(n/64) (finish-launch workgroups)
   int njobs;
 };
+// out[a][c][b] = in[a][b][c] for in [A][B][C] fp32; out fp32 or bf16 (glue.hip)
+int transpose12(const float* in, void* out, int A, int B, int C, bool bf16, hipStream_t st);
 int gather_pack(const float* src, const int* idx, long nb, long ntot, void* outb, float* outf, hipStream_t st,
                 const float* ma = nullptr);
 int head_loss(const float* probs, const int* labels, long rows, int N, float scale, int ce, float* dz, float* out,

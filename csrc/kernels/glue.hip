@@ -227,9 +227,51 @@ __global__ __launch_bounds__(256) void slab_finish_kernel(SlabJobs jobs, const f
   }
 }
 
+// out[a][c][b] = in[a][b][c] (fp32 in, fp32 or bf16 out): the wide NTN head's M <-> M' layouts
+// ([H][H][h] <-> [H][h][H]).  32 x 32 tiles through LDS (row stride 33: conflict-free column reads), coalesced
+// reads along c and writes along b (torch's generic permute copy ran these at ~1.3 TB/s, 40 us per direction).
+template <bool BF>
+__global__ __launch_bounds__(256) void transpose12_kernel(const float* __restrict__ in, void* __restrict__ out, int B,
+                                                          int C) {
+  __shared__ float tile[32][33];
+  const int a = blockIdx.z, b0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+  const float* src = in + (size_t)a * B * C;
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int b = b0 + ty + k, c = c0 + tx;
+    tile[ty + k][tx] = (b < B && c < C) ? src[(size_t)b * C + c] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int c = c0 + ty + k, b = b0 + tx;
+    if (b < B && c < C) {
+      const size_t o = (size_t)a * B * C + (size_t)c * B + b;
+      const float v = tile[tx][ty + k];
+      if constexpr (BF)
+        static_cast<unsigned short*>(out)[o] = f2bf(v);
+      else
+        static_cast<float*>(out)[o] = v;
+    }
+  }
+}
+
 }  // namespace
 
 namespace ina {
+
+int transpose12(const float* in, void* out, int A, int B, int C, bool bf16, hipStream_t st) {
+  if (A <= 0 || B <= 0 || C <= 0) return 0;
+  if (A > 65535) return -1;
+  const dim3 grid((C + 31) / 32, (B + 31) / 32, A);
+  if (bf16)
+    hipLaunchKernelGGL(transpose12_kernel<true>, grid, dim3(256), 0, st, in, out, B, C);
+  else
+    hipLaunchKernelGGL(transpose12_kernel<false>, grid, dim3(256), 0, st, in, out, B, C);
+  INA_CHECK_LAUNCH();
+  return 0;
+}
 
 int gather_pack(const float* src, const int* idx, long nb, long ntot, void* outb, float* outf, hipStream_t st,
                 const float* ma) {

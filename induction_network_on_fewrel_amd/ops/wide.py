@@ -442,7 +442,7 @@ def _wide_head_forward(e, Ws, M, w, b, E, N, K, Q, R, paper):
     sup = ev[:, :NK].reshape(E * NK, H).float()
     eh = torch.mm(sup, Ws.detach().float())                                     # [E*NK, H] fp32
     cls, cls_bf = o.routing_wide_fwd(eh, E * N, K, R)
-    Mt = M.detach().permute(0, 2, 1).reshape(H, h * H).to(torch.bfloat16)      # [a, s*H + b']
+    Mt = o.transpose12(M.detach().contiguous(), True).view(H, h * H)             # [a, s*H + b'] bf16
     P = torch.mm(cls_bf, Mt)                                                    # [E*N, h*H] bf16
     qb = ev[:, NK:].to(torch.bfloat16).contiguous()                             # [E, NQ, H]
     T = torch.bmm(qb, P.view(E, N * h, H).transpose(1, 2), out_dtype=torch.float32)   # [E, NQ, N*h]
@@ -468,7 +468,7 @@ def _wide_head_backward(ctx, saved, dz, g):
     dcls = _splitk_nt(dPf, Mt, 8)                                              # [E*N, H]
     dMt = torch.mm(cls_bf.t(), dPf, out_dtype=torch.float32)                   # [H, h*H] fp32 (one GEMM: 30 us
     # vs 69 us split 4 + sum at the paper configuration, tools/dm_wide_probe.py)
-    dM = dMt.view(H, h, H).permute(0, 2, 1)
+    dM = o.transpose12(dMt.view(H, h, H), False)                                 # [a][b][s] fp32
     deh = o.routing_wide_bwd(eh, dcls, E * N, K, R)                            # [E*NK, H]
     ns = 4 if sup.is_cuda and sup.shape[0] % 4 == 0 and sup.shape[0] >= 4096 else 1
     # (fp32 split-K 4 + ordered sum: 26 vs 44 us for one GEMM at the paper configuration, tools/dm_wide_probe.py)

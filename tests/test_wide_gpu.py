@@ -241,3 +241,15 @@ def test_wide_x_gather_rows(E, table_bf16):
                      torch.ones(S, L, 1, device=DEV)], -1).reshape(S * L, -1)
     ref = torch.nn.functional.pad(ref, (0, xb.shape[1] - ref.shape[1])).to(torch.bfloat16)
     assert torch.equal(xb, ref)
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_transpose12_matches_permute(bf16):
+    """ina.transpose12 (the wide NTN head's M <-> M' layouts, glue.hip): [A, B, C] -> [A, C, B], ragged tiles."""
+    from induction_network_on_fewrel_amd.ops._ext import ops
+    x = torch.randn(5, 70, 37, device=DEV)
+    y = ops().transpose12(x, bf16)
+    want = x.permute(0, 2, 1).contiguous()
+    if bf16:
+        want = want.to(torch.bfloat16)
+    assert y.shape == want.shape and torch.equal(y, want)
