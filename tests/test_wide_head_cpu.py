@@ -14,6 +14,9 @@ class _EmuOps:
     def routing_wide_ok(self, K, H, R):
         return True
 
+    def transpose12(self, x, bf16):
+        return x.permute(0, 2, 1).contiguous()   # (the emulation keeps fp32 where the kernel writes bf16)
+
     def ntn_wide_epi_ok(self, N, paper):
         return True
 
