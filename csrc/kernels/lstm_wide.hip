@@ -666,21 +666,37 @@ __global__ __launch_bounds__(256) void wide_pos_grad_kernel(const float* __restr
                                                             const int* __restrict__ pos1, const int* __restrict__ pos2,
                                                             int S, int L, int PD, int P2, int chunk, int planes,
                                                             float* __restrict__ part) {
+  // The per-sequence first positions p0(s) of both tables are staged through LDS a tile at a time by the
+  // whole block (the inst[s] -> pos[] load chain is paid once per tile, in parallel, instead of serially
+  // by every thread on every sequence).
+  constexpr int TILE = 512;
+  __shared__ int off[2][TILE];
   const int o = blockIdx.x * 256 + threadIdx.x;
   const int nout = 2 * P2 * PD;
-  if (o >= nout) return;
-  const int c = o % PD, p = (o / PD) % P2, tb = o / (PD * P2);
-  const int* pos = tb ? pos2 : pos1;
+  const bool live = o < nout;
+  const int c = o % PD, p = (o / PD) % P2, tb = live ? o / (PD * P2) : 0;
   const int s0 = blockIdx.y * chunk, s1 = min(S, s0 + chunk);
+  const long plane = (long)S * L * 2 * PD;
   float acc = 0.f;
-  for (int s = s0; s < s1; ++s) {
-    const int t = p - pos[(long)inst[s] * L];
-    if (t >= 0 && t < L) {
-      const long i = ((long)s * L + t) * 2 * PD + tb * PD + c;
-      acc += planes == 2 ? dxp[i] + dxp[i + (long)S * L * 2 * PD] : dxp[i];
+  for (int b = s0; b < s1; b += TILE) {
+    const int n = min(TILE, s1 - b);
+    __syncthreads();
+    for (int j = threadIdx.x; j < n; j += 256) {
+      const long r = (long)inst[b + j] * L;
+      off[0][j] = pos1[r];
+      off[1][j] = pos2[r];
     }
+    __syncthreads();
+    if (live)
+      for (int j = 0; j < n; ++j) {
+        const int t = p - off[tb][j];
+        if (t >= 0 && t < L) {
+          const long i = ((long)(b + j) * L + t) * 2 * PD + tb * PD + c;
+          acc += planes == 2 ? dxp[i] + dxp[i + plane] : dxp[i];
+        }
+      }
   }
-  part[(long)blockIdx.y * nout + o] = acc;
+  if (live) part[(long)blockIdx.y * nout + o] = acc;
 }
 
 namespace ina {
