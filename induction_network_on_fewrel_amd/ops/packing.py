@@ -406,6 +406,34 @@ def unpack_wide_grads(dwx: torch.Tensor, dwh: torch.Tensor, db: torch.Tensor, U:
 
 
 @lru_cache(maxsize=None)
+def _merged_wgrad_idx(U: int, D: int, DP: int):
+    """Flat indices into the merged weight-gradient GEMM's output dwall [DP + 2 UP, 2 G4] (rows
+    [x | h_fw | h_bw], columns dir * G4 + permuted gate column; ops/wide.py::WideSeqBiLSTM.backward) for
+    BOTH directions' TF-layout gradients at once: out[d] = [D + U + 1, 4U] = kernel rows (x rows, then
+    the direction's own h rows) and the bias as the last row (x's ones column, row D of dwall).  One
+    gather instead of unpack_wide_grads' zero-fill + index_select + index_copy per block (12 kernels)."""
+    _, _, _, _, src, dst = _wide_idx(U)
+    UP, G4 = wide_shape(U)["UP"], wide_shape(U)["G4"]
+    col = np.empty(4 * U, dtype=np.int64)
+    col[dst.numpy()] = src.numpy()                                   # TF column -> permuted column
+    rows = np.concatenate([np.arange(D), np.zeros(U, dtype=np.int64), [D]])
+    out = np.empty((2, D + U + 1, 4 * U), dtype=np.int64)
+    for d in range(2):
+        r = rows.copy()
+        r[D:D + U] = DP + d * UP + np.arange(U)
+        out[d] = r[:, None] * (2 * G4) + d * G4 + col[None, :]
+    return torch.from_numpy(out.reshape(-1))
+
+
+def unpack_merged_wgrad(dwall: torch.Tensor, U: int, D: int):
+    """dwall [DP + 2 UP, 2 G4] -> ([dK_fw, dK_bw] each [D + U, 4U], [db_fw, db_bw] each [4U]), fp32."""
+    DP = dwall.shape[0] - dwall.shape[1] // 4
+    idx = _on(_merged_wgrad_idx(U, D, DP), dwall.device)
+    g = dwall.float().reshape(-1).index_select(0, idx).view(2, D + U + 1, 4 * U)
+    return [g[0, :D + U], g[1, :D + U]], [g[0, D + U], g[1, D + U]]
+
+
+@lru_cache(maxsize=None)
 def _attn_wide_idx(H: int):
     """Flat indices into a zero-padded [HP, HP] W1 (HP = H rounded up to 32) for the fused attention
     kernels' MFMA A fragments [HP/16 tiles][HP/32 K-steps][64 lanes][8] (csrc/kernels/attn_wide.hip):

@@ -183,7 +183,7 @@ class WideSeqBiLSTM(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        from .packing import unpack_wide_grads
+        from .packing import unpack_merged_wgrad
         o = ops()
         inst, word, pos1, pos2, Xw, wxtc, a2pk, acts, cst = ctx.saved_tensors
         S, L, E, P, U, seed, kp, shift, P2, V = ctx.cfg
@@ -202,13 +202,7 @@ class WideSeqBiLSTM(torch.autograd.Function):
         # cross-direction blocks h_fw^T dG_bw / h_bw^T dG_fw are computed and dropped: 12% more FLOPs, dG read
         # once); x's ones column (row D) makes it the bias gradient as well
         dwall = _wgrad(Xw, dG, 64)                                        # [DP + 2 UP, 2 G4] (split 64; 128 measured slower in the step: 1,325 vs 1,227 us, profiles/r5_merged)
-        dKs, dbs = [], []
-        for d in range(2):
-            c = slice(d * G4, (d + 1) * G4)
-            dwh = dwall[DP + d * UP:DP + (d + 1) * UP, c]
-            dK, db = unpack_wide_grads(dwall[:D, c], dwh, dwall[D, c], U)
-            dKs.append(dK)
-            dbs.append(db)
+        dKs, dbs = unpack_merged_wgrad(dwall, U, D)                      # both directions, one gather
         if fuse:
             dxp = dxpd                                                    # [2, S*L, 2P]: per direction
         else:

@@ -237,3 +237,23 @@ def test_ntn_tile_pack_layout(H, h, N, paper):
     assert di.numel() == NT * (SG if paper else SG * N * N)
     valid = di[di >= 0]
     assert valid.unique().numel() == valid.numel() == (h if paper else h * N * N)
+
+
+def test_unpack_merged_wgrad_matches_per_block_unpack():
+    """ops/packing.py::unpack_merged_wgrad (one gather over the merged [x | h_fw | h_bw] x [fw | bw]
+    weight-gradient GEMM output) equals unpack_wide_grads applied to each direction's diagonal blocks
+    (x rows, the direction's own h rows, bias = row D); the cross-direction blocks are ignored."""
+    import torch
+    from induction_network_on_fewrel_amd.ops.packing import (unpack_merged_wgrad, unpack_wide_grads, wide_shape,
+                                                              wide_x_cols)
+    for U, D in ((100, 310), (128, 60), (64, 15)):
+        s = wide_shape(U)
+        G4, UP = s["G4"], s["UP"]
+        DP = wide_x_cols(D)
+        dwall = torch.randn(DP + 2 * UP, 2 * G4, generator=torch.Generator().manual_seed(U))
+        dKs, dbs = unpack_merged_wgrad(dwall, U, D)
+        for d in range(2):
+            c = slice(d * G4, (d + 1) * G4)
+            dK, db = unpack_wide_grads(dwall[:D, c], dwall[DP + d * UP:DP + (d + 1) * UP, c], dwall[D, c], U)
+            assert dKs[d].shape == (D + U, 4 * U) and torch.equal(dKs[d], dK), (U, d)
+            assert torch.equal(dbs[d], db), (U, d)
