@@ -1,5 +1,6 @@
 // Torch op registrations of the wide BiLSTM cell kernels (csrc/kernels/lstm_wide.hip).
 // Both ops update their output tensors in place (the per-step driver loop lives in ops/wide.py).
+#include <cstdlib>
 #include <algorithm>
 
 #include <ATen/ATen.h>
@@ -241,7 +242,10 @@ Tensor wide_pos_grad(const Tensor& dxp, const Tensor& inst, const Tensor& pos1, 
   const int64_t planes = dxp.dim() == 3 ? 2 : 1;
   const int64_t S = inst.size(0), L = pos1.size(1), PD = dxp.size(-1) / 2;
   chk(dxp, "dxp", at::kFloat, planes * S * L * 2 * PD);
-  const int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(256, S / 64));
+  // sequence chunks (grid.y), cap 1024 (75 -> 45 us vs 256 at the paper configuration, profiles/r5_posc);
+  // INA_POSG_CHUNKS overrides the cap (A/B tuning; deterministic for any value)
+  static const int64_t cap = [] { const char* e = std::getenv("INA_POSG_CHUNKS"); return e ? std::atoll(e) : 1024; }();
+  const int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(cap, 1), S / 16));
   auto part = at::empty({chunks, 2, P2, PD}, dxp.options());
   if (S == 0) return part.sum(0);
   TORCH_CHECK(ina::wide_pos_grad(dxp.data_ptr<float>(), inst.data_ptr<int>(), pos1.data_ptr<int>(), pos2.data_ptr<int>(),
