@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <torch/library.h>
 
+#include <map>
 #include <tuple>
 
 #include "ina_launch.h"
@@ -221,7 +222,9 @@ std::tuple<Tensor, Tensor> bert_gemm(const Tensor& x, const Tensor& w, const c10
   chk(w, "w", at::kBFloat16);
   TORCH_CHECK(w.dim() == 2 && x.size(1) == w.size(1), "ina.bert_gemm: x [M, K], w [N, K]");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0), lda = x.stride(0);
-  TORCH_CHECK(N % 256 == 0 && K % 64 == 0 && K >= 64, "ina.bert_gemm: N must be a multiple of 256, K of 64");
+  TORCH_CHECK(N % 8 == 0 && K % 64 == 0 && K >= 64, "ina.bert_gemm: N must be a multiple of 8, K of 64");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && lda % 8 == 0,
+              "ina.bert_gemm: x must start 16-byte aligned with a row stride that is a multiple of 8");
   TORCH_CHECK(M * lda * 2 < (1LL << 31) && N * K * 2 < (1LL << 31), "ina.bert_gemm: operand too large");
   TORCH_CHECK(epi >= 0 && epi <= 2, "ina.bert_gemm: epi must be 0, 1 or 2");
   const float* bp = nullptr;
@@ -248,6 +251,78 @@ std::tuple<Tensor, Tensor> bert_gemm(const Tensor& x, const Tensor& w, const c10
                              slab.defined() ? slab.data_ptr<float>() : nullptr, (int)epi, stream()),
            "gemm_bf16_nt");
   return {y, epi == 2 ? slab : ax};
+}
+
+// zero bytes for the K-major operands' rows past K (one small buffer per device)
+const void* zero16(const Tensor& like) {
+  static thread_local std::map<int, Tensor> zeros;
+  const int dev = like.get_device();
+  auto it = zeros.find(dev);
+  if (it == zeros.end()) it = zeros.emplace(dev, at::zeros({64}, like.options().dtype(at::kFloat))).first;
+  return it->second.data_ptr();
+}
+
+// y = a b with b K-major (a [M, K], b [K, N]; dx = dy W for a torch-layout weight W [out][in]).  epi 0: plain;
+// 2: y * gelu'(aux) with the column-sum slab [2 ceil(M/256)][N] (FFN dgrad); 4: y added into res IN PLACE (res
+// is returned).  Returns (y, slab-or-empty).
+std::tuple<Tensor, Tensor> gemm_nn(const Tensor& a, const Tensor& b, const c10::optional<Tensor>& aux,
+                                   const c10::optional<Tensor>& res, int64_t epi) {
+  chk(a, "a", at::kBFloat16);
+  chk(b, "b", at::kBFloat16);
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(0), "ina.gemm_nn: a [M, K], b [K, N]");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(1);
+  TORCH_CHECK(N % 8 == 0 && K % 64 == 0 && K >= 64, "ina.gemm_nn: N must be a multiple of 8, K of 64");
+  TORCH_CHECK(M < (1LL << 31), "ina.gemm_nn: too many rows");
+  TORCH_CHECK(epi == 0 || epi == 2 || epi == 4, "ina.gemm_nn: epi must be 0, 2 or 4");
+  Tensor y, ax, slab;
+  if (epi == 4) {
+    TORCH_CHECK(res.has_value() && res->defined(), "ina.gemm_nn: epi 4 needs res");
+    y = *res;
+    chk(y, "res", at::kBFloat16);
+    TORCH_CHECK(y.size(0) == M && y.size(1) == N, "ina.gemm_nn: res must be [M, N]");
+  } else {
+    y = at::empty({M, N}, a.options());
+  }
+  if (epi == 2) {
+    TORCH_CHECK(aux.has_value() && aux->defined(), "ina.gemm_nn: epi 2 needs aux");
+    ax = *aux;
+    chk(ax, "aux", at::kBFloat16);
+    TORCH_CHECK(ax.size(0) == M && ax.size(1) == N, "ina.gemm_nn: aux must be [M, N]");
+    slab = at::empty({2 * ((M + 255) / 256), N}, a.options().dtype(at::kFloat));
+  } else {
+    slab = at::empty({0}, a.options().dtype(at::kFloat));
+  }
+  if (M == 0) return {y, epi == 2 ? slab.zero_() : slab};
+  launched(ina::gemm_bf16(1, a.data_ptr(), (int)K, b.data_ptr(), (int)N, (int)M, (int)N, (int)K, nullptr,
+                          y.data_ptr(), (int)N, epi == 2 ? ax.data_ptr() : nullptr, (int)N,
+                          epi == 2 ? slab.data_ptr<float>() : nullptr, zero16(a), (int)epi, 1, stream()),
+           "gemm_nn");
+  return {y, slab};
+}
+
+// Weight-gradient split-K GEMM: slabs [splits, M, N] fp32 with slabs[s] = sum over the K rows of split s of
+// a[k, :]^T b[k, :] (a [K, M], b [K, N] bf16, K = tokens; splits <= 0: one round of workgroups).  The caller sums
+// the slabs in a fixed order (ina.slab_reduce straight into the flat gradient).
+Tensor gemm_wgrad(const Tensor& a, const Tensor& b, int64_t splits) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16,
+              "ina.gemm_wgrad: bf16 GPU operands");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(0) == b.size(0), "ina.gemm_wgrad: a [K, M], b [K, N]");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1, "ina.gemm_wgrad: unit column stride");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1), lda = a.stride(0), ldb = b.stride(0);
+  TORCH_CHECK(M % 8 == 0 && N % 8 == 0 && M > 0 && N > 0, "ina.gemm_wgrad: M and N must be multiples of 8");
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
+              "ina.gemm_wgrad: 16-byte aligned rows");
+  if (splits <= 0) splits = ina::gemm_wgrad_splits((int)M, (int)N, (int)K);
+  const int64_t ks = (K + 63) / 64;
+  if (splits > ks) splits = ks > 0 ? ks : 1;
+  while (splits > 1 && (splits - 1) * ((ks + splits - 1) / splits) >= ks) --splits;
+  auto out = at::empty({splits, M, N}, a.options().dtype(at::kFloat));
+  if (K == 0) return out.zero_();
+  launched(ina::gemm_bf16(2, a.data_ptr(), (int)lda, b.data_ptr(), (int)ldb, (int)M, (int)N, (int)K, nullptr,
+                          out.data_ptr(), (int)N, nullptr, 0, nullptr, zero16(a), 5, (int)splits, stream()),
+           "gemm_wgrad");
+  return out;
 }
 
 // ------------------------------------------------------------------ fused attention
@@ -331,6 +406,8 @@ TORCH_LIBRARY_FRAGMENT(ina, m) {
   m.def("bert_bias_gelu_fwd", &bert_bias_gelu_fwd);
   m.def("bert_bias_gelu_bwd", &bert_bias_gelu_bwd);
   m.def("bert_gemm", &bert_gemm);
+  m.def("gemm_nn", &gemm_nn);
+  m.def("gemm_wgrad", &gemm_wgrad);
   m.def("bert_mha_fwd", &bert_mha_fwd);
   m.def("bert_mha_bwd", &bert_mha_bwd);
 }

@@ -325,13 +325,20 @@ int embed_ln_bwd(const BertEmbArgs& a, hipStream_t st);
 
 int bias_gelu_fwd(const void* x, const float* b, void* y, long T, int I, hipStream_t st);
 // gemm.hip: C = A B^T (bf16, A [M][K] / B [N][K] K-contiguous), epi 0 plain (+bias), 1 bias+GELU with the
-// pre-activation in aux, 2 C * GELU'(aux) with column-sum slab [2 ceil(M/256)][N].  N % 256 == 0, K % 64 == 0.
+// pre-activation in aux, 2 C * GELU'(aux) with column-sum slab [2 ceil(M/256)][N].  N % 8 == 0, K % 64 == 0.
 // reduction GEMM slab[s][i][j] = sum_{k in split s} A[k][i] B[k][j] (gemm_tn.hip): K % 64 == 0, MI <= 64, MI % 8 == 0
 int gemm_tn_splits(int K, int MI, int NJ);
 int gemm_tn_slab(const void* A, int lda, const void* B, int ldb, int K, int MI, int NJ, const void* zero, float* slab,
                  int splits, hipStream_t st);
 int gemm_bf16_nt(const void* A, int lda, const void* B, int ldb, int M, int N, int K, const float* bias, void* out,
                  int ldo, void* aux, int ldx, float* slab, int epi, hipStream_t st);
+// gemm.hip, every layout: layout 0 NT (A [M][K], B [N][K]), 1 NN (A [M][K], B [K][N]), 2 TN (A [K][M], B [K][N]);
+// epi 0 plain (+bias), 1 bias+GELU (aux), 2 C * GELU'(aux) + column-sum slab, 4 C + out (residual, in place),
+// 5 fp32 split-K slabs out[split][M][ldo] (TN only).  N % 8 == 0; K-major A needs M % 8 == 0; direct operands
+// K % 64 == 0; zero: >= 16 zero bytes (K-major rows past K).
+int gemm_bf16(int layout, const void* A, int lda, const void* B, int ldb, int M, int N, int K, const float* bias,
+              void* out, int ldo, void* aux, int ldx, float* slab, const void* zero, int epi, int splits, hipStream_t st);
+int gemm_wgrad_splits(int M, int N, int K);
 int bias_gelu_bwd(const void* dy, const void* x, const float* b, void* dx, float* slab, int T, int I, int blocks,
                   hipStream_t st);
 

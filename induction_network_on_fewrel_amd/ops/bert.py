@@ -49,8 +49,18 @@ def _contiguous_region(ts: List[torch.Tensor]) -> Optional[torch.Tensor]:
     return torch.as_strided(base.detach(), (total,), (1,), off)
 
 
+def _own_wgrad_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
+    """Shapes the own TN split-K GEMM takes (csrc/kernels/gemm.hip: 16-byte column chunks, bf16 GPU rows)."""
+    return (dy.is_cuda and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.shape[1] % 8 == 0
+            and x.shape[1] % 8 == 0 and dy.stride(1) == 1 and x.stride(1) == 1 and dy.stride(0) % 8 == 0
+            and x.stride(0) % 8 == 0 and dy.shape[0] > 0)
+
+
 def _wgrad_parts(dy: torch.Tensor, x: torch.Tensor):
-    """The 16 fp32 K-chunk partials of dy^T x ([16, o, i]), or None where _wgrad uses one GEMM."""
+    """fp32 split-K partials [splits, o, i] of dy^T x (own TN GEMM: one round of 256x256 output tiles over the
+    CUs, K = tokens split so every CU has a tile), or None where _wgrad uses one GEMM."""
+    if _own_wgrad_ok(dy, x):
+        return ops().gemm_wgrad(dy, x, 0)
     T, o = dy.shape
     i = x.shape[1]
     nc = 16
@@ -60,16 +70,38 @@ def _wgrad_parts(dy: torch.Tensor, x: torch.Tensor):
 
 
 def _wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
-    """dW = dy^T x in fp32.  K = tokens is the long dimension and the output has few 256x256 tiles, so
-    the reduction is split by hand into 16 K-chunks (one batched GEMM, fp32 out) + a sum: 1.4-3x the
-    plain GEMM at the BERT-base shapes (tools/gemm_bench.py, profiles/r1_gemm_bench.log)."""
-    T, o = dy.shape
-    i = x.shape[1]
-    nc = 16
-    if T % nc != 0 or T < 4096:
+    """dW = dy^T x in fp32.  K = tokens is the long dimension and the output has few 256x256 tiles, so the
+    reduction is split-K (own TN GEMM slabs: 380 vs 467 us for hipBLASLt's 16-chunk bmm at the QKV shape,
+    profiles/r6_gemm) + an ordered sum."""
+    part = _wgrad_parts(dy, x)
+    if part is None:
         return torch.mm(dy.t(), x, out_dtype=torch.float32)
-    part = torch.bmm(dy.view(nc, T // nc, o).transpose(1, 2), x.view(nc, T // nc, i), out_dtype=torch.float32)
     return part.sum(0)
+
+
+def _own_nn_ok(dy: torch.Tensor, W: torch.Tensor) -> bool:
+    return (dy.is_cuda and dy.dtype == torch.bfloat16 and W.dtype == torch.bfloat16 and dy.is_contiguous()
+            and W.is_contiguous() and dy.shape[1] % 64 == 0 and W.shape[1] % 8 == 0)
+
+
+def _dgrad(dy: torch.Tensor, W: torch.Tensor, res: Optional[torch.Tensor]) -> torch.Tensor:
+    """dx = dy W (+ res, in place): the own NN GEMM (W [out][in] read K-major, residual added in its epilogue)."""
+    if _own_nn_ok(dy, W) and (res is None or (res.is_contiguous() and res.dtype == torch.bfloat16)):
+        return ops().gemm_nn(dy, W, None, res, 4 if res is not None else 0)[0]
+    return res.addmm_(dy, W) if res is not None else torch.mm(dy, W)
+
+
+def _own_nt() -> bool:
+    """Forward linears on the own NT GEMM (INA_BERT_OWN_NT=1) instead of hipBLASLt addmm."""
+    return os.environ.get("INA_BERT_OWN_NT", "0") == "1"
+
+
+def _fwd_linear(x: torch.Tensor, Wb: torch.Tensor, bias: Optional[torch.Tensor], bb: Optional[torch.Tensor]):
+    """y = x W^T (+ b): own NT GEMM with the fp32 bias in its epilogue (INA_BERT_OWN_NT=1) or hipBLASLt."""
+    if (_own_nt() and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.shape[1] % 64 == 0
+            and Wb.shape[0] % 8 == 0):
+        return ops().bert_gemm(x, Wb, bias, None, 0)[0]
+    return torch.addmm(bb, x, Wb.t()) if bb is not None else torch.mm(x, Wb.t())
 
 
 class _Linear(torch.autograd.Function):
@@ -80,12 +112,12 @@ class _Linear(torch.autograd.Function):
     gradient buffer spans (trainer path) or returns them per parameter (plain autograd)."""
 
     @staticmethod
-    def forward(ctx, x, Wb, bb, gW, gb, nw, on_done, db_ext, dx_acc, *params):
+    def forward(ctx, x, Wb, bb, gW, gb, nw, on_done, db_ext, dx_acc, bf32, *params):
         """db_ext: the bias gradient is produced by the consumer's backward (_LnRes / _Mha: column sums
         of the same dy, fused into their kernels), so this backward skips the dy.sum(0) pass.
         dx_acc: a _ResGrad holder; x's other gradient (the residual branch of the LayerNorm that also
         reads x) is added by the dgrad GEMM itself (addmm, beta = 1) instead of autograd's bf16 add."""
-        y = torch.addmm(bb, x, Wb.t()) if bb is not None else torch.mm(x, Wb.t())
+        y = _fwd_linear(x, Wb, bf32, bb)
         ctx.save_for_backward(x, Wb)
         ctx.cfg = (gW, gb, nw, [tuple(p.shape) for p in params], bb is not None and not db_ext, on_done, dx_acc)
         return y
@@ -96,8 +128,8 @@ class _Linear(torch.autograd.Function):
         gW, gb, nw, shapes, has_b, on_done, dx_acc = ctx.cfg
         dy = dy.contiguous()
         res = dx_acc.take() if dx_acc is not None else None
-        # in place into the LayerNorm's fresh residual gradient (out-of-place addmm copies C first)
-        dx = res.addmm_(dy, Wb) if res is not None else torch.mm(dy, Wb)
+        # in place into the LayerNorm's fresh residual gradient (the own NN GEMM's residual epilogue)
+        dx = _dgrad(dy, Wb, res)
         db = dy.sum(0, dtype=torch.float32) if has_b else None
         outs = [None] * len(shapes)
         part = _wgrad_parts(dy, x) if gW is not None and gW.is_contiguous() else None
@@ -123,7 +155,7 @@ class _Linear(torch.autograd.Function):
                     o += shapes[i][0]
         if on_done is not None:   # last backward op of a layer: its gradient bucket is final
             on_done()
-        return (dx, None, None, None, None, None, None, None, None) + tuple(outs)
+        return (dx, None, None, None, None, None, None, None, None, None) + tuple(outs)
 
 
 def _add_wgrad(gW, dy, x, shape):
@@ -149,9 +181,9 @@ class _Ffn(torch.autograd.Function):
     b2's gradient comes from the following _LnRes (db_ext), as for the unfused path."""
 
     @staticmethod
-    def forward(ctx, x, W1b, W2b, bb2, gW1, gW2, dx_acc, meta, b1name, W1, b1, W2):
+    def forward(ctx, x, W1b, W2b, bb2, gW1, gW2, dx_acc, meta, b1name, b2f, W1, b1, W2):
         h, aux = ops().bert_gemm(x, W1b, b1.detach(), None, 1)
-        o = torch.addmm(bb2, h, W2b.t())
+        o = _fwd_linear(h, W2b, b2f, bb2)
         ctx.save_for_backward(x, W1b, W2b, h, aux)
         ctx.cfg = (gW1, gW2, dx_acc, meta, b1name, tuple(W1.shape), tuple(W2.shape))
         return o
@@ -161,10 +193,10 @@ class _Ffn(torch.autograd.Function):
         x, W1b, W2b, h, aux = ctx.saved_tensors
         gW1, gW2, dx_acc, meta, b1name, s1, s2 = ctx.cfg
         do = do.contiguous()
-        dpre, slab = ops().bert_gemm(do, W2b.t().contiguous(), None, aux, 2)
+        dpre, slab = ops().gemm_nn(do, W2b, aux, None, 2)   # W2 [Hd][I] read K-major: no transposed copy
         dW2 = _add_wgrad(gW2, do, h, s2)
         res = dx_acc.take() if dx_acc is not None else None
-        dx = res.addmm_(dpre, W1b) if res is not None else torch.mm(dpre, W1b)
+        dx = _dgrad(dpre, W1b, res)
         dW1 = _add_wgrad(gW1, dpre, x, s1)
         glue, maps = _glue_maps(meta, [b1name])
         db1 = None
@@ -172,7 +204,7 @@ class _Ffn(torch.autograd.Function):
             glue.add(slab, maps[0], slab.shape[0])
         else:
             db1 = _route_grad(meta, b1name, slab.sum(0))
-        return dx, None, None, None, None, None, None, None, None, dW1, db1, dW2
+        return dx, None, None, None, None, None, None, None, None, None, dW1, db1, dW2
 
 
 def own_ffn_enabled(I: int, Hd: int) -> bool:
@@ -377,10 +409,17 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
         cnt = sum(offs[m][1] for m in ns)
         return torch.as_strided(g0, (cnt,), (1,), g0.storage_offset())
 
+    def bias32(ns):
+        """fp32 bias over consecutive params ns (the own NT GEMM's epilogue operand), detached."""
+        ts = [P(n).detach() for n in ns]
+        r = _contiguous_region(ts)
+        return r if r is not None else torch.cat([t.reshape(-1) for t in ts])
+
     def linear(x, wn, bn, out_dim, in_dim, on_done=None, db_ext=False, dx_acc=None):
         Wb = wspan(wn, (out_dim, in_dim))
         bb = wspan(bn, (out_dim,)) if bn else None
-        return _Linear.apply(x, Wb, bb, gspan(wn), gspan(bn) if bn else None, len(wn), on_done, db_ext, dx_acc,
+        bf = bias32(bn) if bn and _own_nt() else None
+        return _Linear.apply(x, Wb, bb, gspan(wn), gspan(bn) if bn else None, len(wn), on_done, db_ext, dx_acc, bf,
                              *[P(n) for n in wn], *[P(n) for n in (bn or [])])
 
     # DP overlap: the QKV projection's backward is the last backward op of layer i -> bucket i is final
@@ -421,7 +460,8 @@ def bert_encode(model, inst: torch.Tensor, data, training: bool, seed: int,
                               pre + "output.dense.weight", pre + "output.dense.bias")
         if own_ffn:
             o = _Ffn.apply(x, wspan([w1n], (I, Hd)), wspan([w2n], (Hd, I)), wspan([b2n], (Hd,)), gspan([w1n]),
-                           gspan([w2n]), r2, meta, by_name[b1n], P(w1n), P(b1n), P(w2n))
+                           gspan([w2n]), r2, meta, by_name[b1n], bias32([b2n]) if _own_nt() else None, P(w1n),
+                           P(b1n), P(w2n))
         else:
             hpre = linear(x, [w1n], None, I, Hd, dx_acc=r2)
             h = _BiasGelu.apply(hpre, P(b1n), meta, by_name[b1n])
