@@ -1,5 +1,11 @@
 """BERT encoder on the GPU path: hand-written gfx950 kernels + hipBLASLt GEMMs (bf16).
 
+GEMMs (csrc/kernels/gemm.hip is one NT / NN / TN kernel family): every weight gradient dW = dy^T x runs on the
+own TN split-K kernel (fp32 slabs summed into the flat gradient: 377-500 vs 469-581 us for hipBLASLt at the four
+BERT-base shapes, BERT 111.7 vs 109.6 episodes/s, profiles/r6_gemm, r6_bert); the FFN-up forward (bias + GELU)
+and its dgrad (GELU' + db) on the own NT kernel; the other forwards / dgrads on hipBLASLt by default
+(INA_BERT_OWN_NT=1 / INA_BERT_OWN_NN=1 put them on the own kernels: 1-2% slower end to end, see _own_nn_ok).
+
 Per layer (post-LN BERT, models/bert.py is the oracle):
     qkv = x Wqkv^T + bqkv            torch.addmm (bf16 -> hipBLASLt); Wqkv is ONE [3Hd, Hd] view of the
                                      flat bf16 weight copy (q/k/v are adjacent in the flat buffer)
@@ -50,8 +56,9 @@ def _contiguous_region(ts: List[torch.Tensor]) -> Optional[torch.Tensor]:
 
 
 def _own_wgrad_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
-    """Shapes the own TN split-K GEMM takes (csrc/kernels/gemm.hip: 16-byte column chunks, bf16 GPU rows)."""
-    return (dy.is_cuda and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.shape[1] % 8 == 0
+    """Shapes the own TN split-K GEMM takes (csrc/kernels/gemm.hip: 16-byte column chunks, bf16 GPU rows);
+    INA_BERT_OWN_WGRAD=0 selects hipBLASLt (A/B)."""
+    return (os.environ.get("INA_BERT_OWN_WGRAD", "1") != "0" and dy.is_cuda and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.shape[1] % 8 == 0
             and x.shape[1] % 8 == 0 and dy.stride(1) == 1 and x.stride(1) == 1 and dy.stride(0) % 8 == 0
             and x.stride(0) % 8 == 0 and dy.shape[0] > 0)
 
@@ -80,7 +87,11 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
 
 
 def _own_nn_ok(dy: torch.Tensor, W: torch.Tensor) -> bool:
-    return (dy.is_cuda and dy.dtype == torch.bfloat16 and W.dtype == torch.bfloat16 and dy.is_contiguous()
+    """The own NN dgrad GEMM, opt-in (INA_BERT_OWN_NN=1).  Measured in the BERT step (profiles/r6_bert1): 2% slower
+    than hipBLASLt -- ~6% tile quantization at N = 768 (400 x 3 tiles over 256 CUs: 5 rounds for 4.69 of work;
+    hipBLASLt's stream-K kernels split the last round), and its GELU' epilogue at N = 3072 takes 875 us against
+    761 us for the NT kernel's (+ a 5 us transposed weight copy)."""
+    return (os.environ.get("INA_BERT_OWN_NN", "0") == "1" and dy.is_cuda and dy.dtype == torch.bfloat16 and W.dtype == torch.bfloat16 and dy.is_contiguous()
             and W.is_contiguous() and dy.shape[1] % 64 == 0 and W.shape[1] % 8 == 0)
 
 
@@ -193,7 +204,10 @@ class _Ffn(torch.autograd.Function):
         x, W1b, W2b, h, aux = ctx.saved_tensors
         gW1, gW2, dx_acc, meta, b1name, s1, s2 = ctx.cfg
         do = do.contiguous()
-        dpre, slab = ops().gemm_nn(do, W2b, aux, None, 2)   # W2 [Hd][I] read K-major: no transposed copy
+        if _own_nn_ok(do, W2b):   # W2 [Hd][I] read K-major: no transposed copy
+            dpre, slab = ops().gemm_nn(do, W2b, aux, None, 2)
+        else:
+            dpre, slab = ops().bert_gemm(do, W2b.t().contiguous(), None, aux, 2)
         dW2 = _add_wgrad(gW2, do, h, s2)
         res = dx_acc.take() if dx_acc is not None else None
         dx = _dgrad(dpre, W1b, res)
