@@ -22,14 +22,6 @@
 
 using namespace ina;
 
-#ifndef INA_FWD_PIPE
-#define INA_FWD_PIPE 1
-#endif
-#ifndef INA_BWD_TC_FROM_H
-// lean BPTT: tanh(c_t) = h_t / o_t = h_t (1 + 2^-z_o) from the step record's h_t and the o gate's exp (no
-// exp / rcp pair per unit and step for tanh(c_t); h_t is the forward's bf16 h, relative error <= 2^-9)
-#define INA_BWD_TC_FROM_H 1
-#endif
 namespace {
 
 template <int U, int NX, bool BF16>
@@ -561,6 +553,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     const uint32_t wvo = valid ? (uint32_t)rb0 * 16u + 4u * (uint32_t)q : 0x80000000u;
     const int R = 2 * L;
     const uint32_t vm = valid ? 0xFFFFFFFFu : 0u;   // padding sequences: x = 0
+    // (the table reads are 47% LDS bank conflicts -- 16 lanes at random rows -- but prefetched a step ahead: a
+    // timing-only build with every lane at row t (broadcast, conflict-free) ran lstm_fwd 770 vs 786 us,
+    // 0.4% of the step, profiles/r6_bcast; a private table per lane would cost the kernel its occupancy)
     const int o1 = valid ? pos1[rb0] : 0, o2 = valid ? pos2[rb0] : 0;
     const char* tb1 = reinterpret_cast<const char*>(ids_all) + ((q * 2) * R + o1) * 8;
     const char* tb2 = reinterpret_cast<const char*>(ids_all) + ((q * 2 + 1) * R + o2) * 8;
@@ -654,16 +649,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     return;
   }
   float xa[NX], xb[NX];
-#if INA_FWD_PIPE == 0
-  // simple loop: prefetch x_{tau+1}, copy at the end of the step
-  load_x(tof(0), xa);
-  for (int tau = 0; tau < L; ++tau) {
-    load_x(tof(min(tau + 1, L - 1)), xb);
-    step(tau, xa);
-#pragma unroll
-    for (int xi = 0; xi < NX; ++xi) xa[xi] = xb[xi];
-  }
-#else
   // sched_barrier pins each prefetch ahead of the step it overlaps (the machine scheduler would
   // otherwise sink the loads next to their uses to save registers)
   auto pair = [&](int tau) __attribute__((always_inline)) {
@@ -686,7 +671,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   }
   for (; tau + 1 < L; tau += 2) pair(tau);
   if (tau < L) step(tau, xa);
-#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1222,15 +1206,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
             acc = mma(lA[(m * NKS + ks) * 64 + lane],
                       __builtin_bit_cast(u16x8_t, u32x4_t{bw[4 * ks], bw[4 * ks + 1], bw[4 * ks + 2], bw[4 * ks + 3]}), acc);
           const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]);
-#if INA_BWD_TC_FROM_H
-          // o = 1 / (1 + e), e = 2^-z_o (z clamped: e stays finite, and where o ~ 0 every use of tc is scaled by o)
+          // lean BPTT: tanh(c_t) = h_t / o_t = h_t (1 + 2^-z_o) from the step record's h_t and the o gate's exp
+          // (no exp / rcp pair per unit and step for tanh(c_t); h_t is the forward's bf16 h, relative error
+          // <= 2^-9).  o = 1 / (1 + e), e = 2^-z_o (z clamped: e stays finite, and where o ~ 0 every use of tc is
+          // scaled by o)
           const float eo = __builtin_amdgcn_exp2f(fminf(-acc[3], 126.f));
           const float og = fast_rcp(1.f + eo);
           const float tc = hcv[m] * (1.f + eo);
-#else
-          const float og = sigmoid_l2(acc[3]);
-          const float tc = tanh_l2(ccur[m] * (2.f * LOG2E_F));
-#endif
           const float dh = dh_rec[m] + dhin[m];
           // (shared products: the step is VALU-issue bound -- README "ISA budget"; 14 instead of 16 ops per unit)
           const float dho = dh * og;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel timing of the encoder ops at the bench shape (hip events, median of reps).
 
-Used to A/B kernel variants: build one with ``INA_BUILD_TAG=v1 INA_VARIANT_FLAGS=-DINA_FWD_PIPE=0
+Used to A/B kernel variants: build one with ``INA_BUILD_TAG=v1 INA_VARIANT_FLAGS=-DSOME_KNOB=0
 python csrc/build.py`` and run ``INA_KERNEL_LIB=variants/_ina_kernels_v1.so python tools/kbench.py``.
 Prints one JSON line {op: ms}.
 """
