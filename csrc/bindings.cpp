@@ -671,11 +671,15 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> ntn_bwd(const Tensor& cls, const Tens
 
 int64_t ntn_slices_per_tile(int64_t N) { return ina::ntn_slices_per_tile((int)N); }
 
-// slab [splits, MI, NJ] fp32 = per-split sums over k of A[k, :MI]^T B[k, :] (A [K, lda], B [K, NJ] bf16; K % 64 == 0)
+// slab [splits, MI, NJ] fp32 = per-split sums over k of A[k, :MI]^T B[k, :NJ] (A [K, >= MI], B [K, >= NJ] bf16 rows
+// with unit column stride, row strides multiples of 8, 16-byte aligned bases; K % 64 == 0)
 Tensor gemm_tn_slab(const Tensor& A, const Tensor& B, int64_t MI, int64_t splits) {
-  check(A, "A", at::kBFloat16);
-  check(B, "B", at::kBFloat16);
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16,
+              "ina.gemm_tn_slab: bf16 GPU operands");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(0) == B.size(0), "ina.gemm_tn_slab: A [K, lda], B [K, NJ]");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
+              "ina.gemm_tn_slab: rows with unit column stride, strides % 8 == 0, 16-byte aligned");
   const int64_t K = A.size(0), NJ = B.size(1);
   TORCH_CHECK(K % 64 == 0 && MI % 8 == 0 && MI > 0 && MI <= 64 && MI <= A.size(1) && NJ % 8 == 0 && NJ >= 8,
               "ina.gemm_tn_slab: needs K % 64 == 0, MI % 8 == 0, MI <= 64, NJ % 8 == 0");
@@ -685,8 +689,8 @@ Tensor gemm_tn_slab(const Tensor& A, const Tensor& B, int64_t MI, int64_t splits
   const int dev = A.get_device();
   auto it = zeros.find(dev);
   if (it == zeros.end()) it = zeros.emplace(dev, at::zeros({64}, A.options())).first;
-  check_launch(ina::gemm_tn_slab(A.data_ptr(), (int)A.size(1), B.data_ptr(), (int)NJ, (int)K, (int)MI, (int)NJ,
-                                 it->second.data_ptr(), slab.data_ptr<float>(), (int)splits, cur_stream()),
+  check_launch(ina::gemm_tn_slab(A.data_ptr(), (int)A.stride(0), B.data_ptr(), (int)B.stride(0), (int)K, (int)MI,
+                                 (int)NJ, it->second.data_ptr(), slab.data_ptr<float>(), (int)splits, cur_stream()),
                "gemm_tn_slab");
   return slab;
 }

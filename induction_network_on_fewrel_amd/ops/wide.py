@@ -20,11 +20,23 @@ import torch
 from ._ext import ops
 
 
+def _own_tn_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Operands the own TN split-K GEMM takes (csrc/kernels/gemm.hip): bf16 GPU rows, unit column stride, widths and
+    row strides multiples of 8.  INA_WIDE_OWN_WGRAD=0 selects hipBLASLt (A/B)."""
+    import os
+    return (os.environ.get("INA_WIDE_OWN_WGRAD", "1") != "0" and a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2
+            and a.stride(1) == 1 and b.stride(1) == 1 and a.shape[1] % 8 == 0 and b.shape[1] % 8 == 0
+            and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0 and a.shape[0] > 0)
+
+
 def _wgrad(a: torch.Tensor, b: torch.Tensor, split: int = 16) -> torch.Tensor:
-    """a^T b in fp32 for tall bf16 a [T, m], b [T, n] (K = T split into `split` chunks: hipBLASLt runs a
-    single K = 1.2 M GEMM on a handful of output tiles; tools/gemm_probe.py measured 16-64 best for the
-    x-projection, 128 for the 256 x 256 attention weight).  A T that `split` does not divide takes the
-    largest smaller power-of-two split that does."""
+    """a^T b in fp32 for tall bf16 a [T, m], b [T, n]: the own TN split-K GEMM (one round of 256 x 256 output tiles
+    over the CUs, fp32 slabs + an ordered sum; 242 vs 245 us for hipBLASLt's split-128 batch at the paper
+    attention dW1, profiles/r6_gemm) or, for other operands, hipBLASLt with K = T split into `split` chunks
+    (a single K = 1.2 M GEMM runs on a handful of output tiles; a T that `split` does not divide takes the largest
+    smaller power-of-two split that does)."""
+    if _own_tn_ok(a, b):
+        return ops().gemm_wgrad(a, b, 0).sum(0)
     T = a.shape[0]
     sp = split
     while sp > 1 and (T % sp or T < 256 * sp):
@@ -33,6 +45,24 @@ def _wgrad(a: torch.Tensor, b: torch.Tensor, split: int = 16) -> torch.Tensor:
         part = torch.bmm(a.view(sp, T // sp, -1).transpose(1, 2), b.view(sp, T // sp, -1), out_dtype=torch.float32)
         return part.sum(0)
     return torch.mm(a.t(), b, out_dtype=torch.float32)
+
+
+def merged_wgrad(Xw: torch.Tensor, dG: torch.Tensor, UP: int) -> torch.Tensor:
+    """dwall = Xw^T dG for the merged weight gradient ([x | h_fw | h_bw] rows, [dG_fw | dG_bw] columns): the rows
+    that fill whole 256-row tiles on the own TN split-K GEMM and a ragged tail of h_bw rows (<= 64, needed only
+    against dG_bw) on the MI <= 64 reduction GEMM (gemm_tn.hip) -- no 256-row tile computed for 64 rows.  The
+    cross-direction blocks are never read (unpack_merged_wgrad); the tail's h_bw x dG_fw block is left unset."""
+    R, C = Xw.shape[1], dG.shape[1]
+    full = R // 256 * 256
+    tail = R - full
+    if not (_own_tn_ok(Xw, dG) and 0 < tail <= 64 and tail % 8 == 0 and full >= R - UP and Xw.shape[0] % 64 == 0):
+        return _wgrad(Xw, dG, 64)
+    o = ops()
+    dwall = torch.empty(R, C, device=Xw.device, dtype=torch.float32)
+    torch.sum(o.gemm_wgrad(Xw[:, :full], dG, 0), 0, out=dwall[:full])
+    half = C // 2
+    dwall[full:, half:] = o.gemm_tn_slab(Xw[:, full:], dG[:, half:], tail, 0).sum(0)
+    return dwall
 
 
 class WideBiLSTM(torch.autograd.Function):
@@ -201,7 +231,7 @@ class WideSeqBiLSTM(torch.autograd.Function):
         # ONE GEMM for both directions' x- and h-kernel gradients over the rows [x | h_fw | h_bw] (the two
         # cross-direction blocks h_fw^T dG_bw / h_bw^T dG_fw are computed and dropped: 12% more FLOPs, dG read
         # once); x's ones column (row D) makes it the bias gradient as well
-        dwall = _wgrad(Xw, dG, 64)                                        # [DP + 2 UP, 2 G4] (split 64; 128 measured slower in the step: 1,325 vs 1,227 us, profiles/r5_merged)
+        dwall = merged_wgrad(Xw, dG, UP)                                  # [DP + 2 UP, 2 G4]
         dKs, dbs = unpack_merged_wgrad(dwall, U, D)                      # both directions, one gather
         if fuse:
             dxp = dxpd                                                    # [2, S*L, 2P]: per direction
