@@ -29,13 +29,13 @@ def _own_tn_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
             and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0 and a.shape[0] > 0)
 
 
-def _wgrad(a: torch.Tensor, b: torch.Tensor, split: int = 16) -> torch.Tensor:
+def _wgrad(a: torch.Tensor, b: torch.Tensor, split: int = 16, own: bool = True) -> torch.Tensor:
     """a^T b in fp32 for tall bf16 a [T, m], b [T, n]: the own TN split-K GEMM (one round of 256 x 256 output tiles
     over the CUs, fp32 slabs + an ordered sum; 242 vs 245 us for hipBLASLt's split-128 batch at the paper
     attention dW1, profiles/r6_gemm) or, for other operands, hipBLASLt with K = T split into `split` chunks
     (a single K = 1.2 M GEMM runs on a handful of output tiles; a T that `split` does not divide takes the largest
     smaller power-of-two split that does)."""
-    if _own_tn_ok(a, b):
+    if own and _own_tn_ok(a, b):
         return ops().gemm_wgrad(a, b, 0).sum(0)
     T = a.shape[0]
     sp = split
@@ -45,24 +45,6 @@ def _wgrad(a: torch.Tensor, b: torch.Tensor, split: int = 16) -> torch.Tensor:
         part = torch.bmm(a.view(sp, T // sp, -1).transpose(1, 2), b.view(sp, T // sp, -1), out_dtype=torch.float32)
         return part.sum(0)
     return torch.mm(a.t(), b, out_dtype=torch.float32)
-
-
-def merged_wgrad(Xw: torch.Tensor, dG: torch.Tensor, UP: int) -> torch.Tensor:
-    """dwall = Xw^T dG for the merged weight gradient ([x | h_fw | h_bw] rows, [dG_fw | dG_bw] columns): the rows
-    that fill whole 256-row tiles on the own TN split-K GEMM and a ragged tail of h_bw rows (<= 64, needed only
-    against dG_bw) on the MI <= 64 reduction GEMM (gemm_tn.hip) -- no 256-row tile computed for 64 rows.  The
-    cross-direction blocks are never read (unpack_merged_wgrad); the tail's h_bw x dG_fw block is left unset."""
-    R, C = Xw.shape[1], dG.shape[1]
-    full = R // 256 * 256
-    tail = R - full
-    if not (_own_tn_ok(Xw, dG) and 0 < tail <= 64 and tail % 8 == 0 and full >= R - UP and Xw.shape[0] % 64 == 0):
-        return _wgrad(Xw, dG, 64)
-    o = ops()
-    dwall = torch.empty(R, C, device=Xw.device, dtype=torch.float32)
-    torch.sum(o.gemm_wgrad(Xw[:, :full], dG, 0), 0, out=dwall[:full])
-    half = C // 2
-    dwall[full:, half:] = o.gemm_tn_slab(Xw[:, full:], dG[:, half:], tail, 0).sum(0)
-    return dwall
 
 
 class WideBiLSTM(torch.autograd.Function):
@@ -231,7 +213,11 @@ class WideSeqBiLSTM(torch.autograd.Function):
         # ONE GEMM for both directions' x- and h-kernel gradients over the rows [x | h_fw | h_bw] (the two
         # cross-direction blocks h_fw^T dG_bw / h_bw^T dG_fw are computed and dropped: 12% more FLOPs, dG read
         # once); x's ones column (row D) makes it the bias gradient as well
-        dwall = merged_wgrad(Xw, dG, UP)                                  # [DP + 2 UP, 2 G4]
+        # [DP + 2 UP, 2 G4] on hipBLASLt split-64: 1,227 us in the step (profiles/r5_merged); the own TN kernel on the
+        # 512 rows that fill 256-row tiles + gemm_tn.hip for the 64-row h_bw tail took 1,190 + 224 us (paper 32.2-32.6k
+        # vs 32.9-33.1k episodes/s, profiles/r6_paper1): at this shape hipBLASLt's main loop (1.14 PF/s) beats the own
+        # one (1.04)
+        dwall = _wgrad(Xw, dG, 64, own=False)
         dKs, dbs = unpack_merged_wgrad(dwall, U, D)                      # both directions, one gather
         if fuse:
             dxp = dxpd                                                    # [2, S*L, 2P]: per direction

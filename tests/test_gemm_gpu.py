@@ -193,18 +193,3 @@ def test_gemm_tn_slab(K, MI, NJ, splits):
     # fp32 accumulation of exact bf16 products: only summation-order differences
     assert (err / (ref.abs() + (K ** 0.5))).max().item() < 1e-4, err.max().item()
 
-
-def test_merged_wgrad_split():
-    """The paper configuration's merged weight gradient (ops/wide.py::merged_wgrad): 512 rows on the own TN split-K
-    GEMM + the 64-row h_bw tail on gemm_tn.hip against dG_bw only -- every block unpack_merged_wgrad reads matches
-    fp32 torch (the tail's cross-direction block is not computed)."""
-    from induction_network_on_fewrel_amd.ops.wide import merged_wgrad
-    torch.manual_seed(3)
-    T, R, C, UP = 64 * 150, 576, 1024, 128
-    Xw = torch.randn(T, R, device=dev).bfloat16()
-    dG = torch.randn(T, C, device=dev).bfloat16()
-    got = merged_wgrad(Xw, dG, UP)
-    ref = Xw.float().t() @ dG.float()
-    scale = T ** 0.5
-    assert ((got[:512] - ref[:512]).abs() / (ref[:512].abs() + scale)).max().item() < 1e-4
-    assert ((got[512:, 512:] - ref[512:, 512:]).abs() / (ref[512:, 512:].abs() + scale)).max().item() < 1e-4
