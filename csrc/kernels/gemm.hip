@@ -46,11 +46,13 @@
 // owns 4 consecutive output columns of one row -> 16-byte stores after two permlane swaps (widen), fp32 slab
 // rows as float4, and the bias-gradient column sums are in-lane adds + one 16-lane DPP reduction.
 //
-// Ragged shapes: direct-operand rows past M / N are clamped to the last row on load (every thread issues the
-// same DMA count, so the counted waits stay exact) and never stored; K-major operand columns past M / N are
-// clamped to the last 16-byte chunk (M, N multiples of 8) and never stored; K-major rows past K read a zero
-// buffer, so a K-major K may be any multiple of 8 and split-K ranges may run past it.  Direct operands need
-// K % 64 == 0.
+// Staging cost (profiles/r6_gpmc): every lane keeps its 8 piece offsets relative to the tile origin; the tile
+// origin and the K-step are the uniform soffset, so a K-step's 8 DMAs cost no address VALU.
+// Ragged shapes: direct-operand rows past M / N (every thread still issues the same DMA count, so the counted
+// waits stay exact) and never stored; K-major operand columns past M / N are
+// out of range and never stored (M, N multiples of 8); K-major rows past K are out of range, so a K-major K may be
+// any value and split-K ranges may run past it.  Out-of-range pieces are buffer loads at an offset past the
+// descriptor's byte count: they write zeros (no clamp, no zero buffer).  Direct operands need K % 64 == 0.
 #include "ina_common.h"
 #include "ina_launch.h"
 
@@ -71,7 +73,6 @@ enum { EPI_PLAIN = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_PLAIN_B = 3, EPI_RES = 4,
 struct GemmArgs {
   const unsigned short* A;
   const unsigned short* B;
-  const unsigned short* zero;   // >= 16 zero bytes (K-major rows past K)
   const float* bias;
   void* out;                    // bf16 [M][ldo], or fp32 slabs [splits][M][ldo] (EPI_SLAB)
   unsigned short* aux;
@@ -159,49 +160,77 @@ INA_DEVICE TilePos tile_coords(int ti, int NT, int MB, int NB, int T) {
 
 extern __shared__ __attribute__((aligned(16))) unsigned char gemm_lds[];
 
+// Two 16-byte-per-lane LDS-DMA pieces (1 KiB each, lane-linear from the wave-uniform LDS byte addresses dst / dst +
+// 1024) by buffer loads: per-lane voffset, uniform soffset, one M0 save / restore for both (cdna_hip_programming.md
+// 5.7: M0 is written in the statement that reads it; s_nop 4 covers an soffset / descriptor fresh from a
+// v_readfirstlane, s_nop 0 the M0 write -> LDS-DMA).  A voffset of 0x80000000 is out of range: the piece reads zeros.
+INA_DEVICE void bdma2(__amdgpu_buffer_rsrc_t rs, uint32_t v0, uint32_t v1, uint32_t soff, uint32_t dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_nop 4\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, %5 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %5 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(v0), "v"(v1), "s"(rs), "s"(dst), "s"(soff)
+      : "memory");
+}
+constexpr uint32_t OOB = 0x80000000u;   // > every descriptor's byte count (operands < 2 GiB: checked on the host)
+
 // One operand's DMA geometry.  KMAJ = false: direct image of rows [R][ld] (K contiguous); true: K-major image.
+// voff[h][j]: the lane's byte offset of piece j of half h relative to the tile origin (tile-invariant); the tile's
+// rows / columns and the K-step go into the uniform soffset.  Rows / columns past the operand (the last tile) and
+// K-major rows past K take the out-of-range offset (a uniform branch decides whether any lane needs the check).
 template <bool KMAJ>
 struct OpStage {
-  const unsigned char* g;
-  const unsigned char* zero;
+  __amdgpu_buffer_rsrc_t rs;
   int ld2;    // row stride in bytes
-  int lim;    // direct: last row (R - 1); K-major: last 16-byte column chunk (C - 8)
-  int K;      // K-major: rows past K read zeros
-  int r[2];   // image row of piece j
-  int c[2];   // direct: source byte offset of the chunk; K-major: logical column offset (elements)
-  INA_DEVICE void init(int w, int lane, const unsigned short* base, const unsigned short* zbuf, int ld, int last, int Kk) {
-    g = reinterpret_cast<const unsigned char*>(base);
-    zero = reinterpret_cast<const unsigned char*>(zbuf);
+  int lim;    // direct: rows R; K-major: columns C
+  int K;
+  uint32_t voff[2][2];
+  INA_DEVICE void init(int w, int lane, const unsigned short* base, int ld, int width, int rows, int Kk) {
     ld2 = ld * 2;
-    lim = last;
+    lim = KMAJ ? width : rows;
     K = Kk;
+    // byte count: through the last row's last element (a column slice of wider rows ends before its row stride)
+    const uint32_t bytes = (uint32_t)((size_t)(rows - 1) * ld2 + (size_t)width * 2);
+    rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(base), (short)0, (int)bytes, 0x00020000);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if constexpr (!KMAJ) {
-        r[j] = 16 * w + 8 * j + (lane >> 3);
-        c[j] = ((lane & 7) ^ ((r[j] >> 1) & 7)) * 16;
-      } else {
-        r[j] = 8 * w + 4 * j + (lane >> 4);
-        c[j] = 8 * ((lane & 15) ^ kswz(r[j]));
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (!KMAJ) {
+          const int r = 16 * w + 8 * j + (lane >> 3);
+          voff[h][j] = (uint32_t)((h * 128 + r) * ld2 + ((lane & 7) ^ ((r >> 1) & 7)) * 16);
+        } else {
+          const int r = 8 * w + 4 * j + (lane >> 4);
+          voff[h][j] = (uint32_t)(r * ld2 + (h * 128 + 8 * ((lane & 15) ^ kswz(r))) * 2);
+        }
       }
-    }
   }
-  // half h (0, 1) of the tile whose rows start at row0, absolute K-step kt -> LDS byte address dst (this wave's
-  // first piece)
+  // half h (0, 1) of the tile whose rows (direct) / columns (K-major) start at row0, absolute K-step kt ->
+  // LDS byte address dst (this wave's first piece)
   INA_DEVICE void stage(uint32_t dst, int row0, int h, int kt) const {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const unsigned char* src;
-      if constexpr (!KMAJ) {
-        const int row = min(row0 + h * 128 + r[j], lim);
-        src = g + (size_t)row * ld2 + kt * (G_BK * 2) + c[j];
-      } else {
-        const int k = kt * G_BK + r[j];
-        const int col = min(row0 + h * 128 + c[j], lim);
-        src = k < K ? g + (size_t)k * ld2 + col * 2 : zero;
+    uint32_t v0 = voff[h][0], v1 = voff[h][1];
+    uint32_t soff;
+    if constexpr (!KMAJ) {
+      soff = (uint32_t)(row0 * ld2 + kt * (G_BK * 2));
+      if (row0 + 256 > lim) {   // ragged last row tile
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        const int r0 = row0 + h * 128 + 16 * w + (lane >> 3);
+        v0 = r0 < lim ? v0 : OOB;
+        v1 = r0 + 8 < lim ? v1 : OOB;
       }
-      glds16_asm(src, dst + j * 1024);
+    } else {
+      soff = (uint32_t)(kt * G_BK * ld2 + row0 * 2);
+      if (row0 + 256 > lim || (kt + 1) * G_BK > K) {   // ragged last column tile / K tail
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        // pieces 0 / 1: image rows r and r + 4 (same swizzle), the same logical column chunk
+        const int r = 8 * w + (lane >> 4), k = kt * G_BK + r;
+        const int c = row0 + h * 128 + 8 * ((lane & 15) ^ kswz(r));
+        v0 = (c < lim && k < K) ? v0 : OOB;
+        v1 = (c < lim && k + 4 < K) ? v1 : OOB;
+      }
     }
+    bdma2(rs, v0, v1, soff, dst);
   }
 };
 
@@ -237,7 +266,7 @@ struct Ops {
   OpRead<TB, 2> rb;
   uint32_t dst0;   // this wave's first DMA piece in a half-tile image (wave-uniform: an SGPR for M0)
   INA_DEVICE void stage(int buf, int H, const TilePos& p) const {
-    const uint32_t dst = dst0 + buf * G_BUF + H * G_HALF;
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(dst0 + buf * G_BUF + H * G_HALF);
     if (H < 2) sa.stage(dst, p.m, H, p.k);
     else sb.stage(dst, p.n, H - 2, p.k);
   }
@@ -452,8 +481,8 @@ __global__ __launch_bounds__(G_THREADS, 1) void gemm_bf16_kernel(GemmArgs g) {
 
   Ops<LAYOUT> op;
   constexpr bool TA = LAYOUT == L_TN, TB = LAYOUT != L_NT;
-  op.sa.init(w, lane, g.A, g.zero, g.lda, TA ? g.M - 8 : g.M - 1, g.K);
-  op.sb.init(w, lane, g.B, g.zero, g.ldb, TB ? g.N - 8 : g.N - 1, g.K);
+  op.sa.init(w, lane, g.A, g.lda, TA ? g.M : g.K, TA ? g.K : g.M, g.K);
+  op.sb.init(w, lane, g.B, g.ldb, TB ? g.N : g.K, TB ? g.K : g.N, g.K);
   op.ra.init(4 * wr, lane);
   op.rb.init(2 * wc, lane);
   op.dst0 = __builtin_amdgcn_readfirstlane(lds_addr(gemm_lds) + 2 * w * 1024);
@@ -583,7 +612,10 @@ int gemm_bf16(int layout, const void* A, int lda, const void* B, int ldb, int M,
   const bool ta = layout == L_TN, tb = layout != L_NT;
   // direct operands: K a multiple of 64 (whole K-steps); K-major operands: 16-byte column chunks, rows past K zero
   if ((!ta || !tb) && K % G_BK != 0) return 1;
-  if ((ta || tb) && zero == nullptr) return 1;
+  (void)zero;
+  // buffer descriptors: each operand's bytes < 2 GiB (the out-of-range offset 0x80000000 must exceed them)
+  if ((ta ? (long)(K - 1) * lda + M : (long)(M - 1) * lda + K) * 2 >= (1L << 31)) return 1;
+  if ((tb ? (long)(K - 1) * ldb + N : (long)(N - 1) * ldb + K) * 2 >= (1L << 31)) return 1;
   if (ta && M % 8 != 0) return 1;
   if (N % 8 != 0) return 1;
   if (lda % 8 != 0 || ldb % 8 != 0 || ldo % (epi == EPI_SLAB ? 4 : 8) != 0 || ldo < N) return 1;
@@ -598,7 +630,7 @@ int gemm_bf16(int layout, const void* A, int lda, const void* B, int ldb, int M,
   const int ks = (K + G_BK - 1) / G_BK;
   const int T = (ks + splits - 1) / splits;
   if ((long)(splits - 1) * T >= ks) return 1;   // every split has >= 1 K-step
-  GemmArgs a{(const unsigned short*)A, (const unsigned short*)B, (const unsigned short*)zero, bias, out,
+  GemmArgs a{(const unsigned short*)A, (const unsigned short*)B, bias, out,
              (unsigned short*)aux, slab, M, N, K, lda, ldb, ldo, ldx, T, splits};
   if (layout == L_TN) return epi == EPI_SLAB ? launch_gemm<L_TN, EPI_SLAB>(a, st) : 1;
   if (layout == L_NN) return dispatch<L_NN>(a, epi, st);
