@@ -47,7 +47,9 @@ def main(argv=None):
         base = Config.from_dict(meta.get("config", {}))
     cfg = config_from_args(args, base).replace(resume=False, episodes_per_step=max(1, base.episodes_per_step))
     tr_data, va_data = T.load_data(cfg, args)
-    te = T.load_test(cfg, tr_data) if cfg.test_file else va_data
+    # --test_file (another domain) > the task's held-out test relations (synthetic transfer, --fold with
+    # --val_relations) > the validation data
+    te = T.load_test(cfg, tr_data) if cfg.test_file else (getattr(args, "_test_split", None) or va_data)
     trainer = Trainer(cfg, tr_data, va_data, device=cfg.device, log=False)
     if stem is not None:
         trainer.load(stem, args.checkpoint_format)
@@ -62,8 +64,8 @@ def main(argv=None):
             rep = evaluate_dataset(trainer, te, args.iters, N, K, cfg.eQ, r, thr if r > 0 else None,
                                    cfg.eval_batch or None, tune_on=va_data)
             if trainer.dist.is_main:
-                print(json.dumps(dict(rep.to_dict(), data=os.path.basename(cfg.test_file or cfg.val_file),
-                                      step=trainer.global_step)))
+                print(json.dumps(dict(rep.to_dict(), data=os.path.basename(cfg.test_file) if cfg.test_file
+                                      else te.name, head=cfg.relation_head, step=trainer.global_step)))
     trainer.dist.destroy()
 
 

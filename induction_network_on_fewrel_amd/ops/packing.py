@@ -339,7 +339,7 @@ def wide_x_cols(D: int) -> int:
     """Row width of the wide path's encoder input Xb: the D = E + 2PD embedding columns, a ones column
     (index D: the x-projection GEMM's bias row, so dW_x's GEMM yields the bias gradient as row D) and
     zero padding to a multiple of 32 (64-byte rows; a K multiple of 32 moves hipBLASLt's x-projection
-    GEMM off its edge-tile kernels: 1.60 -> 1.16 ms at the paper configuration, tools/gemm_probe.py)."""
+    GEMM off its edge-tile kernels: 1.60 -> 1.16 ms at the paper configuration, a round-5 probe, profiles/r5_merged)."""
     return (D + 1 + 31) // 32 * 32
 
 

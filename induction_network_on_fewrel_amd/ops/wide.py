@@ -179,7 +179,7 @@ class WideSeqBiLSTM(torch.autograd.Function):
         DP = (D + 1 + 31) // 32 * 32
         # training: each x row is followed by the two directions' h_{t-1} stash columns (written by the forward
         # kernel), so ONE split-K GEMM over [x | h_fw | h_bw] rows gives dW_x, db and both dW_h reading dG once
-        # (1,385 vs 1,506 us for the three GEMMs at the paper configuration, tools/gemm_probe.py)
+        # (1,385 vs 1,506 us for the three GEMMs at the paper configuration, a round-5 probe, profiles/r5_merged)
         Xw = o.wide_x_gather(inst, word, pos1, pos2, wtab, p1emb.detach().float().contiguous(),
                              p2emb.detach().float().contiguous(), 2 * UP if need else 0)
         Xb = Xw[:, :DP]
@@ -431,7 +431,7 @@ def _splitk_nt(a: torch.Tensor, b: torch.Tensor, ns: int) -> torch.Tensor:
     """a b^T in fp32 for a [M, K], b [N, K] with a long K and a small output: K split into ns chunks as ONE
     strided batched GEMM + an ordered sum (deterministic).  The head's dcls = dP M'^T (K = h H = 25,600, a
     [1280, 256] output at the paper configuration) ran as one GEMM on ~44 workgroups: 104 -> 32 us with
-    ns = 8 (tools/dm_wide_probe.py)."""
+    ns = 8 (a round-5 probe, profiles/r5_dcls)."""
     M, K = a.shape
     N = b.shape[0]
     if ns <= 1 or K % ns or not (a.is_cuda and a.is_contiguous() and b.is_contiguous()):
@@ -477,11 +477,11 @@ def _wide_head_backward(ctx, saved, dz, g):
     dPf = dP.view(E * N, h * H)
     dcls = _splitk_nt(dPf, Mt, 8)                                              # [E*N, H]
     dMt = torch.mm(cls_bf.t(), dPf, out_dtype=torch.float32)                   # [H, h*H] fp32 (one GEMM: 30 us
-    # vs 69 us split 4 + sum at the paper configuration, tools/dm_wide_probe.py)
+    # vs 69 us split 4 + sum at the paper configuration, profiles/r5_dm1 / r5_dws)
     dM = o.transpose12(dMt.view(H, h, H), False)                                 # [a][b][s] fp32
     deh = o.routing_wide_bwd(eh, dcls, E * N, K, R)                            # [E*NK, H]
     ns = 4 if sup.is_cuda and sup.shape[0] % 4 == 0 and sup.shape[0] >= 4096 else 1
-    # (fp32 split-K 4 + ordered sum: 26 vs 44 us for one GEMM at the paper configuration, tools/dm_wide_probe.py)
+    # (fp32 split-K 4 + ordered sum: 26 vs 44 us for one GEMM at the paper configuration, profiles/r5_dm1 / r5_dws)
     dWs = (torch.bmm(sup.view(ns, -1, H).transpose(1, 2), deh.view(ns, -1, H)).sum(0) if ns > 1
            else torch.mm(sup.t(), deh))
     dsup = torch.mm(deh, Ws.t())

@@ -28,18 +28,46 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def _meanpool_accuracy(ds, W, K, episodes, seed, N=5, Q=5):
-    """Mean of the frozen word vectors over the valid tokens -> nearest class prototype (cosine)."""
+def _meanpool_scores(ds, W, K, episodes, seed, N=5, Q=5, nota_rate=0.0):
+    """Mean of the frozen word vectors over the valid tokens -> cosine similarity of each query to each class
+    prototype (mean of its K support vectors).  -> (scores [B, N Q, N], labels [B, N Q]; label N = NOTA)."""
     from induction_network_on_fewrel_amd.data import EpisodeSampler
     valid = (ds.data_mask > 0).astype(np.float32)
     vec = (W[ds.data_word] * valid[..., None]).sum(1) / np.maximum(valid.sum(1, keepdims=True), 1.0)
     vec /= np.maximum(np.linalg.norm(vec, axis=1, keepdims=True), 1e-12)
-    s = EpisodeSampler(ds, seed=seed)
+    s = EpisodeSampler(ds, seed=seed, nota_rate=nota_rate)
     idx, labels = s.next_batch_indices(episodes, N, K, Q)
     sup = vec[idx[:, : N * K]].reshape(episodes, N, K, -1).mean(2)
     sup /= np.maximum(np.linalg.norm(sup, axis=-1, keepdims=True), 1e-12)
-    pred = np.einsum("bqd,bnd->bqn", vec[idx[:, N * K:]], sup).argmax(-1)
-    return float((pred == labels).mean())
+    return np.einsum("bqd,bnd->bqn", vec[idx[:, N * K:]], sup), labels
+
+
+def _predict(scores, thr, N):
+    pred = scores.argmax(-1)
+    return pred if thr is None else np.where(scores.max(-1) < thr, N, pred)
+
+
+def _meanpool_accuracy(ds, W, K, episodes, seed, N=5, Q=5):
+    """Nearest class prototype (cosine) accuracy."""
+    scores, labels = _meanpool_scores(ds, W, K, episodes, seed, N, Q)
+    return float((scores.argmax(-1) == labels).mean())
+
+
+def _meanpool_nota(tune, test, W, K, episodes, seed, rate, N=5, Q=5):
+    """FewRel 2.0 NOTA rule for the control, as runtime/evaluate.py does for the model: a query whose best score is
+    below a threshold is NOTA; the threshold maximises accuracy on ``tune`` episodes (the validation relations)."""
+    ts, tl = _meanpool_scores(tune, W, K, 500, seed + 1, N, Q, rate)
+    grid = np.linspace(-1.0, 1.0, 201)
+    accs = [float((_predict(ts, t, N) == tl).mean()) for t in grid]
+    thr = float(grid[int(np.argmax(accs))])
+    sc, lab = _meanpool_scores(test, W, K, episodes, seed, N, Q, rate)
+    pred = _predict(sc, thr, N)
+    nota, pn = lab == N, pred == N
+    return dict(threshold=round(thr, 3), accuracy=round(float((pred == lab).mean()), 4),
+                in_class_accuracy=round(float((pred == lab)[~nota].mean()), 4),
+                nota_precision=round(float((pn & nota).sum()) / max(1, int(pn.sum())), 4),
+                nota_recall=round(float((pn & nota).sum()) / max(1, int(nota.sum())), 4),
+                nota_fraction=round(float(nota.mean()), 4))
 
 
 def main():
@@ -59,6 +87,10 @@ def main():
     ap.add_argument("--instances", type=int, default=300, help="transfer: instances per relation")
     ap.add_argument("--vocab", type=int, default=20000, help="transfer: --synthetic_vocab")
     ap.add_argument("--seed", type=int, default=None, help="transfer: --seed (default Config.seed)")
+    ap.add_argument("--nota_rates", default="", help="transfer: also the FewRel 2.0 NOTA rule at these rates "
+                    "(threshold tuned on the validation relations), e.g. 0,0.15,0.5")
+    ap.add_argument("--test_file", default="", help="transfer: also a domain-shifted FewRel JSON (e.g. "
+                    "data/synthetic.py --shifted_test) tensorised with the task's vocabulary")
     args = ap.parse_args()
     cfg = Config()
     rows = []
@@ -68,7 +100,20 @@ def main():
         for dim in (int(x) for x in args.dims.split(",")):
             _, va, te = make_transfer_splits(args.relations, cfg.synthetic_val_relations, cfg.synthetic_test_relations,
                                              args.instances, cfg.max_length, args.vocab, dim, seed=seed)
-            for split in (va, te):
+            splits = [va, te]
+            if args.test_file:
+                splits.append(FewRelDataset.from_fewrel_json_with_vocab(args.test_file, te.word2id, te.word_vec_mat,
+                                                                        cfg.max_length))
+            if args.nota_rates:
+                for split in splits[1:]:
+                    for K in (int(x) for x in args.shots.split(",")):
+                        for rate in (float(x) for x in args.nota_rates.split(",")):
+                            r = dict(control="meanpool-nearest-prototype", task="transfer", split=split.name, dim=dim,
+                                     N=5, K=K, nota_rate=rate, episodes=args.episodes,
+                                     **_meanpool_nota(va, split, split.word_vec_mat, K, args.episodes, cfg.seed, rate))
+                            rows.append(r)
+                            print(json.dumps(r), flush=True)
+            for split in splits:
                 for K in (int(x) for x in args.shots.split(",")):
                     acc = _meanpool_accuracy(split, split.word_vec_mat, K, args.episodes, cfg.seed)
                     r = dict(control="meanpool-nearest-prototype", task="transfer", split=split.name, dim=dim, N=5,
