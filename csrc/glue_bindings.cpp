@@ -86,10 +86,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> ragged_sort(const Tensor& inst, const
 }
 
 // probs [rows, N] fp32, labels int32 [rows]; writes dz [rows, N] and out [N + 3] =
-// (loss, accuracy, db[0..N), db_total); part: workspace [blocks * 18].  ce: softmax cross-entropy
-// over the pre-sigmoid scores instead of the reference MSE
+// (loss, accuracy, db[0..N), db_total); part: workspace [blocks * 18].  ce: 0 the reference MSE, 1 softmax
+// cross-entropy over the pre-sigmoid scores, 2 the NOTA-aware cross-entropy (an extra class of logit 0)
 void head_loss(const Tensor& probs, const Tensor& labels, double scale, Tensor dz, Tensor out, Tensor part,
-               int64_t blocks, bool ce) {
+               int64_t blocks, int64_t ce) {
   const char* op = "ina.head_loss";
   need(probs, op, "probs", at::kFloat);
   need(labels, op, "labels", at::kInt);
@@ -100,8 +100,9 @@ void head_loss(const Tensor& probs, const Tensor& labels, double scale, Tensor d
   TORCH_CHECK(N >= 1 && N <= 16, op, ": N must be in [1, 16]");
   TORCH_CHECK(labels.numel() == rows && dz.numel() == probs.numel() && out.numel() >= N + 3, op, ": shapes");
   TORCH_CHECK(blocks >= 1 && part.numel() >= blocks * ina::head_loss_part_floats(), op, ": workspace too small");
+  TORCH_CHECK(ce >= 0 && ce <= 2, op, ": ce must be 0 (mse), 1 (ce) or 2 (ce_nota)");
   TORCH_CHECK(ina::head_loss(probs.data_ptr<float>(), labels.data_ptr<int>(), (long)rows, (int)N, (float)scale,
-                             ce ? 1 : 0, dz.data_ptr<float>(), out.data_ptr<float>(), part.data_ptr<float>(), (int)blocks,
+                             (int)ce, dz.data_ptr<float>(), out.data_ptr<float>(), part.data_ptr<float>(), (int)blocks,
                              stream()) == 0,
               op, ": launch failed");
 }

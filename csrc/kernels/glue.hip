@@ -48,6 +48,10 @@ constexpr float CE_P_MIN = 1e-30f;     // models/reference.py::CE_P_MIN (z >= -6
 // rows = E * NQ; probs/dz [rows][N]; labels int32 [rows] (N = NOTA).
 // ce = 0: MSE on the sigmoid scores vs one-hot (reference).  ce = 1: softmax cross-entropy over the
 // pre-sigmoid scores z = log p - log(1 - p) (models/reference.py::ce_loss); NOTA rows contribute 0.
+// ce = 2: NOTA-aware cross-entropy (FewRel 2.0 training with none-of-the-above queries,
+// models/reference.py::ce_nota_loss): the softmax runs over the N scores plus a NOTA class whose logit is
+// fixed at 0 (the score 0.5); a NOTA row's target is that class, so it pushes every z_c below 0.  The
+// accuracy counts a row as NOTA when its best score is below 0.5.
 // NT: compile-time class count (0 = runtime N <= HL_NMAX): the 5-way instantiation loads each row's
 // scores unconditionally and reduces 5 bias-gradient columns instead of 16
 template <int NT>
@@ -76,22 +80,23 @@ __global__ __launch_bounds__(256) void head_loss_kernel(const float* __restrict_
         arg = c;
       }
     }
-    cor += (arg == lab) ? 1.f : 0.f;
+    const bool nota = ce == 2;
+    cor += ((nota && best < 0.5f ? N : arg) == lab) ? 1.f : 0.f;
     if (ce) {
-      float z[HL_NMAX], zm = -INFINITY, zl = 0.f;
+      float z[HL_NMAX], zm = nota ? 0.f : -INFINITY, zl = 0.f;   // nota: the fixed NOTA logit 0 (zl if lab == N)
 #pragma unroll
       for (int c = 0; c < HL_NMAX; ++c) {
         z[c] = c < N ? logf(fmaxf(pv[c], CE_P_MIN)) - logf(fmaxf(1.f - pv[c], CE_ODDS_EPS)) : -INFINITY;
         zm = fmaxf(zm, z[c]);
         if (c == lab) zl = z[c];
       }
-      float s = 0.f;
+      float s = nota ? expf(-zm) : 0.f;
 #pragma unroll
       for (int c = 0; c < HL_NMAX; ++c) {
         z[c] = c < N ? expf(z[c] - zm) : 0.f;
         s += z[c];
       }
-      const bool has = lab < N;
+      const bool has = lab < N || nota;
       const float inv = 1.f / s;
 #pragma unroll
       for (int c = 0; c < HL_NMAX; ++c) {

@@ -94,7 +94,9 @@ class Config:
     l2_lambda: float = 1e-5
     use_l2: bool = False               # reference computes then discards it (graph.py:108-109)
     loss_reduction: str = "mean"       # "mean" (reference) | "sum" (paper Eq.12)
-    loss_type: str = "mse"             # "mse" on sigmoid scores (reference) | "ce": softmax over the N scores
+    loss_type: str = "mse"             # "mse" on sigmoid scores (reference) | "ce": softmax over the N scores |
+                                       # "ce_nota": softmax over the N scores + a NOTA class of logit 0 (train
+                                       # with nota_rate > 0: FewRel 2.0)
 
     # ---------------- loop cadence (model/base.py:115-116) ----------------
     train_iter: int = 30000
@@ -174,7 +176,7 @@ class Config:
             raise ValueError(f"unknown relation_head {self.relation_head}")
         if self.dtype not in ("bf16", "fp32"):
             raise ValueError(f"unknown dtype {self.dtype}")
-        if self.loss_type not in ("mse", "ce"):
+        if self.loss_type not in ("mse", "ce", "ce_nota"):
             raise ValueError(f"unknown loss_type {self.loss_type}")
         if self.optimizer not in ("adam", "adagrad"):
             raise ValueError(f"unknown optimizer {self.optimizer}")

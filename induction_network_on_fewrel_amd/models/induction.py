@@ -194,8 +194,8 @@ class InductionNetwork(nn.Module):
             probs, _ = self.forward(inst, data, B, N, K, Q, training=True, dropout_seed=dropout_seed,
                                     grad_views=grad_views, overlap=overlap, seed_dev=seed_dev, glue=glue)
             loss = self.loss(probs, labels)
-            with torch.no_grad():
-                acc = ref.accuracy(probs.detach(), labels.long())
+            with torch.no_grad():   # ce_nota: a query is predicted NOTA below the score 0.5 (its loss's NOTA class)
+                acc = ref.accuracy(probs.detach(), labels.long(), 0.5 if cfg.loss_type == "ce_nota" else None)
             return loss, acc, probs
         from ..ops.encoder import encode
         from ..ops.glue import lstm_din
@@ -213,9 +213,7 @@ class InductionNetwork(nn.Module):
 
     # ------------------------------------------------------------------
     def loss(self, probs: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-        if self.cfg.loss_type == "ce":
-            return ref.ce_loss(probs, labels.long(), self.cfg.loss_reduction)
-        return ref.mse_loss(probs, labels.long(), self.cfg.loss_reduction)
+        return ref.loss_fn(self.cfg.loss_type)(probs, labels.long(), self.cfg.loss_reduction)
 
     def l2_value(self) -> torch.Tensor:
         return sum((v.detach() ** 2).sum() / 2 for v in self.params.l2_vars()) * self.cfg.l2_lambda

@@ -218,6 +218,25 @@ def ce_loss(probs: torch.Tensor, labels: torch.Tensor, reduction: str = "mean") 
     return nll.sum() / max(1, probs.shape[0])
 
 
+def ce_nota_loss(probs: torch.Tensor, labels: torch.Tensor, reduction: str = "mean") -> torch.Tensor:
+    """NOTA-aware softmax cross-entropy (``loss_type='ce_nota'``, FewRel 2.0 training with none-of-the-above
+    queries; no reference counterpart): the softmax runs over the N relation logits plus a NOTA class whose logit
+    is fixed at 0 (relation score 0.5), and a NOTA query (label == N) targets that class.  ``mean`` over all
+    queries; ``sum`` divided by the episode count."""
+    N = probs.shape[-1]
+    z = relation_logits(probs).reshape(-1, N)
+    z = torch.cat([z, torch.zeros_like(z[:, :1])], 1)
+    nll = torch.nn.functional.cross_entropy(z, labels.reshape(-1).long(), reduction="sum")
+    return nll / max(1, int(labels.numel())) if reduction == "mean" else nll / max(1, probs.shape[0])
+
+
+LOSS_MODES = {"mse": 0, "ce": 1, "ce_nota": 2}   # the fused loss kernel's mode (glue.hip head_loss)
+
+
+def loss_fn(loss_type: str):
+    return {"mse": mse_loss, "ce": ce_loss, "ce_nota": ce_nota_loss}[loss_type]
+
+
 def predict(probs: torch.Tensor, nota_threshold: Optional[float] = None) -> torch.Tensor:
     pred = probs.argmax(-1)
     if nota_threshold is not None:

@@ -90,14 +90,16 @@ class HeadLossFn(torch.autograd.Function):
         tiles = pk["ntn_tiles"]
         probs = o.ntn_fwd(cls, e, tiles, b.detach().float().contiguous(), E, N, K, Q, h, paper, 0)
         rows = E * N * Q
-        ce = meta.get("loss_type", "mse") == "ce"
+        lt = meta.get("loss_type", "mse")
+        ce = lt != "mse"   # scale: mean over the queries (ce, ce_nota) or over queries x classes (mse)
+        mode = {"mse": 0, "ce": 1, "ce_nota": 2}[lt]
         if meta.get("reduction", "mean") == "mean":
             scale = 1.0 / rows if ce else 1.0 / (rows * N)
         else:
             scale = 1.0 / max(1, E)
         dz = torch.empty_like(probs)
         out = torch.empty(N + 3, dtype=torch.float32, device=e.device)
-        o.head_loss(probs, labels.reshape(-1), scale, dz, out, glue.loss_part, _loss_blocks(glue, rows), ce)
+        o.head_loss(probs, labels.reshape(-1), scale, dz, out, glue.loss_part, _loss_blocks(glue, rows), mode)
         ctx.save_for_backward(e, Wsd, cls, tiles, dz, out)
         ctx.meta = dict(meta, H=H, h=h)
         ctx.set_materialize_grads(False)   # no zero-fill launches for the non-differentiable outputs

@@ -532,13 +532,14 @@ class HeadWideLossFn(torch.autograd.Function):
         E, N, K, Q, R, paper = cfg
         probs, saved = _wide_head_forward(e, Ws, M, w, b, E, N, K, Q, R, paper)
         rows = E * N * Q
-        ce = loss_type == "ce"
+        ce = loss_type != "mse"
+        mode = {"mse": 0, "ce": 1, "ce_nota": 2}[loss_type]
         scale = (1.0 / rows if ce else 1.0 / (rows * N)) if reduction == "mean" else 1.0 / max(1, E)
         dz = torch.empty(rows, N, dtype=torch.float32, device=e.device)
         out = torch.empty(N + 3, dtype=torch.float32, device=e.device)
         blocks = max(1, min(HeadWideLossFn.LOSS_BLOCKS, (rows + 255) // 256))
         part = torch.empty(blocks * 18, dtype=torch.float32, device=e.device)
-        o.head_loss(probs.view(rows, N), labels.reshape(-1).int().contiguous(), scale, dz, out, part, blocks, ce)
+        o.head_loss(probs.view(rows, N), labels.reshape(-1).int().contiguous(), scale, dz, out, part, blocks, mode)
         ctx.save_for_backward(*saved, Ws.detach().float())
         ctx.dz = dz
         ctx.cfg = cfg

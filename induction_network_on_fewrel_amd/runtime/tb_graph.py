@@ -123,7 +123,7 @@ def model_graph(model, N: int, K: int, Q: int) -> bytes:
                       k("ntn_fwd / ntn_bwd (ntn.hip)")))
     nodes.append(node("RelationModule/fc", "MatMul", ["RelationModule/ntn", var["ntn_w"]], k("ntn.hip epilogue")))
     nodes.append(node("RelationModule/probs", "Sigmoid", ["RelationModule/fc", var["ntn_b"]], k("ntn.hip epilogue")))
-    loss_op = "SoftmaxCrossEntropy" if cfg.loss_type == "ce" else "MeanSquaredError"
+    loss_op = "SoftmaxCrossEntropy" if cfg.loss_type != "mse" else "MeanSquaredError"
     nodes.append(node("loss/loss", loss_op, ["RelationModule/probs", "query_label"], k("head_loss (glue.hip)")))
     nodes.append(node("predictions", "ArgMax", ["RelationModule/probs"]))
     nodes.append(node("accuracy", "Mean", ["predictions", "query_label"]))

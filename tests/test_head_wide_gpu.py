@@ -81,15 +81,18 @@ def test_routing_wide_kernels_fp32_exact(H, K, R):
     assert _relerr(deh, x.grad.view(items * K, H)) < 1e-4
 
 
-@pytest.mark.parametrize("loss_type", ["mse", "ce"])
+@pytest.mark.parametrize("loss_type", ["mse", "ce", "ce_nota"])
 @pytest.mark.parametrize("head", ["reference", "paper"])
 def test_wide_head_loss_node(loss_type, head):
-    """HeadWideLossFn (head + ina.head_loss) == oracle head + loss: value, accuracy and gradients."""
+    """HeadWideLossFn (head + ina.head_loss) == oracle head + loss: value, accuracy and gradients (ce_nota: a
+    quarter of the queries are NOTA, label N)."""
     E, N, K, Q, H, h, R = 8, 5, 5, 20, 256, 100, 3
     gen = torch.Generator().manual_seed(7)
     p = _params(H, N, h, head, gen)
     e = (torch.randn(E * (N * K + N * Q), H, generator=gen) * 0.3).to(DEV).requires_grad_(True)
     labels = torch.arange(N, device=DEV).repeat_interleave(Q).repeat(E).view(E, N * Q).int()
+    if loss_type == "ce_nota":
+        labels[:, ::4] = N
     loss, acc, probs = HeadWideLossFn.apply(e, p["W_s"], p["M"], p["ntn_w"], p["ntn_b"], labels,
                                             (E, N, K, Q, R, head == "paper"), loss_type, "mean")
     (loss * 3.0).backward()
@@ -98,11 +101,11 @@ def test_wide_head_loss_node(loss_type, head):
     for v in list(p.values()) + [e]:
         v.grad = None
     pr = ref.head_forward(p, e, E, N, K, Q, R, head, bf16=True)
-    lf = ref.ce_loss if loss_type == "ce" else ref.mse_loss
-    lr = lf(pr, labels.long())
+    lr = ref.loss_fn(loss_type)(pr, labels.long())
     (lr * 3.0).backward()
     assert abs(float(loss) - float(lr)) <= 2e-2 * abs(float(lr)) + 1e-6
-    assert abs(float(acc) - float(ref.accuracy(probs, labels.long()))) < 1e-6
+    thr = 0.5 if loss_type == "ce_nota" else None   # ce_nota: NOTA predicted below the score 0.5
+    assert abs(float(acc) - float(ref.accuracy(probs, labels.long(), thr))) < 1e-6
     assert _nrel(ge, e.grad) < 2e-2
     for k in p:   # paper head + CE: the shared bias cancels in the softmax (its exact gradient is 0)
         assert _nrel(got[k], p[k].grad) < 2e-2 or float((got[k] - p[k].grad).abs().max()) < 1e-5, k

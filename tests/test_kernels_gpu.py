@@ -649,17 +649,20 @@ def test_hip_graph_step_matches_eager(tmp_path):
     assert _relerr(p1, p0) < 1e-4
 
 
-@pytest.mark.parametrize("head,loss", [("reference", "mse"), ("paper", "mse"), ("paper", "ce"), ("reference", "ce")])
+@pytest.mark.parametrize("head,loss", [("reference", "mse"), ("paper", "mse"), ("paper", "ce"), ("reference", "ce"),
+                                       ("paper", "ce_nota"), ("reference", "ce_nota")])
 def test_step_glue_matches_unfused(tmp_path, head, loss):
     """ops/glue.py: the low-launch step (one pack gather, fused loss node, one slab scatter-add)
     produces the same losses, accuracies and parameter trajectory as the per-op path (whose loss
-    is the autograd oracle: ref.mse_loss / ref.ce_loss)."""
+    is the autograd oracle: ref.mse_loss / ref.ce_loss / ref.ce_nota_loss; ce_nota trains on episodes with 30%
+    none-of-the-above queries)."""
     from induction_network_on_fewrel_amd.runtime.trainer import Trainer
     data = make_synthetic(num_relations=12, instances_per_relation=40, vocab=500, seed=0)
     runs = []
     for glue in (False, True):
         cfg = Config(N=5, K=3, Q=4, episodes_per_step=24, model_dir=str(tmp_path / f"s{int(glue)}{head}"), seed=6,
-                     resume=False, step_glue=glue, relation_head=head, learning_rate=1e-3, loss_type=loss)
+                     resume=False, step_glue=glue, relation_head=head, learning_rate=1e-3, loss_type=loss,
+                     nota_rate=0.3 if loss == "ce_nota" else 0.0)
         tr = Trainer(cfg, data, None, device="cuda", log=False)
         assert (tr.glue is not None) == glue
         hist = [tr.train_step() for _ in range(4)]

@@ -112,6 +112,25 @@ def test_ce_loss_on_presigmoid_scores_and_nota():
     cfg.validate()
 
 
+def test_ce_nota_loss_extra_class_of_logit_zero():
+    """loss_type='ce_nota': softmax over the N pre-sigmoid scores + a NOTA class of logit 0; NOTA rows (label N)
+    target that class, in-class rows their class; mean over all query rows.  The gradient of a NOTA row pushes
+    every relation logit down."""
+    z = torch.randn(2, 6, 3, dtype=torch.float64, requires_grad=True)
+    labels = torch.tensor([[0, 1, 2, 0, 1, 3], [2, 2, 1, 0, 3, 3]])
+    loss = ref.ce_nota_loss(torch.sigmoid(z), labels)
+    zz = torch.cat([z.detach(), torch.zeros(2, 6, 1, dtype=torch.float64)], -1)
+    want = torch.nn.functional.cross_entropy(zz.view(-1, 4), labels.view(-1), reduction="sum") / labels.numel()
+    assert torch.allclose(loss, want)
+    loss.backward()
+    sm = torch.softmax(zz, -1)[..., :3]
+    g = (sm - torch.nn.functional.one_hot(labels, 4)[..., :3]) / labels.numel()
+    assert torch.allclose(z.grad, g, atol=1e-7)
+    assert bool((z.grad[labels == 3] > 0).all())   # NOTA rows: d loss / d z_c > 0 -> every logit pushed down
+    assert ref.LOSS_MODES["ce_nota"] == 2 and ref.loss_fn("ce_nota") is ref.ce_nota_loss
+    Config(loss_type="ce_nota").validate()
+
+
 def test_param_names_shapes_and_init():
     cfg = Config(N=5, K=2, Q=5, hidden_size=20, max_length=37)
     wv = np.random.randn(1002, 5).astype(np.float32)

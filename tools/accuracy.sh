@@ -14,8 +14,10 @@
 # MODE transfer_sweep                      same with 64 training relations (FewRel's train split), SEEDS (default
 #      "1 2 3"), LOSSES / SCHEDS arms.
 # MODE nota [HEADS] [KS]                   FewRel 2.0 NOTA + domain adaptation (BASELINE.json config 5): transfer-task
-#      models (as MODE transfer) evaluated by fewrel_eval.py at NOTA rates NOTA_RATES (default 0,0.15,0.5; threshold
-#      tuned on the validation relations) on (a) the held-out test relations and (b) a domain-shifted test set
+#      models trained WITH none-of-the-above queries (NOTA_TRAIN, default 0.3, loss ce_nota: softmax over the N
+#      scores + a NOTA class of logit 0; NOTA_TRAIN=0 trains as MODE transfer), evaluated by fewrel_eval.py at NOTA
+#      rates NOTA_RATES (default 0,0.15,0.5; threshold tuned on the validation relations) on (a) the held-out test
+#      relations and (b) a domain-shifted test set
 #      (data/synthetic.py --shifted_test: new relations, wider entity gaps, more distractors, shifted filler words)
 #      read through --test_file; the control under the same NOTA rule on both.
 # Runs PAR (default 4) trainings at once on the one GPU (small, launch-bound models).  Checkpoints go to /tmp.
@@ -82,10 +84,14 @@ folds3)
   parallel "$OUT/cmds.txt"; summary ;;
 transfer|nota)
   HEADS=${1:-"reference paper"}; KS=${2:-"1 5"}
+  LOSS="--loss_type ce"
+  if [ "$MODE" = nota ] && [ "${NOTA_TRAIN:-0.3}" != 0 ]; then
+    LOSS="--loss_type ce_nota --nota_rate ${NOTA_TRAIN:-0.3} --nota_threshold 0.5"   # val: NOTA below score 0.5
+  fi
   : > "$OUT/cmds.txt"
   for h in $HEADS; do for k in $KS; do
     name=transfer_${h}_5w${k}s
-    echo "timeout -k 10 1000 python -u train.py induction 5 $k $TRANSFER --train_iter ${STEPS:-3000} --lr_schedule constant --loss_type ce --relation_head $h --model_dir /tmp/acc_$name > $OUT/$name.log 2>&1" >> "$OUT/cmds.txt"
+    echo "timeout -k 10 1000 python -u train.py induction 5 $k $TRANSFER --train_iter ${STEPS:-3000} --lr_schedule constant $LOSS --relation_head $h --model_dir /tmp/acc_$name > $OUT/$name.log 2>&1" >> "$OUT/cmds.txt"
   done; done
   parallel "$OUT/cmds.txt"; summary
   if [ "$MODE" = nota ]; then
@@ -97,7 +103,7 @@ transfer|nota)
       name=transfer_${h}_5w${k}s
       for tf in "" "--test_file $SHIFT"; do
         timeout -k 10 600 python -u fewrel_eval.py induction 5 $k $TRANSFER --relation_head $h --model_dir /tmp/acc_$name \
-          --settings 5-$k --nota_rates $RATES --iters 3000 $tf 2> $OUT/eval_${name}.err | grep '^{' >> "$OUT/eval.jsonl" || exit 1
+          --settings 5-$k --nota_rates $RATES --nota_threshold -1 --iters 3000 $tf 2> $OUT/eval_${name}.err | grep '^{' >> "$OUT/eval.jsonl" || exit 1
       done
     done; done
     timeout -k 10 900 python tools/control_baseline.py --task transfer --dims 50 --episodes 3000 --shots ${KS// /,} \
