@@ -163,7 +163,7 @@ def test_bert_encoder_end_to_end(own_gemm, monkeypatch):
 
 
 def test_split_k_weight_grad_accumulated_into_flat_span():
-    """_Linear's trainer path: the 16 split-K partials of dW = dy^T x are summed by ina.slab_reduce
+    """_Linear's trainer path: the split-K partials of dW = dy^T x are summed by ina.slab_reduce
     straight into the (pre-filled) flat-gradient span, float4 path and scalar tail path."""
     from induction_network_on_fewrel_amd.ops import ops
     from induction_network_on_fewrel_amd.ops.bert import _wgrad_parts
@@ -175,12 +175,89 @@ def test_split_k_weight_grad_accumulated_into_flat_span():
         g = torch.randn(o, i, device=dev)
         want = g + dy.float().t() @ x.float()
         part = _wgrad_parts(dy, x)
-        assert part is not None and part.shape == (16, o, i)
+        assert part is not None and part.shape[1:] == (o, i)   # own TN slabs (o, i % 8 == 0) or 16 bmm chunks
         ops().slab_reduce(part, g, True)
         torch.testing.assert_close(g, want, rtol=1e-4, atol=1e-3)
         out = torch.empty(o, i, device=dev)
         ops().slab_reduce(part, out, False)
         torch.testing.assert_close(out, part.sum(0), rtol=1e-5, atol=1e-4)
+
+
+# BERT-base width, element-wise criteria as tests/test_scale_gpu.py (bf16 operands vs the fp32 oracle)
+BB_MAXREL, BB_RTOL, BB_ATOL_FRAC, BB_MIN_FRAC = 4e-2, 5e-2, 1e-2, 0.999
+
+
+def _bb_stats(g, r):
+    g, r = g.double().flatten(), r.double().flatten()
+    scale = float(r.abs().max()) + 1e-30
+    ok = (g - r).abs() <= BB_ATOL_FRAC * scale + BB_RTOL * r.abs()
+    return float((g - r).abs().max()) / scale, float(ok.double().mean())
+
+
+@pytest.mark.parametrize("own", ["default", "all_own"])
+def test_bert_base_width_every_gradient_vs_fp32_oracle(own, monkeypatch):
+    """BERT-base width (hidden 768, FFN 3072, 12 heads), 2 layers, L = 128, dropout 0.1 on hidden states and
+    attention probabilities: ops.bert.bert_encode (fused MHA / LayerNorm / embedding kernels, own TN split-K weight
+    gradients, own FFN GEMMs; "all_own": every forward and dgrad on the own NT / NN GEMMs too) vs the fp32 oracle
+    models/bert.py::encode_ref.  The output and EVERY parameter gradient pass two criteria:
+      max-relative  max |g - r| / max |r| <= BB_MAXREL, and
+      element-wise  >= 99.9 % of entries within BB_ATOL_FRAC max |r| + BB_RTOL |r|."""
+    if own == "all_own":
+        monkeypatch.setenv("INA_BERT_OWN_NT", "1")
+        monkeypatch.setenv("INA_BERT_OWN_NN", "1")
+    from induction_network_on_fewrel_amd.config import Config
+    from induction_network_on_fewrel_amd.models import InductionNetwork
+    from induction_network_on_fewrel_amd.ops.bert import bert_encode
+    L = 128
+    cfg = Config(encoder="bert", bert_layers=2, bert_hidden=768, bert_heads=12, bert_intermediate=3072,
+                 bert_vocab=2000, bert_max_position=L, bert_max_length=L, bert_out_dim=64, bert_dropout=0.1,
+                 bert_attn_dropout=0.1)
+    torch.manual_seed(6)
+    m = InductionNetwork(cfg, None, vocab_size=10).to(dev)
+    NI = 10
+    ids = torch.randint(9, 2000, (NI, L), device=dev, dtype=torch.int32)
+    mask = torch.ones(NI, L, device=dev, dtype=torch.int32)
+    for i in range(NI):
+        mask[i, 40 + 9 * i:] = 0
+        ids[i, 40 + 9 * i:] = 0
+    e1 = torch.randint(1, 30, (NI,), device=dev, dtype=torch.int32)
+    e2 = torch.randint(1, 30, (NI,), device=dev, dtype=torch.int32)
+    inst = torch.tensor([0, 3, 5, 7, 9, 2, 1, 8], device=dev, dtype=torch.int32)
+    out = bert_encode(m, inst, (ids, mask, e1, e2), True, 91)
+    p = m.bert_pdict()
+    ref = B.encode_ref(p, ids[inst.long()], mask[inst.long()], e1[inst.long()], e2[inst.long()], cfg, True, 91)
+    mr, fr = _bb_stats(out.detach(), ref.detach())
+    print(f"  output: maxrel {mr:.2e} within {fr:.5f}")
+    assert mr <= BB_MAXREL and fr >= BB_MIN_FRAC
+    w = torch.randn_like(ref)
+    (out * w).sum().backward()
+    got = {n: t.grad.clone() for n, t in p.items() if t.grad is not None}
+    for t in p.values():
+        t.grad = None
+    (ref * w).sum().backward()
+    worst, fails = [], []
+    for n, t in p.items():
+        if t.grad is None or float(t.grad.abs().max()) == 0.0:
+            continue
+        assert n in got, n
+        if n.endswith("attention.self.key.bias"):
+            # exactly zero in exact arithmetic (q . (k + b) adds one constant to a query's scores: softmax-invariant);
+            # both sides are rounding noise -- bounded against the same layer's query-bias gradient instead
+            qb = p[n.replace("key.bias", "query.bias")].grad
+            r = float(got[n].abs().max()) / float(qb.abs().max())
+            print(f"  {n}: max |g| / max |g_query_bias| = {r:.2e}")
+            if r > 1e-2:
+                fails.append((n, r))
+            continue
+        mr, fr = _bb_stats(got[n], t.grad)
+        worst.append((mr, fr, n))
+        if not (mr <= BB_MAXREL and fr >= BB_MIN_FRAC):
+            fails.append((n, mr, fr))
+    worst.sort(reverse=True)
+    for w in worst[:6]:
+        print(f"  maxrel {w[0]:.2e} within {w[1]:.5f} {w[2]}")
+    print(f"  {len(worst)} parameter gradients; min within {min(x[1] for x in worst):.5f}")
+    assert not fails, fails
 
 
 @pytest.mark.parametrize("own_gemm", ["1", "0"])
