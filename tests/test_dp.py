@@ -1,4 +1,4 @@
-"""Episode data parallelism, multi-process on CPU with the gloo backend (world_size 2 and 4).
+"""Episode data parallelism, multi-process on CPU with the gloo backend (world_size 2, 4 and 8).
 
 Checks:
 * the DP step's gradient (all-reduce of the per-rank gradients, then the optimizer's 1/world scale)
@@ -116,7 +116,7 @@ def test_dp_resume_keeps_per_rank_samplers(tmp_path):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dp_gloo_world(tmp_path, world):
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
@@ -128,23 +128,26 @@ def test_dp_gloo_world(tmp_path, world):
         assert not torch.equal(r[0]["idx"], r[i]["idx"])   # rank-folded sampling
 
 
-def test_bench_self_launch_world2_cpu():
-    """``bench.py --gpus 2`` with no torch.distributed.run: the parent starts both ranks, rank 0 prints
-    one JSON line with the real collective world size; a failing rank fails the whole job."""
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_self_launch_cpu(world):
+    """``bench.py --gpus N`` with no torch.distributed.run: the parent starts the N ranks, rank 0 prints
+    one JSON line with the real collective world size; a failing rank fails the whole job.  N = 8 rehearses the
+    driver's 8-GPU scaling run (gloo on CPU: the rank bootstrap, the bucketed all-reduce and the MAX-over-ranks
+    timing at the world size of one MI355X node)."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, OMP_NUM_THREADS="1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "INA_FAULT_STEP"):
         env.pop(k, None)
-    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--device", "cpu", "--steps", "2",
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--device", "cpu", "--steps", "2",
            "--warmup", "1", "--episodes-per-gpu", "2", "--launch-timeout", "240"]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["rccl_world"] == 2 and out["backend"] == "gloo"
-    assert out["params_in_sync"] is True and len(out["rank_ms_per_step"]) == 2
-    assert out["config"]["global_batch"] == 4 and out["config"]["parallelism"] == "dp2"
-    bad = subprocess.run(cmd, cwd=root, env=dict(env, INA_FAULT_STEP="1", INA_FAULT_RANK="1"), capture_output=True,
+    assert out["n_gpus"] == world and out["rccl_world"] == world and out["backend"] == "gloo"
+    assert out["params_in_sync"] is True and len(out["rank_ms_per_step"]) == world
+    assert out["config"]["global_batch"] == 2 * world and out["config"]["parallelism"] == f"dp{world}"
+    bad = subprocess.run(cmd, cwd=root, env=dict(env, INA_FAULT_STEP="1", INA_FAULT_RANK=str(world - 1)), capture_output=True,
                          text=True, timeout=300)
     assert bad.returncode != 0
