@@ -76,7 +76,18 @@ def _run(cmd):
     return r.stdout
 
 
+def build_host() -> str:
+    """The host-only CPython extension (no torch / HIP: checkpoint CRC32C on any host, csrc/host/ina_host.c).
+    Built FIRST by build() and on its own by ``python csrc/build.py --host`` (a CPU-only host without hipcc)."""
+    hsrc = os.path.join(CSRC, "host", "ina_host.c")
+    if _newer(HOST_LIB, [hsrc, __file__]):
+        _run([shutil.which("gcc") or "cc", "-O2", "-fPIC", "-shared", "-I" + sysconfig.get_paths()["include"], hsrc,
+              "-o", HOST_LIB])
+    return HOST_LIB
+
+
 def build(verbose: bool = False, jobs: int = 0) -> str:
+    build_host()
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     os.makedirs(OUT_DIR, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
@@ -113,11 +124,6 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
         for out in ex.map(_run, tasks):
             if verbose and out.strip():
                 print(out)
-    # host-only CPython extension (no torch / HIP): checkpoint CRC32C on any host
-    hsrc = os.path.join(CSRC, "host", "ina_host.c")
-    if _newer(HOST_LIB, [hsrc, __file__]):
-        _run([shutil.which("gcc") or "cc", "-O2", "-fPIC", "-shared", "-I" + sysconfig.get_paths()["include"], hsrc,
-              "-o", HOST_LIB])
     if tasks or not os.path.exists(LIB) or _newer(LIB, objs):
         cmd = [hipcc, "-shared", "-fPIC", "-o", LIB, *objs, f"-L{tlib}", "-ltorch", "-ltorch_cpu", "-lc10",
                "-lc10_hip", "-ltorch_hip", "-lrccl", f"-Wl,-rpath,{tlib}"]
@@ -129,4 +135,4 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
 
 
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
+    print(build_host() if "--host" in sys.argv else build(verbose="-v" in sys.argv))

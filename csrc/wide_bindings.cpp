@@ -242,9 +242,13 @@ Tensor wide_pos_grad(const Tensor& dxp, const Tensor& inst, const Tensor& pos1, 
   const int64_t planes = dxp.dim() == 3 ? 2 : 1;
   const int64_t S = inst.size(0), L = pos1.size(1), PD = dxp.size(-1) / 2;
   chk(dxp, "dxp", at::kFloat, planes * S * L * 2 * PD);
-  // sequence chunks (grid.y), cap 1024 (75 -> 45 us vs 256 at the paper configuration, profiles/r5_posc);
-  // INA_POSG_CHUNKS overrides the cap (A/B tuning; deterministic for any value)
-  static const int64_t cap = [] { const char* e = std::getenv("INA_POSG_CHUNKS"); return e ? std::atoll(e) : 1024; }();
+  // sequence chunks (grid.y), cap 1024 (75 -> 45 us vs 256 at the paper configuration, profiles/r5_posc).  The cap
+  // sets the partial sums' order, so it is a compile-time constant (A/B builds: -DINA_POSG_CHUNKS=n), not an
+  // environment knob that would make two runs' gradients differ bitwise
+#ifndef INA_POSG_CHUNKS
+#define INA_POSG_CHUNKS 1024
+#endif
+  constexpr int64_t cap = INA_POSG_CHUNKS;
   const int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(cap, 1), S / 16));
   auto part = at::empty({chunks, 2, P2, PD}, dxp.options());
   if (S == 0) return part.sum(0);

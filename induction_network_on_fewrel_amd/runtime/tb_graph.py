@@ -147,8 +147,13 @@ def _collection(name: str, kind: int, values: Sequence[bytes]) -> bytes:
 
 
 def meta_graph(model, N: int, K: int, Q: int, max_to_keep: int = 5) -> bytes:
-    """Serialized MetaGraphDef, as ``tf.train.Saver.save`` writes next to the bundle
-    (/root/reference/model/base.py:124,177): meta_info_def {meta_graph_version "v0", tags}, the model's
+    """Serialized DESCRIPTIVE MetaGraphDef in the place ``tf.train.Saver.save`` writes one
+    (/root/reference/model/base.py:124,177).  It is not importable by ``tf.train.import_meta_graph``: the compute
+    nodes carry this framework's op types (BasicLSTMCell, SelfAttention, DynamicRouting, ... -- each tagged with the
+    kernel that runs it), the SaveV2 / RestoreV2 nodes lack TF's tensor_names / shape_and_slices inputs and dtypes
+    attrs, and the variables collection lists the parameters and global_step only (the bundle also holds the
+    optimizer slots <var>/Adam, <var>/Adam_1 or /Adagrad and beta1_power / beta2_power).  Contents:
+    meta_info_def {meta_graph_version "v0", tags}, the model's
     GraphDef plus the Saver's nodes (save/Const filename, save/SaveV2, save/control_dependency,
     save/RestoreV2, save/Assign_i, save/restore_all), a V2 SaverDef (tensor / op names as TF1's Saver names
     them, max_to_keep, keep_checkpoint_every_n_hours 10000) and the variables / trainable_variables /

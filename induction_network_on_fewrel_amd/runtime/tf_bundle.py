@@ -40,14 +40,22 @@ _DT_INV = {v: k for k, v in _DT.items()}
 
 
 # ------------------------------------------------------------------ CRC32C
+_CRC_WARNED = False
+
+
 def crc32c(data, crc: int = 0) -> int:
     """CRC-32C of a bytes-like object; the host-only native module (csrc/host/ina_host.c, no torch / HIP
     dependency) when it is built, else a table loop."""
+    global _CRC_WARNED
     try:
         from .. import _ina_host
         return _ina_host.crc32c(data, crc)
     except ImportError:
-        pass
+        if not _CRC_WARNED:
+            _CRC_WARNED = True
+            import warnings
+            warnings.warn("ina: the host CRC32C extension is not built (python csrc/build.py --host); checkpoint "
+                          "CRCs use the per-byte Python loop (slow for large bundles)")
     from .metrics import _TABLE
     c = crc ^ 0xFFFFFFFF
     for b in bytes(data):

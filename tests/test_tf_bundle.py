@@ -173,8 +173,22 @@ def test_meta_graph_written_and_parsed(tmp_path):
     kind, vals = mg["collections"]["variables"]
     assert len(vals) == len(tr.model.params.names()) + 1
     assert mg["collections"]["train_op"] == (1, [b"OptimizeLoss/Adam"])
-    # the rotation removes .meta with the rest of a checkpoint
+    # tf_checkpoint=False writes neither the bundle nor the .meta
     cfg2 = Config(**dict(cfg.to_dict(), tf_checkpoint=False, model_dir=str(tmp_path / "n")))
     tr2 = Trainer(cfg2, data, None, device="cpu")
     s2 = tr2.save()
     assert os.path.exists(s2 + ".safetensors") and not os.path.exists(s2 + ".meta") and not os.path.exists(s2 + ".index")
+
+
+def test_meta_rotated_out_with_its_checkpoint(tmp_path):
+    """checkpoint._remove drops a rotated-out stem's .meta with its .index / .data / .safetensors (max_to_keep)."""
+    from collections import OrderedDict
+    from induction_network_on_fewrel_amd.runtime import checkpoint as ckpt
+    md = str(tmp_path / "m")
+    t = OrderedDict(w=torch.arange(6, dtype=torch.float32))
+    stems = [ckpt.save(md, "inductionNetwork", s, t, {"step": s}, max_to_keep=2, tf_format=True, meta_graph=b"\x0a\x00")
+             for s in range(1, 5)]
+    for st in stems[:2]:   # rotated out
+        assert not any(os.path.exists(st + ext) for ext in (".meta", ".index", ".data-00000-of-00001", ".safetensors"))
+    for st in stems[2:]:   # kept
+        assert all(os.path.exists(st + ext) for ext in (".meta", ".index", ".safetensors"))
