@@ -22,6 +22,7 @@
 
 using namespace ina;
 
+
 namespace {
 
 template <int U, int NX, bool BF16>
@@ -373,10 +374,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   extern __shared__ __attribute__((aligned(16))) int2 ids_all[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = lane >> 4, n = lane & 15;
-  const int dir = blockIdx.y;
+  // longest work first: the backward direction (all L steps) dispatches before the forward one, whose ragged tiles
+  // (length-sorted ascending by the plan) run longest first -- no long tile left for the kernel's tail (lstm_fwd
+  // 784 -> 772, lstm_bwd 1343 -> 1322, rec_attn_fwd 365 -> 354 us, same box: profiles/r6_lpt)
+  const int dir = 1 - (int)blockIdx.y;
   const int ntiles = (S + 15) / 16;
-  const int tile = blockIdx.x * 4 + wave;
-  int2* ids = ids_all + wave * 16 * L;
+  const int tile = dir == 0 ? ntiles - 1 - ((int)blockIdx.x * 4 + wave) : (int)blockIdx.x * 4 + wave;
+  int2* ids = ids_all + (wave * 16) * L;
   if constexpr (XD) {   // the block's position tables (xg = x_gather's global copy; before any wave leaves)
     xd_copy(ids_all, xg, L);
     __syncthreads();
@@ -388,7 +392,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
       int sn = i / L, t = i - sn * L;
       int sq = tile * 16 + sn;
       int2 v = make_int2(0, 0);
-      if (tile < ntiles && sq < S) {
+      if (tile >= 0 && tile < ntiles && sq < S) {
         long r = (long)inst[sq] * L + t;
         v.x = word[r];
         v.y = pos1[r] | (pos2[r] << 16);
@@ -397,7 +401,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     }
     wave_lds_sync();
   }
-  if (tile >= ntiles) return;
+  if (tile < 0 || tile >= ntiles) return;
   const int seq = tile * 16 + n;  // rows >= S are padding rows of hnat (allocated to 16 * ntiles)
   const uint32_t salt = dropout_salt(seed, (uint32_t)dir);
   // ragged tiles: processing steps [tb, te).  Forward direction: t < Lt (the tile's longest length; later
@@ -779,7 +783,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   constexpr int NA = NMT * NKS * 64, NA2 = NMT2 * NKS2 * 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = lane >> 4, n = lane & 15;
-  const int dir = blockIdx.y;
+  // longest work first (as lstm_fwd): the backward direction's workgroups (all L steps) dispatch first, the forward
+  // direction's ragged tile groups in descending length
+  const int dir = 1 - (int)blockIdx.y;
   const int ntiles = (S + 15) / 16;
   const int ngroups = (ntiles + 3) / 4;
   const int P2 = 2 * L;  // pos table rows
@@ -862,7 +868,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
   for (int xi = 0; xi < NX; ++xi)
     pofs[xi] = ((uint32_t)(xs[xi].sel - 1) < 2u ? 4 * xi + q - E : NPF) * 16 + n;
 
-  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+  for (int gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
+    const int g = dir == 0 ? ngroups - 1 - gi : gi;
     const int tile = g * 4 + wave;
     if (tile >= ntiles) continue;  // no block-level barrier inside the group loop
     const int seq = tile * 16 + n;

@@ -29,6 +29,7 @@
 
 using namespace ina;
 
+
 namespace {
 
 template <int U>
@@ -183,7 +184,10 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
   using C = RA<U>;
   constexpr int U4 = C::U4, H2 = C::H2, NV = C::NV, NKR = C::NKR, MT = C::MT;
   const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15;
-  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // longest tiles first (the ragged plan sorts rows by length ascending; dispatching in that order left the longest
+  // tiles for the kernel's tail): tile = ntiles - 1 - (4 blockIdx.x + wave)
+  const int ntl = (S + 15) / 16, tix = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int tile = ntl - 1 - tix;
   // weights shared by the workgroup in LDS (registers kept for occupancy: the loop is latency-bound
   // on the record loads, so resident waves are what hides them)
   __shared__ u16x8_t lA[MT * NKR * 64];
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
     lbw[MT * 16 + i] = i < H2 ? w2[i] : 0.f;
   }
   __syncthreads();
-  if (tile * 16 >= S) return;   // wave-uniform; no workgroup barrier after this point
+  if (tile < 0 || tile * 16 >= S) return;   // wave-uniform; no workgroup barrier after this point
   const int seq = tile * 16 + n;
   const bool valid = seq < S;
   const int seqc = valid ? seq : S - 1;
