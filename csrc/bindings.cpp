@@ -10,7 +10,6 @@
 #include <hip/hip_runtime.h>
 #include <torch/library.h>
 
-#include <cstdlib>
 #include <tuple>
 
 #include "ina_launch.h"
@@ -341,10 +340,11 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(
   TORCH_CHECK(a2pack.numel() == 2 * ((NSLOT + 3) / 4) * ((4 * U4 + KPL - 1) / KPL) * 64 * KPL, "ina.lstm_bwd: a2pack");
   TORCH_CHECK(ina::lstm_bwd_lds_bytes((int)U, (int)NX, bf16, (int)L, (int)PD) <= 160 * 1024, "ina.lstm_bwd: LDS budget");
   const int64_t ngroups = ((S + 15) / 16 + 3) / 4;
-  // 512 workgroups per direction: ~2 rounds of 3-4 tile groups each, back-filled by the dispatcher.
-  // (A grid of exactly the resident workgroups, ina::lstm_bwd_resident_blocks, measured slower:
+  // 768 workgroups per direction (the backward direction's first, longest-first order), back-filled by the
+  // dispatcher: 23.79-23.81 vs 23.87-24.06 ms per 18 calls for 512, 25.5 for 640, 24.4 for 896 (profiles/r6_blocks).
+  // (A grid of exactly the resident workgroups, ina::lstm_bwd_resident_blocks, measured slower in round 3:
   // 616 vs 580 us -- its critical path is the 7-group workgroups.)
-  if (blocks <= 0) blocks = 512;
+  if (blocks <= 0) blocks = 768;
   blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, ngroups));
   auto opt = wemb.options();
   auto dw_slab = at::empty({blocks, 2, 4 * U, NF}, opt);
