@@ -230,7 +230,8 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
                                                       unsigned short* __restrict__ posb,
                                                       unsigned char* __restrict__ dmask, int U, uint32_t seed,
                                                       const int* __restrict__ seed_dev, uint32_t thr,
-                                                      const int* __restrict__ perm, unsigned short* __restrict__ xdtab) {
+                                                      const int* __restrict__ perm, unsigned short* __restrict__ xdtab,
+                                                      const int* __restrict__ tlen) {
   // direct x: block (0, 0) also builds the recurrences' position tables (xd_build) in global memory
   if (xdtab != nullptr && blockIdx.x == 0 && blockIdx.y == 0) xd_build(xdtab, L, E, PD, p1emb, p2emb);
   // the two position tables ([2L, PD] each, tiny) in LDS: per-feature loads from them were most of
@@ -258,6 +259,9 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
   const uint32_t sd = seed_dev ? (uint32_t)seed_dev[0] : seed;
   const uint32_t pv = perm ? (uint32_t)perm[valid ? seq : S - 1] : 0u;   // (clamped: no lane-dependent branch)
   const uint32_t oseq = (perm && valid) ? pv : (uint32_t)seq;
+  // ragged tiles: keep bits of steps t >= the tile's longest length are never consumed (the attention stops
+  // there and lstm_bwd's dH loads past it return 0): not hashed, stored as 0 (~30% of the hashes at FewRel lengths)
+  const int Lhash = tlen ? tlen[tile] : L;
   int p1c[XG_C], p2c[XG_C], widc[XG_C];
   u16x8_t wrc[XG_C];
   // direct x: only the t = 0 position ids are consumed (pos_shift_gemm's per-sequence offsets); every
@@ -319,6 +323,7 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
       const uint32_t salt = dropout_salt(sd, (uint32_t)d);
       const uint32_t pbase = ((oseq * L + t) * U) >> 1;   // U even: the row's first unit pair
       uint32_t by[4] = {0u, 0u, 0u, 0u};                            // keep byte of lane group q
+      if (t < Lhash)
 #pragma unroll
       for (int k = 0; k < 16; ++k) {                                // units 2k, 2k + 1 (lstm_keep)
         if (2 * k >= U) break;
@@ -1983,7 +1988,7 @@ int x_gather(const LstmArgs& a, int U, int NX, hipStream_t st) {
 #define INA_XG_LAUNCH(NXV, DIR, ...)                                                                     \
   hipLaunchKernelGGL((x_gather_kernel<NXV, DIR, ##__VA_ARGS__>), grid, dim3(256), 0, st, a.inst, a.S, a.word, a.pos1, a.pos2, a.L, \
                      a.wemb, wr16, a.E, a.p1emb, a.p2emb, a.PD, xg, posb, a.drop ? a.dmask : nullptr, U, a.seed, \
-                     a.seed_dev, a.thr, a.perm, a.xd ? (unsigned short*)a.xdtab : nullptr)
+                     a.seed_dev, a.thr, a.perm, a.xd ? (unsigned short*)a.xdtab : nullptr, a.tlen)
   if (NX == 4 && a.wrows && U == 20 && a.E == 5 && a.PD == 5)
     INA_XG_LAUNCH(4, true, 20, 5, 5);
   else if (NX == 4 && a.wrows)

@@ -350,7 +350,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? I
   const bool drop = dmask != nullptr;
   const int ntiles = (S + 15) / 16;
 
-  for (int tile = blockIdx.x * 4 + wave; tile < ntiles; tile += gridDim.x * 4) {   // wave-uniform
+  // static round robin over the tiles in DESCENDING length (the plan sorts ascending): a wave's extra tile in the
+  // last round is one of the shortest, not of the longest
+  for (int ti = blockIdx.x * 4 + wave; ti < ntiles; ti += gridDim.x * 4) {   // wave-uniform
+    const int tile = ntiles - 1 - ti;
     const int seq = tile * 16 + n;
     const bool valid = seq < S;
     const int seqc = valid ? seq : S - 1;
