@@ -354,7 +354,8 @@ std::tuple<Tensor, Tensor, Tensor> lstm_bwd(
   const int64_t pblocks = std::max<int64_t>(1, std::min<int64_t>(1024, (pitems + 31) / 32));
   if (bf16) TORCH_CHECK(2 * PD <= 16 && 2 * L <= 128, "ina.lstm_bwd: bf16 path needs pos_dim <= 8 and L <= 64");
   // pos_shift (caller-checked pos[s][t] = pos[s][0] + t, pos[s][0] <= L): per-sequence one-hot GEMM -> ONE slab
-  const bool shift = bf16 && pos_shift && (L + 1 + 15) / 16 <= 5;
+  // (pos_shift_gemm addresses one direction of dxp through a 32-bit buffer offset: < 2 GiB, ~2M sequences at L=38)
+  const bool shift = bf16 && pos_shift && (L + 1 + 15) / 16 <= 5 && ((S + 15) / 16) * L * (2 * PD + 1) * 32 < (1LL << 31);
   // (direct x: x_gather wrote only the t = 0 position ids -- the shifted-form reduction's per-sequence offsets)
   TORCH_CHECK(!(bf16 && xg.numel() == ((S + 15) / 16) * L * 16 + 64 * L) || shift,
               "ina.lstm_bwd: direct x needs the shifted-position gradient path");

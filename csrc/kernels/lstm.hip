@@ -1669,7 +1669,8 @@ __global__ __launch_bounds__(256) void pos_grad_kernel(const unsigned short* __r
 template <int NRT>
 __global__ __launch_bounds__(256) void pos_shift_gemm_kernel(const unsigned short* __restrict__ dxp,
                                                              const unsigned short* __restrict__ posb, int S, int L,
-                                                             int PD, int kps, float* __restrict__ gpart) {
+                                                             int PD, int kps, float* __restrict__ gpart,
+                                                             const int* __restrict__ tlen) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = lane >> 4, n = lane & 15;
   const int ntiles = (S + 15) / 16, NPF = 2 * PD;
@@ -1690,12 +1691,18 @@ __global__ __launch_bounds__(256) void pos_shift_gemm_kernel(const unsigned shor
   for (int pt = 0; pt < NRT; ++pt) acc[pt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   // B fragment: lane (q, n) holds sequences 8(q&1)..+7 of tile 2ks + (q>>1) at column n (16 B, both
   // directions); the one-hot A row n of tile pt marks the sequences whose offset is pt*16 + n
+  // ragged tiles: the forward direction's dxp rows t >= the tile's length are zero (lstm_bwd never processes those
+  // steps): read through a buffer descriptor at an out-of-range offset -> 0, no bytes moved (~15% of the reads)
+  const auto rd0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(dxp), (short)0, (int)(dstride * 2),
+                                                     0x00020000);
   auto load = [&](int ks, u16x8_t& b0, u16x8_t& b1, u16x8_t& pp, bool& ok) {
     const int tile = 2 * ks + (q >> 1);
     ok = cval && tile < ntiles && ks < k1;
     const int tl = tile < ntiles ? tile : ntiles - 1;
     const size_t o = (((size_t)tl * L + t) * (NPF + 1) + f) * 16 + half;
-    b0 = *reinterpret_cast<const u16x8_t*>(dxp + o);
+    const bool live0 = tlen == nullptr || t < tlen[tl];
+    b0 = __builtin_bit_cast(u16x8_t, __builtin_amdgcn_raw_buffer_load_b128(rd0, live0 ? (uint32_t)(o * 2) : 0x80000000u,
+                                                                            0, 0));
     b1 = *reinterpret_cast<const u16x8_t*>(dxp + dstride + o);
     pp = *reinterpret_cast<const u16x8_t*>(posb + (size_t)tl * L * 16 + half);   // ids at t = 0
   };
@@ -1933,9 +1940,9 @@ int pos_grad_shift(const LstmArgs& a, float* gpart, float* out, hipStream_t st) 
   const auto* dxp = (const unsigned short*)a.dxp;
   dim3 grid((2 * NT + 3) / 4, nchunk), block(256);
   if (NRT <= 3)
-    hipLaunchKernelGGL(pos_shift_gemm_kernel<3>, grid, block, 0, st, dxp, a.posb, a.S, a.L, a.PD, kps, gpart);
+    hipLaunchKernelGGL(pos_shift_gemm_kernel<3>, grid, block, 0, st, dxp, a.posb, a.S, a.L, a.PD, kps, gpart, a.tlen);
   else
-    hipLaunchKernelGGL(pos_shift_gemm_kernel<5>, grid, block, 0, st, dxp, a.posb, a.S, a.L, a.PD, kps, gpart);
+    hipLaunchKernelGGL(pos_shift_gemm_kernel<5>, grid, block, 0, st, dxp, a.posb, a.S, a.L, a.PD, kps, gpart, a.tlen);
   INA_CHECK_LAUNCH();
   const int rows = (NRT <= 3 ? 3 : 5) * 16;
   hipLaunchKernelGGL(pos_shift_finish_kernel, dim3(2 * 2 * a.L * a.PD), dim3(256), 0, st, gpart, nchunk, a.L, a.PD,
