@@ -454,7 +454,82 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
       for (int xi = 0; xi < NX; ++xi) xv[xi] = gather_x(xs[xi], r);
     }
   };
-  // one recurrence step at processing index tau with input features xv
+  // bf16: the recurrent h as packed bf16 pairs (units 2k, 2k + 1) -- the value the gate MFMA, the step record and
+  // the next step read, converted ONCE per pair.  (h kept in fp32 rounded to bf16 cost a convert + a shift per
+  // unit and step, and the B operand and the record store converted it again; x went bf16 -> fp32 -> bf16.)
+  constexpr int NHW = (U4 + 1) / 2;
+  uint32_t hw[NHW];
+#pragma unroll
+  for (int k = 0; k < NHW; ++k) hw[k] = 0u;
+  // B operand word of slots (s0, s0 + 1): slot s < U4 is h unit s, U4 <= s < U4 + NX the x feature slot s - U4
+  // (xw: NX / 2 words of packed bf16 pairs), past them zero.  Same-word aligned pairs pass through, the rest is one
+  // v_perm (bytes 0-3 of src1 = the lo word, 4-7 of src0 = the hi word).
+  auto bword = [&](const int s0, const uint32_t* xw) __attribute__((always_inline)) -> uint32_t {
+    // source of slot s: word id (h word k -> k, x word k -> NHW + k, none -> -1) and 16-bit half
+    auto wid = [&](int s) { return s < U4 ? (s >> 1) : (s - U4 < NX ? NHW + ((s - U4) >> 1) : -1); };
+    auto half = [&](int s) { return s < U4 ? (s & 1) : ((s - U4) & 1); };
+    auto word = [&](int id) { return id < NHW ? hw[id] : xw[id - NHW]; };
+    const int il = wid(s0), ih = wid(s0 + 1), lh = half(s0), hh = half(s0 + 1);
+    if (il < 0 && ih < 0) return 0u;
+    if (il == ih && lh == 0 && hh == 1) return word(il);
+    const uint32_t sl = il >= 0 ? (uint32_t)((2 * lh) | ((2 * lh + 1) << 8)) : 0x0C0Cu;
+    const uint32_t sh = ih >= 0 ? (uint32_t)((4 + 2 * hh) | ((5 + 2 * hh) << 8)) : 0x0C0Cu;
+    return __builtin_amdgcn_perm(ih >= 0 ? word(ih) : 0u, il >= 0 ? word(il) : 0u, sl | (sh << 16));
+  };
+  auto pk2 = [](float a, float b) {   // two floats -> packed bf16 pair (one v_cvt_pk_bf16_f32, RNE as f2bf)
+    typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+    const bf2_t v = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
+  };
+  // one bf16 recurrence step at processing index tau with input feature words xw
+  auto step_bf = [&](const int tau, const uint32_t* xw) __attribute__((always_inline)) {
+    const int t = dir ? (L - 1 - tau) : tau;
+    frag B[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      if constexpr (BF16) {
+        const u32x4_t v = {bword(ks * 8, xw), bword(ks * 8 + 2, xw), bword(ks * 8 + 4, xw), bword(ks * 8 + 6, xw)};
+        B[ks] = __builtin_bit_cast(frag, v);
+      }
+    }
+    float hv[U4];
+#pragma unroll
+    for (int m = 0; m < NMT; ++m) {
+      f32x4_t acc = {bm[m][0], bm[m][1], bm[m][2], bm[m][3]};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) acc = mma(A[m][ks], B[ks], acc);
+      const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
+      c[m] = c[m] * fg + ig * jg;
+      hv[m] = tanh_l2(c[m] * (2.f * LOG2E_F)) * og;
+    }
+    if constexpr (SKIP) {   // backward direction past the row's length: state (and output) reset to zero
+      if (dir == 1 && t >= mylen) {
+#pragma unroll
+        for (int m = 0; m < U4; ++m) hv[m] = c[m] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NHW; ++k) hw[k] = pk2(hv[2 * k], 2 * k + 1 < U4 ? hv[2 * k + 1] : 0.f);
+    // bf16 step record [tile][dir][t][2][U4][64] (16-bit): slot 0 = the raw recurrent h (bf16), slot 1 = the cell
+    // state (fp16, training only); every store is a coalesced 128-B lane-layout run off ONE address.  The h slot is
+    // both the backward's stash and the attention input (the attention applies the DropoutWrapper mask from the keep
+    // bits).  32-bit offsets (checked on the host); padding rows are stored too.
+    unsigned short* rec = reinterpret_cast<unsigned short*>(hnat) + ((uint32_t)((tile * 2 + dir) * L + t) * (2 * U4)) * 64 + lane;
+#pragma unroll
+    for (int m = 0; m < U4; ++m) rec[m * 64] = (unsigned short)(hw[m >> 1] >> (16 * (m & 1)));
+    if constexpr (STORE) {
+#pragma unroll
+      for (int m = 0; m < U4; ++m) rec[(U4 + m) * 64] = __builtin_bit_cast(unsigned short, (_Float16)c[m]);
+    }
+    if constexpr (DROP) {
+      const uint32_t base = ((uint32_t)seq * L + t) * U + q;
+      uint32_t bits = 0;
+#pragma unroll
+      for (int m = 0; m < U4; ++m) bits |= lstm_keep(salt, base + 4 * m, thr) ? (1u << m) : 0u;
+      dmask[(uint32_t)((tile * 2 + dir) * L + t) * 64 + lane] = (unsigned char)bits;
+    }
+  };
+  // one fp32 recurrence step at processing index tau with input features xv
   auto step = [&](const int tau, const float* xv) __attribute__((always_inline)) {
     const int t = dir ? (L - 1 - tau) : tau;
     frag B[NKS];
@@ -477,9 +552,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
       for (int ks = 0; ks < NKS; ++ks) acc = mma(A[m][ks], B[ks], acc);
       const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
       c[m] = c[m] * fg + ig * jg;
-      float hv = tanh_l2(c[m] * (2.f * LOG2E_F)) * og;
-      if (BF16) hv = round_bf(hv);  // the stored / recurrent operand value
-      h[m] = hv;
+      h[m] = tanh_l2(c[m] * (2.f * LOG2E_F)) * og;
     }
     if constexpr (SKIP) {   // backward direction past the row's length: state (and output) reset to zero
       if (dir == 1 && t >= mylen) {
@@ -487,29 +560,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
         for (int m = 0; m < U4; ++m) h[m] = c[m] = 0.f;
       }
     }
-    if constexpr (BF16) {
-      // bf16 step record [tile][dir][t][2][U4][64] (16-bit): slot 0 = the raw recurrent h (bf16), slot 1
-      // = the cell state (fp16, training only); every store is a coalesced 128-B lane-layout run off
-      // ONE address.  The h slot is both the backward's stash and the attention input:
-      // h_natural_kernel transposes it to natural rows and applies the DropoutWrapper mask from the
-      // keep bits stored here.  (Natural [seq][t][2U] rows from here scatter each store over 16 rows,
-      // ~300 us of ~550; a separate dropped copy costs 303 MB more on a write-bandwidth-bound kernel.)
-      // 32-bit offsets (checked on the host); padding rows are stored too.
-      typename FragT<BF16>::elem* rec = hnat + ((uint32_t)((tile * 2 + dir) * L + t) * (2 * U4)) * 64 + lane;
-#pragma unroll
-      for (int m = 0; m < U4; ++m) rec[m * 64] = to_elem(h[m], (typename FragT<BF16>::elem*)nullptr);
-      if constexpr (STORE) {
-#pragma unroll
-        for (int m = 0; m < U4; ++m) rec[(U4 + m) * 64] = __builtin_bit_cast(unsigned short, (_Float16)c[m]);
-      }
-      if constexpr (DROP) {
-        const uint32_t base = ((uint32_t)seq * L + t) * U + q;
-        uint32_t bits = 0;
-#pragma unroll
-        for (int m = 0; m < U4; ++m) bits |= lstm_keep(salt, base + 4 * m, thr) ? (1u << m) : 0u;
-        dmask[(uint32_t)((tile * 2 + dir) * L + t) * 64 + lane] = (unsigned char)bits;
-      }
-    } else {
+    if constexpr (!BF16) {
       // fp32: the attention input (dropout applied) in natural rows, h / c stash in the lane layout
       typename FragT<BF16>::elem* hn = hnat + (((uint32_t)seq * L + t) * (2 * U) + dir * U + q);
       if constexpr (DROP) {
@@ -585,11 +636,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     auto step_xr = [&](const int tau, const XR& r0) __attribute__((always_inline)) {
       XR r = r0;
       asm volatile("" : "+v"(r.w), "+v"(r.a), "+v"(r.b));
-      const uint32_t w0 = (r.w | (uint32_t)r.a | (uint32_t)r.b) & vm;
-      const uint32_t w1 = ((uint32_t)(r.a >> 32) | (uint32_t)(r.b >> 32)) & vm;
-      float xv[4] = {bf2f((unsigned short)w0), bf2f((unsigned short)(w0 >> 16)), bf2f((unsigned short)w1),
-                     bf2f((unsigned short)(w1 >> 16))};
-      step(tau, xv);
+      const uint32_t xw[2] = {(r.w | (uint32_t)r.a | (uint32_t)r.b) & vm,
+                              ((uint32_t)(r.a >> 32) | (uint32_t)(r.b >> 32)) & vm};
+      step_bf(tau, xw);
     };
     auto xpair = [&](int tau) __attribute__((always_inline)) {
       load_xr(tof(tau + 1), rb);
@@ -627,12 +676,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
         rr[c] = r[c];
         asm volatile("" : "+v"(rr[c]));
       }
-      float xv[NX];
+      uint32_t xw[NX / 2];
 #pragma unroll
-      for (int c = 0; c < NX / 4; ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) xv[4 * c + e] = bf2f(rr[c][e]);
-      step(tau, xv);
+      for (int c = 0; c < NX / 4; ++c) {
+        const uint2 v = __builtin_bit_cast(uint2, rr[c]);
+        xw[2 * c] = v.x;
+        xw[2 * c + 1] = v.y;
+      }
+      step_bf(tau, xw);
     };
     // pair structure as below: sched_barrier pins each prefetch ahead of the step it overlaps, and the
     // first pair is peeled so the loop header is entered with the same outstanding-VMEM state from

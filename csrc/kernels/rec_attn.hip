@@ -140,21 +140,20 @@ INA_DEVICE void rec_steps(int L, LD&& load, F&& step) {
   }
 }
 // DropoutWrapper output (model/graph.py:36-38): keep ? bf16(h / keep_prob) : 0 -- the same rounding
-// as h_natural_kernel, so both attention paths see identical H.  Branch-free (a select here compiled
-// to one branch per element): scale = keep bit * inv_kp (inv_kp = 1 and all bits set without
-// dropout, which reproduces h exactly).  Two values per call: packed bf16 pair (B operand word) and
-// the rounded fp32 values.
-// the DropoutWrapper scale of the lane's slot i: keep bit * inv_kp
+// as h_natural_kernel, so both attention paths see identical H.  Branch-free: the lane's keep bit of slot i as a
+// 0 / all-ones mask (v_bfe_i32 of the 1-bit field) ANDed into the raw bf16 value (inv_kp = 1 and all bits set
+// without dropout, which reproduces h exactly).  (Scaling by keep bit * inv_kp took an extract, a convert and a
+// multiply per value.)  Two values per call: packed bf16 pair (B operand word) and the rounded fp32 values.
 template <int U>
-INA_DEVICE float rec_scale(const RecStep<U>& s, int i, float inv_kp) {
+INA_DEVICE uint32_t rec_kmask(const RecStep<U>& s, int i) {
   constexpr int U4 = RA<U>::U4;
   const int b = i < U4 ? i : 8 + i - U4;
-  return (float)((s.kb >> b) & 1u) * inv_kp;
+  return (uint32_t)__builtin_amdgcn_sbfe((int)s.kb, b, 1);
 }
 template <int U>
 INA_DEVICE uint32_t rec_drop2(const RecStep<U>& s, int i, float inv_kp, float& v0, float& v1) {
-  const float x0 = bf2f(s.h[i]) * rec_scale<U>(s, i, inv_kp);
-  const float x1 = bf2f(s.h[i + 1]) * rec_scale<U>(s, i + 1, inv_kp);
+  const float x0 = __builtin_bit_cast(float, ((uint32_t)s.h[i] & rec_kmask<U>(s, i)) << 16) * inv_kp;
+  const float x1 = __builtin_bit_cast(float, ((uint32_t)s.h[i + 1] & rec_kmask<U>(s, i + 1)) << 16) * inv_kp;
   const uint32_t w = (uint32_t)f2bf(x0) | ((uint32_t)f2bf(x1) << 16);
   v0 = __builtin_bit_cast(float, w << 16);
   v1 = __builtin_bit_cast(float, w & 0xFFFF0000u);
@@ -455,7 +454,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? I
           const int fi = 4 * T + r;
           if (fi < NV) {
             const int dd = fi / U4, m = fi % U4;
-            d0[((size_t)dd * L + t) * U4 * 64 + m * 64] = f2bf((acc[r] + alv * dev[fi]) * rec_scale<U>(cur, fi, inv_kp));
+            d0[((size_t)dd * L + t) * U4 * 64 + m * 64] =
+                (unsigned short)((uint32_t)f2bf((acc[r] + alv * dev[fi]) * inv_kp) & rec_kmask<U>(cur, fi));
           }
         }
       }
