@@ -212,6 +212,17 @@ __global__ __launch_bounds__(256) void xd_ids_kernel(const int* __restrict__ ins
 // x enters the gate MFMAs as bf16 in this mode, so the values are exactly the ones the per-step
 // gather produced.
 // ------------------------------------------------------------------------------------------
+// a_lo = 2 a_lo + (x[15:0] < thr16), a_hi = 2 a_hi + (x[31:16] < thr16): an SDWA compare into VCC and an
+// add-with-carry per bit (hipcc emits compare, select and or)
+INA_DEVICE void keep_acc2(uint32_t x, uint32_t thr16, uint32_t& a_lo, uint32_t& a_hi) {
+  asm("v_cmp_lt_u32_sdwa vcc, %2, %3 src0_sel:WORD_0 src1_sel:DWORD\n\t"
+      "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_lt_u32_sdwa vcc, %2, %3 src0_sel:WORD_1 src1_sel:DWORD\n\t"
+      "v_addc_co_u32_e32 %1, vcc, %1, %1, vcc"
+      : "+v"(a_lo), "+v"(a_hi)
+      : "v"(x), "s"(thr16)
+      : "vcc");
+}
 constexpr int XG_T = 16;   // steps per workgroup pass (16 sequences x 16 steps = 256 threads)
 constexpr int XG_C = 3;    // passes per workgroup (L = 37: one workgroup per tile): the token loads of all
                            // passes are issued before any is consumed, the pos tables staged once
@@ -323,14 +334,22 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
       const uint32_t salt = dropout_salt(sd, (uint32_t)d);
       const uint32_t pbase = ((oseq * L + t) * U) >> 1;   // U even: the row's first unit pair
       uint32_t by[4] = {0u, 0u, 0u, 0u};                            // keep byte of lane group q
-      if (t < Lhash)
+      if (t < Lhash) {
+        // dropout_mix(salt, pbase + k) with the counter multiply strength-reduced (salt folded into the row's
+        // base), and the keep bits shift-accumulated (compare + add-with-carry per bit): unit 2k goes to byte
+        // (2k) & 3 at bit k >> 1, so walking k DOWN leaves each bit at its place (lstm_keep's bits exactly)
+        uint32_t b0 = pbase * 0x6C8E9CF5u + salt;
+        asm volatile("" : "+v"(b0));   // one add per hash below (hipcc re-split it into base + k C1, then + salt)
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {                                // units 2k, 2k + 1 (lstm_keep)
-        if (2 * k >= U) break;
-        const uint32_t x = dropout_mix(salt, pbase + k);
-        const int u0 = 2 * k, u1 = 2 * k + 1;
-        by[u0 & 3] |= ((x & 0xFFFFu) < thr16 ? 1u : 0u) << (u0 >> 2);
-        by[u1 & 3] |= ((x >> 16) < thr16 ? 1u : 0u) << (u1 >> 2);
+        for (int k = 15; k >= 0; --k) {                             // units 2k, 2k + 1 (lstm_keep)
+          if (2 * k >= U) continue;
+          uint32_t x = b0 + (uint32_t)k * 0x6C8E9CF5u;
+          x ^= x >> 16;
+          x *= 0x7FEB352Du;
+          x ^= x >> 15;
+          const int g = (2 * k) & 3;
+          keep_acc2(x, thr16, by[g], by[g + 1]);
+        }
       }
       // staged in LDS, stored below as coalesced dwords (per-lane byte stores to global were most of
       // this kernel's time once direct x removed its x rows)
