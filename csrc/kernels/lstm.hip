@@ -517,9 +517,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
       f32x4_t acc = {bm[m][0], bm[m][1], bm[m][2], bm[m][3]};
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) acc = mma(A[m][ks], B[ks], acc);
-      const float ig = sigmoid_l2(acc[0]), jg = tanh_l2(acc[1]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
-      c[m] = c[m] * fg + ig * jg;
-      hv[m] = tanh_l2(c[m] * (2.f * LOG2E_F)) * og;
+      // c[m] holds the cell state times 2 log2(e) (tanh_l2's argument scale): the scale rides on the g gate's
+      // 1 - 2r form (k - 2k r, same fma) and the fp16 record's conversion (x 1/k), so tanh(c) needs no multiply
+      const float ig = sigmoid_l2(acc[0]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
+      const float jk = fmaf(fast_rcp(__builtin_amdgcn_exp2f(acc[1]) + 1.0f), -2.f * (2.f * LOG2E_F), 2.f * LOG2E_F);
+      c[m] = c[m] * fg + ig * jk;
+      hv[m] = tanh_l2(c[m]) * og;
     }
     if constexpr (SKIP) {   // backward direction past the row's length: state (and output) reset to zero
       if (dir == 1 && t >= mylen) {
@@ -538,7 +541,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     for (int m = 0; m < U4; ++m) rec[m * 64] = (unsigned short)(hw[m >> 1] >> (16 * (m & 1)));
     if constexpr (STORE) {
 #pragma unroll
-      for (int m = 0; m < U4; ++m) rec[(U4 + m) * 64] = __builtin_bit_cast(unsigned short, (_Float16)c[m]);
+      for (int m = 0; m < U4; ++m)
+        rec[(U4 + m) * 64] = __builtin_bit_cast(unsigned short, (_Float16)(c[m] * (0.5f / LOG2E_F)));
     }
     if constexpr (DROP) {
       const uint32_t base = ((uint32_t)seq * L + t) * U + q;
