@@ -14,8 +14,8 @@ timeout -k 10 200 python bench.py --steps 30 --warmup 5 --episodes-per-gpu 2048 
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --mode eval > $OUT/beval.log 2>&1 && \
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --mode eval --shot 1 > $OUT/beval1.log 2>&1 && \
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --mode eval --nota 0.5 > $OUT/bevaln.log 2>&1 && \
-timeout -k 10 300 python bench.py --steps 5 --warmup 2 --encoder bert > $OUT/bbert.log 2>&1 && \
-timeout -k 10 300 python bench.py --hidden 128 --word-dim 300 --query 20 --episodes-per-gpu 256 --steps 5 --warmup 2 > $OUT/bpaper.log 2>&1 && \
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 --encoder bert > $OUT/bbert.log 2>&1 && \
+timeout -k 10 300 python bench.py --hidden 128 --word-dim 300 --query 20 --episodes-per-gpu 256 --steps 10 --warmup 3 > $OUT/bpaper.log 2>&1 && \
 cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_rd -o run --output-format rocpd -- python3 $ROOT/bench.py --steps 20 --warmup 5 > $ROOT/$OUT/pb.log 2>&1 && \
 cd $ROOT && python tools/rocpd_summary.py $(ls /tmp/prof_rd/*/*.db /tmp/prof_rd/*.db 2>/dev/null | head -1) --steps 25 --md $OUT/stats.md --csv $OUT/stats.csv > $OUT/sum.txt 2>&1
