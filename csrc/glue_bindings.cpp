@@ -131,20 +131,22 @@ int64_t slab_scatter_add(Tensor dst, const std::vector<Tensor>& srcs, const std:
     jobs.map[j] = maps[j].data_ptr<int>();
     jobs.n[j] = (long)n;
     jobs.nblk[j] = (int)nblks[j];
-    // ~sqrt(nblk) chunks: both launches then sum ~sqrt(nblk) values per lane
-    int nch = 1;
-    while ((int64_t)nch * nch < nblks[j]) ++nch;
-    jobs.nch[j] = std::min(nch, 256);
+    // chunks of ~32 slab rows (8 per wave): ~sqrt(nblk) chunks gave the wide, short dM slabs (32 x 160,000) 3,750
+    // workgroups of ~5 rows each (launch-bound: 33-36 us for ~50 MB at the headline step)
+    jobs.nch[j] = (int)std::min<int64_t>(256, std::max<int64_t>(1, (nblks[j] + 31) / 32));
     if (scales[j].numel() > 0) {
       need(scales[j], op, "scale", at::kFloat);
       jobs.scale[j] = scales[j].data_ptr<float>();
     }
     const long ncol = (long)((n + 63) / 64);
+    // float4 columns for the partial sums when every row (slab and workspace) is 16-byte aligned
+    jobs.vec[j] = (n % 4 == 0 && ((uintptr_t)jobs.src[j] & 15) == 0 && wsb % 4 == 0) ? 1 : 0;
+    const long ncolp = jobs.vec[j] ? (long)((n + 255) / 256) : ncol;
     jobs.wsbase[j] = wsb;
     jobs.bbase[j] = bb;
     jobs.fbase[j] = fb;
     wsb += (long)jobs.nch[j] * (long)n;
-    bb += ncol * jobs.nch[j];
+    bb += ncolp * jobs.nch[j];
     fb += ncol;
   }
   jobs.bbase[J] = bb;

@@ -157,7 +157,8 @@ struct SlabJobs {   // passed by value as a kernel argument (no per-step host->d
   int nblk[SLAB_MAX_JOBS];
   int nch[SLAB_MAX_JOBS];             // row chunks of the job (partial sums)
   long wsbase[SLAB_MAX_JOBS];         // job's partials in the workspace: [nch][n]
-  long bbase[SLAB_MAX_JOBS + 1];      // prefix sums of ceil(n/64) * nch (partial-launch workgroups)
+  int vec[SLAB_MAX_JOBS];             // partial launch in float4 columns (n % 4 == 0, 16-byte aligned rows)
+  long bbase[SLAB_MAX_JOBS + 1];      // prefix sums of ceil(n/cw) * nch, cw = 256 (vec) or 64 (partial workgroups)
   long fbase[SLAB_MAX_JOBS + 1];      // prefix sums of ceil(n/64) (finish-launch workgroups)
   int njobs;
 };

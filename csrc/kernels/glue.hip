@@ -178,17 +178,43 @@ INA_DEVICE int find_job(const long* base, int njobs, long x) {
 }
 
 __global__ __launch_bounds__(256) void slab_partial_kernel(SlabJobs jobs, float* __restrict__ ws) {
-  __shared__ float red[4][64];
+  __shared__ float red[4][256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long bid = blockIdx.x;
   const int j = find_job(jobs.bbase, jobs.njobs, bid);
   const long loc = bid - jobs.bbase[j];
-  const int ncol = (int)((jobs.n[j] + 63) / 64), nch = jobs.nch[j];
+  const bool vec = jobs.vec[j] != 0;   // uniform
+  const int ncol = (int)((jobs.n[j] + (vec ? 255 : 63)) / (vec ? 256 : 64)), nch = jobs.nch[j];
   const int cg = (int)(loc % ncol), ch = (int)(loc / ncol);
   const long n = jobs.n[j];
-  const long col = (long)cg * 64 + lane;
   const int nb = jobs.nblk[j];
   const int b0 = (int)(((long)nb * ch) / nch), b1 = (int)(((long)nb * (ch + 1)) / nch);
+  if (vec) {   // lane = 4 consecutive columns (16-byte loads: a wave reads 1 KiB per row), the same row order per column
+    const long c4 = (long)cg * 256 + 4 * lane;
+    f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+    if (c4 < n) {
+      const float* s = jobs.src[j] + c4;
+      int b = b0 + wave;
+      for (; b + 12 < b1; b += 16) {
+        a0 += *reinterpret_cast<const f32x4_t*>(s + (long)b * n);
+        a1 += *reinterpret_cast<const f32x4_t*>(s + (long)(b + 4) * n);
+        a2 += *reinterpret_cast<const f32x4_t*>(s + (long)(b + 8) * n);
+        a3 += *reinterpret_cast<const f32x4_t*>(s + (long)(b + 12) * n);
+      }
+      for (; b < b1; b += 4) a0 += *reinterpret_cast<const f32x4_t*>(s + (long)b * n);
+    }
+    *reinterpret_cast<f32x4_t*>(&red[wave][4 * lane]) = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (wave == 0 && c4 < n) {
+      const f32x4_t r0 = *reinterpret_cast<const f32x4_t*>(&red[0][4 * lane]);
+      const f32x4_t r1 = *reinterpret_cast<const f32x4_t*>(&red[1][4 * lane]);
+      const f32x4_t r2 = *reinterpret_cast<const f32x4_t*>(&red[2][4 * lane]);
+      const f32x4_t r3 = *reinterpret_cast<const f32x4_t*>(&red[3][4 * lane]);
+      *reinterpret_cast<f32x4_t*>(ws + jobs.wsbase[j] + (long)ch * n + c4) = (r0 + r1) + (r2 + r3);
+    }
+    return;
+  }
+  const long col = (long)cg * 64 + lane;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (col < n) {
     const float* s = jobs.src[j] + col;
