@@ -147,7 +147,7 @@ int64_t slab_scatter_add(Tensor dst, const std::vector<Tensor>& srcs, const std:
     jobs.fbase[j] = fb;
     wsb += (long)jobs.nch[j] * (long)n;
     bb += ncolp * jobs.nch[j];
-    fb += ncol;
+    fb += (long)((n + 255) / 256);   // finish: one thread per column
   }
   jobs.bbase[J] = bb;
   jobs.fbase[J] = fb;

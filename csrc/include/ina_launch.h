@@ -159,7 +159,7 @@ struct SlabJobs {   // passed by value as a kernel argument (no per-step host->d
   long wsbase[SLAB_MAX_JOBS];         // job's partials in the workspace: [nch][n]
   int vec[SLAB_MAX_JOBS];             // partial launch in float4 columns (n % 4 == 0, 16-byte aligned rows)
   long bbase[SLAB_MAX_JOBS + 1];      // prefix sums of ceil(n/cw) * nch, cw = 256 (vec) or 64 (partial workgroups)
-  long fbase[SLAB_MAX_JOBS + 1];      // prefix sums of ceil(n/64) (finish-launch workgroups)
+  long fbase[SLAB_MAX_JOBS + 1];      // prefix sums of ceil(n/256) (finish-launch workgroups, a thread per column)
   int njobs;
 };
 // out[a][c][b] = in[a][b][c] for in [A][B][C] fp32; out fp32 or bf16 (glue.hip)

@@ -235,26 +235,29 @@ __global__ __launch_bounds__(256) void slab_partial_kernel(SlabJobs jobs, float*
 
 __global__ __launch_bounds__(256) void slab_finish_kernel(SlabJobs jobs, const float* __restrict__ ws,
                                                           float* __restrict__ dst) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // one thread per column: its nch chunk partials in 4 interleaved accumulators (fixed order), then the
+  // scatter-add (4-wave workgroups per 64 columns left 3 waves idle at the 1-2 chunks of the wide slabs)
   const long bid = blockIdx.x;
   const int j = find_job(jobs.fbase, jobs.njobs, bid);
   const long n = jobs.n[j];
-  const long col = (bid - jobs.fbase[j]) * 64 + lane;
-  float a = 0.f;
-  if (col < n) {
-    const float* w = ws + jobs.wsbase[j] + col;
-    for (int c = wave; c < jobs.nch[j]; c += 4) a += w[(long)c * n];
+  const long col = (bid - jobs.fbase[j]) * 256 + threadIdx.x;
+  if (col >= n) return;
+  const float* w = ws + jobs.wsbase[j] + col;
+  const int nch = jobs.nch[j];
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int c = 0;
+  for (; c + 3 < nch; c += 4) {
+    a0 += w[(long)c * n];
+    a1 += w[(long)(c + 1) * n];
+    a2 += w[(long)(c + 2) * n];
+    a3 += w[(long)(c + 3) * n];
   }
-  red[wave][lane] = a;
-  __syncthreads();
-  if (wave == 0 && col < n) {
-    const int m = jobs.map[j][col];
-    if (m >= 0) {
-      float s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-      if (jobs.scale[j]) s *= jobs.scale[j][0];
-      dst[m] += s;
-    }
+  for (; c < nch; ++c) a0 += w[(long)c * n];
+  const int m = jobs.map[j][col];
+  if (m >= 0) {
+    float s = (a0 + a1) + (a2 + a3);
+    if (jobs.scale[j]) s *= jobs.scale[j][0];
+    dst[m] += s;
   }
 }
 

@@ -138,7 +138,9 @@ class InductionNetwork(nn.Module):
                 from ..ops.wide import encode_wide
                 if cfg.lstm_skip_padding:
                     raise NotImplementedError("lstm_skip_padding: the wide GPU path runs the reference's full L")
-                e, alphas = encode_wide(inst, data, pe, up, kp, int(dropout_seed))
+                # training with the step glue: the kernel path's gradients go to its scatter-add (flat parameters only)
+                gl = glue if (training and glue is not None and grad_views is not None and real is None) else None
+                e, alphas = encode_wide(inst, data, pe, up, kp, int(dropout_seed), glue=gl)
             if real is not None:   # the real units of the zero-padded encoder
                 e = e[:, real]
             if embeddings_only:
@@ -189,7 +191,7 @@ class InductionNetwork(nn.Module):
                                 grad_views=grad_views, overlap=overlap, seed_dev=seed_dev, embeddings_only=True,
                                 glue=glue)
             return head_wide_loss(e, p, labels, B, N, K, Q, cfg.routing_iters, cfg.relation_head, cfg.loss_type,
-                                  cfg.loss_reduction)
+                                  cfg.loss_reduction, glue=glue if grad_views is not None else None)
         if not fused:
             probs, _ = self.forward(inst, data, B, N, K, Q, training=True, dropout_seed=dropout_seed,
                                     grad_views=grad_views, overlap=overlap, seed_dev=seed_dev, glue=glue)

@@ -169,6 +169,39 @@ class StepGlue:
             self._maps[key] = m
         return m
 
+    def map_index(self, t: torch.Tensor, idx: np.ndarray, tag) -> torch.Tensor:
+        """Slab column j -> element idx[j] of parameter t (-1: dropped), cached under (tag, offset of t)."""
+        key = ("ix", tag, self.off(t), t.numel())
+        m = self._maps.get(key)
+        if m is None:
+            idx = np.asarray(idx, dtype=np.int64)
+            if idx.size and (idx.max() >= t.numel()):
+                raise ValueError("StepGlue.map_index: index past the parameter")
+            m = self._dev_i32(np.where(idx >= 0, self.off(t) + idx, -1))
+            self._maps[key] = m
+        return m
+
+    def map_merged_lstm(self, p, U: int, D: int, DP: int, G4: int) -> torch.Tensor:
+        """The wide BiLSTM's merged weight-gradient GEMM output dwall [DP + 2 UP, 2 G4] (ops/packing.py::
+        _merged_wgrad_idx) -> both directions' kernel [D + U, 4U] and bias [4U]; the dropped cross-direction
+        blocks and padding map to -1."""
+        from .packing import _merged_wgrad_idx
+        ks = (self.off(p["lstm_fw_kernel"]), self.off(p["lstm_bw_kernel"]))
+        bs = (self.off(p["lstm_fw_bias"]), self.off(p["lstm_bw_bias"]))
+        key = ("merged", U, D, DP, G4, ks, bs)
+        m = self._maps.get(key)
+        if m is None:
+            src = _merged_wgrad_idx(U, D, DP).numpy().reshape(2, D + U + 1, 4 * U)
+            tgt = np.empty_like(src)
+            for d in range(2):
+                tgt[d, :D + U] = ks[d] + np.arange((D + U) * 4 * U).reshape(D + U, 4 * U)
+                tgt[d, D + U] = bs[d] + np.arange(4 * U)
+            mm = np.full((DP + 2 * (G4 // 4)) * 2 * G4, -1, dtype=np.int64)
+            mm[src.reshape(-1)] = tgt.reshape(-1)
+            m = self._dev_i32(mm)
+            self._maps[key] = m
+        return m
+
     def map_ntn_M(self, Mt: torch.Tensor) -> torch.Tensor:
         """dM GEMM output [a][s*H + b] -> M [a][b][s]."""
         H, _, h = Mt.shape

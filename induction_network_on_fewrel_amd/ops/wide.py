@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import weakref
 
+import numpy as np
 import torch
 
 from ._ext import ops
@@ -29,22 +30,28 @@ def _own_tn_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
             and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0 and a.shape[0] > 0)
 
 
+def _wgrad_parts(a: torch.Tensor, b: torch.Tensor, split: int = 16, own: bool = True):
+    """(partials [ns, m, n] fp32, ns) of a^T b, summed by _wgrad or by the step glue's ordered slab reduction."""
+    if own and _own_tn_ok(a, b):
+        part = ops().gemm_wgrad(a, b, 0)
+        return part, part.shape[0]
+    T = a.shape[0]
+    sp = split
+    while sp > 1 and (T % sp or T < 256 * sp):
+        sp //= 2
+    if sp > 1:
+        return torch.bmm(a.view(sp, T // sp, -1).transpose(1, 2), b.view(sp, T // sp, -1), out_dtype=torch.float32), sp
+    return torch.mm(a.t(), b, out_dtype=torch.float32).unsqueeze(0), 1
+
+
 def _wgrad(a: torch.Tensor, b: torch.Tensor, split: int = 16, own: bool = True) -> torch.Tensor:
     """a^T b in fp32 for tall bf16 a [T, m], b [T, n]: the own TN split-K GEMM (one round of 256 x 256 output tiles
     over the CUs, fp32 slabs + an ordered sum; 242 vs 245 us for hipBLASLt's split-128 batch at the paper
     attention dW1, profiles/r6_gemm) or, for other operands, hipBLASLt with K = T split into `split` chunks
     (a single K = 1.2 M GEMM runs on a handful of output tiles; a T that `split` does not divide takes the largest
     smaller power-of-two split that does)."""
-    if own and _own_tn_ok(a, b):
-        return ops().gemm_wgrad(a, b, 0).sum(0)
-    T = a.shape[0]
-    sp = split
-    while sp > 1 and (T % sp or T < 256 * sp):
-        sp //= 2
-    if sp > 1:
-        part = torch.bmm(a.view(sp, T // sp, -1).transpose(1, 2), b.view(sp, T // sp, -1), out_dtype=torch.float32)
-        return part.sum(0)
-    return torch.mm(a.t(), b, out_dtype=torch.float32)
+    part, ns = _wgrad_parts(a, b, split, own)
+    return part.sum(0) if ns > 1 else part[0]
 
 
 class WideBiLSTM(torch.autograd.Function):
@@ -166,7 +173,7 @@ class WideSeqBiLSTM(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, inst, word, pos1, pos2, wemb, p1emb, p2emb, Kf, bf, Kb, bb, U, seed, keep_prob, pos_shift,
-                packs=None):
+                packs=None, gl=None):
         from .packing import pack_lstm_wide
         o = ops()
         S, L = inst.shape[0], word.shape[1]
@@ -191,6 +198,9 @@ class WideSeqBiLSTM(torch.autograd.Function):
         if need:
             ctx.save_for_backward(inst, word, pos1, pos2, Xw, pk["wxtc"], pk["a2pk"], acts, cst)
             ctx.cfg = (S, L, E, P, U, int(seed), float(keep_prob), bool(pos_shift), p1emb.shape[0], wemb.shape[0])
+            # gl = (StepGlue, params): the gradients go to the glue's single scatter-add into the flat gradient (no
+            # .sum(0) of the split-K partials, no unpack gather, no autograd accumulation adds)
+            ctx.gl = gl
         return hout
 
     @staticmethod
@@ -217,8 +227,15 @@ class WideSeqBiLSTM(torch.autograd.Function):
         # 512 rows that fill 256-row tiles + gemm_tn.hip for the 64-row h_bw tail took 1,190 + 224 us (paper 32.2-32.6k
         # vs 32.9-33.1k episodes/s, profiles/r6_paper1): at this shape hipBLASLt's main loop (1.14 PF/s) beats the own
         # one (1.04)
-        dwall = _wgrad(Xw, dG, 64, own=False)
-        dKs, dbs = unpack_merged_wgrad(dwall, U, D)                      # both directions, one gather
+        gl = ctx.gl if not need_w else None
+        if gl is not None:
+            glue, p = gl
+            part, ns = _wgrad_parts(Xw, dG, 64, own=False)
+            glue.add(part, glue.map_merged_lstm(p, U, D, DP, G4), ns)
+            dKs, dbs = [None, None], [None, None]
+        else:
+            dwall = _wgrad(Xw, dG, 64, own=False)
+            dKs, dbs = unpack_merged_wgrad(dwall, U, D)                  # both directions, one gather
         if fuse:
             dxp = dxpd                                                    # [2, S*L, 2P]: per direction
         else:
@@ -228,6 +245,10 @@ class WideSeqBiLSTM(torch.autograd.Function):
         if shift:
             tp = o.wide_pos_grad(dxp, inst, pos1, pos2, P2)             # sums the direction planes
             dp1, dp2 = tp[0], tp[1]
+            if gl is not None:
+                glue.add(tp, glue.map_cat([glue.map_identity(p["pos1_embedding"]),
+                                           glue.map_identity(p["pos2_embedding"])]), 1)
+                dp1 = dp2 = None
         else:
             if dxp.dim() == 3:
                 dxp = dxp.sum(0)
@@ -237,7 +258,8 @@ class WideSeqBiLSTM(torch.autograd.Function):
         dw = None
         if need_w:
             dw = table_grad(word[inst.long()].reshape(-1).long(), dX[:, :E], V)
-        return (None, None, None, None, dw, dp1, dp2, dKs[0], dbs[0], dKs[1], dbs[1], None, None, None, None, None)
+        return (None, None, None, None, dw, dp1, dp2, dKs[0], dbs[0], dKs[1], dbs[1], None, None, None, None, None,
+                None)
 
 
 def pos_frags(wxtc: torch.Tensor, E: int, D: int) -> torch.Tensor:
@@ -319,12 +341,13 @@ class WideAttn(torch.autograd.Function):
     gradient (the reference fetches them for inspection only, model/base.py:144)."""
 
     @staticmethod
-    def forward(ctx, Hb, inst, mask, W1, b1, w2, packs=None):
+    def forward(ctx, Hb, inst, mask, W1, b1, w2, packs=None, gl=None):
         from .packing import pack_attn_wide
         pk = packs if packs is not None else pack_attn_wide(W1, b1, w2)
         e, alpha = ops().wide_attn_fwd(Hb, inst, mask, pk["w1t"], pk["b1"], pk["w2"])
         ctx.save_for_backward(Hb, inst, mask, alpha)
         ctx.pk = pk
+        ctx.gl = gl   # (StepGlue, params): gradients into the glue (see WideSeqBiLSTM)
         ctx.mark_non_differentiable(alpha)
         return e, alpha
 
@@ -335,9 +358,18 @@ class WideAttn(torch.autograd.Function):
         H = Hb.shape[-1]
         dH, dZ, part = ops().wide_attn_bwd(Hb, inst, mask, pk["w1t"], pk["w1"], pk["b1"], pk["w2"], alpha,
                                            de.contiguous().float())
+        if ctx.gl is not None and ctx.needs_input_grad[3]:
+            glue, p = ctx.gl
+            w1p, ns = _wgrad_parts(Hb.reshape(-1, H), dZ, 128)
+            glue.add(w1p, glue.map_identity(p["attn_kernel"]), ns)
+            X = part.shape[-1]                                            # part [blocks][w2 | b1][X >= H]
+            j = np.where(np.arange(X) < H, np.arange(X), -1)
+            glue.add(part, glue.map_cat([glue.map_index(p["attn_w2"], j, ("attn_w2", X)),
+                                         glue.map_index(p["attn_bias"], j, ("attn_b1", X))]), part.shape[0])
+            return dH, None, None, None, None, None, None, None
         dW1 = _wgrad(Hb.reshape(-1, H), dZ, 128) if ctx.needs_input_grad[3] else None
         ps = part.sum(0)
-        return dH, None, None, dW1, ps[1, :H], ps[0, :H].unsqueeze(1), None
+        return dH, None, None, dW1, ps[1, :H], ps[0, :H].unsqueeze(1), None, None
 
 
 def attention_wide(H, mask, W1, b1, w2):
@@ -357,8 +389,9 @@ def attention_wide(H, mask, W1, b1, w2):
     return e, alphas
 
 
-def encode_wide(inst, data, p, U: int, keep_prob: float, seed: int):
-    """Wide GPU encoder: embedding gather + WideBiLSTM + self-attention (GEMM formulation)."""
+def encode_wide(inst, data, p, U: int, keep_prob: float, seed: int, glue=None):
+    """Wide GPU encoder: embedding gather + WideBiLSTM + self-attention (GEMM formulation).  ``glue``: the step's
+    StepGlue (training, parameters in the flat buffer): the kernel path's gradients go to its scatter-add."""
     from ..models import reference as ref
     if ops().lstm_wide_seq_ok(U):   # hand-written kernels end to end (u in {64, 100, 128})
         wa, p1a, p2a, ma = data
@@ -371,11 +404,12 @@ def encode_wide(inst, data, p, U: int, keep_prob: float, seed: int):
                                p["attn_kernel"], p["attn_bias"], p["attn_w2"], U, D)
         H = WideSeqBiLSTM.apply(inst, wa, p1a, p2a, p["word_embedding"], p["pos1_embedding"], p["pos2_embedding"],
                                 p["lstm_fw_kernel"], p["lstm_fw_bias"], p["lstm_bw_kernel"], p["lstm_bw_bias"], U,
-                                int(seed), float(keep_prob), bool(getattr(data, "pos_shift", False)), packs)
+                                int(seed), float(keep_prob), bool(getattr(data, "pos_shift", False)), packs,
+                                (glue, p) if glue is not None and attn_fused else None)
         if attn_fused:
             mi = ma if ma.dtype == torch.int32 else ma.int()
             return WideAttn.apply(H, inst.int(), mi.contiguous(), p["attn_kernel"], p["attn_bias"], p["attn_w2"],
-                                  packs)
+                                  packs, (glue, p) if glue is not None else None)
         e, alphas = attention_wide(H, ma[inst.long()] > 0, p["attn_kernel"], p["attn_bias"], p["attn_w2"])
         return e, alphas.squeeze(-1)
     word, pos1, pos2, mask = (t[inst.long()] for t in data)
@@ -417,6 +451,14 @@ def head_wide_ok(H: int, N: int, K: int, R: int, head: str) -> bool:
     """Shapes the hand-written wide head (csrc/kernels/head_wide.hip) covers."""
     o = ops()
     return bool(o.routing_wide_ok(K, H, R)) and bool(o.ntn_wide_epi_ok(N, head == "paper"))
+
+
+def _split_parts_mm(a: torch.Tensor, b: torch.Tensor, nb: int = 64):
+    """(partials [nb, m, n], nb) of a^T b for tall a [T, m], b [T, n] (the slabs _split_sum_mm sums)."""
+    T = a.shape[0]
+    if T % nb or T < 64 * nb:
+        nb = 1
+    return torch.bmm(a.view(nb, T // nb, -1).transpose(1, 2), b.view(nb, T // nb, -1)), nb
 
 
 def _split_sum_mm(a: torch.Tensor, b: torch.Tensor, nb: int = 64) -> torch.Tensor:
@@ -461,7 +503,7 @@ def _wide_head_forward(e, Ws, M, w, b, E, N, K, Q, R, paper):
     return probs.view(E, NQ, N), (sup, eh, cls_bf, Mt, P, qb, T, wf)
 
 
-def _wide_head_backward(ctx, saved, dz, g):
+def _wide_head_backward(ctx, saved, dz, g, gl=None):
     """Shared backward of HeadWideProbsFn / HeadWideLossFn: dz = dL/dlogit [E*NQ, N] (g: upstream scale);
     saved = the forward's (sup, eh, cls_bf, Mt, P, qb, T, wf, Ws).  T is overwritten with ReLU(T) (the FC
     weight-gradient operand): the backward runs once (no retain_graph double backward)."""
@@ -478,15 +520,32 @@ def _wide_head_backward(ctx, saved, dz, g):
     dcls = _splitk_nt(dPf, Mt, 8)                                              # [E*N, H]
     dMt = torch.mm(cls_bf.t(), dPf, out_dtype=torch.float32)                   # [H, h*H] fp32 (one GEMM: 30 us
     # vs 69 us split 4 + sum at the paper configuration, profiles/r5_dm1 / r5_dws)
+    # dM stays on the LDS-tiled transpose (+ autograd's one add): through the glue, the 6.5 M-entry scatter into
+    # M's [a][b][s] layout ran as 102,400 single-row finish workgroups, ~100 us at the paper configuration
     dM = o.transpose12(dMt.view(H, h, H), False)                                 # [a][b][s] fp32
+    if gl is not None:   # (StepGlue, W_s, M, ntn_w, ntn_b): the other head gradients into the glue's scatter-add
+        glue, pWs, pM, pw, pb = gl
     deh = o.routing_wide_bwd(eh, dcls, E * N, K, R)                            # [E*NK, H]
     ns = 4 if sup.is_cuda and sup.shape[0] % 4 == 0 and sup.shape[0] >= 4096 else 1
     # (fp32 split-K 4 + ordered sum: 26 vs 44 us for one GEMM at the paper configuration, profiles/r5_dm1 / r5_dws)
-    dWs = (torch.bmm(sup.view(ns, -1, H).transpose(1, 2), deh.view(ns, -1, H)).sum(0) if ns > 1
-           else torch.mm(sup.t(), deh))
+    wsp = (torch.bmm(sup.view(ns, -1, H).transpose(1, 2), deh.view(ns, -1, H)) if ns > 1
+           else torch.mm(sup.t(), deh).unsqueeze(0))
     dsup = torch.mm(deh, Ws.t())
     de = torch.cat([dsup.view(E, NK, H), dQ], 1).view(E * (NK + NQ), H)
     V = T.view(E * NQ, N * h)
+    if gl is not None:
+        glue.add(wsp, glue.map_identity(pWs), ns)
+        if paper:
+            wp, nb = _split_parts_mm(V.view(-1, h), dzs.view(-1, 1))           # [nb, h, 1] -> ntn_w [h, 1]
+            glue.add(wp, glue.map_identity(pw), nb)
+            glue.add(dzs.reshape(-1, 1), glue.map_identity(pb), dzs.numel())  # db = sum of dz
+        else:
+            wp, nb = _split_parts_mm(V, dzs)                                  # [nb, N*h (c*h + s), N]
+            c, sh, c2 = np.meshgrid(np.arange(N), np.arange(h), np.arange(N), indexing="ij")
+            glue.add(wp, glue.map_index(pw, ((sh * N + c) * N + c2).reshape(-1), ("ntn_w_ref", N, h)), nb)
+            glue.add(dzs, glue.map_identity(pb), dzs.shape[0])
+        return de, None, dM, None, None
+    dWs = wsp.sum(0) if ns > 1 else wsp[0]
     if paper:
         dw = _split_sum_mm(V.view(-1, h), dzs.view(-1, 1))                     # [h, 1]
         db = dzs.sum().view(1)
@@ -527,7 +586,7 @@ class HeadWideLossFn(torch.autograd.Function):
     LOSS_BLOCKS = 64
 
     @staticmethod
-    def forward(ctx, e, Ws, M, w, b, labels, cfg, loss_type, reduction):
+    def forward(ctx, e, Ws, M, w, b, labels, cfg, loss_type, reduction, glue=None):
         o = ops()
         E, N, K, Q, R, paper = cfg
         probs, saved = _wide_head_forward(e, Ws, M, w, b, E, N, K, Q, R, paper)
@@ -544,6 +603,7 @@ class HeadWideLossFn(torch.autograd.Function):
         ctx.dz = dz
         ctx.cfg = cfg
         ctx.edtype = e.dtype
+        ctx.gl = (glue, Ws, M, w, b) if glue is not None else None
         ctx.set_materialize_grads(False)
         loss, acc = out[0], out[1]
         ctx.mark_non_differentiable(acc, probs)
@@ -553,8 +613,8 @@ class HeadWideLossFn(torch.autograd.Function):
     def backward(ctx, gloss, _gacc, _gprobs):
         g = (gloss.reshape(1).float().contiguous() if gloss is not None
              else torch.zeros(1, device=ctx.dz.device))
-        de, dWs, dM, dw, db = _wide_head_backward(ctx, ctx.saved_tensors, ctx.dz, g)
-        return de.to(ctx.edtype), dWs, dM, dw, db, None, None, None, None
+        de, dWs, dM, dw, db = _wide_head_backward(ctx, ctx.saved_tensors, ctx.dz, g, ctx.gl)
+        return de.to(ctx.edtype), dWs, dM, dw, db, None, None, None, None, None
 
 
 def head_wide(e, p, B: int, N: int, K: int, Q: int, iters: int, head: str):
@@ -566,10 +626,11 @@ def head_wide(e, p, B: int, N: int, K: int, Q: int, iters: int, head: str):
 
 
 def head_wide_loss(e, p, labels, B: int, N: int, K: int, Q: int, iters: int, head: str, loss_type: str,
-                   reduction: str):
-    """(loss, accuracy, probs) of the wide head with the fused loss kernel."""
+                   reduction: str, glue=None):
+    """(loss, accuracy, probs) of the wide head with the fused loss kernel (``glue``: gradients into the step
+    glue's scatter-add, see WideSeqBiLSTM)."""
     return HeadWideLossFn.apply(e, p["W_s"], p["M"], p["ntn_w"], p["ntn_b"], labels,
-                                (B, N, K, Q, iters, head == "paper"), loss_type, reduction)
+                                (B, N, K, Q, iters, head == "paper"), loss_type, reduction, glue)
 
 
 def head_wide_torch(e, p, B: int, N: int, K: int, Q: int, iters: int, head: str):
