@@ -1296,10 +1296,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdWaves<U,
           // (no exp / rcp pair per unit and step for tanh(c_t); h_t is the forward's bf16 h, relative error
           // <= 2^-9).  o = 1 / (1 + e), e = 2^-z_o (z clamped: e stays finite, and where o ~ 0 every use of tc is
           // scaled by o)
-          // (fminf costs a canonicalize + v_min; __builtin_amdgcn_fmed3f(-acc[3], -3e38, 126), one v_med3 reading the
-          // accumulator directly, failed test_encoder_backward at u = 32 (1.6% of the attention-bias gradient off:
-          // profiles/r6_med3, presumably the MFMA -> VALU hazard of gemm.hip's permlane note) -- not used)
-          const float eo = __builtin_amdgcn_exp2f(fminf(-acc[3], 126.f));
+          // (the clamp on exp2's result, 2^126: the exp reads the accumulator as the forward's gate exps do, and the
+          // v_min needs no canonicalize (fminf(-acc[3], 126) cost a v_max + v_min).  __builtin_amdgcn_fmed3f(-acc[3],
+          // -3e38, 126), one v_med3 on the accumulator, failed test_encoder_backward at u = 32: profiles/r6_med3)
+          const float eo = fminf(__builtin_amdgcn_exp2f(-acc[3]), 0x1p126f);
           const float og = fast_rcp(1.f + eo);
           const float tc = hcv[m] * (1.f + eo);
           const float dh = dh_rec[m] + dhin[m];
