@@ -378,8 +378,11 @@ __global__ __launch_bounds__(256) void x_gather_kernel(const int* __restrict__ i
 // the stores issued after each prefetch and wait only for the prefetched loads.
 // SKIP (bf16): sequence_length semantics for the backward direction (lstm_skip_padding): it starts at the
 // tile's longest length and each row's state is reset to zero past its own length (TF dynamic_rnn)
+#ifndef INA_FWD_WAVES
+#define INA_FWD_WAVES 5   // bf16 waves per SIMD (the gate fragments in LDS free the registers)
+#endif
 template <int U, int NX, bool BF16, bool DROP, bool STORE, bool SKIP = false, bool XD = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void lstm_fwd_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF16 && U <= 20 ? INA_FWD_WAVES : 4))) void lstm_fwd_kernel(
     const int* __restrict__ inst, int S, const int* __restrict__ word, const int* __restrict__ pos1,
     const int* __restrict__ pos2, int L, const float* __restrict__ wemb, int E,
     const float* __restrict__ p1emb, const float* __restrict__ p2emb, int PD,
@@ -405,10 +408,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   const int ntiles = (S + 15) / 16;
   const int tile = dir == 0 ? ntiles - 1 - ((int)blockIdx.x * 4 + wave) : (int)blockIdx.x * 4 + wave;
   int2* ids = ids_all + (wave * 16) * L;
-  if constexpr (XD) {   // the block's position tables (xg = x_gather's global copy; before any wave leaves)
-    xd_copy(ids_all, xg, L);
-    __syncthreads();
+  // bf16: the direction's gate weight fragments (pre-scaled) live in LDS and are read per step instead of held in
+  // 4 * NMT * NKS VGPRs per lane -- the registers that let a 5th wave per SIMD fit (u = 20: 128 -> 82 VGPRs,
+  // kernel 732 -> 703 us; 6 waves spill in the step loop and measure 707: profiles/r6_flds)
+  __shared__ frag lA[BF16 ? NMT * NKS * 64 : 1];
+  const frag* ap = apack + (size_t)dir * NMT * NKS * 64;
+  if constexpr (BF16) {
+    for (int i = threadIdx.x; i < NMT * NKS * 64; i += 256) lA[i] = fscale(ap[i], gate_scale(i & 3));
   }
+  if constexpr (XD) xd_copy(ids_all, xg, L);   // the block's position tables (xg = x_gather's global copy)
+  if constexpr (BF16 || XD) __syncthreads();   // (before any wave leaves)
   constexpr bool FG = !BF16;   // fp32 mode gathers x per step
   if constexpr (FG) {
     // fp32 mode gathers x per step: stage (word, pos1 | pos2 << 16) of the wave's 16 sequences into LDS
@@ -435,12 +444,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
   const int tb = (SKIP && dir == 1) ? L - Lt : 0, te = dir == 0 ? Lt : L;
   const int mylen = SKIP ? (seq < S ? slen[seq] : 0) : L;
 
-  frag A[NMT][NKS];
-  const frag* ap = apack + (size_t)dir * NMT * NKS * 64;
+  frag A[NMT][NKS];   // fp32: the fragments in registers
+  if constexpr (!BF16) {
 #pragma unroll
-  for (int m = 0; m < NMT; ++m)
+    for (int m = 0; m < NMT; ++m)
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) A[m][ks] = fscale(ap[(m * NKS + ks) * 64 + lane], gate_scale(lane & 3));
+      for (int ks = 0; ks < NKS; ++ks) A[m][ks] = fscale(ap[(m * NKS + ks) * 64 + lane], gate_scale(lane & 3));
+  }
   float bm[NMT][4];   // pre-scaled gate biases (gate_bias)
 #pragma unroll
   for (int m = 0; m < NMT; ++m)
@@ -516,7 +526,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     for (int m = 0; m < NMT; ++m) {
       f32x4_t acc = {bm[m][0], bm[m][1], bm[m][2], bm[m][3]};
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) acc = mma(A[m][ks], B[ks], acc);
+      for (int ks = 0; ks < NKS; ++ks) acc = mma(lA[(m * NKS + ks) * 64 + lane], B[ks], acc);
       // c[m] holds the cell state times 2 log2(e) (tanh_l2's argument scale): the scale rides on the g gate's
       // 1 - 2r form (k - 2k r, same fma) and the fp16 record's conversion (x 1/k), so tanh(c) needs no multiply
       const float ig = sigmoid_l2(acc[0]), fg = sigmoid_l2(acc[2]), og = sigmoid_l2(acc[3]);
