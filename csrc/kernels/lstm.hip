@@ -399,7 +399,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF16 && U <
   using celem = typename CT<BF16>::type;
   constexpr int U4 = Sh::U4, KPL = Sh::KPL, NKS = Sh::NKS, NMT = Sh::NMT;
   extern __shared__ __attribute__((aligned(16))) int2 ids_all[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave index as an SGPR: the tile, its step count and every per-step record / x address derive from it, and as a
+  // VGPR each step paid a v_mul_lo_u32 + 64-bit address add for the record stores and the loop counters on the VALU
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int q = lane >> 4, n = lane & 15;
   // longest work first: the backward direction (all L steps) dispatches before the forward one, whose ragged tiles
   // (length-sorted ascending by the plan) run longest first -- no long tile left for the kernel's tail (lstm_fwd

@@ -265,7 +265,7 @@ template <int MTH, int QT, int SG>
 __global__ __launch_bounds__(NT_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void ntn_fwd_kernel(NtnArgs k) {
   constexpr int GM = QT <= 2 ? 2 : 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char ntn_lds[];
-  const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const Geo g = geo(k, n);
   const int t0 = (int)((long)k.ntile * blockIdx.y / gridDim.y), t1 = (int)((long)k.ntile * (blockIdx.y + 1) / gridDim.y);
   unsigned char* const zero = ntn_lds + 2 * k.tpb;

@@ -185,7 +185,7 @@ __global__ __launch_bounds__(256) void rec_attn_fwd_kernel(
   const int lane = threadIdx.x & 63, q = lane >> 4, n = lane & 15;
   // longest tiles first (the ragged plan sorts rows by length ascending; dispatching in that order left the longest
   // tiles for the kernel's tail): tile = ntiles - 1 - (4 blockIdx.x + wave)
-  const int ntl = (S + 15) / 16, tix = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int ntl = (S + 15) / 16, tix = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tile = ntl - 1 - tix;
   // weights shared by the workgroup in LDS (registers kept for occupancy: the loop is latency-bound
   // on the record loads, so resident waves are what hides them)
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 20 ? I
   using C = RA<U>;
   constexpr int U4 = C::U4, H2 = C::H2, NV = C::NV, NKR = C::NKR, MT = C::MT, NJ = C::NJ, NKS2 = C::NKS2,
                 NRT = C::NRT, NVP = C::NVP, HT = C::HT, HCP = C::HCP, JCP = C::JCP, DEPC = C::DEP;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, n = lane & 15;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4, n = lane & 15;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   u16x8_t* lA = reinterpret_cast<u16x8_t*>(smem);
   u16x8_t* lAT = lA + C::NA;

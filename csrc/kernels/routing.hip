@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256) void routing_g_fwd_kernel(const float* __restr
   constexpr int HF = RGShape<H>::HF, HP = RGShape<H>::HP;
   extern __shared__ __attribute__((aligned(16))) float rgs[];
   float* wsh = rgs;                                   // W_s[a][h] (h padded to HP with zeros)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4, j = lane & 15;
   float* S = rgs + H * HP + wave * 4 * K * HP;        // this wave's [4K][HP] support rows
   for (int i = threadIdx.x; i < H * HP; i += 256) {
     const int a = i / HP, hh = i - a * HP;
@@ -377,7 +377,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void r
   extern __shared__ __attribute__((aligned(16))) float rgs[];
   float* wsh = rgs;                 // W_s[a][h]
   float* wst = rgs + H * HP;        // W_s^T[h][a]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4, j = lane & 15;
   float* S = rgs + 2 * H * HP + wave * 8 * K * HP;   // [4K][HP] support rows
   float* D = S + 4 * K * HP;                          // [4K][HP] dE_hat rows
   for (int i = threadIdx.x; i < H * HP; i += 256) {
