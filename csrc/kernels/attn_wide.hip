@@ -296,7 +296,7 @@ __global__ __launch_bounds__(AttnCfg<HP>::NTH) void wide_attn_bwd_kernel(WideAtt
   float* abuf = debuf + 2 * SB * HP;                                            // [2][R] alphas
   float* dsv = abuf + 2 * R;                                                    // [R]
   float* bwj = dsv + R;                                                         // [2][HP]: b1 (pre-scaled), w2
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4, n = lane & 15;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4, n = lane & 15;
   u16x8_t A1[2][KS], A2[2][KS];
   load_frags<HP>(reinterpret_cast<const u16x8_t*>(a.w1t), w, lane, A1);
   load_frags<HP>(reinterpret_cast<const u16x8_t*>(a.w1), w, lane, A2);

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void ln_res_fwd_kernel(const unsigned short* _
                                                          int T, uint32_t salt, uint32_t thr, float inv_kp, int drop) {
   constexpr int HD = 256 * NCH;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row >= T) return;
   const size_t base = (size_t)row * HD;
   float x[NCH][4];
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(256) void ln_res_bwd_kernel(
     int drop) {
   constexpr int HD = 256 * NCH;
   __shared__ float red[4][3][HD];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // slab rows: d gamma, d beta, and the column sums of da (the bias gradient of the projection that
   // produced a: one pass instead of a separate reduction over the [T, HD] activation gradient)
   float dg[NCH][4], db[NCH][4], dd[NCH][4];
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256) void embed_ln_fwd_kernel(
     uint32_t thr, float inv_kp, int drop) {
   constexpr int HD = 256 * NCH;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row >= S * L) return;
   const int s = row / L, t = row - s * L;
   const int id = ids_all[(size_t)inst[s] * L + t];
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void embed_ln_bwd_kernel(
     uint32_t salt, uint32_t thr, float inv_kp, int drop) {
   constexpr int HD = 256 * NCH;
   __shared__ float red[4][2][HD];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float dg[NCH][4], db[NCH][4];
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
@@ -501,7 +501,7 @@ __global__ __launch_bounds__(64 * NWV) void mha_fwd_kernel(const unsigned short*
   __shared__ float madd[LP];
   const int s = blockIdx.x / nh, hh = blockIdx.x - s * nh;
   const int HDm = nh * HDIM, ROW = 3 * HDm;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int n = lane & 15, g = lane >> 4;
   const size_t tok0 = (size_t)s * L;
   const unsigned short* kbase = qkv + tok0 * ROW + HDm + hh * HDIM;
@@ -641,7 +641,7 @@ __global__ __launch_bounds__(64 * NWV) void mha_bwd_kernel(const unsigned short*
   unsigned short* Kn = TA;
   const int s = blockIdx.x / nh, hh = blockIdx.x - s * nh;
   const int HDm = nh * HDIM, ROW = 3 * HDm;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int n = lane & 15, g = lane >> 4;
   const size_t tok0 = (size_t)s * L;
   const unsigned short* qb = qkv + tok0 * ROW + hh * HDIM;

@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256) void ntn_wide_epi_fwd_kernel(const float* __re
                                                                const float* __restrict__ bias,
                                                                float* __restrict__ probs) {
   const int lane = threadIdx.x & 63;
-  for (long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += (long)gridDim.x * 4) {
+  for (long row = (long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); row < rows; row += (long)gridDim.x * 4) {
     const float* t = T + row * N * h;
     if constexpr (PAPER) {
       for (int c = 0; c < N; ++c) {
@@ -266,7 +266,7 @@ __global__ __launch_bounds__(256) void ntn_wide_epi_bwd_kernel(float* __restrict
                                                                float* __restrict__ dzs) {
   const int lane = threadIdx.x & 63;
   const float gs = g != nullptr ? g[0] : 1.f;
-  for (long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += (long)gridDim.x * 4) {
+  for (long row = (long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); row < rows; row += (long)gridDim.x * 4) {
     float* t = T + row * N * h;
     unsigned short* dt = dT + row * N * h;
     const float* z = dz + row * N;

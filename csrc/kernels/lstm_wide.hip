@@ -236,7 +236,7 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_fwd_kernel(
   constexpr int UP = C::UP, NW = C::NW, M = C::M, KS = C::KS, G4 = C::G4, NT = C::NT, HS = C::HS, SEQ = C::SEQ;
   constexpr int NTH = NW * 64;
   __shared__ __attribute__((aligned(16))) unsigned short himg[2][SEQ * HS];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4, n = lane & 15;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4, n = lane & 15;
   const int dir = blockIdx.y, s0 = blockIdx.x * SEQ;
   const uint32_t salt = dir ? salt1 : salt0, thr16 = thr >> 16;
   u16x8_t A[M][KS];
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(WideCfg<U>::NW * 64) void lstm_wide_seq_bwd_kernel(
   static_assert(NW % 2 == 0 && 4 * NG == KS2, "dX_pos: NW / 2 wave pairs x 4 K-steps cover the gate columns");
   __shared__ __attribute__((aligned(16))) unsigned short gimg[2][SEQ * GS];
   __shared__ __attribute__((aligned(16))) float pimg[2][NG * NT * 16 * 16];   // [buf][kg][nt][seq][16 cols]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4, n = lane & 15;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4, n = lane & 15;
   const int dir = blockIdx.y, s0 = blockIdx.x * SEQ;
   const uint32_t salt = dir ? salt1 : salt0;
   u16x8_t A2[KS2];
@@ -577,7 +577,7 @@ __global__ __launch_bounds__(256) void wide_x_gather_kernel(const int* __restric
   const int lane = threadIdx.x & 63;
   const int D = E + 2 * PD;
   const long rows = (long)S * L;
-  const long r0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RW;
+  const long r0 = ((long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * RW;
   if (r0 >= rows) return;
   typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
   long tok[RW], wbase[RW];
